@@ -1,0 +1,189 @@
+// pybind11 / torch bindings of the gfx950 kernels (csrc/kernels/*.hip).
+// Every op launches on the current HIP stream so it can be captured into a hipGraph
+// (torch.cuda.CUDAGraph) and ordered with RCCL collectives issued by torch.distributed.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
+             hipStream_t stream);
+int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
+                    const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
+                    hipStream_t s);
+int lsa_rope_append(const void* qkv, const int* pos, const int* tok_seq, const int* block_tables, int max_blocks,
+                    const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int T, int H, int Hkv,
+                    hipStream_t s);
+int lsa_silu_mul(const void* g, const void* u, void* o, long n, hipStream_t s);
+int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
+                    const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit, void* out,
+                    float* opart, float* mlpart, hipStream_t s);
+int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
+                     const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
+                     void* out, hipStream_t s);
+int lsa_argmax_commit(const float* logits, int B, int V, unsigned long long* part, int* out_tokens, int max_new,
+                      int* gen_len, int* input_ids, int* positions, int* finished, const int* eos, int neos,
+                      hipStream_t s);
+int lsa_sample_commit(float* logits, int B, int V, unsigned long long* part, unsigned long long* cand, const int* hist,
+                      int window, const float* penalty, const float* temperature, const int* top_k,
+                      const float* top_p, const unsigned long long* seeds, int* out_tokens, int max_new, int* gen_len,
+                      int* input_ids, int* positions, int* finished, const int* eos, int neos, hipStream_t s);
+int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out, int epi,
+                 int nb, int splitk, hipStream_t stream);
+int lsa_fp8_dequant(const void* Wq, const float* wscale, int N, int K, void* Wf, hipStream_t s);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(int rc, const char* what) { TORCH_CHECK(rc == 0, "lsa kernel '", what, "' failed: rc=", rc); }
+
+void need(const at::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+
+template <typename T>
+T* ptr(const c10::optional<at::Tensor>& t) {
+  return t.has_value() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// out = x @ W^T with W in fragment-major layout (see kernels/gemm.hip)
+void gemm(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, int64_t nb,
+          int64_t splitk) {
+  need(x, at::kBFloat16, "x");
+  need(wf, at::kBFloat16, "wf");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(wf.numel() == N * K, "weight numel mismatch: ", wf.numel(), " vs ", N, "x", K);
+  if (epi == 1) {
+    need(out, at::kFloat, "out");
+    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small");
+  } else {
+    need(out, at::kBFloat16, "out");
+    TORCH_CHECK(out.numel() >= M * (epi == 2 ? N / 2 : N), "bf16 out too small");
+  }
+  check(lsa_gemm(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, nb, splitk, cur_stream()),
+        "gemm");
+}
+
+void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscale, int64_t N, at::Tensor& out,
+              int64_t epi, int64_t nb, int64_t splitk) {
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1, "wq must be a 1-byte GPU tensor");
+  need(wscale, at::kFloat, "wscale");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(wq.numel() == N * K, "fp8 weight numel mismatch");
+  check(lsa_fp8_gemm(x.data_ptr(), x.stride(0), M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(), epi,
+                     nb, splitk, cur_stream()),
+        "fp8_gemm");
+}
+
+void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t nparts, int64_t part_stride,
+                 const c10::optional<at::Tensor>& ids, const c10::optional<at::Tensor>& emb,
+                 const c10::optional<at::Tensor>& row_idx, bool write_h, const at::Tensor& w, double eps,
+                 at::Tensor& xn, int64_t rows) {
+  need(h, at::kFloat, "h");
+  need(w, at::kBFloat16, "w");
+  need(xn, at::kBFloat16, "xn");
+  const int D = w.numel();
+  check(lsa_add_rmsnorm(h.data_ptr<float>(), ptr<const float>(parts), parts.has_value() ? nparts : 0, part_stride,
+                        ptr<const int>(ids), ptr<const void>(emb), ptr<const int>(row_idx), write_h ? 1 : 0,
+                        w.data_ptr(), (float)eps, xn.data_ptr(), rows, D, cur_stream()),
+        "add_rmsnorm");
+}
+
+void rope_append(const at::Tensor& qkv, const at::Tensor& pos, const c10::optional<at::Tensor>& tok_seq,
+                 const at::Tensor& block_tables, const at::Tensor& cos_t, const at::Tensor& sin_t, at::Tensor& q_out,
+                 at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv) {
+  need(qkv, at::kBFloat16, "qkv");
+  need(pos, at::kInt, "pos");
+  need(block_tables, at::kInt, "block_tables");
+  const int T = qkv.size(0);
+  check(lsa_rope_append(qkv.data_ptr(), pos.data_ptr<int>(), ptr<const int>(tok_seq), block_tables.data_ptr<int>(),
+                        block_tables.size(1), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), q_out.data_ptr(),
+                        kc.data_ptr(), vc.data_ptr(), T, H, Hkv, cur_stream()),
+        "rope_append");
+}
+
+void silu_mul(const at::Tensor& g, const at::Tensor& u, at::Tensor& o) {
+  need(g, at::kBFloat16, "g");
+  check(lsa_silu_mul(g.data_ptr(), u.data_ptr(), o.data_ptr(), g.numel(), cur_stream()), "silu_mul");
+}
+
+void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
+                 const at::Tensor& pos, int64_t H, int64_t Hkv, double scale, int64_t chunk_blocks, int64_t nsplit,
+                 at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart) {
+  need(q, at::kBFloat16, "q");
+  need(pos, at::kInt, "pos");
+  const int B = pos.size(0);
+  check(lsa_attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
+                        block_tables.size(1), pos.data_ptr<int>(), B, H, Hkv, (float)scale, chunk_blocks, nsplit,
+                        out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), cur_stream()),
+        "attn_decode");
+}
+
+void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
+                  const at::Tensor& cu_q, const at::Tensor& ctx_lens, const at::Tensor& work, int64_t H, int64_t Hkv,
+                  double scale, at::Tensor& out) {
+  need(q, at::kBFloat16, "q");
+  need(work, at::kInt, "work");
+  check(lsa_attn_prefill(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
+                         block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
+                         work.size(0), H, Hkv, (float)scale, out.data_ptr(), cur_stream()),
+        "attn_prefill");
+}
+
+void argmax_commit(const at::Tensor& logits, at::Tensor& part, at::Tensor& out_tokens, at::Tensor& gen_len,
+                   at::Tensor& input_ids, at::Tensor& positions, at::Tensor& finished, const at::Tensor& eos) {
+  need(logits, at::kFloat, "logits");
+  const int B = logits.size(0), V = logits.size(1);
+  check(lsa_argmax_commit(logits.data_ptr<float>(), B, V, reinterpret_cast<unsigned long long*>(part.data_ptr()),
+                          out_tokens.data_ptr<int>(), out_tokens.size(1), gen_len.data_ptr<int>(),
+                          input_ids.data_ptr<int>(), positions.data_ptr<int>(), finished.data_ptr<int>(),
+                          eos.data_ptr<int>(), eos.numel(), cur_stream()),
+        "argmax_commit");
+}
+
+void sample_commit(at::Tensor& logits, at::Tensor& part, at::Tensor& cand, const c10::optional<at::Tensor>& hist,
+                   const c10::optional<at::Tensor>& penalty, const at::Tensor& temperature, const at::Tensor& top_k,
+                   const at::Tensor& top_p, const at::Tensor& seeds, at::Tensor& out_tokens, at::Tensor& gen_len,
+                   at::Tensor& input_ids, at::Tensor& positions, at::Tensor& finished, const at::Tensor& eos) {
+  need(logits, at::kFloat, "logits");
+  const int B = logits.size(0), V = logits.size(1);
+  const int window = hist.has_value() ? hist->size(1) : 0;
+  check(lsa_sample_commit(logits.data_ptr<float>(), B, V, reinterpret_cast<unsigned long long*>(part.data_ptr()),
+                          reinterpret_cast<unsigned long long*>(cand.data_ptr()), ptr<const int>(hist), window,
+                          ptr<const float>(penalty), temperature.data_ptr<float>(), top_k.data_ptr<int>(),
+                          top_p.data_ptr<float>(), reinterpret_cast<const unsigned long long*>(seeds.data_ptr()),
+                          out_tokens.data_ptr<int>(), out_tokens.size(1), gen_len.data_ptr<int>(),
+                          input_ids.data_ptr<int>(), positions.data_ptr<int>(), finished.data_ptr<int>(),
+                          eos.data_ptr<int>(), eos.numel(), cur_stream()),
+        "sample_commit");
+}
+
+void fp8_dequant(const at::Tensor& wq, const at::Tensor& wscale, int64_t N, int64_t K, at::Tensor& wf) {
+  need(wscale, at::kFloat, "wscale");
+  need(wf, at::kBFloat16, "wf");
+  TORCH_CHECK(wq.numel() == N * K && wf.numel() >= N * K, "fp8_dequant size mismatch");
+  check(lsa_fp8_dequant(wq.data_ptr(), wscale.data_ptr<float>(), N, K, wf.data_ptr(), cur_stream()), "fp8_dequant");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels for the MI355X NL->SQL / Spark-error inference engine";
+  m.def("gemm", &gemm);
+  m.def("fp8_gemm", &fp8_gemm);
+  m.def("add_rmsnorm", &add_rmsnorm);
+  m.def("rope_append", &rope_append);
+  m.def("silu_mul", &silu_mul);
+  m.def("attn_decode", &attn_decode);
+  m.def("attn_prefill", &attn_prefill);
+  m.def("argmax_commit", &argmax_commit);
+  m.def("sample_commit", &sample_commit);
+  m.def("fp8_dequant", &fp8_dequant);
+  m.attr("arch") = "gfx950";
+}

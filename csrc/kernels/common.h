@@ -1,0 +1,90 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of this package.
+//
+// Everything here is written for wave64 + MFMA 16x16x32 bf16.  Conventions used by every
+// kernel in this directory:
+//   * bf16 tensors travel as raw uint16 bit patterns (uint16_t / uint4 = 8 bf16);
+//   * the MFMA "fragment" of a 16x32 operand tile is 64 lanes x 16 B: lane l holds row (l & 15),
+//     k-columns 8*(l >> 4) .. 8*(l >> 4) + 7 (cdna_hip_programming.md §3 operand maps);
+//   * the D (accumulator) map of mfma_f32_16x16x32_bf16 is D[row = 4*(l >> 4) + i][col = l & 15].
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// non-temporal 16-byte load (weights streamed once per forward: 'nt-weights' in MI355X_MICROARCH.md)
+__device__ __forceinline__ uint4 ldg_nt(const uint4* p) {
+  u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+#define LSA_WAVE 64
+
+__device__ __forceinline__ float bf2f(uint32_t h16) { return __uint_as_float(h16 << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // RNE, lowers to v_cvt_pk_bf16_f32 on gfx950
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// 8 bf16 (one uint4) -> 8 floats
+__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack2bf(f[0], f[1]); r.y = pack2bf(f[2], f[3]);
+  r.z = pack2bf(f[4], f[5]); r.w = pack2bf(f[6], f[7]);
+  return r;
+}
+
+__device__ __forceinline__ f32x4_t mfma16x16x32(const uint4 a, const uint4 b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+// Orderable 32-bit key of a float (larger float -> larger unsigned key).
+__device__ __forceinline__ uint32_t float_key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_float(uint32_t k) {
+  const uint32_t mask = (uint32_t)((int32_t)k >> 31);  // all ones iff the sign bit of the key is set
+  return __uint_as_float(k ^ (~mask | 0x80000000u));
+}

@@ -1,0 +1,323 @@
+// Linear layers on MFMA for gfx950:  out[M, N] = X[M, K] @ W[N, K]^T   (bf16 in, f32 accumulate)
+//
+// Weights live in the "fragment-major" layout produced by ops.shuffle_weight():
+//     Wf[nb][kb][lane][8 bf16]  with  nb = n / 16, kb = k / 32, lane = 16 * ((k % 32) / 8) + n % 16
+// i.e. one 1 KiB MFMA A-fragment (16 rows x 32 k) per (nb, kb), lane-linear.  Every weight load
+// is therefore a fully coalesced 1 KiB wave-instruction (global_load_dwordx4) and, in the tiled
+// kernel, a lane-linear global_load_lds_dwordx4 whose LDS image is read back with conflict-free
+// ds_read_b128 at lane*16 (no swizzle needed: cdna_hip_programming.md §5 Caveat / rule 21).
+//
+// Two kernels:
+//   * gemm_skinny  — decode (M <= 64).  Memory-bound weight stream: 8 waves/WG split K, each wave
+//     keeps 16 x 1 KiB weight fragments in flight straight into VGPRs (no LDS round trip, the
+//     'GEMV / M <= 16 decode weights' row of the guide), non-temporal weight loads, cross-wave
+//     reduction through LDS, fused epilogues (bf16 store, f32 split-K slab for the following
+//     residual+RMSNorm kernel, SiLU(gate)*up for the interleaved gate_up projection).
+//   * gemm_tile    — prefill (M > 64).  128x128x64 LDS tile, both operands staged by
+//     global_load_lds (16 B), double-buffered, 4 waves of 64x64.
+//
+// Epilogue modes: EPI_BF16 -> bf16 [M, N];  EPI_F32 -> f32 [splitk][M][N];
+//                 EPI_SILU -> bf16 [M, N/2] = silu(gate) * up, gate/up rows interleaved per 16.
+#include "common.h"
+
+#define EPI_BF16 0
+#define EPI_F32 1
+#define EPI_SILU 2
+
+template <int EPI>
+__device__ __forceinline__ void store4(void* out, int ldo, size_t slab, int m, int n, f32x4_t v) {
+  if constexpr (EPI == EPI_F32) {
+    float* o = reinterpret_cast<float*>(out) + slab + (size_t)m * ldo + n;
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    uint16_t* o = reinterpret_cast<uint16_t*>(out) + (size_t)m * ldo + n;
+    uint2 p;
+    p.x = pack2bf(v[0], v[1]);
+    p.y = pack2bf(v[2], v[3]);
+    *reinterpret_cast<uint2*>(o) = p;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// decode / small-M kernel
+// ------------------------------------------------------------------------------------------------
+template <int MT, int NB, int EPI>
+__global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
+                                                          int KB, const uint4* __restrict__ Wf,
+                                                          void* __restrict__ out, int ldo,
+                                                          int kb_per_split) {
+  constexpr int WAVES = 8;
+  constexpr int U = 16 / NB;  // weight fragments in flight per wave = NB * U = 16
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int nb0 = blockIdx.x * NB;
+  const int kbA = blockIdx.y * kb_per_split;
+  const int kbB = min(KB, kbA + kb_per_split);
+  const int nk = kbB - kbA;
+  const int kw0 = kbA + (nk * w) / WAVES;
+  const int kw1 = kbA + (nk * (w + 1)) / WAVES;
+
+  f32x4_t acc[NB][MT];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const uint16_t* xp[MT];
+  bool xvalid[MT];
+#pragma unroll
+  for (int j = 0; j < MT; ++j) {
+    const int m = j * 16 + r;
+    xvalid[j] = m < M;
+    xp[j] = X + (size_t)(xvalid[j] ? m : 0) * ldx + 8 * g;
+  }
+  const uint4* wp[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) wp[i] = Wf + (size_t)(nb0 + i) * KB * 64 + lane;
+
+  for (int kb = kw0; kb < kw1; kb += U) {
+    uint4 wr[U][NB];
+    uint4 xr[U][MT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = min(kb + u, kw1 - 1);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = min(kb + u, kw1 - 1);
+#pragma unroll
+      for (int j = 0; j < MT; ++j) xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * 32);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool live = (kb + u) < kw1;
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const bool ok = live && xvalid[j];
+        uint4 xv = xr[u][j];
+        xv.x = ok ? xv.x : 0u; xv.y = ok ? xv.y : 0u; xv.z = ok ? xv.z : 0u; xv.w = ok ? xv.w : 0u;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) acc[i][j] = mfma16x16x32(wr[u][i], xv, acc[i][j]);
+      }
+    }
+  }
+
+  // cross-wave reduction: red[w][tile][lane]
+  __shared__ __attribute__((aligned(16))) f32x4_t red[WAVES][NB * MT][64];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) red[w][i * MT + j][lane] = acc[i][j];
+  __syncthreads();
+
+  if constexpr (EPI == EPI_SILU) {
+    for (int idx = threadIdx.x; idx < (NB / 2) * MT * 64; idx += 64 * WAVES) {
+      const int l = idx & 63;
+      const int t = idx >> 6;
+      const int j = t % MT, p = t / MT;
+      f32x4_t gs = red[0][(2 * p) * MT + j][l], us = red[0][(2 * p + 1) * MT + j][l];
+#pragma unroll
+      for (int ww = 1; ww < WAVES; ++ww) {
+        gs += red[ww][(2 * p) * MT + j][l];
+        us += red[ww][(2 * p + 1) * MT + j][l];
+      }
+      const int m = j * 16 + (l & 15);
+      if (m < M) {
+        const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
+        f32x4_t v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = silu(gs[q]) * us[q];
+        store4<EPI_SILU>(out, ldo, 0, m, n, v);
+      }
+    }
+  } else {
+    const size_t slab = (size_t)blockIdx.y * M * ldo;
+    for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
+      const int l = idx & 63;
+      const int t = idx >> 6;
+      const int j = t % MT, i = t / MT;
+      f32x4_t s = red[0][t][l];
+#pragma unroll
+      for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
+      const int m = j * 16 + (l & 15);
+      if (m < M) store4<EPI>(out, ldo, slab, m, (nb0 + i) * 16 + 4 * (l >> 4), s);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// prefill / large-M kernel: 128 (N) x 128 (M) x 64 (K) tile, 4 waves (2 x 2) of 64 x 64
+// ------------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void glds16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)l, 16, 0, 0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
+                                                        const uint4* __restrict__ Wf, int NBtot,
+                                                        void* __restrict__ out, int ldo) {
+  // [stage][operand 0 = W, 1 = X][frag = sub * 2 + kf][lane]
+  __shared__ __attribute__((aligned(16))) uint4 lds[2][2][16][64];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int nbase = blockIdx.x * 8;
+  const int mbase = blockIdx.y * 128;
+
+  // staging sources: this wave stages frags f = 4w .. 4w+3 of each operand
+  const uint4* wsrc[4];
+  const uint16_t* xsrc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int f = 4 * w + q;
+    const int sub = f >> 1, kf = f & 1;
+    const int nb = min(nbase + sub, NBtot - 1);
+    wsrc[q] = Wf + ((size_t)nb * KB + kf) * 64 + lane;
+    const int m = min(mbase + sub * 16 + (lane & 15), M - 1);
+    xsrc[q] = X + (size_t)m * ldx + kf * 32 + 8 * (lane >> 4);
+  }
+
+  auto stage = [&](int st, int kb0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = 4 * w + q;
+      const int kf = f & 1;
+      const int kbo = min(kb0 + kf, KB - 1) - kf;  // clamp the odd tail fragment (masked in compute)
+      glds16(wsrc[q] + (size_t)kbo * 64, &lds[st][0][f][0]);
+      glds16(xsrc[q] + (size_t)kbo * 32, &lds[st][1][f][0]);
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int T = (KB + 1) >> 1;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const int st = t & 1;
+    if (t + 1 < T) stage(st ^ 1, 2 * (t + 1));
+    const int nkf = min(2, KB - 2 * t);
+#pragma unroll
+    for (int kf = 0; kf < 2; ++kf) {
+      if (kf < nkf) {
+        uint4 a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = lds[st][0][(wn * 4 + i) * 2 + kf][lane];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = lds[st][1][(wm * 4 + j) * 2 + kf][lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const int g = lane >> 4;
+  if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+      const int nb = nbase + wn * 4 + i;  // even -> gate block, nb + 1 -> up block
+      if (nb + 1 >= NBtot) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mbase + (wm * 4 + j) * 16 + (lane & 15);
+        if (m >= M) continue;
+        f32x4_t v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = silu(acc[i][j][q]) * acc[i + 1][j][q];
+        store4<EPI_SILU>(out, ldo, 0, m, (nb >> 1) * 16 + 4 * g, v);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nb = nbase + wn * 4 + i;
+      if (nb >= NBtot) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mbase + (wm * 4 + j) * 16 + (lane & 15);
+        if (m >= M) continue;
+        store4<EPI>(out, ldo, 0, m, nb * 16 + 4 * g, acc[i][j]);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------------
+template <int MT, int NB, int EPI>
+static void launch_skinny_t(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
+                            int ldo, int splitk, hipStream_t s) {
+  const int kbps = (KB + splitk - 1) / splitk;
+  dim3 grid(NBtot / NB, splitk);
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI>), grid, dim3(512), 0, s, X, ldx, M, KB, Wf, out, ldo, kbps);
+}
+
+template <int EPI>
+static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
+                            int ldo, int nb, int splitk, hipStream_t s) {
+  const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+#define LSA_SK(MTV, NBV)                                                                         \
+  if (mt == MTV && nb == NBV) {                                                                  \
+    launch_skinny_t<MTV, NBV, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);               \
+    return;                                                                                      \
+  }
+  LSA_SK(1, 2) LSA_SK(1, 4) LSA_SK(2, 2) LSA_SK(2, 4) LSA_SK(4, 2)
+  if constexpr (EPI != EPI_SILU) { LSA_SK(1, 1) LSA_SK(2, 1) LSA_SK(4, 1) }
+#undef LSA_SK
+  // fallback (nb=4 with mt=4 or unsupported): use nb=2
+  launch_skinny_t<4, 2, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);
+}
+
+extern "C" int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
+                        int splitk, hipStream_t stream) {
+  if (K % 32 != 0 || N % 16 != 0 || M <= 0) return -1;
+  const int KB = K / 32, NBtot = N / 16;
+  const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
+  const uint4* w = reinterpret_cast<const uint4*>(Wf);
+  const int ldo = (epi == EPI_SILU) ? N / 2 : N;
+  if (M <= 64) {
+    if (nb <= 0) nb = 1;
+    if (epi == EPI_SILU && nb < 2) nb = 2;
+    if (NBtot % nb != 0) return -2;
+    if (splitk < 1) splitk = 1;
+    if (epi != EPI_F32 && splitk != 1) return -3;
+    if (M > 32 && nb > 2) nb = 2;
+    switch (epi) {
+      case EPI_BF16: launch_skinny_e<EPI_BF16>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
+      case EPI_F32: launch_skinny_e<EPI_F32>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
+      case EPI_SILU: launch_skinny_e<EPI_SILU>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
+      default: return -4;
+    }
+  } else {
+    if (splitk != 1) return -3;
+    dim3 grid((NBtot + 7) / 8, (M + 127) / 128);
+    switch (epi) {
+      case EPI_BF16:
+        hipLaunchKernelGGL(gemm_tile_kernel<EPI_BF16>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo);
+        break;
+      case EPI_F32:
+        hipLaunchKernelGGL(gemm_tile_kernel<EPI_F32>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo);
+        break;
+      case EPI_SILU:
+        hipLaunchKernelGGL(gemm_tile_kernel<EPI_SILU>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo);
+        break;
+      default: return -4;
+    }
+  }
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,241 @@
+// fp8 (OCP e4m3fn, gfx950-native) weight-only linear layers:  out = X[M,K] @ (Wq[N,K] * scale[n])^T
+//
+// Weight layout (ops.shuffle_weight_fp8): Wq[nb][kb64][lane][16 B], lane = 16*g + r holds
+// W[16*nb + r][64*kb64 + 16*g + 0..15].  One 16 B load per lane = 1 KiB per wave-instruction feeds TWO
+// mfma_f32_16x16x32_bf16 k-steps: step 0 uses k-slots 16g + 0..7, step 1 uses 16g + 8..15 (the k order
+// inside an MFMA step only has to agree between A and B, so the activation fragment of lane (m, g) is
+// simply x[m][64*kb64 + 16g .. +15] as two uint4).  fp8 -> bf16 with v_cvt_scalef32_pk_bf16_fp8
+// (one VALU op per 2 weights, far below the HBM-bound budget), per-output-channel scale in the epilogue.
+// Decode therefore streams half the bytes of the bf16 path.  For prefill (M > 64) the layer is
+// dequantised (lsa_fp8_dequant) into a bf16 fragment-layout scratch buffer owned by the caller
+// and run through gemm_tile.
+#include "common.h"
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+template <bool HI>
+__device__ __forceinline__ uint32_t cvt2(uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w, 1.0f, HI));
+}
+// 16 fp8 -> two bf16 fragments (k-slots 0..7 and 8..15)
+__device__ __forceinline__ void fp8x16_to_bf16(const uint4 q, uint4& a, uint4& b) {
+  a.x = cvt2<false>(q.x); a.y = cvt2<true>(q.x); a.z = cvt2<false>(q.y); a.w = cvt2<true>(q.y);
+  b.x = cvt2<false>(q.z); b.y = cvt2<true>(q.z); b.z = cvt2<false>(q.w); b.w = cvt2<true>(q.w);
+}
+
+#define EPI_BF16 0
+#define EPI_F32 1
+#define EPI_SILU 2
+
+template <int MT, int NB, int EPI>
+__global__ __launch_bounds__(512) void gemm_fp8_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB64,
+                                                              const uint4* __restrict__ Wq,
+                                                              const float* __restrict__ wscale,
+                                                              void* __restrict__ out, int ldo, int kb_per_split) {
+  constexpr int WAVES = 8;
+  constexpr int U = 16 / NB;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int nb0 = blockIdx.x * NB;
+  const int kbA = blockIdx.y * kb_per_split;
+  const int kbB = min(KB64, kbA + kb_per_split);
+  const int nk = kbB - kbA;
+  const int kw0 = kbA + (nk * w) / WAVES;
+  const int kw1 = kbA + (nk * (w + 1)) / WAVES;
+
+  f32x4_t acc[NB][MT];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const uint16_t* xp[MT];
+  bool xvalid[MT];
+#pragma unroll
+  for (int j = 0; j < MT; ++j) {
+    const int m = j * 16 + r;
+    xvalid[j] = m < M;
+    xp[j] = X + (size_t)(xvalid[j] ? m : 0) * ldx + 16 * g;
+  }
+  const uint4* wp[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) wp[i] = Wq + (size_t)(nb0 + i) * KB64 * 64 + lane;
+
+  for (int kb = kw0; kb < kw1; kb += U) {
+    uint4 wr[U][NB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = min(kb + u, kw1 - 1);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = min(kb + u, kw1 - 1);
+      const bool live = (kb + u) < kw1;
+      uint4 x0[MT], x1[MT];
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const uint4* px = reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * 64);
+        x0[j] = px[0];
+        x1[j] = px[1];
+        const bool ok = live && xvalid[j];
+        x0[j].x = ok ? x0[j].x : 0u; x0[j].y = ok ? x0[j].y : 0u; x0[j].z = ok ? x0[j].z : 0u; x0[j].w = ok ? x0[j].w : 0u;
+        x1[j].x = ok ? x1[j].x : 0u; x1[j].y = ok ? x1[j].y : 0u; x1[j].z = ok ? x1[j].z : 0u; x1[j].w = ok ? x1[j].w : 0u;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        uint4 a0, a1;
+        fp8x16_to_bf16(wr[u][i], a0, a1);
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+          acc[i][j] = mfma16x16x32(a0, x0[j], acc[i][j]);
+          acc[i][j] = mfma16x16x32(a1, x1[j], acc[i][j]);
+        }
+      }
+    }
+  }
+
+  __shared__ __attribute__((aligned(16))) f32x4_t red[WAVES][NB * MT][64];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) red[w][i * MT + j][lane] = acc[i][j];
+  __syncthreads();
+
+  if constexpr (EPI == EPI_SILU) {
+    for (int idx = threadIdx.x; idx < (NB / 2) * MT * 64; idx += 64 * WAVES) {
+      const int l = idx & 63, t = idx >> 6;
+      const int j = t % MT, p = t / MT;
+      f32x4_t gs = red[0][(2 * p) * MT + j][l], us = red[0][(2 * p + 1) * MT + j][l];
+#pragma unroll
+      for (int ww = 1; ww < WAVES; ++ww) {
+        gs += red[ww][(2 * p) * MT + j][l];
+        us += red[ww][(2 * p + 1) * MT + j][l];
+      }
+      const int m = j * 16 + (l & 15);
+      if (m < M) {
+        const int nrow_g = (nb0 + 2 * p) * 16 + 4 * (l >> 4);
+        const int nrow_u = nrow_g + 16;
+        const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
+        uint2 pk;
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = silu(gs[q] * wscale[nrow_g + q]) * (us[q] * wscale[nrow_u + q]);
+        pk.x = pack2bf(v[0], v[1]);
+        pk.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + (size_t)m * ldo + n) = pk;
+      }
+    }
+  } else {
+    const size_t slab = (size_t)blockIdx.y * M * ldo;
+    for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
+      const int l = idx & 63, t = idx >> 6;
+      const int j = t % MT, i = t / MT;
+      f32x4_t s = red[0][t][l];
+#pragma unroll
+      for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
+      const int m = j * 16 + (l & 15);
+      if (m >= M) continue;
+      const int n = (nb0 + i) * 16 + 4 * (l >> 4);
+      const float4 sc = *reinterpret_cast<const float4*>(wscale + n);
+      s[0] *= sc.x; s[1] *= sc.y; s[2] *= sc.z; s[3] *= sc.w;
+      if constexpr (EPI == EPI_F32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + slab + (size_t)m * ldo + n) =
+            make_float4(s[0], s[1], s[2], s[3]);
+      } else {
+        uint2 pk;
+        pk.x = pack2bf(s[0], s[1]);
+        pk.y = pack2bf(s[2], s[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + (size_t)m * ldo + n) = pk;
+      }
+    }
+  }
+}
+
+// fp8 [nb][kb64][lane][16] -> bf16 fragment layout [nb][kb32][lane][8] with the channel scale applied
+__global__ __launch_bounds__(256) void fp8_dequant_kernel(const uint4* __restrict__ Wq, const float* __restrict__ wscale,
+                                                          int KB64, long nfrag, uint4* __restrict__ Wf) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nfrag * 64; i += (long)gridDim.x * blockDim.x) {
+    const int lane = (int)(i & 63);
+    const long f = i >> 6;  // (nb, kb64)
+    const long nb = f / KB64;
+    const int kb64 = (int)(f % KB64);
+    const int r = lane & 15, g = lane >> 4;
+    const float sc = wscale[nb * 16 + r];
+    uint4 a0, a1;
+    fp8x16_to_bf16(Wq[i], a0, a1);
+    // elements k = 64*kb64 + 16g + e  (e = 0..15) -> bf16 fragment kb32 = 2*kb64 + (16g + e) / 32,
+    // lane' = 16 * (((16g + e) % 32) / 8) + r
+    float f0[8], f1[8];
+    unpack8(a0, f0);
+    unpack8(a1, f1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { f0[j] *= sc; f1[j] *= sc; }
+    const int k0 = 16 * g;  // e = 0..7 -> k0 .. k0+7 ; e = 8..15 -> k0+8 ..
+    const long kb32 = 2 * kb64 + (k0 >> 5);
+    const int lane0 = 16 * ((k0 & 31) >> 3) + r;
+    const int lane1 = 16 * (((k0 + 8) & 31) >> 3) + r;
+    Wf[((nb * (2L * KB64)) + kb32) * 64 + lane0] = pack8(f0);
+    Wf[((nb * (2L * KB64)) + kb32) * 64 + lane1] = pack8(f1);
+  }
+}
+
+template <int MT, int NB, int EPI>
+static void launch_t(const uint16_t* X, int ldx, int M, int KB64, const uint4* Wq, const float* sc, int NBtot, void* out,
+                     int ldo, int splitk, hipStream_t s) {
+  const int kbps = (KB64 + splitk - 1) / splitk;
+  hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI>), dim3(NBtot / NB, splitk), dim3(512), 0, s, X, ldx, M, KB64, Wq,
+                     sc, out, ldo, kbps);
+}
+
+template <int EPI>
+static void launch_e(const uint16_t* X, int ldx, int M, int KB64, const uint4* Wq, const float* sc, int NBtot, void* out,
+                     int ldo, int nb, int splitk, hipStream_t s) {
+  const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+#define LSA_F8(MTV, NBV)                                                       \
+  if (mt == MTV && nb == NBV) {                                                \
+    launch_t<MTV, NBV, EPI>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, splitk, s); \
+    return;                                                                    \
+  }
+  LSA_F8(1, 2) LSA_F8(1, 4) LSA_F8(2, 2) LSA_F8(2, 4) LSA_F8(4, 2)
+  if constexpr (EPI != EPI_SILU) { LSA_F8(1, 1) LSA_F8(2, 1) LSA_F8(4, 1) }
+#undef LSA_F8
+  launch_t<4, 2, EPI>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, splitk, s);
+}
+
+extern "C" int lsa_fp8_dequant(const void* Wq, const float* wscale, int N, int K, void* Wf, hipStream_t s) {
+  if (K % 64 || N % 16) return -1;
+  const int KB64 = K / 64;
+  const long nfrag = (long)(N / 16) * KB64;
+  const long tot = nfrag * 64;
+  const long gl = (tot + 255) / 256;
+  hipLaunchKernelGGL(fp8_dequant_kernel, dim3((unsigned)(gl < 8192 ? gl : 8192)), dim3(256), 0, s,
+                     reinterpret_cast<const uint4*>(Wq), wscale, KB64, nfrag, reinterpret_cast<uint4*>(Wf));
+  return (int)hipGetLastError();
+}
+
+extern "C" int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
+                            int epi, int nb, int splitk, hipStream_t stream) {
+  if (K % 64 != 0 || N % 16 != 0 || M <= 0) return -1;
+  const int KB64 = K / 64, NBtot = N / 16;
+  const int ldo = (epi == EPI_SILU) ? N / 2 : N;
+  if (M <= 64) {
+    if (nb <= 0) nb = 1;
+    if (epi == EPI_SILU && nb < 2) nb = 2;
+    if (NBtot % nb != 0) return -2;
+    if (splitk < 1) splitk = 1;
+    if (epi != EPI_F32 && splitk != 1) return -3;
+    if (M > 32 && nb > 2) nb = 2;
+    const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
+    const uint4* w = reinterpret_cast<const uint4*>(Wq);
+    switch (epi) {
+      case EPI_BF16: launch_e<EPI_BF16>(x, ldx, M, KB64, w, wscale, NBtot, out, ldo, nb, splitk, stream); break;
+      case EPI_F32: launch_e<EPI_F32>(x, ldx, M, KB64, w, wscale, NBtot, out, ldo, nb, splitk, stream); break;
+      case EPI_SILU: launch_e<EPI_SILU>(x, ldx, M, KB64, w, wscale, NBtot, out, ldo, nb, splitk, stream); break;
+      default: return -4;
+    }
+    return (int)hipGetLastError();
+  }
+  return -6;  // M > 64: caller dequantises (lsa_fp8_dequant) and runs the bf16 tile GEMM
+}

@@ -1,0 +1,180 @@
+// Residual-stream kernels (memory-bound, vectorised 16 B / lane everywhere):
+//
+//   lsa_add_rmsnorm   h[r] (+)= emb[ids[r]] | sum_s parts[s][r];  xn[m] = rmsnorm(h[r]) * w   (bf16 out)
+//                     One kernel covers: embedding gather + first input norm, the split-K combine of
+//                     the O / down projections (f32 slabs written by gemm EPI_F32) + residual add +
+//                     next norm, and the final norm over gathered last-token rows (row_idx).
+//   lsa_rope_append   rotary embedding (rotate-half convention, cos/sin table from the host) of the
+//                     q and k heads of the fused QKV output + paged KV-cache append of k and v.
+//   lsa_silu_mul      standalone silu(g) * u for non-interleaved inputs.
+#include "common.h"
+
+// one workgroup per output row; D % 8 == 0; D <= 256 * 8 * 8
+template <int VPT>  // 8-element vectors per thread
+__global__ __launch_bounds__(256) void add_rmsnorm_kernel(float* __restrict__ h, const float* __restrict__ parts,
+                                                          int nparts, size_t part_stride, const int* __restrict__ ids,
+                                                          const uint16_t* __restrict__ emb,
+                                                          const int* __restrict__ row_idx, int write_h,
+                                                          const uint16_t* __restrict__ w, float eps,
+                                                          uint16_t* __restrict__ xn, int D) {
+  __shared__ float red[16];
+  const int m = blockIdx.x;
+  const int r = row_idx ? row_idx[m] : m;
+  float* hr = h + (size_t)r * D;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int c = (threadIdx.x + q * 256) * 8;
+    if (c < D) {
+      if (ids) {
+        const uint4 e = *reinterpret_cast<const uint4*>(emb + (size_t)ids[r] * D + c);
+        unpack8(e, v[q]);
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(hr + c);
+        const float4 b = *reinterpret_cast<const float4*>(hr + c + 4);
+        v[q][0] = a.x; v[q][1] = a.y; v[q][2] = a.z; v[q][3] = a.w;
+        v[q][4] = b.x; v[q][5] = b.y; v[q][6] = b.z; v[q][7] = b.w;
+      }
+      for (int s = 0; s < nparts; ++s) {
+        const float* p = parts + s * part_stride + (size_t)r * D + c;
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(p + 4);
+        v[q][0] += a.x; v[q][1] += a.y; v[q][2] += a.z; v[q][3] += a.w;
+        v[q][4] += b.x; v[q][5] += b.y; v[q][6] += b.z; v[q][7] += b.w;
+      }
+      if (write_h) {
+        *reinterpret_cast<float4*>(hr + c) = make_float4(v[q][0], v[q][1], v[q][2], v[q][3]);
+        *reinterpret_cast<float4*>(hr + c + 4) = make_float4(v[q][4], v[q][5], v[q][6], v[q][7]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[q][j] * v[q][j];
+    }
+  }
+  const float tot = block_sum(ss, red);
+  const float inv = rsqrtf(tot / (float)D + eps);
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int c = (threadIdx.x + q * 256) * 8;
+    if (c < D) {
+      float wf[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(w + c), wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[q][j] * inv * wf[j];
+      *reinterpret_cast<uint4*>(xn + (size_t)m * D + c) = pack8(o);
+    }
+  }
+}
+
+extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids,
+                               const void* emb, const int* row_idx, int write_h, const void* w, float eps, void* xn,
+                               int rows, int D, hipStream_t s) {
+  if (D % 8 != 0 || rows <= 0) return -1;
+  const int vpt = (D / 8 + 255) / 256;
+  const uint16_t* e = reinterpret_cast<const uint16_t*>(emb);
+  const uint16_t* ww = reinterpret_cast<const uint16_t*>(w);
+  uint16_t* o = reinterpret_cast<uint16_t*>(xn);
+#define LSA_RN(V)                                                                                            \
+  hipLaunchKernelGGL(add_rmsnorm_kernel<V>, dim3(rows), dim3(256), 0, s, h, parts, nparts, (size_t)part_stride, \
+                     ids, e, row_idx, write_h, ww, eps, o, D)
+  if (vpt <= 1) LSA_RN(1);
+  else if (vpt <= 2) LSA_RN(2);
+  else if (vpt <= 4) LSA_RN(4);
+  else if (vpt <= 8) LSA_RN(8);
+  else return -2;
+#undef LSA_RN
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// RoPE + paged KV append.  qkv: [T, (H + 2*Hkv) * 128]; q_out: [T, H, 128];
+// cache: [nblk, Hkv, 64, 128]; token t of sequence seq(t) at position pos(t) goes to
+// block_tables[seq * max_blocks + pos / 64], slot pos % 64.  cos/sin: [max_pos, 64] f32.
+// One workgroup per token; each thread rotates 4 (d, d+64) pairs (8 B loads of both halves).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rope_append_kernel(const uint16_t* __restrict__ qkv, const int* __restrict__ pos,
+                                                          const int* __restrict__ tok_seq,
+                                                          const int* __restrict__ block_tables, int max_blocks,
+                                                          const float* __restrict__ cos_t,
+                                                          const float* __restrict__ sin_t, uint16_t* __restrict__ q_out,
+                                                          uint16_t* __restrict__ kc, uint16_t* __restrict__ vc, int H,
+                                                          int Hkv) {
+  constexpr int D = 128;
+  const int t = blockIdx.x;
+  const int p = pos[t];
+  const int seq = tok_seq ? tok_seq[t] : t;
+  const int blk = block_tables[(size_t)seq * max_blocks + (p >> 6)];
+  const int off = p & 63;
+  const uint16_t* row = qkv + (size_t)t * (H + 2 * Hkv) * D;
+  const float* cr = cos_t + (size_t)p * (D / 2);
+  const float* sr = sin_t + (size_t)p * (D / 2);
+  // rotation work items: (head, quad) with quad = 4 consecutive d in [0, 64)
+  const int nrot = (H + Hkv) * 16;
+  for (int it = threadIdx.x; it < nrot; it += blockDim.x) {
+    const int hd = it >> 4, d0 = (it & 15) * 4;
+    const uint16_t* src = row + hd * D;
+    const uint2 lo = *reinterpret_cast<const uint2*>(src + d0);
+    const uint2 hi = *reinterpret_cast<const uint2*>(src + d0 + 64);
+    const float4 c = *reinterpret_cast<const float4*>(cr + d0);
+    const float4 s = *reinterpret_cast<const float4*>(sr + d0);
+    const float x0[4] = {bf2f(lo.x & 0xffff), bf2f(lo.x >> 16), bf2f(lo.y & 0xffff), bf2f(lo.y >> 16)};
+    const float x1[4] = {bf2f(hi.x & 0xffff), bf2f(hi.x >> 16), bf2f(hi.y & 0xffff), bf2f(hi.y >> 16)};
+    const float cc[4] = {c.x, c.y, c.z, c.w}, sn[4] = {s.x, s.y, s.z, s.w};
+    float y0[4], y1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      y0[j] = x0[j] * cc[j] - x1[j] * sn[j];
+      y1[j] = x1[j] * cc[j] + x0[j] * sn[j];
+    }
+    uint2 olo, ohi;
+    olo.x = pack2bf(y0[0], y0[1]); olo.y = pack2bf(y0[2], y0[3]);
+    ohi.x = pack2bf(y1[0], y1[1]); ohi.y = pack2bf(y1[2], y1[3]);
+    uint16_t* dst;
+    if (hd < H) {
+      dst = q_out + ((size_t)t * H + hd) * D;
+    } else {
+      dst = kc + (((size_t)blk * Hkv + (hd - H)) * 64 + off) * D;
+    }
+    *reinterpret_cast<uint2*>(dst + d0) = olo;
+    *reinterpret_cast<uint2*>(dst + d0 + 64) = ohi;
+  }
+  // v copy: Hkv * 16 chunks of 8 bf16
+  for (int it = threadIdx.x; it < Hkv * 16; it += blockDim.x) {
+    const int hv = it >> 4, c = (it & 15) * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(row + (H + Hkv + hv) * D + c);
+    *reinterpret_cast<uint4*>(vc + (((size_t)blk * Hkv + hv) * 64 + off) * D + c) = v;
+  }
+}
+
+extern "C" int lsa_rope_append(const void* qkv, const int* pos, const int* tok_seq, const int* block_tables,
+                               int max_blocks, const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc,
+                               int T, int H, int Hkv, hipStream_t s) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(rope_append_kernel, dim3(T), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(qkv), pos, tok_seq,
+                     block_tables, max_blocks, cos_t, sin_t, reinterpret_cast<uint16_t*>(q_out),
+                     reinterpret_cast<uint16_t*>(kc), reinterpret_cast<uint16_t*>(vc), H, Hkv);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void silu_mul_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u,
+                                                       uint16_t* __restrict__ o, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float a[8], b[8], c[8];
+    unpack8(reinterpret_cast<const uint4*>(g)[i], a);
+    unpack8(reinterpret_cast<const uint4*>(u)[i], b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = silu(a[j]) * b[j];
+    reinterpret_cast<uint4*>(o)[i] = pack8(c);
+  }
+}
+
+extern "C" int lsa_silu_mul(const void* g, const void* u, void* o, long n, hipStream_t s) {
+  if (n % 8) return -1;
+  const long n8 = n / 8;
+  const long gl = (n8 + 255) / 256;
+  const int grid = (int)(gl < 2048 ? gl : 2048);
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(g),
+                     reinterpret_cast<const uint16_t*>(u), reinterpret_cast<uint16_t*>(o), n8);
+  return (int)hipGetLastError();
+}

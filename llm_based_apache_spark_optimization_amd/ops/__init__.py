@@ -1,0 +1,282 @@
+"""Fused operators of the decode engine.
+
+GPU tensors run the hand-written gfx950 kernels of ``csrc/kernels`` through the in-tree extension
+``_lsa_hip``; there is no silent fallback — if the extension is missing while a GPU tensor is passed,
+the op raises.  CPU tensors run ``ops.reference`` (the fp32 oracle the GPU tests compare against) so
+the engine and its scheduler can be exercised on a machine without a GPU.
+
+Weights are held as :class:`PackedWeight`: on the GPU in the MFMA fragment-major layout
+(``shuffle_weight``) or fp8-e4m3fn with per-channel scales (``quantize_fp8``); on the CPU as the
+plain ``[N, K]`` matrix.
+"""
+from __future__ import annotations
+
+import dataclasses
+import importlib
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_ext = None
+_ext_err: Optional[BaseException] = None
+
+EPI = {"bf16": 0, "f32": 1, "silu": 2}
+
+
+def ext():
+    """The compiled gfx950 extension (raises if it cannot be loaded)."""
+    global _ext, _ext_err
+    if _ext is None and _ext_err is None:
+        try:
+            _ext = importlib.import_module(__name__ + "._lsa_hip")
+        except BaseException as e:  # noqa: BLE001 - record and re-raise on use
+            _ext_err = e
+    if _ext is None:
+        raise RuntimeError(
+            "gfx950 extension _lsa_hip is not built/loadable; run "
+            "`python -m llm_based_apache_spark_optimization_amd.ops.build`"
+        ) from _ext_err
+    return _ext
+
+
+def hip_available() -> bool:
+    try:
+        ext()
+        return True
+    except RuntimeError:
+        return False
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ----------------------------------------------------------------------------------- weights
+def shuffle_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] -> fragment-major [N/16, K/32, 64 lanes, 8]: lane = 16*((k%32)//8) + n%16."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 32 == 0, (N, K)
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+
+
+def unshuffle_weight(wf: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    return wf.reshape(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(N, K)
+
+
+def interleave_gate_up(wg: torch.Tensor, wu: torch.Tensor) -> torch.Tensor:
+    """Stack gate and up rows interleaved per 16 so one skinny-GEMM wave owns matching pairs."""
+    F, K = wg.shape
+    return torch.stack([wg.view(F // 16, 16, K), wu.view(F // 16, 16, K)], dim=1).reshape(2 * F, K)
+
+
+def quantize_fp8(w: torch.Tensor):
+    """Per-output-channel e4m3fn quantisation -> (packed uint8 [N/16, K/64, 64, 16], scale f32 [N])."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 64 == 0, (N, K)
+    wf = w.float()
+    scale = (wf.abs().amax(dim=1) / 448.0).clamp(min=1e-12)
+    q = (wf / scale[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    packed = q.view(torch.uint8).reshape(N // 16, 16, K // 64, 4, 16).permute(0, 2, 3, 1, 4).contiguous()
+    return packed, scale
+
+
+def dequantize_fp8(packed: torch.Tensor, scale: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    q = packed.reshape(N // 16, K // 64, 4, 16, 16).permute(0, 3, 1, 2, 4).reshape(N, K)
+    return q.view(torch.float8_e4m3fn).float() * scale[:, None]
+
+
+@dataclasses.dataclass
+class PackedWeight:
+    """A linear layer's weight in the layout its kernel streams."""
+
+    N: int
+    K: int
+    kind: str  # "dense" (CPU reference) | "bf16" (fragment layout) | "fp8"
+    data: torch.Tensor
+    scale: Optional[torch.Tensor] = None
+
+    @staticmethod
+    def from_dense(w: torch.Tensor, kind: str = "bf16") -> "PackedWeight":
+        N, K = w.shape
+        if not w.is_cuda:
+            return PackedWeight(N, K, "dense", w.to(torch.bfloat16).contiguous())
+        if kind == "fp8":
+            q, s = quantize_fp8(w)
+            return PackedWeight(N, K, "fp8", q, s.contiguous())
+        return PackedWeight(N, K, "bf16", shuffle_weight(w.to(torch.bfloat16)))
+
+    def dense(self) -> torch.Tensor:
+        if self.kind == "dense":
+            return self.data
+        if self.kind == "bf16":
+            return unshuffle_weight(self.data, self.N, self.K)
+        return dequantize_fp8(self.data, self.scale, self.N, self.K).to(torch.bfloat16)
+
+    @property
+    def nbytes(self) -> int:
+        return self.data.numel() * self.data.element_size()
+
+
+def pick_nb_splitk(M: int, N: int, K: int, epi: str) -> tuple[int, int]:
+    """Skinny-GEMM decomposition: >= ~2 workgroups per CU, split-K only for f32 slabs."""
+    nbt = N // 16
+    nb = 2 if (nbt % 2 == 0 and nbt // 2 >= 512) else 1
+    if epi == "silu":
+        nb = 2
+    if M > 32 and nb > 2:
+        nb = 2
+    splitk = 1
+    if epi == "f32":
+        wgs = nbt // nb
+        while wgs * splitk < 384 and splitk < 4 and K // (32 * splitk * 2) >= 16:
+            splitk *= 2
+    return nb, splitk
+
+
+# ----------------------------------------------------------------------------------- linear
+_dq_scratch: dict = {}
+
+
+def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
+           splitk: Optional[int] = None, nb: Optional[int] = None) -> torch.Tensor:
+    """y = x @ W^T with a fused epilogue.  epi='f32' returns [splitk, M, N] partial slabs."""
+    M, K = x.shape
+    assert K == w.K, (K, w.K)
+    if not _gpu(x):
+        y = ref.linear(x, w.dense(), epi)
+        if epi == "f32":
+            y = y.unsqueeze(0)
+        if out is not None:
+            out.view(-1)[: y.numel()].copy_(y.reshape(-1))
+            return out
+        return y
+    nb0, sk0 = pick_nb_splitk(M, w.N, K, epi)
+    nb = nb0 if nb is None else nb
+    splitk = sk0 if splitk is None else splitk
+    if M > 64:
+        splitk = 1
+    if out is None:
+        if epi == "f32":
+            out = torch.empty(splitk, M, w.N, device=x.device, dtype=torch.float32)
+        else:
+            out = torch.empty(M, w.N // 2 if epi == "silu" else w.N, device=x.device, dtype=torch.bfloat16)
+    e = ext()
+    if w.kind == "bf16":
+        e.gemm(x, w.data, w.N, out, EPI[epi], nb, splitk)
+    elif w.kind == "fp8":
+        if M <= 64:
+            e.fp8_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk)
+        else:
+            key = (x.device, w.N * w.K)
+            buf = _dq_scratch.get(x.device)
+            if buf is None or buf.numel() < w.N * w.K:
+                buf = torch.empty(w.N * w.K, device=x.device, dtype=torch.bfloat16)
+                _dq_scratch[x.device] = buf
+            e.fp8_dequant(w.data, w.scale, w.N, w.K, buf)
+            e.gemm(x, buf[: w.N * w.K], w.N, out, EPI[epi], nb, 1)
+            del key
+    else:
+        raise ValueError(f"weight kind {w.kind} on GPU")
+    return out
+
+
+# ----------------------------------------------------------------------------------- norms / rope
+def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
+                parts: Optional[torch.Tensor] = None, ids: Optional[torch.Tensor] = None,
+                emb: Optional[torch.Tensor] = None, row_idx: Optional[torch.Tensor] = None,
+                write_h: bool = True) -> torch.Tensor:
+    """h[r] (= emb[ids[r]]) (+= sum parts[:, r]); xn[m] = rmsnorm(h[row_idx[m]]) * w."""
+    if not _gpu(h):
+        return ref.add_rmsnorm(h, w, eps, xn, parts, ids, emb, row_idx, write_h)
+    nparts = parts.shape[0] if parts is not None else 0
+    stride = parts.stride(0) if parts is not None else 0
+    ext().add_rmsnorm(h, parts, nparts, stride, ids, emb, row_idx, write_h, w, eps, xn, xn.shape[0])
+    return xn
+
+
+def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv):
+    if not _gpu(qkv):
+        return ref.rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
+    ext().rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
+
+
+def silu_mul(g: torch.Tensor, u: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if out is None:
+        out = torch.empty_like(g)
+    if not _gpu(g):
+        out.copy_((torch.nn.functional.silu(g.float()) * u.float()).to(out.dtype))
+        return out
+    ext().silu_mul(g, u, out)
+    return out
+
+
+# ----------------------------------------------------------------------------------- attention
+def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int]:
+    """(chunk_blocks, nsplit) for split-KV decode: aim for >= 512 workgroups."""
+    nblk = max(1, (max_ctx + 63) // 64)
+    chunk = nblk
+    while chunk > 1 and B * Hkv * ((nblk + chunk - 1) // chunk) < 512:
+        chunk = (chunk + 1) // 2
+    return chunk, (nblk + chunk - 1) // chunk
+
+
+def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None):
+    """q [B,H,128] vs paged cache, context = pos + 1.  workspace = (opart, mlpart) for split-KV."""
+    if not _gpu(q):
+        return ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out)
+    B = pos.shape[0]
+    chunk, nsplit = plan if plan is not None else decode_split_plan(B, Hkv, block_tables.shape[1] * 64)
+    if workspace is None:
+        opart = torch.empty(B * H * nsplit * 128, device=q.device, dtype=torch.float32)
+        mlpart = torch.empty(B * H * nsplit * 2, device=q.device, dtype=torch.float32)
+    else:
+        opart, mlpart = workspace
+    ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart)
+    return out
+
+
+def prefill_work(cu_q: list[int], qblock: int = 64) -> list[tuple[int, int]]:
+    """(seq, q_start) work items, heaviest (latest) query blocks first for causal balance."""
+    items = []
+    for s in range(len(cu_q) - 1):
+        ql = cu_q[s + 1] - cu_q[s]
+        for qs in range(0, ql, qblock):
+            items.append((s, qs))
+    items.sort(key=lambda t: -t[1])
+    return items
+
+
+def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, work=None):
+    if not _gpu(q):
+        return ref.attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out)
+    if work is None:
+        work = torch.tensor(prefill_work(cu_q.tolist()), dtype=torch.int32).to(q.device)
+    ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, work, H, Hkv, scale, out)
+    return out
+
+
+# ----------------------------------------------------------------------------------- sampling
+def argmax_commit(logits, out_tokens, gen_len, input_ids, positions, finished, eos, part=None):
+    if not _gpu(logits):
+        return ref.argmax_commit(logits, out_tokens, gen_len, input_ids, positions, finished, eos)
+    B, V = logits.shape
+    if part is None:
+        part = torch.empty(B * ((V + 4095) // 4096), device=logits.device, dtype=torch.int64)
+    ext().argmax_commit(logits, part, out_tokens, gen_len, input_ids, positions, finished, eos)
+
+
+def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len, input_ids,
+                  positions, finished, eos, workspace=None):
+    if not _gpu(logits):
+        return ref.sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len,
+                                 input_ids, positions, finished, eos)
+    B, V = logits.shape
+    if workspace is None:
+        part = torch.empty(B * ((V + 4095) // 4096), device=logits.device, dtype=torch.int64)
+        cand = torch.empty(B * ((V + 2047) // 2048) * 64, device=logits.device, dtype=torch.int64)
+    else:
+        part, cand = workspace
+    ext().sample_commit(logits, part, cand, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len,
+                        input_ids, positions, finished, eos)
