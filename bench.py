@@ -1,0 +1,144 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: NL->SQL serving throughput + end-to-end latency on MI355X.
+
+Metric (BASELINE.json): output tokens/sec + p50 end-to-end latency, duckdb-nsql-7B (default) or
+Llama-3.2-3B (``--model llama3.2``).  One "step" = one complete serving round of ``--batch``
+requests per replica: packed prefill of synthetic ``--prompt-len``-token prompts + ``--new-tokens``
+greedy decode tokens (EOS ignored, so every request emits exactly that many tokens), i.e. the
+request's end-to-end latency.  Random-init weights of the named architecture (no checkpoints can be
+downloaded), bf16 (or ``--dtype fp8`` weights).
+
+    python bench.py                      # 1 GPU, defaults
+    torchrun --nproc-per-node 8 bench.py --gpus 8     # 8 DP replicas (``--tp 2``: 4 x TP2)
+
+Prints ONE JSON line on rank 0.  ``value`` = whole-job output tokens/s (sum over replicas, timed by
+the slowest rank); ``vs_baseline`` = value / 4.0 tok/s, the only throughput figure BASELINE.md
+derives for the reference (its measured numbers are latencies: ``vs_baseline_p50_latency`` =
+5.2381 s / our p50).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REF_TOK_S = 4.0        # "<= 4 tok/s end-to-end for duckdb-nsql" (derived)
+REF_P50_S = 5.2381     # duckdb-nsql p50 end-to-end latency, run B
+REF_P50_S_LLAMA = 22.7463
+
+MODEL_NAMES = {"duckdb-nsql": "duckdb-nsql-7B", "llama3.2": "Llama-3.2-3B-Instruct", "mistral": "Mistral-7B-v0.3"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="duckdb-nsql")
+    ap.add_argument("--batch", type=int, default=32, help="requests per replica per step")
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--new-tokens", type=int, default=128)
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--no-graphs", action="store_true")
+    args = ap.parse_args()
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from llm_based_apache_spark_optimization_amd.engine import build_engine, SamplingParams
+    from llm_based_apache_spark_optimization_amd.parallel import init_distributed, make_replica_groups
+
+    rank, world, local = init_distributed()
+    if not torch.cuda.is_available():
+        print("bench.py needs a GPU", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    tp = max(1, args.tp)
+    replica, tpg = make_replica_groups(world, tp, rank, device) if world > 1 else (0, None)
+    dp = world // tp
+
+    max_len = args.prompt_len + args.new_tokens + 64
+    eng = build_engine(args.model, device=str(device), dtype=args.dtype, max_slots=args.batch,
+                       max_model_len=max_len, seed=0, tp=tpg, use_graphs=not args.no_graphs,
+                       max_prefill_tokens=max(16384, args.batch * args.prompt_len))
+    V = eng.spec.vocab_size
+    g = torch.Generator().manual_seed(1234 + replica)
+    prompts = [[eng.spec.bos_id if eng.spec.bos_id < V else 1]
+               + torch.randint(3, V, (args.prompt_len - 1,), generator=g).tolist() for _ in range(args.batch)]
+    params = SamplingParams(max_tokens=args.new_tokens, temperature=0.0, ignore_eos=True)
+
+    def one_step():
+        res = eng.generate(prompts, params)
+        assert all(r.eval_count == args.new_tokens for r in res), [r.eval_count for r in res]
+        return res
+
+    for _ in range(args.warmup):
+        one_step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    lat = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s = time.perf_counter()
+        one_step()
+        lat.append(time.perf_counter() - s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], device=device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    tokens = dp * args.batch * args.new_tokens * args.steps
+    value = tokens / elapsed
+    p50 = statistics.median(lat)
+    ms_step = 1000.0 * elapsed / args.steps
+    decode_ms_tok = 1000.0 * eng.stats["decode_s"] / max(1, eng.stats["decode_steps"])
+    if rank == 0:
+        ref_p50 = REF_P50_S_LLAMA if args.model.startswith("llama") else REF_P50_S
+        par = f"dp{dp}" if tp == 1 else f"tp{tp}dp{dp}"
+        out = {
+            "metric": "output_tokens_per_sec",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / REF_TOK_S, 2),
+            "dtype": args.dtype if args.dtype == "bf16" else "fp8-weights/bf16-act",
+            "data": "synthetic prompts, random-init weights",
+            "config": {
+                "model": MODEL_NAMES.get(args.model, args.model),
+                "global_batch": dp * args.batch,
+                "seq_len": args.prompt_len + args.new_tokens,
+                "prompt_len": args.prompt_len,
+                "new_tokens": args.new_tokens,
+                "parallelism": par,
+                "decode": "greedy",
+            },
+            "p50_e2e_latency_s": round(p50, 4),
+            "vs_baseline_p50_latency": round(ref_p50 / p50, 2),
+            "decode_ms_per_token_step": round(decode_ms_tok, 3),
+            "per_gpu_tokens_per_sec": round(value / world, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

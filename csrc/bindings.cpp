@@ -23,11 +23,12 @@ int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* b
                      void* out, hipStream_t s);
 int lsa_argmax_commit(const float* logits, int B, int V, unsigned long long* part, int* out_tokens, int max_new,
                       int* gen_len, int* input_ids, int* positions, int* finished, const int* eos, int neos,
-                      hipStream_t s);
+                      const int* limit, const int* eos_on, hipStream_t s);
 int lsa_sample_commit(float* logits, int B, int V, unsigned long long* part, unsigned long long* cand, const int* hist,
                       int window, const float* penalty, const float* temperature, const int* top_k,
                       const float* top_p, const unsigned long long* seeds, int* out_tokens, int max_new, int* gen_len,
-                      int* input_ids, int* positions, int* finished, const int* eos, int neos, hipStream_t s);
+                      int* input_ids, int* positions, int* finished, const int* eos, int neos, const int* limit,
+                      const int* eos_on, hipStream_t s);
 int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out, int epi,
                  int nb, int splitk, hipStream_t stream);
 int lsa_fp8_dequant(const void* Wq, const float* wscale, int N, int K, void* Wf, hipStream_t s);
@@ -137,20 +138,22 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& v
 }
 
 void argmax_commit(const at::Tensor& logits, at::Tensor& part, at::Tensor& out_tokens, at::Tensor& gen_len,
-                   at::Tensor& input_ids, at::Tensor& positions, at::Tensor& finished, const at::Tensor& eos) {
+                   at::Tensor& input_ids, at::Tensor& positions, at::Tensor& finished, const at::Tensor& eos,
+                   const at::Tensor& limit, const at::Tensor& eos_on) {
   need(logits, at::kFloat, "logits");
   const int B = logits.size(0), V = logits.size(1);
   check(lsa_argmax_commit(logits.data_ptr<float>(), B, V, reinterpret_cast<unsigned long long*>(part.data_ptr()),
                           out_tokens.data_ptr<int>(), out_tokens.size(1), gen_len.data_ptr<int>(),
                           input_ids.data_ptr<int>(), positions.data_ptr<int>(), finished.data_ptr<int>(),
-                          eos.data_ptr<int>(), eos.numel(), cur_stream()),
+                          eos.data_ptr<int>(), eos.numel(), limit.data_ptr<int>(), eos_on.data_ptr<int>(), cur_stream()),
         "argmax_commit");
 }
 
 void sample_commit(at::Tensor& logits, at::Tensor& part, at::Tensor& cand, const c10::optional<at::Tensor>& hist,
                    const c10::optional<at::Tensor>& penalty, const at::Tensor& temperature, const at::Tensor& top_k,
                    const at::Tensor& top_p, const at::Tensor& seeds, at::Tensor& out_tokens, at::Tensor& gen_len,
-                   at::Tensor& input_ids, at::Tensor& positions, at::Tensor& finished, const at::Tensor& eos) {
+                   at::Tensor& input_ids, at::Tensor& positions, at::Tensor& finished, const at::Tensor& eos,
+                   const at::Tensor& limit, const at::Tensor& eos_on) {
   need(logits, at::kFloat, "logits");
   const int B = logits.size(0), V = logits.size(1);
   const int window = hist.has_value() ? hist->size(1) : 0;
@@ -160,7 +163,7 @@ void sample_commit(at::Tensor& logits, at::Tensor& part, at::Tensor& cand, const
                           top_p.data_ptr<float>(), reinterpret_cast<const unsigned long long*>(seeds.data_ptr()),
                           out_tokens.data_ptr<int>(), out_tokens.size(1), gen_len.data_ptr<int>(),
                           input_ids.data_ptr<int>(), positions.data_ptr<int>(), finished.data_ptr<int>(),
-                          eos.data_ptr<int>(), eos.numel(), cur_stream()),
+                          eos.data_ptr<int>(), eos.numel(), limit.data_ptr<int>(), eos_on.data_ptr<int>(), cur_stream()),
         "sample_commit");
 }
 

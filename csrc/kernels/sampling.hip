@@ -52,6 +52,8 @@ struct DecodeState {
   int* finished;    // [B]
   const int* eos;   // [neos]
   int neos;
+  const int* limit;   // [B] per-row max new tokens (<= max_new)
+  const int* eos_on;  // [B] 0 = ignore EOS for this row
 };
 
 __device__ void commit_token(const DecodeState& st, int b, int tok) {
@@ -59,8 +61,9 @@ __device__ void commit_token(const DecodeState& st, int b, int tok) {
   const int n = st.gen_len[b];
   if (n < st.max_new) st.out_tokens[(size_t)b * st.max_new + n] = tok;
   st.gen_len[b] = n + 1;
-  bool done = (n + 1) >= st.max_new;
-  for (int e = 0; e < st.neos; ++e) done |= (tok == st.eos[e]);
+  bool done = (n + 1) >= min(st.max_new, st.limit[b]);
+  if (st.eos_on[b])
+    for (int e = 0; e < st.neos; ++e) done |= (tok == st.eos[e]);
   st.input_ids[b] = tok;
   if (done) {
     st.finished[b] = 1;
@@ -226,11 +229,11 @@ __global__ __launch_bounds__(1024) void sample_commit_kernel(const unsigned long
 
 extern "C" int lsa_argmax_commit(const float* logits, int B, int V, unsigned long long* part, int* out_tokens,
                                  int max_new, int* gen_len, int* input_ids, int* positions, int* finished,
-                                 const int* eos, int neos, hipStream_t s) {
+                                 const int* eos, int neos, const int* limit, const int* eos_on, hipStream_t s) {
   const int chunk = 4096;
   const int nch = (V + chunk - 1) / chunk;
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(nch, B), dim3(256), 0, s, logits, V, chunk, part, nch);
-  DecodeState st{out_tokens, max_new, gen_len, input_ids, positions, finished, eos, neos};
+  DecodeState st{out_tokens, max_new, gen_len, input_ids, positions, finished, eos, neos, limit, eos_on};
   hipLaunchKernelGGL(argmax_commit_kernel, dim3(B), dim3(64), 0, s, part, nch, st);
   return (int)hipGetLastError();
 }
@@ -240,7 +243,8 @@ extern "C" int lsa_sample_commit(float* logits, int B, int V, unsigned long long
                                  const int* hist, int window, const float* penalty, const float* temperature,
                                  const int* top_k, const float* top_p, const unsigned long long* seeds,
                                  int* out_tokens, int max_new, int* gen_len, int* input_ids, int* positions,
-                                 int* finished, const int* eos, int neos, hipStream_t s) {
+                                 int* finished, const int* eos, int neos, const int* limit, const int* eos_on,
+                                 hipStream_t s) {
   if (hist && window > 0 && penalty)
     hipLaunchKernelGGL(repeat_penalty_kernel, dim3(B), dim3(64), 0, s, logits, V, hist, window, penalty);
   const int chunk = 4096;
@@ -252,7 +256,7 @@ extern "C" int lsa_sample_commit(float* logits, int B, int V, unsigned long long
   int p2 = 64;
   while (p2 < ncand) p2 <<= 1;
   if (p2 > 8192) return -1;  // V > 262144 unsupported
-  DecodeState st{out_tokens, max_new, gen_len, input_ids, positions, finished, eos, neos};
+  DecodeState st{out_tokens, max_new, gen_len, input_ids, positions, finished, eos, neos, limit, eos_on};
   hipLaunchKernelGGL(sample_commit_kernel, dim3(B), dim3(1024), p2 * sizeof(unsigned long long), s, cand, p2, ncand,
                      part, nch, temperature, top_k, top_p, seeds, st);
   return (int)hipGetLastError();

@@ -1,0 +1,244 @@
+"""LLMEngine: continuous-batching text generation over a ModelRunner.
+
+The request lifecycle mirrors what the reference gets from the Ollama daemon behind
+``ollama.generate(model=, system=, prompt=)`` (FastAPI/app.py:85-90,105-109; Flask/app.py:102-107,
+160-164; Model_Evaluation_&_Comparision.py:23,114): template -> tokenize -> prefill -> decode loop ->
+detokenize, with the timing fields Ollama reports (and the reference ignored).
+
+Scheduling is native (``runtime/_lsa_runtime.Scheduler``): FCFS admission into fixed decode slots
+with KV reserved for prompt + max_new tokens.  Each engine iteration prefills newly admitted
+requests (packed, one launch sequence) and then replays the captured decode graph for
+``sync_every`` steps before reading the finished flags back — the host touches the GPU once per
+``sync_every`` tokens, not once per token.
+"""
+from __future__ import annotations
+
+import dataclasses
+import itertools
+import threading
+import time
+from typing import Callable, Optional, Sequence
+
+import torch
+
+from ..models.templates import apply_stops, render
+from ..models.tokenizer import tokenizer_for
+from ..runtime import native
+from .runner import BLOCK, ModelRunner
+
+
+@dataclasses.dataclass
+class SamplingParams:
+    """Ollama-compatible options (temperature 0 = greedy, as the benchmark configs require)."""
+
+    max_tokens: int = 128
+    temperature: float = 0.0
+    top_k: int = 40
+    top_p: float = 0.9
+    seed: Optional[int] = None
+    ignore_eos: bool = False
+    stop: tuple = ()
+
+    @staticmethod
+    def from_ollama_options(opts: Optional[dict], default_max: int = 128) -> "SamplingParams":
+        opts = opts or {}
+        n = opts.get("num_predict", default_max)
+        if n is None or n < 0:
+            n = default_max
+        stop = opts.get("stop") or ()
+        return SamplingParams(max_tokens=int(n), temperature=float(opts.get("temperature", 0.0)),
+                              top_k=int(opts.get("top_k", 40)), top_p=float(opts.get("top_p", 0.9)),
+                              seed=opts.get("seed"), stop=tuple(stop))
+
+
+@dataclasses.dataclass
+class Request:
+    rid: int
+    prompt_ids: list
+    params: SamplingParams
+    arrival: float
+    admitted: float = 0.0
+    first_token: float = 0.0
+    finished_at: float = 0.0
+    output_ids: list = dataclasses.field(default_factory=list)
+    done: threading.Event = dataclasses.field(default_factory=threading.Event)
+    slot: int = -1
+    gen_host: int = 0  # generated-token count as of the last device sync
+    error: Optional[str] = None
+
+
+@dataclasses.dataclass
+class GenerationResult:
+    text: str
+    token_ids: list
+    prompt_tokens: int
+    eval_count: int
+    total_duration_ns: int
+    load_duration_ns: int
+    prompt_eval_duration_ns: int
+    eval_duration_ns: int
+    done_reason: str
+
+
+class LLMEngine:
+    def __init__(self, runner: ModelRunner, tokenizer=None, max_prefill_tokens: int = 16384, sync_every: int = 8,
+                 name: Optional[str] = None):
+        self.runner = runner
+        self.spec = runner.spec
+        self.name = name or self.spec.name
+        self.tok = tokenizer or tokenizer_for(self.spec)
+        tok_eos = [e for e in getattr(self.tok, "eos_ids", ()) if 0 <= e < self.spec.vocab_size]
+        if tok_eos and sorted(tok_eos) != sorted(runner.eos_list):
+            runner.set_eos(sorted(set(tok_eos) | set(e for e in runner.eos_list if e >= 0)))
+        self.sched = native.Scheduler(runner.num_kv_blocks, BLOCK, runner.max_slots, max_prefill_tokens,
+                                      runner.max_blocks)
+        self.sync_every = sync_every
+        self.max_prefill_tokens = max_prefill_tokens
+        self._ids = itertools.count(1)
+        self._reqs: dict[int, Request] = {}
+        self._lock = threading.RLock()
+        self._slot_owner: dict[int, int] = {}
+        self.load_time_s = 0.0
+        self.stats = {"requests": 0, "prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0,
+                      "prefill_s": 0.0, "decode_s": 0.0}
+
+    # -------------------------------------------------------------------------------- prompts
+    def render(self, prompt: str, system: str = "", raw: bool = False) -> str:
+        return prompt if raw else render(self.spec.template, prompt, system)
+
+    def encode(self, text: str) -> list[int]:
+        ids = self.tok.encode(text, add_bos=True)
+        limit = self.runner.max_model_len - 1
+        return ids[-limit:] if len(ids) > limit else ids
+
+    # -------------------------------------------------------------------------------- request API
+    def add_request(self, prompt_ids: Sequence[int], params: SamplingParams) -> Request:
+        room = self.runner.max_model_len - len(prompt_ids)
+        if room < 1:
+            raise ValueError("prompt longer than the model context")
+        p = dataclasses.replace(params, max_tokens=max(1, min(params.max_tokens, room, self.runner.max_new_cap)))
+        req = Request(next(self._ids), list(map(int, prompt_ids)), p, time.perf_counter())
+        with self._lock:
+            self.sched.add(req.rid, len(req.prompt_ids), p.max_tokens)
+            self._reqs[req.rid] = req
+        return req
+
+    def has_work(self) -> bool:
+        return self.sched.num_waiting > 0 or self.sched.num_running > 0
+
+    def step(self) -> list[Request]:
+        """One engine iteration: admit + prefill new requests, run decode steps, retire finished."""
+        r = self.runner
+        with self._lock:
+            admitted = self.sched.admit()
+            if admitted:
+                t0 = time.perf_counter()
+                seqs = []
+                any_sample = False
+                for rid in admitted:
+                    req = self._reqs[rid]
+                    slot = self.sched.slot(rid)
+                    req.slot, req.admitted = slot, t0
+                    self._slot_owner[slot] = rid
+                    sp = req.params
+                    seed = sp.seed if sp.seed is not None else (rid * 7919 + 17)
+                    r.set_slot(slot, self.sched.block_table(rid), sp.max_tokens, sp.temperature, sp.top_k, sp.top_p,
+                               seed, eos_on=not sp.ignore_eos)
+                    any_sample |= sp.temperature > 0
+                    seqs.append((slot, req.prompt_ids, 0))
+                self._prefill_packed(seqs, any_sample)
+                t1 = time.perf_counter()
+                for rid in admitted:
+                    self._reqs[rid].first_token = t1
+                    self._reqs[rid].gen_host = 1
+                self.stats["prefill_s"] += t1 - t0
+                self.stats["prompt_tokens"] += sum(len(s[1]) for s in seqs)
+            running = self.sched.running()
+            if not running:
+                return []
+            B = r.bucket(self.sched.highest_slot + 1)
+            sample = any(self._reqs[rid].params.temperature > 0 for rid in running)
+            # steps until the earliest request can hit its length limit; with EOS possible, at most
+            # sync_every steps between host checks
+            reqs = [self._reqs[rid] for rid in running]
+            remaining = max(1, min(q.params.max_tokens - q.gen_host for q in reqs))
+            n_steps = remaining if all(q.params.ignore_eos for q in reqs) else min(self.sync_every, remaining)
+            t0 = time.perf_counter()
+            r.decode(B, n_steps, sample)
+            fin, gl, _ = r.read_rows([q.slot for q in reqs])
+            self.stats["decode_s"] += time.perf_counter() - t0
+            self.stats["decode_steps"] += n_steps
+            done = []
+            now = time.perf_counter()
+            for i, rid in enumerate(running):
+                self._reqs[rid].gen_host = int(gl[i])
+                if int(fin[i]):
+                    req = self._reqs.pop(rid)
+                    n = min(int(gl[i]), req.params.max_tokens)
+                    req.output_ids = r.tokens_of(req.slot, n)
+                    req.finished_at = now
+                    r.release_slot(req.slot)
+                    self._slot_owner.pop(req.slot, None)
+                    self.sched.finish(rid)
+                    self.stats["generated_tokens"] += n
+                    self.stats["requests"] += 1
+                    req.done.set()
+                    done.append(req)
+            return done
+
+    def _prefill_packed(self, seqs, any_sample: bool) -> None:
+        """Prefill in chunks of at most max_prefill_tokens tokens (long prompts split across calls)."""
+        r = self.runner
+        batch, tokens = [], 0
+        for slot, ids, _ in seqs:
+            if len(ids) > self.max_prefill_tokens:  # chunked prefill of one long prompt
+                if batch:
+                    r.prefill(batch, any_sample)
+                    batch, tokens = [], 0
+                c = self.max_prefill_tokens
+                for s in range(0, len(ids) - c, c):
+                    r.prefill_chunk([(slot, ids[s:s + c], s)])
+                s = ((len(ids) - 1) // c) * c
+                r.prefill([(slot, ids[s:], s)], any_sample)
+                continue
+            if tokens + len(ids) > self.max_prefill_tokens and batch:
+                r.prefill(batch, any_sample)
+                batch, tokens = [], 0
+            batch.append((slot, ids, 0))
+            tokens += len(ids)
+        if batch:
+            r.prefill(batch, any_sample)
+
+    def run_until_done(self, reqs: Sequence[Request]) -> None:
+        while not all(q.done.is_set() for q in reqs):
+            self.step()
+
+    # -------------------------------------------------------------------------------- one-shot API
+    def result(self, req: Request, template: Optional[str] = None) -> GenerationResult:
+        text = self.tok.decode(req.output_ids)
+        text = apply_stops(text, template or self.spec.template, req.params.stop)
+        ns = lambda s: int(max(0.0, s) * 1e9)  # noqa: E731
+        ended_eos = bool(req.output_ids) and req.output_ids[-1] in self.runner.eos_list and not req.params.ignore_eos
+        return GenerationResult(
+            text=text, token_ids=req.output_ids, prompt_tokens=len(req.prompt_ids), eval_count=len(req.output_ids),
+            total_duration_ns=ns(req.finished_at - req.arrival), load_duration_ns=ns(self.load_time_s),
+            prompt_eval_duration_ns=ns(req.first_token - req.admitted),
+            eval_duration_ns=ns(req.finished_at - req.first_token), done_reason="stop" if ended_eos else "length")
+
+    def generate(self, prompts: Sequence, params: Optional[SamplingParams] = None, system: str = "",
+                 raw: bool = False) -> list[GenerationResult]:
+        """Batch generate. ``prompts``: strings (templated + tokenized) or token-id lists."""
+        params = params or SamplingParams()
+        reqs = []
+        for p in prompts:
+            ids = self.encode(self.render(p, system, raw)) if isinstance(p, str) else list(p)
+            reqs.append(self.add_request(ids, params))
+        self.run_until_done(reqs)
+        return [self.result(q) for q in reqs]
+
+    def generate_text(self, prompt: str, system: str = "", params: Optional[SamplingParams] = None,
+                      on_token: Optional[Callable[[str], None]] = None) -> GenerationResult:
+        res = self.generate([prompt], params, system)[0]
+        if on_token is not None:
+            on_token(res.text)
+        return res

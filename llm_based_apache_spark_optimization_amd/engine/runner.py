@@ -1,0 +1,358 @@
+"""ModelRunner: one model replica (optionally one tensor-parallel shard of it) on one device.
+
+Owns the packed weights, the paged KV cache, the RoPE tables, every decode workspace and the
+device-resident decode state, and executes
+
+* ``prefill(seqs)`` — packed variable-length prefill (eager launches; shapes change per call),
+  which also commits each sequence's first generated token into its decode slot;
+* ``decode(B, steps)`` — ``steps`` decode steps over slot rows ``[0, B)``, replayed from a captured
+  hipGraph (``torch.cuda.CUDAGraph``) per (batch bucket, sampler mode).  The whole step — 32 layers of
+  fused kernels, the TP all-reduces, LM head, token selection and the state update — runs without
+  the host: positions, context lengths, finished flags and the generated tokens live on the device, so
+  a graph replays for as many steps as the host wants between synchronisations.
+
+Decode-step kernel sequence per layer (``L`` layers, B tokens):
+  add_rmsnorm(+embedding | +down partials) -> gemm qkv -> rope_append (RoPE + paged KV write)
+  -> attn_decode (split-KV) -> gemm o (f32 split-K slabs) [-> all_reduce] -> add_rmsnorm(+o partials)
+  -> gemm gate_up (fused SiLU*up) -> gemm down (f32 slabs) [-> all_reduce]
+then add_rmsnorm(final) -> gemm lm_head [-> all_gather] -> argmax/sample + commit.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import torch
+
+from .. import ops
+from ..models.llama import LlamaWeights
+from ..ops import reference as ref
+
+BLOCK = 64
+SAMPLE_HIST = 64  # repetition-penalty window (Ollama repeat_last_n default)
+
+
+class ModelRunner:
+    def __init__(self, weights: LlamaWeights, max_slots: int = 32, max_model_len: int = 4096,
+                 num_kv_blocks: Optional[int] = None, kv_memory_fraction: float = 0.85,
+                 max_new_cap: Optional[int] = None, tp=None, use_graphs: bool = True, steps_per_graph: int = 1):
+        self.w = weights
+        self.spec = spec = weights.spec
+        self.device = weights.device
+        self.tp = tp
+        tps = tp.size if tp is not None else 1
+        self.H = spec.n_heads // tps
+        self.Hkv = spec.n_kv_heads // tps
+        self.D = spec.head_dim
+        assert self.D == 128, "kernels are specialised for head_dim 128"
+        self.d = spec.hidden
+        self.L = spec.n_layers
+        self.V = spec.vocab_size
+        self.Vl = weights.lm_head.N
+        self.ffn_l = spec.ffn // tps
+        self.eps = spec.rms_eps
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.max_slots = max_slots
+        self.max_model_len = min(max_model_len, spec.max_position)
+        self.max_blocks = (self.max_model_len + BLOCK - 1) // BLOCK
+        self.max_new_cap = max_new_cap or self.max_model_len
+        self.on_gpu = self.device.type == "cuda"
+        self.use_graphs = use_graphs and self.on_gpu
+        self.steps_per_graph = steps_per_graph
+        dev = self.device
+
+        # ---------------- KV cache: [L, 2, blocks, Hkv, 64, D] bf16
+        per_block = self.L * 2 * self.Hkv * BLOCK * self.D * 2
+        want = max_slots * self.max_blocks + 1
+        if num_kv_blocks is None:
+            if self.on_gpu:
+                free, _ = torch.cuda.mem_get_info(dev)
+                budget = int(free * kv_memory_fraction) - (1 << 30)
+                num_kv_blocks = max(2, min(want, budget // per_block))
+            else:
+                num_kv_blocks = want
+        self.num_kv_blocks = int(num_kv_blocks)
+        self.kv = torch.zeros(self.L, 2, self.num_kv_blocks, self.Hkv, BLOCK, self.D, dtype=torch.bfloat16,
+                              device=dev)
+        cos, sin = ref.rope_tables(self.D, self.max_model_len, spec.rope_theta, spec.rope_scaling, device=dev)
+        self.cos, self.sin = cos.contiguous(), sin.contiguous()
+
+        # ---------------- device decode state (one row per slot)
+        S = max_slots
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.input_ids = torch.zeros(S, **i32)
+        self.positions = torch.zeros(S, **i32)
+        self.gen_len = torch.zeros(S, **i32)
+        self.finished = torch.ones(S, **i32)
+        self.limit = torch.full((S,), self.max_new_cap, **i32)
+        self.eos_on = torch.ones(S, **i32)
+        self.out_tokens = torch.zeros(S, self.max_new_cap, **i32)
+        self.block_tables = torch.zeros(S, self.max_blocks, **i32)
+        self.temperature = torch.zeros(S, dtype=torch.float32, device=dev)
+        self.top_k = torch.full((S,), 40, **i32)
+        self.top_p = torch.full((S,), 0.9, dtype=torch.float32, device=dev)
+        self.seeds = torch.zeros(S, dtype=torch.int64, device=dev)
+        self.eos_list = list(spec.eos_ids) or [-1]
+        self.eos = torch.tensor(self.eos_list, **i32)
+
+        # ---------------- decode workspaces sized for S rows
+        f32 = dict(dtype=torch.float32, device=dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.h = torch.zeros(S, self.d, **f32)
+        self.xn = torch.zeros(S, self.d, **bf)
+        self.qkv = torch.zeros(S, (self.H + 2 * self.Hkv) * self.D, **bf)
+        self.q = torch.zeros(S, self.H, self.D, **bf)
+        self.attn = torch.zeros(S, self.H * self.D, **bf)
+        self.act = torch.zeros(S, self.ffn_l, **bf)
+        self.o_buf = torch.zeros(4 * S * self.d, **f32)
+        self.down_buf = torch.zeros(4 * S * self.d, **f32)
+        self.logits_l = torch.zeros(S, self.Vl, **f32)
+        self.logits = self.logits_l if tps == 1 else torch.zeros(S, self.V, **f32)
+        self.gather_buf = None if tps == 1 else torch.zeros(tps * S * self.Vl, **f32)
+        _, nsplit_max = ops.decode_split_plan(1, self.Hkv, self.max_model_len)
+        self.opart = torch.zeros(S * self.H * max(nsplit_max, 1) * self.D, **f32)
+        self.mlpart = torch.zeros(S * self.H * max(nsplit_max, 1) * 2, **f32)
+        self.amax_part = torch.zeros(S * ((self.V + 4095) // 4096), dtype=torch.int64, device=dev)
+        self.cand = torch.zeros(S * ((self.V + 2047) // 2048) * 64, dtype=torch.int64, device=dev)
+        self.graphs: dict = {}
+
+    # ------------------------------------------------------------------------------------ helpers
+    def _allreduce(self, t: torch.Tensor) -> None:
+        if self.tp is not None and self.tp.size > 1:
+            self.tp.all_reduce(t)
+
+    def _splitk(self, M: int, K: int) -> int:
+        if not self.on_gpu or (self.tp is not None and self.tp.size > 1) or M > 64:
+            return 1
+        return ops.pick_nb_splitk(M, self.d, K, "f32")[1]
+
+    def _lm_head(self, xn: torch.Tensor, M: int) -> torch.Tensor:
+        """logits [M, V] (f32) for the normalised rows xn [M, d]."""
+        loc = self.logits_l[:M] if M <= self.max_slots else torch.empty(M, self.Vl, dtype=torch.float32,
+                                                                         device=self.device)
+        ops.linear(xn, self.w.lm_head, "f32", out=loc, splitk=1)
+        if self.tp is None or self.tp.size == 1:
+            return loc
+        tps = self.tp.size
+        gb = self.gather_buf[: tps * M * self.Vl] if M <= self.max_slots else torch.empty(
+            tps * M * self.Vl, dtype=torch.float32, device=self.device)
+        self.tp.all_gather(gb, loc.reshape(-1))
+        full = self.logits[:M] if M <= self.max_slots else torch.empty(M, self.V, dtype=torch.float32,
+                                                                      device=self.device)
+        full.view(M, tps, self.Vl).copy_(gb.view(tps, M, self.Vl).transpose(0, 1))
+        return full
+
+    # ------------------------------------------------------------------------------------ decode
+    def _decode_step(self, B: int, sample: bool) -> None:
+        w, d = self.w, self.d
+        ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
+        h, xn = self.h[:B], self.xn[:B]
+        sk_o = self._splitk(B, self.H * self.D)
+        sk_d = self._splitk(B, self.ffn_l)
+        o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
+        d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
+        plan = ops.decode_split_plan(B, self.Hkv, self.max_model_len)
+        ws = (self.opart, self.mlpart)
+        for l, lw in enumerate(w.layers):
+            if l == 0:
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
+            else:
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts)
+            ops.linear(xn, lw.wqkv, "bf16", out=self.qkv[:B])
+            kc, vc = self.kv[l, 0], self.kv[l, 1]
+            ops.rope_append(self.qkv[:B], pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv)
+            ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale, self.attn[:B].view(B, self.H,
+                                                                                                          self.D),
+                            workspace=ws, plan=plan)
+            ops.linear(self.attn[:B], lw.wo, "f32", out=o_parts, splitk=sk_o)
+            self._allreduce(o_parts)
+            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
+            ops.linear(xn, lw.w_gate_up, "silu", out=self.act[:B])
+            ops.linear(self.act[:B], lw.w_down, "f32", out=d_parts, splitk=sk_d)
+            self._allreduce(d_parts)
+        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_parts)
+        logits = self._lm_head(xn, B)
+        st = (self.out_tokens[:B], self.gen_len[:B], self.input_ids[:B], self.positions[:B], self.finished[:B])
+        if sample:
+            ops.sample_commit(logits, None, None, self.temperature[:B], self.top_k[:B], self.top_p[:B],
+                              self.seeds[:B], *st, self.eos, self.limit[:B], self.eos_on[:B],
+                              workspace=(self.amax_part, self.cand) if self.on_gpu else None)
+        else:
+            ops.argmax_commit(logits, *st, self.eos, self.limit[:B], self.eos_on[:B],
+                              part=self.amax_part if self.on_gpu else None)
+
+    def bucket(self, n: int) -> int:
+        b = 1
+        while b < n:
+            b *= 2
+        return min(b, self.max_slots) if n <= self.max_slots else self.max_slots
+
+    def capture(self, B: int, sample: bool) -> None:
+        key = (B, sample)
+        if key in self.graphs:
+            return
+        if self.tp is not None and self.tp.size > 1:
+            self.tp.warmup()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            # state must not change during capture: kernels are recorded, not executed
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(self.steps_per_graph):
+                    self._decode_step(B, sample)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.graphs[key] = g
+
+    def decode(self, B: int, steps: int, sample: bool = False) -> None:
+        """Run ``steps`` decode steps over slot rows [0, B) (B a bucket size)."""
+        if not self.use_graphs:
+            for _ in range(steps):
+                self._decode_step(B, sample)
+            return
+        self.capture(B, sample)
+        g = self.graphs[(B, sample)]
+        n = (steps + self.steps_per_graph - 1) // self.steps_per_graph
+        for _ in range(n):
+            g.replay()
+
+    # ------------------------------------------------------------------------------------ slots
+    def set_slot(self, slot: int, blocks: Sequence[int], limit: int, temperature: float = 0.0, top_k: int = 40,
+                 top_p: float = 0.9, seed: int = 0, eos_on: bool = True) -> None:
+        row = torch.zeros(self.max_blocks, dtype=torch.int32)
+        row[: len(blocks)] = torch.tensor(list(blocks), dtype=torch.int32)
+        self.block_tables[slot].copy_(row.to(self.device, non_blocking=True))
+        self.limit[slot] = min(int(limit), self.max_new_cap)
+        self.temperature[slot] = float(temperature)
+        self.top_k[slot] = int(top_k)
+        self.top_p[slot] = float(top_p)
+        self.seeds[slot] = int(seed)
+        self.eos_on[slot] = 1 if eos_on else 0
+
+    def set_eos(self, ids: Sequence[int]) -> None:
+        """Replace the stop-token set (same length keeps captured graphs valid; otherwise recapture)."""
+        ids = list(ids) or [-1]
+        if len(ids) != self.eos.numel():
+            self.graphs.clear()
+            self.eos = torch.tensor(ids, dtype=torch.int32, device=self.device)
+        else:
+            self.eos.copy_(torch.tensor(ids, dtype=torch.int32))
+        self.eos_list = ids
+
+    def release_slot(self, slot: int) -> None:
+        self.finished[slot] = 1
+        self.positions[slot] = 0
+        self.gen_len[slot] = 0
+        self.block_tables[slot].zero_()
+
+    # ------------------------------------------------------------------------------------ prefill
+    def prefill(self, seqs: list[tuple[int, Sequence[int], int]], sample_any: bool = False) -> None:
+        """Prefill ``seqs`` = [(slot, token_ids, start_pos)] and commit each first token into its slot.
+
+        ``start_pos`` > 0 continues a chunked prefill (the cache already holds positions < start_pos);
+        only the final chunk of a prompt should be passed with ``commit=True`` semantics — a chunk whose
+        prompt continues is passed through ``prefill_chunk``.
+        """
+        self._prefill(seqs, commit=True, sample_any=sample_any)
+
+    def prefill_chunk(self, seqs: list[tuple[int, Sequence[int], int]]) -> None:
+        self._prefill(seqs, commit=False)
+
+    def _prefill(self, seqs, commit: bool, sample_any: bool = False) -> None:
+        dev, w, d = self.device, self.w, self.d
+        n = len(seqs)
+        lens = [len(t) for _, t, _ in seqs]
+        T = sum(lens)
+        cu = [0]
+        for x in lens:
+            cu.append(cu[-1] + x)
+        toks, pos, tseq = [], [], []
+        for i, (_, t, p0) in enumerate(seqs):
+            toks.extend(int(x) for x in t)
+            pos.extend(range(p0, p0 + len(t)))
+            tseq.extend([i] * len(t))
+        ctx = [p0 + len(t) for _, t, p0 in seqs]
+        slots = [s for s, _, _ in seqs]
+        host = torch.tensor(toks + pos + tseq + cu + ctx + [c - 1 for c in cu[1:]], dtype=torch.int32)
+        if self.on_gpu:
+            host = host.pin_memory()
+        dv = host.to(dev, non_blocking=True)
+        o = 0
+        ids = dv[o:o + T]; o += T
+        posd = dv[o:o + T]; o += T
+        tsd = dv[o:o + T]; o += T
+        cud = dv[o:o + n + 1]; o += n + 1
+        ctxd = dv[o:o + n]; o += n
+        last = dv[o:o + n]
+        slot_t = torch.tensor(slots, dtype=torch.long, device=dev)
+        bt = self.block_tables.index_select(0, slot_t)
+        work = None
+        if self.on_gpu:
+            work = torch.tensor(ops.prefill_work(cu), dtype=torch.int32).to(dev, non_blocking=True)
+
+        f32 = dict(dtype=torch.float32, device=dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        h = torch.empty(T, d, **f32)
+        xn = torch.empty(T, d, **bf)
+        qkv = torch.empty(T, (self.H + 2 * self.Hkv) * self.D, **bf)
+        q = torch.empty(T, self.H, self.D, **bf)
+        attn = torch.empty(T, self.H * self.D, **bf)
+        sk_o = self._splitk(T, self.H * self.D)
+        sk_d = self._splitk(T, self.ffn_l)
+        d_parts = None
+        for l, lw in enumerate(w.layers):
+            if l == 0:
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
+            else:
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts)
+            ops.linear(xn, lw.wqkv, "bf16", out=qkv)
+            kc, vc = self.kv[l, 0], self.kv[l, 1]
+            ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
+            ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
+                             work=work)
+            o_parts = ops.linear(attn, lw.wo, "f32", splitk=sk_o)
+            if not self.on_gpu:
+                o_parts = o_parts.view(1, T, d)
+            self._allreduce(o_parts)
+            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
+            act = ops.linear(xn, lw.w_gate_up, "silu")
+            d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
+            if not self.on_gpu:
+                d_parts = d_parts.view(1, T, d)
+            self._allreduce(d_parts)
+        if not commit:
+            return
+        xl = torch.empty(n, d, **bf)
+        ops.add_rmsnorm(h, w.final_norm, self.eps, xl, parts=d_parts, row_idx=last, write_h=False)
+        logits = self._lm_head(xl, n)
+        # commit the first generated token of each sequence into its slot row
+        i32 = dict(dtype=torch.int32, device=dev)
+        out_t = torch.zeros(n, self.max_new_cap, **i32)
+        gl = torch.zeros(n, **i32)
+        iid = torch.zeros(n, **i32)
+        pp = ctxd - 1
+        fin = torch.zeros(n, **i32)
+        lim = self.limit.index_select(0, slot_t)
+        eon = self.eos_on.index_select(0, slot_t)
+        if sample_any:
+            ops.sample_commit(logits, None, None, self.temperature.index_select(0, slot_t),
+                              self.top_k.index_select(0, slot_t), self.top_p.index_select(0, slot_t),
+                              self.seeds.index_select(0, slot_t), out_t, gl, iid, pp, fin, self.eos, lim, eon)
+        else:
+            ops.argmax_commit(logits, out_t, gl, iid, pp, fin, self.eos, lim, eon)
+        self.out_tokens.index_copy_(0, slot_t, out_t)
+        self.gen_len.index_copy_(0, slot_t, gl)
+        self.input_ids.index_copy_(0, slot_t, iid)
+        self.positions.index_copy_(0, slot_t, pp)
+        self.finished.index_copy_(0, slot_t, fin)
+
+    # ------------------------------------------------------------------------------------ readback
+    def read_rows(self, slots: Sequence[int]):
+        """(finished, gen_len, tokens) for ``slots`` (one device->host sync)."""
+        idx = torch.tensor(list(slots), dtype=torch.long, device=self.device)
+        fin = self.finished.index_select(0, idx).cpu()
+        gl = self.gen_len.index_select(0, idx).cpu()
+        return fin, gl, idx
+
+    def tokens_of(self, slot: int, n: int) -> list[int]:
+        return self.out_tokens[slot, :n].tolist()

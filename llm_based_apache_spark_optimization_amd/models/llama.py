@@ -1,0 +1,157 @@
+"""Llama-family weights in the layouts the gfx950 kernels stream, plus tensor-parallel sharding.
+
+Per layer: ``wqkv`` (fused q|k|v rows, column-parallel), ``wo`` (row-parallel), ``w_gate_up``
+(gate/up interleaved per 16 rows for the fused SiLU epilogue, column-parallel), ``w_down``
+(row-parallel), two RMSNorm vectors.  Embedding is replicated; the LM head is vocab-parallel.
+
+Sources: seeded random init directly on the device (the benchmark path: the reference's models are
+Ollama GGUF blobs we cannot download), a HuggingFace-format state dict (``from_hf_state_dict``),
+or safetensors files (``load_safetensors_dir``).  ``kind='fp8'`` quantises every projection to
+e4m3fn with per-output-channel scales at load time (BASELINE config 5).
+"""
+from __future__ import annotations
+
+import dataclasses
+import glob
+import json
+import os
+from typing import Optional
+
+import torch
+
+from .. import ops
+from .spec import ModelSpec, spec_from_hf_config
+
+
+@dataclasses.dataclass
+class LayerWeights:
+    wqkv: ops.PackedWeight
+    wo: ops.PackedWeight
+    w_gate_up: ops.PackedWeight
+    w_down: ops.PackedWeight
+    attn_norm: torch.Tensor
+    mlp_norm: torch.Tensor
+
+
+@dataclasses.dataclass
+class LlamaWeights:
+    spec: ModelSpec
+    embed: torch.Tensor  # [V, d] bf16 (replicated)
+    layers: list
+    final_norm: torch.Tensor
+    lm_head: ops.PackedWeight  # [V / tp, d]
+    tp_rank: int = 0
+    tp_size: int = 1
+
+    @property
+    def device(self) -> torch.device:
+        return self.embed.device
+
+    def nbytes(self) -> int:
+        n = self.embed.numel() * 2 + self.lm_head.nbytes
+        for lw in self.layers:
+            n += lw.wqkv.nbytes + lw.wo.nbytes + lw.w_gate_up.nbytes + lw.w_down.nbytes
+        return n
+
+
+def _shard_rows(w: torch.Tensor, rank: int, size: int) -> torch.Tensor:
+    n = w.shape[0] // size
+    return w[rank * n:(rank + 1) * n]
+
+
+def _shard_cols(w: torch.Tensor, rank: int, size: int) -> torch.Tensor:
+    n = w.shape[1] // size
+    return w[:, rank * n:(rank + 1) * n]
+
+
+def check_tp(spec: ModelSpec, tp: int) -> None:
+    if spec.n_kv_heads % tp or spec.n_heads % tp:
+        raise ValueError(f"{spec.name}: heads {spec.n_heads}/{spec.n_kv_heads} not divisible by tp={tp}")
+    if spec.ffn % (16 * tp) or spec.vocab_size % (16 * tp):
+        raise ValueError(f"{spec.name}: ffn/vocab not divisible by 16*tp={16 * tp}")
+
+
+def pack_layer(spec: ModelSpec, wq, wk, wv, wo, wg, wu, wd, an, mn, rank=0, tp=1, kind="bf16") -> LayerWeights:
+    """HF-layout layer tensors -> packed, TP-sharded LayerWeights on wq's device."""
+    hd = spec.head_dim
+    hq, hk = spec.n_heads // tp, spec.n_kv_heads // tp
+    q = wq.view(spec.n_heads, hd, -1)[rank * hq:(rank + 1) * hq].reshape(hq * hd, -1)
+    k = wk.view(spec.n_kv_heads, hd, -1)[rank * hk:(rank + 1) * hk].reshape(hk * hd, -1)
+    v = wv.view(spec.n_kv_heads, hd, -1)[rank * hk:(rank + 1) * hk].reshape(hk * hd, -1)
+    wqkv = torch.cat([q, k, v], 0)
+    wo_s = _shard_cols(wo, rank, tp)
+    gu = ops.interleave_gate_up(_shard_rows(wg, rank, tp), _shard_rows(wu, rank, tp))
+    wd_s = _shard_cols(wd, rank, tp)
+    P = ops.PackedWeight.from_dense
+    return LayerWeights(P(wqkv.contiguous(), kind), P(wo_s.contiguous(), kind), P(gu.contiguous(), kind),
+                        P(wd_s.contiguous(), kind), an.to(torch.bfloat16).contiguous(),
+                        mn.to(torch.bfloat16).contiguous())
+
+
+def init_random(spec: ModelSpec, device="cpu", seed: int = 0, kind: str = "bf16", std: float = 0.02,
+                tp_rank: int = 0, tp_size: int = 1) -> LlamaWeights:
+    """Seeded random-init weights generated on ``device`` (identical across TP ranks / DP replicas)."""
+    check_tp(spec, tp_size)
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    d, hd = spec.hidden, spec.head_dim
+
+    def rnd(*shape, s=std):
+        return (torch.randn(*shape, generator=g, device=dev, dtype=torch.float32) * s).to(torch.bfloat16)
+
+    def ones(n):
+        return (1.0 + 0.1 * torch.randn(n, generator=g, device=dev)).to(torch.bfloat16)
+
+    embed = rnd(spec.vocab_size, d, s=1.0)
+    layers = []
+    for _ in range(spec.n_layers):
+        wq = rnd(spec.n_heads * hd, d)
+        wk = rnd(spec.n_kv_heads * hd, d)
+        wv = rnd(spec.n_kv_heads * hd, d)
+        wo = rnd(d, spec.n_heads * hd)
+        wg = rnd(spec.ffn, d)
+        wu = rnd(spec.ffn, d)
+        wd = rnd(d, spec.ffn)
+        layers.append(pack_layer(spec, wq, wk, wv, wo, wg, wu, wd, ones(d), ones(d), tp_rank, tp_size, kind))
+        del wq, wk, wv, wo, wg, wu, wd
+    final_norm = ones(d)
+    head = embed if spec.tie_embeddings else rnd(spec.vocab_size, d)
+    lm_head = ops.PackedWeight.from_dense(_shard_rows(head, tp_rank, tp_size).contiguous(), kind)
+    return LlamaWeights(spec, embed, layers, final_norm, lm_head, tp_rank, tp_size)
+
+
+def from_hf_state_dict(spec: ModelSpec, sd: dict, device="cpu", kind: str = "bf16", tp_rank: int = 0,
+                       tp_size: int = 1) -> LlamaWeights:
+    """HF LlamaForCausalLM / MistralForCausalLM state dict -> LlamaWeights."""
+    check_tp(spec, tp_size)
+    dev = torch.device(device)
+
+    def t(name):
+        return sd[name].to(device=dev, dtype=torch.bfloat16)
+
+    layers = []
+    for i in range(spec.n_layers):
+        p = f"model.layers.{i}."
+        layers.append(pack_layer(
+            spec, t(p + "self_attn.q_proj.weight"), t(p + "self_attn.k_proj.weight"), t(p + "self_attn.v_proj.weight"),
+            t(p + "self_attn.o_proj.weight"), t(p + "mlp.gate_proj.weight"), t(p + "mlp.up_proj.weight"),
+            t(p + "mlp.down_proj.weight"), t(p + "input_layernorm.weight"), t(p + "post_attention_layernorm.weight"),
+            tp_rank, tp_size, kind))
+    embed = t("model.embed_tokens.weight").contiguous()
+    head = embed if (spec.tie_embeddings or "lm_head.weight" not in sd) else t("lm_head.weight")
+    lm_head = ops.PackedWeight.from_dense(_shard_rows(head, tp_rank, tp_size).contiguous(), kind)
+    return LlamaWeights(spec, embed, layers, t("model.norm.weight").contiguous(), lm_head, tp_rank, tp_size)
+
+
+def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[str] = None, template="raw",
+                         tp_rank=0, tp_size=1) -> LlamaWeights:
+    """Load an HF checkpoint directory (config.json + *.safetensors) with the safe loader."""
+    from safetensors.torch import load_file
+
+    with open(os.path.join(path, "config.json")) as f:
+        cfg = json.load(f)
+    spec = spec_from_hf_config(cfg, name or os.path.basename(path.rstrip("/")), template)
+    sd = {}
+    for fn in sorted(glob.glob(os.path.join(path, "*.safetensors"))):
+        sd.update(load_file(fn))
+    return from_hf_state_dict(spec, sd, device, kind, tp_rank, tp_size)

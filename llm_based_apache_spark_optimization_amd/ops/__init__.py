@@ -258,25 +258,39 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, wo
 
 
 # ----------------------------------------------------------------------------------- sampling
-def argmax_commit(logits, out_tokens, gen_len, input_ids, positions, finished, eos, part=None):
-    if not _gpu(logits):
-        return ref.argmax_commit(logits, out_tokens, gen_len, input_ids, positions, finished, eos)
+def _row_defaults(B, out_tokens, limit, eos_on):
+    dev = out_tokens.device
+    if limit is None:
+        limit = torch.full((B,), out_tokens.shape[1], dtype=torch.int32, device=dev)
+    if eos_on is None:
+        eos_on = torch.ones(B, dtype=torch.int32, device=dev)
+    return limit, eos_on
+
+
+def argmax_commit(logits, out_tokens, gen_len, input_ids, positions, finished, eos, limit=None, eos_on=None,
+                  part=None):
+    """Greedy token + in-place decode-state update (see kernels/sampling.hip)."""
     B, V = logits.shape
+    limit, eos_on = _row_defaults(B, out_tokens, limit, eos_on)
+    if not _gpu(logits):
+        return ref.argmax_commit(logits, out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on)
     if part is None:
         part = torch.empty(B * ((V + 4095) // 4096), device=logits.device, dtype=torch.int64)
-    ext().argmax_commit(logits, part, out_tokens, gen_len, input_ids, positions, finished, eos)
+    ext().argmax_commit(logits, part, out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on)
 
 
 def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len, input_ids,
-                  positions, finished, eos, workspace=None):
+                  positions, finished, eos, limit=None, eos_on=None, workspace=None):
+    """Temperature / top-k / top-p draw (+ optional repetition penalty) + decode-state update."""
+    B, V = logits.shape
+    limit, eos_on = _row_defaults(B, out_tokens, limit, eos_on)
     if not _gpu(logits):
         return ref.sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len,
-                                 input_ids, positions, finished, eos)
-    B, V = logits.shape
+                                 input_ids, positions, finished, eos, limit, eos_on)
     if workspace is None:
         part = torch.empty(B * ((V + 4095) // 4096), device=logits.device, dtype=torch.int64)
         cand = torch.empty(B * ((V + 2047) // 2048) * 64, device=logits.device, dtype=torch.int64)
     else:
         part, cand = workspace
     ext().sample_commit(logits, part, cand, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len,
-                        input_ids, positions, finished, eos)
+                        input_ids, positions, finished, eos, limit, eos_on)

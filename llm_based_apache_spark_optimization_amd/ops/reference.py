@@ -125,7 +125,7 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out):
     return out
 
 
-def commit(tok, out_tokens, gen_len, input_ids, positions, finished, eos):
+def commit(tok, out_tokens, gen_len, input_ids, positions, finished, eos, limit=None, eos_on=None):
     eos_set = set(eos.tolist()) if eos is not None else set()
     max_new = out_tokens.shape[1]
     for b in range(tok.shape[0]):
@@ -137,14 +137,16 @@ def commit(tok, out_tokens, gen_len, input_ids, positions, finished, eos):
             out_tokens[b, n] = t
         gen_len[b] = n + 1
         input_ids[b] = t
-        if n + 1 >= max_new or t in eos_set:
+        lim = min(max_new, int(limit[b])) if limit is not None else max_new
+        use_eos = bool(int(eos_on[b])) if eos_on is not None else True
+        if n + 1 >= lim or (use_eos and t in eos_set):
             finished[b] = 1
         else:
             positions[b] += 1
 
 
-def argmax_commit(logits, out_tokens, gen_len, input_ids, positions, finished, eos):
-    commit(logits.float().argmax(-1), out_tokens, gen_len, input_ids, positions, finished, eos)
+def argmax_commit(logits, out_tokens, gen_len, input_ids, positions, finished, eos, limit=None, eos_on=None):
+    commit(logits.float().argmax(-1), out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on)
 
 
 def sample_probs(logits_row: torch.Tensor, temperature: float, top_k: int, top_p: float, topk_cap: int = 64):
@@ -161,7 +163,7 @@ def sample_probs(logits_row: torch.Tensor, temperature: float, top_k: int, top_p
 
 
 def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len, input_ids,
-                  positions, finished, eos, generator: torch.Generator | None = None):
+                  positions, finished, eos, limit=None, eos_on=None, generator: torch.Generator | None = None):
     B = logits.shape[0]
     toks = torch.empty(B, dtype=torch.long)
     for b in range(B):
@@ -175,5 +177,7 @@ def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_t
             toks[b] = int(row.argmax())
             continue
         idx, p = sample_probs(row, T, int(top_k[b]), float(top_p[b]))
+        if generator is None:
+            generator = torch.Generator().manual_seed(int(seeds[b]) + int(gen_len[b]))
         toks[b] = int(idx[torch.multinomial(p.cpu(), 1, generator=generator)])
-    commit(toks, out_tokens, gen_len, input_ids, positions, finished, eos)
+    commit(toks, out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on)

@@ -1,0 +1,67 @@
+"""Tensor-parallel process groups over RCCL (torch.distributed backend "nccl" is RCCL on ROCm).
+
+Megatron-style split (SURVEY.md §2.6 P-TP): QKV and gate/up column-parallel, O and down row-parallel
+followed by one all-reduce each (2 per layer), LM head vocab-parallel followed by an all-gather.
+On MI355X every GPU pair has its own xGMI link, so a TP=2 replica uses exactly one link; the
+decode-size all-reduce (B x d f32, 16-512 KiB) is latency-bound and is captured inside the decode
+hipGraph together with the kernels around it.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+class TPGroup:
+    def __init__(self, group, rank: int, size: int, device: torch.device):
+        self.group, self.rank, self.size, self.device = group, rank, size, device
+        self._warm = False
+
+    def all_reduce(self, t: torch.Tensor) -> None:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        dist.all_gather_into_tensor(out, inp, group=self.group)
+
+    def warmup(self) -> None:
+        """Initialise the communicator outside graph capture."""
+        if not self._warm:
+            t = torch.zeros(16, device=self.device)
+            self.all_reduce(t)
+            torch.cuda.synchronize(self.device)
+            self._warm = True
+
+
+def init_distributed(backend: Optional[str] = None) -> tuple[int, int, int]:
+    """(rank, world, local_rank) from torchrun env; initialises the default group once."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local
+
+
+def make_replica_groups(world: int, tp: int, rank: int, device: torch.device) -> tuple[int, Optional[TPGroup]]:
+    """Split ``world`` ranks into world/tp replicas of ``tp`` consecutive ranks ({0,1},{2,3},... for tp=2).
+
+    Every rank must call this (new_group is collective).  Returns (replica index, this rank's TP group).
+    """
+    if world % tp:
+        raise ValueError(f"world {world} not divisible by tp {tp}")
+    mine = None
+    for r0 in range(0, world, tp):
+        ranks = list(range(r0, r0 + tp))
+        g = dist.new_group(ranks) if (tp > 1 and world > 1) else None
+        if rank in ranks and tp > 1:
+            mine = TPGroup(g, rank - r0, tp, device)
+    return rank // tp, mine

@@ -1,0 +1,68 @@
+"""BASELINE config 1 (CPU plumbing): the engine's model path vs HuggingFace transformers on CPU.
+
+A tiny random-init Llama of each served architecture (MHA duckdb-nsql shape; GQA + llama3-scaled
+RoPE + tied embeddings Llama-3.2 shape) is built in transformers, its state dict loaded into the
+engine (CPU reference ops, bf16 weights / bf16 activations) and compared: prefill logits and
+teacher-forced greedy decoding through the paged KV cache and the native scheduler.
+"""
+import pytest
+import torch
+
+from llm_based_apache_spark_optimization_amd.engine import LLMEngine, ModelRunner, SamplingParams
+from llm_based_apache_spark_optimization_amd.models import get_spec
+from llm_based_apache_spark_optimization_amd.models.llama import from_hf_state_dict
+from llm_based_apache_spark_optimization_amd.ops import reference as ref
+
+
+def hf_model(name, init=0.08, seed=0):
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    spec = get_spec(name)
+    torch.manual_seed(seed)
+    m = LlamaForCausalLM(LlamaConfig(**spec.to_hf_config(), initializer_range=init))
+    inv = m.model.rotary_emb.inv_freq.clone()
+    m = m.to(torch.bfloat16).float().eval()
+    m.model.rotary_emb.inv_freq.copy_(inv)
+    return spec, m
+
+
+@pytest.mark.parametrize("name", ["tiny-nsql", "tiny-llama3"])
+def test_greedy_matches_transformers(name):
+    spec, m = hf_model(name)
+    eng = LLMEngine(ModelRunner(from_hf_state_dict(spec, m.state_dict(), "cpu"), max_slots=4, max_model_len=512))
+    prompts = [[1] + list(range(5, 60)), [1] + list(range(100, 300, 3))]
+    res = eng.generate(prompts, SamplingParams(max_tokens=10, ignore_eos=True))
+    for p, r in zip(prompts, res):
+        with torch.no_grad():
+            lg = m(torch.tensor([p + r.token_ids])).logits[0, len(p) - 1:-1]
+        chosen = lg.gather(1, torch.tensor(r.token_ids).view(-1, 1)).squeeze(1)
+        gap = lg.max(1).values - chosen
+        assert (gap <= 0.05 * lg.max(1).values.abs() + 0.05).all(), gap
+
+
+@pytest.mark.parametrize("name", ["tiny-nsql", "tiny-llama3"])
+def test_prefill_logits(name):
+    spec, m = hf_model(name)
+    r = ModelRunner(from_hf_state_dict(spec, m.state_dict(), "cpu"), max_slots=2, max_model_len=512)
+    p = [1] + list(range(7, 300))
+    r.set_slot(0, list(range(1, 6)), 4)
+    r.prefill([(0, p, 0)])
+    with torch.no_grad():
+        want = m(torch.tensor([p])).logits[0, -1:]
+    rel = (r.logits_l[:1] - want).norm() / want.norm()
+    assert rel < 3e-2
+
+
+def test_rope_tables_match_transformers():
+    spec, m = hf_model("tiny-llama3")
+    c, s = ref.rope_tables(128, 300, spec.rope_theta, spec.rope_scaling)
+    hc, hs = m.model.rotary_emb(torch.zeros(1, 300, 128), torch.arange(300)[None])
+    assert torch.allclose(c, hc[0, :, :64], atol=1e-4) and torch.allclose(s, hs[0, :, :64], atol=1e-4)
+
+
+def test_llama3_scaling_changes_low_frequencies():
+    sc = get_spec("llama3.2").rope_scaling
+    c, _ = ref.rope_tables(128, 20000, 500000.0, sc)
+    c0, _ = ref.rope_tables(128, 20000, 500000.0, None)
+    assert torch.allclose(c[:, :8], c0[:, :8], atol=1e-6)
+    assert not torch.allclose(c[-1, -4:], c0[-1, -4:])
