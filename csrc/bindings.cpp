@@ -11,7 +11,7 @@ int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* 
 int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
                     const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
                     hipStream_t s);
-int lsa_rope_append(const void* qkv, const int* pos, const int* tok_seq, const int* block_tables, int max_blocks,
+int lsa_rope_append(const void* qkv, const float* qkv_parts, int nparts, long part_stride, const int* pos, const int* tok_seq, const int* block_tables, int max_blocks,
                     const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int T, int H, int Hkv,
                     hipStream_t s);
 int lsa_silu_mul(const void* g, const void* u, void* o, long n, hipStream_t s);
@@ -32,6 +32,7 @@ int lsa_sample_commit(float* logits, int B, int V, unsigned long long* part, uns
 int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out, int epi,
                  int nb, int splitk, hipStream_t stream);
 int lsa_fp8_dequant(const void* Wq, const float* wscale, int N, int K, void* Wf, hipStream_t s);
+void lsa_set_skinny_waves(int w);
 }
 
 namespace {
@@ -99,11 +100,14 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
 void rope_append(const at::Tensor& qkv, const at::Tensor& pos, const c10::optional<at::Tensor>& tok_seq,
                  const at::Tensor& block_tables, const at::Tensor& cos_t, const at::Tensor& sin_t, at::Tensor& q_out,
                  at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv) {
-  need(qkv, at::kBFloat16, "qkv");
   need(pos, at::kInt, "pos");
   need(block_tables, at::kInt, "block_tables");
-  const int T = qkv.size(0);
-  check(lsa_rope_append(qkv.data_ptr(), pos.data_ptr<int>(), ptr<const int>(tok_seq), block_tables.data_ptr<int>(),
+  // qkv: bf16 [T, n] or f32 split-K slabs [S, T, n]
+  const bool parts = qkv.scalar_type() == at::kFloat;
+  TORCH_CHECK(parts || qkv.scalar_type() == at::kBFloat16, "qkv must be bf16 or f32 slabs");
+  const int T = parts ? qkv.size(1) : qkv.size(0);
+  check(lsa_rope_append(parts ? nullptr : qkv.data_ptr(), parts ? qkv.data_ptr<float>() : nullptr,
+                        parts ? qkv.size(0) : 0, parts ? qkv.stride(0) : 0, pos.data_ptr<int>(), ptr<const int>(tok_seq), block_tables.data_ptr<int>(),
                         block_tables.size(1), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), q_out.data_ptr(),
                         kc.data_ptr(), vc.data_ptr(), T, H, Hkv, cur_stream()),
         "rope_append");
@@ -188,5 +192,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);
   m.def("fp8_dequant", &fp8_dequant);
+  m.def("set_skinny_waves", [](int64_t w) { lsa_set_skinny_waves((int)w); });
   m.attr("arch") = "gfx950";
 }

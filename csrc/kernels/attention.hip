@@ -56,21 +56,18 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
   }
 
   const int* bt = block_tables + (size_t)b * max_blocks;
-  for (int blk = blk0; blk < blk1; ++blk) {
+  // K/V of block blk+1 are in flight while block blk is scored (two register sets, static names)
+  uint4 kA[4], vA[4], kB[4], vB[4];
+  auto fetch = [&](uint4 (&kr)[4], uint4 (&vr)[4], int blk) {
     const size_t base = ((size_t)bt[blk] * Hkv + hk) * 64 * D;
-    const uint16_t* kb = kc + base;
-    const uint16_t* vb = vc + base;
-    uint4 kr[4], vr[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int tok = wv * 16 + u * 4 + (lg & 3);
-      kr[u] = *reinterpret_cast<const uint4*>(kb + tok * D + li * 8);
+      kr[u] = *reinterpret_cast<const uint4*>(kc + base + tok * D + li * 8);
+      vr[u] = *reinterpret_cast<const uint4*>(vc + base + tok * D + li * 8);
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int tok = wv * 16 + u * 4 + (lg & 3);
-      vr[u] = *reinterpret_cast<const uint4*>(vb + tok * D + li * 8);
-    }
+  };
+  auto score = [&](const uint4 (&kr)[4], const uint4 (&vr)[4], int blk) {
     float s[4][G];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -109,6 +106,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
         for (int j = 0; j < 8; ++j) o[g][j] = fmaf(p[u], vf[j], o[g][j]);
       }
     }
+  };
+  if (blk0 < blk1) {
+    fetch(kA, vA, blk0);
+    int blk = blk0;
+    for (; blk + 1 < blk1; blk += 2) {
+      fetch(kB, vB, blk + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      score(kA, vA, blk);
+      __builtin_amdgcn_sched_barrier(0);
+      fetch(kA, vA, min(blk + 2, blk1 - 1));
+      __builtin_amdgcn_sched_barrier(0);
+      score(kB, vB, blk + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (blk < blk1) score(kA, vA, blk);
   }
 
   // merge the 16 lane groups

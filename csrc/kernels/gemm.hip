@@ -40,14 +40,25 @@ __device__ __forceinline__ void store4(void* out, int ldo, size_t slab, int m, i
 
 // ------------------------------------------------------------------------------------------------
 // decode / small-M kernel
+//
+// Work split: workgroup = 8 waves over NB n-blocks (16 rows each) and one split-K range; the range is
+// cut into chunks of U k-steps dealt round-robin to the waves.  Each wave streams its chunks with a
+// two-deep register pipeline: chunk i+1's NB*U weight fragments (+ the activation fragments) are in
+// flight while chunk i's MFMAs run, so the memory pipe never drains between chunks.  Out-of-range
+// k-steps are clamped (duplicate L2 hits) and masked by zeroing the activation fragment, never by a
+// per-load branch (which would force vmcnt(0) per element).
 // ------------------------------------------------------------------------------------------------
-template <int MT, int NB, int EPI>
-__global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
-                                                          int KB, const uint4* __restrict__ Wf,
-                                                          void* __restrict__ out, int ldo,
-                                                          int kb_per_split) {
-  constexpr int WAVES = 8;
-  constexpr int U = 16 / NB;  // weight fragments in flight per wave = NB * U = 16
+template <int MT, int NB>
+struct SkinnyCfg {
+  static constexpr int U = (16 / (NB > 2 * MT ? NB : 2 * MT)) < 2 ? 2 : (16 / (NB > 2 * MT ? NB : 2 * MT));
+};
+
+template <int MT, int NB, int EPI, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
+                                                                 int KB, const uint4* __restrict__ Wf,
+                                                                 void* __restrict__ out, int ldo,
+                                                                 int kb_per_split) {
+  constexpr int U = SkinnyCfg<MT, NB>::U;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -55,8 +66,9 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint16_t* __rest
   const int kbA = blockIdx.y * kb_per_split;
   const int kbB = min(KB, kbA + kb_per_split);
   const int nk = kbB - kbA;
-  const int kw0 = kbA + (nk * w) / WAVES;
-  const int kw1 = kbA + (nk * (w + 1)) / WAVES;
+  const int nch = (nk + U - 1) / U;                     // chunks in this split
+  const int n_it = nch > w ? (nch - w + WAVES - 1) / WAVES : 0;  // chunks of this wave
+  const int last_c = w + WAVES * (n_it - 1);
 
   f32x4_t acc[NB][MT];
 #pragma unroll
@@ -76,24 +88,26 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint16_t* __rest
 #pragma unroll
   for (int i = 0; i < NB; ++i) wp[i] = Wf + (size_t)(nb0 + i) * KB * 64 + lane;
 
-  for (int kb = kw0; kb < kw1; kb += U) {
-    uint4 wr[U][NB];
-    uint4 xr[U][MT];
+  auto load = [&](uint4 (&wr)[U][NB], uint4 (&xr)[U][MT], int c) {
+    const int kb = kbA + c * U;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int kk = min(kb + u, kw1 - 1);
+      const int kk = min(kb + u, kbB - 1);
 #pragma unroll
       for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int kk = min(kb + u, kw1 - 1);
+      const int kk = min(kb + u, kbB - 1);
 #pragma unroll
       for (int j = 0; j < MT; ++j) xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * 32);
     }
+  };
+  auto comp = [&](const uint4 (&wr)[U][NB], const uint4 (&xr)[U][MT], int c) {
+    const int kb = kbA + c * U;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool live = (kb + u) < kw1;
+      const bool live = (kb + u) < kbB;
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         const bool ok = live && xvalid[j];
@@ -103,6 +117,25 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const uint16_t* __rest
         for (int i = 0; i < NB; ++i) acc[i][j] = mfma16x16x32(wr[u][i], xv, acc[i][j]);
       }
     }
+  };
+
+  if (n_it > 0) {
+    uint4 wA[U][NB], xA[U][MT], wB[U][NB], xB[U][MT];
+    load(wA, xA, w);
+    int i = 0;
+    // sched_barrier(0) pins the issue order: the next chunk's loads all leave before this chunk's
+    // MFMAs (hipcc otherwise interleaves them and keeps only ~8 loads in flight)
+    for (; i + 1 < n_it; i += 2) {
+      load(wB, xB, w + WAVES * (i + 1));
+      __builtin_amdgcn_sched_barrier(0);
+      comp(wA, xA, w + WAVES * i);
+      __builtin_amdgcn_sched_barrier(0);
+      load(wA, xA, min(w + WAVES * (i + 2), last_c));  // clamped: the tail re-reads a cached chunk
+      __builtin_amdgcn_sched_barrier(0);
+      comp(wB, xB, w + WAVES * (i + 1));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (i < n_it) comp(wA, xA, w + WAVES * i);
   }
 
   // cross-wave reduction: red[w][tile][lane]
@@ -259,13 +292,20 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restri
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
+static int g_skinny_waves = 4;  // waves per workgroup (4 -> two 256-thread WGs resident per CU)
+
 template <int MT, int NB, int EPI>
 static void launch_skinny_t(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
                             int ldo, int splitk, hipStream_t s) {
   const int kbps = (KB + splitk - 1) / splitk;
   dim3 grid(NBtot / NB, splitk);
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI>), grid, dim3(512), 0, s, X, ldx, M, KB, Wf, out, ldo, kbps);
+  if (g_skinny_waves == 8)
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 8>), grid, dim3(512), 0, s, X, ldx, M, KB, Wf, out, ldo, kbps);
+  else
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 4>), grid, dim3(256), 0, s, X, ldx, M, KB, Wf, out, ldo, kbps);
 }
+
+extern "C" void lsa_set_skinny_waves(int w) { g_skinny_waves = (w == 8) ? 8 : 4; }
 
 template <int EPI>
 static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,

@@ -92,7 +92,9 @@ extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long pa
 // block_tables[seq * max_blocks + pos / 64], slot pos % 64.  cos/sin: [max_pos, 64] f32.
 // One workgroup per token; each thread rotates 4 (d, d+64) pairs (8 B loads of both halves).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rope_append_kernel(const uint16_t* __restrict__ qkv, const int* __restrict__ pos,
+template <bool PARTS>
+__global__ __launch_bounds__(256) void rope_append_kernel(const uint16_t* __restrict__ qkv, const float* __restrict__ qkv_parts,
+                                                          int nparts, size_t part_stride, const int* __restrict__ pos,
                                                           const int* __restrict__ tok_seq,
                                                           const int* __restrict__ block_tables, int max_blocks,
                                                           const float* __restrict__ cos_t,
@@ -105,20 +107,34 @@ __global__ __launch_bounds__(256) void rope_append_kernel(const uint16_t* __rest
   const int seq = tok_seq ? tok_seq[t] : t;
   const int blk = block_tables[(size_t)seq * max_blocks + (p >> 6)];
   const int off = p & 63;
-  const uint16_t* row = qkv + (size_t)t * (H + 2 * Hkv) * D;
+  const size_t row_off = (size_t)t * (H + 2 * Hkv) * D;
+  const uint16_t* row = qkv + row_off;
+  const float* prow = qkv_parts + row_off;
+  // 4 consecutive values of the fused q|k|v row: bf16 row or the sum of f32 split-K slabs
+  auto load4 = [&](int off, float* v) {
+    if constexpr (PARTS) {
+      float4 a = *reinterpret_cast<const float4*>(prow + off);
+      for (int s = 1; s < nparts; ++s) {
+        const float4 b = *reinterpret_cast<const float4*>(prow + s * part_stride + off);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    } else {
+      const uint2 u = *reinterpret_cast<const uint2*>(row + off);
+      v[0] = bf2f(u.x & 0xffff); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffff); v[3] = bf2f(u.y >> 16);
+    }
+  };
   const float* cr = cos_t + (size_t)p * (D / 2);
   const float* sr = sin_t + (size_t)p * (D / 2);
   // rotation work items: (head, quad) with quad = 4 consecutive d in [0, 64)
   const int nrot = (H + Hkv) * 16;
   for (int it = threadIdx.x; it < nrot; it += blockDim.x) {
     const int hd = it >> 4, d0 = (it & 15) * 4;
-    const uint16_t* src = row + hd * D;
-    const uint2 lo = *reinterpret_cast<const uint2*>(src + d0);
-    const uint2 hi = *reinterpret_cast<const uint2*>(src + d0 + 64);
+    float x0[4], x1[4];
+    load4(hd * D + d0, x0);
+    load4(hd * D + d0 + 64, x1);
     const float4 c = *reinterpret_cast<const float4*>(cr + d0);
     const float4 s = *reinterpret_cast<const float4*>(sr + d0);
-    const float x0[4] = {bf2f(lo.x & 0xffff), bf2f(lo.x >> 16), bf2f(lo.y & 0xffff), bf2f(lo.y >> 16)};
-    const float x1[4] = {bf2f(hi.x & 0xffff), bf2f(hi.x >> 16), bf2f(hi.y & 0xffff), bf2f(hi.y >> 16)};
     const float cc[4] = {c.x, c.y, c.z, c.w}, sn[4] = {s.x, s.y, s.z, s.w};
     float y0[4], y1[4];
 #pragma unroll
@@ -141,18 +157,33 @@ __global__ __launch_bounds__(256) void rope_append_kernel(const uint16_t* __rest
   // v copy: Hkv * 16 chunks of 8 bf16
   for (int it = threadIdx.x; it < Hkv * 16; it += blockDim.x) {
     const int hv = it >> 4, c = (it & 15) * 8;
-    const uint4 v = *reinterpret_cast<const uint4*>(row + (H + Hkv + hv) * D + c);
+    uint4 v;
+    if constexpr (PARTS) {
+      float f[8];
+      load4((H + Hkv + hv) * D + c, f);
+      load4((H + Hkv + hv) * D + c + 4, f + 4);
+      v = pack8(f);
+    } else {
+      v = *reinterpret_cast<const uint4*>(row + (H + Hkv + hv) * D + c);
+    }
     *reinterpret_cast<uint4*>(vc + (((size_t)blk * Hkv + hv) * 64 + off) * D + c) = v;
   }
 }
 
-extern "C" int lsa_rope_append(const void* qkv, const int* pos, const int* tok_seq, const int* block_tables,
+extern "C" int lsa_rope_append(const void* qkv, const float* qkv_parts, int nparts, long part_stride, const int* pos, const int* tok_seq, const int* block_tables,
                                int max_blocks, const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc,
                                int T, int H, int Hkv, hipStream_t s) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL(rope_append_kernel, dim3(T), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(qkv), pos, tok_seq,
-                     block_tables, max_blocks, cos_t, sin_t, reinterpret_cast<uint16_t*>(q_out),
-                     reinterpret_cast<uint16_t*>(kc), reinterpret_cast<uint16_t*>(vc), H, Hkv);
+  if (qkv_parts)
+    hipLaunchKernelGGL(rope_append_kernel<true>, dim3(T), dim3(256), 0, s, nullptr, qkv_parts, nparts,
+                       (size_t)part_stride, pos, tok_seq, block_tables, max_blocks, cos_t, sin_t,
+                       reinterpret_cast<uint16_t*>(q_out), reinterpret_cast<uint16_t*>(kc),
+                       reinterpret_cast<uint16_t*>(vc), H, Hkv);
+  else
+    hipLaunchKernelGGL(rope_append_kernel<false>, dim3(T), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(qkv),
+                       nullptr, 0, (size_t)0, pos, tok_seq, block_tables, max_blocks, cos_t, sin_t,
+                       reinterpret_cast<uint16_t*>(q_out), reinterpret_cast<uint16_t*>(kc),
+                       reinterpret_cast<uint16_t*>(vc), H, Hkv);
   return (int)hipGetLastError();
 }
 

@@ -104,8 +104,9 @@ class ModelRunner:
         self.q = torch.zeros(S, self.H, self.D, **bf)
         self.attn = torch.zeros(S, self.H * self.D, **bf)
         self.act = torch.zeros(S, self.ffn_l, **bf)
-        self.o_buf = torch.zeros(4 * S * self.d, **f32)
-        self.down_buf = torch.zeros(4 * S * self.d, **f32)
+        self.o_buf = torch.zeros(8 * S * self.d, **f32)
+        self.down_buf = torch.zeros(8 * S * self.d, **f32)
+        self.qkv_buf = torch.zeros(8 * S * (self.H + 2 * self.Hkv) * self.D, **f32)
         self.logits_l = torch.zeros(S, self.Vl, **f32)
         self.logits = self.logits_l if tps == 1 else torch.zeros(S, self.V, **f32)
         self.gather_buf = None if tps == 1 else torch.zeros(tps * S * self.Vl, **f32)
@@ -121,10 +122,10 @@ class ModelRunner:
         if self.tp is not None and self.tp.size > 1:
             self.tp.all_reduce(t)
 
-    def _splitk(self, M: int, K: int) -> int:
-        if not self.on_gpu or (self.tp is not None and self.tp.size > 1) or M > 64:
+    def _splitk(self, M: int, K: int, N: Optional[int] = None, tp_reduced: bool = True) -> int:
+        if not self.on_gpu or M > 64 or (tp_reduced and self.tp is not None and self.tp.size > 1):
             return 1
-        return ops.pick_nb_splitk(M, self.d, K, "f32")[1]
+        return ops.pick_nb_splitk(M, N or self.d, K, "f32")[1]
 
     def _lm_head(self, xn: torch.Tensor, M: int) -> torch.Tensor:
         """logits [M, V] (f32) for the normalised rows xn [M, d]."""
@@ -149,8 +150,11 @@ class ModelRunner:
         h, xn = self.h[:B], self.xn[:B]
         sk_o = self._splitk(B, self.H * self.D)
         sk_d = self._splitk(B, self.ffn_l)
+        nqkv = (self.H + 2 * self.Hkv) * self.D
+        sk_q = self._splitk(B, d, nqkv, tp_reduced=False)
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
+        qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
         plan = ops.decode_split_plan(B, self.Hkv, self.max_model_len)
         ws = (self.opart, self.mlpart)
         for l, lw in enumerate(w.layers):
@@ -158,9 +162,10 @@ class ModelRunner:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
             else:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts)
-            ops.linear(xn, lw.wqkv, "bf16", out=self.qkv[:B])
+            # QKV as f32 split-K slabs; rope_append sums them while rotating (no extra reduction pass)
+            ops.linear(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
             kc, vc = self.kv[l, 0], self.kv[l, 1]
-            ops.rope_append(self.qkv[:B], pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv)
+            ops.rope_append(qkv_parts, pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv)
             ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale, self.attn[:B].view(B, self.H,
                                                                                                           self.D),
                             workspace=ws, plan=plan)

@@ -120,17 +120,25 @@ class PackedWeight:
 
 
 def pick_nb_splitk(M: int, N: int, K: int, epi: str) -> tuple[int, int]:
-    """Skinny-GEMM decomposition: >= ~2 workgroups per CU, split-K only for f32 slabs."""
+    """Skinny-GEMM decomposition (from scripts/bench_gemm.py sweeps on MI355X).
+
+    M <= 16: one 16-row block per wave-group (x traffic is negligible), split-K until >= 1024
+    workgroups.  M > 16: 4 blocks (64 rows) per workgroup so each activation fragment feeds 4 MFMAs,
+    split-K until >= 256 workgroups.  Only the f32 epilogue (partial slabs summed by the consumer)
+    can split K.
+    """
     nbt = N // 16
-    nb = 2 if (nbt % 2 == 0 and nbt // 2 >= 512) else 1
+    if M <= 16:
+        nb, target = 1, 1024
+    else:
+        nb, target = (4 if M <= 32 else 2), 256
     if epi == "silu":
-        nb = 2
-    if M > 32 and nb > 2:
-        nb = 2
+        nb = max(nb, 2)
+    while nb > 1 and nbt % nb:
+        nb //= 2
     splitk = 1
-    if epi == "f32":
-        wgs = nbt // nb
-        while wgs * splitk < 384 and splitk < 4 and K // (32 * splitk * 2) >= 16:
+    if epi == "f32" and M <= 64:
+        while (nbt // nb) * splitk < target and splitk < 8 and K // (32 * splitk * 2) >= 16:
             splitk *= 2
     return nb, splitk
 

@@ -70,6 +70,8 @@ def _slots(pos, tok_seq, block_tables):
 
 
 def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv):
+    if qkv.dtype == torch.float32 and qkv.dim() == 3:  # f32 split-K slabs [S, T, n]
+        qkv = qkv.sum(0)
     T = qkv.shape[0]
     D = 128
     x = qkv.float().view(T, H + 2 * Hkv, D)

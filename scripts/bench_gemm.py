@@ -1,0 +1,56 @@
+"""Decode-GEMM sweep on the GPU: effective HBM bandwidth of ops.linear for the 7B / 3B decode
+shapes at M = 1 and 32 over (nb, splitk).  Weights rotate over enough copies (> 256 MiB) that every
+call streams from HBM, as in a real decode step (13.5 GB of weights per token)."""
+import sys, time, json
+import torch
+sys.path.insert(0, ".")
+from llm_based_apache_spark_optimization_amd import ops
+
+dev = torch.device("cuda:0")
+SHAPES = {  # name: (N, K, epi)
+    "7b_qkv": (12288, 4096, "f32"), "7b_o": (4096, 4096, "f32"), "7b_gateup": (22016, 4096, "silu"),
+    "7b_down": (4096, 11008, "f32"), "7b_head": (32000, 4096, "f32"),
+    "3b_qkv": (5120, 3072, "f32"), "3b_o": (3072, 3072, "f32"), "3b_gateup": (16384, 3072, "silu"),
+    "3b_down": (3072, 8192, "f32"), "3b_head": (128256, 3072, "f32"),
+}
+Ms = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 32]
+res = []
+for name, (N, K, epi) in SHAPES.items():
+    nbytes = N * K * 2
+    ncopy = max(2, (600 << 20) // nbytes + 1)
+    ws = [ops.PackedWeight.from_dense((torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)) for _ in range(ncopy)]
+    for M in Ms:
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        best = None
+        for waves in (4, 8):
+         ops.ext().set_skinny_waves(waves)
+         for nb in (1, 2, 4):
+            if (N // 16) % nb or (epi == "silu" and nb == 1) or (M > 32 and nb > 2):
+                continue
+            for sk in ((1, 2, 4, 8) if epi == "f32" else (1,)):
+                if K // 32 // sk < 8:
+                    continue
+                out = torch.empty(sk * M * N if epi == "f32" else M * N, device=dev,
+                                  dtype=torch.float32 if epi == "f32" else torch.bfloat16)
+                o = out.view(sk, M, N) if epi == "f32" else out.view(M, N)[:, : N // 2 if epi == "silu" else N]
+                if epi == "silu":
+                    o = out[: M * N // 2].view(M, N // 2)
+                for i in range(3):
+                    ops.linear(x, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb)
+                torch.cuda.synchronize()
+                it = 60
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for i in range(it):
+                    ops.linear(x, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb)
+                e1.record(); torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1000 / it
+                tbs = nbytes / us / 1e6
+                r = dict(shape=name, M=M, waves=waves, nb=nb, splitk=sk, us=round(us, 2), TBps=round(tbs, 3))
+                res.append(r)
+                if best is None or us < best["us"]:
+                    best = r
+        print("BEST", json.dumps(best), flush=True)
+    del ws
+    torch.cuda.empty_cache()
+json.dump(res, open("gpurun_out/gemm_sweep.json", "w"), indent=0)

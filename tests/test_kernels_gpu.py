@@ -166,6 +166,13 @@ def test_rope_append(gpu, HH):
     assert _rel(q, q2) < 1e-2
     assert _rel(kc, kc2) < 1e-2
     assert torch.equal(vc, vc2)
+    # f32 split-K slab input (the decode path): the kernel sums the slabs while rotating
+    parts = torch.randn(3, T, (H + 2 * Hkv) * D, device=gpu)
+    kc3, vc3, q3 = kc.clone(), vc.clone(), q.clone()
+    kc4, vc4, q4 = kc.clone(), vc.clone(), q.clone()
+    ops.rope_append(parts, pos, tok_seq, bt, cos, sin, q3, kc3, vc3, H, Hkv)
+    ref.rope_append(parts, pos, tok_seq, bt, cos, sin, q4, kc4, vc4, H, Hkv)
+    assert _rel(q3, q4) < 1e-2 and _rel(kc3, kc4) < 1e-2 and _rel(vc3, vc4) < 1e-2
 
 
 # ----------------------------------------------------------------------------------------- attention
