@@ -1,0 +1,239 @@
+"""Ollama-compatible client API.
+
+The reference's only model interface is ``ollama.generate(model=..., system=..., prompt=...)`` and it
+reads ``.response`` (FastAPI/app.py:85-90,105-111; Flask/app.py:102-107,160-165;
+Model_Evaluation_&_Comparision.py:23,114).  This module keeps that call shape::
+
+    from llm_based_apache_spark_optimization_amd import client
+    res = client.generate(model="duckdb-nsql", system=..., prompt=...)
+    sql = res.response            # or res["response"]
+
+and returns the timing fields Ollama reports (``eval_count``, ``eval_duration``, ``prompt_eval_*``,
+``load_duration``, ``total_duration``).  Backends (``set_backend``):
+
+* ``EngineService`` — in-process MI355X engines (one ``LLMEngine`` per model, continuous batching on a
+  background thread so concurrent callers share decode steps);
+* ``FakeBackend`` — deterministic canned outputs for tests (with fault injection);
+* ``RemoteBackend`` — HTTP ``POST /api/generate`` on an Ollama-compatible server (this package's
+  FastAPI app, or a real Ollama daemon);
+* ``parallel.router.ReplicaRouter`` — data-parallel dispatch across engine replica processes.
+"""
+from __future__ import annotations
+
+import dataclasses
+import datetime as _dt
+import json
+import threading
+import time
+from typing import Callable, Dict, Optional
+
+from .engine.engine import SamplingParams
+
+
+@dataclasses.dataclass
+class GenerateResponse:
+    model: str
+    response: str
+    done: bool = True
+    done_reason: str = "stop"
+    created_at: str = ""
+    total_duration: int = 0
+    load_duration: int = 0
+    prompt_eval_count: int = 0
+    prompt_eval_duration: int = 0
+    eval_count: int = 0
+    eval_duration: int = 0
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+    def get(self, k, default=None):
+        return getattr(self, k, default)
+
+    def to_dict(self) -> dict:
+        return dataclasses.asdict(self)
+
+    @property
+    def tokens_per_second(self) -> float:
+        return self.eval_count / (self.eval_duration / 1e9) if self.eval_duration else 0.0
+
+
+def _now() -> str:
+    return _dt.datetime.now(_dt.timezone.utc).isoformat()
+
+
+class Backend:
+    def generate(self, model: str, prompt: str, system: str = "", options: Optional[dict] = None,
+                 raw: bool = False) -> GenerateResponse:
+        raise NotImplementedError
+
+    def models(self) -> list:
+        return []
+
+    def health(self) -> dict:
+        return {"ok": True}
+
+
+# -------------------------------------------------------------------------------------- engines
+class _EngineLoop:
+    """Drives one LLMEngine from a background thread; callers block on their request's event."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        self._cv = threading.Condition()
+        self._stop = False
+        self._err: Optional[BaseException] = None
+        self._t = threading.Thread(target=self._run, name=f"engine-{engine.name}", daemon=True)
+        self._t.start()
+
+    def submit(self, ids, params):
+        req = self.engine.add_request(ids, params)
+        with self._cv:
+            self._cv.notify()
+        return req
+
+    def _run(self):
+        while not self._stop:
+            with self._cv:
+                while not self._stop and not self.engine.has_work():
+                    self._cv.wait(timeout=0.5)
+            if self._stop:
+                return
+            try:
+                self.engine.step()
+            except BaseException as e:  # noqa: BLE001 - surface to waiting callers
+                self._err = e
+                for r in list(self.engine._reqs.values()):
+                    r.error = repr(e)
+                    r.done.set()
+                return
+
+    def alive(self) -> bool:
+        return self._t.is_alive() and self._err is None
+
+    def close(self):
+        self._stop = True
+        with self._cv:
+            self._cv.notify_all()
+
+
+class EngineService(Backend):
+    """Named in-process engines (built lazily through ``factory``) behind the Ollama call shape."""
+
+    def __init__(self, factory: Callable[[str], object], defaults: Optional[dict] = None,
+                 timeout_s: float = 300.0):
+        self._factory = factory
+        self._loops: Dict[str, _EngineLoop] = {}
+        self._lock = threading.Lock()
+        self.defaults = defaults or {}
+        self.timeout_s = timeout_s
+
+    def loop(self, model: str) -> _EngineLoop:
+        with self._lock:
+            if model not in self._loops:
+                self._loops[model] = _EngineLoop(self._factory(model))
+            return self._loops[model]
+
+    def generate(self, model, prompt, system="", options=None, raw=False) -> GenerateResponse:
+        lp = self.loop(model)
+        eng = lp.engine
+        opts = dict(self.defaults)
+        opts.update(options or {})
+        params = SamplingParams.from_ollama_options(opts, default_max=int(opts.get("num_predict", 256)))
+        ids = eng.encode(eng.render(prompt, system, raw))
+        req = lp.submit(ids, params)
+        if not req.done.wait(self.timeout_s):
+            raise TimeoutError(f"generation on {model} timed out after {self.timeout_s}s")
+        if req.error:
+            raise RuntimeError(f"engine {model} failed: {req.error}")
+        r = eng.result(req)
+        return GenerateResponse(model=model, response=r.text, done_reason=r.done_reason, created_at=_now(),
+                                total_duration=r.total_duration_ns, load_duration=r.load_duration_ns,
+                                prompt_eval_count=r.prompt_tokens, prompt_eval_duration=r.prompt_eval_duration_ns,
+                                eval_count=r.eval_count, eval_duration=r.eval_duration_ns)
+
+    def models(self) -> list:
+        return sorted(self._loops)
+
+    def health(self) -> dict:
+        return {"ok": all(lp.alive() for lp in self._loops.values()),
+                "engines": {m: {"alive": lp.alive(), "running": lp.engine.sched.num_running,
+                                "waiting": lp.engine.sched.num_waiting, "kv_usage": lp.engine.sched.kv_usage,
+                                **lp.engine.stats} for m, lp in self._loops.items()}}
+
+
+# -------------------------------------------------------------------------------------- fake
+class FakeBackend(Backend):
+    """Deterministic stand-in for tests: NL->SQL returns ``sql_for(prompt)``, explain returns a fixed
+    analysis.  ``fail_next`` injects an exception (failure-path tests)."""
+
+    def __init__(self, sql: Optional[Callable[[str, str], str]] = None, explanation: str = ""):
+        self.sql = sql or (lambda prompt, system: "SELECT * FROM temp_view LIMIT 10;")
+        self.explanation = explanation or ("The query references a column that does not exist in temp_view. "
+                                           "Check the column names in the table schema and correct the query.")
+        self.calls = []
+        self.fail_next: Optional[BaseException] = None
+        self._lock = threading.Lock()
+
+    def generate(self, model, prompt, system="", options=None, raw=False) -> GenerateResponse:
+        with self._lock:
+            self.calls.append({"model": model, "prompt": prompt, "system": system, "options": options})
+            if self.fail_next is not None:
+                e, self.fail_next = self.fail_next, None
+                raise e
+        t0 = time.perf_counter()
+        if options and options.get("fake_delay"):
+            time.sleep(float(options["fake_delay"]))
+        text = self.explanation if "Spark error" in prompt or "troubleshoot" in system else self.sql(prompt, system)
+        dt = int((time.perf_counter() - t0) * 1e9)
+        return GenerateResponse(model=model, response=text, created_at=_now(), total_duration=dt,
+                                eval_count=len(text.split()), eval_duration=dt, prompt_eval_count=len(prompt.split()))
+
+    def models(self):
+        return ["duckdb-nsql", "llama3.2", "mistral"]
+
+
+# -------------------------------------------------------------------------------------- remote
+class RemoteBackend(Backend):
+    def __init__(self, url: str = "http://127.0.0.1:8000", timeout_s: float = 300.0):
+        self.url = url.rstrip("/")
+        self.timeout_s = timeout_s
+
+    def generate(self, model, prompt, system="", options=None, raw=False) -> GenerateResponse:
+        import urllib.request
+
+        body = json.dumps({"model": model, "prompt": prompt, "system": system, "options": options or {},
+                           "stream": False, "raw": raw}).encode()
+        req = urllib.request.Request(self.url + "/api/generate", data=body, headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=self.timeout_s) as f:
+            d = json.loads(f.read())
+        fields = {f.name for f in dataclasses.fields(GenerateResponse)}
+        return GenerateResponse(**{k: v for k, v in d.items() if k in fields})
+
+
+# -------------------------------------------------------------------------------------- module API
+_backend: Optional[Backend] = None
+_blk = threading.Lock()
+
+
+def set_backend(b: Backend) -> None:
+    global _backend
+    with _blk:
+        _backend = b
+
+
+def get_backend() -> Backend:
+    global _backend
+    with _blk:
+        if _backend is None:
+            from .serving.service import backend_from_settings
+            from .config import Settings
+
+            _backend = backend_from_settings(Settings())
+        return _backend
+
+
+def generate(model: str, prompt: str = "", system: str = "", options: Optional[dict] = None, raw: bool = False,
+             **_ignored) -> GenerateResponse:
+    """Drop-in for ``ollama.generate(model=, system=, prompt=)``."""
+    return get_backend().generate(model, prompt, system, options, raw)
