@@ -85,13 +85,18 @@ def timestamp() -> str:
 
 
 def unique_path(path: str) -> str:
-    if not os.path.exists(path):
-        return path
+    """Atomically reserve ``path`` (or ``base_N.ext``) with O_CREAT|O_EXCL: concurrent requests that
+    compute the same name in the same second never share a file."""
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     base, ext = os.path.splitext(path)
-    i = 1
-    while os.path.exists(f"{base}_{i}{ext}"):
-        i += 1
-    return f"{base}_{i}{ext}"
+    cand, i = path, 0
+    while True:
+        try:
+            os.close(os.open(cand, os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o644))
+            return cand
+        except FileExistsError:
+            i += 1
+            cand = f"{base}_{i}{ext}"
 
 
 class Pipeline:
