@@ -32,7 +32,9 @@ int lsa_sample_commit(float* logits, int B, int V, unsigned long long* part, uns
 int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out, int epi,
                  int nb, int splitk, hipStream_t stream);
 int lsa_fp8_dequant(const void* Wq, const float* wscale, int N, int K, void* Wf, hipStream_t s);
-void lsa_set_skinny_waves(int w);
+int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
+                 int waves, int div, int xlds, hipStream_t stream);
+int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 }
 
 namespace {
@@ -53,7 +55,7 @@ T* ptr(const c10::optional<at::Tensor>& t) {
 
 // out = x @ W^T with W in fragment-major layout (see kernels/gemm.hip)
 void gemm(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, int64_t nb,
-          int64_t splitk) {
+          int64_t splitk, int64_t waves, int64_t div, int64_t xlds) {
   need(x, at::kBFloat16, "x");
   need(wf, at::kBFloat16, "wf");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
@@ -66,7 +68,8 @@ void gemm(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out,
     need(out, at::kBFloat16, "out");
     TORCH_CHECK(out.numel() >= M * (epi == 2 ? N / 2 : N), "bf16 out too small");
   }
-  check(lsa_gemm(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, nb, splitk, cur_stream()),
+  check(lsa_gemm_cfg(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, nb, splitk, waves, div,
+                     xlds, cur_stream()),
         "gemm");
 }
 
@@ -182,7 +185,8 @@ void fp8_dequant(const at::Tensor& wq, const at::Tensor& wscale, int64_t N, int6
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the MI355X NL->SQL / Spark-error inference engine";
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"),
+        py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4, py::arg("xlds") = 0);
   m.def("fp8_gemm", &fp8_gemm);
   m.def("add_rmsnorm", &add_rmsnorm);
   m.def("rope_append", &rope_append);
@@ -192,6 +196,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);
   m.def("fp8_dequant", &fp8_dequant);
-  m.def("set_skinny_waves", [](int64_t w) { lsa_set_skinny_waves((int)w); });
+  m.def("silu_parts", [](const at::Tensor& parts, at::Tensor& out) {
+    // parts: f32 [S, M, 2F] (gate/up interleaved per 16 rows) -> out bf16 [M, F] = silu(gate) * up
+    need(parts, at::kFloat, "parts");
+    need(out, at::kBFloat16, "out");
+    const int S = parts.size(0), M = parts.size(1), F = parts.size(2) / 2;
+    check(lsa_silu_parts(parts.data_ptr<float>(), S, parts.stride(0), M, F, out.data_ptr(), cur_stream()),
+          "silu_parts");
+  });
   m.attr("arch") = "gfx950";
 }

@@ -48,17 +48,18 @@ __device__ __forceinline__ void store4(void* out, int ldo, size_t slab, int m, i
 // k-steps are clamped (duplicate L2 hits) and masked by zeroing the activation fragment, never by a
 // per-load branch (which would force vmcnt(0) per element).
 // ------------------------------------------------------------------------------------------------
-template <int MT, int NB>
+template <int MT, int NB, int DIV = 1>
 struct SkinnyCfg {
-  static constexpr int U = (16 / (NB > 2 * MT ? NB : 2 * MT)) < 2 ? 2 : (16 / (NB > 2 * MT ? NB : 2 * MT));
+  static constexpr int U0 = (16 / (NB > 2 * MT ? NB : 2 * MT)) < 2 ? 2 : (16 / (NB > 2 * MT ? NB : 2 * MT));
+  static constexpr int U = (U0 / DIV) < 1 ? 1 : (U0 / DIV);
 };
 
-template <int MT, int NB, int EPI, int WAVES>
+template <int MT, int NB, int EPI, int WAVES, int DIV = 1>
 __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
                                                                  int KB, const uint4* __restrict__ Wf,
                                                                  void* __restrict__ out, int ldo,
                                                                  int kb_per_split) {
-  constexpr int U = SkinnyCfg<MT, NB>::U;
+  constexpr int U = SkinnyCfg<MT, NB, DIV>::U;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -182,6 +183,119 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 }
 
 // ------------------------------------------------------------------------------------------------
+// decode kernel with the activation block staged in LDS (M in 17..64, f32 split-K slabs only)
+//
+// At M = 32 the fragment-shaped activation loads (16 rows x 64 B per wave-instruction) cost as much
+// memory-pipe issue as the weight stream itself (rocprofv3: +20 % VMEM instructions, +18 % issue
+// stalls vs M = 1).  Here the workgroup first copies its x[0:M, k-range] block into LDS with
+// full-line, coalesced 16 B loads (XOR-swizzled by row so the 16 rows a ds_read_b128 lane group
+// reads sit in distinct bank slots), then the waves stream only weights from HBM and read their
+// B fragments from LDS.  No x registers -> ~100 fewer VGPRs -> more resident waves.
+// ------------------------------------------------------------------------------------------------
+template <int MT, int NB, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void gemm_xlds_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
+                                                               const uint4* __restrict__ Wf, float* __restrict__ out,
+                                                               int ldo, int kb_per_split) {
+  constexpr int U = 16 / NB;
+  extern __shared__ __attribute__((aligned(16))) uint4 xs[];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int nb0 = blockIdx.x * NB;
+  const int kbA = blockIdx.y * kb_per_split;
+  const int kbB = min(KB, kbA + kb_per_split);
+  const int nk = kbB - kbA;
+  const int ppr = nk * 4;                       // 16 B pieces per staged row
+  const int swz = (ppr & 15) == 0 ? 15 : 0;     // row XOR (needs >= 16 pieces per row)
+  // 1) stage x[0:16*MT, k-range] (rows >= M zero-filled)
+  for (int idx = threadIdx.x; idx < 16 * MT * ppr; idx += 64 * WAVES) {
+    const int row = idx / ppr, pc = idx - row * ppr;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (row < M) v = *reinterpret_cast<const uint4*>(X + (size_t)row * ldx + (size_t)kbA * 32 + pc * 8);
+    xs[row * ppr + (pc ^ (row & swz))] = v;
+  }
+  __syncthreads();
+
+  const int nch = (nk + U - 1) / U;
+  const int n_it = nch > w ? (nch - w + WAVES - 1) / WAVES : 0;
+  const int last_c = w + WAVES * (n_it - 1);
+  f32x4_t acc[NB][MT];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const uint4* wp[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) wp[i] = Wf + (size_t)(nb0 + i) * KB * 64 + lane;
+
+  auto load = [&](uint4 (&wr)[U][NB], int c) {
+    const int kb = kbA + c * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = min(kb + u, kbB - 1);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
+    }
+  };
+  auto comp = [&](uint4 (&wr)[U][NB], int c) {
+    const int rel0 = c * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rel = rel0 + u;
+      const bool live = rel < nk;
+      const int pc = min(rel, nk - 1) * 4 + g;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        uint4 wv = wr[u][i];
+        wv.x = live ? wv.x : 0u; wv.y = live ? wv.y : 0u; wv.z = live ? wv.z : 0u; wv.w = live ? wv.w : 0u;
+        wr[u][i] = wv;
+      }
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        const int row = j * 16 + r;
+        const uint4 xv = xs[row * ppr + (pc ^ (row & swz))];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) acc[i][j] = mfma16x16x32(wr[u][i], xv, acc[i][j]);
+      }
+    }
+  };
+  if (n_it > 0) {
+    uint4 wA[U][NB], wB[U][NB];
+    load(wA, w);
+    int i = 0;
+    for (; i + 1 < n_it; i += 2) {
+      load(wB, w + WAVES * (i + 1));
+      __builtin_amdgcn_sched_barrier(0);
+      comp(wA, w + WAVES * i);
+      __builtin_amdgcn_sched_barrier(0);
+      load(wA, min(w + WAVES * (i + 2), last_c));
+      __builtin_amdgcn_sched_barrier(0);
+      comp(wB, w + WAVES * (i + 1));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (i < n_it) comp(wA, w + WAVES * i);
+  }
+  // cross-wave reduction reuses the x staging area (all waves are past their last x read)
+  __syncthreads();
+  f32x4_t* red = reinterpret_cast<f32x4_t*>(xs);  // [WAVES][NB*MT][64]
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) red[(w * NB * MT + i * MT + j) * 64 + lane] = acc[i][j];
+  __syncthreads();
+  const size_t slab = (size_t)blockIdx.y * M * ldo;
+  for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
+    const int l = idx & 63, t = idx >> 6;
+    const int j = t % MT, i = t / MT;
+    f32x4_t sacc = red[t * 64 + l];
+#pragma unroll
+    for (int ww = 1; ww < WAVES; ++ww) sacc += red[(ww * NB * MT + t) * 64 + l];
+    const int m = j * 16 + (l & 15);
+    if (m < M) store4<EPI_F32>(out, ldo, slab, m, (nb0 + i) * 16 + 4 * (l >> 4), sacc);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // prefill / large-M kernel: 128 (N) x 128 (M) x 64 (K) tile, 4 waves (2 x 2) of 64 x 64
 // ------------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -292,20 +406,43 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restri
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
-static int g_skinny_waves = 4;  // waves per workgroup (4 -> two 256-thread WGs resident per CU)
+// Per-call tuning knobs (chosen by ops.pick_gemm_config from the measured table):
+//   waves 4|8 per workgroup; div 1|2|4 divides the chunk depth U (fewer VGPRs -> more resident waves;
+//   on MI355X div 4 won most decode shapes, scripts/bench_gemm.py).
+static thread_local int g_skinny_waves = 4;
+static thread_local int g_skinny_div = 4;
 
 template <int MT, int NB, int EPI>
 static void launch_skinny_t(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
                             int ldo, int splitk, hipStream_t s) {
   const int kbps = (KB + splitk - 1) / splitk;
   dim3 grid(NBtot / NB, splitk);
+  if (g_skinny_div == 2) {
+    if (g_skinny_waves == 8)
+      hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 8, 2>), grid, dim3(512), 0, s, X, ldx, M, KB, Wf, out, ldo,
+                         kbps);
+    else
+      hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 4, 2>), grid, dim3(256), 0, s, X, ldx, M, KB, Wf, out, ldo,
+                         kbps);
+    return;
+  }
+  if (g_skinny_div == 4) {
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 4, 4>), grid, dim3(256), 0, s, X, ldx, M, KB, Wf, out, ldo,
+                       kbps);
+    return;
+  }
   if (g_skinny_waves == 8)
     hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 8>), grid, dim3(512), 0, s, X, ldx, M, KB, Wf, out, ldo, kbps);
   else
     hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 4>), grid, dim3(256), 0, s, X, ldx, M, KB, Wf, out, ldo, kbps);
 }
 
-extern "C" void lsa_set_skinny_waves(int w) { g_skinny_waves = (w == 8) ? 8 : 4; }
+
+
+// LDS-staged activation kernel for 16 < M <= 64 (f32 epilogue): measured slower than the register
+// pipeline with div 4 on every decode shape (its x prologue delays the weight stream), so it is off
+// unless a tuning entry asks for it.
+static thread_local int g_xlds = 0;
 
 template <int EPI>
 static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
@@ -323,13 +460,48 @@ static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uin
   launch_skinny_t<4, 2, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);
 }
 
+extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
+                            int splitk, int waves, int div, int xlds, hipStream_t stream);
+
 extern "C" int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
                         int splitk, hipStream_t stream) {
+  return lsa_gemm_cfg(X, ldx, M, K, Wf, N, out, epi, nb, splitk, 4, 4, 0, stream);
+}
+
+extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
+                            int splitk, int waves, int div, int xlds, hipStream_t stream) {
+  g_skinny_waves = (waves == 8) ? 8 : 4;
+  g_skinny_div = (div == 1 || div == 2) ? div : 4;
+  g_xlds = xlds ? 1 : 0;
   if (K % 32 != 0 || N % 16 != 0 || M <= 0) return -1;
   const int KB = K / 32, NBtot = N / 16;
   const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
   const uint4* w = reinterpret_cast<const uint4*>(Wf);
   const int ldo = (epi == EPI_SILU) ? N / 2 : N;
+  if (M > 16 && M <= 64 && epi == EPI_F32 && g_xlds) {
+    if (nb <= 0) nb = 4;
+    if (M > 32 && nb > 2) nb = 2;
+    if (NBtot % nb != 0) return -2;
+    if (splitk < 1) splitk = 1;
+    const int kbps = (KB + splitk - 1) / splitk;
+    const int mt = M <= 32 ? 2 : 4;
+    const size_t xbytes = (size_t)16 * mt * kbps * 64;
+    const size_t rbytes = (size_t)g_skinny_waves * nb * mt * 64 * 16;
+    const size_t lds = xbytes > rbytes ? xbytes : rbytes;
+    if (lds <= 64 * 1024) {
+      dim3 grid(NBtot / nb, splitk);
+      float* o = reinterpret_cast<float*>(out);
+#define LSA_XL(MTV, NBV, WV)                                                                               \
+  if (mt == MTV && nb == NBV && g_skinny_waves == WV) {                                                    \
+    hipLaunchKernelGGL((gemm_xlds_kernel<MTV, NBV, WV>), grid, dim3(64 * WV), lds, stream, x, ldx, M, KB, w, o, \
+                       N, kbps);                                                                           \
+    return (int)hipGetLastError();                                                                        \
+  }
+      LSA_XL(2, 4, 4) LSA_XL(2, 2, 4) LSA_XL(2, 1, 4) LSA_XL(4, 2, 4) LSA_XL(4, 1, 4)
+      LSA_XL(2, 4, 8) LSA_XL(2, 2, 8) LSA_XL(2, 1, 8) LSA_XL(4, 2, 8) LSA_XL(4, 1, 8)
+#undef LSA_XL
+    }
+  }
   if (M <= 64) {
     if (nb <= 0) nb = 1;
     if (epi == EPI_SILU && nb < 2) nb = 2;

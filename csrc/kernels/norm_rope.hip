@@ -209,3 +209,39 @@ extern "C" int lsa_silu_mul(const void* g, const void* u, void* o, long n, hipSt
                      reinterpret_cast<const uint16_t*>(u), reinterpret_cast<uint16_t*>(o), n8);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------
+// silu(gate) * up from f32 split-K slabs of the interleaved gate_up projection:
+// parts [S][M][2F], column block 2j = gate rows 16j..16j+15, block 2j+1 = up rows 16j..  -> out [M][F] bf16
+__global__ __launch_bounds__(256) void silu_parts_kernel(const float* __restrict__ parts, int nparts, size_t stride,
+                                                         int M, int F, uint16_t* __restrict__ out) {
+  const long total4 = (long)M * F / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+    const long e = i * 4;
+    const int m = (int)(e / F), f = (int)(e - (long)m * F);
+    const int blk = f >> 4, off = f & 15;
+    const size_t gi = (size_t)m * 2 * F + (size_t)(2 * blk) * 16 + off;
+    float4 gs = *reinterpret_cast<const float4*>(parts + gi);
+    float4 us = *reinterpret_cast<const float4*>(parts + gi + 16);
+    for (int s = 1; s < nparts; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(parts + s * stride + gi);
+      const float4 b = *reinterpret_cast<const float4*>(parts + s * stride + gi + 16);
+      gs.x += a.x; gs.y += a.y; gs.z += a.z; gs.w += a.w;
+      us.x += b.x; us.y += b.y; us.z += b.z; us.w += b.w;
+    }
+    uint2 pk;
+    pk.x = pack2bf(silu(gs.x) * us.x, silu(gs.y) * us.y);
+    pk.y = pack2bf(silu(gs.z) * us.z, silu(gs.w) * us.w);
+    *reinterpret_cast<uint2*>(out + e) = pk;
+  }
+}
+
+extern "C" int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out,
+                              hipStream_t s) {
+  if (F % 16) return -1;
+  const long total4 = (long)M * F / 4;
+  const long gl = (total4 + 255) / 256;
+  hipLaunchKernelGGL(silu_parts_kernel, dim3((unsigned)(gl < 4096 ? gl : 4096)), dim3(256), 0, s, parts, nparts,
+                     (size_t)part_stride, M, F, reinterpret_cast<uint16_t*>(out));
+  return (int)hipGetLastError();
+}

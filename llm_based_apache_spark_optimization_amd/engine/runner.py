@@ -125,7 +125,7 @@ class ModelRunner:
     def _splitk(self, M: int, K: int, N: Optional[int] = None, tp_reduced: bool = True) -> int:
         if not self.on_gpu or M > 64 or (tp_reduced and self.tp is not None and self.tp.size > 1):
             return 1
-        return ops.pick_nb_splitk(M, N or self.d, K, "f32")[1]
+        return ops.pick_gemm_config(M, N or self.d, K, "f32")[1]
 
     def _lm_head(self, xn: torch.Tensor, M: int) -> torch.Tensor:
         """logits [M, V] (f32) for the normalised rows xn [M, d]."""

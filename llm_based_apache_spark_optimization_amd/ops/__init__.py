@@ -13,6 +13,8 @@ from __future__ import annotations
 
 import dataclasses
 import importlib
+import json
+import os
 from typing import Optional
 
 import torch
@@ -143,12 +145,43 @@ def pick_nb_splitk(M: int, N: int, K: int, epi: str) -> tuple[int, int]:
     return nb, splitk
 
 
+# ----------------------------------------------------------------------------------- tuning
+_TUNING_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
+_tuning: Optional[dict] = None
+
+
+def _tuning_table() -> dict:
+    """Measured best decode-GEMM configs on MI355X ({"NxK:epi:s|m": {nb, splitk, waves, div}}),
+    produced by scripts/bench_gemm.py (median of 3 interleaved runs per config)."""
+    global _tuning
+    if _tuning is None:
+        try:
+            with open(_TUNING_PATH) as f:
+                _tuning = json.load(f)
+        except (OSError, ValueError):
+            _tuning = {}
+    return _tuning
+
+
+def pick_gemm_config(M: int, N: int, K: int, epi: str) -> tuple[int, int, int, int]:
+    """(nb, splitk, waves, div) for a decode GEMM: the tuning table when it has the shape, else the
+    heuristic below (div 4, 4-wave workgroups won most measured shapes)."""
+    if M <= 64:
+        key = f"{N}x{K}:{epi}:{'s' if M <= 16 else 'm'}"
+        e = _tuning_table().get(key)
+        if e is not None and not (M > 32 and e["nb"] > 2):
+            return e["nb"], e["splitk"], e["waves"], e["div"]
+    nb, sk = pick_nb_splitk(M, N, K, epi)
+    return nb, sk, 4, 4
+
+
 # ----------------------------------------------------------------------------------- linear
 _dq_scratch: dict = {}
 
 
 def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
-           splitk: Optional[int] = None, nb: Optional[int] = None) -> torch.Tensor:
+           splitk: Optional[int] = None, nb: Optional[int] = None, waves: Optional[int] = None,
+           div: Optional[int] = None) -> torch.Tensor:
     """y = x @ W^T with a fused epilogue.  epi='f32' returns [splitk, M, N] partial slabs."""
     M, K = x.shape
     assert K == w.K, (K, w.K)
@@ -160,9 +193,11 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
             out.view(-1)[: y.numel()].copy_(y.reshape(-1))
             return out
         return y
-    nb0, sk0 = pick_nb_splitk(M, w.N, K, epi)
+    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi)
     nb = nb0 if nb is None else nb
     splitk = sk0 if splitk is None else splitk
+    waves = wv0 if waves is None else waves
+    div = dv0 if div is None else div
     if M > 64:
         splitk = 1
     if out is None:
@@ -172,7 +207,7 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
             out = torch.empty(M, w.N // 2 if epi == "silu" else w.N, device=x.device, dtype=torch.bfloat16)
     e = ext()
     if w.kind == "bf16":
-        e.gemm(x, w.data, w.N, out, EPI[epi], nb, splitk)
+        e.gemm(x, w.data, w.N, out, EPI[epi], nb, splitk, waves, div)
     elif w.kind == "fp8":
         if M <= 64:
             e.fp8_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk)
@@ -183,7 +218,7 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
                 buf = torch.empty(w.N * w.K, device=x.device, dtype=torch.bfloat16)
                 _dq_scratch[x.device] = buf
             e.fp8_dequant(w.data, w.scale, w.N, w.K, buf)
-            e.gemm(x, buf[: w.N * w.K], w.N, out, EPI[epi], nb, 1)
+            e.gemm(x, buf[: w.N * w.K], w.N, out, EPI[epi], nb, 1, waves, div)
             del key
     else:
         raise ValueError(f"weight kind {w.kind} on GPU")
@@ -208,6 +243,18 @@ def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H,
     if not _gpu(qkv):
         return ref.rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
     ext().rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
+
+
+def silu_parts(parts: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out [M, F] = silu(gate) * up from f32 split-K slabs [S, M, 2F] of the interleaved gate_up GEMM."""
+    if not _gpu(parts):
+        S, M, N = parts.shape
+        y = parts.float().sum(0).view(M, N // 32, 2, 16)
+        g, u = y[:, :, 0, :].reshape(M, N // 2), y[:, :, 1, :].reshape(M, N // 2)
+        out.copy_((torch.nn.functional.silu(g) * u).to(out.dtype))
+        return out
+    ext().silu_parts(parts, out)
+    return out
 
 
 def silu_mul(g: torch.Tensor, u: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

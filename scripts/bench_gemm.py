@@ -9,11 +9,14 @@ from llm_based_apache_spark_optimization_amd import ops
 dev = torch.device("cuda:0")
 SHAPES = {  # name: (N, K, epi)
     "7b_qkv": (12288, 4096, "f32"), "7b_o": (4096, 4096, "f32"), "7b_gateup": (22016, 4096, "silu"),
-    "7b_down": (4096, 11008, "f32"), "7b_head": (32000, 4096, "f32"),
+    "7b_down": (4096, 11008, "f32"), "7b_head": (32000, 4096, "f32"), "7b_gateup_f32": (22016, 4096, "f32"),
     "3b_qkv": (5120, 3072, "f32"), "3b_o": (3072, 3072, "f32"), "3b_gateup": (16384, 3072, "silu"),
-    "3b_down": (3072, 8192, "f32"), "3b_head": (128256, 3072, "f32"),
+    "3b_down": (3072, 8192, "f32"), "3b_head": (128256, 3072, "f32"), "3b_gateup_f32": (16384, 3072, "f32"),
 }
 Ms = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 32]
+only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+if only:
+    SHAPES = {k: v for k, v in SHAPES.items() if k in only}
 res = []
 for name, (N, K, epi) in SHAPES.items():
     nbytes = N * K * 2
@@ -22,8 +25,7 @@ for name, (N, K, epi) in SHAPES.items():
     for M in Ms:
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
         best = None
-        for waves in (4, 8):
-         ops.ext().set_skinny_waves(waves)
+        for waves, xl, dv in ((4, 0, 1), (4, 0, 2), (8, 0, 2), (4, 0, 4), (8, 0, 4)):
          for nb in (1, 2, 4):
             if (N // 16) % nb or (epi == "silu" and nb == 1) or (M > 32 and nb > 2):
                 continue
@@ -36,17 +38,20 @@ for name, (N, K, epi) in SHAPES.items():
                 if epi == "silu":
                     o = out[: M * N // 2].view(M, N // 2)
                 for i in range(3):
-                    ops.linear(x, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb)
+                    ops.linear(x, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb, waves=waves, div=dv)
                 torch.cuda.synchronize()
-                it = 60
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for i in range(it):
-                    ops.linear(x, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb)
-                e1.record(); torch.cuda.synchronize()
-                us = e0.elapsed_time(e1) * 1000 / it
+                it = 40
+                reps = []
+                for _rep in range(3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for i in range(it):
+                        ops.linear(x, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb, waves=waves, div=dv)
+                    e1.record(); torch.cuda.synchronize()
+                    reps.append(e0.elapsed_time(e1) * 1000 / it)
+                us = sorted(reps)[1]
                 tbs = nbytes / us / 1e6
-                r = dict(shape=name, M=M, waves=waves, nb=nb, splitk=sk, us=round(us, 2), TBps=round(tbs, 3))
+                r = dict(shape=name, M=M, waves=waves, xlds=xl, div=dv, nb=nb, splitk=sk, us=round(us, 2), TBps=round(tbs, 3))
                 res.append(r)
                 if best is None or us < best["us"]:
                     best = r
@@ -54,3 +59,11 @@ for name, (N, K, epi) in SHAPES.items():
     del ws
     torch.cuda.empty_cache()
 json.dump(res, open("gpurun_out/gemm_sweep.json", "w"), indent=0)
+# tuning table: (N, K, epi, M-class) -> best (waves, nb, splitk)
+table = {}
+for r in res:
+    N, K, epi = SHAPES[r["shape"]]
+    key = f"{N}x{K}:{epi}:{'s' if r['M'] <= 16 else 'm'}"
+    if key not in table or r["us"] < table[key]["us"]:
+        table[key] = {"waves": r["waves"], "div": r["div"], "nb": r["nb"], "splitk": r["splitk"], "us": r["us"], "TBps": r["TBps"]}
+json.dump(table, open("gpurun_out/gemm_tuning.json", "w"), indent=1)

@@ -58,6 +58,37 @@ def test_gemm_silu(gpu, M):
     assert _rel(y, yr) < 1e-2
 
 
+@pytest.mark.parametrize("M", [17, 32, 48, 64])
+@pytest.mark.parametrize("splitk", [1, 4, 8])
+def test_gemm_xlds_f32(gpu, M, splitk):
+    """16 < M <= 64, f32 slabs: the LDS-staged activation kernel (when the block fits) vs fp32."""
+    N, K = 1024, 4096
+    torch.manual_seed(M + splitk)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    y = torch.empty(splitk, M, N, device=gpu)
+    ops.ext().gemm(x, pw.data, N, y, 1, 4 if M <= 32 else 2, splitk, 4, 4, 1)  # xlds=1
+    assert _rel(y.sum(0), x.float() @ w.float().t()) < 1e-4
+    for div in (1, 2, 4):
+        y2 = ops.linear(x, pw, "f32", splitk=splitk, div=div)
+        assert _rel(y2.sum(0), y.sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("M", [1, 32])
+def test_silu_parts(gpu, M):
+    F, K = 512, 1024
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    wg = (torch.randn(F, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+    wu = (torch.randn(F, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(ops.interleave_gate_up(wg, wu))
+    parts = ops.linear(x, pw, "f32", splitk=2)
+    act = torch.empty(M, F, device=gpu, dtype=torch.bfloat16)
+    ops.silu_parts(parts, act)
+    yr = torch.nn.functional.silu(x.float() @ wg.float().t()) * (x.float() @ wu.float().t())
+    assert _rel(act, yr) < 1e-2
+
+
 @pytest.mark.parametrize("M", [65, 128, 200, 1000])
 @pytest.mark.parametrize("NK", [(800, 4096), (1024, 1376), (4096, 512)])
 @pytest.mark.parametrize("epi", ["bf16", "f32"])
