@@ -165,19 +165,36 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
   }
 }
 
+// merge the split-KV partials of one (sequence, head): the split maxima / weights go through LDS once,
+// then every thread sums its output dim over the splits with independent (pipelined) loads
 __global__ __launch_bounds__(128) void attn_combine_kernel(const float* __restrict__ opart,
                                                            const float* __restrict__ mlpart, int nsplit,
                                                            uint16_t* __restrict__ out) {
+  __shared__ float wts[256];
+  __shared__ float red[2];
   const int bh = blockIdx.x, d = threadIdx.x;
   const float* ml = mlpart + (size_t)bh * nsplit * 2;
-  float M = LSA_NEG;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
-  float L = 0.f, O = 0.f;
-  for (int s = 0; s < nsplit; ++s) {
+  float mloc = LSA_NEG;
+  for (int s = d; s < nsplit; s += 128) mloc = fmaxf(mloc, ml[2 * s]);
+  mloc = wave_max(mloc);
+  if ((d & 63) == 0) red[d >> 6] = mloc;
+  __syncthreads();
+  const float M = fmaxf(red[0], red[1]);
+  float lloc = 0.f;
+  for (int s = d; s < nsplit; s += 128) {
     const float w = exp2f(ml[2 * s] - M);
-    L += ml[2 * s + 1] * w;
-    O += opart[((size_t)bh * nsplit + s) * 128 + d] * w;
+    wts[s] = w;
+    lloc += ml[2 * s + 1] * w;
   }
+  lloc = wave_sum(lloc);
+  __syncthreads();
+  if ((d & 63) == 0) red[d >> 6] = lloc;
+  __syncthreads();
+  const float L = red[0] + red[1];
+  const float* op = opart + (size_t)bh * nsplit * 128 + d;
+  float O = 0.f;
+#pragma unroll 8
+  for (int s = 0; s < nsplit; ++s) O = fmaf(op[(size_t)s * 128], wts[s], O);
   out[(size_t)bh * 128 + d] = f2bf(L > 0.f ? O / L : 0.f);
 }
 
@@ -185,6 +202,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
                                const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit,
                                void* out, float* opart, float* mlpart, hipStream_t s) {
   if (H % Hkv) return -1;
+  if (nsplit > 256) return -3;
   const int G = H / Hkv;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid(nsplit, Hkv, B);

@@ -27,13 +27,13 @@ __device__ __forceinline__ void fp8x16_to_bf16(const uint4 q, uint4& a, uint4& b
 #define EPI_F32 1
 #define EPI_SILU 2
 
-template <int MT, int NB, int EPI>
-__global__ __launch_bounds__(512) void gemm_fp8_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB64,
-                                                              const uint4* __restrict__ Wq,
-                                                              const float* __restrict__ wscale,
-                                                              void* __restrict__ out, int ldo, int kb_per_split) {
-  constexpr int WAVES = 8;
-  constexpr int U = 16 / NB;
+template <int MT, int NB, int EPI, int WAVES, int U>
+__global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
+                                                                     int KB64, const uint4* __restrict__ Wq,
+                                                                     const float* __restrict__ wscale,
+                                                                     void* __restrict__ out, int ldo, int kb_per_split) {
+  // same work split as gemm_skinny_kernel: chunks of U k64-steps round-robin over the waves, two-deep
+  // register pipeline pinned with sched_barrier(0)
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -41,8 +41,9 @@ __global__ __launch_bounds__(512) void gemm_fp8_skinny_kernel(const uint16_t* __
   const int kbA = blockIdx.y * kb_per_split;
   const int kbB = min(KB64, kbA + kb_per_split);
   const int nk = kbB - kbA;
-  const int kw0 = kbA + (nk * w) / WAVES;
-  const int kw1 = kbA + (nk * (w + 1)) / WAVES;
+  const int nch = (nk + U - 1) / U;
+  const int n_it = nch > w ? (nch - w + WAVES - 1) / WAVES : 0;
+  const int last_c = w + WAVES * (n_it - 1);
 
   f32x4_t acc[NB][MT];
 #pragma unroll
@@ -61,25 +62,36 @@ __global__ __launch_bounds__(512) void gemm_fp8_skinny_kernel(const uint16_t* __
 #pragma unroll
   for (int i = 0; i < NB; ++i) wp[i] = Wq + (size_t)(nb0 + i) * KB64 * 64 + lane;
 
-  for (int kb = kw0; kb < kw1; kb += U) {
-    uint4 wr[U][NB];
+  auto load = [&](uint4 (&wr)[U][NB], uint4 (&xr)[U][MT][2], int c) {
+    const int kb = kbA + c * U;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int kk = min(kb + u, kw1 - 1);
+      const int kk = min(kb + u, kbB - 1);
 #pragma unroll
       for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int kk = min(kb + u, kw1 - 1);
-      const bool live = (kb + u) < kw1;
-      uint4 x0[MT], x1[MT];
+      const int kk = min(kb + u, kbB - 1);
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         const uint4* px = reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * 64);
-        x0[j] = px[0];
-        x1[j] = px[1];
+        xr[u][j][0] = px[0];
+        xr[u][j][1] = px[1];
+      }
+    }
+  };
+  auto comp = [&](const uint4 (&wr)[U][NB], const uint4 (&xr)[U][MT][2], int c) {
+    const int kb = kbA + c * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool live = (kb + u) < kbB;
+      uint4 x0[MT], x1[MT];
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
         const bool ok = live && xvalid[j];
+        x0[j] = xr[u][j][0];
+        x1[j] = xr[u][j][1];
         x0[j].x = ok ? x0[j].x : 0u; x0[j].y = ok ? x0[j].y : 0u; x0[j].z = ok ? x0[j].z : 0u; x0[j].w = ok ? x0[j].w : 0u;
         x1[j].x = ok ? x1[j].x : 0u; x1[j].y = ok ? x1[j].y : 0u; x1[j].z = ok ? x1[j].z : 0u; x1[j].w = ok ? x1[j].w : 0u;
       }
@@ -94,6 +106,22 @@ __global__ __launch_bounds__(512) void gemm_fp8_skinny_kernel(const uint16_t* __
         }
       }
     }
+  };
+  if (n_it > 0) {
+    uint4 wA[U][NB], xA[U][MT][2], wB[U][NB], xB[U][MT][2];
+    load(wA, xA, w);
+    int i = 0;
+    for (; i + 1 < n_it; i += 2) {
+      load(wB, xB, w + WAVES * (i + 1));
+      __builtin_amdgcn_sched_barrier(0);
+      comp(wA, xA, w + WAVES * i);
+      __builtin_amdgcn_sched_barrier(0);
+      load(wA, xA, min(w + WAVES * (i + 2), last_c));
+      __builtin_amdgcn_sched_barrier(0);
+      comp(wB, xB, w + WAVES * (i + 1));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (i < n_it) comp(wA, xA, w + WAVES * i);
   }
 
   __shared__ __attribute__((aligned(16))) f32x4_t red[WAVES][NB * MT][64];
@@ -184,9 +212,12 @@ __global__ __launch_bounds__(256) void fp8_dequant_kernel(const uint4* __restric
 template <int MT, int NB, int EPI>
 static void launch_t(const uint16_t* X, int ldx, int M, int KB64, const uint4* Wq, const float* sc, int NBtot, void* out,
                      int ldo, int splitk, hipStream_t s) {
+  // 4 waves, 4 fragments (NB * U) per chunk: the shallow-chunk / high-occupancy point that won the
+  // bf16 sweeps (each fp8 fragment feeds twice the MFMA work of a bf16 one)
+  constexpr int U = (4 / NB) < 1 ? 1 : (4 / NB);
   const int kbps = (KB64 + splitk - 1) / splitk;
-  hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI>), dim3(NBtot / NB, splitk), dim3(512), 0, s, X, ldx, M, KB64, Wq,
-                     sc, out, ldo, kbps);
+  hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, 4, U>), dim3(NBtot / NB, splitk), dim3(256), 0, s, X, ldx, M,
+                     KB64, Wq, sc, out, ldo, kbps);
 }
 
 template <int EPI>

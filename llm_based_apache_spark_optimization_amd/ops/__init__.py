@@ -269,11 +269,14 @@ def silu_mul(g: torch.Tensor, u: torch.Tensor, out: Optional[torch.Tensor] = Non
 
 # ----------------------------------------------------------------------------------- attention
 def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int]:
-    """(chunk_blocks, nsplit) for split-KV decode: aim for >= 512 workgroups."""
+    """(chunk_blocks, nsplit) for split-KV decode: aim for >= 512 workgroups, but keep >= 2 blocks per
+    split (the kernel double-buffers K/V across blocks) and <= 256 splits (the combine's LDS)."""
     nblk = max(1, (max_ctx + 63) // 64)
     chunk = nblk
-    while chunk > 1 and B * Hkv * ((nblk + chunk - 1) // chunk) < 512:
+    while chunk > 2 and B * Hkv * ((nblk + chunk - 1) // chunk) < 512:
         chunk = (chunk + 1) // 2
+    while (nblk + chunk - 1) // chunk > 256:
+        chunk += 1
     return chunk, (nblk + chunk - 1) // chunk
 
 

@@ -7,4 +7,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 600 python bench.py "$@" > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
 bash scripts/profile_bench.sh b32 --steps 2 --warmup 1 > /dev/null 2>&1
-python scripts/prof_summary.py gpurun_out/prof_b32/run_kernel_stats.csv | head -20
+python scripts/prof_summary.py gpurun_out/prof_b32/run_kernel_stats.csv > gpurun_out/prof_b32/summary.txt; head -20 gpurun_out/prof_b32/summary.txt
