@@ -10,14 +10,14 @@ int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* 
              hipStream_t stream);
 int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
                     const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
-                    hipStream_t s);
+                    int xf_mt, hipStream_t s);
 int lsa_rope_append(const void* qkv, const float* qkv_parts, int nparts, long part_stride, const int* pos, const int* tok_seq, const int* block_tables, int max_blocks,
                     const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int T, int H, int Hkv,
                     hipStream_t s);
 int lsa_silu_mul(const void* g, const void* u, void* o, long n, hipStream_t s);
 int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                     const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit, void* out,
-                    float* opart, float* mlpart, hipStream_t s);
+                    float* opart, float* mlpart, int xf_mt, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                      const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
                      void* out, hipStream_t s);
@@ -73,6 +73,27 @@ void gemm(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out,
         "gemm");
 }
 
+// same, with X in the fragment-major activation layout (ops.to_xfrag): xf holds ceil(M/16) row tiles
+void gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wf, int64_t N, at::Tensor& out,
+             int64_t epi, int64_t nb, int64_t splitk, int64_t waves, int64_t div) {
+  need(xf, at::kBFloat16, "xf");
+  need(wf, at::kBFloat16, "wf");
+  TORCH_CHECK(M >= 1 && M <= 64 && K % 32 == 0, "gemm_xf: M in 1..64, K % 32 == 0");
+  const int64_t mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  TORCH_CHECK(xf.is_contiguous() && xf.numel() >= mt * 16 * K, "xf too small for M=", M, " K=", K);
+  TORCH_CHECK(wf.numel() == N * K, "weight numel mismatch");
+  if (epi == 1) {
+    need(out, at::kFloat, "out");
+    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small");
+  } else {
+    need(out, at::kBFloat16, "out");
+    TORCH_CHECK(out.numel() >= (epi == 2 ? mt * 16 * (N / 2) : M * N), "bf16 out too small");
+  }
+  check(lsa_gemm_cfg(xf.data_ptr(), K, M, K, wf.data_ptr(), N, out.data_ptr(), epi, nb, splitk, waves, div, 2,
+                     cur_stream()),
+        "gemm_xf");
+}
+
 void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscale, int64_t N, at::Tensor& out,
               int64_t epi, int64_t nb, int64_t splitk) {
   need(x, at::kBFloat16, "x");
@@ -89,14 +110,14 @@ void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscal
 void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t nparts, int64_t part_stride,
                  const c10::optional<at::Tensor>& ids, const c10::optional<at::Tensor>& emb,
                  const c10::optional<at::Tensor>& row_idx, bool write_h, const at::Tensor& w, double eps,
-                 at::Tensor& xn, int64_t rows) {
+                 at::Tensor& xn, int64_t rows, int64_t xf_mt) {
   need(h, at::kFloat, "h");
   need(w, at::kBFloat16, "w");
   need(xn, at::kBFloat16, "xn");
   const int D = w.numel();
   check(lsa_add_rmsnorm(h.data_ptr<float>(), ptr<const float>(parts), parts.has_value() ? nparts : 0, part_stride,
                         ptr<const int>(ids), ptr<const void>(emb), ptr<const int>(row_idx), write_h ? 1 : 0,
-                        w.data_ptr(), (float)eps, xn.data_ptr(), rows, D, cur_stream()),
+                        w.data_ptr(), (float)eps, xn.data_ptr(), rows, D, xf_mt, cur_stream()),
         "add_rmsnorm");
 }
 
@@ -123,13 +144,13 @@ void silu_mul(const at::Tensor& g, const at::Tensor& u, at::Tensor& o) {
 
 void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                  const at::Tensor& pos, int64_t H, int64_t Hkv, double scale, int64_t chunk_blocks, int64_t nsplit,
-                 at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart) {
+                 at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, int64_t xf_mt) {
   need(q, at::kBFloat16, "q");
   need(pos, at::kInt, "pos");
   const int B = pos.size(0);
   check(lsa_attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                         block_tables.size(1), pos.data_ptr<int>(), B, H, Hkv, (float)scale, chunk_blocks, nsplit,
-                        out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), cur_stream()),
+                        out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), xf_mt, cur_stream()),
         "attn_decode");
 }
 
@@ -187,11 +208,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the MI355X NL->SQL / Spark-error inference engine";
   m.def("gemm", &gemm, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"),
         py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4, py::arg("xlds") = 0);
+  m.def("gemm_xf", &gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wf"), py::arg("N"), py::arg("out"),
+        py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4);
   m.def("fp8_gemm", &fp8_gemm);
-  m.def("add_rmsnorm", &add_rmsnorm);
+  m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
+        py::arg("ids"), py::arg("emb"), py::arg("row_idx"), py::arg("write_h"), py::arg("w"), py::arg("eps"),
+        py::arg("xn"), py::arg("rows"), py::arg("xf_mt") = 0);
   m.def("rope_append", &rope_append);
   m.def("silu_mul", &silu_mul);
-  m.def("attn_decode", &attn_decode);
+  m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
+        py::arg("pos"), py::arg("H"), py::arg("Hkv"), py::arg("scale"), py::arg("chunk_blocks"), py::arg("nsplit"),
+        py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("xf_mt") = 0);
   m.def("attn_prefill", &attn_prefill);
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);

@@ -27,7 +27,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
                                                           const int* __restrict__ block_tables, int max_blocks,
                                                           const int* __restrict__ pos, int Hkv, float scale_log2,
                                                           int chunk_blocks, int nsplit, uint16_t* __restrict__ out,
-                                                          float* __restrict__ opart, float* __restrict__ mlpart) {
+                                                          float* __restrict__ opart, float* __restrict__ mlpart,
+                                                          int xf_mt) {
   constexpr int D = 128;
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int H = Hkv * G;
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
     }
     const int h = hk * G + g;
     if (nsplit == 1) {
-      out[((size_t)b * H + h) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+      out[xf_mt ? xf_off(b, h * D + d, xf_mt) : ((size_t)b * H + h) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
     } else {
       const size_t pi = ((size_t)b * H + h) * nsplit + split;
       opart[pi * D + d] = O;
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
 // then every thread sums its output dim over the splits with independent (pipelined) loads
 __global__ __launch_bounds__(128) void attn_combine_kernel(const float* __restrict__ opart,
                                                            const float* __restrict__ mlpart, int nsplit,
-                                                           uint16_t* __restrict__ out) {
+                                                           uint16_t* __restrict__ out, int H, int xf_mt) {
   __shared__ float wts[256];
   __shared__ float red[2];
   const int bh = blockIdx.x, d = threadIdx.x;
@@ -195,13 +196,15 @@ __global__ __launch_bounds__(128) void attn_combine_kernel(const float* __restri
   float O = 0.f;
 #pragma unroll 8
   for (int s = 0; s < nsplit; ++s) O = fmaf(op[(size_t)s * 128], wts[s], O);
-  out[(size_t)bh * 128 + d] = f2bf(L > 0.f ? O / L : 0.f);
+  const size_t oi = xf_mt ? xf_off(bh / H, (bh % H) * 128 + d, xf_mt) : (size_t)bh * 128 + d;
+  out[oi] = f2bf(L > 0.f ? O / L : 0.f);
 }
 
 extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit,
-                               void* out, float* opart, float* mlpart, hipStream_t s) {
+                               void* out, float* opart, float* mlpart, int xf_mt, hipStream_t s) {
   if (H % Hkv) return -1;
+  if (xf_mt && B > 16 * xf_mt) return -4;
   if (nsplit > 256) return -3;
   const int G = H / Hkv;
   const float sl2 = scale * 1.4426950408889634f;
@@ -213,14 +216,15 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
 #define LSA_AD(GV)                                                                                                 \
   case GV:                                                                                                         \
     hipLaunchKernelGGL(attn_decode_kernel<GV>, grid, dim3(256), 0, s, qq, kk, vv, block_tables, max_blocks, pos, Hkv, \
-                       sl2, chunk_blocks, nsplit, oo, opart, mlpart);                                             \
+                       sl2, chunk_blocks, nsplit, oo, opart, mlpart, xf_mt);                                      \
     break;
   switch (G) {
     LSA_AD(1) LSA_AD(2) LSA_AD(3) LSA_AD(4) LSA_AD(8)
     default: return -2;
   }
 #undef LSA_AD
-  if (nsplit > 1) hipLaunchKernelGGL(attn_combine_kernel, dim3(B * H), dim3(128), 0, s, opart, mlpart, nsplit, oo);
+  if (nsplit > 1) hipLaunchKernelGGL(attn_combine_kernel, dim3(B * H), dim3(128), 0, s, opart, mlpart, nsplit, oo, H,
+                                     xf_mt);
   return (int)hipGetLastError();
 }
 

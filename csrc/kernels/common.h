@@ -77,6 +77,13 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// Element offset of activation (m, k) in the fragment-major decode layout Xf[k/32][mt][64 lanes][8]
+// (lane = 16 * ((k % 32) / 8) + m % 16): one MFMA B-fragment per (k-step, 16-row tile) is 1 KiB
+// lane-linear.  8 consecutive k starting at a multiple of 8 are contiguous.
+__device__ __forceinline__ size_t xf_off(int m, int k, int mt) {
+  return ((((size_t)(k >> 5) * mt + (m >> 4)) * 64) + 16 * ((k & 31) >> 3) + (m & 15)) * 8 + (k & 7);
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 
 // Orderable 32-bit key of a float (larger float -> larger unsigned key).

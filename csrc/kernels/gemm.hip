@@ -54,7 +54,10 @@ struct SkinnyCfg {
   static constexpr int U = (U0 / DIV) < 1 ? 1 : (U0 / DIV);
 };
 
-template <int MT, int NB, int EPI, int WAVES, int DIV = 1>
+// XF: X is in the fragment-major activation layout Xf[k/32][MT][64 lanes][8 bf16] (ops.to_xfrag,
+// written directly by the producing kernels in the decode path), so an activation fragment is one
+// lane-linear 1 KiB load (8 full lines) instead of 16 half-used row segments.
+template <int MT, int NB, int EPI, int WAVES, int DIV = 1, bool XF = false>
 __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
                                                                  int KB, const uint4* __restrict__ Wf,
                                                                  void* __restrict__ out, int ldo,
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
   for (int j = 0; j < MT; ++j) {
     const int m = j * 16 + r;
     xvalid[j] = m < M;
-    xp[j] = X + (size_t)(xvalid[j] ? m : 0) * ldx + 8 * g;
+    xp[j] = XF ? X + ((size_t)j * 64 + lane) * 8 : X + (size_t)(xvalid[j] ? m : 0) * ldx + 8 * g;
   }
   const uint4* wp[NB];
 #pragma unroll
@@ -101,7 +104,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
     for (int u = 0; u < U; ++u) {
       const int kk = min(kb + u, kbB - 1);
 #pragma unroll
-      for (int j = 0; j < MT; ++j) xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * 32);
+      for (int j = 0; j < MT; ++j)
+        xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * (XF ? MT * 512 : 32));
     }
   };
   auto comp = [&](const uint4 (&wr)[U][NB], const uint4 (&xr)[U][MT], int c) {
@@ -164,7 +168,14 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
         f32x4_t v;
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = silu(gs[q]) * us[q];
-        store4<EPI_SILU>(out, ldo, 0, m, n, v);
+        if constexpr (XF) {  // fragment-major in -> fragment-major out (the down projection's input)
+          uint2 pk;
+          pk.x = pack2bf(v[0], v[1]);
+          pk.y = pack2bf(v[2], v[3]);
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + xf_off(m, n, MT)) = pk;
+        } else {
+          store4<EPI_SILU>(out, ldo, 0, m, n, v);
+        }
       }
     }
   } else {
@@ -412,32 +423,34 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restri
 static thread_local int g_skinny_waves = 4;
 static thread_local int g_skinny_div = 4;
 
-template <int MT, int NB, int EPI>
-static void launch_skinny_t(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
+template <int MT, int NB, int EPI, bool XF>
+static void launch_skinny_x(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
                             int ldo, int splitk, hipStream_t s) {
   const int kbps = (KB + splitk - 1) / splitk;
   dim3 grid(NBtot / NB, splitk);
+#define LSA_SKL(WV, DV) \
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF>), grid, dim3(64 * WV), 0, s, X, ldx, M, KB, Wf, out, \
+                     ldo, kbps)
   if (g_skinny_div == 2) {
-    if (g_skinny_waves == 8)
-      hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 8, 2>), grid, dim3(512), 0, s, X, ldx, M, KB, Wf, out, ldo,
-                         kbps);
-    else
-      hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 4, 2>), grid, dim3(256), 0, s, X, ldx, M, KB, Wf, out, ldo,
-                         kbps);
-    return;
+    if (g_skinny_waves == 8) LSA_SKL(8, 2);
+    else LSA_SKL(4, 2);
+  } else if (g_skinny_div == 4) {
+    LSA_SKL(4, 4);
+  } else {
+    if (g_skinny_waves == 8) LSA_SKL(8, 1);
+    else LSA_SKL(4, 1);
   }
-  if (g_skinny_div == 4) {
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 4, 4>), grid, dim3(256), 0, s, X, ldx, M, KB, Wf, out, ldo,
-                       kbps);
-    return;
-  }
-  if (g_skinny_waves == 8)
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 8>), grid, dim3(512), 0, s, X, ldx, M, KB, Wf, out, ldo, kbps);
-  else
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, 4>), grid, dim3(256), 0, s, X, ldx, M, KB, Wf, out, ldo, kbps);
+#undef LSA_SKL
 }
 
+static thread_local int g_xfrag = 0;
 
+template <int MT, int NB, int EPI>
+static void launch_skinny_t(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
+                            int ldo, int splitk, hipStream_t s) {
+  if (g_xfrag) launch_skinny_x<MT, NB, EPI, true>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);
+  else launch_skinny_x<MT, NB, EPI, false>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);
+}
 
 // LDS-staged activation kernel for 16 < M <= 64 (f32 epilogue): measured slower than the register
 // pipeline with div 4 on every decode shape (its x prologue delays the weight stream), so it is off
@@ -456,8 +469,10 @@ static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uin
   LSA_SK(1, 2) LSA_SK(1, 4) LSA_SK(2, 2) LSA_SK(2, 4) LSA_SK(4, 2)
   if constexpr (EPI != EPI_SILU) { LSA_SK(1, 1) LSA_SK(2, 1) LSA_SK(4, 1) }
 #undef LSA_SK
-  // fallback (nb=4 with mt=4 or unsupported): use nb=2
-  launch_skinny_t<4, 2, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);
+  // fallback (nb=4 with mt=4 or unsupported): nb=2 at the same row-tile count
+  if (mt == 1) launch_skinny_t<1, 2, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);
+  else if (mt == 2) launch_skinny_t<2, 2, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);
+  else launch_skinny_t<4, 2, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);
 }
 
 extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
@@ -472,8 +487,11 @@ extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf
                             int splitk, int waves, int div, int xlds, hipStream_t stream) {
   g_skinny_waves = (waves == 8) ? 8 : 4;
   g_skinny_div = (div == 1 || div == 2) ? div : 4;
-  g_xlds = xlds ? 1 : 0;
+  // xlds: 0 = row-major X, 1 = row-major X staged through LDS, 2 = fragment-major X (ops.to_xfrag)
+  g_xlds = xlds == 1 ? 1 : 0;
+  g_xfrag = xlds == 2 ? 1 : 0;
   if (K % 32 != 0 || N % 16 != 0 || M <= 0) return -1;
+  if (g_xfrag && M > 64) return -5;
   const int KB = K / 32, NBtot = N / 16;
   const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
   const uint4* w = reinterpret_cast<const uint4*>(Wf);

@@ -9,39 +9,55 @@
 //   lsa_silu_mul      standalone silu(g) * u for non-interleaved inputs.
 #include "common.h"
 
-// one workgroup per output row; D % 8 == 0; D <= 256 * 8 * 8
-template <int VPT>  // 8-element vectors per thread
-__global__ __launch_bounds__(256) void add_rmsnorm_kernel(float* __restrict__ h, const float* __restrict__ parts,
-                                                          int nparts, size_t part_stride, const int* __restrict__ ids,
-                                                          const uint16_t* __restrict__ emb,
-                                                          const int* __restrict__ row_idx, int write_h,
-                                                          const uint16_t* __restrict__ w, float eps,
-                                                          uint16_t* __restrict__ xn, int D) {
+// One workgroup per output row, one 8-wide vector per thread and pass (blockDim = D/8 rounded up to a
+// wave when D <= 8192).  NP = number of split-K slabs known at compile time, so every slab load of a
+// thread is issued before the first add (the kernel is pure latency at decode sizes); NP < 0 = runtime.
+template <int NP, int VPT>
+__global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h, const float* __restrict__ parts,
+                                                           int nparts, size_t part_stride, const int* __restrict__ ids,
+                                                           const uint16_t* __restrict__ emb,
+                                                           const int* __restrict__ row_idx, int write_h,
+                                                           const uint16_t* __restrict__ w, float eps,
+                                                           uint16_t* __restrict__ xn, int D, int xf_mt) {
   __shared__ float red[16];
   const int m = blockIdx.x;
   const int r = row_idx ? row_idx[m] : m;
   float* hr = h + (size_t)r * D;
+  const int nt = blockDim.x;
   float v[VPT][8];
   float ss = 0.f;
+  auto add8 = [](float* x, const float* p) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    x[0] += a.x; x[1] += a.y; x[2] += a.z; x[3] += a.w;
+    x[4] += b.x; x[5] += b.y; x[6] += b.z; x[7] += b.w;
+  };
 #pragma unroll
   for (int q = 0; q < VPT; ++q) {
-    const int c = (threadIdx.x + q * 256) * 8;
+    const int c = (threadIdx.x + q * nt) * 8;
     if (c < D) {
       if (ids) {
-        const uint4 e = *reinterpret_cast<const uint4*>(emb + (size_t)ids[r] * D + c);
-        unpack8(e, v[q]);
+        unpack8(*reinterpret_cast<const uint4*>(emb + (size_t)ids[r] * D + c), v[q]);
       } else {
-        const float4 a = *reinterpret_cast<const float4*>(hr + c);
-        const float4 b = *reinterpret_cast<const float4*>(hr + c + 4);
-        v[q][0] = a.x; v[q][1] = a.y; v[q][2] = a.z; v[q][3] = a.w;
-        v[q][4] = b.x; v[q][5] = b.y; v[q][6] = b.z; v[q][7] = b.w;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[q][j] = 0.f;
+        add8(v[q], hr + c);
       }
-      for (int s = 0; s < nparts; ++s) {
-        const float* p = parts + s * part_stride + (size_t)r * D + c;
-        const float4 a = *reinterpret_cast<const float4*>(p);
-        const float4 b = *reinterpret_cast<const float4*>(p + 4);
-        v[q][0] += a.x; v[q][1] += a.y; v[q][2] += a.z; v[q][3] += a.w;
-        v[q][4] += b.x; v[q][5] += b.y; v[q][6] += b.z; v[q][7] += b.w;
+      const float* p = parts + (size_t)r * D + c;
+      if constexpr (NP >= 0) {
+        float t[NP > 0 ? NP : 1][8];
+#pragma unroll
+        for (int s = 0; s < NP; ++s) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) t[s][j] = 0.f;
+          add8(t[s], p + s * part_stride);
+        }
+#pragma unroll
+        for (int s = 0; s < NP; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[q][j] += t[s][j];
+      } else {
+        for (int s = 0; s < nparts; ++s) add8(v[q], p + s * part_stride);
       }
       if (write_h) {
         *reinterpret_cast<float4*>(hr + c) = make_float4(v[q][0], v[q][1], v[q][2], v[q][3]);
@@ -55,34 +71,54 @@ __global__ __launch_bounds__(256) void add_rmsnorm_kernel(float* __restrict__ h,
   const float inv = rsqrtf(tot / (float)D + eps);
 #pragma unroll
   for (int q = 0; q < VPT; ++q) {
-    const int c = (threadIdx.x + q * 256) * 8;
+    const int c = (threadIdx.x + q * nt) * 8;
     if (c < D) {
       float wf[8], o[8];
       unpack8(*reinterpret_cast<const uint4*>(w + c), wf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[q][j] * inv * wf[j];
-      *reinterpret_cast<uint4*>(xn + (size_t)m * D + c) = pack8(o);
+      *reinterpret_cast<uint4*>(xn + (xf_mt ? xf_off(m, c, xf_mt) : (size_t)m * D + c)) = pack8(o);
     }
   }
 }
 
+template <int VPT>
+static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, const float* parts, size_t ps,
+                           const int* ids, const uint16_t* e, const int* row_idx, int write_h, const uint16_t* w,
+                           float eps, uint16_t* o, int D, int xf_mt) {
+#define LSA_RN(NP)                                                                                         \
+  hipLaunchKernelGGL((add_rmsnorm_kernel<NP, VPT>), dim3(rows), dim3(nt), 0, s, h, parts, np, ps, ids, e, \
+                     row_idx, write_h, w, eps, o, D, xf_mt)
+  switch (parts ? np : 0) {
+    case 0: LSA_RN(0); break;
+    case 1: LSA_RN(1); break;
+    case 2: LSA_RN(2); break;
+    case 3: LSA_RN(3); break;
+    case 4: LSA_RN(4); break;
+    case 6: LSA_RN(6); break;
+    case 8: LSA_RN(8); break;
+    default: LSA_RN(-1); break;
+  }
+#undef LSA_RN
+}
+
 extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids,
                                const void* emb, const int* row_idx, int write_h, const void* w, float eps, void* xn,
-                               int rows, int D, hipStream_t s) {
+                               int rows, int D, int xf_mt, hipStream_t s) {
   if (D % 8 != 0 || rows <= 0) return -1;
-  const int vpt = (D / 8 + 255) / 256;
+  if (xf_mt && (D % 32 != 0 || rows > 16 * xf_mt)) return -3;
+  const int vec = D / 8;
   const uint16_t* e = reinterpret_cast<const uint16_t*>(emb);
   const uint16_t* ww = reinterpret_cast<const uint16_t*>(w);
   uint16_t* o = reinterpret_cast<uint16_t*>(xn);
-#define LSA_RN(V)                                                                                            \
-  hipLaunchKernelGGL(add_rmsnorm_kernel<V>, dim3(rows), dim3(256), 0, s, h, parts, nparts, (size_t)part_stride, \
-                     ids, e, row_idx, write_h, ww, eps, o, D)
-  if (vpt <= 1) LSA_RN(1);
-  else if (vpt <= 2) LSA_RN(2);
-  else if (vpt <= 4) LSA_RN(4);
-  else if (vpt <= 8) LSA_RN(8);
-  else return -2;
-#undef LSA_RN
+  if (vec <= 1024) {
+    launch_rmsnorm<1>(nparts, rows, (vec + 63) / 64 * 64, s, h, parts, (size_t)part_stride, ids, e, row_idx, write_h,
+                      ww, eps, o, D, xf_mt);
+  } else if (vec <= 4096) {
+    launch_rmsnorm<4>(nparts, rows, 1024, s, h, parts, (size_t)part_stride, ids, e, row_idx, write_h, ww, eps, o, D, xf_mt);
+  } else {
+    return -2;
+  }
   return (int)hipGetLastError();
 }
 
@@ -92,8 +128,8 @@ extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long pa
 // block_tables[seq * max_blocks + pos / 64], slot pos % 64.  cos/sin: [max_pos, 64] f32.
 // One workgroup per token; each thread rotates 4 (d, d+64) pairs (8 B loads of both halves).
 // ------------------------------------------------------------------------------------------------
-template <bool PARTS>
-__global__ __launch_bounds__(256) void rope_append_kernel(const uint16_t* __restrict__ qkv, const float* __restrict__ qkv_parts,
+template <int NP>  // NP = 0: bf16 qkv rows; NP > 0: that many f32 split-K slabs; NP < 0: runtime count
+__global__ __launch_bounds__(1024) void rope_append_kernel(const uint16_t* __restrict__ qkv, const float* __restrict__ qkv_parts,
                                                           int nparts, size_t part_stride, const int* __restrict__ pos,
                                                           const int* __restrict__ tok_seq,
                                                           const int* __restrict__ block_tables, int max_blocks,
@@ -112,7 +148,15 @@ __global__ __launch_bounds__(256) void rope_append_kernel(const uint16_t* __rest
   const float* prow = qkv_parts + row_off;
   // 4 consecutive values of the fused q|k|v row: bf16 row or the sum of f32 split-K slabs
   auto load4 = [&](int off, float* v) {
-    if constexpr (PARTS) {
+    if constexpr (NP > 0) {
+      float4 b[NP];
+#pragma unroll
+      for (int s = 0; s < NP; ++s) b[s] = *reinterpret_cast<const float4*>(prow + s * part_stride + off);
+      float4 a = b[0];
+#pragma unroll
+      for (int s = 1; s < NP; ++s) { a.x += b[s].x; a.y += b[s].y; a.z += b[s].z; a.w += b[s].w; }
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    } else if constexpr (NP < 0) {
       float4 a = *reinterpret_cast<const float4*>(prow + off);
       for (int s = 1; s < nparts; ++s) {
         const float4 b = *reinterpret_cast<const float4*>(prow + s * part_stride + off);
@@ -158,7 +202,7 @@ __global__ __launch_bounds__(256) void rope_append_kernel(const uint16_t* __rest
   for (int it = threadIdx.x; it < Hkv * 16; it += blockDim.x) {
     const int hv = it >> 4, c = (it & 15) * 8;
     uint4 v;
-    if constexpr (PARTS) {
+    if constexpr (NP != 0) {
       float f[8];
       load4((H + Hkv + hv) * D + c, f);
       load4((H + Hkv + hv) * D + c + 4, f + 4);
@@ -174,16 +218,26 @@ extern "C" int lsa_rope_append(const void* qkv, const float* qkv_parts, int npar
                                int max_blocks, const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc,
                                int T, int H, int Hkv, hipStream_t s) {
   if (T <= 0) return 0;
-  if (qkv_parts)
-    hipLaunchKernelGGL(rope_append_kernel<true>, dim3(T), dim3(256), 0, s, nullptr, qkv_parts, nparts,
-                       (size_t)part_stride, pos, tok_seq, block_tables, max_blocks, cos_t, sin_t,
-                       reinterpret_cast<uint16_t*>(q_out), reinterpret_cast<uint16_t*>(kc),
-                       reinterpret_cast<uint16_t*>(vc), H, Hkv);
-  else
-    hipLaunchKernelGGL(rope_append_kernel<false>, dim3(T), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(qkv),
-                       nullptr, 0, (size_t)0, pos, tok_seq, block_tables, max_blocks, cos_t, sin_t,
-                       reinterpret_cast<uint16_t*>(q_out), reinterpret_cast<uint16_t*>(kc),
-                       reinterpret_cast<uint16_t*>(vc), H, Hkv);
+  // one rotation item per thread where possible (the decode case is latency-bound)
+  const int items = (H + Hkv) * 16;
+  const int nt = items >= 1024 ? 1024 : (items + 63) / 64 * 64;
+  const uint16_t* q16 = reinterpret_cast<const uint16_t*>(qkv);
+  uint16_t* qo = reinterpret_cast<uint16_t*>(q_out);
+  uint16_t* k16 = reinterpret_cast<uint16_t*>(kc);
+  uint16_t* v16 = reinterpret_cast<uint16_t*>(vc);
+#define LSA_RA(NP)                                                                                              \
+  hipLaunchKernelGGL(rope_append_kernel<NP>, dim3(T), dim3(nt), 0, s, q16, qkv_parts, nparts, (size_t)part_stride, \
+                     pos, tok_seq, block_tables, max_blocks, cos_t, sin_t, qo, k16, v16, H, Hkv)
+  switch (qkv_parts ? nparts : 0) {
+    case 0: LSA_RA(0); break;
+    case 1: LSA_RA(1); break;
+    case 2: LSA_RA(2); break;
+    case 3: LSA_RA(3); break;
+    case 4: LSA_RA(4); break;
+    case 8: LSA_RA(8); break;
+    default: LSA_RA(-1); break;
+  }
+#undef LSA_RA
   return (int)hipGetLastError();
 }
 

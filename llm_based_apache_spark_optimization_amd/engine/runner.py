@@ -104,6 +104,12 @@ class ModelRunner:
         self.q = torch.zeros(S, self.H, self.D, **bf)
         self.attn = torch.zeros(S, self.H * self.D, **bf)
         self.act = torch.zeros(S, self.ffn_l, **bf)
+        # fragment-major decode activations (ops.to_xfrag) for 16 < B <= 64 bf16 buckets: the norm,
+        # attention and gate_up kernels write the next GEMM's MFMA B-fragments directly
+        xr = 16 * ops.xfrag_tiles(min(S, 64))
+        self.xn_f = torch.zeros(xr * self.d, **bf)
+        self.attn_f = torch.zeros(xr * self.H * self.D, **bf)
+        self.act_f = torch.zeros(xr * self.ffn_l, **bf)
         self.o_buf = torch.zeros(8 * S * self.d, **f32)
         self.down_buf = torch.zeros(8 * S * self.d, **f32)
         self.qkv_buf = torch.zeros(8 * S * (self.H + 2 * self.Hkv) * self.D, **f32)
@@ -122,16 +128,24 @@ class ModelRunner:
         if self.tp is not None and self.tp.size > 1:
             self.tp.all_reduce(t)
 
-    def _splitk(self, M: int, K: int, N: Optional[int] = None, tp_reduced: bool = True) -> int:
+    def _splitk(self, M: int, K: int, N: Optional[int] = None, tp_reduced: bool = True, xf: bool = False) -> int:
         if not self.on_gpu or M > 64 or (tp_reduced and self.tp is not None and self.tp.size > 1):
             return 1
-        return ops.pick_gemm_config(M, N or self.d, K, "f32")[1]
+        return ops.pick_gemm_config(M, N or self.d, K, "f32", xf=xf)[1]
 
-    def _lm_head(self, xn: torch.Tensor, M: int) -> torch.Tensor:
-        """logits [M, V] (f32) for the normalised rows xn [M, d]."""
+    def use_xfrag(self, B: int) -> bool:
+        """Fragment-major activations pay off once a decode batch spans >1 row tile (B > 16):
+        measured 8-20 % faster GEMMs at B = 32 (scripts/bench_xf.py); bf16 weights only."""
+        return self.on_gpu and 16 < B <= 64 and self.w.layers[0].wqkv.kind == "bf16"
+
+    def _lm_head(self, xn: torch.Tensor, M: int, xf: bool = False) -> torch.Tensor:
+        """logits [M, V] (f32) for the normalised rows xn [M, d] (fragment-major when xf)."""
         loc = self.logits_l[:M] if M <= self.max_slots else torch.empty(M, self.Vl, dtype=torch.float32,
                                                                          device=self.device)
-        ops.linear(xn, self.w.lm_head, "f32", out=loc, splitk=1)
+        if xf:
+            ops.linear_xf(xn, M, self.w.lm_head, "f32", out=loc, splitk=1)
+        else:
+            ops.linear(xn, self.w.lm_head, "f32", out=loc, splitk=1)
         if self.tp is None or self.tp.size == 1:
             return loc
         tps = self.tp.size
@@ -147,36 +161,44 @@ class ModelRunner:
     def _decode_step(self, B: int, sample: bool) -> None:
         w, d = self.w, self.d
         ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
-        h, xn = self.h[:B], self.xn[:B]
-        sk_o = self._splitk(B, self.H * self.D)
-        sk_d = self._splitk(B, self.ffn_l)
+        h = self.h[:B]
+        xf = self.use_xfrag(B)
+        sk_o = self._splitk(B, self.H * self.D, xf=xf)
+        sk_d = self._splitk(B, self.ffn_l, xf=xf)
         nqkv = (self.H + 2 * self.Hkv) * self.D
-        sk_q = self._splitk(B, d, nqkv, tp_reduced=False)
+        sk_q = self._splitk(B, d, nqkv, tp_reduced=False, xf=xf)
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
         plan = ops.decode_split_plan(B, self.Hkv, self.max_model_len)
         ws = (self.opart, self.mlpart)
+        if xf:  # every GEMM input lives in the fragment-major layout, written by its producer
+            xn, attn, act = self.xn_f, self.attn_f, self.act_f
+
+            def lin(x, wt, epi, **kw):
+                return ops.linear_xf(x, B, wt, epi, **kw)
+        else:
+            xn, attn, act = self.xn[:B], self.attn[:B], self.act[:B]
+            lin = ops.linear
         for l, lw in enumerate(w.layers):
             if l == 0:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf)
             else:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts)
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
             # QKV as f32 split-K slabs; rope_append sums them while rotating (no extra reduction pass)
-            ops.linear(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
+            lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
             kc, vc = self.kv[l, 0], self.kv[l, 1]
             ops.rope_append(qkv_parts, pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv)
-            ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale, self.attn[:B].view(B, self.H,
-                                                                                                          self.D),
-                            workspace=ws, plan=plan)
-            ops.linear(self.attn[:B], lw.wo, "f32", out=o_parts, splitk=sk_o)
+            ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale,
+                            attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf)
+            lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
             self._allreduce(o_parts)
-            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
-            ops.linear(xn, lw.w_gate_up, "silu", out=self.act[:B])
-            ops.linear(self.act[:B], lw.w_down, "f32", out=d_parts, splitk=sk_d)
+            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts, rows=B, xf=xf)
+            lin(xn, lw.w_gate_up, "silu", out=act)
+            lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
             self._allreduce(d_parts)
-        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_parts)
-        logits = self._lm_head(xn, B)
+        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
+        logits = self._lm_head(xn, B, xf)
         st = (self.out_tokens[:B], self.gen_len[:B], self.input_ids[:B], self.positions[:B], self.finished[:B])
         if sample:
             ops.sample_commit(logits, None, None, self.temperature[:B], self.top_k[:B], self.top_p[:B],

@@ -163,12 +163,15 @@ def _tuning_table() -> dict:
     return _tuning
 
 
-def pick_gemm_config(M: int, N: int, K: int, epi: str) -> tuple[int, int, int, int]:
-    """(nb, splitk, waves, div) for a decode GEMM: the tuning table when it has the shape, else the
-    heuristic below (div 4, 4-wave workgroups won most measured shapes)."""
+def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False) -> tuple[int, int, int, int]:
+    """(nb, splitk, waves, div) for a decode GEMM: the tuning table when it has the shape (entries
+    measured with fragment-major activations carry a ':xf' suffix), else the heuristic below (div 4,
+    4-wave workgroups won most measured shapes)."""
     if M <= 64:
         key = f"{N}x{K}:{epi}:{'s' if M <= 16 else 'm'}"
-        e = _tuning_table().get(key)
+        tab = _tuning_table()
+        e = tab.get(key + ":xf") if xf else None
+        e = e if e is not None else tab.get(key)
         if e is not None and not (M > 32 and e["nb"] > 2):
             return e["nb"], e["splitk"], e["waves"], e["div"]
     nb, sk = pick_nb_splitk(M, N, K, epi)
@@ -225,17 +228,78 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
     return out
 
 
+def xfrag_tiles(M: int) -> int:
+    """Row tiles (16 rows each) of the fragment-major activation layout for M rows (decode: M <= 64)."""
+    return 1 if M <= 16 else (2 if M <= 32 else 4)
+
+
+def to_xfrag(x: torch.Tensor) -> torch.Tensor:
+    """[M, K] -> fragment-major activations Xf[K/32][MT][64 lanes][8] (lane = 16*((k%32)/8) + m%16,
+    rows >= M zero): one MFMA B-fragment per (k-step, row tile) is 1 KiB lane-linear."""
+    M, K = x.shape
+    mt = xfrag_tiles(M)
+    xp = torch.zeros(mt * 16, K, dtype=x.dtype, device=x.device)
+    xp[:M] = x
+    return xp.view(mt, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).contiguous().view(-1)
+
+
+def from_xfrag(xf: torch.Tensor, M: int, K: int) -> torch.Tensor:
+    mt = xfrag_tiles(M)
+    return xf[: mt * 16 * K].view(K // 32, mt, 4, 16, 8).permute(1, 3, 0, 2, 4).reshape(mt * 16, K)[:M]
+
+
+def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
+              splitk: Optional[int] = None, nb: Optional[int] = None, waves: Optional[int] = None,
+              div: Optional[int] = None) -> torch.Tensor:
+    """``linear`` with the activations in the fragment-major layout (``to_xfrag``), M <= 64, bf16 weights.
+    epi='silu' writes its [M, N/2] output in the fragment-major layout too (the next GEMM's input);
+    for that epilogue ``out`` is a flat buffer of at least xfrag_tiles(M) * 16 * N/2 elements."""
+    if not _gpu(xf) or w.kind != "bf16":
+        if epi != "silu":
+            return linear(from_xfrag(xf, M, w.K), w, epi, out, splitk, nb, waves, div)
+        y = to_xfrag(linear(from_xfrag(xf, M, w.K), w, epi, None, splitk, nb, waves, div))
+        if out is None:
+            return y
+        out.view(-1)[: y.numel()].copy_(y)
+        return out
+    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, w.K, epi, xf=True)
+    nb = nb0 if nb is None else nb
+    splitk = sk0 if splitk is None else splitk
+    waves = wv0 if waves is None else waves
+    div = dv0 if div is None else div
+    if out is None:
+        if epi == "f32":
+            out = torch.empty(splitk, M, w.N, device=xf.device, dtype=torch.float32)
+        elif epi == "silu":
+            out = torch.zeros(xfrag_tiles(M) * 16 * (w.N // 2), device=xf.device, dtype=torch.bfloat16)
+        else:
+            out = torch.empty(M, w.N, device=xf.device, dtype=torch.bfloat16)
+    ext().gemm_xf(xf, M, w.K, w.data, w.N, out, EPI[epi], nb, splitk, waves, div)
+    return out
+
+
 # ----------------------------------------------------------------------------------- norms / rope
 def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
                 parts: Optional[torch.Tensor] = None, ids: Optional[torch.Tensor] = None,
                 emb: Optional[torch.Tensor] = None, row_idx: Optional[torch.Tensor] = None,
-                write_h: bool = True) -> torch.Tensor:
-    """h[r] (= emb[ids[r]]) (+= sum parts[:, r]); xn[m] = rmsnorm(h[row_idx[m]]) * w."""
+                write_h: bool = True, rows: Optional[int] = None, xf: bool = False) -> torch.Tensor:
+    """h[r] (= emb[ids[r]]) (+= sum parts[:, r]); xn[m] = rmsnorm(h[row_idx[m]]) * w.
+    xf=True: xn is a flat buffer receiving the fragment-major layout (``to_xfrag``) of ``rows`` rows."""
+    if rows is None:
+        assert not xf, "xf output needs rows"
+        rows = xn.shape[0]
     if not _gpu(h):
-        return ref.add_rmsnorm(h, w, eps, xn, parts, ids, emb, row_idx, write_h)
+        if not xf:
+            return ref.add_rmsnorm(h, w, eps, xn, parts, ids, emb, row_idx, write_h)
+        tmp = torch.empty(rows, w.numel(), dtype=torch.bfloat16, device=h.device)
+        ref.add_rmsnorm(h, w, eps, tmp, parts, ids, emb, row_idx, write_h)
+        f = to_xfrag(tmp)
+        xn.view(-1)[: f.numel()].copy_(f)
+        return xn
     nparts = parts.shape[0] if parts is not None else 0
     stride = parts.stride(0) if parts is not None else 0
-    ext().add_rmsnorm(h, parts, nparts, stride, ids, emb, row_idx, write_h, w, eps, xn, xn.shape[0])
+    ext().add_rmsnorm(h, parts, nparts, stride, ids, emb, row_idx, write_h, w, eps, xn, rows,
+                      xfrag_tiles(rows) if xf else 0)
     return xn
 
 
@@ -280,18 +344,26 @@ def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int]:
     return chunk, (nblk + chunk - 1) // chunk
 
 
-def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None):
-    """q [B,H,128] vs paged cache, context = pos + 1.  workspace = (opart, mlpart) for split-KV."""
-    if not _gpu(q):
-        return ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out)
+def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None, xf=False):
+    """q [B,H,128] vs paged cache, context = pos + 1.  workspace = (opart, mlpart) for split-KV.
+    xf=True: out is a flat buffer receiving the fragment-major layout of the [B, H*128] output."""
     B = pos.shape[0]
+    if not _gpu(q):
+        if not xf:
+            return ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out)
+        tmp = torch.empty(B, H, q.shape[-1], dtype=torch.bfloat16, device=q.device)
+        ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, tmp)
+        f = to_xfrag(tmp.view(B, -1))
+        out.view(-1)[: f.numel()].copy_(f)
+        return out
     chunk, nsplit = plan if plan is not None else decode_split_plan(B, Hkv, block_tables.shape[1] * 64)
     if workspace is None:
         opart = torch.empty(B * H * nsplit * 128, device=q.device, dtype=torch.float32)
         mlpart = torch.empty(B * H * nsplit * 2, device=q.device, dtype=torch.float32)
     else:
         opart, mlpart = workspace
-    ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart)
+    ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart,
+                      xfrag_tiles(B) if xf else 0)
     return out
 
 

@@ -41,6 +41,25 @@ def test_hf_parity_gpu(gpu, name, graphs):
         assert (gap <= 0.05 * lg.max(1).values.abs() + 0.05).all(), (gap, r.token_ids)
 
 
+@pytest.mark.parametrize("name", ["tiny-nsql", "tiny-llama3"])
+def test_hf_parity_gpu_xfrag_batch(gpu, name):
+    """A 20-sequence decode batch (bucket 32) runs the fragment-major activation path end to end."""
+    spec, m = _hf(name, seed=3)
+    w = from_hf_state_dict(spec, m.state_dict(), gpu)
+    runner = ModelRunner(w, max_slots=32, max_model_len=256, use_graphs=True)
+    assert runner.use_xfrag(32) and not runner.use_xfrag(16)
+    eng = LLMEngine(runner)
+    prompts = [[1] + list(range(5 + 7 * i, 30 + 9 * i)) for i in range(20)]
+    res = eng.generate(prompts, SamplingParams(max_tokens=8, ignore_eos=True))
+    for p, r in zip(prompts, res):
+        seq = torch.tensor([p + r.token_ids])
+        with torch.no_grad():
+            lg = m(seq).logits[0, len(p) - 1:-1].float()
+        chosen = lg.gather(1, torch.tensor(r.token_ids).view(-1, 1)).squeeze(1)
+        gap = lg.max(1).values - chosen
+        assert (gap <= 0.05 * lg.max(1).values.abs() + 0.05).all(), (gap, r.token_ids)
+
+
 def test_prefill_logits_match_hf(gpu):
     spec, m = _hf("tiny-llama3")
     w = from_hf_state_dict(spec, m.state_dict(), gpu)

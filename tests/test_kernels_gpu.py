@@ -58,6 +58,35 @@ def test_gemm_silu(gpu, M):
     assert _rel(y, yr) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 9, 20, 32, 48, 64])
+@pytest.mark.parametrize("epi", ["bf16", "f32", "silu"])
+@pytest.mark.parametrize("nb,waves,div", [(2, 4, 4), (4, 8, 2), (1, 4, 1)])
+def test_gemm_xfrag(gpu, M, epi, nb, waves, div):
+    """Fragment-major activations (ops.to_xfrag) through every epilogue and tuning knob vs fp32."""
+    if epi == "silu" and nb == 1:
+        pytest.skip("silu needs nb >= 2")
+    N, K = 1024, 2048
+    torch.manual_seed(M * 3 + nb)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    if epi == "silu":
+        wg = (torch.randn(N // 2, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+        wu = (torch.randn(N // 2, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+        pw = ops.PackedWeight.from_dense(ops.interleave_gate_up(wg, wu))
+        yr = torch.nn.functional.silu(x.float() @ wg.float().t()) * (x.float() @ wu.float().t())
+    else:
+        w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+        pw = ops.PackedWeight.from_dense(w)
+        yr = x.float() @ w.float().t()
+    xf = ops.to_xfrag(x)
+    sk = 2 if epi == "f32" else 1
+    y = ops.linear_xf(xf, M, pw, epi, splitk=sk, nb=nb, waves=waves, div=div)
+    if epi == "f32":
+        y = y.sum(0)
+    elif epi == "silu":  # fragment-major in -> fragment-major out
+        y = ops.from_xfrag(y, M, N // 2)
+    assert _rel(y, yr) < (1e-4 if epi == "f32" else 1e-2)
+
+
 @pytest.mark.parametrize("M", [17, 32, 48, 64])
 @pytest.mark.parametrize("splitk", [1, 4, 8])
 def test_gemm_xlds_f32(gpu, M, splitk):
@@ -178,6 +207,22 @@ def test_add_rmsnorm(gpu, D):
     assert _rel(xs, ref_xs) < 1e-2
 
 
+@pytest.mark.parametrize("rows", [3, 20, 33])
+def test_add_rmsnorm_xfrag(gpu, rows):
+    """Fragment-major output of the norm (decode GEMM input) == to_xfrag of the row-major output."""
+    D = 4096
+    h = torch.randn(rows, D, device=gpu)
+    parts = torch.randn(2, rows, D, device=gpu)
+    w = torch.randn(D, device=gpu).to(torch.bfloat16)
+    xr = torch.empty(rows, D, device=gpu, dtype=torch.bfloat16)
+    h2 = h.clone()
+    ops.add_rmsnorm(h2, w, 1e-5, xr, parts=parts)
+    xf = torch.zeros(ops.xfrag_tiles(rows) * 16 * D, device=gpu, dtype=torch.bfloat16)
+    ops.add_rmsnorm(h, w, 1e-5, xf, parts=parts, rows=rows, xf=True)
+    assert torch.equal(h, h2)
+    assert torch.equal(ops.from_xfrag(xf, rows, D), xr)
+
+
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
 def test_rope_append(gpu, HH):
     H, Hkv = HH
@@ -243,6 +288,12 @@ def test_attn_decode(gpu, HH, lens):
     out3 = torch.empty_like(out)
     ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, out3, plan=(bt.shape[1], 1))
     assert _rel(out3, out2) < 1e-2
+    # fragment-major output (O-projection input), split and single-split paths
+    for plan in (None, (bt.shape[1], 1)):
+        xf = torch.zeros(ops.xfrag_tiles(B) * 16 * H * D, device=gpu, dtype=torch.bfloat16)
+        ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, xf, plan=plan, xf=True)
+        ro = out if plan is None else out3
+        assert torch.equal(ops.from_xfrag(xf, B, H * D), ro.view(B, -1))
 
 
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
