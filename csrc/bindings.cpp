@@ -17,7 +17,9 @@ int lsa_rope_append(const void* qkv, const float* qkv_parts, int nparts, long pa
 int lsa_silu_mul(const void* g, const void* u, void* o, long n, hipStream_t s);
 int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                     const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit, void* out,
-                    float* opart, float* mlpart, int xf_mt, hipStream_t s);
+                    float* opart, float* mlpart, int* counters, int xf_mt, const float* qkv_parts, int nparts,
+                    long part_stride,
+                    const float* cos_t, const float* sin_t, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                      const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
                      void* out, hipStream_t s);
@@ -34,6 +36,9 @@ int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq, const flo
 int lsa_fp8_dequant(const void* Wq, const float* wscale, int N, int K, void* Wf, hipStream_t s);
 int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
                  int waves, int div, int xlds, hipStream_t stream);
+int lsa_gemm_norm(const void* X, int ldx, int M, int K, const void* Wf, int N, float* out, int nb, int splitk,
+                  int waves, int div, int xfrag, float* h, const void* nw, float eps, void* xn, int xf_mt, int* counter,
+                  hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 }
 
@@ -94,6 +99,28 @@ void gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wf, i
         "gemm_xf");
 }
 
+// f32 split-K GEMM whose last workgroups apply h += sum(slabs); xn = rmsnorm(h) * nw (decode, M <= 64).
+// x is row-major [M, K] (xfrag = 0) or fragment-major (xfrag = 1); xn is written fragment-major when
+// xf_mt > 0.  counter: 2 int32 zeros owned by the call site (left zeroed by the kernel).
+void gemm_norm(const at::Tensor& x, int64_t M, int64_t K, const at::Tensor& wf, int64_t N, at::Tensor& out,
+               int64_t nb, int64_t splitk, int64_t waves, int64_t div, bool xfrag, at::Tensor& h, const at::Tensor& nw,
+               double eps, at::Tensor& xn, int64_t xf_mt, at::Tensor& counter) {
+  need(x, at::kBFloat16, "x");
+  need(wf, at::kBFloat16, "wf");
+  need(out, at::kFloat, "out");
+  need(h, at::kFloat, "h");
+  need(nw, at::kBFloat16, "nw");
+  need(xn, at::kBFloat16, "xn");
+  need(counter, at::kInt, "counter");
+  TORCH_CHECK(M >= 1 && M <= 64 && K % 32 == 0 && nw.numel() == N, "gemm_norm: bad shapes");
+  TORCH_CHECK(wf.numel() == N * K && out.numel() >= splitk * M * N && h.numel() >= M * N, "gemm_norm: sizes");
+  TORCH_CHECK(x.is_contiguous() && x.numel() >= M * K, "gemm_norm: x");
+  check(lsa_gemm_norm(x.data_ptr(), K, M, K, wf.data_ptr(), N, out.data_ptr<float>(), nb, splitk, waves, div,
+                      xfrag ? 1 : 0, h.data_ptr<float>(), nw.data_ptr(), (float)eps, xn.data_ptr(), xf_mt,
+                      counter.data_ptr<int>(), cur_stream()),
+        "gemm_norm");
+}
+
 void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscale, int64_t N, at::Tensor& out,
               int64_t epi, int64_t nb, int64_t splitk) {
   need(x, at::kBFloat16, "x");
@@ -144,13 +171,34 @@ void silu_mul(const at::Tensor& g, const at::Tensor& u, at::Tensor& o) {
 
 void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                  const at::Tensor& pos, int64_t H, int64_t Hkv, double scale, int64_t chunk_blocks, int64_t nsplit,
-                 at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, int64_t xf_mt) {
+                 at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, at::Tensor& counters, int64_t xf_mt,
+                 const c10::optional<at::Tensor>& qkv_parts, const c10::optional<at::Tensor>& cos_t,
+                 const c10::optional<at::Tensor>& sin_t) {
   need(q, at::kBFloat16, "q");
   need(pos, at::kInt, "pos");
   const int B = pos.size(0);
+  need(opart, at::kFloat, "opart");
+  need(mlpart, at::kFloat, "mlpart");
+  need(counters, at::kInt, "counters");
+  TORCH_CHECK(opart.numel() >= (int64_t)B * H * nsplit * 128 && mlpart.numel() >= (int64_t)B * H * nsplit * 2 &&
+                  counters.numel() >= (int64_t)B * Hkv,
+              "attn_decode workspace too small");
+  TORCH_CHECK(opart.numel() * 4 < 0x7fffffffLL, "opart must stay below 2 GiB (buffer descriptor range)");
+  if (qkv_parts.has_value()) {  // fused RoPE + KV append from the QKV projection's f32 split-K slabs
+    need(*qkv_parts, at::kFloat, "qkv_parts");
+    TORCH_CHECK(qkv_parts->dim() == 3 && qkv_parts->size(1) >= B && qkv_parts->size(2) == (H + 2 * Hkv) * 128 &&
+                    qkv_parts->stride(1) == qkv_parts->size(2) && qkv_parts->stride(2) == 1,
+                "qkv_parts must be [S, B, (H + 2 Hkv) * 128] row-major slabs");
+    TORCH_CHECK(cos_t.has_value() && sin_t.has_value(), "fused rope needs cos/sin tables");
+    need(*cos_t, at::kFloat, "cos");
+    need(*sin_t, at::kFloat, "sin");
+  }
   check(lsa_attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                         block_tables.size(1), pos.data_ptr<int>(), B, H, Hkv, (float)scale, chunk_blocks, nsplit,
-                        out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), xf_mt, cur_stream()),
+                        out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), counters.data_ptr<int>(), xf_mt,
+                        ptr<const float>(qkv_parts), qkv_parts.has_value() ? qkv_parts->size(0) : 0,
+                        qkv_parts.has_value() ? qkv_parts->stride(0) : 0, ptr<const float>(cos_t),
+                        ptr<const float>(sin_t), cur_stream()),
         "attn_decode");
 }
 
@@ -210,6 +258,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4, py::arg("xlds") = 0);
   m.def("gemm_xf", &gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wf"), py::arg("N"), py::arg("out"),
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4);
+  m.def("gemm_norm", &gemm_norm);
   m.def("fp8_gemm", &fp8_gemm);
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
         py::arg("ids"), py::arg("emb"), py::arg("row_idx"), py::arg("write_h"), py::arg("w"), py::arg("eps"),
@@ -218,7 +267,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("silu_mul", &silu_mul);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("pos"), py::arg("H"), py::arg("Hkv"), py::arg("scale"), py::arg("chunk_blocks"), py::arg("nsplit"),
-        py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("xf_mt") = 0);
+        py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("counters"), py::arg("xf_mt") = 0,
+        py::arg("qkv_parts") = py::none(),
+        py::arg("cos") = py::none(), py::arg("sin") = py::none());
   m.def("attn_prefill", &attn_prefill);
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);

@@ -9,7 +9,8 @@
 //                        straight to VGPRs (no LDS round trip: the guide's decode-attention row),
 //                        16-lane dot products + xor-shuffle reductions, online softmax in exp2 domain,
 //                        cross-lane-group merge through LDS, and either the final output (1 split) or an
-//                        (o, m, l) partial merged by attn_combine_kernel.
+//                        (o, m, l) partial merged in the same launch by the last-arriving split of the
+//                        (sequence, kv-head).  Optionally fuses RoPE + the KV-cache append of the new token.
 //   attn_prefill_kernel  causal flash attention for (chunked) prefill of packed variable-length
 //                        sequences, MFMA 16x16x32 bf16.  4 waves x 16 query rows per workgroup; K/V tiles
 //                        of 64 keys staged through LDS (register staging, issue-early / write-late);
@@ -20,41 +21,57 @@
 #include "common.h"
 
 #define LSA_NEG (-1.0e30f)
+#define LSA_SC1 16  // buffer cache-policy aux bit: sc1 (write-through store / L1-bypassing load)
 
-template <int G>
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+typedef __attribute__((address_space(1))) int g_i32;
+
+// Per-sequence split of the context (the grid is sized for the longest context a captured graph can
+// see; each sequence uses what its own length needs): <= 4 blocks run unsplit (a split costs a combine
+// pass, measured slower below ~256 keys, scripts/bench_attn.py), longer contexts use splits of
+// chunk_blocks blocks, widened when the grid has fewer splits than that needs.
+__device__ __forceinline__ void eff_split(int nblk, int chunk_blocks, int nsplit, int& ech, int& nse) {
+  ech = nblk <= 4 ? max(nblk, 1) : max(chunk_blocks, (nblk + nsplit - 1) / nsplit);
+  nse = (nblk + ech - 1) / ech;
+}
+
+// Fused RoPE + KV append (decode): q/k/v of the new token come straight from the QKV projection's f32
+// split-K slabs; every workgroup rotates its own G query heads, the workgroup holding the last block
+// appends the rotated k and v to the cache, and the new token's key/value are substituted from
+// registers where the score loop meets position p (no dependency on the cache write completing).
+struct RopeArgs {
+  const float* parts;  // [nparts][B][(H + 2 Hkv) * 128] f32
+  size_t part_stride;
+  int nparts;
+  const float* cos_t;  // [max_pos][64]
+  const float* sin_t;
+  uint16_t* kc;        // cache (writable aliases of the kernel's kc / vc)
+  uint16_t* vc;
+};
+
+template <int G, int ROPE>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime slab count
 __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc,
                                                           const int* __restrict__ block_tables, int max_blocks,
                                                           const int* __restrict__ pos, int Hkv, float scale_log2,
                                                           int chunk_blocks, int nsplit, uint16_t* __restrict__ out,
                                                           float* __restrict__ opart, float* __restrict__ mlpart,
-                                                          int xf_mt) {
+                                                          int* __restrict__ counters, int xf_mt, RopeArgs ra) {
   constexpr int D = 128;
-  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  // heads fastest: consecutive workgroups (round-robin over the 8 XCDs) are different (b, kv-head) pairs of
+  // the same split, so splits a sequence does not need (eff_split) never leave whole XCDs idle
+  const int hk = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int H = Hkv * G;
   const int tid = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(opart, 0, 0x7fffffff, 0x00020000);
   const int lg = tid >> 4, li = tid & 15, wv = tid >> 6;
   const int ctx = pos[b] + 1;
   const int nblk = (ctx + 63) >> 6;
-  const int blk0 = split * chunk_blocks;
-  const int blk1 = min(nblk, blk0 + chunk_blocks);
-
-  float qf[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const uint4 v = *reinterpret_cast<const uint4*>(q + ((size_t)(b * H + hk * G + g)) * D + li * 8);
-    unpack8(v, qf[g]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[g][j] *= scale_log2;
-  }
-  float m[G], l[G], o[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    m[g] = LSA_NEG;
-    l[g] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
-  }
+  int ech, nse;
+  eff_split(nblk, chunk_blocks, nsplit, ech, nse);
+  if (split >= nse) return;  // whole workgroup: this sequence needs fewer splits
+  const int blk0 = split * ech;
+  const int blk1 = min(nblk, blk0 + ech);
 
   const int* bt = block_tables + (size_t)b * max_blocks;
   // K/V of block blk+1 are in flight while block blk is scored (two register sets, static names)
@@ -68,13 +85,104 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
       vr[u] = *reinterpret_cast<const uint4*>(vc + base + tok * D + li * 8);
     }
   };
+  // the first K/V block is in flight while the query (and, fused, RoPE) is prepared
+  if (blk0 < blk1) fetch(kA, vA, blk0);
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int tpos = ctx - 1;  // position of the new token
+  float qf[G][8];
+  float knew[8], vnew[8];
+  if constexpr (ROPE != 0) {
+    // lane group j < G builds query head j, group G the new key, group G + 1 the new value (each lane
+    // 8 dims, summed over the split-K slabs, rotated in f32, rounded to bf16 like the unfused path);
+    // the results go through LDS to all 16 lane groups
+    static_assert(G + 2 <= 16, "fused rope: one lane group per q head + k + v");
+    __shared__ __attribute__((aligned(16))) float qkv_s[G + 2][D];
+    if (lg < G + 2) {
+      const float* row = ra.parts + (size_t)b * (H + 2 * Hkv) * D;
+      const int dd = li * 8;  // own 8 dims; the rotate-half partners live in lane li ^ 8
+      const int off = lg < G ? (hk * G + lg) * D : (lg == G ? (H + hk) * D : (H + Hkv + hk) * D);
+      float x[8];
+      const float4 a0 = *reinterpret_cast<const float4*>(row + off + dd);
+      const float4 a1 = *reinterpret_cast<const float4*>(row + off + dd + 4);
+      x[0] = a0.x; x[1] = a0.y; x[2] = a0.z; x[3] = a0.w; x[4] = a1.x; x[5] = a1.y; x[6] = a1.z; x[7] = a1.w;
+      const int np = ROPE > 0 ? ROPE : ra.nparts;
+#pragma unroll
+      for (int sp = 1; sp < np; ++sp) {
+        const float* r2 = row + sp * ra.part_stride + off + dd;
+        const float4 b0 = *reinterpret_cast<const float4*>(r2);
+        const float4 b1 = *reinterpret_cast<const float4*>(r2 + 4);
+        x[0] += b0.x; x[1] += b0.y; x[2] += b0.z; x[3] += b0.w; x[4] += b1.x; x[5] += b1.y; x[6] += b1.z; x[7] += b1.w;
+      }
+      float y[8];
+      if (lg <= G) {  // rotate q heads and k
+        const float4 c0 = *reinterpret_cast<const float4*>(ra.cos_t + (size_t)tpos * 64 + (dd & 63));
+        const float4 c1 = *reinterpret_cast<const float4*>(ra.cos_t + (size_t)tpos * 64 + (dd & 63) + 4);
+        const float4 s0 = *reinterpret_cast<const float4*>(ra.sin_t + (size_t)tpos * 64 + (dd & 63));
+        const float4 s1 = *reinterpret_cast<const float4*>(ra.sin_t + (size_t)tpos * 64 + (dd & 63) + 4);
+        const float sg = li < 8 ? -1.f : 1.f;
+        const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = x[j] * cc[j] + sg * __shfl_xor(x[j], 8, 64) * sn[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = x[j];
+      }
+      const uint4 yq = pack8(y);
+      unpack8(yq, y);
+      *reinterpret_cast<float4*>(&qkv_s[lg][dd]) = make_float4(y[0], y[1], y[2], y[3]);
+      *reinterpret_cast<float4*>(&qkv_s[lg][dd + 4]) = make_float4(y[4], y[5], y[6], y[7]);
+      // the workgroup covering position tpos appends the new token's k / v to the cache
+      if (lg >= G && blk0 < nblk && blk1 == nblk) {
+        const size_t co = (((size_t)block_tables[(size_t)b * max_blocks + (tpos >> 6)] * Hkv + hk) * 64 +
+                           (tpos & 63)) * D + dd;
+        *reinterpret_cast<uint4*>((lg == G ? ra.kc : ra.vc) + co) = yq;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[g][j] = qkv_s[g][li * 8 + j] * scale_log2;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      knew[j] = qkv_s[G][li * 8 + j];
+      vnew[j] = qkv_s[G + 1][li * 8 + j];
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint4 v = *reinterpret_cast<const uint4*>(q + ((size_t)(b * H + hk * G + g)) * D + li * 8);
+      unpack8(v, qf[g]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[g][j] *= scale_log2;
+    }
+  }
+  float m[G], l[G], o[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m[g] = LSA_NEG;
+    l[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
+  }
+
   auto score = [&](const uint4 (&kr)[4], const uint4 (&vr)[4], int blk) {
     float s[4][G];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float kf[8];
       unpack8(kr[u], kf);
-      const bool valid = (blk * 64 + wv * 16 + u * 4 + (lg & 3)) < ctx;
+      const int tp = blk * 64 + wv * 16 + u * 4 + (lg & 3);
+      const bool valid = tp < ctx;
+      if constexpr (ROPE != 0) {
+        if (tp == tpos) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) kf[j] = knew[j];
+        }
+      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float d = 0.f;
@@ -103,13 +211,18 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
       for (int u = 0; u < 4; ++u) {
         float vf[8];
         unpack8(vr[u], vf);
+        if constexpr (ROPE != 0) {
+          if (blk * 64 + wv * 16 + u * 4 + (lg & 3) == tpos) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) vf[j] = vnew[j];
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[g][j] = fmaf(p[u], vf[j], o[g][j]);
       }
     }
   };
   if (blk0 < blk1) {
-    fetch(kA, vA, blk0);
     int blk = blk0;
     for (; blk + 1 < blk1; blk += 2) {
       fetch(kB, vB, blk + 1);
@@ -140,91 +253,121 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
     *reinterpret_cast<float4*>(&so[lg][g][li * 8 + 4]) = make_float4(o[g][4], o[g][5], o[g][6], o[g][7]);
   }
   __syncthreads();
-  for (int e = tid; e < G * D; e += 256) {
-    const int g = e / D, d = e % D;
+  // each thread finishes 4 consecutive dims of one head
+  for (int e = tid; e < G * 32; e += 256) {
+    const int g = e >> 5, d0 = (e & 31) * 4;
     float M = LSA_NEG;
 #pragma unroll
     for (int k = 0; k < 16; ++k) M = fmaxf(M, sm[k][g]);
-    float L = 0.f, O = 0.f;
+    float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const float wgt = exp2f(sm[k][g] - M);
       L += sl[k][g] * wgt;
-      O += so[k][g][d] * wgt;
+      const float4 v = *reinterpret_cast<const float4*>(&so[k][g][d0]);
+      O[0] += v.x * wgt; O[1] += v.y * wgt; O[2] += v.z * wgt; O[3] += v.w * wgt;
     }
     const int h = hk * G + g;
-    if (nsplit == 1) {
-      out[xf_mt ? xf_off(b, h * D + d, xf_mt) : ((size_t)b * H + h) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+    if (nse == 1) {
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+      uint2 pk;
+      pk.x = pack2bf(O[0] * inv, O[1] * inv);
+      pk.y = pack2bf(O[2] * inv, O[3] * inv);
+      *reinterpret_cast<uint2*>(out + (xf_mt ? xf_off(b, h * D + d0, xf_mt) : ((size_t)b * H + h) * D + d0)) = pk;
     } else {
+      // publish the partial write-through (sc1): the reducing workgroup may sit on another XCD
       const size_t pi = ((size_t)b * H + h) * nsplit + split;
-      opart[pi * D + d] = O;
-      if (d == 0) {
-        mlpart[pi * 2] = M;
-        mlpart[pi * 2 + 1] = L;
-      }
+      const u32x4_t v = {__float_as_uint(O[0]), __float_as_uint(O[1]), __float_as_uint(O[2]), __float_as_uint(O[3])};
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs_o, (int)((pi * D + d0) * 4), 0, LSA_SC1);
+      if (d0 == 0)
+        __hip_atomic_store((g_u64*)(mlpart) + pi,
+                           ((unsigned long long)__float_as_uint(L) << 32) | __float_as_uint(M), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-}
+  if (nse == 1) return;
 
-// merge the split-KV partials of one (sequence, head): the split maxima / weights go through LDS once,
-// then every thread sums its output dim over the splits with independent (pipelined) loads
-__global__ __launch_bounds__(128) void attn_combine_kernel(const float* __restrict__ opart,
-                                                           const float* __restrict__ mlpart, int nsplit,
-                                                           uint16_t* __restrict__ out, int H, int xf_mt) {
-  __shared__ float wts[256];
-  __shared__ float red[2];
-  const int bh = blockIdx.x, d = threadIdx.x;
-  const float* ml = mlpart + (size_t)bh * nsplit * 2;
-  float mloc = LSA_NEG;
-  for (int s = d; s < nsplit; s += 128) mloc = fmaxf(mloc, ml[2 * s]);
-  mloc = wave_max(mloc);
-  if ((d & 63) == 0) red[d >> 6] = mloc;
+  // split-KV combine inside the launch: the last of this (sequence, kv-head)'s nse workgroups to arrive
+  // merges all partials (guide §6 G16 counter form: sc1 stores drained -> barrier -> one relaxed agent
+  // ticket add; the reducer reads every partial with sc1 loads, no fences).  The ticket word is reset by
+  // the reducer for the next layer / replay.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const float M = fmaxf(red[0], red[1]);
-  float lloc = 0.f;
-  for (int s = d; s < nsplit; s += 128) {
-    const float w = exp2f(ml[2 * s] - M);
-    wts[s] = w;
-    lloc += ml[2 * s + 1] * w;
+  __shared__ int s_last;
+  g_i32* ctr = (g_i32*)(counters) + (size_t)b * Hkv + hk;
+  if (tid == 0) s_last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nse - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  float* cm = &so[0][0][0];          // [G][256] split maxima, then weights
+  float* cl = cm + G * 256;          // [G][256] split sums
+  for (int i = tid; i < G * nse; i += 256) {
+    const int g = i / nse, sp = i - g * nse;
+    const size_t pi = ((size_t)b * H + hk * G + g) * nsplit + sp;
+    const unsigned long long ml =
+        __hip_atomic_load((g_u64*)(mlpart) + pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cm[g * 256 + sp] = __uint_as_float((uint32_t)ml);
+    cl[g * 256 + sp] = __uint_as_float((uint32_t)(ml >> 32));
   }
-  lloc = wave_sum(lloc);
   __syncthreads();
-  if ((d & 63) == 0) red[d >> 6] = lloc;
-  __syncthreads();
-  const float L = red[0] + red[1];
-  const float* op = opart + (size_t)bh * nsplit * 128 + d;
-  float O = 0.f;
-#pragma unroll 8
-  for (int s = 0; s < nsplit; ++s) O = fmaf(op[(size_t)s * 128], wts[s], O);
-  const size_t oi = xf_mt ? xf_off(bh / H, (bh % H) * 128 + d, xf_mt) : (size_t)bh * 128 + d;
-  out[oi] = f2bf(L > 0.f ? O / L : 0.f);
+  for (int e = tid; e < G * 32; e += 256) {
+    const int g = e >> 5, d0 = (e & 31) * 4;
+    float M = LSA_NEG;
+    for (int sp = 0; sp < nse; ++sp) M = fmaxf(M, cm[g * 256 + sp]);
+    float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
+    const size_t pi0 = ((size_t)b * H + hk * G + g) * nsplit;
+#pragma unroll 4
+    for (int sp = 0; sp < nse; ++sp) {
+      const float wgt = exp2f(cm[g * 256 + sp] - M);
+      L += cl[g * 256 + sp] * wgt;
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs_o, (int)(((pi0 + sp) * D + d0) * 4), 0, LSA_SC1);
+      O[0] += __uint_as_float(v[0]) * wgt; O[1] += __uint_as_float(v[1]) * wgt;
+      O[2] += __uint_as_float(v[2]) * wgt; O[3] += __uint_as_float(v[3]) * wgt;
+    }
+    const int h = hk * G + g;
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    uint2 pk;
+    pk.x = pack2bf(O[0] * inv, O[1] * inv);
+    pk.y = pack2bf(O[2] * inv, O[3] * inv);
+    *reinterpret_cast<uint2*>(out + (xf_mt ? xf_off(b, h * D + d0, xf_mt) : ((size_t)b * H + h) * D + d0)) = pk;
+  }
 }
 
 extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit,
-                               void* out, float* opart, float* mlpart, int xf_mt, hipStream_t s) {
+                               void* out, float* opart, float* mlpart, int* counters, int xf_mt,
+                               const float* qkv_parts, int nparts,
+                               long part_stride, const float* cos_t, const float* sin_t, hipStream_t s) {
   if (H % Hkv) return -1;
   if (xf_mt && B > 16 * xf_mt) return -4;
   if (nsplit > 256) return -3;
   const int G = H / Hkv;
   const float sl2 = scale * 1.4426950408889634f;
-  dim3 grid(nsplit, Hkv, B);
+  dim3 grid(Hkv, B, nsplit);
   const uint16_t* qq = reinterpret_cast<const uint16_t*>(q);
   const uint16_t* kk = reinterpret_cast<const uint16_t*>(kc);
   const uint16_t* vv = reinterpret_cast<const uint16_t*>(vc);
   uint16_t* oo = reinterpret_cast<uint16_t*>(out);
-#define LSA_AD(GV)                                                                                                 \
-  case GV:                                                                                                         \
-    hipLaunchKernelGGL(attn_decode_kernel<GV>, grid, dim3(256), 0, s, qq, kk, vv, block_tables, max_blocks, pos, Hkv, \
-                       sl2, chunk_blocks, nsplit, oo, opart, mlpart, xf_mt);                                      \
+  const RopeArgs ra{qkv_parts, (size_t)part_stride, nparts, cos_t, sin_t, const_cast<uint16_t*>(kk),
+                    const_cast<uint16_t*>(vv)};
+#define LSA_ADK(GV, RP)                                                                                      \
+  hipLaunchKernelGGL((attn_decode_kernel<GV, RP>), grid, dim3(256), 0, s, qq, kk, vv, block_tables, max_blocks, pos, \
+                     Hkv, sl2, chunk_blocks, nsplit, oo, opart, mlpart, counters, xf_mt, ra)
+#define LSA_AD(GV)                                  \
+  case GV:                                          \
+    if (!qkv_parts) LSA_ADK(GV, 0);                 \
+    else if (nparts == 1) LSA_ADK(GV, 1);           \
+    else if (nparts == 2) LSA_ADK(GV, 2);           \
+    else if (nparts == 4) LSA_ADK(GV, 4);           \
+    else if (nparts == 8) LSA_ADK(GV, 8);           \
+    else LSA_ADK(GV, -1);                           \
     break;
   switch (G) {
     LSA_AD(1) LSA_AD(2) LSA_AD(3) LSA_AD(4) LSA_AD(8)
     default: return -2;
   }
+#undef LSA_ADK
 #undef LSA_AD
-  if (nsplit > 1) hipLaunchKernelGGL(attn_combine_kernel, dim3(B * H), dim3(128), 0, s, opart, mlpart, nsplit, oo, H,
-                                     xf_mt);
   return (int)hipGetLastError();
 }
 

@@ -19,6 +19,8 @@ then add_rmsnorm(final) -> gemm lm_head [-> all_gather] -> argmax/sample + commi
 """
 from __future__ import annotations
 
+import os
+
 import math
 from typing import Optional, Sequence
 
@@ -35,8 +37,12 @@ SAMPLE_HIST = 64  # repetition-penalty window (Ollama repeat_last_n default)
 class ModelRunner:
     def __init__(self, weights: LlamaWeights, max_slots: int = 32, max_model_len: int = 4096,
                  num_kv_blocks: Optional[int] = None, kv_memory_fraction: float = 0.85,
-                 max_new_cap: Optional[int] = None, tp=None, use_graphs: bool = True, steps_per_graph: int = 1):
+                 max_new_cap: Optional[int] = None, tp=None, use_graphs: bool = True, steps_per_graph: int = 1,
+                 fuse_norm: bool = False, fuse_rope: Optional[bool] = None):
         self.w = weights
+        self._fuse_norm = fuse_norm
+        # decode RoPE + KV append inside the attention kernel (LSA_FUSE_ROPE=0 restores the separate launch)
+        self.fuse_rope = (os.environ.get("LSA_FUSE_ROPE", "1") != "0") if fuse_rope is None else fuse_rope
         self.spec = spec = weights.spec
         self.device = weights.device
         self.tp = tp
@@ -110,6 +116,8 @@ class ModelRunner:
         self.xn_f = torch.zeros(xr * self.d, **bf)
         self.attn_f = torch.zeros(xr * self.H * self.D, **bf)
         self.act_f = torch.zeros(xr * self.ffn_l, **bf)
+        # per-call-site counters of the GEMM + fused residual/RMSNorm kernels (left zeroed by them)
+        self.norm_ctr = torch.zeros(2 * self.L, 2, dtype=torch.int32, device=dev)
         self.o_buf = torch.zeros(8 * S * self.d, **f32)
         self.down_buf = torch.zeros(8 * S * self.d, **f32)
         self.qkv_buf = torch.zeros(8 * S * (self.H + 2 * self.Hkv) * self.D, **f32)
@@ -117,8 +125,7 @@ class ModelRunner:
         self.logits = self.logits_l if tps == 1 else torch.zeros(S, self.V, **f32)
         self.gather_buf = None if tps == 1 else torch.zeros(tps * S * self.Vl, **f32)
         _, nsplit_max = ops.decode_split_plan(1, self.Hkv, self.max_model_len)
-        self.opart = torch.zeros(S * self.H * max(nsplit_max, 1) * self.D, **f32)
-        self.mlpart = torch.zeros(S * self.H * max(nsplit_max, 1) * 2, **f32)
+        self.attn_ws = ops.decode_workspace(S, self.H, self.Hkv, nsplit_max, dev)
         self.amax_part = torch.zeros(S * ((self.V + 4095) // 4096), dtype=torch.int64, device=dev)
         self.cand = torch.zeros(S * ((self.V + 2047) // 2048) * 64, dtype=torch.int64, device=dev)
         self.graphs: dict = {}
@@ -132,6 +139,15 @@ class ModelRunner:
         if not self.on_gpu or M > 64 or (tp_reduced and self.tp is not None and self.tp.size > 1):
             return 1
         return ops.pick_gemm_config(M, N or self.d, K, "f32", xf=xf)[1]
+
+    @property
+    def fuse_norm(self) -> bool:
+        """Decode O/down GEMMs run the next residual+RMSNorm in-kernel (bf16 weights, no TP all-reduce).
+        Off by default: on MI355X the cross-XCD completion protocol (a ticket atomic per workgroup on one
+        counter + the workers' L2 invalidate) measured 3-13 us slower than a separate ~3.5 us norm launch
+        (scripts/bench_fuse.py, profiles/fuse_norm_mi355x.txt)."""
+        return (self._fuse_norm and self.on_gpu and self.w.layers[0].wo.kind == "bf16"
+                and (self.tp is None or self.tp.size == 1))
 
     def use_xfrag(self, B: int) -> bool:
         """Fragment-major activations pay off once a decode batch spans >1 row tile (B > 16):
@@ -171,7 +187,7 @@ class ModelRunner:
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
         plan = ops.decode_split_plan(B, self.Hkv, self.max_model_len)
-        ws = (self.opart, self.mlpart)
+        ws = self.attn_ws
         if xf:  # every GEMM input lives in the fragment-major layout, written by its producer
             xn, attn, act = self.xn_f, self.attn_f, self.act_f
 
@@ -180,24 +196,43 @@ class ModelRunner:
         else:
             xn, attn, act = self.xn[:B], self.attn[:B], self.act[:B]
             lin = ops.linear
+        # O / down projections carry the following residual add + RMSNorm in their last workgroups
+        # (one launch instead of two) unless a TP all-reduce has to sit between them
+        fuse = self.fuse_norm
+        L = len(w.layers)
         for l, lw in enumerate(w.layers):
             if l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf)
-            else:
+            elif not fuse:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
-            # QKV as f32 split-K slabs; rope_append sums them while rotating (no extra reduction pass)
+            # QKV as f32 split-K slabs; the attention kernel sums them, applies RoPE and appends the new
+            # token's k/v to the paged cache itself (no separate rope/append launch)
             lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
             kc, vc = self.kv[l, 0], self.kv[l, 1]
-            ops.rope_append(qkv_parts, pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv)
+            if not self.fuse_rope:
+                ops.rope_append(qkv_parts, pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv)
+            fr = self.fuse_rope
             ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale,
-                            attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf)
-            lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
-            self._allreduce(o_parts)
-            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts, rows=B, xf=xf)
+                            attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
+                            qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
+                            sin=self.sin if fr else None)
+            if fuse:
+                ops.linear_norm(attn, B, lw.wo, o_parts, h, lw.mlp_norm, self.eps, xn, self.norm_ctr[2 * l],
+                                x_frag=xf, xn_frag=xf, splitk=sk_o)
+            else:
+                lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
+                self._allreduce(o_parts)
+                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts, rows=B, xf=xf)
             lin(xn, lw.w_gate_up, "silu", out=act)
-            lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
-            self._allreduce(d_parts)
-        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
+            if fuse:
+                nxt = w.layers[l + 1].attn_norm if l + 1 < L else w.final_norm
+                ops.linear_norm(act, B, lw.w_down, d_parts, h, nxt, self.eps, xn, self.norm_ctr[2 * l + 1],
+                                x_frag=xf, xn_frag=xf, splitk=sk_d)
+            else:
+                lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
+                self._allreduce(d_parts)
+        if not fuse:
+            ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
         logits = self._lm_head(xn, B, xf)
         st = (self.out_tokens[:B], self.gen_len[:B], self.input_ids[:B], self.positions[:B], self.finished[:B])
         if sample:

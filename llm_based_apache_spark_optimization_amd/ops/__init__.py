@@ -278,6 +278,28 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
     return out
 
 
+def linear_norm(x: torch.Tensor, M: int, w: PackedWeight, out: torch.Tensor, h: torch.Tensor,
+                norm_w: torch.Tensor, eps: float, xn: torch.Tensor, counter: torch.Tensor, x_frag: bool = False,
+                xn_frag: bool = False, splitk: Optional[int] = None, nb: Optional[int] = None,
+                waves: Optional[int] = None, div: Optional[int] = None) -> torch.Tensor:
+    """Decode projection + the next residual/RMSNorm in one kernel (M <= 64, bf16 weights):
+    out = f32 split-K slabs of x @ W^T;  h[:M] += sum(out);  xn = rmsnorm(h[:M]) * norm_w.
+    x is fragment-major when x_frag; xn is written fragment-major when xn_frag.  ``counter`` is a
+    2-int32 zero tensor owned by the call site (the kernel leaves it zeroed)."""
+    if not _gpu(h) or w.kind != "bf16":
+        xr = from_xfrag(x, M, w.K) if x_frag else x[:M]
+        parts = linear(xr, w, "f32", None, splitk, nb, waves, div)
+        return add_rmsnorm(h, norm_w, eps, xn, parts=parts, rows=M, xf=xn_frag)
+    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, w.K, "f32", xf=x_frag)
+    nb = nb0 if nb is None else nb
+    splitk = sk0 if splitk is None else splitk
+    waves = wv0 if waves is None else waves
+    div = dv0 if div is None else div
+    ext().gemm_norm(x, M, w.K, w.data, w.N, out, nb, splitk, waves, div, x_frag, h, norm_w, eps, xn,
+                    xfrag_tiles(M) if xn_frag else 0, counter)
+    return xn
+
+
 # ----------------------------------------------------------------------------------- norms / rope
 def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
                 parts: Optional[torch.Tensor] = None, ids: Optional[torch.Tensor] = None,
@@ -333,22 +355,39 @@ def silu_mul(g: torch.Tensor, u: torch.Tensor, out: Optional[torch.Tensor] = Non
 
 # ----------------------------------------------------------------------------------- attention
 def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int]:
-    """(chunk_blocks, nsplit) for split-KV decode: aim for >= 512 workgroups, but keep >= 2 blocks per
-    split (the kernel double-buffers K/V across blocks) and <= 256 splits (the combine's LDS)."""
+    """(chunk_blocks, nsplit) grid plan of split-KV decode for contexts up to max_ctx.  The kernel picks
+    each sequence's own split from its length (csrc/kernels/attention.hip eff_split): <= 4 blocks run
+    unsplit, longer contexts split into chunk_blocks-block pieces.  chunk 2 while the (sequence, kv-head)
+    grid is small (B * Hkv < 128, e.g. one 3B sequence at 2k context: 17 splits measured best), else 4;
+    at most 256 splits (the combine's LDS)."""
     nblk = max(1, (max_ctx + 63) // 64)
-    chunk = nblk
-    while chunk > 2 and B * Hkv * ((nblk + chunk - 1) // chunk) < 512:
-        chunk = (chunk + 1) // 2
+    if nblk <= 4:  # every sequence runs unsplit (eff_split): no empty split workgroups, no combine
+        return nblk, 1
+    chunk = 2 if B * Hkv < 128 else 4
     while (nblk + chunk - 1) // chunk > 256:
         chunk += 1
     return chunk, (nblk + chunk - 1) // chunk
 
 
-def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None, xf=False):
-    """q [B,H,128] vs paged cache, context = pos + 1.  workspace = (opart, mlpart) for split-KV.
-    xf=True: out is a flat buffer receiving the fragment-major layout of the [B, H*128] output."""
+def decode_workspace(B: int, H: int, Hkv: int, nsplit: int, device) -> tuple:
+    """(opart, mlpart, counters) for split-KV decode: per-split partial outputs / (max, sum) pairs and the
+    per-(sequence, kv-head) arrival tickets of the in-kernel combine (must start zeroed; the kernel
+    leaves them zeroed)."""
+    return (torch.empty(B * H * max(nsplit, 1) * 128, device=device, dtype=torch.float32),
+            torch.empty(B * H * max(nsplit, 1) * 2, device=device, dtype=torch.float32),
+            torch.zeros(B * Hkv, device=device, dtype=torch.int32))
+
+
+def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None, xf=False,
+                qkv_parts=None, cos=None, sin=None):
+    """q [B,H,128] vs paged cache, context = pos + 1.  workspace = decode_workspace(...) for split-KV.
+    xf=True: out is a flat buffer receiving the fragment-major layout of the [B, H*128] output.
+    qkv_parts ([S, B, (H+2Hkv)*128] f32 split-K slabs of the QKV projection) + cos/sin: RoPE and the
+    KV-cache append of the new token are fused in (``q`` is then only a [B, H, 128] scratch buffer)."""
     B = pos.shape[0]
-    if not _gpu(q):
+    if not _gpu(pos):
+        if qkv_parts is not None:
+            ref.rope_append(qkv_parts, pos, None, block_tables, cos, sin, q, kc, vc, H, Hkv)
         if not xf:
             return ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out)
         tmp = torch.empty(B, H, q.shape[-1], dtype=torch.bfloat16, device=q.device)
@@ -358,12 +397,10 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
         return out
     chunk, nsplit = plan if plan is not None else decode_split_plan(B, Hkv, block_tables.shape[1] * 64)
     if workspace is None:
-        opart = torch.empty(B * H * nsplit * 128, device=q.device, dtype=torch.float32)
-        mlpart = torch.empty(B * H * nsplit * 2, device=q.device, dtype=torch.float32)
-    else:
-        opart, mlpart = workspace
-    ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart,
-                      xfrag_tiles(B) if xf else 0)
+        workspace = decode_workspace(B, H, Hkv, nsplit, q.device)
+    opart, mlpart, counters = workspace
+    ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart, counters,
+                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin)
     return out
 
 

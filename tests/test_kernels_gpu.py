@@ -207,6 +207,38 @@ def test_add_rmsnorm(gpu, D):
     assert _rel(xs, ref_xs) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 4, 20, 32, 64])
+@pytest.mark.parametrize("frag", [False, True])
+@pytest.mark.parametrize("splitk", [1, 4])
+@pytest.mark.parametrize("N", [4096, 256])
+def test_gemm_fused_norm(gpu, M, frag, splitk, N):
+    """GEMM -> f32 slabs -> (last workgroups) residual add + RMSNorm == GEMM then add_rmsnorm.
+    N = 256 gives fewer workgroups than rows (every workgroup then normalises several rows)."""
+    K = 2048
+    torch.manual_seed(M + splitk)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(torch.bfloat16)
+    h = torch.randn(M, N, device=gpu)
+    h_ref = h.clone()
+    parts_ref = ops.linear(x, pw, "f32", splitk=splitk)
+    xn_ref = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    ops.add_rmsnorm(h_ref, nw, 1e-5, xn_ref, parts=parts_ref)
+    counter = torch.zeros(2, device=gpu, dtype=torch.int32)
+    out = torch.empty(splitk, M, N, device=gpu)
+    xin = ops.to_xfrag(x) if frag else x
+    xn = torch.zeros(ops.xfrag_tiles(M) * 16 * N if frag else M * N, device=gpu, dtype=torch.bfloat16)
+    for _ in range(3):  # repeated launches: the counter must come back to zero every time
+        hh = h.clone()
+        ops.linear_norm(xin, M, pw, out, hh, nw, 1e-5, xn, counter, x_frag=frag, xn_frag=frag, splitk=splitk)
+        torch.cuda.synchronize()
+        assert counter.tolist() == [0, 0]
+        assert torch.allclose(hh, h_ref, atol=1e-4, rtol=1e-5)
+        got = ops.from_xfrag(xn, M, N) if frag else xn.view(M, N)
+        assert _rel(got, xn_ref) < 1e-2
+
+
 @pytest.mark.parametrize("rows", [3, 20, 33])
 def test_add_rmsnorm_xfrag(gpu, rows):
     """Fragment-major output of the norm (decode GEMM input) == to_xfrag of the row-major output."""
@@ -288,12 +320,44 @@ def test_attn_decode(gpu, HH, lens):
     out3 = torch.empty_like(out)
     ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, out3, plan=(bt.shape[1], 1))
     assert _rel(out3, out2) < 1e-2
+    # a grid planned for a much longer context (graph capture at max_model_len): per-sequence splits
+    out4 = torch.empty_like(out)
+    ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, out4, plan=ops.decode_split_plan(B, Hkv, 16384))
+    assert _rel(out4, out2) < 1e-2
     # fragment-major output (O-projection input), split and single-split paths
     for plan in (None, (bt.shape[1], 1)):
         xf = torch.zeros(ops.xfrag_tiles(B) * 16 * H * D, device=gpu, dtype=torch.bfloat16)
         ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, xf, plan=plan, xf=True)
         ro = out if plan is None else out3
         assert torch.equal(ops.from_xfrag(xf, B, H * D), ro.view(B, -1))
+
+
+@pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
+@pytest.mark.parametrize("lens", [[1, 64, 65, 300], [2000]])
+@pytest.mark.parametrize("nparts", [1, 3, 8])
+def test_attn_decode_fused_rope(gpu, HH, lens, nparts):
+    """RoPE + KV append fused into decode attention == rope_append then attn_decode (cache and output)."""
+    H, Hkv = HH
+    D = 128
+    kc, vc, bt = _paged(lens, Hkv, D, gpu, seed=7)
+    B = len(lens)
+    pos = torch.tensor([n - 1 for n in lens], device=gpu, dtype=torch.int32)
+    cos, sin = ref.rope_tables(D, 4096, 500000.0, device=gpu)
+    parts = torch.randn(nparts, B, (H + 2 * Hkv) * D, device=gpu)
+    scale = 1 / math.sqrt(D)
+    k1, v1 = kc.clone(), vc.clone()
+    q1 = torch.empty(B, H, D, device=gpu, dtype=torch.bfloat16)
+    ops.rope_append(parts, pos, None, bt, cos, sin, q1, k1, v1, H, Hkv)
+    o1 = torch.empty(B, H, D, device=gpu, dtype=torch.bfloat16)
+    ops.attn_decode(q1, k1, v1, bt, pos, H, Hkv, scale, o1)
+    k2, v2 = kc.clone(), vc.clone()
+    o2 = torch.empty_like(o1)
+    ops.attn_decode(torch.empty_like(q1), k2, v2, bt, pos, H, Hkv, scale, o2, qkv_parts=parts, cos=cos, sin=sin)
+    torch.cuda.synchronize()
+    assert torch.equal(v1, v2)  # v is copied
+    assert torch.allclose(k1.float(), k2.float(), rtol=1e-2, atol=1e-2)  # fma contraction may differ by 1 ulp
+    assert (k1 != k2).float().mean() < 0.01
+    assert _rel(o2, o1) < 1e-2
 
 
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
