@@ -27,6 +27,10 @@
 #define EPI_F32 1
 #define EPI_SILU 2
 #define EPI_F32N 3
+#ifndef LSA_XSAME
+#define LSA_XSAME 0  // experiment knob (LSA_HIP_EXTRA=-DLSA_XSAME=1): every k-step reads the same 2 activation
+                     // fragments (L1-resident) -> upper bound of removing activation traffic
+#endif
 
 // Fused residual + RMSNorm tail of an EPI_F32N GEMM (see fused_norm_tail).
 struct NormArgs {
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       const int kk = min(kb + u, kbB - 1);
 #pragma unroll
       for (int j = 0; j < MT; ++j)
-        xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * (XF ? MT * 512 : 32));
+        xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)(LSA_XSAME ? (kk & 1) : kk) * (XF ? MT * 512 : 32));
     }
   };
   auto comp = [&](const uint4 (&wr)[U][NB], const uint4 (&xr)[U][MT], int c) {

@@ -11,6 +11,7 @@ kernel recompiles one file.  ``python -m llm_based_apache_spark_optimization_amd
 from __future__ import annotations
 
 import hashlib
+import shlex
 import os
 import subprocess
 import sys
@@ -73,6 +74,7 @@ def build_hip(jobs: int = 8, verbose: bool = False) -> Path:
     kdir = CSRC / "kernels"
     headers = sorted(kdir.glob("*.h"))
     kflags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast", "-Wno-unused-result"]
+    kflags += shlex.split(os.environ.get("LSA_HIP_EXTRA", ""))  # experiment knobs, e.g. -DLSA_XSAME=1
     srcs = sorted(kdir.glob("*.hip"))
     tflags, ldflags = _torch_flags()
     bflags = ["-O2", "-std=c++17", "-fPIC", "-Wno-deprecated-declarations", "-Wno-unused-result", *tflags]

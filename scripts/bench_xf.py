@@ -13,6 +13,9 @@ SHAPES = {"7b_qkv": (12288, 4096, "f32"), "7b_o": (4096, 4096, "f32"), "7b_gateu
           "7b_down": (4096, 11008, "f32"), "3b_qkv": (5120, 3072, "f32"), "3b_gateup": (16384, 3072, "silu"),
           "3b_down": (3072, 8192, "f32"), "3b_o": (3072, 3072, "f32")}
 Ms = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else [32]
+if len(sys.argv) > 2:
+    SHAPES = {k: v for k, v in SHAPES.items() if k in sys.argv[2].split(",")}
+MODES = sys.argv[3].split(",") if len(sys.argv) > 3 else ["row", "xf"]
 
 
 def timeit(fn, it=40):
@@ -40,7 +43,7 @@ for name, (N, K, epi) in SHAPES.items():
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
         xf = ops.to_xfrag(x)
         best = {}
-        for mode in ("row", "xf"):
+        for mode in MODES:
             for waves, dv in ((4, 1), (4, 2), (8, 2), (4, 4), (8, 1)):
                 for nb in (1, 2, 4):
                     if (N // 16) % nb or (epi == "silu" and nb == 1) or (M > 32 and nb > 2):
@@ -53,15 +56,17 @@ for name, (N, K, epi) in SHAPES.items():
                         if mode == "row":
                             f = lambda i: ops.linear(x, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb, waves=waves, div=dv)  # noqa: E731
                         else:
-                            f = lambda i: ops.linear_xf(xf, M, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb, waves=waves, div=dv)  # noqa: E731
+                            f = lambda i: ops.linear_xf(xf, M, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb,  # noqa: E731
+                                                        waves=waves, div=dv)
                         us = timeit(f)
                         r = dict(shape=name, M=M, mode=mode, nb=nb, splitk=sk, waves=waves, div=dv, us=round(us, 2),
                                  TBps=round(nbytes / us / 1e6, 3))
                         out_rows.append(r)
                         if mode not in best or us < best[mode]["us"]:
                             best[mode] = r
-        print("BEST", json.dumps(best["row"]), flush=True)
-        print("BEST", json.dumps(best["xf"]), flush=True)
+        for mode in MODES:
+            if mode in best:
+                print("BEST", json.dumps(best[mode]), flush=True)
     del ws
     torch.cuda.empty_cache()
 json.dump(out_rows, open("gpurun_out/xf_sweep.json", "w"), indent=0)
