@@ -27,6 +27,8 @@ import threading
 import time
 from typing import Callable, Dict, Optional
 
+import torch
+
 from .engine.engine import SamplingParams
 
 
@@ -78,8 +80,16 @@ class Backend:
 class _EngineLoop:
     """Drives one LLMEngine from a background thread; callers block on their request's event."""
 
-    def __init__(self, engine):
+    def __init__(self, engine, run_ahead: int = 16):
         self.engine = engine
+        engine.run_ahead = run_ahead  # serving: bound each decode run so arrivals are admitted promptly
+        # each engine runs on its own HIP stream: co-served models overlap on the GPU, and one engine's
+        # host syncs never wait for the other's queued kernels
+        self.stream = None
+        dev = getattr(getattr(engine, "runner", None), "device", None)
+        if dev is not None and torch.device(dev).type == "cuda":
+            self.stream = torch.cuda.Stream(device=dev)
+            self.stream.wait_stream(torch.cuda.current_stream(dev))
         self._cv = threading.Condition()
         self._stop = False
         self._err: Optional[BaseException] = None
@@ -100,7 +110,11 @@ class _EngineLoop:
             if self._stop:
                 return
             try:
-                self.engine.step()
+                if self.stream is not None:
+                    with torch.cuda.stream(self.stream):
+                        self.engine.step()
+                else:
+                    self.engine.step()
             except BaseException as e:  # noqa: BLE001 - surface to waiting callers
                 self._err = e
                 for r in list(self.engine._reqs.values()):

@@ -47,6 +47,9 @@ class Settings:
     dp: int = dataclasses.field(default_factory=lambda: _env("DP", 1, int))
     max_batch: int = dataclasses.field(default_factory=lambda: _env("MAX_BATCH", 32, int))
     max_model_len: int = dataclasses.field(default_factory=lambda: _env("MAX_MODEL_LEN", 4096, int))
+    # share of the free GPU memory each engine's paged KV arena takes when it is built (two co-served
+    # models: the first gets 45 %, the second 45 % of what is left)
+    kv_memory_fraction: float = dataclasses.field(default_factory=lambda: _env("KV_MEMORY_FRACTION", 0.45, float))
     max_new_tokens: int = dataclasses.field(default_factory=lambda: _env("MAX_NEW_TOKENS", 256, int))
     # sampling defaults: greedy (the reference sampled at Ollama defaults; pass options to match)
     temperature: float = dataclasses.field(default_factory=lambda: _env("TEMPERATURE", 0.0, float))

@@ -46,9 +46,10 @@ class SamplingParams:
         if n is None or n < 0:
             n = default_max
         stop = opts.get("stop") or ()
+        # ignore_eos: benchmark extension (fixed-length outputs from random-init weights), not an Ollama option
         return SamplingParams(max_tokens=int(n), temperature=float(opts.get("temperature", 0.0)),
                               top_k=int(opts.get("top_k", 40)), top_p=float(opts.get("top_p", 0.9)),
-                              seed=opts.get("seed"), stop=tuple(stop))
+                              seed=opts.get("seed"), stop=tuple(stop), ignore_eos=bool(opts.get("ignore_eos", False)))
 
 
 @dataclasses.dataclass
@@ -93,6 +94,9 @@ class LLMEngine:
         self.sched = native.Scheduler(runner.num_kv_blocks, BLOCK, runner.max_slots, max_prefill_tokens,
                                       runner.max_blocks)
         self.sync_every = sync_every
+        # decode steps per iteration when every running request ignores EOS: None = run to the first
+        # length limit (offline batches); a server sets a bound so new arrivals are admitted promptly
+        self.run_ahead: Optional[int] = None
         self.max_prefill_tokens = max_prefill_tokens
         self._ids = itertools.count(1)
         self._reqs: dict[int, Request] = {}
@@ -162,10 +166,15 @@ class LLMEngine:
             # sync_every steps between host checks
             reqs = [self._reqs[rid] for rid in running]
             remaining = max(1, min(q.params.max_tokens - q.gen_host for q in reqs))
-            n_steps = remaining if all(q.params.ignore_eos for q in reqs) else min(self.sync_every, remaining)
-            t0 = time.perf_counter()
-            r.decode(B, n_steps, sample)
-            fin, gl, _ = r.read_rows([q.slot for q in reqs])
+            if all(q.params.ignore_eos for q in reqs):
+                n_steps = remaining if self.run_ahead is None else min(self.run_ahead, remaining)
+            else:
+                n_steps = min(self.sync_every, remaining)
+        # the decode run needs no scheduler state: new requests may be added meanwhile
+        t0 = time.perf_counter()
+        r.decode(B, n_steps, sample)
+        fin, gl, _ = r.read_rows([q.slot for q in reqs])
+        with self._lock:
             self.stats["decode_s"] += time.perf_counter() - t0
             self.stats["decode_steps"] += n_steps
             done = []

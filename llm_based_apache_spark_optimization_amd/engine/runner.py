@@ -266,6 +266,23 @@ class ModelRunner:
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graphs[key] = g
 
+    def buckets(self) -> list[int]:
+        out, b = [], 1
+        while b < self.max_slots:
+            out.append(b)
+            b *= 2
+        return out + [self.max_slots]
+
+    def capture_all(self, sample_modes: Sequence[bool] = (False, True)) -> None:
+        """Capture every (bucket, sampling-mode) decode graph up front, so a server never pays a
+        capture inside a request."""
+        if not self.use_graphs:
+            return
+        for b in self.buckets():
+            for sm in sample_modes:
+                self.capture(b, sm)
+        torch.cuda.synchronize(self.device)
+
     def decode(self, B: int, steps: int, sample: bool = False) -> None:
         """Run ``steps`` decode steps over slot rows [0, B) (B a bucket size)."""
         if not self.use_graphs:

@@ -21,8 +21,10 @@ def engine_factory(settings: Settings):
 
         dtype = settings.dtype if model == settings.nl2sql_model else settings.explain_dtype
         log.info("building engine %s (%s, max_batch=%d)", model, dtype, settings.max_batch)
+        # two models co-serve one GPU: each engine's KV arena takes a share of the memory free at its build
         return build_engine(model, checkpoint=settings.checkpoint_dir if model == settings.nl2sql_model else None,
-                            dtype=dtype, max_slots=settings.max_batch, max_model_len=settings.max_model_len)
+                            dtype=dtype, max_slots=settings.max_batch, max_model_len=settings.max_model_len,
+                            kv_memory_fraction=settings.kv_memory_fraction, warm_graphs=True)
 
     return build
 
