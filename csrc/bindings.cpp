@@ -39,6 +39,8 @@ int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, vo
 int lsa_gemm_norm(const void* X, int ldx, int M, int K, const void* Wf, int N, float* out, int nb, int splitk,
                   int waves, int div, int xfrag, float* h, const void* nw, float eps, void* xn, int xf_mt, int* counter,
                   hipStream_t stream);
+int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
+                     int epi, int nb, int splitk, int xfrag, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 }
 
@@ -119,6 +121,27 @@ void gemm_norm(const at::Tensor& x, int64_t M, int64_t K, const at::Tensor& wf, 
                       xfrag ? 1 : 0, h.data_ptr<float>(), nw.data_ptr(), (float)eps, xn.data_ptr(), xf_mt,
                       counter.data_ptr<int>(), cur_stream()),
         "gemm_norm");
+}
+
+// fp8 weights, activations in the fragment-major decode layout (ops.to_xfrag), M <= 64
+void fp8_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wq, const at::Tensor& wscale, int64_t N,
+                 at::Tensor& out, int64_t epi, int64_t nb, int64_t splitk) {
+  need(xf, at::kBFloat16, "xf");
+  need(wscale, at::kFloat, "wscale");
+  TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
+  TORCH_CHECK(M >= 1 && M <= 64 && K % 64 == 0, "fp8_gemm_xf: M in 1..64, K % 64 == 0");
+  const int64_t mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  TORCH_CHECK(xf.is_contiguous() && xf.numel() >= mt * 16 * K, "xf too small");
+  if (epi == 1) {
+    need(out, at::kFloat, "out");
+    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small");
+  } else {
+    need(out, at::kBFloat16, "out");
+    TORCH_CHECK(out.numel() >= (epi == 2 ? mt * 16 * (N / 2) : M * N), "bf16 out too small");
+  }
+  check(lsa_fp8_gemm_cfg(xf.data_ptr(), K, M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(), epi, nb,
+                         splitk, 1, cur_stream()),
+        "fp8_gemm_xf");
 }
 
 void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscale, int64_t N, at::Tensor& out,
@@ -260,6 +283,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4);
   m.def("gemm_norm", &gemm_norm);
   m.def("fp8_gemm", &fp8_gemm);
+  m.def("fp8_gemm_xf", &fp8_gemm_xf);
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
         py::arg("ids"), py::arg("emb"), py::arg("row_idx"), py::arg("write_h"), py::arg("w"), py::arg("eps"),
         py::arg("xn"), py::arg("rows"), py::arg("xf_mt") = 0);

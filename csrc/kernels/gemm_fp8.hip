@@ -27,7 +27,9 @@ __device__ __forceinline__ void fp8x16_to_bf16(const uint4 q, uint4& a, uint4& b
 #define EPI_F32 1
 #define EPI_SILU 2
 
-template <int MT, int NB, int EPI, int WAVES, int U>
+// XF: X in the fragment-major decode layout (common.h xf_off): lane (r, g)'s 16 activations
+// k = 64 kb64 + 16 g .. +15 are the two 16-B pieces (g' = 2 (g & 1), g' + 1) of bf16 k-step 2 kb64 + g / 2
+template <int MT, int NB, int EPI, int WAVES, int U, bool XF = false>
 __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
                                                                      int KB64, const uint4* __restrict__ Wq,
                                                                      const float* __restrict__ wscale,
@@ -56,7 +58,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
   for (int j = 0; j < MT; ++j) {
     const int m = j * 16 + r;
     xvalid[j] = m < M;
-    xp[j] = X + (size_t)(xvalid[j] ? m : 0) * ldx + 16 * g;
+    xp[j] = XF ? X + (((size_t)(g >> 1) * MT + j) * 64 + 32 * (g & 1) + r) * 8
+               : X + (size_t)(xvalid[j] ? m : 0) * ldx + 16 * g;
   }
   const uint4* wp[NB];
 #pragma unroll
@@ -75,9 +78,15 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
       const int kk = min(kb + u, kbB - 1);
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
-        const uint4* px = reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * 64);
-        xr[u][j][0] = px[0];
-        xr[u][j][1] = px[1];
+        if constexpr (XF) {
+          const uint4* px = reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * 2 * MT * 512);
+          xr[u][j][0] = px[0];
+          xr[u][j][1] = px[16];
+        } else {
+          const uint4* px = reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * 64);
+          xr[u][j][0] = px[0];
+          xr[u][j][1] = px[1];
+        }
       }
     }
   };
@@ -152,7 +161,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
         for (int q = 0; q < 4; ++q) v[q] = silu(gs[q] * wscale[nrow_g + q]) * (us[q] * wscale[nrow_u + q]);
         pk.x = pack2bf(v[0], v[1]);
         pk.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + (size_t)m * ldo + n) = pk;
+        // fragment-major in -> fragment-major out (the down projection's input)
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + (XF ? xf_off(m, n, MT) : (size_t)m * ldo + n)) = pk;
       }
     }
   } else {
@@ -209,6 +219,8 @@ __global__ __launch_bounds__(256) void fp8_dequant_kernel(const uint4* __restric
   }
 }
 
+static thread_local int g_fp8_xfrag = 0;
+
 template <int MT, int NB, int EPI>
 static void launch_t(const uint16_t* X, int ldx, int M, int KB64, const uint4* Wq, const float* sc, int NBtot, void* out,
                      int ldo, int splitk, hipStream_t s) {
@@ -216,8 +228,12 @@ static void launch_t(const uint16_t* X, int ldx, int M, int KB64, const uint4* W
   // bf16 sweeps (each fp8 fragment feeds twice the MFMA work of a bf16 one)
   constexpr int U = (4 / NB) < 1 ? 1 : (4 / NB);
   const int kbps = (KB64 + splitk - 1) / splitk;
-  hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, 4, U>), dim3(NBtot / NB, splitk), dim3(256), 0, s, X, ldx, M,
-                     KB64, Wq, sc, out, ldo, kbps);
+  if (g_fp8_xfrag)
+    hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, 4, U, true>), dim3(NBtot / NB, splitk), dim3(256), 0, s, X,
+                       ldx, M, KB64, Wq, sc, out, ldo, kbps);
+  else
+    hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, 4, U, false>), dim3(NBtot / NB, splitk), dim3(256), 0, s,
+                       X, ldx, M, KB64, Wq, sc, out, ldo, kbps);
 }
 
 template <int EPI>
@@ -232,7 +248,10 @@ static void launch_e(const uint16_t* X, int ldx, int M, int KB64, const uint4* W
   LSA_F8(1, 2) LSA_F8(1, 4) LSA_F8(2, 2) LSA_F8(2, 4) LSA_F8(4, 2)
   if constexpr (EPI != EPI_SILU) { LSA_F8(1, 1) LSA_F8(2, 1) LSA_F8(4, 1) }
 #undef LSA_F8
-  launch_t<4, 2, EPI>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, splitk, s);
+  // fallback (unsupported nb): nb = 2 at the same row-tile count
+  if (mt == 1) launch_t<1, 2, EPI>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, splitk, s);
+  else if (mt == 2) launch_t<2, 2, EPI>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, splitk, s);
+  else launch_t<4, 2, EPI>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, splitk, s);
 }
 
 extern "C" int lsa_fp8_dequant(const void* Wq, const float* wscale, int N, int K, void* Wf, hipStream_t s) {
@@ -246,9 +265,20 @@ extern "C" int lsa_fp8_dequant(const void* Wq, const float* wscale, int N, int K
   return (int)hipGetLastError();
 }
 
+extern "C" int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N,
+                                void* out, int epi, int nb, int splitk, int xfrag, hipStream_t stream);
+
 extern "C" int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                             int epi, int nb, int splitk, hipStream_t stream) {
+  return lsa_fp8_gemm_cfg(X, ldx, M, K, Wq, wscale, N, out, epi, nb, splitk, 0, stream);
+}
+
+// xfrag = 1: X in the fragment-major decode layout (M <= 64); a SiLU output is written in it too
+extern "C" int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N,
+                                void* out, int epi, int nb, int splitk, int xfrag, hipStream_t stream) {
   if (K % 64 != 0 || N % 16 != 0 || M <= 0) return -1;
+  if (xfrag && M > 64) return -5;
+  g_fp8_xfrag = xfrag ? 1 : 0;
   const int KB64 = K / 64, NBtot = N / 16;
   const int ldo = (epi == EPI_SILU) ? N / 2 : N;
   if (M <= 64) {

@@ -251,10 +251,10 @@ def from_xfrag(xf: torch.Tensor, M: int, K: int) -> torch.Tensor:
 def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
               splitk: Optional[int] = None, nb: Optional[int] = None, waves: Optional[int] = None,
               div: Optional[int] = None) -> torch.Tensor:
-    """``linear`` with the activations in the fragment-major layout (``to_xfrag``), M <= 64, bf16 weights.
+    """``linear`` with the activations in the fragment-major layout (``to_xfrag``), M <= 64, bf16 or fp8 weights.
     epi='silu' writes its [M, N/2] output in the fragment-major layout too (the next GEMM's input);
     for that epilogue ``out`` is a flat buffer of at least xfrag_tiles(M) * 16 * N/2 elements."""
-    if not _gpu(xf) or w.kind != "bf16":
+    if not _gpu(xf) or w.kind not in ("bf16", "fp8"):
         if epi != "silu":
             return linear(from_xfrag(xf, M, w.K), w, epi, out, splitk, nb, waves, div)
         y = to_xfrag(linear(from_xfrag(xf, M, w.K), w, epi, None, splitk, nb, waves, div))
@@ -274,7 +274,10 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
             out = torch.zeros(xfrag_tiles(M) * 16 * (w.N // 2), device=xf.device, dtype=torch.bfloat16)
         else:
             out = torch.empty(M, w.N, device=xf.device, dtype=torch.bfloat16)
-    ext().gemm_xf(xf, M, w.K, w.data, w.N, out, EPI[epi], nb, splitk, waves, div)
+    if w.kind == "fp8":
+        ext().fp8_gemm_xf(xf, M, w.K, w.data, w.scale, w.N, out, EPI[epi], nb, splitk)
+    else:
+        ext().gemm_xf(xf, M, w.K, w.data, w.N, out, EPI[epi], nb, splitk, waves, div)
     return out
 
 

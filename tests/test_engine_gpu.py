@@ -125,6 +125,19 @@ def test_fp8_engine_runs(gpu):
     assert len(a) == 8 and a[0] == b[0]
 
 
+def test_fp8_engine_batch20_xfrag(gpu):
+    """fp8 weights through the fragment-major decode path (bucket 32) agree with the bf16 engine."""
+    eng = build_engine("tiny-llama3", device=str(gpu), dtype="fp8", max_slots=32, max_model_len=256)
+    assert eng.runner.use_xfrag(32)
+    small = build_engine("tiny-llama3", device=str(gpu), dtype="fp8", max_slots=8, max_model_len=256)
+    assert not small.runner.use_xfrag(8)
+    ps = [[1] + list(range(10 + i, 40 + 2 * i)) for i in range(20)]
+    a = eng.generate(ps, SamplingParams(max_tokens=8, ignore_eos=True))  # one bucket-32 batch: xf kernels
+    b = small.generate(ps, SamplingParams(max_tokens=8, ignore_eos=True))  # 8 at a time: row-major kernels
+    agree = sum(p == q for x, y in zip(a, b) for p, q in zip(x.token_ids, y.token_ids))
+    assert agree >= 0.9 * 160  # same fp8 weights; only split-K summation order differs
+
+
 def test_sampling_engine(gpu):
     eng = build_engine("tiny-nsql", device=str(gpu), max_slots=4, max_model_len=256)
     sp = SamplingParams(max_tokens=16, temperature=0.8, top_k=40, top_p=0.9, seed=7, ignore_eos=True)

@@ -160,7 +160,7 @@ def test_fp8_cvt_matches_torch(gpu):
     assert torch.allclose(y, (x.float() @ deq.t()), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("M", [1, 16, 40, 130])
+@pytest.mark.parametrize("M", [1, 16, 20, 32, 40, 64, 130])
 @pytest.mark.parametrize("epi", ["bf16", "f32", "silu"])
 def test_fp8_gemm(gpu, M, epi):
     N, K = 1024, 4096
@@ -174,6 +174,13 @@ def test_fp8_gemm(gpu, M, epi):
     if epi == "f32":
         y = y.sum(0)
     assert _rel(y, yr) < 1e-2
+    if M <= 64:  # fragment-major activations (the decode path at B > 16)
+        yx = ops.linear_xf(ops.to_xfrag(x), M, pw, epi, splitk=2 if epi == "f32" else 1)
+        if epi == "f32":
+            yx = yx.sum(0)
+        elif epi == "silu":
+            yx = ops.from_xfrag(yx, M, N // 2)
+        assert _rel(yx, yr) < 1e-2
 
 
 # ----------------------------------------------------------------------------------------- norm / rope
