@@ -49,8 +49,10 @@ struct RopeArgs {
   uint16_t* vc;
 };
 
-template <int G, int ROPE>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime slab count
-__global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+// WV = waves per workgroup: 8 for G <= 2 (two keys per lane group per block -> half the K/V registers,
+// so four 4-wave-equivalents fit per CU and a B x Hkv = 1024 grid runs in whole rounds), else 4
+template <int G, int ROPE, int WV>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime slab count
+__global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc,
                                                           const int* __restrict__ block_tables, int max_blocks,
                                                           const int* __restrict__ pos, int Hkv, float scale_log2,
@@ -58,6 +60,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
                                                           float* __restrict__ opart, float* __restrict__ mlpart,
                                                           int* __restrict__ counters, int xf_mt, RopeArgs ra) {
   constexpr int D = 128;
+  constexpr int NT = 64 * WV;      // threads
+  constexpr int NLG = 4 * WV;      // 16-lane groups
+  constexpr int TU = 16 / WV;      // 4-key quads per lane group and block
+  constexpr int TW = 64 / WV;      // keys per wave and block
   // heads fastest: consecutive workgroups (round-robin over the 8 XCDs) are different (b, kv-head) pairs of
   // the same split, so splits a sequence does not need (eff_split) never leave whole XCDs idle
   const int hk = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
@@ -65,6 +71,23 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
   const int tid = threadIdx.x;
   const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(opart, 0, 0x7fffffff, 0x00020000);
   const int lg = tid >> 4, li = tid & 15, wv = tid >> 6;
+  const int* bt = block_tables + (size_t)b * max_blocks;
+  // K/V of block blk+1 are in flight while block blk is scored (two register sets, static names)
+  uint4 kA[TU], vA[TU], kB[TU], vB[TU];
+  // keys past the context in the last block re-read the last valid row (a cache hit, not HBM traffic);
+  // they are masked in the score
+  auto fetch = [&](uint4 (&kr)[TU], uint4 (&vr)[TU], int blk, int last_tok) {
+    const size_t base = ((size_t)bt[blk] * Hkv + hk) * 64 * D;
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int tok = min(wv * TW + u * 4 + (lg & 3), last_tok);
+      kr[u] = *reinterpret_cast<const uint4*>(kc + base + tok * D + li * 8);
+      vr[u] = *reinterpret_cast<const uint4*>(vc + base + tok * D + li * 8);
+    }
+  };
+  // split 0 always starts at block 0, which every sequence owns (padding rows map it to the scratch
+  // block): its first K/V fetch leaves before the context length is even known
+  if (split == 0) fetch(kA, vA, 0, 63);
   const int ctx = pos[b] + 1;
   const int nblk = (ctx + 63) >> 6;
   int ech, nse;
@@ -73,20 +96,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
   const int blk0 = split * ech;
   const int blk1 = min(nblk, blk0 + ech);
 
-  const int* bt = block_tables + (size_t)b * max_blocks;
-  // K/V of block blk+1 are in flight while block blk is scored (two register sets, static names)
-  uint4 kA[4], vA[4], kB[4], vB[4];
-  auto fetch = [&](uint4 (&kr)[4], uint4 (&vr)[4], int blk) {
-    const size_t base = ((size_t)bt[blk] * Hkv + hk) * 64 * D;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int tok = wv * 16 + u * 4 + (lg & 3);
-      kr[u] = *reinterpret_cast<const uint4*>(kc + base + tok * D + li * 8);
-      vr[u] = *reinterpret_cast<const uint4*>(vc + base + tok * D + li * 8);
-    }
-  };
   // the first K/V block is in flight while the query (and, fused, RoPE) is prepared
-  if (blk0 < blk1) fetch(kA, vA, blk0);
+  if (split != 0 && blk0 < blk1) fetch(kA, vA, blk0, ctx - 1 - blk0 * 64);
   __builtin_amdgcn_sched_barrier(0);
 
   const int tpos = ctx - 1;  // position of the new token
@@ -95,8 +106,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
   if constexpr (ROPE != 0) {
     // lane group j < G builds query head j, group G the new key, group G + 1 the new value (each lane
     // 8 dims, summed over the split-K slabs, rotated in f32, rounded to bf16 like the unfused path);
-    // the results go through LDS to all 16 lane groups
-    static_assert(G + 2 <= 16, "fused rope: one lane group per q head + k + v");
+    // the results go through LDS to all lane groups
+    static_assert(G + 2 <= NLG, "fused rope: one lane group per q head + k + v");
     __shared__ __attribute__((aligned(16))) float qkv_s[G + 2][D];
     if (lg < G + 2) {
       const float* row = ra.parts + (size_t)b * (H + 2 * Hkv) * D;
@@ -169,13 +180,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
     for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
   }
 
-  auto score = [&](const uint4 (&kr)[4], const uint4 (&vr)[4], int blk) {
-    float s[4][G];
+  auto score = [&](const uint4 (&kr)[TU], const uint4 (&vr)[TU], int blk) {
+    float s[TU][G];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < TU; ++u) {
       float kf[8];
       unpack8(kr[u], kf);
-      const int tp = blk * 64 + wv * 16 + u * 4 + (lg & 3);
+      const int tp = blk * 64 + wv * TW + u * 4 + (lg & 3);
       const bool valid = tp < ctx;
       if constexpr (ROPE != 0) {
         if (tp == tpos) {
@@ -197,22 +208,27 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const float mx = fmaxf(fmaxf(s[0][g], s[1][g]), fmaxf(s[2][g], s[3][g]));
+      float mx = s[0][g];
+#pragma unroll
+      for (int u = 1; u < TU; ++u) mx = fmaxf(mx, s[u][g]);
       const float mn = fmaxf(m[g], mx);
       const float alpha = exp2f(m[g] - mn);
       m[g] = mn;
-      float p[4];
+      float p[TU], ps = 0.f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) p[u] = exp2f(s[u][g] - mn);
-      l[g] = l[g] * alpha + (p[0] + p[1]) + (p[2] + p[3]);
+      for (int u = 0; u < TU; ++u) {
+        p[u] = exp2f(s[u][g] - mn);
+        ps += p[u];
+      }
+      l[g] = l[g] * alpha + ps;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[g][j] *= alpha;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < TU; ++u) {
         float vf[8];
         unpack8(vr[u], vf);
         if constexpr (ROPE != 0) {
-          if (blk * 64 + wv * 16 + u * 4 + (lg & 3) == tpos) {
+          if (blk * 64 + wv * TW + u * 4 + (lg & 3) == tpos) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) vf[j] = vnew[j];
           }
@@ -225,11 +241,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
   if (blk0 < blk1) {
     int blk = blk0;
     for (; blk + 1 < blk1; blk += 2) {
-      fetch(kB, vB, blk + 1);
+      fetch(kB, vB, blk + 1, ctx - 1 - (blk + 1) * 64);
       __builtin_amdgcn_sched_barrier(0);
       score(kA, vA, blk);
       __builtin_amdgcn_sched_barrier(0);
-      fetch(kA, vA, min(blk + 2, blk1 - 1));
+      fetch(kA, vA, min(blk + 2, blk1 - 1), ctx - 1 - min(blk + 2, blk1 - 1) * 64);
       __builtin_amdgcn_sched_barrier(0);
       score(kB, vB, blk + 1);
       __builtin_amdgcn_sched_barrier(0);
@@ -237,9 +253,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
     if (blk < blk1) score(kA, vA, blk);
   }
 
-  // merge the 16 lane groups
-  __shared__ float sm[16][G], sl[16][G];
-  __shared__ __attribute__((aligned(16))) float so[16][G][D];
+  // merge the lane groups
+  __shared__ float sm[NLG][G], sl[NLG][G];
+  __shared__ __attribute__((aligned(16))) float so[NLG][G][D];
   if (li == 0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -254,14 +270,14 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
   }
   __syncthreads();
   // each thread finishes 4 consecutive dims of one head
-  for (int e = tid; e < G * 32; e += 256) {
+  for (int e = tid; e < G * 32; e += NT) {
     const int g = e >> 5, d0 = (e & 31) * 4;
     float M = LSA_NEG;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) M = fmaxf(M, sm[k][g]);
+    for (int k = 0; k < NLG; ++k) M = fmaxf(M, sm[k][g]);
     float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < NLG; ++k) {
       const float wgt = exp2f(sm[k][g] - M);
       L += sl[k][g] * wgt;
       const float4 v = *reinterpret_cast<const float4*>(&so[k][g][d0]);
@@ -301,7 +317,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
   if (tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float* cm = &so[0][0][0];          // [G][256] split maxima, then weights
   float* cl = cm + G * 256;          // [G][256] split sums
-  for (int i = tid; i < G * nse; i += 256) {
+  for (int i = tid; i < G * nse; i += NT) {
     const int g = i / nse, sp = i - g * nse;
     const size_t pi = ((size_t)b * H + hk * G + g) * nsplit + sp;
     const unsigned long long ml =
@@ -310,7 +326,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const uint16_t* __rest
     cl[g * 256 + sp] = __uint_as_float((uint32_t)(ml >> 32));
   }
   __syncthreads();
-  for (int e = tid; e < G * 32; e += 256) {
+  for (int e = tid; e < G * 32; e += NT) {
     const int g = e >> 5, d0 = (e & 31) * 4;
     float M = LSA_NEG;
     for (int sp = 0; sp < nse; ++sp) M = fmaxf(M, cm[g * 256 + sp]);
@@ -351,8 +367,9 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
   const RopeArgs ra{qkv_parts, (size_t)part_stride, nparts, cos_t, sin_t, const_cast<uint16_t*>(kk),
                     const_cast<uint16_t*>(vv)};
 #define LSA_ADK(GV, RP)                                                                                      \
-  hipLaunchKernelGGL((attn_decode_kernel<GV, RP>), grid, dim3(256), 0, s, qq, kk, vv, block_tables, max_blocks, pos, \
-                     Hkv, sl2, chunk_blocks, nsplit, oo, opart, mlpart, counters, xf_mt, ra)
+  hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 2 ? 8 : 4)>), grid, dim3(GV <= 2 ? 512 : 256), 0, s, qq, kk, \
+                     vv, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, oo, opart, mlpart, counters,  \
+                     xf_mt, ra)
 #define LSA_AD(GV)                                  \
   case GV:                                          \
     if (!qkv_parts) LSA_ADK(GV, 0);                 \
