@@ -41,6 +41,7 @@ int lsa_gemm_norm(const void* X, int ldx, int M, int K, const void* Wf, int N, f
                   hipStream_t stream);
 int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
+int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 }
 
@@ -142,6 +143,24 @@ void fp8_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& w
   check(lsa_fp8_gemm_cfg(xf.data_ptr(), K, M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(), epi, nb,
                          splitk, 1, cur_stream()),
         "fp8_gemm_xf");
+}
+
+// large-M (prefill) linear layer on the 256x256 tile kernel (kernels/gemm_tile256.hip)
+void gemm_t256(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi) {
+  need(x, at::kBFloat16, "x");
+  need(wf, at::kBFloat16, "wf");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(wf.numel() == N * K, "weight numel mismatch");
+  if (epi == 1) {
+    need(out, at::kFloat, "out");
+    TORCH_CHECK(out.numel() >= M * N, "f32 out too small");
+  } else {
+    need(out, at::kBFloat16, "out");
+    TORCH_CHECK(out.numel() >= M * (epi == 2 ? N / 2 : N), "bf16 out too small");
+  }
+  check(lsa_gemm_t256(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, cur_stream()),
+        "gemm_t256");
 }
 
 void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscale, int64_t N, at::Tensor& out,
@@ -282,6 +301,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_xf", &gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wf"), py::arg("N"), py::arg("out"),
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4);
   m.def("gemm_norm", &gemm_norm);
+  m.def("gemm_t256", &gemm_t256);
   m.def("fp8_gemm", &fp8_gemm);
   m.def("fp8_gemm_xf", &fp8_gemm_xf);
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),

@@ -13,8 +13,9 @@
 //     'GEMV / M <= 16 decode weights' row of the guide), non-temporal weight loads, cross-wave
 //     reduction through LDS, fused epilogues (bf16 store, f32 split-K slab for the following
 //     residual+RMSNorm kernel, SiLU(gate)*up for the interleaved gate_up projection).
-//   * gemm_tile    — prefill (M > 64).  128x128x64 LDS tile, both operands staged by
-//     global_load_lds (16 B), double-buffered, 4 waves of 64x64.
+//   * gemm_tile    — prefill (M > 64) when the 256^2 kernel (gemm_tile256.hip) would under-fill the
+//     chip.  128x128x64 LDS tile, both operands staged by global_load_lds (16 B), double-buffered,
+//     4 waves of 64x64.
 //
 // Epilogue modes: EPI_BF16 -> bf16 [M, N];  EPI_F32 -> f32 [splitk][M][N];
 //                 EPI_F32N -> f32 slabs, then the last workgroups to finish run the residual add +
@@ -583,6 +584,8 @@ static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uin
 
 extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
                             int splitk, int waves, int div, int xlds, hipStream_t stream);
+extern "C" int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi,
+                             hipStream_t stream);
 
 extern "C" int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
                         int splitk, hipStream_t stream) {
@@ -642,6 +645,10 @@ extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf
     }
   } else {
     if (splitk != 1 || epi == EPI_F32N) return -3;
+    // the 256^2 8-phase kernel (gemm_tile256.hip) once its grid fills half the CUs; measured 1.2-1.34 PF
+    // vs 0.73-0.86 PF for the 128^2 tile at the 7B/3B prefill shapes (scripts/bench_prefill_gemm.py)
+    if (((M + 255) / 256) * ((NBtot + 15) / 16) >= 128 && (epi != EPI_SILU || NBtot % 2 == 0))
+      return lsa_gemm_t256(X, ldx, M, K, Wf, N, out, epi, stream);
     dim3 grid((NBtot + 7) / 8, (M + 127) / 128);
     switch (epi) {
       case EPI_BF16:

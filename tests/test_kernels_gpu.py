@@ -136,6 +136,26 @@ def test_gemm_tile(gpu, M, NK, epi):
         assert _rel(y, yr) < 1e-2
 
 
+@pytest.mark.parametrize("M", [65, 256, 300, 777])
+@pytest.mark.parametrize("NK", [(800, 4096), (1024, 1376), (4096, 512), (256, 96)])
+@pytest.mark.parametrize("epi", ["bf16", "f32", "silu"])
+def test_gemm_tile256(gpu, M, NK, epi):
+    """256^2 8-phase prefill kernel: M / N edges, odd K/32 (1376 -> 43 k-steps), every epilogue."""
+    N, K = NK
+    torch.manual_seed(M + N + K)
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    ncol = N // 2 if epi == "silu" else N
+    out = torch.empty(M, ncol, device=gpu, dtype=torch.float32 if epi == "f32" else torch.bfloat16)
+    ops.ext().gemm_t256(x, pw.data, N, out, ops.EPI[epi])
+    yr = x.float() @ w.float().t()
+    if epi == "silu":
+        r3 = yr.view(M, N // 32, 2, 16)
+        yr = (torch.nn.functional.silu(r3[:, :, 0]) * r3[:, :, 1]).reshape(M, N // 2)
+    assert _rel(out, yr) < (1e-5 if epi == "f32" else 1e-2)
+
+
 def test_gemm_asymmetric_exact(gpu):
     """Small-integer operands: the result is exact, so any lane/row/col map error shows up."""
     M, N, K = 7, 48, 64
