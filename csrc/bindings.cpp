@@ -36,9 +36,6 @@ int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq, const flo
 int lsa_fp8_dequant(const void* Wq, const float* wscale, int N, int K, void* Wf, hipStream_t s);
 int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
                  int waves, int div, int xlds, hipStream_t stream);
-int lsa_gemm_norm(const void* X, int ldx, int M, int K, const void* Wf, int N, float* out, int nb, int splitk,
-                  int waves, int div, int xfrag, float* h, const void* nw, float eps, void* xn, int xf_mt, int* counter,
-                  hipStream_t stream);
 int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
 int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, hipStream_t stream);
@@ -102,27 +99,6 @@ void gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wf, i
         "gemm_xf");
 }
 
-// f32 split-K GEMM whose last workgroups apply h += sum(slabs); xn = rmsnorm(h) * nw (decode, M <= 64).
-// x is row-major [M, K] (xfrag = 0) or fragment-major (xfrag = 1); xn is written fragment-major when
-// xf_mt > 0.  counter: 2 int32 zeros owned by the call site (left zeroed by the kernel).
-void gemm_norm(const at::Tensor& x, int64_t M, int64_t K, const at::Tensor& wf, int64_t N, at::Tensor& out,
-               int64_t nb, int64_t splitk, int64_t waves, int64_t div, bool xfrag, at::Tensor& h, const at::Tensor& nw,
-               double eps, at::Tensor& xn, int64_t xf_mt, at::Tensor& counter) {
-  need(x, at::kBFloat16, "x");
-  need(wf, at::kBFloat16, "wf");
-  need(out, at::kFloat, "out");
-  need(h, at::kFloat, "h");
-  need(nw, at::kBFloat16, "nw");
-  need(xn, at::kBFloat16, "xn");
-  need(counter, at::kInt, "counter");
-  TORCH_CHECK(M >= 1 && M <= 64 && K % 32 == 0 && nw.numel() == N, "gemm_norm: bad shapes");
-  TORCH_CHECK(wf.numel() == N * K && out.numel() >= splitk * M * N && h.numel() >= M * N, "gemm_norm: sizes");
-  TORCH_CHECK(x.is_contiguous() && x.numel() >= M * K, "gemm_norm: x");
-  check(lsa_gemm_norm(x.data_ptr(), K, M, K, wf.data_ptr(), N, out.data_ptr<float>(), nb, splitk, waves, div,
-                      xfrag ? 1 : 0, h.data_ptr<float>(), nw.data_ptr(), (float)eps, xn.data_ptr(), xf_mt,
-                      counter.data_ptr<int>(), cur_stream()),
-        "gemm_norm");
-}
 
 // fp8 weights, activations in the fragment-major decode layout (ops.to_xfrag), M <= 64
 void fp8_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wq, const at::Tensor& wscale, int64_t N,
@@ -300,7 +276,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4, py::arg("xlds") = 0);
   m.def("gemm_xf", &gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wf"), py::arg("N"), py::arg("out"),
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4);
-  m.def("gemm_norm", &gemm_norm);
   m.def("gemm_t256", &gemm_t256);
   m.def("fp8_gemm", &fp8_gemm);
   m.def("fp8_gemm_xf", &fp8_gemm_xf);

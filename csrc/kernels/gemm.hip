@@ -18,41 +18,21 @@
 //     4 waves of 64x64.
 //
 // Epilogue modes: EPI_BF16 -> bf16 [M, N];  EPI_F32 -> f32 [splitk][M][N];
-//                 EPI_F32N -> f32 slabs, then the last workgroups to finish run the residual add +
-//                 RMSNorm of the following layer step (h += sum slabs; xn = rmsnorm(h) * w), which
-//                 removes a kernel launch (~4 us of fixed cost at decode sizes) per projection;
 //                 EPI_SILU -> bf16 [M, N/2] = silu(gate) * up, gate/up rows interleaved per 16.
 #include "common.h"
 
 #define EPI_BF16 0
 #define EPI_F32 1
 #define EPI_SILU 2
-#define EPI_F32N 3
 #ifndef LSA_XSAME
 #define LSA_XSAME 0  // experiment knob (LSA_HIP_EXTRA=-DLSA_XSAME=1): every k-step reads the same 2 activation
                      // fragments (L1-resident) -> upper bound of removing activation traffic
 #endif
 
-// Fused residual + RMSNorm tail of an EPI_F32N GEMM (see fused_norm_tail).
-struct NormArgs {
-  float* h;              // [M][N] residual stream (f32), updated in place
-  const uint16_t* w;     // [N] norm weight (bf16)
-  uint16_t* xn;          // normalised output: [M][N] row-major, or fragment-major when xf_mt > 0
-  int* counter;          // 2 ints, zero at launch; restored to zero by the kernel
-  float eps;
-  int xf_mt;
-  int R;                 // workgroups that run the norm (<= M): role r handles rows r, r + R, ...
-};
 
 template <int EPI>
 __device__ __forceinline__ void store4(void* out, int ldo, size_t slab, int m, int n, f32x4_t v) {
-  if constexpr (EPI == EPI_F32N) {
-    // agent-scope stores (write through the XCD-private L2) so the norm workers on other XCDs can read
-    // them after the ticket count, with no L2 writeback/invalidate fences
-    float* o = reinterpret_cast<float*>(out) + slab + (size_t)m * ldo + n;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) __hip_atomic_store(o + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if constexpr (EPI == EPI_F32) {
+  if constexpr (EPI == EPI_F32) {
     float* o = reinterpret_cast<float*>(out) + slab + (size_t)m * ldo + n;
     *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
   } else {
@@ -64,83 +44,6 @@ __device__ __forceinline__ void store4(void* out, int ldo, size_t slab, int m, i
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Fused residual + RMSNorm after an f32 split-K GEMM.
-//
-// The slabs were stored with agent-scope (L2 write-through) stores; every workgroup waits for its stores
-// to be acknowledged (vmcnt(0), a workgroup-scope release: no L2 writeback/invalidate, which would cost
-// every other running workgroup its cached activations) and takes a ticket.  The last R ticket holders are the norm workers: each waits until all
-// tickets are taken (every slab is globally visible), then normalises rows role, role + R, ...  The
-// workers were the last to arrive, so every other workgroup has already been dispatched and the spin
-// cannot starve one of them.  The final worker restores the counters for the next launch / graph replay.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void fused_norm_tail(const NormArgs& na, const float* __restrict__ parts, size_t part_stride,
-                                             int nparts, int M, int D) {
-  __shared__ int s_ticket;
-  __shared__ float red[16];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __syncthreads();
-  const int total = gridDim.x * gridDim.y;
-  if (threadIdx.x == 0) s_ticket = atomicAdd(na.counter, 1);
-  __syncthreads();
-  const int R = min(na.R, total);
-  const int role = s_ticket - (total - R);
-  if (role < 0) return;
-  if (threadIdx.x == 0) {
-    while (__hip_atomic_load(na.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < total)
-      __builtin_amdgcn_s_sleep(1);
-  }
-  __syncthreads();
-  // one agent-scope acquire (L2 invalidate of this XCD) after the count: every GEMM workgroup is done,
-  // so nothing useful is evicted, and the slab reads below can be plain vector loads
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int nt = blockDim.x;
-  for (int m = role; m < M; m += R) {
-    float* hr = na.h + (size_t)m * D;
-    float ss = 0.f;
-    float v[2][8];  // D <= 16 * nt
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int c = (threadIdx.x + q * nt) * 8;
-      if (c < D) {
-        const float4 a0 = *reinterpret_cast<const float4*>(hr + c);
-        const float4 a1 = *reinterpret_cast<const float4*>(hr + c + 4);
-        v[q][0] = a0.x; v[q][1] = a0.y; v[q][2] = a0.z; v[q][3] = a0.w;
-        v[q][4] = a1.x; v[q][5] = a1.y; v[q][6] = a1.z; v[q][7] = a1.w;
-        for (int s = 0; s < nparts; ++s) {
-          const float* p = parts + s * part_stride + (size_t)m * D + c;
-          const float4 b0 = *reinterpret_cast<const float4*>(p);
-          const float4 b1 = *reinterpret_cast<const float4*>(p + 4);
-          v[q][0] += b0.x; v[q][1] += b0.y; v[q][2] += b0.z; v[q][3] += b0.w;
-          v[q][4] += b1.x; v[q][5] += b1.y; v[q][6] += b1.z; v[q][7] += b1.w;
-        }
-        *reinterpret_cast<float4*>(hr + c) = make_float4(v[q][0], v[q][1], v[q][2], v[q][3]);
-        *reinterpret_cast<float4*>(hr + c + 4) = make_float4(v[q][4], v[q][5], v[q][6], v[q][7]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ss += v[q][j] * v[q][j];
-      }
-    }
-    const float inv = rsqrtf(block_sum(ss, red) / (float)D + na.eps);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int c = (threadIdx.x + q * nt) * 8;
-      if (c < D) {
-        float wf[8], o[8];
-        unpack8(*reinterpret_cast<const uint4*>(na.w + c), wf);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = v[q][j] * inv * wf[j];
-        *reinterpret_cast<uint4*>(na.xn + (na.xf_mt ? xf_off(m, c, na.xf_mt) : (size_t)m * D + c)) = pack8(o);
-      }
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (atomicAdd(na.counter + 1, 1) == R - 1) {
-      atomicExch(na.counter, 0);
-      atomicExch(na.counter + 1, 0);
-    }
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
 // decode / small-M kernel
@@ -165,7 +68,7 @@ template <int MT, int NB, int EPI, int WAVES, int DIV = 1, bool XF = false>
 __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
                                                                  int KB, const uint4* __restrict__ Wf,
                                                                  void* __restrict__ out, int ldo,
-                                                                 int kb_per_split, NormArgs na) {
+                                                                 int kb_per_split) {
   constexpr int U = SkinnyCfg<MT, NB, DIV>::U;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -196,7 +99,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 #pragma unroll
   for (int i = 0; i < NB; ++i) wp[i] = Wf + (size_t)(nb0 + i) * KB * 64 + lane;
 
-  auto load = [&](uint4 (&wr)[U][NB], uint4 (&xr)[U][MT], int c) {
+  auto wload = [&](uint4 (&wr)[U][NB], int c) {
     const int kb = kbA + c * U;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -204,6 +107,9 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 #pragma unroll
       for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
     }
+  };
+  auto xload = [&](uint4 (&xr)[U][MT], int c) {
+    const int kb = kbA + c * U;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kk = min(kb + u, kbB - 1);
@@ -211,6 +117,10 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       for (int j = 0; j < MT; ++j)
         xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)(LSA_XSAME ? (kk & 1) : kk) * (XF ? MT * 512 : 32));
     }
+  };
+  auto load = [&](uint4 (&wr)[U][NB], uint4 (&xr)[U][MT], int c) {
+    wload(wr, c);
+    xload(xr, c);
   };
   auto comp = [&](const uint4 (&wr)[U][NB], const uint4 (&xr)[U][MT], int c) {
     const int kb = kbA + c * U;
@@ -294,8 +204,6 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       const int m = j * 16 + (l & 15);
       if (m < M) store4<EPI>(out, ldo, slab, m, (nb0 + i) * 16 + 4 * (l >> 4), s);
     }
-    if constexpr (EPI == EPI_F32N)
-      fused_norm_tail(na, reinterpret_cast<const float*>(out), (size_t)M * ldo, gridDim.y, M, ldo);
   }
 }
 
@@ -527,7 +435,6 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restri
 //   waves 4|8 per workgroup; div 1|2|4 divides the chunk depth U (fewer VGPRs -> more resident waves;
 //   on MI355X div 4 won most decode shapes, scripts/bench_gemm.py).
 static thread_local int g_skinny_waves = 4;
-static thread_local NormArgs g_norm = {};
 static thread_local int g_skinny_div = 4;
 
 template <int MT, int NB, int EPI, bool XF>
@@ -536,8 +443,8 @@ static void launch_skinny_x(const uint16_t* X, int ldx, int M, int KB, const uin
   const int kbps = (KB + splitk - 1) / splitk;
   dim3 grid(NBtot / NB, splitk);
 #define LSA_SKL(WV, DV) \
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF>), grid, dim3(64 * WV), 0, s, X, ldx, M, KB, Wf, out, \
-                     ldo, kbps, g_norm)
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF>), grid, dim3(64 * WV), 0, s, X, ldx, M, KB, Wf, \
+                     out, ldo, kbps)
   if (g_skinny_div == 2) {
     if (g_skinny_waves == 8) LSA_SKL(8, 2);
     else LSA_SKL(4, 2);
@@ -634,17 +541,16 @@ extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf
     if (epi == EPI_SILU && nb < 2) nb = 2;
     if (NBtot % nb != 0) return -2;
     if (splitk < 1) splitk = 1;
-    if (epi != EPI_F32 && epi != EPI_F32N && splitk != 1) return -3;
+    if (epi != EPI_F32 && splitk != 1) return -3;
     if (M > 32 && nb > 2) nb = 2;
     switch (epi) {
       case EPI_BF16: launch_skinny_e<EPI_BF16>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
       case EPI_F32: launch_skinny_e<EPI_F32>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
-      case EPI_F32N: launch_skinny_e<EPI_F32N>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
       case EPI_SILU: launch_skinny_e<EPI_SILU>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
       default: return -4;
     }
   } else {
-    if (splitk != 1 || epi == EPI_F32N) return -3;
+    if (splitk != 1) return -3;
     // the 256^2 8-phase kernel (gemm_tile256.hip) once its grid fills half the CUs; measured 1.2-1.34 PF
     // vs 0.73-0.86 PF for the 128^2 tile at the 7B/3B prefill shapes (scripts/bench_prefill_gemm.py)
     if (((M + 255) / 256) * ((NBtot + 15) / 16) >= 128 && (epi != EPI_SILU || NBtot % 2 == 0))
@@ -664,21 +570,4 @@ extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf
     }
   }
   return (int)hipGetLastError();
-}
-
-// f32 split-K GEMM + fused residual/RMSNorm (EPI_F32N); counter: 2 zeroed ints owned by this call site
-extern "C" int lsa_gemm_norm(const void* X, int ldx, int M, int K, const void* Wf, int N, float* out, int nb,
-                             int splitk, int waves, int div, int xfrag, float* h, const void* nw, float eps, void* xn,
-                             int xf_mt, int* counter, hipStream_t stream) {
-  if (M > 64 || N > 16 * 64 * (waves == 8 ? 8 : 4) || N % 8) return -7;
-  g_norm.h = h;
-  g_norm.w = reinterpret_cast<const uint16_t*>(nw);
-  g_norm.xn = reinterpret_cast<uint16_t*>(xn);
-  g_norm.counter = counter;
-  g_norm.eps = eps;
-  g_norm.xf_mt = xf_mt;
-  g_norm.R = M;
-  const int rc = lsa_gemm_cfg(X, ldx, M, K, Wf, N, out, EPI_F32N, nb, splitk, waves, div, xfrag ? 2 : 0, stream);
-  g_norm = NormArgs{};
-  return rc;
 }

@@ -38,9 +38,8 @@ class ModelRunner:
     def __init__(self, weights: LlamaWeights, max_slots: int = 32, max_model_len: int = 4096,
                  num_kv_blocks: Optional[int] = None, kv_memory_fraction: float = 0.85,
                  max_new_cap: Optional[int] = None, tp=None, use_graphs: bool = True, steps_per_graph: int = 1,
-                 fuse_norm: bool = False, fuse_rope: Optional[bool] = None):
+                 fuse_rope: Optional[bool] = None):
         self.w = weights
-        self._fuse_norm = fuse_norm
         # decode RoPE + KV append inside the attention kernel (LSA_FUSE_ROPE=0 restores the separate launch)
         self.fuse_rope = (os.environ.get("LSA_FUSE_ROPE", "1") != "0") if fuse_rope is None else fuse_rope
         self.spec = spec = weights.spec
@@ -116,8 +115,6 @@ class ModelRunner:
         self.xn_f = torch.zeros(xr * self.d, **bf)
         self.attn_f = torch.zeros(xr * self.H * self.D, **bf)
         self.act_f = torch.zeros(xr * self.ffn_l, **bf)
-        # per-call-site counters of the GEMM + fused residual/RMSNorm kernels (left zeroed by them)
-        self.norm_ctr = torch.zeros(2 * self.L, 2, dtype=torch.int32, device=dev)
         self.o_buf = torch.zeros(8 * S * self.d, **f32)
         self.down_buf = torch.zeros(8 * S * self.d, **f32)
         self.qkv_buf = torch.zeros(8 * S * (self.H + 2 * self.Hkv) * self.D, **f32)
@@ -140,15 +137,6 @@ class ModelRunner:
             return 1
         return ops.pick_gemm_config(M, N or self.d, K, "f32", xf=xf)[1]
 
-    @property
-    def fuse_norm(self) -> bool:
-        """Decode O/down GEMMs run the next residual+RMSNorm in-kernel (bf16 weights, no TP all-reduce).
-        Off by default: on MI355X the cross-XCD completion protocol (a ticket atomic per workgroup on one
-        counter + the workers' L2 invalidate) measured 3-13 us slower than a separate ~3.5 us norm launch
-        (scripts/bench_fuse.py, profiles/fuse_norm_mi355x.txt)."""
-        return (self._fuse_norm and self.on_gpu and self.w.layers[0].wo.kind == "bf16"
-                and (self.tp is None or self.tp.size == 1))
-
     def use_xfrag(self, B: int) -> bool:
         """Fragment-major activations pay off once a decode batch spans >1 row tile (B > 16):
         measured 8-20 % faster GEMMs at B = 32 (scripts/bench_xf.py); bf16 and fp8 weights."""
@@ -162,6 +150,10 @@ class ModelRunner:
             ops.linear_xf(xn, M, self.w.lm_head, "f32", out=loc, splitk=1)
         else:
             ops.linear(xn, self.w.lm_head, "f32", out=loc, splitk=1)
+        return self._gather_logits(loc, M)
+
+    def _gather_logits(self, loc: torch.Tensor, M: int) -> torch.Tensor:
+        """vocab-parallel logits -> full [M, V] (all-gather over the TP group)."""
         if self.tp is None or self.tp.size == 1:
             return loc
         tps = self.tp.size
@@ -196,14 +188,10 @@ class ModelRunner:
         else:
             xn, attn, act = self.xn[:B], self.attn[:B], self.act[:B]
             lin = ops.linear
-        # O / down projections carry the following residual add + RMSNorm in their last workgroups
-        # (one launch instead of two) unless a TP all-reduce has to sit between them
-        fuse = self.fuse_norm
-        L = len(w.layers)
         for l, lw in enumerate(w.layers):
             if l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf)
-            elif not fuse:
+            else:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
             # QKV as f32 split-K slabs; the attention kernel sums them, applies RoPE and appends the new
             # token's k/v to the paged cache itself (no separate rope/append launch)
@@ -216,23 +204,13 @@ class ModelRunner:
                             attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
                             qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
                             sin=self.sin if fr else None)
-            if fuse:
-                ops.linear_norm(attn, B, lw.wo, o_parts, h, lw.mlp_norm, self.eps, xn, self.norm_ctr[2 * l],
-                                x_frag=xf, xn_frag=xf, splitk=sk_o)
-            else:
-                lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
-                self._allreduce(o_parts)
-                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts, rows=B, xf=xf)
+            lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
+            self._allreduce(o_parts)
+            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts, rows=B, xf=xf)
             lin(xn, lw.w_gate_up, "silu", out=act)
-            if fuse:
-                nxt = w.layers[l + 1].attn_norm if l + 1 < L else w.final_norm
-                ops.linear_norm(act, B, lw.w_down, d_parts, h, nxt, self.eps, xn, self.norm_ctr[2 * l + 1],
-                                x_frag=xf, xn_frag=xf, splitk=sk_d)
-            else:
-                lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
-                self._allreduce(d_parts)
-        if not fuse:
-            ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
+            lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
+            self._allreduce(d_parts)
+        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
         logits = self._lm_head(xn, B, xf)
         st = (self.out_tokens[:B], self.gen_len[:B], self.input_ids[:B], self.positions[:B], self.finished[:B])
         if sample:

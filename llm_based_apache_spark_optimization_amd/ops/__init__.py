@@ -281,28 +281,6 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
     return out
 
 
-def linear_norm(x: torch.Tensor, M: int, w: PackedWeight, out: torch.Tensor, h: torch.Tensor,
-                norm_w: torch.Tensor, eps: float, xn: torch.Tensor, counter: torch.Tensor, x_frag: bool = False,
-                xn_frag: bool = False, splitk: Optional[int] = None, nb: Optional[int] = None,
-                waves: Optional[int] = None, div: Optional[int] = None) -> torch.Tensor:
-    """Decode projection + the next residual/RMSNorm in one kernel (M <= 64, bf16 weights):
-    out = f32 split-K slabs of x @ W^T;  h[:M] += sum(out);  xn = rmsnorm(h[:M]) * norm_w.
-    x is fragment-major when x_frag; xn is written fragment-major when xn_frag.  ``counter`` is a
-    2-int32 zero tensor owned by the call site (the kernel leaves it zeroed)."""
-    if not _gpu(h) or w.kind != "bf16":
-        xr = from_xfrag(x, M, w.K) if x_frag else x[:M]
-        parts = linear(xr, w, "f32", None, splitk, nb, waves, div)
-        return add_rmsnorm(h, norm_w, eps, xn, parts=parts, rows=M, xf=xn_frag)
-    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, w.K, "f32", xf=x_frag)
-    nb = nb0 if nb is None else nb
-    splitk = sk0 if splitk is None else splitk
-    waves = wv0 if waves is None else waves
-    div = dv0 if div is None else div
-    ext().gemm_norm(x, M, w.K, w.data, w.N, out, nb, splitk, waves, div, x_frag, h, norm_w, eps, xn,
-                    xfrag_tiles(M) if xn_frag else 0, counter)
-    return xn
-
-
 # ----------------------------------------------------------------------------------- norms / rope
 def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
                 parts: Optional[torch.Tensor] = None, ids: Optional[torch.Tensor] = None,

@@ -234,38 +234,6 @@ def test_add_rmsnorm(gpu, D):
     assert _rel(xs, ref_xs) < 1e-2
 
 
-@pytest.mark.parametrize("M", [1, 4, 20, 32, 64])
-@pytest.mark.parametrize("frag", [False, True])
-@pytest.mark.parametrize("splitk", [1, 4])
-@pytest.mark.parametrize("N", [4096, 256])
-def test_gemm_fused_norm(gpu, M, frag, splitk, N):
-    """GEMM -> f32 slabs -> (last workgroups) residual add + RMSNorm == GEMM then add_rmsnorm.
-    N = 256 gives fewer workgroups than rows (every workgroup then normalises several rows)."""
-    K = 2048
-    torch.manual_seed(M + splitk)
-    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
-    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
-    pw = ops.PackedWeight.from_dense(w)
-    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(torch.bfloat16)
-    h = torch.randn(M, N, device=gpu)
-    h_ref = h.clone()
-    parts_ref = ops.linear(x, pw, "f32", splitk=splitk)
-    xn_ref = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
-    ops.add_rmsnorm(h_ref, nw, 1e-5, xn_ref, parts=parts_ref)
-    counter = torch.zeros(2, device=gpu, dtype=torch.int32)
-    out = torch.empty(splitk, M, N, device=gpu)
-    xin = ops.to_xfrag(x) if frag else x
-    xn = torch.zeros(ops.xfrag_tiles(M) * 16 * N if frag else M * N, device=gpu, dtype=torch.bfloat16)
-    for _ in range(3):  # repeated launches: the counter must come back to zero every time
-        hh = h.clone()
-        ops.linear_norm(xin, M, pw, out, hh, nw, 1e-5, xn, counter, x_frag=frag, xn_frag=frag, splitk=splitk)
-        torch.cuda.synchronize()
-        assert counter.tolist() == [0, 0]
-        assert torch.allclose(hh, h_ref, atol=1e-4, rtol=1e-5)
-        got = ops.from_xfrag(xn, M, N) if frag else xn.view(M, N)
-        assert _rel(got, xn_ref) < 1e-2
-
-
 @pytest.mark.parametrize("rows", [3, 20, 33])
 def test_add_rmsnorm_xfrag(gpu, rows):
     """Fragment-major output of the norm (decode GEMM input) == to_xfrag of the row-major output."""
