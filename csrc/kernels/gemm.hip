@@ -443,8 +443,8 @@ static void launch_skinny_x(const uint16_t* X, int ldx, int M, int KB, const uin
   const int kbps = (KB + splitk - 1) / splitk;
   dim3 grid(NBtot / NB, splitk);
 #define LSA_SKL(WV, DV) \
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF>), grid, dim3(64 * WV), 0, s, X, ldx, M, KB, Wf, \
-                     out, ldo, kbps)
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF>), grid, dim3(64 * WV), 0, s, X, \
+                     ldx, M, KB, Wf, out, ldo, kbps)
   if (g_skinny_div == 2) {
     if (g_skinny_waves == 8) LSA_SKL(8, 2);
     else LSA_SKL(4, 2);

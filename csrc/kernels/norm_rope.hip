@@ -26,6 +26,12 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
   const int nt = blockDim.x;
   float v[VPT][8];
   float ss = 0.f;
+  uint4 wq[VPT];  // norm weights: requested up front, they do not depend on the reduction
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int c = (threadIdx.x + q * nt) * 8;
+    wq[q] = c < D ? *reinterpret_cast<const uint4*>(w + c) : make_uint4(0u, 0u, 0u, 0u);
+  }
   auto add8 = [](float* x, const float* p) {
     const float4 a = *reinterpret_cast<const float4*>(p);
     const float4 b = *reinterpret_cast<const float4*>(p + 4);
@@ -74,7 +80,7 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
     const int c = (threadIdx.x + q * nt) * 8;
     if (c < D) {
       float wf[8], o[8];
-      unpack8(*reinterpret_cast<const uint4*>(w + c), wf);
+      unpack8(wq[q], wf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[q][j] * inv * wf[j];
       *reinterpret_cast<uint4*>(xn + (xf_mt ? xf_off(m, c, xf_mt) : (size_t)m * D + c)) = pack8(o);
