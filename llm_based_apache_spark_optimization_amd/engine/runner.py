@@ -135,7 +135,7 @@ class ModelRunner:
     def _splitk(self, M: int, K: int, N: Optional[int] = None, tp_reduced: bool = True, xf: bool = False) -> int:
         if not self.on_gpu or M > 64 or (tp_reduced and self.tp is not None and self.tp.size > 1):
             return 1
-        return ops.pick_gemm_config(M, N or self.d, K, "f32", xf=xf)[1]
+        return ops.pick_gemm_config(M, N or self.d, K, "f32", xf=xf, kind=self.w.layers[0].wo.kind)[1]
 
     def use_xfrag(self, B: int) -> bool:
         """Fragment-major activations pay off once a decode batch spans >1 row tile (B > 16):

@@ -163,14 +163,17 @@ def _tuning_table() -> dict:
     return _tuning
 
 
-def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False) -> tuple[int, int, int, int]:
+def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
+                     kind: str = "bf16") -> tuple[int, int, int, int]:
     """(nb, splitk, waves, div) for a decode GEMM: the tuning table when it has the shape (entries
-    measured with fragment-major activations carry a ':xf' suffix), else the heuristic below (div 4,
-    4-wave workgroups won most measured shapes)."""
+    measured with fragment-major activations carry a ':xf' suffix, fp8-weight entries ':fp8'), else
+    the heuristic below (div 4, 4-wave workgroups won most measured shapes)."""
     if M <= 64:
         key = f"{N}x{K}:{epi}:{'s' if M <= 16 else 'm'}"
         tab = _tuning_table()
-        e = tab.get(key + ":xf") if xf else None
+        e = tab.get(key + ":fp8") if kind == "fp8" else None
+        if e is None and xf:
+            e = tab.get(key + ":xf")
         e = e if e is not None else tab.get(key)
         if e is not None and not (M > 32 and e["nb"] > 2):
             return e["nb"], e["splitk"], e["waves"], e["div"]
@@ -196,7 +199,7 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
             out.view(-1)[: y.numel()].copy_(y.reshape(-1))
             return out
         return y
-    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi)
+    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi, kind=w.kind)
     nb = nb0 if nb is None else nb
     splitk = sk0 if splitk is None else splitk
     waves = wv0 if waves is None else waves
@@ -262,7 +265,7 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
             return y
         out.view(-1)[: y.numel()].copy_(y)
         return out
-    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, w.K, epi, xf=True)
+    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, w.K, epi, xf=True, kind=w.kind)
     nb = nb0 if nb is None else nb
     splitk = sk0 if splitk is None else splitk
     waves = wv0 if waves is None else waves
