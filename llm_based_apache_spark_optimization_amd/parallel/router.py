@@ -8,8 +8,9 @@ own continuous-batching engines.  No GPU collective is needed in steady state: r
 independent and initialise identical random weights from the same seed (or load the same
 checkpoint).
 
-* dispatch: least outstanding requests (ties -> lowest replica id), per request;
-* failure detection: a dead worker process (exit) or a missed heartbeat marks the replica down; its
+* dispatch: least outstanding requests (ties -> fewest dispatched, then lowest replica id);
+* failure detection: a dead worker process (exit) or, once the replica has sent its first heartbeat
+  (backends built), a missed heartbeat marks the replica down; its
   in-flight requests are re-dispatched to the remaining replicas (at-least-once; generation is
   idempotent for greedy decoding and seeded sampling);
 * drain: ``close()`` stops accepting, waits for in-flight requests, then stops the workers.
@@ -53,11 +54,11 @@ def _worker(conn, replica: int, devices: str, kind: str, settings_kw: dict, hear
 
     def beat():
         while True:
-            time.sleep(heartbeat_s)
             try:
                 send(("hb", replica, time.time()))
             except (OSError, EOFError):
                 return
+            time.sleep(heartbeat_s)
 
     threading.Thread(target=beat, daemon=True).start()
 
@@ -90,6 +91,7 @@ class _Replica:
         self.inflight: dict = {}
         self.alive = True
         self.last_hb = time.time()
+        self.ready = False  # first heartbeat seen: start-up (imports, weight load) is not a missed beat
         self.served = 0
         self.send_lock = threading.Lock()
 
@@ -135,7 +137,8 @@ class ReplicaRouter(Backend):
                 self._mark_dead(r, "pipe closed")
                 return
             if msg[0] == "hb":
-                r.last_hb = msg[2]
+                r.last_hb = time.time()
+                r.ready = True
                 continue
             kind, rid, payload = msg
             with self._lock:
@@ -150,7 +153,8 @@ class ReplicaRouter(Backend):
         while not self._closing:
             time.sleep(0.5)
             for r in self.replicas:
-                if r.alive and (not r.proc.is_alive() or time.time() - r.last_hb > self.dead_after_s):
+                hb_lost = r.ready and time.time() - r.last_hb > self.dead_after_s
+                if r.alive and (not r.proc.is_alive() or hb_lost):
                     self._mark_dead(r, "process exited" if not r.proc.is_alive() else "heartbeat lost")
 
     def _mark_dead(self, r: _Replica, why: str):
@@ -174,7 +178,7 @@ class ReplicaRouter(Backend):
         live = [r for r in self.replicas if r.alive]
         if not live:
             raise RuntimeError("no live replicas")
-        return min(live, key=lambda r: (len(r.inflight), r.idx))
+        return min(live, key=lambda r: (len(r.inflight), r.served + len(r.inflight), r.idx))
 
     def _dispatch(self, rid: int, req: tuple):
         while True:
