@@ -40,6 +40,16 @@ int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
 int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
+int lsa_ar_alloc(size_t bytes, void** out);
+int lsa_ar_free(void* p);
+int lsa_ar_handle(void* p, char* out64);
+int lsa_ar_open(const char* in64, void** out);
+int lsa_ar_close(void* p);
+int lsa_ar_max_world();
+int lsa_ar_wallclock_khz(int* out);
+int lsa_ar_header_bytes();
+int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
+               int nblocks, long long timeout_ticks, int* err, hipStream_t s);
 }
 
 namespace {
@@ -268,6 +278,44 @@ void fp8_dequant(const at::Tensor& wq, const at::Tensor& wscale, int64_t N, int6
   check(lsa_fp8_dequant(wq.data_ptr(), wscale.data_ptr<float>(), N, K, wf.data_ptr(), cur_stream()), "fp8_dequant");
 }
 
+// ---- one-shot IPC all-reduce (kernels/allreduce.hip); regions are raw device addresses (int64)
+int64_t ar_alloc(int64_t bytes) {
+  void* p = nullptr;
+  check(lsa_ar_alloc((size_t)bytes, &p), "ar_alloc");
+  return reinterpret_cast<int64_t>(p);
+}
+
+py::bytes ar_handle(int64_t p) {
+  char h[64];
+  check(lsa_ar_handle(reinterpret_cast<void*>(p), h), "ar_handle");
+  return py::bytes(h, 64);
+}
+
+int64_t ar_open(const std::string& h) {
+  TORCH_CHECK(h.size() == 64, "IPC handle must be 64 bytes");
+  void* p = nullptr;
+  check(lsa_ar_open(h.data(), &p), "ar_open");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Tensor& regions, int64_t rank,
+            int64_t maxb, int64_t nblocks, int64_t timeout_ticks, at::Tensor& err) {
+  need(data, at::kFloat, "data");
+  need(regions, at::kLong, "regions");
+  need(err, at::kInt, "err");
+  TORCH_CHECK(data.is_contiguous() && data.numel() % 4 == 0, "all-reduce data: contiguous, numel % 4 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(data.data_ptr()) % 16 == 0, "all-reduce data must be 16-B aligned");
+  TORCH_CHECK(data.numel() * 4 <= maxb, "all-reduce payload exceeds the registered slot size");
+  if (out.has_value()) {
+    need(*out, at::kFloat, "out");
+    TORCH_CHECK(out->is_contiguous() && out->numel() == data.numel() * regions.numel(), "all-gather out size");
+  }
+  check(lsa_ar_run(data.data_ptr<float>(), data.numel(), ptr<float>(out),
+                   reinterpret_cast<uint8_t* const*>(regions.data_ptr()),
+                   rank, regions.numel(), maxb, nblocks, timeout_ticks, err.data_ptr<int>(), cur_stream()),
+        "ar_run");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -301,5 +349,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     check(lsa_silu_parts(parts.data_ptr<float>(), S, parts.stride(0), M, F, out.data_ptr(), cur_stream()),
           "silu_parts");
   });
+  m.def("ar_alloc", &ar_alloc);
+  m.def("ar_free", [](int64_t p) { check(lsa_ar_free(reinterpret_cast<void*>(p)), "ar_free"); });
+  m.def("ar_handle", &ar_handle);
+  m.def("ar_open", &ar_open);
+  m.def("ar_close", [](int64_t p) { check(lsa_ar_close(reinterpret_cast<void*>(p)), "ar_close"); });
+  m.def("ar_run", &ar_run);
+  m.def("ar_wallclock_khz", []() {
+    int k = 0;
+    check(lsa_ar_wallclock_khz(&k), "ar_wallclock_khz");
+    return k;
+  });
+  m.attr("ar_max_world") = lsa_ar_max_world();
+  m.attr("ar_header_bytes") = lsa_ar_header_bytes();
   m.attr("arch") = "gfx950";
 }

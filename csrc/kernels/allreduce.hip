@@ -1,0 +1,188 @@
+// One-shot tensor-parallel all-reduce (and all-gather) over IPC-mapped peer buffers.
+//
+// Decode-size TP all-reduces (B x d f32 = 16 KiB .. 512 KiB, 2 per layer) are latency-bound on
+// xGMI: a generic ring pays n-1 dependent hops plus a collective launch.  Here every rank PUSHES its
+// whole tensor straight into a receive slot of every peer (one xGMI link per peer on the MI355X
+// mesh, all links at once), raises one flag per (block, source) in the peer's signal area, waits for
+// the peers' flags of the same block, then sums the slots locally in rank order (bitwise identical
+// results on every rank, so TP replicas never diverge in argmax).
+//
+// Region layout (one hipExtMallocWithFlags(hipDeviceMallocUncached) allocation per rank, opened by
+// the peers with hipIpcOpenMemHandle):
+//   [0,      8 KiB)  flags[AR_MAX_BLOCKS][AR_MAX_WORLD]  u32, written by peers (epoch numbers)
+//   [8 KiB, 9 KiB)   epoch[AR_MAX_BLOCKS]                u32, this rank's per-block call counter
+//   [16 KiB, ...)    recv[2 parities][world][maxb]       pushed payloads
+// Uncached memory keeps remote pushes coherent with the receiver's reads (no stale L2 lines of a slot
+// from two calls ago).  The epoch lives on the device, so the launch has fixed arguments and replays
+// inside a captured hipGraph.  Protocol invariants (per block b):
+//   * a peer can be at most one epoch ahead (it needs our flag to finish), so flags are compared
+//     with (int)(flag - ep) >= 0 and payload slots alternate by epoch parity;
+//   * pushing into parity p at epoch ep is safe: reaching ep means the peer raised ep-1, which it
+//     does only after finishing ep-2 (the previous user of parity p).
+// Every wait is bounded by a wall-clock timeout that sets *err and drains the grid, so a missing
+// peer can never leave waves spinning on the GPU.
+#include "common.h"
+#include <cstring>
+
+#define AR_MAX_WORLD 8
+#define AR_MAX_BLOCKS 256
+#define AR_FLAGS_OFF 0
+#define AR_EPOCH_OFF 8192
+#define AR_DATA_OFF 16384
+#define AR_THREADS 256
+
+__device__ __forceinline__ uint32_t ld_relaxed_sys(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_release_sys(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// GATHER = 0: in-place sum into data.  GATHER = 1: all-gather, out[p * n4 + i] = rank p's data[i].
+template <int W, int GATHER>
+__global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restrict__ data, const long n4,
+                                                                 float4* __restrict__ out,
+                                                                 uint8_t* const* __restrict__ regions, const int rank,
+                                                                 const size_t maxb, const long long timeout_ticks,
+                                                                 int* __restrict__ err) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  uint8_t* mine = regions[rank];
+  uint32_t* my_epoch = reinterpret_cast<uint32_t*>(mine + AR_EPOCH_OFF);
+  __shared__ uint32_t s_ep;
+  if (tid == 0) s_ep = my_epoch[b] + 1u;
+  __syncthreads();
+  const uint32_t ep = s_ep;
+  const size_t slot_off = AR_DATA_OFF + (size_t)(ep & 1u) * W * maxb;
+  const long stride = (long)gridDim.x * AR_THREADS;
+
+  // 1. push this block's chunk into every peer's recv[parity][rank]
+  for (long i = (long)b * AR_THREADS + tid; i < n4; i += stride) {
+    const float4 v = data[i];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      if (p == rank) continue;
+      float4* dst = reinterpret_cast<float4*>(regions[p] + slot_off + (size_t)rank * maxb);
+      dst[i] = v;
+    }
+  }
+  __threadfence_system();  // this thread's pushes are visible system-wide before any flag below
+  __syncthreads();
+
+  // 2. raise our flag for block b at every peer, then wait for theirs
+  if (tid < W && tid != rank) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(regions[tid] + AR_FLAGS_OFF) + b * AR_MAX_WORLD + rank;
+    st_release_sys(f, ep);
+    const uint32_t* mf = reinterpret_cast<const uint32_t*>(mine + AR_FLAGS_OFF) + b * AR_MAX_WORLD + tid;
+    const long long t0 = wall_clock64();
+    while ((int)(ld_relaxed_sys(mf) - ep) < 0) {  // relaxed spin, one acquire fence after it
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > timeout_ticks) {
+        atomicExch(err, 1);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+
+  if (GATHER) {  // 3'. concatenate the slots in rank order
+    for (long i = (long)b * AR_THREADS + tid; i < n4; i += stride) {
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        out[(long)p * n4 + i] = (p == rank) ? data[i]
+                                            : reinterpret_cast<const float4*>(mine + slot_off + (size_t)p * maxb)[i];
+    }
+    if (tid == 0) my_epoch[b] = ep;
+    return;
+  }
+  // 3. rank-ordered sum of the local slots (own contribution read from data)
+  for (long i = (long)b * AR_THREADS + tid; i < n4; i += stride) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      const float4 v = (p == rank)
+                           ? data[i]
+                           : reinterpret_cast<const float4*>(mine + slot_off + (size_t)p * maxb)[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    data[i] = acc;
+  }
+  if (tid == 0) my_epoch[b] = ep;
+}
+
+extern "C" {
+
+int lsa_ar_alloc(size_t bytes, void** out) {
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(p, 0, bytes);
+  if (e != hipSuccess) return (int)e;
+  e = hipDeviceSynchronize();
+  *out = p;
+  return (int)e;
+}
+
+int lsa_ar_free(void* p) { return (int)hipFree(p); }
+
+int lsa_ar_handle(void* p, char* out64) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) return (int)e;
+  static_assert(sizeof(h) == 64, "hipIpcMemHandle_t is 64 bytes");
+  std::memcpy(out64, &h, 64);
+  return 0;
+}
+
+int lsa_ar_open(const char* in64, void** out) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, in64, 64);
+  return (int)hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+int lsa_ar_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
+
+int lsa_ar_max_world() { return AR_MAX_WORLD; }
+
+// constant-rate clock read by wall_clock64() (s_memrealtime), in kHz, of the current device
+int lsa_ar_wallclock_khz(int* out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceGetAttribute(out, hipDeviceAttributeWallClockRate, dev);
+}
+int lsa_ar_header_bytes() { return AR_DATA_OFF; }
+
+// data: n floats (n % 4 == 0, 16-B aligned), regions: device array of `world` region pointers;
+// out == nullptr: in-place all-reduce; otherwise all-gather into out[world * n]
+int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
+               int nblocks, long long timeout_ticks, int* err, hipStream_t s) {
+  if (n % 4 || (size_t)n * 4 > maxb || world < 2 || world > AR_MAX_WORLD || rank < 0 || rank >= world) return -1;
+  const long n4 = n / 4;
+  long want = (n4 + AR_THREADS - 1) / AR_THREADS;
+  int grid = (int)(want < nblocks ? want : nblocks);
+  if (grid < 1) grid = 1;
+  if (grid > AR_MAX_BLOCKS) grid = AR_MAX_BLOCKS;
+#define AR_LAUNCH(WV)                                                                                        \
+  if (out)                                                                                                     \
+    hipLaunchKernelGGL((ar_oneshot_kernel<WV, 1>), dim3(grid), dim3(AR_THREADS), 0, s,                         \
+                       reinterpret_cast<float4*>(data), n4, reinterpret_cast<float4*>(out), regions, rank, maxb, \
+                       timeout_ticks, err);                                                                    \
+  else                                                                                                         \
+    hipLaunchKernelGGL((ar_oneshot_kernel<WV, 0>), dim3(grid), dim3(AR_THREADS), 0, s,                         \
+                       reinterpret_cast<float4*>(data), n4, nullptr, regions, rank, maxb, timeout_ticks, err)
+  switch (world) {
+    case 2: AR_LAUNCH(2); break;
+    case 3: AR_LAUNCH(3); break;
+    case 4: AR_LAUNCH(4); break;
+    case 5: AR_LAUNCH(5); break;
+    case 6: AR_LAUNCH(6); break;
+    case 7: AR_LAUNCH(7); break;
+    case 8: AR_LAUNCH(8); break;
+    default: return -1;
+  }
+#undef AR_LAUNCH
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -126,6 +126,8 @@ class ModelRunner:
         self.amax_part = torch.zeros(S * ((self.V + 4095) // 4096), dtype=torch.int64, device=dev)
         self.cand = torch.zeros(S * ((self.V + 2047) // 2048) * 64, dtype=torch.int64, device=dev)
         self.graphs: dict = {}
+        if self.tp is not None and self.tp.size > 1 and self.on_gpu:
+            self.tp.warmup()  # communicators (RCCL + the one-shot IPC all-reduce) before any launch
 
     # ------------------------------------------------------------------------------------ helpers
     def _allreduce(self, t: torch.Tensor) -> None:

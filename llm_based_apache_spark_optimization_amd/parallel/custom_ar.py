@@ -1,0 +1,97 @@
+"""One-shot all-reduce (and all-gather) over IPC-mapped peer buffers for decode-size TP messages (SURVEY.md §2.5 K15,
+§2.6 P-COMM).
+
+RCCL's generic all-reduce pays a collective launch and n-1 dependent ring hops; a TP=2 decode step
+issues 64 of them (2 per layer, 7B) on B x 4096 f32 tensors of 16-512 KiB, each latency-bound on one
+xGMI link.  ``IpcAllReduce`` replaces those with one kernel (``csrc/kernels/allreduce.hip``) that
+pushes the tensor into every peer's receive slot over xGMI, raises per-block flags and sums locally
+in rank order.  It is graph-capturable (fixed launch arguments, epochs on the device), so it sits
+inside the captured decode hipGraph exactly where the RCCL call was.  Larger messages (prefill
+[T, d] activations) keep using RCCL, which is bandwidth-optimal there.
+
+The per-rank region is exchanged once through ``torch.distributed.all_gather_object`` on the TP
+group (any backend), so the same code runs on one node of 8 GPUs over RCCL and in the 2/4-process
+single-GPU tests over gloo.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+DEFAULT_MAX_BYTES = 8 << 20  # B=64 x d=4096 f32 all-reduces; B=32 x 64128 vocab-parallel logit gathers (3B, TP2)
+DEFAULT_TIMEOUT_S = 60.0
+
+
+class IpcAllReduce:
+    """In-place f32 sum over the ``world`` ranks of ``group`` for tensors up to ``max_bytes``."""
+
+    def __init__(self, group, rank: int, world: int, device: torch.device, max_bytes: int = DEFAULT_MAX_BYTES,
+                 nblocks: int = 128, timeout_s: float = DEFAULT_TIMEOUT_S):
+        ext = ops.ext()
+        if not 2 <= world <= ext.ar_max_world:
+            raise ValueError(f"IpcAllReduce supports 2..{ext.ar_max_world} ranks, got {world}")
+        self.rank, self.world, self.device = rank, world, device
+        self.max_bytes = int(max_bytes)
+        self.nblocks = int(nblocks)
+        with torch.cuda.device(device):
+            self._base = ext.ar_alloc(ext.ar_header_bytes + 2 * world * self.max_bytes)
+            handle = ext.ar_handle(self._base)
+            handles: list = [None] * world
+            dist.all_gather_object(handles, handle, group=group)
+            self._opened = []
+            ptrs = []
+            for r, h in enumerate(handles):
+                if r == rank:
+                    ptrs.append(self._base)
+                else:
+                    p = ext.ar_open(h)
+                    self._opened.append(p)
+                    ptrs.append(p)
+            self.regions = torch.tensor(ptrs, dtype=torch.int64, device=device)
+            self.err = torch.zeros(1, dtype=torch.int32, device=device)
+            self.timeout_ticks = int(timeout_s * ext.ar_wallclock_khz() * 1000)
+        # every rank has mapped every peer before anyone pushes
+        dist.barrier(group=group)
+
+    def fits(self, t: torch.Tensor) -> bool:
+        return (t.dtype == torch.float32 and t.is_cuda and t.is_contiguous() and t.numel() % 4 == 0
+                and t.numel() * 4 <= self.max_bytes and t.data_ptr() % 16 == 0)
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        ops.ext().ar_run(t, None, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err)
+        return t
+
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+        """out[world * n] = concatenation of every rank's t[n] in rank order (same push protocol)."""
+        ops.ext().ar_run(t, out, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err)
+        return out
+
+    def check(self) -> None:
+        """Raise if any wait timed out since construction (a peer never arrived)."""
+        if int(self.err.item()):
+            raise RuntimeError("IpcAllReduce: a peer did not arrive within the timeout")
+
+    def close(self) -> None:
+        ext = ops.ext()
+        torch.cuda.synchronize(self.device)
+        for p in self._opened:
+            ext.ar_close(p)
+        self._opened = []
+        if self._base:
+            ext.ar_free(self._base)
+            self._base = 0
+
+
+def maybe_ipc_allreduce(group, rank: int, world: int, device: torch.device) -> Optional[IpcAllReduce]:
+    """The one-shot all-reduce for a GPU TP group, unless disabled (``LSA_CUSTOM_AR=0``) or unavailable."""
+    if device.type != "cuda" or world < 2 or os.environ.get("LSA_CUSTOM_AR", "1") == "0":
+        return None
+    if world > ops.ext().ar_max_world:
+        return None
+    return IpcAllReduce(group, rank, world, device,
+                        max_bytes=int(os.environ.get("LSA_CUSTOM_AR_MAX_BYTES", DEFAULT_MAX_BYTES)))

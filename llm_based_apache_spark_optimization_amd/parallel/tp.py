@@ -4,7 +4,8 @@ Megatron-style split (SURVEY.md §2.6 P-TP): QKV and gate/up column-parallel, O 
 followed by one all-reduce each (2 per layer), LM head vocab-parallel followed by an all-gather.
 On MI355X every GPU pair has its own xGMI link, so a TP=2 replica uses exactly one link; the
 decode-size all-reduce (B x d f32, 16-512 KiB) is latency-bound and is captured inside the decode
-hipGraph together with the kernels around it.
+hipGraph together with the kernels around it.  On GPU groups those decode-size all-reduces run on
+the one-shot IPC kernel (``custom_ar.IpcAllReduce``); RCCL keeps the large ones.
 """
 from __future__ import annotations
 
@@ -19,19 +20,32 @@ class TPGroup:
     def __init__(self, group, rank: int, size: int, device: torch.device):
         self.group, self.rank, self.size, self.device = group, rank, size, device
         self._warm = False
+        self.car = None  # IpcAllReduce once warmed up on a GPU group
 
     def all_reduce(self, t: torch.Tensor) -> None:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        if self.car is not None and self.car.fits(t):
+            self.car(t)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
-        dist.all_gather_into_tensor(out, inp, group=self.group)
+        if self.car is not None and self.car.fits(inp) and out.is_contiguous():
+            self.car.all_gather(out, inp)
+        else:
+            dist.all_gather_into_tensor(out, inp, group=self.group)
 
     def warmup(self) -> None:
-        """Initialise the communicator outside graph capture."""
+        """Initialise the communicators outside graph capture (collective over the group)."""
         if not self._warm:
             t = torch.zeros(16, device=self.device)
-            self.all_reduce(t)
-            torch.cuda.synchronize(self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            if self.device.type == "cuda":
+                from .custom_ar import maybe_ipc_allreduce
+
+                self.car = maybe_ipc_allreduce(self.group, self.rank, self.size, self.device)
+                if self.car is not None:
+                    self.car(t)
+                torch.cuda.synchronize(self.device)
             self._warm = True
 
 

@@ -134,7 +134,7 @@ def test_sampling_engine(gpu):
     assert len(c.token_ids) == 16
 
 
-def _tp_gpu_worker(rank, world, port, q):
+def _tp_gpu_worker(rank, world, port, q, graphs=False):
     import os
 
     import torch.distributed as dist
@@ -145,15 +145,18 @@ def _tp_gpu_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     tp = TPGroup(dist.group.WORLD, rank, world, dev)
-    e = build_engine("tiny-nsql", device=str(dev), max_slots=4, max_model_len=256, tp=tp, use_graphs=False)
+    e = build_engine("tiny-nsql", device=str(dev), max_slots=4, max_model_len=256, tp=tp, use_graphs=graphs)
     toks = e.generate([[1] + list(range(5, 40)), [1, 7, 7]], SamplingParams(max_tokens=6, ignore_eos=True))
     q.put((rank, [t.token_ids for t in toks]))
     dist.destroy_process_group()
 
 
-def test_tensor_parallel_kernels_gpu(gpu):
-    """TP=2 sharded shapes through the HIP kernels: two ranks on the one GPU of the test box, gloo for the
-    collectives (RCCL needs one GPU per rank; the 8-GPU node runs it), eager (gloo is not capturable)."""
+@pytest.mark.parametrize("graphs", [False, True])
+def test_tensor_parallel_kernels_gpu(gpu, graphs):
+    """TP=2 sharded shapes through the HIP kernels: two ranks on the one GPU of the test box.  Decode-size
+    all-reduces / logit all-gathers run on the one-shot IPC kernel (graph-capturable, so the decode step
+    is captured when ``graphs``); gloo carries the handle exchange and the large prefill all-reduces (RCCL
+    needs one GPU per rank; the 8-GPU node runs it)."""
     import socket
 
     import torch.multiprocessing as tmp
@@ -166,7 +169,7 @@ def test_tensor_parallel_kernels_gpu(gpu):
         port = s.getsockname()[1]
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_tp_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_tp_gpu_worker, args=(r, 2, port, q, graphs)) for r in range(2)]
     [p.start() for p in ps]
     import queue
     import time
