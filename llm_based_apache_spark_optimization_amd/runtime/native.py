@@ -38,6 +38,7 @@ class _PyBlockAllocator:
             raise ValueError("need at least 2 KV blocks (block 0 is scratch)")
         self.num_blocks, self.block_size = num_blocks, block_size
         self._free = list(range(num_blocks - 1, 0, -1))
+        self._owned = set()
 
     def blocks_for(self, tokens):
         return (tokens + self.block_size - 1) // self.block_size
@@ -46,16 +47,25 @@ class _PyBlockAllocator:
         return len(self._free) >= n
 
     def alloc(self, n):
+        if n < 0:
+            raise ValueError("negative block count")
         if not self.can_alloc(n):
             raise RuntimeError("KV cache exhausted")
+        if n == 0:
+            return []
         out = self._free[-n:][::-1]
         del self._free[-n:]
+        self._owned.update(out)
         return out
 
     def release(self, blocks):
+        blocks = list(blocks)
+        if any(b <= 0 or b >= self.num_blocks or b not in self._owned for b in blocks):
+            raise ValueError("bad or already-free block id")
+        if len(set(blocks)) != len(blocks):
+            raise ValueError("block listed twice")
         for b in blocks:
-            if b <= 0 or b >= self.num_blocks:
-                raise ValueError("bad block id")
+            self._owned.discard(b)
             self._free.append(b)
 
     @property
