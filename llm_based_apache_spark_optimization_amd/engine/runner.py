@@ -38,8 +38,12 @@ class ModelRunner:
     def __init__(self, weights: LlamaWeights, max_slots: int = 32, max_model_len: int = 4096,
                  num_kv_blocks: Optional[int] = None, kv_memory_fraction: float = 0.85,
                  max_new_cap: Optional[int] = None, tp=None, use_graphs: bool = True, steps_per_graph: int = 1,
-                 fuse_rope: Optional[bool] = None):
+                 fuse_rope: Optional[bool] = None, seq_parallel: Optional[bool] = None, sp_min_tokens: Optional[int] = None):
         self.w = weights
+        # Megatron sequence parallelism for TP prefill (SURVEY.md §2.6 P-SP): reduce-scatter the row-parallel
+        # outputs, residual + RMSNorm on T/tp rows, all-gather the bf16 normalised activations
+        self.seq_parallel = (os.environ.get("LSA_SEQ_PARALLEL", "1") != "0") if seq_parallel is None else seq_parallel
+        self.sp_min_tokens = int(os.environ.get("LSA_SP_MIN_TOKENS", 256)) if sp_min_tokens is None else sp_min_tokens
         # decode RoPE + KV append inside the attention kernel (LSA_FUSE_ROPE=0 restores the separate launch)
         self.fuse_rope = (os.environ.get("LSA_FUSE_ROPE", "1") != "0") if fuse_rope is None else fuse_rope
         self.spec = spec = weights.spec
@@ -349,40 +353,13 @@ class ModelRunner:
         if self.on_gpu:
             work = torch.tensor(ops.prefill_work(cu), dtype=torch.int32).to(dev, non_blocking=True)
 
-        f32 = dict(dtype=torch.float32, device=dev)
-        bf = dict(dtype=torch.bfloat16, device=dev)
-        h = torch.empty(T, d, **f32)
-        xn = torch.empty(T, d, **bf)
-        qkv = torch.empty(T, (self.H + 2 * self.Hkv) * self.D, **bf)
-        q = torch.empty(T, self.H, self.D, **bf)
-        attn = torch.empty(T, self.H * self.D, **bf)
-        sk_o = self._splitk(T, self.H * self.D)
-        sk_d = self._splitk(T, self.ffn_l)
-        d_parts = None
-        for l, lw in enumerate(w.layers):
-            if l == 0:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
-            else:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts)
-            ops.linear(xn, lw.wqkv, "bf16", out=qkv)
-            kc, vc = self.kv[l, 0], self.kv[l, 1]
-            ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
-            ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
-                             work=work)
-            o_parts = ops.linear(attn, lw.wo, "f32", splitk=sk_o)
-            if not self.on_gpu:
-                o_parts = o_parts.view(1, T, d)
-            self._allreduce(o_parts)
-            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
-            act = ops.linear(xn, lw.w_gate_up, "silu")
-            d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
-            if not self.on_gpu:
-                d_parts = d_parts.view(1, T, d)
-            self._allreduce(d_parts)
+        tps = self.tp.size if self.tp is not None else 1
+        if self.seq_parallel and tps > 1 and T >= self.sp_min_tokens:
+            xl = self._prefill_layers_sp(T, ids, posd, tsd, bt, cud, ctxd, last, work, n, commit)
+        else:
+            xl = self._prefill_layers(T, ids, posd, tsd, bt, cud, ctxd, last, work, n, commit)
         if not commit:
             return
-        xl = torch.empty(n, d, **bf)
-        ops.add_rmsnorm(h, w.final_norm, self.eps, xl, parts=d_parts, row_idx=last, write_h=False)
         logits = self._lm_head(xl, n)
         # commit the first generated token of each sequence into its slot row
         i32 = dict(dtype=torch.int32, device=dev)
@@ -404,6 +381,93 @@ class ModelRunner:
         self.input_ids.index_copy_(0, slot_t, iid)
         self.positions.index_copy_(0, slot_t, pp)
         self.finished.index_copy_(0, slot_t, fin)
+
+    def _prefill_layers(self, T, ids, posd, tsd, bt, cud, ctxd, last, work, n, commit):
+        """Prefill layer stack with full-sequence residuals; returns the last rows' normalised states."""
+        dev, w, d = self.device, self.w, self.d
+        f32 = dict(dtype=torch.float32, device=dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        h = torch.empty(T, d, **f32)
+        xn = torch.empty(T, d, **bf)
+        qkv = torch.empty(T, (self.H + 2 * self.Hkv) * self.D, **bf)
+        q = torch.empty(T, self.H, self.D, **bf)
+        attn = torch.empty(T, self.H * self.D, **bf)
+        sk_o = self._splitk(T, self.H * self.D)
+        sk_d = self._splitk(T, self.ffn_l)
+        d_parts = None
+        for l, lw in enumerate(w.layers):
+            if l == 0:
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
+            else:
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts)
+            self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T)
+            o_parts = ops.linear(attn, lw.wo, "f32", splitk=sk_o)
+            if not self.on_gpu:
+                o_parts = o_parts.view(1, T, d)
+            self._allreduce(o_parts)
+            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
+            act = ops.linear(xn, lw.w_gate_up, "silu")
+            d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
+            if not self.on_gpu:
+                d_parts = d_parts.view(1, T, d)
+            self._allreduce(d_parts)
+        if not commit:
+            return None
+        xl = torch.empty(n, d, **bf)
+        ops.add_rmsnorm(h, w.final_norm, self.eps, xl, parts=d_parts, row_idx=last, write_h=False)
+        return xl
+
+    def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T):
+        ops.linear(xn, lw.wqkv, "bf16", out=qkv)
+        kc, vc = self.kv[l, 0], self.kv[l, 1]
+        ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
+        ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
+                         work=work)
+
+    def _prefill_layers_sp(self, T, ids, posd, tsd, bt, cud, ctxd, last, work, n, commit):
+        """Sequence-parallel prefill under TP: rank r owns rows [r*Tl, (r+1)*Tl) of the residual stream.
+        Row-parallel outputs (O, down; f32 [Tp, d]) are reduce-scattered instead of all-reduced, the
+        residual add + RMSNorm runs on the local Tl rows only, and the bf16 normalised rows are
+        all-gathered for the next column-parallel GEMM: half the all-reduce's second-phase bytes (bf16
+        instead of f32) and 1/tp of the norm work.  Rows past T (padding to a multiple of tp) are
+        row-independent garbage that is never read back."""
+        dev, w, d, tp = self.device, self.w, self.d, self.tp
+        f32 = dict(dtype=torch.float32, device=dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        tps, r = tp.size, tp.rank
+        Tl = (T + tps - 1) // tps
+        Tp = Tl * tps
+        ids_p = ids if Tp == T else torch.cat([ids, torch.zeros(Tp - T, dtype=ids.dtype, device=dev)])
+        ids_l = ids_p[r * Tl:(r + 1) * Tl]
+        h_l = torch.empty(Tl, d, **f32)
+        xn_l = torch.empty(Tl, d, **bf)
+        xn_full = torch.empty(Tp, d, **bf)
+        xn = xn_full[:T]
+        full = torch.zeros(Tp, d, **f32)  # row-parallel GEMM output (padding rows stay zero)
+        loc = torch.empty(Tl, d, **f32)
+        qkv = torch.empty(T, (self.H + 2 * self.Hkv) * self.D, **bf)
+        q = torch.empty(T, self.H, self.D, **bf)
+        attn = torch.empty(T, self.H * self.D, **bf)
+        parts = loc.view(1, Tl, d)
+        for l, lw in enumerate(w.layers):
+            if l == 0:
+                ops.add_rmsnorm(h_l, lw.attn_norm, self.eps, xn_l, ids=ids_l, emb=w.embed)
+            else:
+                ops.add_rmsnorm(h_l, lw.attn_norm, self.eps, xn_l, parts=parts)
+            tp.all_gather(xn_full.view(-1), xn_l.view(-1))
+            self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T)
+            ops.linear(attn, lw.wo, "f32", out=full, splitk=1)
+            tp.reduce_scatter(loc, full)
+            ops.add_rmsnorm(h_l, lw.mlp_norm, self.eps, xn_l, parts=parts)
+            tp.all_gather(xn_full.view(-1), xn_l.view(-1))
+            act = ops.linear(xn, lw.w_gate_up, "silu")
+            ops.linear(act, lw.w_down, "f32", out=full, splitk=1)
+            tp.reduce_scatter(loc, full)
+        if not commit:
+            return None
+        ops.add_rmsnorm(h_l, w.final_norm, self.eps, xn_l, parts=parts)
+        tp.all_gather(xn_full.view(-1), xn_l.view(-1))
+        return xn_full.index_select(0, last.long())
 
     # ------------------------------------------------------------------------------------ readback
     def read_rows(self, slots: Sequence[int]):

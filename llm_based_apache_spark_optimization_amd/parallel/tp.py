@@ -34,6 +34,15 @@ class TPGroup:
         else:
             dist.all_gather_into_tensor(out, inp, group=self.group)
 
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """out = rank's 1/size row block of the sum over ranks of inp (sequence-parallel prefill)."""
+        if inp.is_cuda and dist.get_backend(self.group) == "gloo":  # gloo: CPU tensors only (test boxes)
+            tmp = inp.clone()
+            dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=self.group)
+            out.copy_(tmp.view(self.size, -1)[self.rank].view_as(out))
+            return
+        dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group)
+
     def warmup(self) -> None:
         """Initialise the communicators outside graph capture (collective over the group)."""
         if not self._warm:

@@ -80,8 +80,13 @@ def _tp_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     tp = TPGroup(dist.group.WORLD, rank, world, torch.device("cpu"))
     e = build_engine("tiny-nsql", device="cpu", max_slots=2, max_model_len=256, tp=tp)
-    toks = e.generate([[1] + list(range(5, 40)), [1, 7, 7]], SamplingParams(max_tokens=6, ignore_eos=True))
-    q.put((rank, [t.token_ids for t in toks]))
+    prompts = [[1] + list(range(5, 40)), [1, 7, 7]]
+    toks = e.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+    # sequence-parallel prefill (forced for these short prompts; T = 39 is not a multiple of tp: padded)
+    e.runner.sp_min_tokens = 1
+    sp_toks = e.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+    e.runner.sp_min_tokens = 1 << 30
+    q.put((rank, [t.token_ids for t in toks], [t.token_ids for t in sp_toks]))
     dist.destroy_process_group()
 
 
@@ -100,8 +105,11 @@ def test_tensor_parallel_matches_single():
     q = ctx.Queue()
     ps = [ctx.Process(target=_tp_worker, args=(r, 2, port, q)) for r in range(2)]
     [p.start() for p in ps]
-    got = dict(q.get(timeout=240) for _ in ps)
+    res = [q.get(timeout=240) for _ in ps]
     [p.join(timeout=60) for p in ps]
+    got = {r: t for r, t, _ in res}
+    got_sp = {r: t for r, _, t in res}
     assert got[0] == got[1]  # every rank decodes the same tokens
+    assert got_sp[0] == got_sp[1] == got[0]  # SP prefill: same tokens as the all-reduce prefill
     agree = sum(a == b for x, y in zip(got[0], want) for a, b in zip(x, y))
     assert agree >= 10, (got[0], want)  # fp32 reduction order differs across shards only

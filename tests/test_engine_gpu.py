@@ -146,8 +146,11 @@ def _tp_gpu_worker(rank, world, port, q, graphs=False):
     dev = torch.device("cuda", 0)
     tp = TPGroup(dist.group.WORLD, rank, world, dev)
     e = build_engine("tiny-nsql", device=str(dev), max_slots=4, max_model_len=256, tp=tp, use_graphs=graphs)
-    toks = e.generate([[1] + list(range(5, 40)), [1, 7, 7]], SamplingParams(max_tokens=6, ignore_eos=True))
-    q.put((rank, [t.token_ids for t in toks]))
+    prompts = [[1] + list(range(5, 40)), [1, 7, 7]]
+    toks = e.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+    e.runner.sp_min_tokens = 1  # sequence-parallel prefill (reduce-scatter / all-gather), padded T = 39
+    sp_toks = e.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+    q.put((rank, [t.token_ids for t in toks], [t.token_ids for t in sp_toks]))
     dist.destroy_process_group()
 
 
@@ -174,14 +177,15 @@ def test_tensor_parallel_kernels_gpu(gpu, graphs):
     import queue
     import time
 
-    got, t0 = {}, time.time()
+    got, got_sp, t0 = {}, {}, time.time()
     try:
         while len(got) < 2:
             assert time.time() - t0 < 240, "TP workers timed out"
             assert not any(p.exitcode not in (None, 0) for p in ps), [p.exitcode for p in ps]
             try:
-                r, toks = q.get(timeout=2)
+                r, toks, sp_toks = q.get(timeout=2)
                 got[r] = toks
+                got_sp[r] = sp_toks
             except queue.Empty:
                 pass
     finally:
@@ -190,3 +194,6 @@ def test_tensor_parallel_kernels_gpu(gpu, graphs):
     assert got[0] == got[1]
     agree = sum(a == b for x, y in zip(got[0], want) for a, b in zip(x, y))
     assert agree >= 10, (got[0], want)
+    assert got_sp[0] == got_sp[1]
+    agree_sp = sum(a == b for x, y in zip(got_sp[0], got[0]) for a, b in zip(x, y))
+    assert agree_sp >= 10, (got_sp[0], got[0])  # SP vs all-reduce prefill: same math, other sum order
