@@ -184,3 +184,17 @@ def test_history_store_sqlite_contract(tmp_path):
     h.insert("a.csv", "q", "SELECT 1", "o.csv")
     recs, nxt = h.page(1, 8)
     assert set(recs[0]) == {"id", "input_file_name", "input_data", "sql_query", "output_file"} and not nxt
+
+
+def test_run_client_against_app(api, ctx):
+    """The manual client (reference FastAPI/run.ipynb, C20) drives every JSON endpoint."""
+    from llm_based_apache_spark_optimization_amd.tools.run_client import ApiClient
+
+    c = ApiClient(base_url="", session=api)
+    d = c.process_data("Listofstartups.csv", "Select 10 records")
+    assert d["message"] == "Query executed successfully!"
+    assert c.nl2sql("Name (string)\nAge (int)", "Select 10 records")["sql_query"].startswith("SELECT")
+    assert c.explain_error("[UNRESOLVED_COLUMN.WITH_SUGGESTION] x")["explanation"]
+    assert c.generate("duckdb-nsql", "Select 10 records", "T (int)")["response"].startswith("SELECT")
+    with pytest.raises(ValueError):
+        c.process_data("", "")  # the notebook's empty payload is rejected client-side
