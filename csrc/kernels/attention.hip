@@ -21,6 +21,9 @@
 #include "common.h"
 
 #define LSA_NEG (-1.0e30f)
+#ifndef LSA_ATTN_NT
+#define LSA_ATTN_NT 1  // non-temporal K/V loads in decode attention (read once per step: 3-5 % faster at B = 32)
+#endif
 #define LSA_SC1 16  // buffer cache-policy aux bit: sc1 (write-through store / L1-bypassing load)
 
 typedef __attribute__((address_space(1))) unsigned long long g_u64;
@@ -81,8 +84,13 @@ __global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __
 #pragma unroll
     for (int u = 0; u < TU; ++u) {
       const int tok = min(wv * TW + u * 4 + (lg & 3), last_tok);
+#if LSA_ATTN_NT
+      kr[u] = ldg_nt(reinterpret_cast<const uint4*>(kc + base + tok * D + li * 8));
+      vr[u] = ldg_nt(reinterpret_cast<const uint4*>(vc + base + tok * D + li * 8));
+#else
       kr[u] = *reinterpret_cast<const uint4*>(kc + base + tok * D + li * 8);
       vr[u] = *reinterpret_cast<const uint4*>(vc + base + tok * D + li * 8);
+#endif
     }
   };
   // split 0 always starts at block 0, which every sequence owns (padding rows map it to the scratch
