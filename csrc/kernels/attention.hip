@@ -52,8 +52,10 @@ struct RopeArgs {
   uint16_t* vc;
 };
 
-// WV = waves per workgroup: 8 for G <= 2 (two keys per lane group per block -> half the K/V registers,
-// so four 4-wave-equivalents fit per CU and a B x Hkv = 1024 grid runs in whole rounds), else 4
+// WV = waves per workgroup: 8 for G <= 3 (two keys per lane group per block -> half the K/V registers,
+// so four 4-wave-equivalents fit per CU and a B x Hkv = 1024 grid runs in whole rounds; G = 3: half the
+// per-wave score work on the latency-bound small grids, 3B B=32 ctx 200 11.1 -> 10.0 us), else 4 (the
+// [NLG][G][128] merge buffer of G >= 4 would not fit 64 KiB of LDS with 32 lane groups)
 template <int G, int ROPE, int WV>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime slab count
 __global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc,
@@ -94,7 +96,9 @@ __global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __
     }
   };
   // split 0 always starts at block 0, which every sequence owns (padding rows map it to the scratch
-  // block): its first K/V fetch leaves before the context length is even known
+  // block): its first K/V fetch leaves before the context length is even known.  (Speculating the other
+  // splits' first blocks too was measured: splits a short sequence does not need then cost a wasted
+  // block read each, 23 -> 36 us at B = 32, ctx 200, 4 splits.)
   if (split == 0) fetch(kA, vA, 0, 63);
   const int ctx = pos[b] + 1;
   const int nblk = (ctx + 63) >> 6;
@@ -375,7 +379,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
   const RopeArgs ra{qkv_parts, (size_t)part_stride, nparts, cos_t, sin_t, const_cast<uint16_t*>(kk),
                     const_cast<uint16_t*>(vv)};
 #define LSA_ADK(GV, RP)                                                                                      \
-  hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 2 ? 8 : 4)>), grid, dim3(GV <= 2 ? 512 : 256), 0, s, qq, kk, \
+  hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4)>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, qq, kk, \
                      vv, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, oo, opart, mlpart, counters,  \
                      xf_mt, ra)
 #define LSA_AD(GV)                                  \

@@ -170,9 +170,11 @@ class LLMEngine:
                 n_steps = remaining if self.run_ahead is None else min(self.run_ahead, remaining)
             else:
                 n_steps = min(self.sync_every, remaining)
+            # host-side bound on every row's context during the run (selects the decode graph's split plan)
+            max_ctx = max(len(q.prompt_ids) + min(q.gen_host + n_steps, q.params.max_tokens) for q in reqs) + 1
         # the decode run needs no scheduler state: new requests may be added meanwhile
         t0 = time.perf_counter()
-        r.decode(B, n_steps, sample)
+        r.decode(B, n_steps, sample, max_ctx=max_ctx)
         fin, gl, _ = r.read_rows([q.slot for q in reqs])
         with self._lock:
             self.stats["decode_s"] += time.perf_counter() - t0

@@ -172,7 +172,19 @@ class ModelRunner:
         return full
 
     # ------------------------------------------------------------------------------------ decode
-    def _decode_step(self, B: int, sample: bool) -> None:
+    def ctx_plan(self, B: int, max_ctx: Optional[int] = None) -> tuple[int, int]:
+        """Split-KV grid plan for a decode run whose contexts stay <= max_ctx.  Contexts are rounded up to
+        a power-of-two tier (>= 256) so only a few plans (= captured graphs) exist per bucket.  Any plan is
+        correct for any context (the kernel widens its splits); the tier only avoids launching split
+        workgroups that short contexts leave empty: B = 32 at ctx 200 costs 24 us planned for 512 keys,
+        31 us for 4096 and 42 us for 8192 (scripts/attn_scaling.py)."""
+        t = self.max_model_len if max_ctx is None else min(self.max_model_len, max(256, max_ctx))
+        tier = 256
+        while tier < t:
+            tier *= 2
+        return ops.decode_split_plan(B, self.Hkv, min(tier, self.max_model_len))
+
+    def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         w, d = self.w, self.d
         ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
         h = self.h[:B]
@@ -184,7 +196,7 @@ class ModelRunner:
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
-        plan = ops.decode_split_plan(B, self.Hkv, self.max_model_len)
+        plan = plan or ops.decode_split_plan(B, self.Hkv, self.max_model_len)
         ws = self.attn_ws
         if xf:  # every GEMM input lives in the fragment-major layout, written by its producer
             xn, attn, act = self.xn_f, self.attn_f, self.act_f
@@ -233,8 +245,9 @@ class ModelRunner:
             b *= 2
         return min(b, self.max_slots) if n <= self.max_slots else self.max_slots
 
-    def capture(self, B: int, sample: bool) -> None:
-        key = (B, sample)
+    def capture(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
+        plan = tuple(plan or self.ctx_plan(B))
+        key = (B, sample, plan)
         if key in self.graphs:
             return
         if self.tp is not None and self.tp.size > 1:
@@ -246,7 +259,7 @@ class ModelRunner:
             # state must not change during capture: kernels are recorded, not executed
             with torch.cuda.graph(g, stream=s):
                 for _ in range(self.steps_per_graph):
-                    self._decode_step(B, sample)
+                    self._decode_step(B, sample, plan)
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graphs[key] = g
 
@@ -257,24 +270,38 @@ class ModelRunner:
             b *= 2
         return out + [self.max_slots]
 
+    def plans(self, B: int) -> list[tuple]:
+        """Distinct split plans over the context tiers 256, 512, ... max_model_len."""
+        out, t = [], 256
+        while True:
+            p = self.ctx_plan(B, t)
+            if p not in out:
+                out.append(p)
+            if t >= self.max_model_len:
+                return out
+            t *= 2
+
     def capture_all(self, sample_modes: Sequence[bool] = (False, True)) -> None:
-        """Capture every (bucket, sampling-mode) decode graph up front, so a server never pays a
-        capture inside a request."""
+        """Capture every (bucket, sampling mode, context tier) decode graph up front, so a server never
+        pays a capture inside a request."""
         if not self.use_graphs:
             return
         for b in self.buckets():
             for sm in sample_modes:
-                self.capture(b, sm)
+                for p in self.plans(b):
+                    self.capture(b, sm, p)
         torch.cuda.synchronize(self.device)
 
-    def decode(self, B: int, steps: int, sample: bool = False) -> None:
-        """Run ``steps`` decode steps over slot rows [0, B) (B a bucket size)."""
+    def decode(self, B: int, steps: int, sample: bool = False, max_ctx: Optional[int] = None) -> None:
+        """Run ``steps`` decode steps over slot rows [0, B) (B a bucket size); ``max_ctx`` bounds every
+        row's context length during the run (picks the graph planned for that tier)."""
+        plan = tuple(self.ctx_plan(B, max_ctx))
         if not self.use_graphs:
             for _ in range(steps):
-                self._decode_step(B, sample)
+                self._decode_step(B, sample, plan)
             return
-        self.capture(B, sample)
-        g = self.graphs[(B, sample)]
+        self.capture(B, sample, plan)
+        g = self.graphs[(B, sample, plan)]
         n = (steps + self.steps_per_graph - 1) // self.steps_per_graph
         for _ in range(n):
             g.replay()
