@@ -451,29 +451,36 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
   float mrow = LSA_NEG, lrow = 0.f;
 
   const int* bt = block_tables + (size_t)seq * max_blocks;
-  uint4 kr[4], vr[4];
-  auto fetch = [&](int t) {
-    const size_t base = ((size_t)bt[t] * Hkv + hk) * 64 * D;
-    const uint4* kb = reinterpret_cast<const uint4*>(kc + base);
-    const uint4* vb = reinterpret_cast<const uint4*>(vc + base);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      kr[i] = kb[tid + 256 * i];
-      vr[i] = vb[tid + 256 * i];
-    }
-  };
-  if (ntiles > 0) fetch(0);
+  // register staging of the next K/V tile: issued unconditionally (tile index clamped) right after the
+  // LDS image of the current tile is written, consumed one iteration later, so the global latency hides
+  // behind the current tile's MFMAs.  (A conditional refill inside the loop made hipcc keep kr/vr in
+  // scratch and wait for every fetch immediately: 233 us -> see scripts/bench_attn_prefill.py.)
+  uint4 kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3;
+#define LSA_PF_FETCH(T)                                                                  \
+  {                                                                                      \
+    const size_t base_ = ((size_t)bt[(T)] * Hkv + hk) * 64 * D;                          \
+    const uint4* kb_ = reinterpret_cast<const uint4*>(kc + base_) + tid;                 \
+    const uint4* vb_ = reinterpret_cast<const uint4*>(vc + base_) + tid;                 \
+    kr0 = kb_[0]; kr1 = kb_[256]; kr2 = kb_[512]; kr3 = kb_[768];                        \
+    vr0 = vb_[0]; vr1 = vb_[256]; vr2 = vb_[512]; vr3 = vb_[768];                        \
+  }
+  LSA_PF_FETCH(0);
   for (int t = 0; t < ntiles; ++t) {
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c >> 4, ch = c & 15;
-      *reinterpret_cast<uint4*>(&Ks[k_off(row, ch)]) = kr[i];
-      *reinterpret_cast<uint4*>(&Vs[v_off(row, ch * 8)]) = vr[i];
+    {
+      const int row = tid >> 4, ch = tid & 15;  // chunk c = tid + 256 i -> row + 16 i, same ch
+      *reinterpret_cast<uint4*>(&Ks[k_off(row, ch)]) = kr0;
+      *reinterpret_cast<uint4*>(&Ks[k_off(row + 16, ch)]) = kr1;
+      *reinterpret_cast<uint4*>(&Ks[k_off(row + 32, ch)]) = kr2;
+      *reinterpret_cast<uint4*>(&Ks[k_off(row + 48, ch)]) = kr3;
+      *reinterpret_cast<uint4*>(&Vs[v_off(row, ch * 8)]) = vr0;
+      *reinterpret_cast<uint4*>(&Vs[v_off(row + 16, ch * 8)]) = vr1;
+      *reinterpret_cast<uint4*>(&Vs[v_off(row + 32, ch * 8)]) = vr2;
+      *reinterpret_cast<uint4*>(&Vs[v_off(row + 48, ch * 8)]) = vr3;
     }
     __syncthreads();
-    if (t + 1 < ntiles) fetch(t + 1);
+    LSA_PF_FETCH(min(t + 1, ntiles - 1));
+#undef LSA_PF_FETCH
 
     // S^T[key][q] = K Q^T over 4 subtiles of 16 keys
     f32x4_t st[4];
