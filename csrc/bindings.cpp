@@ -46,6 +46,7 @@ int lsa_ar_handle(void* p, char* out64);
 int lsa_ar_open(const char* in64, void** out);
 int lsa_ar_close(void* p);
 int lsa_ar_max_world();
+int lsa_prefill_qblock();
 int lsa_ar_wallclock_khz(int* out);
 int lsa_ar_header_bytes();
 int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
@@ -362,5 +363,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.attr("ar_max_world") = lsa_ar_max_world();
   m.attr("ar_header_bytes") = lsa_ar_header_bytes();
+  m.attr("prefill_qblock") = lsa_prefill_qblock();
   m.attr("arch") = "gfx950";
 }

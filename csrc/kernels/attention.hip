@@ -21,6 +21,11 @@
 #include "common.h"
 
 #define LSA_NEG (-1.0e30f)
+#ifndef LSA_PREFILL_QG
+#define LSA_PREFILL_QG 1  // 16-row query groups per wave in prefill attention (work items of 64 * QG rows);
+                          // QG = 2 halves LDS reads per FLOP but needs 300 registers -> 1 wave/SIMD: measured
+                          // 1.6x slower (3B 2k: 129 -> 205 us), so 1 ships
+#endif
 #ifndef LSA_ATTN_NT
 #define LSA_ATTN_NT 1  // non-temporal K/V loads in decode attention (read once per step: 3-5 % faster at B = 32)
 #endif
@@ -416,6 +421,10 @@ __device__ __forceinline__ uint2 ds_read_tr16(const uint16_t* p) {
 __device__ __forceinline__ int k_off(int r, int ch) { return r * 128 + ((ch ^ (r & 15)) << 3); }
 __device__ __forceinline__ int v_off(int r, int col) { return r * 128 + ((((col >> 3) ^ ((r & 7) << 1))) << 3) + (col & 7); }
 
+// QG query groups of 16 rows per wave (WG = 4 waves x 16*QG rows): every K / V fragment read from LDS
+// feeds QG MFMAs, so QG = 2 halves the LDS traffic per FLOP (the kernel is LDS-read bound at QG = 1:
+// each wave re-reads the whole 64-key K and V tiles for only 16 query rows).
+template <int QG>
 __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                            const uint16_t* __restrict__ vc,
                                                            const int* __restrict__ block_tables, int max_blocks,
@@ -423,6 +432,8 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
                                                            const int* __restrict__ work, int H, int Hkv,
                                                            float scale_log2, uint16_t* __restrict__ out) {
   constexpr int D = 128;
+  constexpr int QW = 16 * QG;   // query rows per wave
+  constexpr int QB = 4 * QW;    // query rows per workgroup
   __shared__ __attribute__((aligned(16))) uint16_t Ks[64 * D];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[64 * D];
   const int wi = blockIdx.x, h = blockIdx.y;
@@ -433,28 +444,37 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
   const int pos0 = ctx - qlen;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, r = lane & 15;
 
-  const int qrow = qs + w * 16 + r;
-  const int qrow_c = min(qrow, qlen - 1);
-  const int qpos = pos0 + qrow;
-  uint4 qf[4];
+  uint4 qf[QG][4];
+  int qpos[QG];
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
-    qf[s] = *reinterpret_cast<const uint4*>(q + ((size_t)(q0 + qrow_c) * H + h) * D + 32 * s + 8 * g);
+  for (int gi = 0; gi < QG; ++gi) {
+    const int qrow = qs + w * QW + gi * 16 + r;
+    const int qrow_c = min(qrow, qlen - 1);
+    qpos[gi] = pos0 + qrow;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      qf[gi][s] = *reinterpret_cast<const uint4*>(q + ((size_t)(q0 + qrow_c) * H + h) * D + 32 * s + 8 * g);
+  }
 
-  const int last_row = min(qs + 63, qlen - 1);
+  const int last_row = min(qs + QB - 1, qlen - 1);
   const int kv_end = min(ctx, pos0 + last_row + 1);
   const int ntiles = (kv_end + 63) >> 6;
 
-  f32x4_t o[8];
+  f32x4_t o[QG][8];
+  float mrow[QG], lrow[QG];
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float mrow = LSA_NEG, lrow = 0.f;
+  for (int gi = 0; gi < QG; ++gi) {
+    mrow[gi] = LSA_NEG;
+    lrow[gi] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[gi][dt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
 
   const int* bt = block_tables + (size_t)seq * max_blocks;
   // register staging of the next K/V tile: issued unconditionally (tile index clamped) right after the
   // LDS image of the current tile is written, consumed one iteration later, so the global latency hides
-  // behind the current tile's MFMAs.  (A conditional refill inside the loop made hipcc keep kr/vr in
-  // scratch and wait for every fetch immediately: 233 us -> see scripts/bench_attn_prefill.py.)
+  // behind the current tile's MFMAs.  (A conditional refill inside the loop made hipcc keep the staging
+  // registers in scratch and wait for every fetch at once: 2x slower, scripts/bench_attn_prefill.py.)
   uint4 kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3;
 #define LSA_PF_FETCH(T)                                                                  \
   {                                                                                      \
@@ -480,63 +500,70 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
     }
     __syncthreads();
     LSA_PF_FETCH(min(t + 1, ntiles - 1));
-#undef LSA_PF_FETCH
 
-    // S^T[key][q] = K Q^T over 4 subtiles of 16 keys
-    f32x4_t st[4];
+    // S^T[key][q] = K Q^T over 4 subtiles of 16 keys; one K fragment feeds QG MFMAs
+    f32x4_t st[QG][4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      st[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int gi = 0; gi < QG; ++gi) st[gi][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       const int krow = 16 * kt + r;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const uint4 a = *reinterpret_cast<const uint4*>(&Ks[k_off(krow, 4 * s + g)]);
-        st[kt] = mfma16x16x32(a, qf[s], st[kt]);
+#pragma unroll
+        for (int gi = 0; gi < QG; ++gi) st[gi][kt] = mfma16x16x32(a, qf[gi][s], st[gi][kt]);
       }
     }
-    float tmax = LSA_NEG;
+    uint4 pa[QG][2];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int gi = 0; gi < QG; ++gi) {
+      float tmax = LSA_NEG;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = t * 64 + 16 * kt + 4 * g + i;
+          float v = st[gi][kt][i] * scale_log2;
+          v = (key > qpos[gi] || key >= ctx) ? LSA_NEG : v;
+          st[gi][kt][i] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(mrow[gi], tmax);
+      const float alpha = exp2f(mrow[gi] - mnew);
+      mrow[gi] = mnew;
+      float psum = 0.f;
+      uint32_t pk[4][2];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        float p[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          p[i] = exp2f(st[gi][kt][i] - mnew);
+          psum += p[i];
+        }
+        pk[kt][0] = pack2bf(p[0], p[1]);
+        pk[kt][1] = pack2bf(p[2], p[3]);
+      }
+      lrow[gi] = lrow[gi] * alpha + psum;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int key = t * 64 + 16 * kt + 4 * g + i;
-        float v = st[kt][i] * scale_log2;
-        v = (key > qpos || key >= ctx) ? LSA_NEG : v;
-        st[kt][i] = v;
-        tmax = fmaxf(tmax, v);
+        const float ai = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[gi][dt][i] *= ai;
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(mrow, tmax);
-    const float alpha = exp2f(mrow - mnew);
-    mrow = mnew;
-    float psum = 0.f;
-    uint32_t pk[4][2];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      float p[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        p[i] = exp2f(st[kt][i] - mnew);
-        psum += p[i];
+      for (int s2 = 0; s2 < 2; ++s2) {
+        pa[gi][s2].x = pk[2 * s2][0]; pa[gi][s2].y = pk[2 * s2][1];
+        pa[gi][s2].z = pk[2 * s2 + 1][0]; pa[gi][s2].w = pk[2 * s2 + 1][1];
       }
-      pk[kt][0] = pack2bf(p[0], p[1]);
-      pk[kt][1] = pack2bf(p[2], p[3]);
     }
-    lrow = lrow * alpha + psum;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float ai = __shfl(alpha, 4 * g + i, 64);
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[dt][i] *= ai;
-    }
-    // O[q][d] += P[q][key] V[key][d]
+    // O[q][d] += P[q][key] V[key][d]; one V fragment feeds QG MFMAs
     const int qq = (lane & 15) >> 2, pp = lane & 3;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      uint4 pa;
-      pa.x = pk[2 * s2][0]; pa.y = pk[2 * s2][1];
-      pa.z = pk[2 * s2 + 1][0]; pa.w = pk[2 * s2 + 1][1];
       const int kb1 = 32 * s2 + 4 * g + qq, kb2 = kb1 + 16;
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) {
@@ -545,24 +572,31 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
         const uint2 v2 = ds_read_tr16(&Vs[v_off(kb2, col)]);
         uint4 vb;
         vb.x = v1.x; vb.y = v1.y; vb.z = v2.x; vb.w = v2.y;
-        o[dt] = mfma16x16x32(pa, vb, o[dt]);
+#pragma unroll
+        for (int gi = 0; gi < QG; ++gi) o[gi][dt] = mfma16x16x32(pa[gi][s2], vb, o[gi][dt]);
       }
     }
   }
-  float lt = lrow + __shfl_xor(lrow, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
+#undef LSA_PF_FETCH
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float li = __shfl(lt, 4 * g + i, 64);
-    const float inv = li > 0.f ? 1.f / li : 0.f;
-    const int qr = qs + w * 16 + 4 * g + i;
-    if (qr < qlen) {
-      uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D;
+  for (int gi = 0; gi < QG; ++gi) {
+    float lt = lrow[gi] + __shfl_xor(lrow[gi], 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) orow[16 * dt + r] = f2bf(o[dt][i] * inv);
+    for (int i = 0; i < 4; ++i) {
+      const float li = __shfl(lt, 4 * g + i, 64);
+      const float inv = li > 0.f ? 1.f / li : 0.f;
+      const int qr = qs + w * QW + gi * 16 + 4 * g + i;
+      if (qr < qlen) {
+        uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) orow[16 * dt + r] = f2bf(o[gi][dt][i] * inv);
+      }
     }
   }
 }
+
+extern "C" int lsa_prefill_qblock() { return 64 * LSA_PREFILL_QG; }
 
 extern "C" int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                 const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv,
@@ -570,7 +604,7 @@ extern "C" int lsa_attn_prefill(const void* q, const void* kc, const void* vc, c
   if (nwork <= 0) return 0;
   if (H % Hkv) return -1;
   dim3 grid(nwork, H);
-  hipLaunchKernelGGL(attn_prefill_kernel, grid, dim3(256), 0, s, reinterpret_cast<const uint16_t*>(q),
+  hipLaunchKernelGGL(attn_prefill_kernel<LSA_PREFILL_QG>, grid, dim3(256), 0, s, reinterpret_cast<const uint16_t*>(q),
                      reinterpret_cast<const uint16_t*>(kc), reinterpret_cast<const uint16_t*>(vc), block_tables,
                      max_blocks, cu_q, ctx_lens, work, H, Hkv, scale * 1.4426950408889634f,
                      reinterpret_cast<uint16_t*>(out));

@@ -388,8 +388,11 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     return out
 
 
-def prefill_work(cu_q: list[int], qblock: int = 64) -> list[tuple[int, int]]:
-    """(seq, q_start) work items, heaviest (latest) query blocks first for causal balance."""
+def prefill_work(cu_q: list[int], qblock: Optional[int] = None) -> list[tuple[int, int]]:
+    """(seq, q_start) work items of the prefill attention kernel's query block (``ext().prefill_qblock``
+    rows), heaviest (latest) query blocks first for causal balance."""
+    if qblock is None:
+        qblock = ext().prefill_qblock
     items = []
     for s in range(len(cu_q) - 1):
         ql = cu_q[s + 1] - cu_q[s]
