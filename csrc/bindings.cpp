@@ -50,7 +50,7 @@ int lsa_prefill_qblock();
 int lsa_ar_wallclock_khz(int* out);
 int lsa_ar_header_bytes();
 int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
-               int nblocks, long long timeout_ticks, int* err, hipStream_t s);
+               int nblocks, long long timeout_ticks, int* err, int nslab, long slab_stride, hipStream_t s);
 }
 
 namespace {
@@ -300,20 +300,23 @@ int64_t ar_open(const std::string& h) {
 }
 
 void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Tensor& regions, int64_t rank,
-            int64_t maxb, int64_t nblocks, int64_t timeout_ticks, at::Tensor& err) {
+            int64_t maxb, int64_t nblocks, int64_t timeout_ticks, at::Tensor& err, int64_t nslab) {
+  // nslab > 1: data is [nslab, n] split-K slabs; the sum lands in slab 0
   need(data, at::kFloat, "data");
   need(regions, at::kLong, "regions");
   need(err, at::kInt, "err");
-  TORCH_CHECK(data.is_contiguous() && data.numel() % 4 == 0, "all-reduce data: contiguous, numel % 4 == 0");
+  TORCH_CHECK(nslab >= 1 && data.numel() % nslab == 0, "all-reduce: numel must split into nslab slabs");
+  const int64_t n = data.numel() / nslab;
+  TORCH_CHECK(data.is_contiguous() && n % 4 == 0, "all-reduce data: contiguous, slab numel % 4 == 0");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(data.data_ptr()) % 16 == 0, "all-reduce data must be 16-B aligned");
-  TORCH_CHECK(data.numel() * 4 <= maxb, "all-reduce payload exceeds the registered slot size");
+  TORCH_CHECK(n * 4 <= maxb, "all-reduce payload exceeds the registered slot size");
   if (out.has_value()) {
+    TORCH_CHECK(nslab == 1, "all-gather takes one slab");
     need(*out, at::kFloat, "out");
-    TORCH_CHECK(out->is_contiguous() && out->numel() == data.numel() * regions.numel(), "all-gather out size");
+    TORCH_CHECK(out->is_contiguous() && out->numel() == n * regions.numel(), "all-gather out size");
   }
-  check(lsa_ar_run(data.data_ptr<float>(), data.numel(), ptr<float>(out),
-                   reinterpret_cast<uint8_t* const*>(regions.data_ptr()),
-                   rank, regions.numel(), maxb, nblocks, timeout_ticks, err.data_ptr<int>(), cur_stream()),
+  check(lsa_ar_run(data.data_ptr<float>(), n, ptr<float>(out), reinterpret_cast<uint8_t* const*>(regions.data_ptr()),
+                   rank, regions.numel(), maxb, nblocks, timeout_ticks, err.data_ptr<int>(), nslab, n, cur_stream()),
         "ar_run");
 }
 
@@ -355,7 +358,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ar_handle", &ar_handle);
   m.def("ar_open", &ar_open);
   m.def("ar_close", [](int64_t p) { check(lsa_ar_close(reinterpret_cast<void*>(p)), "ar_close"); });
-  m.def("ar_run", &ar_run);
+  m.def("ar_run", &ar_run, py::arg("data"), py::arg("out"), py::arg("regions"), py::arg("rank"), py::arg("maxb"),
+        py::arg("nblocks"), py::arg("timeout_ticks"), py::arg("err"), py::arg("nslab") = 1);
   m.def("ar_wallclock_khz", []() {
     int k = 0;
     check(lsa_ar_wallclock_khz(&k), "ar_wallclock_khz");

@@ -38,13 +38,17 @@ __device__ __forceinline__ void st_release_sys(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// GATHER = 0: in-place sum into data.  GATHER = 1: all-gather, out[p * n4 + i] = rank p's data[i].
+// GATHER = 0: sum into data (slab 0).  GATHER = 1: all-gather, out[p * n4 + i] = rank p's data[i].
+// nslab > 1 (sum only): data holds nslab split-K partial slabs [nslab][n] (slab stride slab4 float4s,
+// e.g. a row-parallel GEMM's f32 split-K output); each rank first sums its own slabs in slab order, so
+// the split-K reduction rides along and the GEMM keeps its split-K parallelism under TP.
 template <int W, int GATHER>
 __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restrict__ data, const long n4,
                                                                  float4* __restrict__ out,
                                                                  uint8_t* const* __restrict__ regions, const int rank,
                                                                  const size_t maxb, const long long timeout_ticks,
-                                                                 int* __restrict__ err) {
+                                                                 int* __restrict__ err, const int nslab,
+                                                                 const long slab4) {
   const int b = blockIdx.x, tid = threadIdx.x;
   uint8_t* mine = regions[rank];
   uint32_t* my_epoch = reinterpret_cast<uint32_t*>(mine + AR_EPOCH_OFF);
@@ -55,9 +59,17 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
   const size_t slot_off = AR_DATA_OFF + (size_t)(ep & 1u) * W * maxb;
   const long stride = (long)gridDim.x * AR_THREADS;
 
+  auto own = [&](long i) {  // this rank's contribution: its slabs summed in slab order
+    float4 v = data[i];
+    for (int sl = 1; sl < nslab; ++sl) {
+      const float4 u = data[(long)sl * slab4 + i];
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    return v;
+  };
   // 1. push this block's chunk into every peer's recv[parity][rank]
   for (long i = (long)b * AR_THREADS + tid; i < n4; i += stride) {
-    const float4 v = data[i];
+    const float4 v = own(i);
 #pragma unroll
     for (int p = 0; p < W; ++p) {
       if (p == rank) continue;
@@ -101,7 +113,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
 #pragma unroll
     for (int p = 0; p < W; ++p) {
       const float4 v = (p == rank)
-                           ? data[i]
+                           ? own(i)
                            : reinterpret_cast<const float4*>(mine + slot_off + (size_t)p * maxb)[i];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
@@ -156,8 +168,9 @@ int lsa_ar_header_bytes() { return AR_DATA_OFF; }
 // data: n floats (n % 4 == 0, 16-B aligned), regions: device array of `world` region pointers;
 // out == nullptr: in-place all-reduce; otherwise all-gather into out[world * n]
 int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
-               int nblocks, long long timeout_ticks, int* err, hipStream_t s) {
+               int nblocks, long long timeout_ticks, int* err, int nslab, long slab_stride, hipStream_t s) {
   if (n % 4 || (size_t)n * 4 > maxb || world < 2 || world > AR_MAX_WORLD || rank < 0 || rank >= world) return -1;
+  if (nslab < 1 || (nslab > 1 && (out || slab_stride % 4 || slab_stride < n))) return -1;
   const long n4 = n / 4;
   long want = (n4 + AR_THREADS - 1) / AR_THREADS;
   int grid = (int)(want < nblocks ? want : nblocks);
@@ -167,10 +180,11 @@ int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int ran
   if (out)                                                                                                     \
     hipLaunchKernelGGL((ar_oneshot_kernel<WV, 1>), dim3(grid), dim3(AR_THREADS), 0, s,                         \
                        reinterpret_cast<float4*>(data), n4, reinterpret_cast<float4*>(out), regions, rank, maxb, \
-                       timeout_ticks, err);                                                                    \
+                       timeout_ticks, err, 1, 0L);                                                             \
   else                                                                                                         \
     hipLaunchKernelGGL((ar_oneshot_kernel<WV, 0>), dim3(grid), dim3(AR_THREADS), 0, s,                         \
-                       reinterpret_cast<float4*>(data), n4, nullptr, regions, rank, maxb, timeout_ticks, err)
+                       reinterpret_cast<float4*>(data), n4, nullptr, regions, rank, maxb, timeout_ticks, err, nslab, \
+                       slab_stride / 4)
   switch (world) {
     case 2: AR_LAUNCH(2); break;
     case 3: AR_LAUNCH(3); break;

@@ -134,13 +134,17 @@ class ModelRunner:
             self.tp.warmup()  # communicators (RCCL + the one-shot IPC all-reduce) before any launch
 
     # ------------------------------------------------------------------------------------ helpers
-    def _allreduce(self, t: torch.Tensor) -> None:
-        if self.tp is not None and self.tp.size > 1:
-            self.tp.all_reduce(t)
+    def _reduce_parts(self, parts: torch.Tensor) -> torch.Tensor:
+        """TP all-reduce of a row-parallel GEMM's split-K slabs; returns what the next add_rmsnorm sums."""
+        if self.tp is None or self.tp.size == 1:
+            return parts
+        return self.tp.reduce_parts(parts)
 
     def _splitk(self, M: int, K: int, N: Optional[int] = None, tp_reduced: bool = True, xf: bool = False) -> int:
-        if not self.on_gpu or M > 64 or (tp_reduced and self.tp is not None and self.tp.size > 1):
+        if not self.on_gpu or M > 64:
             return 1
+        if tp_reduced and self.tp is not None and self.tp.size > 1 and not self.tp.can_fold_splitk(M * self.d):
+            return 1  # RCCL reduces one slab; the one-shot kernel folds split-K slabs into the all-reduce
         return ops.pick_gemm_config(M, N or self.d, K, "f32", xf=xf, kind=self.w.layers[0].wo.kind)[1]
 
     def use_xfrag(self, B: int) -> bool:
@@ -210,7 +214,7 @@ class ModelRunner:
             if l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf)
             else:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_red, rows=B, xf=xf)
             # QKV as f32 split-K slabs; the attention kernel sums them, applies RoPE and appends the new
             # token's k/v to the paged cache itself (no separate rope/append launch)
             lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
@@ -223,12 +227,12 @@ class ModelRunner:
                             qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
                             sin=self.sin if fr else None)
             lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
-            self._allreduce(o_parts)
-            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts, rows=B, xf=xf)
+            o_red = self._reduce_parts(o_parts)
+            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf)
             lin(xn, lw.w_gate_up, "silu", out=act)
             lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
-            self._allreduce(d_parts)
-        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_parts, rows=B, xf=xf)
+            d_red = self._reduce_parts(d_parts)
+        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_red, rows=B, xf=xf)
         logits = self._lm_head(xn, B, xf)
         st = (self.out_tokens[:B], self.gen_len[:B], self.input_ids[:B], self.positions[:B], self.finished[:B])
         if sample:
@@ -431,13 +435,13 @@ class ModelRunner:
             o_parts = ops.linear(attn, lw.wo, "f32", splitk=sk_o)
             if not self.on_gpu:
                 o_parts = o_parts.view(1, T, d)
-            self._allreduce(o_parts)
+            o_parts = self._reduce_parts(o_parts)
             ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
             act = ops.linear(xn, lw.w_gate_up, "silu")
             d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
             if not self.on_gpu:
                 d_parts = d_parts.view(1, T, d)
-            self._allreduce(d_parts)
+            d_parts = self._reduce_parts(d_parts)
         if not commit:
             return None
         xl = torch.empty(n, d, **bf)

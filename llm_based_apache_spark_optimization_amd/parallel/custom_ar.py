@@ -66,6 +66,19 @@ class IpcAllReduce:
         ops.ext().ar_run(t, None, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err)
         return t
 
+    def fits_slabs(self, t: torch.Tensor) -> bool:
+        """t = [nslab, ...] split-K slabs whose per-slab payload fits the slot."""
+        return (t.dtype == torch.float32 and t.is_cuda and t.is_contiguous() and t.dim() >= 2
+                and (t.numel() // t.shape[0]) % 4 == 0 and (t.numel() // t.shape[0]) * 4 <= self.max_bytes
+                and t.data_ptr() % 16 == 0)
+
+    def reduce_slabs(self, t: torch.Tensor) -> torch.Tensor:
+        """Sum over ranks of each rank's slab-sum of t [nslab, ...]; the result lands in t[0] (returned
+        as a [1, ...] view) — split-K partials and the TP all-reduce in one kernel."""
+        ops.ext().ar_run(t, None, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err,
+                         t.shape[0])
+        return t[:1]
+
     def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
         """out[world * n] = concatenation of every rank's t[n] in rank order (same push protocol)."""
         ops.ext().ar_run(t, out, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err)

@@ -28,6 +28,23 @@ class TPGroup:
         else:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
+    def can_fold_splitk(self, slab_numel: int) -> bool:
+        """Whether split-K slabs of slab_numel f32 each can be reduced inside the one-shot all-reduce."""
+        return self.car is not None and slab_numel * 4 <= self.car.max_bytes
+
+    def reduce_parts(self, parts: torch.Tensor) -> torch.Tensor:
+        """All-reduce of the sum of parts [nslab, ...] (row-parallel GEMM split-K slabs); returns the [1, ...]
+        view holding the result."""
+        if parts.shape[0] == 1:
+            self.all_reduce(parts)
+            return parts
+        if self.car is not None and self.car.fits_slabs(parts):
+            return self.car.reduce_slabs(parts)
+        red = parts[:1]
+        red.add_(parts[1:].sum(0, keepdim=True))
+        self.all_reduce(red)
+        return red
+
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         if self.car is not None and self.car.fits(inp) and out.is_contiguous():
             self.car.all_gather(out, inp)

@@ -47,6 +47,19 @@ def _worker(rank, world, port, q):
                 if not torch.equal(t.cpu(), _expected(world, it, n)):
                     errs.append(f"eager n={n} it={it}: max err {(t.cpu() - _expected(world, it, n)).abs().max()}")
                 it += 1
+        for ns, n in ((2, 4096), (4, 32 * 4096), (3, 4100)):  # split-K slabs folded into the all-reduce
+            slabs = [_inputs(rank, it + 100 * k, n) for k in range(ns)]
+            t = torch.stack(slabs).to(dev)
+            red = car.reduce_slabs(t)
+            want = torch.zeros(n)
+            for r in range(world):
+                own = _inputs(r, it, n)
+                for k in range(1, ns):
+                    own = own + _inputs(r, it + 100 * k, n)
+                want = want + own
+            if red.shape[0] != 1 or not torch.equal(red[0].cpu(), want):
+                errs.append(f"slabs ns={ns} n={n} it={it}")
+            it += 1
         for n in (4096, 32 * 16000):  # all-gather (vocab-parallel logits), rank-major output
             t = _inputs(rank, it, n).to(dev)
             out = torch.empty(world * n, device=dev)
