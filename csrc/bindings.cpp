@@ -26,8 +26,8 @@ int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* b
 int lsa_argmax_commit(const float* logits, int B, int V, unsigned long long* part, int* out_tokens, int max_new,
                       int* gen_len, int* input_ids, int* positions, int* finished, const int* eos, int neos,
                       const int* limit, const int* eos_on, hipStream_t s);
-int lsa_sample_commit(float* logits, int B, int V, unsigned long long* part, unsigned long long* cand, const int* hist,
-                      int window, const float* penalty, const float* temperature, const int* top_k,
+int lsa_sample_commit(float* logits, int B, int V, unsigned long long* part, unsigned long long* cand, int* hist,
+                      int window, const float* penalty, const int* last_n, const float* temperature, const int* top_k,
                       const float* top_p, const unsigned long long* seeds, int* out_tokens, int max_new, int* gen_len,
                       int* input_ids, int* positions, int* finished, const int* eos, int neos, const int* limit,
                       const int* eos_on, hipStream_t s);
@@ -255,7 +255,8 @@ void argmax_commit(const at::Tensor& logits, at::Tensor& part, at::Tensor& out_t
 }
 
 void sample_commit(at::Tensor& logits, at::Tensor& part, at::Tensor& cand, const c10::optional<at::Tensor>& hist,
-                   const c10::optional<at::Tensor>& penalty, const at::Tensor& temperature, const at::Tensor& top_k,
+                   const c10::optional<at::Tensor>& penalty, const c10::optional<at::Tensor>& last_n,
+                   const at::Tensor& temperature, const at::Tensor& top_k,
                    const at::Tensor& top_p, const at::Tensor& seeds, at::Tensor& out_tokens, at::Tensor& gen_len,
                    at::Tensor& input_ids, at::Tensor& positions, at::Tensor& finished, const at::Tensor& eos,
                    const at::Tensor& limit, const at::Tensor& eos_on) {
@@ -263,8 +264,8 @@ void sample_commit(at::Tensor& logits, at::Tensor& part, at::Tensor& cand, const
   const int B = logits.size(0), V = logits.size(1);
   const int window = hist.has_value() ? hist->size(1) : 0;
   check(lsa_sample_commit(logits.data_ptr<float>(), B, V, reinterpret_cast<unsigned long long*>(part.data_ptr()),
-                          reinterpret_cast<unsigned long long*>(cand.data_ptr()), ptr<const int>(hist), window,
-                          ptr<const float>(penalty), temperature.data_ptr<float>(), top_k.data_ptr<int>(),
+                          reinterpret_cast<unsigned long long*>(cand.data_ptr()), ptr<int>(hist), window,
+                          ptr<const float>(penalty), ptr<const int>(last_n), temperature.data_ptr<float>(), top_k.data_ptr<int>(),
                           top_p.data_ptr<float>(), reinterpret_cast<const unsigned long long*>(seeds.data_ptr()),
                           out_tokens.data_ptr<int>(), out_tokens.size(1), gen_len.data_ptr<int>(),
                           input_ids.data_ptr<int>(), positions.data_ptr<int>(), finished.data_ptr<int>(),

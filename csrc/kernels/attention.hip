@@ -29,6 +29,7 @@
 #ifndef LSA_ATTN_NT
 #define LSA_ATTN_NT 1  // non-temporal K/V loads in decode attention (read once per step: 3-5 % faster at B = 32)
 #endif
+#define LSA_NT 2    // buffer cache-policy aux bit: nt (streaming)
 #define LSA_SC1 16  // buffer cache-policy aux bit: sc1 (write-through store / L1-bypassing load)
 
 typedef __attribute__((address_space(1))) unsigned long long g_u64;
@@ -61,8 +62,24 @@ struct RopeArgs {
 // so four 4-wave-equivalents fit per CU and a B x Hkv = 1024 grid runs in whole rounds; G = 3: half the
 // per-wave score work on the latency-bound small grids, 3B B=32 ctx 200 11.1 -> 10.0 us), else 4 (the
 // [NLG][G][128] merge buffer of G >= 4 would not fit 64 KiB of LDS with 32 lane groups)
+//
+// G = 1 is capped at 80 VGPRs (6 waves per SIMD = three 8-wave workgroups per CU, 64 spills):
+// the 7B B x Hkv = 1024 workgroups run in 1.33 rounds instead of two (7B B=32 ctx 200: 23.4 -> 21.0 us).
+#ifndef LSA_ATTN_WPE
+#define LSA_ATTN_WPE 6
+#endif
+#ifndef LSA_ATTN_BUF_G
+#define LSA_ATTN_BUF_G 2
+#endif
+#ifndef LSA_ATTN_NEWREG_G
+#define LSA_ATTN_NEWREG_G 3
+#endif
+#ifndef LSA_ATTN_DOT2_G
+#define LSA_ATTN_DOT2_G 99
+#endif
 template <int G, int ROPE, int WV>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime slab count
-__global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+__global__ __launch_bounds__(64 * WV)
+__attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc,
                                                           const int* __restrict__ block_tables, int max_blocks,
                                                           const int* __restrict__ pos, int Hkv, float scale_log2,
@@ -86,18 +103,27 @@ __global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __
   uint4 kA[TU], vA[TU], kB[TU], vB[TU];
   // keys past the context in the last block re-read the last valid row (a cache hit, not HBM traffic);
   // they are masked in the score
+  // G >= LSA_ATTN_BUF_G: one buffer resource per (block, kv-head) slab, built in SGPRs from the uniform
+  // block-table entry, the lanes carry 32-bit offsets (3B: 10.3 -> 9.8 us at B = 32); G = 1 keeps 64-bit
+  // global loads (buffer loads measured 20.7 -> 22.4 us for the 7B at B = 32)
+  constexpr bool BUF = G >= LSA_ATTN_BUF_G;
   auto fetch = [&](uint4 (&kr)[TU], uint4 (&vr)[TU], int blk, int last_tok) {
-    const size_t base = ((size_t)bt[blk] * Hkv + hk) * 64 * D;
+    const size_t base = ((size_t)__builtin_amdgcn_readfirstlane(bt[blk]) * Hkv + hk) * 64 * D;
 #pragma unroll
     for (int u = 0; u < TU; ++u) {
       const int tok = min(wv * TW + u * 4 + (lg & 3), last_tok);
-#if LSA_ATTN_NT
-      kr[u] = ldg_nt(reinterpret_cast<const uint4*>(kc + base + tok * D + li * 8));
-      vr[u] = ldg_nt(reinterpret_cast<const uint4*>(vc + base + tok * D + li * 8));
-#else
-      kr[u] = *reinterpret_cast<const uint4*>(kc + base + tok * D + li * 8);
-      vr[u] = *reinterpret_cast<const uint4*>(vc + base + tok * D + li * 8);
-#endif
+      if constexpr (BUF) {
+        const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)(kc + base), 0, 64 * D * 2, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(vc + base), 0, 64 * D * 2, 0x00020000);
+        const int off = (tok * D + li * 8) * 2;
+        const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(rk, off, 0, LSA_ATTN_NT ? LSA_NT : 0);
+        const u32x4_t c = __builtin_amdgcn_raw_buffer_load_b128(rv, off, 0, LSA_ATTN_NT ? LSA_NT : 0);
+        kr[u] = make_uint4(a[0], a[1], a[2], a[3]);
+        vr[u] = make_uint4(c[0], c[1], c[2], c[3]);
+      } else {
+        kr[u] = ldg_nt(reinterpret_cast<const uint4*>(kc + base + tok * D + li * 8));
+        vr[u] = ldg_nt(reinterpret_cast<const uint4*>(vc + base + tok * D + li * 8));
+      }
     }
   };
   // split 0 always starts at block 0, which every sequence owns (padding rows map it to the scratch
@@ -118,14 +144,20 @@ __global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __
   __builtin_amdgcn_sched_barrier(0);
 
   const int tpos = ctx - 1;  // position of the new token
-  float qf[G][8];
-  float knew[8], vnew[8];
+  // q, and the new token's k / v, stay packed bf16 (the dot products run on v_dot2c_f32_bf16 and the
+  // softmax scale is applied to the reduced score): 12 VGPRs instead of 24 f32 for G = 1
+  uint4 qb[G];
+  // the new token's rotated k / v: for G < LSA_ATTN_NEWREG_G they stay in LDS (read back by the one lane
+  // group that meets position tpos: 8 VGPRs fewer in the score loop), else in registers (a select instead
+  // of a branch around an LDS read)
+  constexpr bool NEWREG = G >= LSA_ATTN_NEWREG_G;
+  __shared__ uint4 qkv_s[G + 2][16];
+  uint4 knew = make_uint4(0, 0, 0, 0), vnew = make_uint4(0, 0, 0, 0);
   if constexpr (ROPE != 0) {
     // lane group j < G builds query head j, group G the new key, group G + 1 the new value (each lane
     // 8 dims, summed over the split-K slabs, rotated in f32, rounded to bf16 like the unfused path);
     // the results go through LDS to all lane groups
     static_assert(G + 2 <= NLG, "fused rope: one lane group per q head + k + v");
-    __shared__ __attribute__((aligned(16))) float qkv_s[G + 2][D];
     if (lg < G + 2) {
       const float* row = ra.parts + (size_t)b * (H + 2 * Hkv) * D;
       const int dd = li * 8;  // own 8 dims; the rotate-half partners live in lane li ^ 8
@@ -158,9 +190,7 @@ __global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __
         for (int j = 0; j < 8; ++j) y[j] = x[j];
       }
       const uint4 yq = pack8(y);
-      unpack8(yq, y);
-      *reinterpret_cast<float4*>(&qkv_s[lg][dd]) = make_float4(y[0], y[1], y[2], y[3]);
-      *reinterpret_cast<float4*>(&qkv_s[lg][dd + 4]) = make_float4(y[4], y[5], y[6], y[7]);
+      qkv_s[lg][li] = yq;
       // the workgroup covering position tpos appends the new token's k / v to the cache
       if (lg >= G && blk0 < nblk && blk1 == nblk) {
         const size_t co = (((size_t)block_tables[(size_t)b * max_blocks + (tpos >> 6)] * Hkv + hk) * 64 +
@@ -170,20 +200,23 @@ __global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __
     }
     __syncthreads();
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[g][j] = qkv_s[g][li * 8 + j] * scale_log2;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      knew[j] = qkv_s[G][li * 8 + j];
-      vnew[j] = qkv_s[G + 1][li * 8 + j];
+    for (int g = 0; g < G; ++g) qb[g] = qkv_s[g][li];
+    if constexpr (NEWREG) {
+      knew = qkv_s[G][li];
+      vnew = qkv_s[G + 1][li];
     }
   } else {
 #pragma unroll
+    for (int g = 0; g < G; ++g) qb[g] = *reinterpret_cast<const uint4*>(q + ((size_t)(b * H + hk * G + g)) * D + li * 8);
+  }
+  // G < LSA_ATTN_DOT2_G: scores on v_dot2c_f32_bf16 from the packed q (fewest VGPRs); else q in f32,
+  // pre-scaled, and each key unpacked once for all G heads
+  constexpr bool DOT2 = G < LSA_ATTN_DOT2_G;
+  float qf[DOT2 ? 1 : G][8];
+  if constexpr (!DOT2) {
+#pragma unroll
     for (int g = 0; g < G; ++g) {
-      const uint4 v = *reinterpret_cast<const uint4*>(q + ((size_t)(b * H + hk * G + g)) * D + li * 8);
-      unpack8(v, qf[g]);
+      unpack8(qb[g], qf[g]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[g][j] *= scale_log2;
     }
@@ -201,26 +234,29 @@ __global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __
     float s[TU][G];
 #pragma unroll
     for (int u = 0; u < TU; ++u) {
-      float kf[8];
-      unpack8(kr[u], kf);
+      uint4 kq = kr[u];
       const int tp = blk * 64 + wv * TW + u * 4 + (lg & 3);
       const bool valid = tp < ctx;
       if constexpr (ROPE != 0) {
-        if (tp == tpos) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) kf[j] = knew[j];
-        }
+        if (tp == tpos) kq = NEWREG ? knew : qkv_s[G][li];
       }
+      float kf[8];
+      if constexpr (!DOT2) unpack8(kq, kf);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        float d = 0.f;
+        float d;
+        if constexpr (DOT2) {
+          d = dot8_bf16(qb[g], kq);
+        } else {
+          d = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d = fmaf(qf[g][j], kf[j], d);
+          for (int j = 0; j < 8; ++j) d = fmaf(qf[g][j], kf[j], d);
+        }
         d += __shfl_xor(d, 8, 64);
         d += __shfl_xor(d, 4, 64);
         d += __shfl_xor(d, 2, 64);
         d += __shfl_xor(d, 1, 64);
-        s[u][g] = valid ? d : LSA_NEG;
+        s[u][g] = valid ? (DOT2 ? d * scale_log2 : d) : LSA_NEG;
       }
     }
 #pragma unroll
@@ -242,14 +278,12 @@ __global__ __launch_bounds__(64 * WV) void attn_decode_kernel(const uint16_t* __
       for (int j = 0; j < 8; ++j) o[g][j] *= alpha;
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
-        float vf[8];
-        unpack8(vr[u], vf);
+        uint4 vq = vr[u];
         if constexpr (ROPE != 0) {
-          if (blk * 64 + wv * TW + u * 4 + (lg & 3) == tpos) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) vf[j] = vnew[j];
-          }
+          if (blk * 64 + wv * TW + u * 4 + (lg & 3) == tpos) vq = NEWREG ? vnew : qkv_s[G + 1][li];
         }
+        float vf[8];
+        unpack8(vq, vf);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[g][j] = fmaf(p[u], vf[j], o[g][j]);
       }

@@ -48,6 +48,16 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return r;
 }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// dot product of 8 bf16 pairs on v_dot2c_f32_bf16 (f32 accumulate), no unpacking
+__device__ __forceinline__ float dot8_bf16(const uint4 a, const uint4 b) {
+  float d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a.x), __builtin_bit_cast(bf16x2_t, b.x), 0.f, false);
+  d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a.y), __builtin_bit_cast(bf16x2_t, b.y), d, false);
+  d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a.z), __builtin_bit_cast(bf16x2_t, b.z), d, false);
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a.w), __builtin_bit_cast(bf16x2_t, b.w), d, false);
+}
+
 __device__ __forceinline__ f32x4_t mfma16x16x32(const uint4 a, const uint4 b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);

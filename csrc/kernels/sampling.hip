@@ -54,6 +54,8 @@ struct DecodeState {
   int neos;
   const int* limit;   // [B] per-row max new tokens (<= max_new)
   const int* eos_on;  // [B] 0 = ignore EOS for this row
+  int* hist;          // [B, window] ring of the context's last tokens (slot = position % window), or null
+  int window;
 };
 
 __device__ void commit_token(const DecodeState& st, int b, int tok) {
@@ -65,6 +67,7 @@ __device__ void commit_token(const DecodeState& st, int b, int tok) {
   if (st.eos_on[b])
     for (int e = 0; e < st.neos; ++e) done |= (tok == st.eos[e]);
   st.input_ids[b] = tok;
+  if (st.hist) st.hist[(size_t)b * st.window + (st.positions[b] + 1) % st.window] = tok;  // its position
   if (done) {
     st.finished[b] = 1;
   } else {
@@ -109,23 +112,29 @@ __device__ void bitonic_desc(unsigned long long* a, int n) {
   }
 }
 
-// repetition penalty applied in place to the logits of the last `window` generated/prompt tokens
+// repetition penalty applied in place (llama.cpp / Ollama semantics: logit / pen if > 0, else * pen) to
+// each distinct token among the row's last `last_n` context tokens (prompt + generated), read from the
+// position-indexed ring `hist` ending at the current input position
 __global__ __launch_bounds__(64) void repeat_penalty_kernel(float* __restrict__ logits, int V,
                                                             const int* __restrict__ hist, int window,
-                                                            const float* __restrict__ penalty) {
+                                                            const float* __restrict__ penalty,
+                                                            const int* __restrict__ last_n,
+                                                            const int* __restrict__ positions) {
   const int b = blockIdx.x;
   const float pen = penalty[b];
   if (pen == 1.0f) return;
   const int* hrow = hist + (size_t)b * window;
-  for (int i = threadIdx.x; i < window; i += 64) {
-    const int t = hrow[i];
+  const int p = positions[b];
+  const int n = min(min(last_n ? last_n[b] : window, window), p + 1);
+  for (int i = threadIdx.x; i < n; i += 64) {
+    const int t = hrow[(p - i) % window];
     if (t < 0 || t >= V) continue;
-    bool first = true;
-    for (int k = 0; k < i; ++k) first &= (hrow[k] != t);
+    bool first = true;  // the most recent occurrence applies the penalty, once per distinct token
+    for (int k = 0; k < i; ++k) first &= (hrow[(p - k) % window] != t);
     if (!first) continue;
-    float* p = logits + (size_t)b * V + t;
-    const float v = *p;
-    *p = v > 0.f ? v / pen : v * pen;
+    float* q = logits + (size_t)b * V + t;
+    const float v = *q;
+    *q = v > 0.f ? v / pen : v * pen;
   }
 }
 
@@ -233,20 +242,22 @@ extern "C" int lsa_argmax_commit(const float* logits, int B, int V, unsigned lon
   const int chunk = 4096;
   const int nch = (V + chunk - 1) / chunk;
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(nch, B), dim3(256), 0, s, logits, V, chunk, part, nch);
-  DecodeState st{out_tokens, max_new, gen_len, input_ids, positions, finished, eos, neos, limit, eos_on};
+  DecodeState st{out_tokens, max_new, gen_len, input_ids, positions, finished, eos, neos, limit, eos_on, nullptr, 0};
   hipLaunchKernelGGL(argmax_commit_kernel, dim3(B), dim3(64), 0, s, part, nch, st);
   return (int)hipGetLastError();
 }
 
 // workspace: part (B * ceil(V/4096) u64) + cand (B * ceil(V/2048) * 64 u64)
 extern "C" int lsa_sample_commit(float* logits, int B, int V, unsigned long long* part, unsigned long long* cand,
-                                 const int* hist, int window, const float* penalty, const float* temperature,
+                                 int* hist, int window, const float* penalty, const int* last_n,
+                                 const float* temperature,
                                  const int* top_k, const float* top_p, const unsigned long long* seeds,
                                  int* out_tokens, int max_new, int* gen_len, int* input_ids, int* positions,
                                  int* finished, const int* eos, int neos, const int* limit, const int* eos_on,
                                  hipStream_t s) {
   if (hist && window > 0 && penalty)
-    hipLaunchKernelGGL(repeat_penalty_kernel, dim3(B), dim3(64), 0, s, logits, V, hist, window, penalty);
+    hipLaunchKernelGGL(repeat_penalty_kernel, dim3(B), dim3(64), 0, s, logits, V, hist, window, penalty, last_n,
+                       positions);
   const int chunk = 4096;
   const int nch = (V + chunk - 1) / chunk;
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(nch, B), dim3(256), 0, s, logits, V, chunk, part, nch);
@@ -256,7 +267,8 @@ extern "C" int lsa_sample_commit(float* logits, int B, int V, unsigned long long
   int p2 = 64;
   while (p2 < ncand) p2 <<= 1;
   if (p2 > 8192) return -1;  // V > 262144 unsupported
-  DecodeState st{out_tokens, max_new, gen_len, input_ids, positions, finished, eos, neos, limit, eos_on};
+  DecodeState st{out_tokens, max_new, gen_len, input_ids, positions, finished, eos, neos, limit, eos_on,
+                 window > 0 ? hist : nullptr, window};
   hipLaunchKernelGGL(sample_commit_kernel, dim3(B), dim3(1024), p2 * sizeof(unsigned long long), s, cand, p2, ncand,
                      part, nch, temperature, top_k, top_p, seeds, st);
   return (int)hipGetLastError();

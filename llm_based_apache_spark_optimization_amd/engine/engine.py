@@ -38,6 +38,15 @@ class SamplingParams:
     seed: Optional[int] = None
     ignore_eos: bool = False
     stop: tuple = ()
+    # llama.cpp/Ollama repetition penalty over the last repeat_last_n (<= 64) context tokens.  1.0 = off
+    # unless a request sets it (Ollama's own default is 1.1; the benchmark configs are plain greedy)
+    repeat_penalty: float = 1.0
+    repeat_last_n: int = 64
+
+    @property
+    def needs_sampler(self) -> bool:
+        """Rows that need the sampling path (draw and/or penalty) rather than the argmax-only graph."""
+        return self.temperature > 0 or self.repeat_penalty != 1.0
 
     @staticmethod
     def from_ollama_options(opts: Optional[dict], default_max: int = 128) -> "SamplingParams":
@@ -49,7 +58,9 @@ class SamplingParams:
         # ignore_eos: benchmark extension (fixed-length outputs from random-init weights), not an Ollama option
         return SamplingParams(max_tokens=int(n), temperature=float(opts.get("temperature", 0.0)),
                               top_k=int(opts.get("top_k", 40)), top_p=float(opts.get("top_p", 0.9)),
-                              seed=opts.get("seed"), stop=tuple(stop), ignore_eos=bool(opts.get("ignore_eos", False)))
+                              seed=opts.get("seed"), stop=tuple(stop), ignore_eos=bool(opts.get("ignore_eos", False)),
+                              repeat_penalty=float(opts.get("repeat_penalty", 1.0)),
+                              repeat_last_n=int(opts.get("repeat_last_n", 64)))
 
 
 @dataclasses.dataclass
@@ -147,8 +158,9 @@ class LLMEngine:
                     sp = req.params
                     seed = sp.seed if sp.seed is not None else (rid * 7919 + 17)
                     r.set_slot(slot, self.sched.block_table(rid), sp.max_tokens, sp.temperature, sp.top_k, sp.top_p,
-                               seed, eos_on=not sp.ignore_eos)
-                    any_sample |= sp.temperature > 0
+                               seed, eos_on=not sp.ignore_eos, repeat_penalty=sp.repeat_penalty,
+                               repeat_last_n=sp.repeat_last_n, prompt_ids=req.prompt_ids)
+                    any_sample |= sp.needs_sampler
                     seqs.append((slot, req.prompt_ids, 0))
                 self._prefill_packed(seqs, any_sample)
                 t1 = time.perf_counter()
@@ -161,7 +173,7 @@ class LLMEngine:
             if not running:
                 return []
             B = r.bucket(self.sched.highest_slot + 1)
-            sample = any(self._reqs[rid].params.temperature > 0 for rid in running)
+            sample = any(self._reqs[rid].params.needs_sampler for rid in running)
             # steps until the earliest request can hit its length limit; with EOS possible, at most
             # sync_every steps between host checks
             reqs = [self._reqs[rid] for rid in running]

@@ -31,7 +31,7 @@ from ..models.llama import LlamaWeights
 from ..ops import reference as ref
 
 BLOCK = 64
-SAMPLE_HIST = 64  # repetition-penalty window (Ollama repeat_last_n default)
+REPEAT_WINDOW = 64  # repetition-penalty ring (Ollama repeat_last_n default; larger values are clamped)
 
 
 class ModelRunner:
@@ -101,6 +101,11 @@ class ModelRunner:
         self.top_k = torch.full((S,), 40, **i32)
         self.top_p = torch.full((S,), 0.9, dtype=torch.float32, device=dev)
         self.seeds = torch.zeros(S, dtype=torch.int64, device=dev)
+        # repetition penalty (Ollama repeat_penalty / repeat_last_n): per-row ring of the context's last
+        # REPEAT_WINDOW tokens, indexed by position, written by the sampling commit
+        self.penalty = torch.ones(S, dtype=torch.float32, device=dev)
+        self.last_n = torch.full((S,), REPEAT_WINDOW, **i32)
+        self.hist = torch.full((S, REPEAT_WINDOW), -1, **i32)
         self.eos_list = list(spec.eos_ids) or [-1]
         self.eos = torch.tensor(self.eos_list, **i32)
 
@@ -236,9 +241,10 @@ class ModelRunner:
         logits = self._lm_head(xn, B, xf)
         st = (self.out_tokens[:B], self.gen_len[:B], self.input_ids[:B], self.positions[:B], self.finished[:B])
         if sample:
-            ops.sample_commit(logits, None, None, self.temperature[:B], self.top_k[:B], self.top_p[:B],
-                              self.seeds[:B], *st, self.eos, self.limit[:B], self.eos_on[:B],
-                              workspace=(self.amax_part, self.cand) if self.on_gpu else None)
+            ops.sample_commit(logits, self.hist[:B], self.penalty[:B], self.temperature[:B], self.top_k[:B],
+                              self.top_p[:B], self.seeds[:B], *st, self.eos, self.limit[:B], self.eos_on[:B],
+                              workspace=(self.amax_part, self.cand) if self.on_gpu else None,
+                              last_n=self.last_n[:B])
         else:
             ops.argmax_commit(logits, *st, self.eos, self.limit[:B], self.eos_on[:B],
                               part=self.amax_part if self.on_gpu else None)
@@ -312,7 +318,8 @@ class ModelRunner:
 
     # ------------------------------------------------------------------------------------ slots
     def set_slot(self, slot: int, blocks: Sequence[int], limit: int, temperature: float = 0.0, top_k: int = 40,
-                 top_p: float = 0.9, seed: int = 0, eos_on: bool = True) -> None:
+                 top_p: float = 0.9, seed: int = 0, eos_on: bool = True, repeat_penalty: float = 1.0,
+                 repeat_last_n: int = REPEAT_WINDOW, prompt_ids: Sequence[int] = ()) -> None:
         row = torch.zeros(self.max_blocks, dtype=torch.int32)
         row[: len(blocks)] = torch.tensor(list(blocks), dtype=torch.int32)
         self.block_tables[slot].copy_(row.to(self.device, non_blocking=True))
@@ -322,6 +329,13 @@ class ModelRunner:
         self.top_p[slot] = float(top_p)
         self.seeds[slot] = int(seed)
         self.eos_on[slot] = 1 if eos_on else 0
+        self.penalty[slot] = float(repeat_penalty)
+        self.last_n[slot] = max(0, min(int(repeat_last_n), REPEAT_WINDOW))
+        if repeat_penalty != 1.0:  # seed the ring with the prompt's last tokens (token at p -> column p % W)
+            ring = torch.full((REPEAT_WINDOW,), -1, dtype=torch.int32)
+            for p in range(max(0, len(prompt_ids) - REPEAT_WINDOW), len(prompt_ids)):
+                ring[p % REPEAT_WINDOW] = int(prompt_ids[p])
+            self.hist[slot].copy_(ring.to(self.device, non_blocking=True))
 
     def set_eos(self, ids: Sequence[int]) -> None:
         """Replace the stop-token set (same length keeps captured graphs valid; otherwise recapture)."""
@@ -402,9 +416,13 @@ class ModelRunner:
         lim = self.limit.index_select(0, slot_t)
         eon = self.eos_on.index_select(0, slot_t)
         if sample_any:
-            ops.sample_commit(logits, None, None, self.temperature.index_select(0, slot_t),
+            hist = self.hist.index_select(0, slot_t)
+            ops.sample_commit(logits, hist, self.penalty.index_select(0, slot_t),
+                              self.temperature.index_select(0, slot_t),
                               self.top_k.index_select(0, slot_t), self.top_p.index_select(0, slot_t),
-                              self.seeds.index_select(0, slot_t), out_t, gl, iid, pp, fin, self.eos, lim, eon)
+                              self.seeds.index_select(0, slot_t), out_t, gl, iid, pp, fin, self.eos, lim, eon,
+                              last_n=self.last_n.index_select(0, slot_t))
+            self.hist.index_copy_(0, slot_t, hist)
         else:
             ops.argmax_commit(logits, out_t, gl, iid, pp, fin, self.eos, lim, eon)
         self.out_tokens.index_copy_(0, slot_t, out_t)

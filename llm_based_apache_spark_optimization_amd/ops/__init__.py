@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import dataclasses
 import importlib
+import importlib.util
 import json
 import os
 from typing import Optional
@@ -32,7 +33,13 @@ def ext():
     global _ext, _ext_err
     if _ext is None and _ext_err is None:
         try:
-            _ext = importlib.import_module(__name__ + "._lsa_hip")
+            alt = os.environ.get("LSA_HIP_SO")  # experiment knob: an alternative build of the same extension
+            if alt:
+                spec = importlib.util.spec_from_file_location("_lsa_hip", alt)
+                _ext = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(_ext)
+            else:
+                _ext = importlib.import_module(__name__ + "._lsa_hip")
         except BaseException as e:  # noqa: BLE001 - record and re-raise on use
             _ext_err = e
     if _ext is None:
@@ -434,17 +441,22 @@ def argmax_commit(logits, out_tokens, gen_len, input_ids, positions, finished, e
 
 
 def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len, input_ids,
-                  positions, finished, eos, limit=None, eos_on=None, workspace=None):
-    """Temperature / top-k / top-p draw (+ optional repetition penalty) + decode-state update."""
+                  positions, finished, eos, limit=None, eos_on=None, workspace=None, last_n=None):
+    """Temperature / top-k / top-p draw (+ optional repetition penalty) + decode-state update.
+
+    ``hist`` [B, W] int32 is the ring of each row's last W context tokens (token at position p in column
+    p % W, -1 = empty); with it, rows whose ``penalty`` != 1 have the logits of the distinct tokens among
+    their last ``last_n`` (<= W, default W) positions penalised (Ollama ``repeat_penalty`` /
+    ``repeat_last_n``), and the committed token is written into the ring.  ``logits`` is modified."""
     B, V = logits.shape
     limit, eos_on = _row_defaults(B, out_tokens, limit, eos_on)
     if not _gpu(logits):
         return ref.sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len,
-                                 input_ids, positions, finished, eos, limit, eos_on)
+                                 input_ids, positions, finished, eos, limit, eos_on, last_n=last_n)
     if workspace is None:
         part = torch.empty(B * ((V + 4095) // 4096), device=logits.device, dtype=torch.int64)
         cand = torch.empty(B * ((V + 2047) // 2048) * 64, device=logits.device, dtype=torch.int64)
     else:
         part, cand = workspace
-    ext().sample_commit(logits, part, cand, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len,
-                        input_ids, positions, finished, eos, limit, eos_on)
+    ext().sample_commit(logits, part, cand, hist, penalty, last_n, temperature, top_k, top_p, seeds, out_tokens,
+                        gen_len, input_ids, positions, finished, eos, limit, eos_on)

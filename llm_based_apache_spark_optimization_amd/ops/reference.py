@@ -127,7 +127,7 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out):
     return out
 
 
-def commit(tok, out_tokens, gen_len, input_ids, positions, finished, eos, limit=None, eos_on=None):
+def commit(tok, out_tokens, gen_len, input_ids, positions, finished, eos, limit=None, eos_on=None, hist=None):
     eos_set = set(eos.tolist()) if eos is not None else set()
     max_new = out_tokens.shape[1]
     for b in range(tok.shape[0]):
@@ -139,6 +139,8 @@ def commit(tok, out_tokens, gen_len, input_ids, positions, finished, eos, limit=
             out_tokens[b, n] = t
         gen_len[b] = n + 1
         input_ids[b] = t
+        if hist is not None:  # position-indexed ring of the context's last tokens
+            hist[b, (int(positions[b]) + 1) % hist.shape[1]] = t
         lim = min(max_new, int(limit[b])) if limit is not None else max_new
         use_eos = bool(int(eos_on[b])) if eos_on is not None else True
         if n + 1 >= lim or (use_eos and t in eos_set):
@@ -164,16 +166,27 @@ def sample_probs(logits_row: torch.Tensor, temperature: float, top_k: int, top_p
     return idx, p / p.sum()
 
 
+def repeat_penalty(row, hist_row, pen, pos, last_n):
+    """llama.cpp/Ollama repetition penalty on one row of logits over the distinct tokens at context
+    positions (pos - last_n, pos] of the position-indexed ring ``hist_row``."""
+    W = hist_row.numel()
+    n = min(W if last_n is None else int(last_n), W, pos + 1)
+    for t in {int(hist_row[(pos - i) % W]) for i in range(n)}:
+        if 0 <= t < row.numel():
+            row[t] = row[t] / pen if row[t] > 0 else row[t] * pen
+    return row
+
+
 def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len, input_ids,
-                  positions, finished, eos, limit=None, eos_on=None, generator: torch.Generator | None = None):
+                  positions, finished, eos, limit=None, eos_on=None, generator: torch.Generator | None = None,
+                  last_n=None):
     B = logits.shape[0]
     toks = torch.empty(B, dtype=torch.long)
     for b in range(B):
         row = logits[b].float().clone()
         if hist is not None and penalty is not None and float(penalty[b]) != 1.0:
-            pen = float(penalty[b])
-            for t in set(int(x) for x in hist[b].tolist() if 0 <= int(x) < row.numel()):
-                row[t] = row[t] / pen if row[t] > 0 else row[t] * pen
+            row = repeat_penalty(row, hist[b].cpu(), float(penalty[b]), int(positions[b]),
+                                 None if last_n is None else int(last_n[b]))
         T = float(temperature[b])
         if T <= 0:
             toks[b] = int(row.argmax())
@@ -182,4 +195,4 @@ def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_t
         if generator is None:
             generator = torch.Generator().manual_seed(int(seeds[b]) + int(gen_len[b]))
         toks[b] = int(idx[torch.multinomial(p.cpu(), 1, generator=generator)])
-    commit(toks, out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on)
+    commit(toks, out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on, hist=hist)

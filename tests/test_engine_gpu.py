@@ -197,3 +197,24 @@ def test_tensor_parallel_kernels_gpu(gpu, graphs):
     assert got_sp[0] == got_sp[1]
     agree_sp = sum(a == b for x, y in zip(got_sp[0], got[0]) for a, b in zip(x, y))
     assert agree_sp >= 10, (got_sp[0], got[0])  # SP vs all-reduce prefill: same math, other sum order
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_repeat_penalty_hf_parity_gpu(gpu, graphs):
+    """repeat_penalty through the captured sampling graph (greedy rows) vs HF-semantics penalised
+    teacher-forced logits; the context stays inside the 64-token window."""
+    spec, m = _hf("tiny-llama3")
+    w = from_hf_state_dict(spec, m.state_dict(), gpu)
+    eng = LLMEngine(ModelRunner(w, max_slots=4, max_model_len=256, use_graphs=graphs))
+    prompts = [[1] + [7, 9, 7, 11, 13, 9, 7, 21, 9, 7], [1] + list(range(40, 60))]
+    pen = 1.8
+    res = eng.generate(prompts, SamplingParams(max_tokens=14, ignore_eos=True, repeat_penalty=pen))
+    for p, r in zip(prompts, res):
+        with torch.no_grad():
+            lg = m(torch.tensor([p + r.token_ids])).logits[0, len(p) - 1:-1].float()
+        for i, t in enumerate(r.token_ids):
+            row = lg[i].clone()
+            seen = torch.tensor(sorted(set(p + r.token_ids[:i])))
+            s = row[seen]
+            row[seen] = torch.where(s < 0, s * pen, s / pen)
+            assert row.max() - row[t] <= 0.05 * row.max().abs() + 0.05, (i, t, int(row.argmax()))

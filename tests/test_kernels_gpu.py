@@ -452,3 +452,42 @@ def test_sample_greedy_rows(gpu):
     st = _state(B, 3, gpu)
     ops.sample_commit(logits, None, None, temp, topk, topp, seeds, *st, eos)
     assert torch.equal(st[0][:, 0].long(), logits.argmax(-1))
+
+
+def test_repeat_penalty_ring_matches_reference(gpu):
+    """Repetition penalty over the position-indexed history ring (greedy rows, so deterministic) and the
+    ring write of the committed token, vs the fp32 reference."""
+    V, B, W = 32000, 6, 64
+    torch.manual_seed(3)
+    logits = torch.randn(B, V) * 3
+    hist = torch.randint(0, V, (B, W), dtype=torch.int32)
+    hist[1, 10:] = -1
+    hist[2, :] = hist[2, 0]                                   # one token repeated: penalised once
+    pos = torch.tensor([5, 9, 200, 63, 64, 1000], dtype=torch.int32)
+    pen = torch.tensor([1.3, 2.0, 1.5, 1.0, 0.7, 1.1])
+    last_n = torch.tensor([64, 64, 64, 64, 8, 3], dtype=torch.int32)
+    # make the penalty decide the argmax: each row's top logit sits on one of its recent tokens
+    for b in range(B):
+        t = int(hist[b, int(pos[b]) % W])
+        if t >= 0:
+            logits[b, t] = logits[b].max() + 0.1
+    temp = torch.zeros(B)
+    topk = torch.full((B,), 40, dtype=torch.int32)
+    topp = torch.ones(B)
+    seeds = torch.zeros(B, dtype=torch.int64)
+    eos = torch.tensor([-1], dtype=torch.int32)
+
+    def run(dev):
+        st = [x.to(dev) for x in _state(B, 4, "cpu")]
+        st[3].copy_(pos.to(dev))
+        h = hist.to(dev).clone()
+        ops.sample_commit(logits.to(dev).clone(), h, pen.to(dev), temp.to(dev), topk.to(dev), topp.to(dev),
+                          seeds.to(dev), *st, eos.to(dev), last_n=last_n.to(dev))
+        return st[0][:, 0].cpu(), h.cpu()
+
+    tg, hg = run(gpu)
+    tc, hc = run("cpu")
+    assert torch.equal(tg, tc)
+    assert torch.equal(hg, hc)
+    for b in range(B):  # the committed token landed at column (pos + 1) % W
+        assert int(hg[b, (int(pos[b]) + 1) % W]) == int(tg[b])

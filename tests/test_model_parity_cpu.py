@@ -66,3 +66,28 @@ def test_llama3_scaling_changes_low_frequencies():
     c0, _ = ref.rope_tables(128, 20000, 500000.0, None)
     assert torch.allclose(c[:, :8], c0[:, :8], atol=1e-6)
     assert not torch.allclose(c[-1, -4:], c0[-1, -4:])
+
+
+@pytest.mark.parametrize("name", ["tiny-nsql", "tiny-llama3"])
+def test_repeat_penalty_matches_transformers(name):
+    """Ollama's repeat_penalty through the engine (greedy, context < the 64-token window) vs HF's
+    RepetitionPenaltyLogitsProcessor semantics applied to teacher-forced transformers logits."""
+    spec, m = hf_model(name)
+    eng = LLMEngine(ModelRunner(from_hf_state_dict(spec, m.state_dict(), "cpu"), max_slots=2, max_model_len=256))
+    p = [1] + [7, 9, 7, 11, 13, 9, 7, 21, 9, 7]
+    pen = 1.8
+    r = eng.generate([p], SamplingParams(max_tokens=14, ignore_eos=True, repeat_penalty=pen))[0]
+    with torch.no_grad():
+        lg = m(torch.tensor([p + r.token_ids])).logits[0, len(p) - 1:-1]
+    for i, t in enumerate(r.token_ids):
+        row = lg[i].clone()
+        seen = torch.tensor(sorted(set(p + r.token_ids[:i])))
+        s = row[seen]
+        row[seen] = torch.where(s < 0, s * pen, s / pen)
+        assert row.max() - row[t] <= 0.05 * row.max().abs() + 0.05, (i, t, int(row.argmax()))
+
+
+def test_repeat_penalty_ollama_options():
+    sp = SamplingParams.from_ollama_options({"repeat_penalty": 1.1, "repeat_last_n": 32, "temperature": 0})
+    assert sp.repeat_penalty == 1.1 and sp.repeat_last_n == 32 and sp.needs_sampler
+    assert not SamplingParams.from_ollama_options({}).needs_sampler
