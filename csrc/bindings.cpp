@@ -16,8 +16,8 @@ int lsa_rope_append(const void* qkv, const float* qkv_parts, int nparts, long pa
                     hipStream_t s);
 int lsa_silu_mul(const void* g, const void* u, void* o, long n, hipStream_t s);
 int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
-                    const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit, void* out,
-                    float* opart, float* mlpart, int* counters, int xf_mt, const float* qkv_parts, int nparts,
+                    const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit, int unsplit_max,
+                    void* out, float* opart, float* mlpart, int* counters, int xf_mt, const float* qkv_parts, int nparts,
                     long part_stride,
                     const float* cos_t, const float* sin_t, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
@@ -202,7 +202,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                  const at::Tensor& pos, int64_t H, int64_t Hkv, double scale, int64_t chunk_blocks, int64_t nsplit,
                  at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, at::Tensor& counters, int64_t xf_mt,
                  const c10::optional<at::Tensor>& qkv_parts, const c10::optional<at::Tensor>& cos_t,
-                 const c10::optional<at::Tensor>& sin_t) {
+                 const c10::optional<at::Tensor>& sin_t, int64_t unsplit_max) {
   need(q, at::kBFloat16, "q");
   need(pos, at::kInt, "pos");
   const int B = pos.size(0);
@@ -224,7 +224,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
   }
   check(lsa_attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                         block_tables.size(1), pos.data_ptr<int>(), B, H, Hkv, (float)scale, chunk_blocks, nsplit,
-                        out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), counters.data_ptr<int>(), xf_mt,
+                        (int)unsplit_max, out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), counters.data_ptr<int>(), xf_mt,
                         ptr<const float>(qkv_parts), qkv_parts.has_value() ? qkv_parts->size(0) : 0,
                         qkv_parts.has_value() ? qkv_parts->stride(0) : 0, ptr<const float>(cos_t),
                         ptr<const float>(sin_t), cur_stream()),
@@ -341,7 +341,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pos"), py::arg("H"), py::arg("Hkv"), py::arg("scale"), py::arg("chunk_blocks"), py::arg("nsplit"),
         py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("counters"), py::arg("xf_mt") = 0,
         py::arg("qkv_parts") = py::none(),
-        py::arg("cos") = py::none(), py::arg("sin") = py::none());
+        py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4);
   m.def("attn_prefill", &attn_prefill);
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);

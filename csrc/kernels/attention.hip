@@ -39,8 +39,9 @@ typedef __attribute__((address_space(1))) int g_i32;
 // see; each sequence uses what its own length needs): <= 4 blocks run unsplit (a split costs a combine
 // pass, measured slower below ~256 keys, scripts/bench_attn.py), longer contexts use splits of
 // chunk_blocks blocks, widened when the grid has fewer splits than that needs.
-__device__ __forceinline__ void eff_split(int nblk, int chunk_blocks, int nsplit, int& ech, int& nse) {
-  ech = nblk <= 4 ? max(nblk, 1) : max(chunk_blocks, (nblk + nsplit - 1) / nsplit);
+// unsplit_max: the host plan's unsplit threshold (4; lower for grids too small to fill the chip).
+__device__ __forceinline__ void eff_split(int nblk, int chunk_blocks, int nsplit, int unsplit_max, int& ech, int& nse) {
+  ech = nblk <= unsplit_max ? max(nblk, 1) : max(chunk_blocks, (nblk + nsplit - 1) / nsplit);
   nse = (nblk + ech - 1) / ech;
 }
 
@@ -83,8 +84,8 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
                                                           const uint16_t* __restrict__ vc,
                                                           const int* __restrict__ block_tables, int max_blocks,
                                                           const int* __restrict__ pos, int Hkv, float scale_log2,
-                                                          int chunk_blocks, int nsplit, uint16_t* __restrict__ out,
-                                                          float* __restrict__ opart, float* __restrict__ mlpart,
+                                                          int chunk_blocks, int nsplit, int unsplit_max,
+                                                          uint16_t* __restrict__ out, float* __restrict__ opart, float* __restrict__ mlpart,
                                                           int* __restrict__ counters, int xf_mt, RopeArgs ra) {
   constexpr int D = 128;
   constexpr int NT = 64 * WV;      // threads
@@ -134,7 +135,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   const int ctx = pos[b] + 1;
   const int nblk = (ctx + 63) >> 6;
   int ech, nse;
-  eff_split(nblk, chunk_blocks, nsplit, ech, nse);
+  eff_split(nblk, chunk_blocks, nsplit, unsplit_max, ech, nse);
   if (split >= nse) return;  // whole workgroup: this sequence needs fewer splits
   const int blk0 = split * ech;
   const int blk1 = min(nblk, blk0 + ech);
@@ -402,7 +403,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
 
 extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit,
-                               void* out, float* opart, float* mlpart, int* counters, int xf_mt,
+                               int unsplit_max, void* out, float* opart, float* mlpart, int* counters, int xf_mt,
                                const float* qkv_parts, int nparts,
                                long part_stride, const float* cos_t, const float* sin_t, hipStream_t s) {
   if (H % Hkv) return -1;
@@ -419,7 +420,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
                     const_cast<uint16_t*>(vv)};
 #define LSA_ADK(GV, RP)                                                                                      \
   hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4)>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, qq, kk, \
-                     vv, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, oo, opart, mlpart, counters,  \
+                     vv, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart, counters,  \
                      xf_mt, ra)
 #define LSA_AD(GV)                                  \
   case GV:                                          \

@@ -155,6 +155,8 @@ class EngineService(Backend):
         opts.update(options or {})
         params = SamplingParams.from_ollama_options(opts, default_max=int(opts.get("num_predict", 256)))
         ids = eng.encode(eng.render(prompt, system, raw))
+        if params.num_ctx is not None:
+            ids = eng.fit_context(ids, params.num_ctx, params.num_keep)
         req = lp.submit(ids, params)
         if not req.done.wait(self.timeout_s):
             raise TimeoutError(f"generation on {model} timed out after {self.timeout_s}s")

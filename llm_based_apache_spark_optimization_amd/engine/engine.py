@@ -42,6 +42,8 @@ class SamplingParams:
     # unless a request sets it (Ollama's own default is 1.1; the benchmark configs are plain greedy)
     repeat_penalty: float = 1.0
     repeat_last_n: int = 64
+    num_ctx: Optional[int] = None     # Ollama context window (prompt + generated tokens); None = model's
+    num_keep: int = 4
 
     @property
     def needs_sampler(self) -> bool:
@@ -60,7 +62,9 @@ class SamplingParams:
                               top_k=int(opts.get("top_k", 40)), top_p=float(opts.get("top_p", 0.9)),
                               seed=opts.get("seed"), stop=tuple(stop), ignore_eos=bool(opts.get("ignore_eos", False)),
                               repeat_penalty=float(opts.get("repeat_penalty", 1.0)),
-                              repeat_last_n=int(opts.get("repeat_last_n", 64)))
+                              repeat_last_n=int(opts.get("repeat_last_n", 64)),
+                              num_ctx=int(opts["num_ctx"]) if opts.get("num_ctx") else None,
+                              num_keep=int(opts.get("num_keep", 4)))
 
 
 @dataclasses.dataclass
@@ -121,6 +125,19 @@ class LLMEngine:
     def render(self, prompt: str, system: str = "", raw: bool = False) -> str:
         return prompt if raw else render(self.spec.template, prompt, system)
 
+    @staticmethod
+    def fit_context(ids: Sequence[int], num_ctx: int, num_keep: int = 4) -> list[int]:
+        """Ollama's ``num_ctx`` window: a prompt of more than num_ctx - 1 tokens keeps its
+        first ``num_keep`` tokens (BOS + template head) and its tail, dropping the middle, so at least one
+        token can be generated.  Generation then stops at the window (``add_request`` caps max_tokens);
+        Ollama would shift the context instead."""
+        limit = max(1, int(num_ctx) - 1)
+        ids = list(ids)
+        if len(ids) <= limit:
+            return ids
+        keep = max(0, min(int(num_keep), limit - 1))
+        return ids[:keep] + ids[len(ids) - (limit - keep):]
+
     def encode(self, text: str) -> list[int]:
         ids = self.tok.encode(text, add_bos=True)
         limit = self.runner.max_model_len - 1
@@ -128,7 +145,9 @@ class LLMEngine:
 
     # -------------------------------------------------------------------------------- request API
     def add_request(self, prompt_ids: Sequence[int], params: SamplingParams) -> Request:
-        room = self.runner.max_model_len - len(prompt_ids)
+        window = self.runner.max_model_len if params.num_ctx is None else min(self.runner.max_model_len,
+                                                                               int(params.num_ctx))
+        room = window - len(prompt_ids)
         if room < 1:
             raise ValueError("prompt longer than the model context")
         p = dataclasses.replace(params, max_tokens=max(1, min(params.max_tokens, room, self.runner.max_new_cap)))
@@ -255,6 +274,8 @@ class LLMEngine:
         reqs = []
         for p in prompts:
             ids = self.encode(self.render(p, system, raw)) if isinstance(p, str) else list(p)
+            if params.num_ctx is not None:
+                ids = self.fit_context(ids, params.num_ctx, params.num_keep)
             reqs.append(self.add_request(ids, params))
         self.run_until_done(reqs)
         return [self.result(q) for q in reqs]

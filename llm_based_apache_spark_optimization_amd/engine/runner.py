@@ -130,7 +130,7 @@ class ModelRunner:
         self.logits_l = torch.zeros(S, self.Vl, **f32)
         self.logits = self.logits_l if tps == 1 else torch.zeros(S, self.V, **f32)
         self.gather_buf = None if tps == 1 else torch.zeros(tps * S * self.Vl, **f32)
-        _, nsplit_max = ops.decode_split_plan(1, self.Hkv, self.max_model_len)
+        nsplit_max = max(4, ops.decode_split_plan(1, self.Hkv, self.max_model_len)[1])
         self.attn_ws = ops.decode_workspace(S, self.H, self.Hkv, nsplit_max, dev)
         self.amax_part = torch.zeros(S * ((self.V + 4095) // 4096), dtype=torch.int64, device=dev)
         self.cand = torch.zeros(S * ((self.V + 2047) // 2048) * 64, dtype=torch.int64, device=dev)

@@ -345,19 +345,24 @@ def silu_mul(g: torch.Tensor, u: torch.Tensor, out: Optional[torch.Tensor] = Non
 
 
 # ----------------------------------------------------------------------------------- attention
-def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int]:
-    """(chunk_blocks, nsplit) grid plan of split-KV decode for contexts up to max_ctx.  The kernel picks
-    each sequence's own split from its length (csrc/kernels/attention.hip eff_split): <= 4 blocks run
-    unsplit, longer contexts split into chunk_blocks-block pieces.  chunk 2 while the (sequence, kv-head)
-    grid is small (B * Hkv < 128, e.g. one 3B sequence at 2k context: 17 splits measured best), else 4;
-    at most 256 splits (the combine's LDS)."""
+def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int, int]:
+    """(chunk_blocks, nsplit, unsplit_max) grid plan of split-KV decode for contexts up to max_ctx.  The
+    kernel picks each sequence's own split from its length (csrc/kernels/attention.hip eff_split):
+    <= unsplit_max blocks run unsplit, longer contexts split into chunk_blocks-block pieces.  chunk 2 while
+    the (sequence, kv-head) grid is small (B * Hkv < 128, e.g. one 3B sequence at 2k context: 17 splits
+    measured best), else 4; at most 256 splits (the combine's LDS).  Short contexts (<= 4 blocks) run
+    unsplit, except on grids of <= 8 (sequence, kv-head) pairs (the 3B at batch 1), where one block per
+    split wins despite the combine (scripts/bench_attn.py, MI355X, ctx 200: 8.65 -> 7.32 us; the 7B at
+    batch 1 has 32 pairs and stays unsplit: 7.47 unsplit vs 7.73 split)."""
     nblk = max(1, (max_ctx + 63) // 64)
     if nblk <= 4:  # every sequence runs unsplit (eff_split): no empty split workgroups, no combine
-        return nblk, 1
+        if B * Hkv <= 8 and nblk > 1:
+            return 1, nblk, 0
+        return nblk, 1, 4
     chunk = 2 if B * Hkv < 128 else 4
     while (nblk + chunk - 1) // chunk > 256:
         chunk += 1
-    return chunk, (nblk + chunk - 1) // chunk
+    return chunk, (nblk + chunk - 1) // chunk, 4
 
 
 def decode_workspace(B: int, H: int, Hkv: int, nsplit: int, device) -> tuple:
@@ -386,12 +391,14 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
         f = to_xfrag(tmp.view(B, -1))
         out.view(-1)[: f.numel()].copy_(f)
         return out
-    chunk, nsplit = plan if plan is not None else decode_split_plan(B, Hkv, block_tables.shape[1] * 64)
+    plan = plan if plan is not None else decode_split_plan(B, Hkv, block_tables.shape[1] * 64)
+    chunk, nsplit = plan[0], plan[1]
+    unsplit_max = plan[2] if len(plan) > 2 else 4
     if workspace is None:
         workspace = decode_workspace(B, H, Hkv, nsplit, q.device)
     opart, mlpart, counters = workspace
     ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart, counters,
-                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin)
+                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max)
     return out
 
 

@@ -20,12 +20,13 @@ concurrent requests reach the engine together and share decode steps.
 """
 from __future__ import annotations
 
+import json
 import os
 import time
 from typing import Optional
 
 from fastapi import FastAPI, HTTPException
-from fastapi.responses import PlainTextResponse
+from fastapi.responses import PlainTextResponse, StreamingResponse
 from pydantic import BaseModel
 
 from .. import prompts
@@ -129,6 +130,8 @@ def create_app(ctx: Optional[AppContext] = None) -> FastAPI:
     @app.post("/api/generate")
     def api_generate(req: GenerateRequest):
         r = ctx.backend.generate(req.model, req.prompt, req.system, req.options, req.raw)
+        if req.stream:  # Ollama's NDJSON framing; the whole answer arrives as one final (done) chunk
+            return StreamingResponse(iter([json.dumps(r.to_dict()) + "\n"]), media_type="application/x-ndjson")
         return r.to_dict()
 
     @app.get("/api/tags")

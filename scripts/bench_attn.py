@@ -30,7 +30,8 @@ def timeit(fn, it=50):
     return sorted(reps)[1]
 
 
-cases = {"7b_b1_ctx200": (1, 32, 32, 200, 4), "7b_b32_ctx200": (32, 32, 32, 200, 2),
+cases = {"7b_b1_ctx200": (1, 32, 32, 200, 4), "7b_b1_ctx130": (1, 32, 32, 130, 4),
+         "7b_b32_ctx200": (32, 32, 32, 200, 2), "3b_b1_ctx200": (1, 24, 8, 200, 1),
          "3b_b1_ctx2100": (1, 24, 8, 2100, 8), "3b_b32_ctx200": (32, 24, 8, 200, 8)}
 cos, sin = ref.rope_tables(128, 4096, 500000.0, device=dev)
 for name, (B, H, Hkv, ctx, nparts) in cases.items():
@@ -50,8 +51,13 @@ for name, (B, H, Hkv, ctx, nparts) in cases.items():
         if chunk > nblk:
             continue
         nsplit = (nblk + chunk - 1) // chunk
+        # unsplit threshold 0: the split is forced even for contexts of <= 4 blocks
         res[f"chunk{chunk}/split{nsplit}"] = round(timeit(lambda: ops.attn_decode(
-            q, kc, vc, bt, pos, H, Hkv, 1 / math.sqrt(128), out, workspace=ws, plan=(chunk, nsplit),
+            q, kc, vc, bt, pos, H, Hkv, 1 / math.sqrt(128), out, workspace=ws, plan=(chunk, nsplit, 0),
             qkv_parts=parts, cos=cos, sin=sin)), 2)
-    res["default_plan"] = ops.decode_split_plan(B, Hkv, ctx)
+    plan = ops.decode_split_plan(B, Hkv, ctx)
+    res["default_plan"] = plan
+    res["default_us"] = round(timeit(lambda: ops.attn_decode(
+        q, kc, vc, bt, pos, H, Hkv, 1 / math.sqrt(128), out, workspace=ws, plan=plan,
+        qkv_parts=parts, cos=cos, sin=sin)), 2)
     print(json.dumps(res), flush=True)

@@ -1,6 +1,7 @@
 """Contract tests of the FastAPI and Flask apps with the deterministic fake model backend, the SQLite
 executor and a SQLite history store."""
 import io
+import json
 import os
 import threading
 
@@ -87,6 +88,10 @@ def test_fastapi_ollama_api_and_ops(api):
     r = api.post("/api/generate", json={"model": "duckdb-nsql", "prompt": "q", "system": "s"})
     d = r.json()
     assert d["response"] and d["done"] is True and "eval_count" in d
+    r = api.post("/api/generate", json={"model": "duckdb-nsql", "prompt": "q", "stream": True})
+    lines = [json.loads(x) for x in r.text.splitlines() if x.strip()]
+    assert r.headers["content-type"].startswith("application/x-ndjson") and lines[-1]["done"] is True
+    assert lines[-1]["response"] == d["response"]
     assert any(m["name"] == "llama3.2" for m in api.get("/api/tags").json()["models"])
     assert api.get("/health").json()["ok"] is True
     api.post("/nl2sql", json={"table_schema": "a (int)", "question": "all rows"})

@@ -113,3 +113,18 @@ def test_tensor_parallel_matches_single():
     assert got_sp[0] == got_sp[1] == got[0]  # SP prefill: same tokens as the all-reduce prefill
     agree = sum(a == b for x, y in zip(got[0], want) for a, b in zip(x, y))
     assert agree >= 10, (got[0], want)  # fp32 reduction order differs across shards only
+
+
+def test_num_ctx_window(eng):
+    """Ollama num_ctx / num_keep: long prompts keep their head and tail; generation stops at the window."""
+    ids = list(range(3, 3 + 50))
+    assert eng.fit_context(ids, 64) == ids
+    cut = eng.fit_context(ids, 20, num_keep=4)
+    assert len(cut) == 19 and cut[:4] == ids[:4] and cut[4:] == ids[-15:]
+    sp = SamplingParams.from_ollama_options({"num_ctx": 24, "num_predict": 100, "ignore_eos": True})
+    assert sp.num_ctx == 24 and sp.num_keep == 4
+    r = eng.generate([[1] + ids], sp)[0]
+    assert r.prompt_tokens == 23 and r.eval_count == 1 and r.done_reason == "length"
+    # the truncated prompt generates exactly what the same tokens generate as a plain prompt
+    same = eng.generate([eng.fit_context([1] + ids, 24)], SamplingParams(max_tokens=1, ignore_eos=True))[0]
+    assert same.token_ids == r.token_ids

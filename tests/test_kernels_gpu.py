@@ -319,6 +319,10 @@ def test_attn_decode(gpu, HH, lens):
     out4 = torch.empty_like(out)
     ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, out4, plan=ops.decode_split_plan(B, Hkv, 16384))
     assert _rel(out4, out2) < 1e-2
+    # unsplit threshold 0: every context of >= 2 blocks splits one block per workgroup (in-launch combine)
+    out5 = torch.empty_like(out)
+    ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, out5, plan=(1, bt.shape[1], 0))
+    assert _rel(out5, out2) < 1e-2
     # fragment-major output (O-projection input), split and single-split paths
     for plan in (None, (bt.shape[1], 1)):
         xf = torch.zeros(ops.xfrag_tiles(B) * 16 * H * D, device=gpu, dtype=torch.bfloat16)
