@@ -143,13 +143,22 @@ def from_hf_state_dict(spec: ModelSpec, sd: dict, device="cpu", kind: str = "bf1
     return LlamaWeights(spec, embed, layers, t("model.norm.weight").contiguous(), lm_head, tp_rank, tp_size)
 
 
-def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[str] = None, template="raw",
-                         tp_rank=0, tp_size=1) -> LlamaWeights:
-    """Load an HF checkpoint directory (config.json + *.safetensors) with the safe loader."""
+def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[str] = None,
+                         template: Optional[str] = None, tp_rank=0, tp_size=1) -> LlamaWeights:
+    """Load an HF checkpoint directory (config.json + *.safetensors) with the safe loader.  The prompt
+    template follows the served name when it is a known model (a duckdb-nsql checkpoint served as
+    ``duckdb-nsql`` keeps the Ollama duckdb-nsql template), else ``template`` or raw."""
     from safetensors.torch import load_file
+
+    from .spec import get_spec
 
     with open(os.path.join(path, "config.json")) as f:
         cfg = json.load(f)
+    if template is None:
+        try:
+            template = get_spec(name).template if name else "raw"
+        except KeyError:
+            template = "raw"
     spec = spec_from_hf_config(cfg, name or os.path.basename(path.rstrip("/")), template)
     sd = {}
     for fn in sorted(glob.glob(os.path.join(path, "*.safetensors"))):

@@ -105,10 +105,20 @@ def get_spec(name: str) -> ModelSpec:
 def spec_from_hf_config(cfg: dict, name: str = "custom", template: str = "raw") -> ModelSpec:
     eos = cfg.get("eos_token_id", 2)
     eos = tuple(eos) if isinstance(eos, (list, tuple)) else (eos,)
+    # checkpoints written by transformers >= 5 carry RoPE as one "rope_parameters" dict (rope_theta +
+    # rope_type + the scaling fields); older ones (the hub's Llama-2 / Llama-3.2 / Mistral configs) use
+    # top-level "rope_theta" and an optional "rope_scaling" dict
+    rp = cfg.get("rope_parameters") or {}
+    theta = cfg.get("rope_theta", rp.get("rope_theta", 10000.0))
+    scaling = cfg.get("rope_scaling")
+    if scaling is None and rp.get("rope_type", "default") not in ("default", None):
+        scaling = {k: v for k, v in rp.items() if k != "rope_theta"}
+    if scaling is not None and scaling.get("rope_type", scaling.get("type", "default")) == "default":
+        scaling = None
     return ModelSpec(
         name=name, vocab_size=cfg["vocab_size"], hidden=cfg["hidden_size"], n_layers=cfg["num_hidden_layers"],
         n_heads=cfg["num_attention_heads"], n_kv_heads=cfg.get("num_key_value_heads", cfg["num_attention_heads"]),
-        ffn=cfg["intermediate_size"], rope_theta=cfg.get("rope_theta", 10000.0), rms_eps=cfg.get("rms_norm_eps", 1e-5),
+        ffn=cfg["intermediate_size"], rope_theta=float(theta), rms_eps=cfg.get("rms_norm_eps", 1e-5),
         head_dim=cfg.get("head_dim") or cfg["hidden_size"] // cfg["num_attention_heads"],
         tie_embeddings=cfg.get("tie_word_embeddings", False), max_position=cfg.get("max_position_embeddings", 4096),
-        rope_scaling=cfg.get("rope_scaling"), bos_id=cfg.get("bos_token_id", 1) or 1, eos_ids=eos, template=template)
+        rope_scaling=scaling, bos_id=cfg.get("bos_token_id", 1) or 1, eos_ids=eos, template=template)

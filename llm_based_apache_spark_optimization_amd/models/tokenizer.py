@@ -102,7 +102,9 @@ MISTRAL_SPECIALS = ("[INST]", "[/INST]")
 
 
 def tokenizer_for(spec: ModelSpec, path: Optional[str] = None):
-    if path:
+    # a checkpoint directory with its tokenizer files: the real tokenizer; weights-only directories
+    # fall back to the byte tokenizer below
+    if path and any(os.path.exists(os.path.join(path, f)) for f in ("tokenizer.json", "tokenizer.model")):
         return HFTokenizer(path, spec.bos_id, spec.eos_ids)
     specials = LLAMA3_SPECIALS if spec.template == "llama3" else MISTRAL_SPECIALS if spec.template == "mistral" else ()
     tok = ByteTokenizer(spec.vocab_size, bos_id=spec.bos_id if spec.bos_id < spec.vocab_size else 1,
