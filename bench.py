@@ -47,18 +47,29 @@ def main() -> int:
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="run the same bench flow on CPU over gloo (tests of the multi-rank path; not a measurement)")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from llm_based_apache_spark_optimization_amd.engine import build_engine, SamplingParams
     from llm_based_apache_spark_optimization_amd.parallel import init_distributed, make_replica_groups
 
-    rank, world, local = init_distributed()
-    if not torch.cuda.is_available():
-        print("bench.py needs a GPU", file=sys.stderr)
-        return 2
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    cpu = args.cpu_rehearsal
+    rank, world, local = init_distributed("gloo" if cpu else None)
+    if cpu:
+        device = torch.device("cpu")
+    else:
+        if not torch.cuda.is_available():
+            print("bench.py needs a GPU", file=sys.stderr)
+            return 2
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
     tp = max(1, args.tp)
     replica, tpg = make_replica_groups(world, tp, rank, device) if world > 1 else (0, None)
     dp = world // tp
@@ -82,14 +93,14 @@ def main() -> int:
         one_step()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     lat = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         s = time.perf_counter()
         one_step()
         lat.append(time.perf_counter() - s)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -118,7 +129,7 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / REF_TOK_S, 2),
             "dtype": args.dtype if args.dtype == "bf16" else "fp8-weights/bf16-act",
-            "data": "synthetic prompts, random-init weights",
+            "data": "synthetic prompts, random-init weights" + (" (CPU rehearsal, not a measurement)" if cpu else ""),
             "config": {
                 "model": MODEL_NAMES.get(args.model, args.model),
                 "global_batch": dp * args.batch,
