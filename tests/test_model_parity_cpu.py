@@ -5,6 +5,8 @@ RoPE + tied embeddings Llama-3.2 shape) is built in transformers, its state dict
 engine (CPU reference ops, bf16 weights / bf16 activations) and compared: prefill logits and
 teacher-forced greedy decoding through the paged KV cache and the native scheduler.
 """
+import json
+
 import pytest
 import torch
 
@@ -127,3 +129,42 @@ def test_safetensors_checkpoint_dir_loads(name, tmp_path):
     w1 = load_safetensors_dir(str(tmp_path), "cpu", name=name, tp_rank=1, tp_size=2)
     assert w0.layers[0].wo.K == w.layers[0].wo.K // 2 and w1.layers[0].wqkv.N == w.layers[0].wqkv.N // 2
     assert w0.lm_head.N + w1.lm_head.N == w.lm_head.N
+
+
+def test_hf_tokenizer_checkpoint_llama3_specials(tmp_path):
+    """A checkpoint directory's tokenizer.json (a byte-level BPE trained here with the Llama-3 special
+    tokens; no hub download is possible) is used by the serving factory: the rendered llama3 chat
+    template maps each header/end-of-turn marker to ONE special id, text round-trips, and <|eot_id|>
+    terminates generation."""
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+
+    from llm_based_apache_spark_optimization_amd.engine import build_engine
+    from llm_based_apache_spark_optimization_amd.models.templates import render
+    from llm_based_apache_spark_optimization_amd.models.tokenizer import LLAMA3_SPECIALS, HFTokenizer
+    from llm_based_apache_spark_optimization_amd.prompts import EXPLAIN_SYSTEM
+
+    spec, m = hf_model("tiny-llama3")
+    m.to(torch.bfloat16).save_pretrained(str(tmp_path), safe_serialization=True)
+    bpe = Tokenizer(models.BPE())
+    bpe.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    bpe.decoder = decoders.ByteLevel()
+    corpus = ["The following Spark error occurred: AnalysisException UNRESOLVED_COLUMN", "SELECT * FROM temp_view;",
+              "Please analyze this error and suggest possible solutions.", EXPLAIN_SYSTEM] * 20
+    bpe.train_from_iterator(corpus, trainers.BpeTrainer(vocab_size=420, special_tokens=list(LLAMA3_SPECIALS),
+                                                        initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    bpe.save(str(tmp_path / "tokenizer.json"))
+    ids = {s: bpe.token_to_id(s) for s in LLAMA3_SPECIALS}
+    cfg = json.loads((tmp_path / "config.json").read_text())
+    cfg.update(bos_token_id=ids["<|begin_of_text|>"], eos_token_id=[ids["<|end_of_text|>"], ids["<|eot_id|>"]])
+    (tmp_path / "config.json").write_text(json.dumps(cfg))
+
+    eng = build_engine("llama3.2", device="cpu", checkpoint=str(tmp_path), max_slots=2, max_model_len=512)
+    assert isinstance(eng.tok, HFTokenizer) and eng.spec.template == "llama3"
+    text = render("llama3", "The following Spark error occurred: x", EXPLAIN_SYSTEM)
+    enc = eng.tok.encode(text, add_bos=False)
+    for s in ("<|start_header_id|>", "<|end_header_id|>", "<|eot_id|>"):
+        assert enc.count(ids[s]) == text.count(s) > 0, s
+    assert eng.tok.decode(eng.tok.encode("SELECT * FROM temp_view;", add_bos=False)) == "SELECT * FROM temp_view;"
+    assert ids["<|eot_id|>"] in eng.runner.eos_list
+    r = eng.generate(["SELECT"], SamplingParams(max_tokens=3, ignore_eos=True), system=EXPLAIN_SYSTEM)[0]
+    assert r.eval_count == 3 and isinstance(r.text, str)
