@@ -186,6 +186,8 @@ void rope_append(const at::Tensor& qkv, const at::Tensor& pos, const c10::option
   const bool parts = qkv.scalar_type() == at::kFloat;
   TORCH_CHECK(parts || qkv.scalar_type() == at::kBFloat16, "qkv must be bf16 or f32 slabs");
   const int T = parts ? qkv.size(1) : qkv.size(0);
+  TORCH_CHECK(cos_t.size(0) >= block_tables.size(1) * 64 && sin_t.size(0) >= block_tables.size(1) * 64,
+              "rope tables have fewer rows than the block tables address (", block_tables.size(1) * 64, ")");
   check(lsa_rope_append(parts ? nullptr : qkv.data_ptr(), parts ? qkv.data_ptr<float>() : nullptr,
                         parts ? qkv.size(0) : 0, parts ? qkv.stride(0) : 0, pos.data_ptr<int>(), ptr<const int>(tok_seq), block_tables.data_ptr<int>(),
                         block_tables.size(1), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), q_out.data_ptr(),
@@ -221,6 +223,9 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
     TORCH_CHECK(cos_t.has_value() && sin_t.has_value(), "fused rope needs cos/sin tables");
     need(*cos_t, at::kFloat, "cos");
     need(*sin_t, at::kFloat, "sin");
+    // positions come from the device (no host read); every position the block tables address needs a row
+    TORCH_CHECK(cos_t->size(0) >= block_tables.size(1) * 64 && sin_t->size(0) >= block_tables.size(1) * 64,
+                "rope tables have fewer rows than the block tables address (", block_tables.size(1) * 64, ")");
   }
   check(lsa_attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                         block_tables.size(1), pos.data_ptr<int>(), B, H, Hkv, (float)scale, chunk_blocks, nsplit,

@@ -83,7 +83,8 @@ class ModelRunner:
         self.num_kv_blocks = int(num_kv_blocks)
         self.kv = torch.zeros(self.L, 2, self.num_kv_blocks, self.Hkv, BLOCK, self.D, dtype=torch.bfloat16,
                               device=dev)
-        cos, sin = ref.rope_tables(self.D, self.max_model_len, spec.rope_theta, spec.rope_scaling, device=dev)
+        # one row per position the block tables can address (the kernels check this bound on the host)
+        cos, sin = ref.rope_tables(self.D, self.max_blocks * BLOCK, spec.rope_theta, spec.rope_scaling, device=dev)
         self.cos, self.sin = cos.contiguous(), sin.contiguous()
 
         # ---------------- device decode state (one row per slot)

@@ -348,21 +348,26 @@ def silu_mul(g: torch.Tensor, u: torch.Tensor, out: Optional[torch.Tensor] = Non
 def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int, int]:
     """(chunk_blocks, nsplit, unsplit_max) grid plan of split-KV decode for contexts up to max_ctx.  The
     kernel picks each sequence's own split from its length (csrc/kernels/attention.hip eff_split):
-    <= unsplit_max blocks run unsplit, longer contexts split into chunk_blocks-block pieces.  chunk 2 while
-    the (sequence, kv-head) grid is small (B * Hkv < 128, e.g. one 3B sequence at 2k context: 17 splits
-    measured best), else 4; at most 256 splits (the combine's LDS).  Short contexts (<= 4 blocks) run
-    unsplit, except on grids of <= 8 (sequence, kv-head) pairs (the 3B at batch 1), where one block per
-    split wins despite the combine (scripts/bench_attn.py, MI355X, ctx 200: 8.65 -> 7.32 us; the 7B at
-    batch 1 has 32 pairs and stays unsplit: 7.47 unsplit vs 7.73 split)."""
+    <= unsplit_max blocks run unsplit, longer contexts are cut into nsplit pieces of at least chunk_blocks
+    blocks, so a sequence shorter than max_ctx uses fewer, equally long splits.
+
+    Measured on MI355X (scripts/bench_attn.py, profiles/attn_split_plans_mi355x.jsonl): the best grid is
+    about 256 workgroups, i.e. one per CU of (sequence, kv-head) pairs x splits.  At >= 256 pairs (7B at
+    batch >= 8, 3B at batch >= 32) every context runs unsplit (3B B=32 ctx 2048: 77.2 -> 46.4 us, 7B B=32
+    ctx 512: 53.9 -> 44.6 us vs the earlier fixed 4-block chunks); 64 pairs -> 4 splits (3B B=8 ctx 2048:
+    31.8 -> 16.8 us); 8 pairs (3B at batch 1) -> up to 32 splits of >= 2 blocks (17 at 2k context).
+    Contexts of <= 4 blocks run unsplit (a combine costs more than it spreads), except on grids of <= 8
+    pairs, where one block per split still wins (3B B=1 ctx 200: 8.65 -> 7.32 us)."""
     nblk = max(1, (max_ctx + 63) // 64)
+    pairs = max(1, B * Hkv)
     if nblk <= 4:  # every sequence runs unsplit (eff_split): no empty split workgroups, no combine
-        if B * Hkv <= 8 and nblk > 1:
+        if pairs <= 8 and nblk > 1:
             return 1, nblk, 0
         return nblk, 1, 4
-    chunk = 2 if B * Hkv < 128 else 4
-    while (nblk + chunk - 1) // chunk > 256:
-        chunk += 1
-    return chunk, (nblk + chunk - 1) // chunk, 4
+    nsplit = min(max(1, round(256 / pairs)), (nblk + 1) // 2, 256)
+    if nsplit <= 1:
+        return nblk, 1, 4
+    return 2, nsplit, 4
 
 
 def decode_workspace(B: int, H: int, Hkv: int, nsplit: int, device) -> tuple:

@@ -47,7 +47,7 @@ def run(B, H, Hkv, ctx, nparts=2, plan_ctx=None):
                                         plan=plan, qkv_parts=parts, cos=cos, sin=sin))
     mb = B * ctx * Hkv * 128 * 2 * 2 / 1e6
     return {"B": B, "H": H, "Hkv": Hkv, "ctx": ctx, "plan": plan, "us": round(us, 2), "MB": round(mb, 1),
-            "TBps": round(mb / us / 1e6, 2)}
+            "TBps": round(mb / us, 2)}
 
 
 # graphs are planned for the engine's max_model_len; short live contexts leave most splits empty

@@ -33,7 +33,14 @@ def timeit(fn, it=50):
 cases = {"7b_b1_ctx200": (1, 32, 32, 200, 4), "7b_b1_ctx130": (1, 32, 32, 130, 4),
          "7b_b32_ctx200": (32, 32, 32, 200, 2), "3b_b1_ctx200": (1, 24, 8, 200, 1),
          "3b_b1_ctx2100": (1, 24, 8, 2100, 8), "3b_b32_ctx200": (32, 24, 8, 200, 8)}
-cos, sin = ref.rope_tables(128, 4096, 500000.0, device=dev)
+if len(sys.argv) > 1 and sys.argv[1] == "long":  # larger grids at longer contexts: unsplit vs split plans
+    cases = {f"{m}_b{B}_ctx{c}": (B, H, Hkv, c, 2) for m, H, Hkv in (("7b", 32, 32), ("3b", 24, 8))
+             for B in (8, 32) for c in (320, 512, 1024, 2048)}
+    cases.update({"7b_b1_ctx1024": (1, 32, 32, 1024, 4), "7b_b1_ctx2048": (1, 32, 32, 2048, 4),
+                  "7b_b4_ctx1024": (4, 32, 32, 1024, 4), "3b_b1_ctx2100": (1, 24, 8, 2100, 8),
+                  "3b_b16_ctx1024": (16, 24, 8, 1024, 4), "3b_b2_ctx2048": (2, 24, 8, 2048, 8),
+                  "3b_b1_ctx8192": (1, 24, 8, 8192, 8), "7b_b1_ctx200": (1, 32, 32, 200, 4)})
+cos, sin = ref.rope_tables(128, 64 * max((c[3] + 63) // 64 for c in cases.values()), 500000.0, device=dev)
 for name, (B, H, Hkv, ctx, nparts) in cases.items():
     nblk = (ctx + 63) // 64
     total = B * nblk * 8 + 1  # spread: 8x the live blocks
@@ -48,12 +55,12 @@ for name, (B, H, Hkv, ctx, nparts) in cases.items():
     ws = ops.decode_workspace(B, H, Hkv, 256, dev)
     res = {"case": name}
     for chunk in sorted({1, 2, 4, 8, 16, nblk}):
-        if chunk > nblk:
+        if chunk > nblk or (len(sys.argv) > 1 and chunk < 2):
             continue
         nsplit = (nblk + chunk - 1) // chunk
         # unsplit threshold 0: the split is forced even for contexts of <= 4 blocks
         res[f"chunk{chunk}/split{nsplit}"] = round(timeit(lambda: ops.attn_decode(
-            q, kc, vc, bt, pos, H, Hkv, 1 / math.sqrt(128), out, workspace=ws, plan=(chunk, nsplit, 0),
+            q, kc, vc, bt, pos, H, Hkv, 1 / math.sqrt(128), out, workspace=ws, plan=(chunk, nsplit, 0 if chunk < nblk else nblk),
             qkv_parts=parts, cos=cos, sin=sin)), 2)
     plan = ops.decode_split_plan(B, Hkv, ctx)
     res["default_plan"] = plan

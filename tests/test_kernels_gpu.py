@@ -495,3 +495,19 @@ def test_repeat_penalty_ring_matches_reference(gpu):
     assert torch.equal(hg, hc)
     for b in range(B):  # the committed token landed at column (pos + 1) % W
         assert int(hg[b, (int(pos[b]) + 1) % W]) == int(tg[b])
+
+
+def test_rope_table_bound_checked_on_host(gpu):
+    """Positions live on the device, so the host checks the rope tables cover every position the block
+    tables can address (a short table would otherwise be read out of bounds by the fused kernels)."""
+    H, Hkv, D = 8, 2, 128
+    kc, vc, bt = _paged([100, 300], Hkv, D, gpu)
+    pos = torch.tensor([99, 299], device=gpu, dtype=torch.int32)
+    cos, sin = ref.rope_tables(D, 256, 10000.0, device=gpu)  # bt addresses 6 * 64 = 384 positions
+    parts = torch.randn(1, 2, (H + 2 * Hkv) * D, device=gpu)
+    q = torch.empty(2, H, D, device=gpu, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="rope tables"):
+        ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, 0.1, torch.empty_like(q), qkv_parts=parts, cos=cos, sin=sin)
+    with pytest.raises(RuntimeError, match="rope tables"):
+        ops.rope_append(parts, pos, None, bt, cos, sin, q, kc, vc, H, Hkv)
+    torch.cuda.synchronize()
