@@ -1,0 +1,69 @@
+"""Decode GEMM at the batch buckets between the tuned M = 1 / M = 32 points: the config ops picks from the
+tuning table vs the best of a sweep over (nb, splitk, waves, div), per shape and M (us per call, weights
+rotating over > 600 MiB so they stream from HBM).  Prints one JSON line per (shape, M)."""
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from llm_based_apache_spark_optimization_amd import ops  # noqa: E402
+
+dev = torch.device("cuda:0")
+SHAPES = {"7b_qkv": (12288, 4096, "f32"), "7b_o": (4096, 4096, "f32"), "7b_gateup": (22016, 4096, "silu"),
+          "7b_down": (4096, 11008, "f32"), "3b_qkv": (5120, 3072, "f32"), "3b_gateup": (16384, 3072, "silu"),
+          "3b_down": (3072, 8192, "f32"), "3b_o": (3072, 3072, "f32")}
+Ms = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else [4, 8, 16, 24, 48, 64]
+
+
+def timeit(fn, it=30):
+    for i in range(3):
+        fn(i)
+    torch.cuda.synchronize()
+    reps = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(it):
+            fn(i)
+        e1.record()
+        torch.cuda.synchronize()
+        reps.append(e0.elapsed_time(e1) * 1000 / it)
+    return sorted(reps)[1]
+
+
+for name, (N, K, epi) in SHAPES.items():
+    nbytes = N * K * 2
+    ncopy = max(2, (600 << 20) // nbytes + 1)
+    ws = [ops.PackedWeight.from_dense((torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)) for _ in range(ncopy)]
+    for M in Ms:
+        xf = M > 16 and M <= 64
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        xfr = ops.to_xfrag(x) if xf else None
+
+        def call(cfg):
+            nb, sk, waves, dv = cfg
+            o = (torch.empty(sk, M, N, device=dev) if epi == "f32" else
+                 torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16))
+            if xf:
+                return lambda i: ops.linear_xf(xfr, M, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb, waves=waves, div=dv)
+            return lambda i: ops.linear(x, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb, waves=waves, div=dv)
+
+        picked = ops.pick_gemm_config(M, N, K, epi, xf=xf)
+        res = {"shape": name, "M": M, "xf": xf, "picked": list(picked), "picked_us": round(timeit(call(picked)), 2)}
+        best = None
+        for waves, dv in ((4, 1), (4, 2), (4, 4), (8, 2)):
+            for nb in (1, 2, 4):
+                if (N // 16) % nb or (epi == "silu" and nb == 1) or (M > 32 and nb > 2):
+                    continue
+                for sk in ((1, 2, 4, 8) if epi == "f32" else (1,)):
+                    if K // 32 // sk < 8:
+                        continue
+                    us = timeit(call((nb, sk, waves, dv)))
+                    if best is None or us < best[1]:
+                        best = ((nb, sk, waves, dv), us)
+        res["best"] = list(best[0])
+        res["best_us"] = round(best[1], 2)
+        print(json.dumps(res), flush=True)
+    del ws
+    torch.cuda.empty_cache()
