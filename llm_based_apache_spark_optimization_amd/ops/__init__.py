@@ -178,14 +178,16 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
     if M <= 64:
         key = f"{N}x{K}:{epi}:{'s' if M <= 16 else 'm'}"
         tab = _tuning_table()
-        e = tab.get(key + ":fp8") if kind == "fp8" else None
-        if e is None and kind != "fp8" and os.environ.get("LSA_GEMM_BUCKETS", "1") != "0":
-            # per-batch-bucket entries (power-of-two M between the tuned M = 1 / 32 points) where a sweep
-            # beat the s/m entry by > 3 % (scripts/bench_gemm_buckets.py, profiles/gemm_buckets_mi355x.jsonl)
+        e = None
+        if os.environ.get("LSA_GEMM_BUCKETS", "1") != "0":
+            # per-batch-bucket entries (power-of-two M) where a sweep beat the s/m entry by > 3 %
+            # (scripts/bench_gemm_buckets.py, profiles/gemm_buckets_mi355x.jsonl)
             b = 1
             while b < M:
                 b *= 2
-            e = tab.get(f"{N}x{K}:{epi}:b{b}" + (":xf" if xf else ""))
+            e = tab.get(f"{N}x{K}:{epi}:b{b}" + (":fp8" if kind == "fp8" else ":xf" if xf else ""))
+        if e is None and kind == "fp8":
+            e = tab.get(key + ":fp8")
         if e is None and xf:
             e = tab.get(key + ":xf")
         e = e if e is not None else tab.get(key)
