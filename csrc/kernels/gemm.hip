@@ -330,9 +330,9 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
 }
 
 template <int EPI>
-__global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
+__global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KBtot,
                                                         const uint4* __restrict__ Wf, int NBtot,
-                                                        void* __restrict__ out, int ldo) {
+                                                        void* __restrict__ out, int ldo, int kb_per_split) {
   // [stage][operand 0 = W, 1 = X][frag = sub * 2 + kf][lane]
   __shared__ __attribute__((aligned(16))) uint4 lds[2][2][16][64];
   const int lane = threadIdx.x & 63;
@@ -340,6 +340,10 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restri
   const int wm = w >> 1, wn = w & 1;
   const int nbase = blockIdx.x * 8;
   const int mbase = blockIdx.y * 128;
+  // split-K (f32 slabs only): blockIdx.z owns k-blocks [kbA, kbA + KB) of the KBtot; small prefill grids
+  // (M <= 512: O / down have only N / 128 tiles) would otherwise stream all of K on a few dozen CUs
+  const int kbA = blockIdx.z * kb_per_split;
+  const int KB = min(KBtot - kbA, kb_per_split);
 
   // staging sources: this wave stages frags f = 4w .. 4w+3 of each operand
   const uint4* wsrc[4];
@@ -349,9 +353,9 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restri
     const int f = 4 * w + q;
     const int sub = f >> 1, kf = f & 1;
     const int nb = min(nbase + sub, NBtot - 1);
-    wsrc[q] = Wf + ((size_t)nb * KB + kf) * 64 + lane;
+    wsrc[q] = Wf + ((size_t)nb * KBtot + kbA + kf) * 64 + lane;
     const int m = min(mbase + sub * 16 + (lane & 15), M - 1);
-    xsrc[q] = X + (size_t)m * ldx + kf * 32 + 8 * (lane >> 4);
+    xsrc[q] = X + (size_t)m * ldx + (size_t)(kbA + kf) * 32 + 8 * (lane >> 4);
   }
 
   auto stage = [&](int st, int kb0) {
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restri
       for (int j = 0; j < 4; ++j) {
         const int m = mbase + (wm * 4 + j) * 16 + (lane & 15);
         if (m >= M) continue;
-        store4<EPI>(out, ldo, 0, m, nb * 16 + 4 * g, acc[i][j]);
+        store4<EPI>(out, ldo, (size_t)blockIdx.z * M * ldo, m, nb * 16 + 4 * g, acc[i][j]);
       }
     }
   }
@@ -550,21 +554,24 @@ extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf
       default: return -4;
     }
   } else {
-    if (splitk != 1) return -3;
+    if (splitk < 1) splitk = 1;
+    if (splitk != 1 && (epi != EPI_F32 || splitk > KB)) return -3;
     // the 256^2 8-phase kernel (gemm_tile256.hip) once its grid fills half the CUs; measured 1.2-1.34 PF
     // vs 0.73-0.86 PF for the 128^2 tile at the 7B/3B prefill shapes (scripts/bench_prefill_gemm.py)
-    if (((M + 255) / 256) * ((NBtot + 15) / 16) >= 128 && (epi != EPI_SILU || NBtot % 2 == 0))
+    if (splitk == 1 && ((M + 255) / 256) * ((NBtot + 15) / 16) >= 128 && (epi != EPI_SILU || NBtot % 2 == 0))
       return lsa_gemm_t256(X, ldx, M, K, Wf, N, out, epi, stream);
-    dim3 grid((NBtot + 7) / 8, (M + 127) / 128);
+    const int kbps = (KB + splitk - 1) / splitk;
+    if ((KB + kbps - 1) / kbps != splitk) return -3;  // every slab must own >= 1 k-block (no unwritten slab)
+    dim3 grid((NBtot + 7) / 8, (M + 127) / 128, splitk);
     switch (epi) {
       case EPI_BF16:
-        hipLaunchKernelGGL(gemm_tile_kernel<EPI_BF16>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo);
+        hipLaunchKernelGGL(gemm_tile_kernel<EPI_BF16>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, kbps);
         break;
       case EPI_F32:
-        hipLaunchKernelGGL(gemm_tile_kernel<EPI_F32>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo);
+        hipLaunchKernelGGL(gemm_tile_kernel<EPI_F32>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, kbps);
         break;
       case EPI_SILU:
-        hipLaunchKernelGGL(gemm_tile_kernel<EPI_SILU>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo);
+        hipLaunchKernelGGL(gemm_tile_kernel<EPI_SILU>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, kbps);
         break;
       default: return -4;
     }

@@ -147,8 +147,10 @@ class ModelRunner:
         return self.tp.reduce_parts(parts)
 
     def _splitk(self, M: int, K: int, N: Optional[int] = None, tp_reduced: bool = True, xf: bool = False) -> int:
-        if not self.on_gpu or M > 64:
+        if not self.on_gpu:
             return 1
+        if M > 64:  # prefill: split-K on small tile grids; TP prefill reduces single slabs over RCCL
+            return 1 if (self.tp is not None and self.tp.size > 1) else ops.tile_splitk(M, N or self.d, K)
         if tp_reduced and self.tp is not None and self.tp.size > 1 and not self.tp.can_fold_splitk(M * self.d):
             return 1  # RCCL reduces one slab; the one-shot kernel folds split-K slabs into the all-reduce
         return ops.pick_gemm_config(M, N or self.d, K, "f32", xf=xf, kind=self.w.layers[0].wo.kind)[1]
@@ -456,7 +458,12 @@ class ModelRunner:
                 o_parts = o_parts.view(1, T, d)
             o_parts = self._reduce_parts(o_parts)
             ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
-            act = ops.linear(xn, lw.w_gate_up, "silu")
+            sk_g = self._splitk(T, self.d, lw.w_gate_up.N)
+            if sk_g > 1:  # small tile grid: f32 split-K slabs, then silu(gate) * up over the slabs
+                act = ops.silu_parts(ops.linear(xn, lw.w_gate_up, "f32", splitk=sk_g),
+                                     torch.empty(T, lw.w_gate_up.N // 2, **bf))
+            else:
+                act = ops.linear(xn, lw.w_gate_up, "silu")
             d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
             if not self.on_gpu:
                 d_parts = d_parts.view(1, T, d)
@@ -468,9 +475,14 @@ class ModelRunner:
         return xl
 
     def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T):
-        ops.linear(xn, lw.wqkv, "bf16", out=qkv)
         kc, vc = self.kv[l, 0], self.kv[l, 1]
-        ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
+        sk_q = self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D)
+        if sk_q > 1:  # small tile grid: f32 split-K slabs, summed by rope_append while it rotates
+            parts = ops.linear(xn, lw.wqkv, "f32", splitk=sk_q)
+            ops.rope_append(parts, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
+        else:
+            ops.linear(xn, lw.wqkv, "bf16", out=qkv)
+            ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
         ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
                          work=work)
 

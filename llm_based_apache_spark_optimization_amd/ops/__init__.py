@@ -217,11 +217,11 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
         return y
     nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi, kind=w.kind)
     nb = nb0 if nb is None else nb
+    if M > 64:  # prefill tile kernels: split-K (f32 slabs) only where the tile grid is small
+        splitk = (tile_splitk(M, w.N, K) if splitk is None else splitk) if epi == "f32" else 1
     splitk = sk0 if splitk is None else splitk
     waves = wv0 if waves is None else waves
     div = dv0 if div is None else div
-    if M > 64:
-        splitk = 1
     if out is None:
         if epi == "f32":
             out = torch.empty(splitk, M, w.N, device=x.device, dtype=torch.float32)
@@ -240,11 +240,26 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
                 buf = torch.empty(w.N * w.K, device=x.device, dtype=torch.bfloat16)
                 _dq_scratch[x.device] = buf
             e.fp8_dequant(w.data, w.scale, w.N, w.K, buf)
-            e.gemm(x, buf[: w.N * w.K], w.N, out, EPI[epi], nb, 1, waves, div)
+            e.gemm(x, buf[: w.N * w.K], w.N, out, EPI[epi], nb, splitk, waves, div)
             del key
     else:
         raise ValueError(f"weight kind {w.kind} on GPU")
     return out
+
+
+def tile_splitk(M: int, N: int, K: int) -> int:
+    """Split-K of a prefill GEMM (M > 64, f32 slab epilogue) on the 128x128 tile kernel: 1 where the
+    256x256 kernel takes the shape (its grid fills >= half the CUs), else doubled until the grid has
+    >= 256 workgroups, at most 8 slabs and >= 16 k-blocks (512 of K) per slab.  Without it a 128-token
+    7B prompt runs the O / down projections on 32 workgroups (N / 128 tiles) streaming all of K."""
+    nbt = N // 16
+    if ((M + 255) // 256) * ((nbt + 15) // 16) >= 128:
+        return 1
+    tiles = ((nbt + 7) // 8) * ((M + 127) // 128)
+    sk = 1
+    while tiles * sk < 256 and sk < 8 and (K // 32) // (sk * 2) >= 16:
+        sk *= 2
+    return sk
 
 
 def xfrag_tiles(M: int) -> int:

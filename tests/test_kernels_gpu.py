@@ -130,8 +130,13 @@ def test_gemm_tile(gpu, M, NK, epi):
     y = ops.linear(x, pw, epi)
     yr = x.float() @ w.float().t()
     if epi == "f32":
-        y = y[0]
-        assert _rel(y, yr) < 1e-4
+        assert y.shape[0] == ops.tile_splitk(M, N, K)  # small tile grids split K into f32 slabs
+        assert _rel(y.sum(0), yr) < 1e-4
+        # explicit splits, uneven (K / 32 = 43 k-blocks -> 15 + 15 + 13) and one slab
+        for sk in (1, 3, 8):
+            if (K // 32) >= sk:
+                ys = ops.linear(x, pw, "f32", splitk=sk)
+                assert ys.shape[0] == sk and _rel(ys.sum(0), yr) < 1e-4
     else:
         assert _rel(y, yr) < 1e-2
 
