@@ -196,8 +196,10 @@ class LLMEngine:
             # steps until the earliest request can hit its length limit; with EOS possible, at most
             # sync_every steps between host checks
             reqs = [self._reqs[rid] for rid in running]
-            remaining = max(1, min(q.params.max_tokens - q.gen_host for q in reqs))
-            if all(q.params.ignore_eos for q in reqs):
+            remaining = min(q.params.max_tokens - q.gen_host for q in reqs)
+            if remaining <= 0:
+                n_steps = 0  # a request finished with its prefill token (max_tokens 1): retire it first
+            elif all(q.params.ignore_eos for q in reqs):
                 n_steps = remaining if self.run_ahead is None else min(self.run_ahead, remaining)
             else:
                 n_steps = min(self.sync_every, remaining)
@@ -205,7 +207,8 @@ class LLMEngine:
             max_ctx = max(len(q.prompt_ids) + min(q.gen_host + n_steps, q.params.max_tokens) for q in reqs) + 1
         # the decode run needs no scheduler state: new requests may be added meanwhile
         t0 = time.perf_counter()
-        r.decode(B, n_steps, sample, max_ctx=max_ctx)
+        if n_steps:
+            r.decode(B, n_steps, sample, max_ctx=max_ctx)
         fin, gl, _ = r.read_rows([q.slot for q in reqs])
         with self._lock:
             self.stats["decode_s"] += time.perf_counter() - t0

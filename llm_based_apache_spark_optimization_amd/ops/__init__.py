@@ -256,8 +256,10 @@ def tile_splitk(M: int, N: int, K: int) -> int:
     if ((M + 255) // 256) * ((nbt + 15) // 16) >= 128:
         return 1
     tiles = ((nbt + 7) // 8) * ((M + 127) // 128)
+    target = int(os.environ.get("LSA_TILE_SPLIT_TARGET", "256"))
+    max_sk = int(os.environ.get("LSA_TILE_SPLIT_MAX", "8"))
     sk = 1
-    while tiles * sk < 256 and sk < 8 and (K // 32) // (sk * 2) >= 16:
+    while tiles * sk < target and sk < max_sk and (K // 32) // (sk * 2) >= 16:
         sk *= 2
     return sk
 

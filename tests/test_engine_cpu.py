@@ -128,3 +128,9 @@ def test_num_ctx_window(eng):
     # the truncated prompt generates exactly what the same tokens generate as a plain prompt
     same = eng.generate([eng.fit_context([1] + ids, 24)], SamplingParams(max_tokens=1, ignore_eos=True))[0]
     assert same.token_ids == r.token_ids
+
+
+def test_single_token_request_cpu(eng):
+    steps0 = eng.stats["decode_steps"]
+    r = eng.generate([[1, 9, 8, 7]], SamplingParams(max_tokens=1, ignore_eos=True))[0]
+    assert r.eval_count == 1 and eng.stats["decode_steps"] == steps0

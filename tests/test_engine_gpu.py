@@ -102,6 +102,20 @@ def test_eos_stops(gpu):
     assert r2.done_reason == "stop"
 
 
+def test_single_token_requests_retire_without_decode(gpu):
+    """max_tokens = 1: the prefill's sampled token completes the request; no decode step runs, and a
+    request that needs more tokens batched with it still decodes normally."""
+    eng = build_engine("tiny-nsql", device=str(gpu), max_slots=4, max_model_len=256)
+    full = eng.generate([[1, 5, 6, 7]], SamplingParams(max_tokens=6, ignore_eos=True))[0].token_ids
+    steps0 = eng.stats["decode_steps"]
+    r = eng.generate([[1, 5, 6, 7]], SamplingParams(max_tokens=1, ignore_eos=True))[0]
+    assert r.token_ids == full[:1] and eng.stats["decode_steps"] == steps0
+    a = eng.add_request([1, 5, 6, 7], SamplingParams(max_tokens=1, ignore_eos=True))
+    b = eng.add_request([1, 5, 6, 7], SamplingParams(max_tokens=6, ignore_eos=True))
+    eng.run_until_done([a, b])
+    assert a.output_ids == full[:1] and b.output_ids == full
+
+
 def test_fp8_engine_runs(gpu):
     eng = build_engine("tiny-llama3", device=str(gpu), dtype="fp8", max_slots=4, max_model_len=512)
     bf = build_engine("tiny-llama3", device=str(gpu), dtype="bf16", max_slots=4, max_model_len=512)
