@@ -23,9 +23,10 @@ from __future__ import annotations
 import dataclasses
 import datetime as _dt
 import json
+import queue
 import threading
 import time
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, Iterator, Optional
 
 import torch
 
@@ -69,6 +70,15 @@ class Backend:
                  raw: bool = False) -> GenerateResponse:
         raise NotImplementedError
 
+    def generate_stream(self, model: str, prompt: str, system: str = "", options: Optional[dict] = None,
+                        raw: bool = False) -> Iterator[GenerateResponse]:
+        """Ollama's streaming shape: chunks with ``done=False`` carrying response pieces, then one
+        ``done=True`` chunk with an empty response and the timing fields.  Backends without incremental
+        output send the whole answer as one piece."""
+        r = self.generate(model, prompt, system, options, raw)
+        yield GenerateResponse(model=model, response=r.response, done=False, done_reason="", created_at=r.created_at)
+        yield dataclasses.replace(r, response="")
+
     def models(self) -> list:
         return []
 
@@ -96,8 +106,8 @@ class _EngineLoop:
         self._t = threading.Thread(target=self._run, name=f"engine-{engine.name}", daemon=True)
         self._t.start()
 
-    def submit(self, ids, params):
-        req = self.engine.add_request(ids, params)
+    def submit(self, ids, params, stream: bool = False):
+        req = self.engine.add_request(ids, params, stream=stream)
         with self._cv:
             self._cv.notify()
         return req
@@ -120,6 +130,8 @@ class _EngineLoop:
                 for r in list(self.engine._reqs.values()):
                     r.error = repr(e)
                     r.done.set()
+                    if r.stream is not None:
+                        r.stream.put(("done", None))
                 return
 
     def alive(self) -> bool:
@@ -148,7 +160,7 @@ class EngineService(Backend):
                 self._loops[model] = _EngineLoop(self._factory(model))
             return self._loops[model]
 
-    def generate(self, model, prompt, system="", options=None, raw=False) -> GenerateResponse:
+    def _submit(self, model, prompt, system, options, raw, stream=False):
         lp = self.loop(model)
         eng = lp.engine
         opts = dict(self.defaults)
@@ -157,16 +169,36 @@ class EngineService(Backend):
         ids = eng.encode(eng.render(prompt, system, raw))
         if params.num_ctx is not None:
             ids = eng.fit_context(ids, params.num_ctx, params.num_keep)
-        req = lp.submit(ids, params)
-        if not req.done.wait(self.timeout_s):
-            raise TimeoutError(f"generation on {model} timed out after {self.timeout_s}s")
-        if req.error:
-            raise RuntimeError(f"engine {model} failed: {req.error}")
+        return eng, lp.submit(ids, params, stream=stream)
+
+    @staticmethod
+    def _final(model, eng, req) -> GenerateResponse:
         r = eng.result(req)
         return GenerateResponse(model=model, response=r.text, done_reason=r.done_reason, created_at=_now(),
                                 total_duration=r.total_duration_ns, load_duration=r.load_duration_ns,
                                 prompt_eval_count=r.prompt_tokens, prompt_eval_duration=r.prompt_eval_duration_ns,
                                 eval_count=r.eval_count, eval_duration=r.eval_duration_ns)
+
+    def generate(self, model, prompt, system="", options=None, raw=False) -> GenerateResponse:
+        eng, req = self._submit(model, prompt, system, options, raw)
+        if not req.done.wait(self.timeout_s):
+            raise TimeoutError(f"generation on {model} timed out after {self.timeout_s}s")
+        if req.error:
+            raise RuntimeError(f"engine {model} failed: {req.error}")
+        return self._final(model, eng, req)
+
+    def generate_stream(self, model, prompt, system="", options=None, raw=False) -> Iterator[GenerateResponse]:
+        """Pieces of the answer as the engine's decode runs complete (every ``sync_every`` steps, or
+        ``run_ahead`` steps for requests that ignore EOS), then the final chunk with the timings."""
+        eng, req = self._submit(model, prompt, system, options, raw, stream=True)
+        try:
+            for piece in eng.stream_text(req, timeout_s=self.timeout_s):
+                yield GenerateResponse(model=model, response=piece, done=False, done_reason="", created_at=_now())
+        except queue.Empty:
+            raise TimeoutError(f"generation on {model} timed out after {self.timeout_s}s") from None
+        except RuntimeError as e:
+            raise RuntimeError(f"engine {model} failed: {e}") from None
+        yield dataclasses.replace(self._final(model, eng, req), response="")
 
     def models(self) -> list:
         return sorted(self._loops)

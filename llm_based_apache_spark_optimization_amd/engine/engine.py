@@ -15,13 +15,14 @@ from __future__ import annotations
 
 import dataclasses
 import itertools
+import queue
 import threading
 import time
-from typing import Callable, Optional, Sequence
+from typing import Callable, Iterator, Optional, Sequence
 
 import torch
 
-from ..models.templates import apply_stops, render
+from ..models.templates import STOP_STRINGS, apply_stops, render
 from ..models.tokenizer import tokenizer_for
 from ..runtime import native
 from .runner import BLOCK, ModelRunner
@@ -81,6 +82,9 @@ class Request:
     slot: int = -1
     gen_host: int = 0  # generated-token count as of the last device sync
     error: Optional[str] = None
+    # streaming: ("tokens", ids-so-far) after every host sync that saw new tokens, then ("done", None)
+    stream: Optional[queue.Queue] = None
+    streamed: int = 0
 
 
 @dataclasses.dataclass
@@ -144,14 +148,15 @@ class LLMEngine:
         return ids[-limit:] if len(ids) > limit else ids
 
     # -------------------------------------------------------------------------------- request API
-    def add_request(self, prompt_ids: Sequence[int], params: SamplingParams) -> Request:
+    def add_request(self, prompt_ids: Sequence[int], params: SamplingParams, stream: bool = False) -> Request:
         window = self.runner.max_model_len if params.num_ctx is None else min(self.runner.max_model_len,
                                                                                int(params.num_ctx))
         room = window - len(prompt_ids)
         if room < 1:
             raise ValueError("prompt longer than the model context")
         p = dataclasses.replace(params, max_tokens=max(1, min(params.max_tokens, room, self.runner.max_new_cap)))
-        req = Request(next(self._ids), list(map(int, prompt_ids)), p, time.perf_counter())
+        req = Request(next(self._ids), list(map(int, prompt_ids)), p, time.perf_counter(),
+                      stream=queue.Queue() if stream else None)
         with self._lock:
             self.sched.add(req.rid, len(req.prompt_ids), p.max_tokens)
             self._reqs[req.rid] = req
@@ -217,6 +222,12 @@ class LLMEngine:
             now = time.perf_counter()
             for i, rid in enumerate(running):
                 self._reqs[rid].gen_host = int(gl[i])
+                q = self._reqs[rid]
+                if q.stream is not None and not int(fin[i]):
+                    n = min(int(gl[i]), q.params.max_tokens)
+                    if n > q.streamed:  # the rows are host-visible after read_rows' sync
+                        q.streamed = n
+                        q.stream.put(("tokens", r.tokens_of(q.slot, n)))
                 if int(fin[i]):
                     req = self._reqs.pop(rid)
                     n = min(int(gl[i]), req.params.max_tokens)
@@ -228,6 +239,8 @@ class LLMEngine:
                     self.stats["generated_tokens"] += n
                     self.stats["requests"] += 1
                     req.done.set()
+                    if req.stream is not None:
+                        req.stream.put(("done", None))
                     done.append(req)
             return done
 
@@ -269,6 +282,44 @@ class LLMEngine:
             total_duration_ns=ns(req.finished_at - req.arrival), load_duration_ns=ns(self.load_time_s),
             prompt_eval_duration_ns=ns(req.first_token - req.admitted),
             eval_duration_ns=ns(req.finished_at - req.first_token), done_reason="stop" if ended_eos else "length")
+
+    def text_of(self, token_ids: Sequence[int], req: Request) -> str:
+        """The response text of ``token_ids`` exactly as ``result`` builds it (stop strings applied)."""
+        return apply_stops(self.tok.decode(list(token_ids)), self.spec.template, req.params.stop)
+
+    def stream_text(self, req: Request, timeout_s: Optional[float] = None) -> Iterator[str]:
+        """Text pieces of a request added with ``stream=True``, as the engine's host syncs reveal them.
+        The pieces concatenate to ``result(req).text``: a trailing incomplete UTF-8 sequence and any
+        tail that could still grow into a stop string are held back until later tokens settle them, and
+        nothing past a stop string is sent."""
+        assert req.stream is not None, "add_request(..., stream=True)"
+        stops = tuple(STOP_STRINGS.get(self.spec.template, ())) + tuple(req.params.stop)
+        sent = 0
+        while True:
+            kind, toks = req.stream.get(timeout=timeout_s)
+            if kind == "done":
+                break
+            raw = self.tok.decode(list(toks))
+            text = self.text_of(toks, req)
+            if len(text) < len(raw):  # a stop string appeared: only its prefix is ever sent
+                safe = len(text)
+            else:
+                safe = len(text.rstrip("\ufffd"))
+                hold = 0  # the longest tail that is a proper prefix of a stop string
+                for st in stops:
+                    for k in range(min(len(st) - 1, safe), hold, -1):
+                        if text[safe - k:safe] == st[:k]:
+                            hold = k
+                            break
+                safe -= hold
+            if safe > sent:
+                yield text[sent:safe]
+                sent = safe
+        if req.error:
+            raise RuntimeError(req.error)
+        final = self.result(req).text
+        if len(final) > sent:
+            yield final[sent:]
 
     def generate(self, prompts: Sequence, params: Optional[SamplingParams] = None, system: str = "",
                  raw: bool = False) -> list[GenerationResult]:

@@ -129,10 +129,11 @@ def create_app(ctx: Optional[AppContext] = None) -> FastAPI:
 
     @app.post("/api/generate")
     def api_generate(req: GenerateRequest):
-        r = ctx.backend.generate(req.model, req.prompt, req.system, req.options, req.raw)
-        if req.stream:  # Ollama's NDJSON framing; the whole answer arrives as one final (done) chunk
-            return StreamingResponse(iter([json.dumps(r.to_dict()) + "\n"]), media_type="application/x-ndjson")
-        return r.to_dict()
+        if req.stream:  # Ollama's NDJSON framing: response pieces as decoded, then the done chunk
+            chunks = ctx.backend.generate_stream(req.model, req.prompt, req.system, req.options, req.raw)
+            return StreamingResponse((json.dumps(c.to_dict()) + "\n" for c in chunks),
+                                     media_type="application/x-ndjson")
+        return ctx.backend.generate(req.model, req.prompt, req.system, req.options, req.raw).to_dict()
 
     @app.get("/api/tags")
     def api_tags():

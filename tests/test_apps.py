@@ -91,7 +91,8 @@ def test_fastapi_ollama_api_and_ops(api):
     r = api.post("/api/generate", json={"model": "duckdb-nsql", "prompt": "q", "stream": True})
     lines = [json.loads(x) for x in r.text.splitlines() if x.strip()]
     assert r.headers["content-type"].startswith("application/x-ndjson") and lines[-1]["done"] is True
-    assert lines[-1]["response"] == d["response"]
+    assert all(x["done"] is False for x in lines[:-1]) and lines[-1]["response"] == ""
+    assert "".join(x["response"] for x in lines) == d["response"] and "eval_count" in lines[-1]
     assert any(m["name"] == "llama3.2" for m in api.get("/api/tags").json()["models"])
     assert api.get("/health").json()["ok"] is True
     api.post("/nl2sql", json={"table_schema": "a (int)", "question": "all rows"})

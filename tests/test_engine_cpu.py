@@ -134,3 +134,56 @@ def test_single_token_request_cpu(eng):
     steps0 = eng.stats["decode_steps"]
     r = eng.generate([[1, 9, 8, 7]], SamplingParams(max_tokens=1, ignore_eos=True))[0]
     assert r.eval_count == 1 and eng.stats["decode_steps"] == steps0
+
+
+def test_streaming_pieces_concatenate_to_result(eng):
+    """stream=True: the engine queues token snapshots at every host sync; stream_text turns them into
+    text pieces whose concatenation is exactly the final response."""
+    sp = SamplingParams(max_tokens=40, temperature=0.0, ignore_eos=False)
+    req = eng.add_request([1, 21, 22, 23, 24], sp, stream=True)
+    eng.run_until_done([req])
+    pieces = list(eng.stream_text(req, timeout_s=5))
+    assert "".join(pieces) == eng.result(req).text
+    plain = eng.generate([[1, 21, 22, 23, 24]], sp)[0]
+    assert plain.text == eng.result(req).text
+
+
+def test_stream_text_holds_back_stop_prefixes(eng):
+    """A tail that could still become a stop string is not sent until later tokens settle it; text past
+    a stop string is never sent."""
+    import queue
+    from llm_based_apache_spark_optimization_amd.engine.engine import Request
+
+    class Tok:  # each id is one character
+        def decode(self, ids):
+            return "".join(chr(i) for i in ids)
+
+    old_tok = eng.tok
+    eng.tok = Tok()
+    try:
+        req = Request(0, [1], SamplingParams(max_tokens=64, stop=("STOP",)), 0.0, stream=queue.Queue())
+        text = "SELECT 1; STO"
+        req.stream.put(("tokens", [ord(c) for c in text]))
+        full = "SELECT 1; STOP and more"
+        req.stream.put(("tokens", [ord(c) for c in full]))
+        req.stream.put(("done", None))
+        req.output_ids = [ord(c) for c in full]
+        req.arrival = req.admitted = req.first_token = req.finished_at = 0.0
+        pieces = list(eng.stream_text(req, timeout_s=1))
+        assert pieces[0] == "SELECT 1; "  # "STO" held back (prefix of "STOP")
+        assert "".join(pieces) == "SELECT 1; " == eng.result(req).text
+    finally:
+        eng.tok = old_tok
+
+
+def test_engine_service_streams_ollama_chunks():
+    from llm_based_apache_spark_optimization_amd.client import EngineService
+
+    svc = EngineService(lambda m: build_engine("tiny-nsql", device="cpu", max_slots=2, max_model_len=512))
+    opts = {"temperature": 0, "num_predict": 24, "ignore_eos": True}
+    chunks = list(svc.generate_stream("tiny-nsql", "Select all rows", "Name (string)", opts))
+    whole = svc.generate("tiny-nsql", "Select all rows", "Name (string)", opts)
+    assert chunks[-1].done and chunks[-1].response == "" and chunks[-1].eval_count == 24
+    assert all(not c.done for c in chunks[:-1])
+    assert "".join(c.response for c in chunks) == whole.response
+    svc.loop("tiny-nsql").close()

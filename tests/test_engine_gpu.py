@@ -232,3 +232,14 @@ def test_repeat_penalty_hf_parity_gpu(gpu, graphs):
             s = row[seen]
             row[seen] = torch.where(s < 0, s * pen, s / pen)
             assert row.max() - row[t] <= 0.05 * row.max().abs() + 0.05, (i, t, int(row.argmax()))
+
+
+def test_streaming_on_gpu(gpu):
+    """Token snapshots come from the device output rows after each host sync; the streamed pieces
+    concatenate to the non-streamed answer."""
+    eng = build_engine("tiny-nsql", device=str(gpu), max_slots=4, max_model_len=256)
+    sp = SamplingParams(max_tokens=30, ignore_eos=False)
+    req = eng.add_request([1, 5, 6, 7], sp, stream=True)
+    eng.run_until_done([req])
+    pieces = list(eng.stream_text(req, timeout_s=5))
+    assert "".join(pieces) == eng.result(req).text == eng.generate([[1, 5, 6, 7]], sp)[0].text
