@@ -13,7 +13,9 @@ checkpoint).
   (backends built), a missed heartbeat marks the replica down; its
   in-flight requests are re-dispatched to the remaining replicas (at-least-once; generation is
   idempotent for greedy decoding and seeded sampling);
-* drain: ``close()`` stops accepting, waits for in-flight requests, then stops the workers.
+* drain: ``close()`` stops accepting, waits for in-flight requests, then stops the workers;
+* streaming: a worker forwards its backend's response pieces as they decode; after a re-dispatch the
+  new replica's pieces are replayed from the start and the text already delivered is skipped.
 """
 from __future__ import annotations
 
@@ -24,7 +26,7 @@ import os
 import queue
 import threading
 import time
-from typing import Optional
+from typing import Iterator, Optional
 
 from ..client import Backend, GenerateResponse
 
@@ -62,12 +64,19 @@ def _worker(conn, replica: int, devices: str, kind: str, settings_kw: dict, hear
 
     threading.Thread(target=beat, daemon=True).start()
 
-    def serve(rid, model, prompt, system, options):
+    def serve(rid, model, prompt, system, options, raw=False, stream=False):
         if prompt == "__lsa_crash__":  # fault injection for tests
             os._exit(3)
         try:
-            r = backend.generate(model, prompt, system, options)
-            send(("ok", rid, r.to_dict()))
+            if stream:
+                for c in backend.generate_stream(model, prompt, system, options, raw):
+                    if not c.done:
+                        send(("piece", rid, c.response))
+                    else:
+                        send(("ok", rid, c.to_dict()))
+            else:
+                r = backend.generate(model, prompt, system, options, raw)
+                send(("ok", rid, r.to_dict()))
         except Exception as e:  # noqa: BLE001
             send(("err", rid, repr(e)))
 
@@ -141,13 +150,18 @@ class ReplicaRouter(Backend):
                 r.ready = True
                 continue
             kind, rid, payload = msg
+            if kind == "piece":
+                with self._lock:
+                    w = self._waiters.get(rid) if rid in r.inflight else None  # a stale replica's pieces drop
+                if w is not None and w[2] is not None:
+                    w[2].put(("piece", payload))
+                continue
             with self._lock:
                 r.inflight.pop(rid, None)
                 r.served += 1
                 w = self._waiters.get(rid)
             if w is not None:
-                w[1] = (kind, payload)
-                w[0].set()
+                self._finish(w, (kind, payload))
 
     def _monitor(self):
         while not self._closing:
@@ -166,13 +180,21 @@ class ReplicaRouter(Backend):
             r.inflight.clear()
         log.error("replica %d down (%s); re-dispatching %d request(s)", r.idx, why, len(orphans))
         for rid, req in orphans:
+            w = self._waiters.get(rid)
+            if w is not None and w[2] is not None:
+                w[2].put(("restart", None))
             try:
                 self._dispatch(rid, req)
             except RuntimeError as e:
-                w = self._waiters.get(rid)
                 if w is not None:
-                    w[1] = ("err", repr(e))
-                    w[0].set()
+                    self._finish(w, ("err", repr(e)))
+
+    @staticmethod
+    def _finish(w, result):
+        w[1] = result
+        w[0].set()
+        if w[2] is not None:
+            w[2].put(("end", None))
 
     def _pick(self) -> _Replica:
         live = [r for r in self.replicas if r.alive]
@@ -198,17 +220,54 @@ class ReplicaRouter(Backend):
             raise RuntimeError("router is draining")
         rid = next(self._ids)
         ev = threading.Event()
-        w = [ev, None]
+        w = [ev, None, None]  # done event, (kind, payload), stream queue
         with self._lock:
             self._waiters[rid] = w
         try:
-            self._dispatch(rid, (model, prompt, system, options))
+            self._dispatch(rid, (model, prompt, system, options, raw, False))
             if not ev.wait(self.timeout_s):
                 raise TimeoutError(f"request {rid} timed out")
             kind, payload = w[1]
             if kind != "ok":
                 raise RuntimeError(payload)
             return GenerateResponse(**payload)
+        finally:
+            with self._lock:
+                self._waiters.pop(rid, None)
+
+    def generate_stream(self, model, prompt, system="", options=None, raw=False) -> Iterator[GenerateResponse]:
+        if self._closing:
+            raise RuntimeError("router is draining")
+        rid = next(self._ids)
+        w = [threading.Event(), None, queue.Queue()]
+        with self._lock:
+            self._waiters[rid] = w
+        try:
+            self._dispatch(rid, (model, prompt, system, options, raw, True))
+            sent = got = 0  # chars delivered to the caller / chars of the current replica's stream
+            while True:
+                try:
+                    kind, piece = w[2].get(timeout=self.timeout_s)
+                except queue.Empty:
+                    raise TimeoutError(f"request {rid} timed out") from None
+                if kind == "end":
+                    break
+                if kind == "restart":  # re-dispatched: the new replica's stream starts over
+                    got = 0
+                    continue
+                new = piece[max(0, sent - got):]
+                got += len(piece)
+                if new:
+                    sent += len(new)
+                    yield GenerateResponse(model=model, response=new, done=False, done_reason="")
+            kind, payload = w[1]
+            if kind != "ok":
+                raise RuntimeError(payload)
+            final = GenerateResponse(**payload)
+            full = final.response if final.response else None
+            if full is not None and len(full) > sent:  # a backend that answered in one final chunk
+                yield GenerateResponse(model=model, response=full[sent:], done=False, done_reason="")
+            yield GenerateResponse(**{**payload, "response": ""})
         finally:
             with self._lock:
                 self._waiters.pop(rid, None)

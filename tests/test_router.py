@@ -58,3 +58,26 @@ def test_all_dead_raises():
             r.generate("m", "x")
     finally:
         r.close(drain_s=0.5)
+
+
+def test_streaming_through_router(router):
+    whole = router.generate("duckdb-nsql", "q", "s").response
+    chunks = list(router.generate_stream("duckdb-nsql", "q", "s"))
+    assert chunks[-1].done and chunks[-1].response == "" and all(not c.done for c in chunks[:-1])
+    assert "".join(c.response for c in chunks) == whole
+
+
+def test_streaming_survives_replica_death(router):
+    out = []
+
+    def go():
+        out.append("".join(c.response for c in router.generate_stream("llama3.2", "explain", "troubleshoot",
+                                                                       {"fake_delay": 1.0})))
+
+    ts = [threading.Thread(target=go) for _ in range(3)]
+    [t.start() for t in ts]
+    time.sleep(0.4)
+    router.replicas[0].proc.kill()
+    [t.join() for t in ts]
+    expect = router.generate("llama3.2", "explain", "troubleshoot").response
+    assert out == [expect] * 3
