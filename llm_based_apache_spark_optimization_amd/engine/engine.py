@@ -189,8 +189,12 @@ class LLMEngine:
                 self._prefill_packed(seqs, any_sample)
                 t1 = time.perf_counter()
                 for rid in admitted:
-                    self._reqs[rid].first_token = t1
-                    self._reqs[rid].gen_host = 1
+                    q = self._reqs[rid]
+                    q.first_token = t1
+                    q.gen_host = 1
+                    if q.stream is not None:  # the prefill's token goes out now (one sync, streaming only)
+                        q.streamed = 1
+                        q.stream.put(("tokens", r.tokens_of(q.slot, 1)))
                 self.stats["prefill_s"] += t1 - t0
                 self.stats["prompt_tokens"] += sum(len(s[1]) for s in seqs)
             running = self.sched.running()
