@@ -159,6 +159,18 @@ def run(args) -> dict:
     return phases[0] if len(phases) == 1 else {"phases": phases}
 
 
+def as_generate(route: str, body: dict) -> dict:
+    """The /nl2sql or /explain_error request as the equivalent streaming ``/api/generate`` call (the
+    same model, system and prompt strings the pipeline builds)."""
+    from . import prompts
+
+    if route == "nl2sql":
+        return {"model": "duckdb-nsql", "system": prompts.nl2sql_system(body["table_schema"]),
+                "prompt": body["question"], "options": body.get("options"), "stream": True}
+    return {"model": "llama3.2", "system": prompts.EXPLAIN_SYSTEM,
+            "prompt": prompts.explain_prompt(body["error_message"]), "options": body.get("options"), "stream": True}
+
+
 def _phase(cl, args, qps: float, rng: random.Random, make_request) -> dict:
     """One fixed-rate load phase: a Poisson arrival schedule fixed up front, fired from a thread pool."""
     sched, t = [], 0.0
@@ -177,15 +189,29 @@ def _phase(cl, args, qps: float, rng: random.Random, make_request) -> dict:
         if delay > 0:
             time.sleep(delay)
         t1 = time.perf_counter()
+        ttft = None
         try:
-            r = cl.post("/" + route, json=body)
-            ok = r.status_code == 200
-            d = r.json() if ok else {}
+            if getattr(args, "stream", False):  # Ollama streaming API: time to the first response piece
+                d = {}
+                with cl.stream("POST", "/api/generate", json=as_generate(route, body)) as r:
+                    ok = r.status_code == 200
+                    for line in r.iter_lines():
+                        if not line.strip():
+                            continue
+                        c = json.loads(line)
+                        if ttft is None and c.get("response"):
+                            ttft = time.perf_counter() - t1
+                        if c.get("done"):
+                            d = c
+            else:
+                r = cl.post("/" + route, json=body)
+                ok = r.status_code == 200
+                d = r.json() if ok else {}
         except Exception as e:  # noqa: BLE001 - counted as a failed request
             ok, d = False, {"error": repr(e)}
         lat = time.perf_counter() - t1
         with lock:
-            results.append((route, ok, lat, int(d.get("eval_count", 0)), at))
+            results.append((route, ok, lat, int(d.get("eval_count", 0)), at, ttft))
 
     with ThreadPoolExecutor(max_workers=args.concurrency) as ex:
         list(ex.map(fire, sched))
@@ -199,6 +225,9 @@ def _phase(cl, args, qps: float, rng: random.Random, make_request) -> dict:
         lats = [r[2] for r in results if r[0] == route and r[1]]
         out[route] = {"n": len(lats), "p50_s": _pct(lats, 0.5), "p90_s": _pct(lats, 0.9), "p99_s": _pct(lats, 0.99),
                       "mean_s": round(statistics.fmean(lats), 4) if lats else None}
+        ttfts = [r[5] for r in results if r[0] == route and r[1] and r[5] is not None]
+        if ttfts:
+            out[route].update(ttft_p50_s=_pct(ttfts, 0.5), ttft_p99_s=_pct(ttfts, 0.99))
     ref = {"nl2sql": 5.2381, "explain_error": 22.75}  # BASELINE.md p50s (other hardware, single requests)
     out["vs_baseline_p50_latency"] = {k: (round(ref[k] / out[k]["p50_s"], 2) if out[k]["p50_s"] else None)
                                       for k in ref}
@@ -220,6 +249,8 @@ def main(argv=None) -> None:
     ap.add_argument("--timeout", type=float, default=600.0)
     ap.add_argument("--engine", default="hip", help="hip | fake (plumbing only)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--stream", action="store_true",
+                    help="send each request as a streaming /api/generate call and report time to first piece")
     print(json.dumps(run(ap.parse_args(argv))), flush=True)
 
 

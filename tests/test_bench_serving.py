@@ -9,6 +9,12 @@ def test_bench_serving_fake_engine():
     assert out["nl2sql"]["p50_s"] is not None and out["output_tokens_per_sec"] > 0
 
 
+def test_bench_serving_streaming_fake_engine():
+    out = bench_serving.run(bench_serving_args(qps=40, duration=0.5, stream=True))
+    assert out["failed"] == 0 and out["requests"] > 5
+    assert out["nl2sql"]["ttft_p50_s"] is not None and out["nl2sql"]["ttft_p50_s"] <= out["nl2sql"]["p99_s"]
+
+
 def test_synthetic_prompts_sizes():
     import random
 
