@@ -199,7 +199,7 @@ def _phase(cl, args, qps: float, rng: random.Random, make_request) -> dict:
                         if not line.strip():
                             continue
                         c = json.loads(line)
-                        if ttft is None and c.get("response"):
+                        if ttft is None and not c.get("done"):  # first chunk = first token(s) out
                             ttft = time.perf_counter() - t1
                         if c.get("done"):
                             d = c

@@ -292,7 +292,7 @@ class LLMEngine:
         return apply_stops(self.tok.decode(list(token_ids)), self.spec.template, req.params.stop)
 
     def stream_text(self, req: Request, timeout_s: Optional[float] = None) -> Iterator[str]:
-        """Text pieces of a request added with ``stream=True``, as the engine's host syncs reveal them.
+        """Text pieces of a request added with ``stream=True``, one per host sync that revealed tokens.
         The pieces concatenate to ``result(req).text``: a trailing incomplete UTF-8 sequence and any
         tail that could still grow into a stop string are held back until later tokens settle them, and
         nothing past a stop string is sent."""
@@ -316,9 +316,11 @@ class LLMEngine:
                             hold = k
                             break
                 safe -= hold
-            if safe > sent:
-                yield text[sent:safe]
-                sent = safe
+            # one piece per snapshot, empty while no new text is settled (tokens that decode to nothing,
+            # held-back tails): the client sees progress at every sync, as with Ollama's per-token chunks
+            piece = text[sent:safe] if safe > sent else ""
+            sent = max(sent, safe)
+            yield piece
         if req.error:
             raise RuntimeError(req.error)
         final = self.result(req).text

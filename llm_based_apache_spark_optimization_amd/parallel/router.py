@@ -257,9 +257,8 @@ class ReplicaRouter(Backend):
                     continue
                 new = piece[max(0, sent - got):]
                 got += len(piece)
-                if new:
-                    sent += len(new)
-                    yield GenerateResponse(model=model, response=new, done=False, done_reason="")
+                sent += len(new)
+                yield GenerateResponse(model=model, response=new, done=False, done_reason="")
             kind, payload = w[1]
             if kind != "ok":
                 raise RuntimeError(payload)
