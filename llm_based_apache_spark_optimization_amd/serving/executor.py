@@ -241,42 +241,56 @@ def write_csv(result: Result, path: str) -> str:
     return path
 
 
-class SparkExecutor:  # pragma: no cover - needs pyspark + a JVM
-    """The reference's backend: a process-wide SparkSession in local mode."""
+class SparkExecutor:
+    """The reference's backend: a process-wide SparkSession in local mode (FastAPI/app.py:19,
+    Flask/app.py:16).
+
+    The reference registered every upload as the global view ``temp_view`` on that one session
+    (FastAPI/app.py:94, Flask/app.py:111), so two concurrent requests replaced each other's view and a
+    query could run against another user's CSV.  Here each request gets its own
+    ``spark.newSession()``: sessions share the SparkContext (and its executors) but not the temp-view
+    catalog, so every request sees exactly its own ``temp_view``.  The view is dropped on ``close()``.
+    ``spark`` may be injected (tests use a fake session object; pyspark is optional)."""
 
     name = "spark"
 
-    def __init__(self, app_name: str = "LSA-Spark"):
-        from pyspark.sql import SparkSession
+    def __init__(self, app_name: str = "LSA-Spark", spark=None):
+        if spark is None:  # pragma: no cover - needs pyspark + a JVM
+            from pyspark.sql import SparkSession
 
-        self.spark = SparkSession.builder.appName(app_name).getOrCreate()
+            spark = SparkSession.builder.appName(app_name).getOrCreate()
+        self.spark = spark
 
     def load_csv(self, path: str):
-        df = self.spark.read.csv(path, header=True, inferSchema=True)
-        return Table("temp_view", df.columns, list(df.dtypes), []), df
+        sess = self.spark.newSession()  # request-private temp-view catalog (shared SparkContext)
+        df = sess.read.csv(path, header=True, inferSchema=True)
+        return Table("temp_view", list(df.columns), list(df.dtypes), []), df, sess
 
     @staticmethod
     def table_of(loaded) -> Table:
         return loaded[0]
 
     def session(self, loaded, view: str = "temp_view"):
-        table, df = loaded
-        df.createOrReplaceTempView(view)
-        spark = self.spark
+        table, df, spark = loaded
+        df.createOrReplaceTempView(view)  # registers in the request's own session only
 
         class _S:
             def __init__(self):
                 self.table = table
+                self.spark = spark
 
             def sql(self, q):
                 try:
                     out = spark.sql(q)
-                    return Result(out.columns, [tuple(r) for r in out.collect()])
+                    return Result(list(out.columns), [tuple(r) for r in out.collect()])
                 except Exception as e:  # noqa: BLE001
                     raise SQLExecutionError(str(e)) from None
 
             def close(self):
-                pass
+                try:
+                    spark.catalog.dropTempView(view)
+                except Exception:  # noqa: BLE001 - best effort
+                    pass
 
         return _S()
 

@@ -32,6 +32,7 @@ from pydantic import BaseModel
 from .. import prompts
 from ..utils.metrics import REGISTRY
 from ..utils.tracing import new_request_id
+from .pipeline import resolve_input
 from .service import AppContext, make_context
 
 
@@ -72,12 +73,15 @@ def create_app(ctx: Optional[AppContext] = None) -> FastAPI:
     @app.post("/process-data/")
     def modify_string(data: InputString):
         t0 = time.perf_counter()
-        file_path = os.path.join(s.input_dir, data.file_name)
+        file_path = resolve_input(s.input_dir, data.file_name)
+        if file_path is None:
+            REGISTRY.inc("lsa_requests_total", 1, "requests", route="process-data", outcome="bad_name")
+            return {"error": "Invalid file name: " + data.file_name}
         if not os.path.exists(file_path):
             REGISTRY.inc("lsa_requests_total", 1, "requests", route="process-data", outcome="not_found")
             return {"error": "CSV file not found at " + file_path}
         res = ctx.pipeline.run(file_path, data.file_name, data.input_text,
-                               output_name=lambda ts: f"{ts}_{data.file_name}.csv")
+                               output_name=lambda ts: f"{ts}_{os.path.basename(file_path)}.csv")
         REGISTRY.observe("lsa_request_seconds", time.perf_counter() - t0, "e2e latency", route="process-data")
         if not res.ok:
             REGISTRY.inc("lsa_requests_total", 1, "requests", route="process-data", outcome="sql_error")
@@ -99,7 +103,9 @@ def create_app(ctx: Optional[AppContext] = None) -> FastAPI:
             raise HTTPException(422, "question (or input_text) is required")
         schema = req.table_schema or req.schema_text
         if schema is None and req.file_name:
-            path = os.path.join(s.input_dir, req.file_name)
+            path = resolve_input(s.input_dir, req.file_name)
+            if path is None:
+                raise HTTPException(400, "invalid file_name: " + req.file_name)
             if not os.path.exists(path):
                 return {"error": "CSV file not found at " + path}
             table = ctx.pipeline.executor.table_of(ctx.pipeline.executor.load_csv(path))

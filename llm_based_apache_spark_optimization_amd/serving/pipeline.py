@@ -99,6 +99,19 @@ def unique_path(path: str) -> str:
             cand = f"{base}_{i}{ext}"
 
 
+def resolve_input(input_dir: str, name: str) -> Optional[str]:
+    """``name`` resolved under ``input_dir``, or None when it would leave that directory (absolute
+    paths, ``..`` components, symlinks pointing outside).  The reference joined the untrusted
+    ``file_name`` onto its input directory unchecked (FastAPI/app.py:68)."""
+    if not name or "\x00" in name or os.path.isabs(name):
+        return None
+    root = os.path.realpath(input_dir)
+    path = os.path.realpath(os.path.join(root, name))
+    if os.path.commonpath([root, path]) != root or path == root:
+        return None
+    return path
+
+
 class Pipeline:
     def __init__(self, backend, executor, history: HistoryStore, settings, status: Optional[StatusBoard] = None):
         self.backend = backend
