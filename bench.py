@@ -9,7 +9,12 @@ request's end-to-end latency.  Random-init weights of the named architecture (no
 downloaded), bf16 (or ``--dtype fp8`` weights).
 
     python bench.py                      # 1 GPU, defaults
-    torchrun --nproc-per-node 8 bench.py --gpus 8     # 8 DP replicas (``--tp 2``: 4 x TP2)
+    torchrun --nproc-per-node 8 bench.py --gpus 8     # 8 DP replicas of one GPU each (dp8)
+    torchrun --nproc-per-node 8 bench.py --gpus 8 --tp 2   # BASELINE config 4: 4 replicas x TP2 (tp2dp4)
+
+Before the timed region one request of the first warm-up round is checked against the plain fp32
+PyTorch forward over the same weights (``models.llama.reference_forward``, teacher-forced: every chosen
+token must be within bf16 noise of the oracle's argmax); the result is reported as ``numerics``.
 
 Prints ONE JSON line on rank 0.  ``value`` = whole-job output tokens/s (sum over replicas, timed by
 the slowest rank); ``vs_baseline`` = value / 4.0 tok/s, the only throughput figure BASELINE.md
@@ -33,6 +38,21 @@ REF_P50_S = 5.2381     # duckdb-nsql p50 end-to-end latency, run B
 REF_P50_S_LLAMA = 22.7463
 
 MODEL_NAMES = {"duckdb-nsql": "duckdb-nsql-7B", "llama3.2": "Llama-3.2-3B-Instruct", "mistral": "Mistral-7B-v0.3"}
+
+
+def check_numerics(eng, prompt, tokens, n=16):
+    """Teacher-forced check of the first ``n`` generated tokens against the fp32 reference forward:
+    gap = (oracle max logit - oracle logit of our token) / oracle logit std, worst over the tokens."""
+    from llm_based_apache_spark_optimization_amd.models.llama import reference_forward
+
+    toks = list(tokens[:n])
+    lg = reference_forward(eng.runner.w, list(prompt) + toks[:-1])[len(prompt) - 1:]
+    chosen = lg.gather(1, torch.tensor(toks, device=lg.device).view(-1, 1)).squeeze(1)
+    gap = ((lg.max(1).values - chosen) / lg.std(1)).max().item()
+    agree = int((lg.argmax(1).cpu() == torch.tensor(toks)).sum())
+    del lg
+    return {"tokens_checked": len(toks), "argmax_agree": agree, "max_gap_in_logit_std": round(gap, 4),
+            "ok": gap < 0.15}
 
 
 def main() -> int:
@@ -70,7 +90,14 @@ def main() -> int:
         if not cpu:
             torch.cuda.synchronize()
 
+    if world != args.gpus and not cpu:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; launch with torchrun "
+              f"--nproc-per-node {args.gpus}", file=sys.stderr)
+        return 2
     tp = max(1, args.tp)
+    if world % tp:
+        print(f"bench.py: WORLD_SIZE {world} not divisible by --tp {tp}", file=sys.stderr)
+        return 2
     replica, tpg = make_replica_groups(world, tp, rank, device) if world > 1 else (0, None)
     dp = world // tp
 
@@ -89,8 +116,12 @@ def main() -> int:
         assert all(r.eval_count == args.new_tokens for r in res), [r.eval_count for r in res]
         return res
 
-    for _ in range(args.warmup):
-        one_step()
+    numerics = None
+    for i in range(args.warmup):
+        res = one_step()
+        if i == 0 and tp == 1:
+            numerics = check_numerics(eng, prompts[0], res[0].token_ids)
+    eng.stats.update(decode_s=0.0, decode_steps=0, prefill_s=0.0)  # timed rounds only (no capture/warm-up)
     if world > 1:
         dist.barrier()
     sync()
@@ -143,6 +174,7 @@ def main() -> int:
             "vs_baseline_p50_latency": round(ref_p50 / p50, 2),
             "decode_ms_per_token_step": round(decode_ms_tok, 3),
             "per_gpu_tokens_per_sec": round(value / world, 2),
+            "numerics": numerics,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

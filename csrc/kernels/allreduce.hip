@@ -53,7 +53,11 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
   uint8_t* mine = regions[rank];
   uint32_t* my_epoch = reinterpret_cast<uint32_t*>(mine + AR_EPOCH_OFF);
   __shared__ uint32_t s_ep;
-  if (tid == 0) s_ep = my_epoch[b] + 1u;
+  __shared__ int s_timeout;
+  if (tid == 0) {
+    s_ep = my_epoch[b] + 1u;
+    s_timeout = 0;
+  }
   __syncthreads();
   const uint32_t ep = s_ep;
   const size_t slot_off = AR_DATA_OFF + (size_t)(ep & 1u) * W * maxb;
@@ -90,12 +94,27 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > timeout_ticks) {
         atomicExch(err, 1);
+        s_timeout = 1;
         break;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
+
+  if (s_timeout) {  // a peer never arrived: poison this block's result (NaN), never a silent partial sum
+    const float nan = __builtin_nanf("");
+    const float4 nv = make_float4(nan, nan, nan, nan);
+    for (long i = (long)b * AR_THREADS + tid; i < n4; i += stride) {
+      if (GATHER) {
+        for (int p = 0; p < W; ++p) out[(long)p * n4 + i] = nv;
+      } else {
+        data[i] = nv;
+      }
+    }
+    if (tid == 0) my_epoch[b] = ep;
+    return;
+  }
 
   if (GATHER) {  // 3'. concatenate the slots in rank order
     for (long i = (long)b * AR_THREADS + tid; i < n4; i += stride) {

@@ -34,6 +34,10 @@ BLOCK = 64
 REPEAT_WINDOW = 64  # repetition-penalty ring (Ollama repeat_last_n default; larger values are clamped)
 
 
+class TPCommError(RuntimeError):
+    """A TP peer missed a one-shot all-reduce (the kernel poisoned the result with NaN and set err)."""
+
+
 class ModelRunner:
     def __init__(self, weights: LlamaWeights, max_slots: int = 32, max_model_len: int = 4096,
                  num_kv_blocks: Optional[int] = None, kv_memory_fraction: float = 0.85,
@@ -535,9 +539,16 @@ class ModelRunner:
     def read_rows(self, slots: Sequence[int]):
         """(finished, gen_len, tokens) for ``slots`` (one device->host sync)."""
         idx = torch.tensor(list(slots), dtype=torch.long, device=self.device)
-        fin = self.finished.index_select(0, idx).cpu()
-        gl = self.gen_len.index_select(0, idx).cpu()
-        return fin, gl, idx
+        n = idx.numel()
+        parts = [self.finished.index_select(0, idx), self.gen_len.index_select(0, idx)]
+        car = getattr(self.tp, "car", None) if self.tp is not None else None
+        if car is not None:
+            parts.append(car.err)  # one-shot all-reduce timeout flag, read in the same transfer
+        host = torch.cat(parts).cpu()
+        if car is not None and int(host[2 * n]):
+            raise TPCommError("tensor-parallel all-reduce: a peer did not arrive within the timeout; "
+                              "this replica's outputs since the last sync are invalid")
+        return host[:n], host[n:2 * n], idx
 
     def tokens_of(self, slot: int, n: int) -> list[int]:
         return self.out_tokens[slot, :n].tolist()

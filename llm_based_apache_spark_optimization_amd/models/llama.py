@@ -12,6 +12,7 @@ e4m3fn with per-output-channel scales at load time (BASELINE config 5).
 from __future__ import annotations
 
 import dataclasses
+import math
 import glob
 import json
 import os
@@ -164,3 +165,50 @@ def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[st
     for fn in sorted(glob.glob(os.path.join(path, "*.safetensors"))):
         sd.update(load_file(fn))
     return from_hf_state_dict(spec, sd, device, kind, tp_rank, tp_size)
+
+
+@torch.no_grad()
+def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32) -> torch.Tensor:
+    """fp32 causal forward of one sequence over the weights exactly as packed (``dense()`` undoes the
+    fragment shuffle and the fp8 quantisation, so an fp8 model is compared against its own dequantised
+    weights): logits [T, V] f32.  The numerics oracle for the engine at production shapes
+    (tests/test_prod_shapes_gpu.py); plain PyTorch, one layer's dense weights alive at a time."""
+    from ..ops import reference as ref
+
+    spec, dev = w.spec, w.device
+    ids = torch.as_tensor(ids, dtype=torch.long, device=dev)
+    T, hd = ids.numel(), spec.head_dim
+    H, Hkv = spec.n_heads // w.tp_size, spec.n_kv_heads // w.tp_size
+    G = H // Hkv
+    cos, sin = ref.rope_tables(hd, T, spec.rope_theta, spec.rope_scaling, device=dev)
+    cos, sin = cos.unsqueeze(1), sin.unsqueeze(1)
+
+    def norm(x, g):
+        return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + spec.rms_eps) * g.float()
+
+    def rope(x):
+        lo, hi = x[..., : hd // 2], x[..., hd // 2:]
+        return torch.cat([lo * cos - hi * sin, hi * cos + lo * sin], dim=-1)
+
+    def bf(x):  # the kernels hand activations between ops in bf16
+        return x.to(torch.bfloat16).float()
+
+    h = w.embed[ids].float()
+    mask = torch.full((T, T), float("-inf"), device=dev).triu(1)
+    for lw in w.layers:
+        x = bf(norm(h, lw.attn_norm))
+        qkv = x @ lw.wqkv.dense().float().t()
+        q = qkv[:, : H * hd].view(T, H, hd)
+        k = qkv[:, H * hd:(H + Hkv) * hd].view(T, Hkv, hd)
+        v = qkv[:, (H + Hkv) * hd:].view(T, Hkv, hd)
+        q, k, v = bf(rope(q)), bf(rope(k)), bf(v)
+        k, v = k.repeat_interleave(G, 1), v.repeat_interleave(G, 1)
+        s = torch.einsum("qhd,khd->hqk", q, k) / math.sqrt(hd) + mask
+        a = bf(torch.einsum("hqk,khd->qhd", s.softmax(-1), v).reshape(T, H * hd))
+        h = h + a @ lw.wo.dense().float().t()
+        x = bf(norm(h, lw.mlp_norm))
+        gu = (x @ lw.w_gate_up.dense().float().t()).view(T, -1, 2, 16)
+        act = bf(torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(T, -1)
+        h = h + act @ lw.w_down.dense().float().t()
+    x = bf(norm(h, w.final_norm))
+    return x @ w.lm_head.dense().float().t()

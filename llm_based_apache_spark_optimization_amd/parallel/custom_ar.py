@@ -85,7 +85,8 @@ class IpcAllReduce:
         return out
 
     def check(self) -> None:
-        """Raise if any wait timed out since construction (a peer never arrived)."""
+        """Raise if any wait timed out since construction (a peer never arrived).  The engine reads the
+        same flag at every host sync (``ModelRunner.read_rows``); a timed-out block's result is NaN."""
         if int(self.err.item()):
             raise RuntimeError("IpcAllReduce: a peer did not arrive within the timeout")
 
@@ -107,4 +108,5 @@ def maybe_ipc_allreduce(group, rank: int, world: int, device: torch.device) -> O
     if world > ops.ext().ar_max_world:
         return None
     return IpcAllReduce(group, rank, world, device,
-                        max_bytes=int(os.environ.get("LSA_CUSTOM_AR_MAX_BYTES", DEFAULT_MAX_BYTES)))
+                        max_bytes=int(os.environ.get("LSA_CUSTOM_AR_MAX_BYTES", DEFAULT_MAX_BYTES)),
+                        timeout_s=float(os.environ.get("LSA_CUSTOM_AR_TIMEOUT_S", DEFAULT_TIMEOUT_S)))

@@ -33,20 +33,95 @@ from ..client import Backend, GenerateResponse
 log = logging.getLogger(__name__)
 
 
-def _worker(conn, replica: int, devices: str, kind: str, settings_kw: dict, heartbeat_s: float):
-    """Replica process: build backends lazily, answer requests until told to stop."""
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _visible_gpus() -> int:
+    """GPU count without initialising HIP in this process (the router must not touch the GPU before
+    its workers are spawned)."""
+    env = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    if env:
+        return len([x for x in env.split(",") if x.strip()])
+    try:
+        import torch
+
+        return torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def _init_tp_rank(tp_rank: int, tp_size: int, port: int, shared_device: bool) -> None:
+    """torch.distributed world = this replica's TP ranks (one process per GPU; RCCL when every rank
+    owns its own GPU, gloo when ranks share one device (test boxes) or there is no GPU)."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(tp_rank),
+                      WORLD_SIZE=str(tp_size), LOCAL_RANK="0")
+    if torch.cuda.is_available() and not shared_device:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        if torch.cuda.is_available():
+            torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+
+
+def _tp_engine_factory(settings, tp_rank: int, tp_size: int):
+    """model -> LLMEngine holding this rank's shard; each model gets its own TP group (own RCCL
+    communicator + IPC all-reduce region), created collectively inside the lockstep ``build``."""
+    import torch
+    import torch.distributed as dist
+
+    from ..serving.service import engine_factory
+    from .tp import TPGroup
+
+    def tp_for_model():
+        g = dist.new_group(list(range(tp_size)))
+        dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        return TPGroup(g, tp_rank, tp_size, dev)
+
+    return engine_factory(settings, tp_factory=tp_for_model)
+
+
+def _worker(conn, replica: int, devices: str, kind: str, settings_kw: dict, heartbeat_s: float,
+            tp_rank: int = 0, tp_size: int = 1, port: int = 0, peers=None, shared_device: bool = False):
+    """Replica process: build backends lazily, answer requests until told to stop.
+
+    TP replicas (tp_size > 1): rank 0 is the leader (``conn`` = router pipe, ``peers`` = pipes to its
+    followers); ranks > 0 are followers (``conn`` = pipe from the leader) that mirror its runner calls
+    (parallel/lockstep.py)."""
     if devices:
         os.environ["HIP_VISIBLE_DEVICES"] = devices  # before any HIP call in this process
     from ..config import Settings
-    from ..client import FakeBackend
+    from ..client import EngineService, FakeBackend
 
-    if kind == "fake":
+    chan = None
+    if tp_size > 1:
+        from . import lockstep
+
+        _init_tp_rank(tp_rank, tp_size, port, shared_device)
+        s = Settings(**settings_kw)
+        build = _tp_engine_factory(s, tp_rank, tp_size)
+        if tp_rank > 0:
+            lockstep.follow(conn, build)
+            return
+        chan = lockstep.LeaderChannel(peers or [])
+        defaults = {"temperature": s.temperature, "top_k": s.top_k, "top_p": s.top_p, "num_predict": s.max_new_tokens}
+        backend = EngineService(lockstep.lockstep_factory(build, chan), defaults=defaults,
+                                timeout_s=s.request_timeout_s)
+    elif kind == "fake":
         backend = FakeBackend()
     else:
         from ..serving.service import backend_from_settings
 
         s = Settings(**settings_kw)
-        s.dp = 1
+        s.dp, s.tp = 1, 1
         backend = backend_from_settings(s)
     lock = threading.Lock()
 
@@ -85,8 +160,10 @@ def _worker(conn, replica: int, devices: str, kind: str, settings_kw: dict, hear
         try:
             msg = conn.recv()
         except (EOFError, OSError):
-            return
+            msg = ("stop",)
         if msg[0] == "stop":
+            if chan is not None:
+                chan.close()  # followers leave their replay loops
             return
         if msg[0] == "gen":
             t = threading.Thread(target=serve, args=msg[1:], daemon=True)  # concurrency -> batching
@@ -95,8 +172,9 @@ def _worker(conn, replica: int, devices: str, kind: str, settings_kw: dict, hear
 
 
 class _Replica:
-    def __init__(self, idx: int, proc, conn):
+    def __init__(self, idx: int, proc, conn, followers=()):
         self.idx, self.proc, self.conn = idx, proc, conn
+        self.followers = list(followers)  # TP ranks > 0 of this replica (no pipe to the router)
         self.inflight: dict = {}
         self.alive = True
         self.last_hb = time.time()
@@ -107,8 +185,11 @@ class _Replica:
 
 class ReplicaRouter(Backend):
     def __init__(self, dp: int, kind: str = "hip", devices: Optional[list] = None, settings_kw: Optional[dict] = None,
-                 heartbeat_s: float = 2.0, dead_after_s: float = 30.0, timeout_s: float = 300.0):
+                 heartbeat_s: float = 2.0, dead_after_s: float = 30.0, timeout_s: float = 300.0, tp: int = 1):
+        """``devices[i]``: replica i's GPU ids, one per TP rank (comma-separated string or list); each
+        rank process sees only its own GPU.  ``tp > 1``: every replica is a lockstep TP group."""
         self.kind = kind
+        self.tp = max(1, int(tp))
         self.timeout_s = timeout_s
         self.dead_after_s = dead_after_s
         self._ids = itertools.count(1)
@@ -119,10 +200,32 @@ class ReplicaRouter(Backend):
         self.replicas = []
         for i in range(dp):
             a, b = ctx.Pipe()
-            dev = devices[i] if devices else (str(i) if kind != "fake" else "")
-            p = ctx.Process(target=_worker, args=(b, i, dev, kind, settings_kw or {}, heartbeat_s), daemon=True)
+            if devices:
+                dev = devices[i].split(",") if isinstance(devices[i], str) else [str(x) for x in devices[i]]
+            else:
+                dev = [str(i * self.tp + j) if kind != "fake" else "" for j in range(self.tp)]
+            if self.tp == 1:
+                p = ctx.Process(target=_worker, args=(b, i, ",".join(dev), kind, settings_kw or {}, heartbeat_s),
+                                daemon=True)
+                p.start()
+                self.replicas.append(_Replica(i, p, a))
+                continue
+            # TP replica: rank 0 leads (router pipe + one pipe per follower), ranks > 0 follow
+            assert len(dev) == self.tp, f"replica {i}: {len(dev)} devices for tp={self.tp}"
+            port = _free_port()
+            shared = len(set(dev)) < len(dev)  # ranks sharing one GPU (test boxes): gloo, not RCCL
+            lead_ends, followers = [], []
+            for j in range(1, self.tp):
+                lc, fc = ctx.Pipe()
+                lead_ends.append(lc)
+                fp = ctx.Process(target=_worker, args=(fc, i, dev[j], kind, settings_kw or {}, heartbeat_s, j,
+                                                       self.tp, port, None, shared), daemon=True)
+                fp.start()
+                followers.append(fp)
+            p = ctx.Process(target=_worker, args=(b, i, dev[0], kind, settings_kw or {}, heartbeat_s, 0, self.tp,
+                                                  port, lead_ends, shared), daemon=True)
             p.start()
-            self.replicas.append(_Replica(i, p, a))
+            self.replicas.append(_Replica(i, p, a, followers))
         for r in self.replicas:
             threading.Thread(target=self._reader, args=(r,), daemon=True).start()
         threading.Thread(target=self._monitor, daemon=True).start()
@@ -132,10 +235,15 @@ class ReplicaRouter(Backend):
         import dataclasses
 
         kw = {f.name: getattr(settings, f.name) for f in dataclasses.fields(settings)}
-        tp = max(1, settings.tp)
-        devices = [",".join(str(i * tp + j) for j in range(tp)) for i in range(settings.dp)]
-        return ReplicaRouter(settings.dp, "fake" if settings.engine == "fake" else "hip", devices, kw,
-                             timeout_s=settings.request_timeout_s)
+        tp, dp = max(1, settings.tp), max(1, settings.dp)
+        kind = "fake" if settings.engine == "fake" else "hip"
+        ngpu = _visible_gpus() if kind == "hip" else 0
+        if kind == "hip" and ngpu and dp * tp > ngpu:
+            log.warning("dp=%d x tp=%d needs %d GPUs, %d visible: ranks share GPUs (round-robin)", dp, tp, dp * tp, ngpu)
+        env = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+        ids = [x.strip() for x in env.split(",") if x.strip()] if env else [str(k) for k in range(ngpu)]
+        devices = [[ids[(i * tp + j) % ngpu] if ngpu else "" for j in range(tp)] for i in range(dp)]
+        return ReplicaRouter(dp, kind, devices, kw, timeout_s=settings.request_timeout_s, tp=tp)
 
     # ------------------------------------------------------------------------------ internals
     def _reader(self, r: _Replica):
@@ -168,8 +276,12 @@ class ReplicaRouter(Backend):
             time.sleep(0.5)
             for r in self.replicas:
                 hb_lost = r.ready and time.time() - r.last_hb > self.dead_after_s
-                if r.alive and (not r.proc.is_alive() or hb_lost):
-                    self._mark_dead(r, "process exited" if not r.proc.is_alive() else "heartbeat lost")
+                procs_ok = r.proc.is_alive() and all(f.is_alive() for f in r.followers)
+                if r.alive and (not procs_ok or hb_lost):
+                    self._mark_dead(r, "process exited" if not procs_ok else "heartbeat lost")
+                    for p in [r.proc, *r.followers]:  # a TP group missing a rank can never step again
+                        if p.is_alive():
+                            p.terminate()
 
     def _mark_dead(self, r: _Replica, why: str):
         with self._lock:
@@ -290,6 +402,7 @@ class ReplicaRouter(Backend):
             except (OSError, EOFError):
                 pass
         for r in self.replicas:
-            r.proc.join(timeout=5)
-            if r.proc.is_alive():
-                r.proc.terminate()
+            for p in [r.proc, *r.followers]:
+                p.join(timeout=5)
+                if p.is_alive():
+                    p.terminate()

@@ -13,18 +13,21 @@ from .pipeline import Pipeline, StatusBoard
 log = logging.getLogger(__name__)
 
 
-def engine_factory(settings: Settings):
-    """model name -> LLMEngine on this process's GPU (fp8 for the NL->SQL model when configured)."""
+def engine_factory(settings: Settings, tp_factory=None):
+    """model name -> LLMEngine on this process's GPU (fp8 for the NL->SQL model when configured).
+    ``tp_factory()`` -> this rank's TPGroup for the model being built (TP replicas, parallel/router.py)."""
 
     def build(model: str):
         from ..engine import build_engine
 
         dtype = settings.dtype if model == settings.nl2sql_model else settings.explain_dtype
-        log.info("building engine %s (%s, max_batch=%d)", model, dtype, settings.max_batch)
+        tp = tp_factory() if tp_factory is not None else None
+        log.info("building engine %s (%s, max_batch=%d, tp=%d)", model, dtype, settings.max_batch,
+                 tp.size if tp is not None else 1)
         # two models co-serve one GPU: each engine's KV arena takes a share of the memory free at its build
         return build_engine(model, checkpoint=settings.checkpoint_dir if model == settings.nl2sql_model else None,
                             dtype=dtype, max_slots=settings.max_batch, max_model_len=settings.max_model_len,
-                            kv_memory_fraction=settings.kv_memory_fraction, warm_graphs=True)
+                            kv_memory_fraction=settings.kv_memory_fraction, warm_graphs=True, tp=tp)
 
     return build
 
@@ -36,7 +39,7 @@ def backend_from_settings(settings: Settings) -> Backend:
         return FakeBackend()
     if settings.engine == "remote":
         return RemoteBackend(settings.remote_url, settings.request_timeout_s)
-    if settings.dp > 1:
+    if settings.dp > 1 or settings.tp > 1:  # replica processes (TP groups need one process per GPU)
         from ..parallel.router import ReplicaRouter
 
         return ReplicaRouter.from_settings(settings)

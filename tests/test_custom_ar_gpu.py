@@ -120,3 +120,69 @@ def test_ipc_allreduce_matches_rank_ordered_sum(gpu, world):
         [p.join(timeout=30) for p in ps]
         [p.kill() for p in ps if p.is_alive()]
     assert all(not e for e in got.values()), got
+
+
+def _engine_worker(rank, world, port, q):
+    """TP=2 tiny engine; after one good generate, rank 1 stops participating (alive, idle) and rank 0's
+    next generate must raise (the one-shot all-reduce times out, poisons its output and sets err)."""
+    import datetime
+    import os
+
+    import torch.distributed as dist
+
+    from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build_engine
+    from llm_based_apache_spark_optimization_amd.engine.runner import TPCommError
+    from llm_based_apache_spark_optimization_amd.parallel import TPGroup
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LSA_CUSTOM_AR_TIMEOUT_S="0.3")
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    out = []
+    try:
+        tp = TPGroup(dist.group.WORLD, rank, world, dev)
+        eng = build_engine("tiny-nsql", device=str(dev), max_slots=2, max_model_len=256, tp=tp)
+        assert tp.car is not None
+        sp = SamplingParams(max_tokens=4, ignore_eos=True)
+        good = eng.generate([[1, 5, 6, 7, 8]], sp)[0].token_ids
+        out.append(("good", good))
+        dist.barrier()
+        if rank == 0:
+            try:
+                eng.generate([[1, 5, 6, 7, 8]], sp)
+                out.append(("no-error", None))
+            except TPCommError as e:
+                out.append(("raised", str(e)[:60]))
+        else:
+            time.sleep(8)  # alive but silent: rank 0's all-reduces find no peer
+        torch.cuda.synchronize(dev)
+    except Exception as e:  # noqa: BLE001
+        out.append(("exc", repr(e)))
+    q.put((rank, out))
+
+
+def test_engine_ar_timeout_raises(gpu):
+    import torch.multiprocessing as tmp
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_engine_worker, args=(r, 2, port, q)) for r in range(2)]
+    [p.start() for p in ps]
+    got, t0 = {}, time.time()
+    try:
+        while len(got) < 2:
+            assert time.time() - t0 < 110, "engine workers timed out"
+            assert not any(p.exitcode not in (None, 0) for p in ps), [p.exitcode for p in ps]
+            try:
+                r, out = q.get(timeout=2)
+                got[r] = out
+            except queue.Empty:
+                pass
+    finally:
+        [p.join(timeout=30) for p in ps]
+        [p.kill() for p in ps if p.is_alive()]
+    assert got[0][0][0] == "good" and got[1][0][0] == "good" and got[0][0][1] == got[1][0][1], got
+    assert got[0][1][0] == "raised", got
