@@ -2,8 +2,11 @@
 
     python scripts/pmc_bw.py <rocprofv3 output dir> [COUNTER [BYTES_PER_UNIT]] > profiles/pmc_bw_<tag>.txt
 
-COUNTER defaults to FETCH_SIZE (KiB per dispatch, BYTES_PER_UNIT 1024); TCC_EA0_RDREQ_sum (L2 -> memory
-read requests) with BYTES_PER_UNIT 64 is the raw-counter fallback.
+COUNTER defaults to FETCH_SIZE with BYTES_PER_UNIT 2048: the counter is KiB per dispatch, and on gfx950 it
+reports exactly half the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md § HBM: 128-B requests
+tallied at 64 B), so it is doubled.  Checked on this code base: the 7B gate_up weight stream (180.4 MB) reads
+as 93.2 MiB-units -> 186 MB.  TCC_EA0_RDREQ_sum (L2 -> memory read requests) with BYTES_PER_UNIT 128 is the
+raw-counter fallback.
 
 Joins counter_collection.csv (FETCH_SIZE per dispatch, KiB) with kernel_trace.csv (start/end ns) on the
 dispatch id and prints, per kernel name: calls, mean duration, mean bytes fetched from HBM/MALL and the
@@ -30,7 +33,7 @@ def _col(row: dict, *names: str) -> str:
     raise KeyError(f"none of {names} in {sorted(row)}")
 
 
-def main(root: str, counter: str = "FETCH_SIZE", unit: float = 1024.0) -> None:
+def main(root: str, counter: str = "FETCH_SIZE", unit: float = 2048.0) -> None:
     kt = _one(os.path.join(root, "**", "*kernel_trace.csv"))
     cc = _one(os.path.join(root, "**", "*counter_collection.csv"))
     dur = {}
