@@ -5,12 +5,18 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include "kernels/lsa_epi.h"
+
 extern "C" {
 int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
              hipStream_t stream);
 int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
                     const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
-                    int xf_mt, hipStream_t s);
+                    int xf_mt, float* ss_out, int ss_ld, int ss_nzero, hipStream_t s);
+int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
+                int waves, int div, int xlds, const LsaEpi* ep, hipStream_t stream);
+int lsa_fp8_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
+                    int epi, int nb, int splitk, int xfrag, const LsaEpi* ep, hipStream_t stream);
 int lsa_rope_append(const void* qkv, const float* qkv_parts, int nparts, long part_stride, const int* pos, const int* tok_seq, const int* block_tables, int max_blocks,
                     const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int T, int H, int Hkv,
                     hipStream_t s);
@@ -69,14 +75,78 @@ T* ptr(const c10::optional<at::Tensor>& t) {
   return t.has_value() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
 }
 
+// Decode epilogue extensions (kernels/lsa_epi.h): rowss = per-row sum of squares of the un-normalised
+// input rows (RMS row scale with eps, 1/K); epi 3 (residual) adds into h [M, N] f32, writes bf16(h) to
+// xout (fragment-major with xmt row tiles, or row-major when xmt == 0) and accumulates sum h^2 into ss_out.
+struct EpiOpts {
+  LsaEpi e{};
+  bool on = false;
+};
+
+EpiOpts epi_opts(int64_t epi, int64_t M, int64_t N, int64_t K, const c10::optional<at::Tensor>& rowss, double eps,
+                 const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& xout, int64_t xmt,
+                 const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets, int64_t ncols) {
+  EpiOpts o;
+  if (rowss.has_value()) {
+    need(*rowss, at::kFloat, "rowss");
+    TORCH_CHECK(rowss->numel() >= M, "rowss too small");
+    o.e.rowss = rowss->data_ptr<float>();
+    o.e.inv_k = 1.0f / (float)K;
+    o.e.eps = (float)eps;
+    o.on = true;
+  }
+  if (epi == 3) {
+    TORCH_CHECK(h.has_value() && xout.has_value() && ss_out.has_value(), "residual epilogue needs h, xout, ss_out");
+    need(*h, at::kFloat, "h");
+    need(*xout, at::kBFloat16, "xout");
+    need(*ss_out, at::kFloat, "ss_out");
+    TORCH_CHECK(h->is_contiguous() && h->numel() >= M * N, "h must be a contiguous [M, N] f32 tensor");
+    TORCH_CHECK(ss_out->numel() >= M, "ss_out too small");
+    TORCH_CHECK(xout->numel() >= (xmt ? xmt * 16 * N : M * N), "xout too small");
+    o.e.h = h->data_ptr<float>();
+    o.e.ldh = (int)N;
+    o.e.xout = reinterpret_cast<uint16_t*>(xout->data_ptr());
+    o.e.xmt = (int)xmt;
+    o.e.ss_out = ss_out->data_ptr<float>();
+    if (tickets.has_value()) {
+      need(*tickets, at::kInt, "tickets");
+      TORCH_CHECK(tickets->numel() >= ncols, "tickets: one counter per 16-column block needed");
+      o.e.tickets = tickets->data_ptr<int>();
+    }
+    o.on = true;
+  }
+  return o;
+}
+
+void check_out(int64_t epi, const at::Tensor& out, int64_t splitk, int64_t M, int64_t N, int64_t mt_silu) {
+  if (epi == 3 && splitk <= 1) return;  // the residual epilogue writes through h / xout
+  if (epi == 1 || epi == 3) {  // f32 slabs (split-K residual: the partials of the splits)
+    need(out, at::kFloat, "out");
+    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small");
+  } else {
+    need(out, at::kBFloat16, "out");
+    TORCH_CHECK(out.numel() >= (epi == 2 ? (mt_silu ? mt_silu * 16 : M) * (N / 2) : M * N), "bf16 out too small");
+  }
+}
+
 // out = x @ W^T with W in fragment-major layout (see kernels/gemm.hip)
 void gemm(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, int64_t nb,
-          int64_t splitk, int64_t waves, int64_t div, int64_t xlds) {
+          int64_t splitk, int64_t waves, int64_t div, int64_t xlds, const c10::optional<at::Tensor>& rowss,
+          double eps, const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& xout, int64_t xmt,
+          const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets) {
   need(x, at::kBFloat16, "x");
   need(wf, at::kBFloat16, "wf");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
   const int M = x.size(0), K = x.size(1);
   TORCH_CHECK(wf.numel() == N * K, "weight numel mismatch: ", wf.numel(), " vs ", N, "x", K);
+  const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, h, xout, xmt, ss_out, tickets, N / 16);
+  if (eo.on) {
+    check_out(epi, out, splitk, M, N, 0);
+    check(lsa_gemm_ex(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, nb, splitk, waves, div,
+                      xlds, &eo.e, cur_stream()),
+          "gemm");
+    return;
+  }
   if (epi == 1) {
     need(out, at::kFloat, "out");
     TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small");
@@ -91,44 +161,38 @@ void gemm(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out,
 
 // same, with X in the fragment-major activation layout (ops.to_xfrag): xf holds ceil(M/16) row tiles
 void gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wf, int64_t N, at::Tensor& out,
-             int64_t epi, int64_t nb, int64_t splitk, int64_t waves, int64_t div) {
+             int64_t epi, int64_t nb, int64_t splitk, int64_t waves, int64_t div,
+             const c10::optional<at::Tensor>& rowss, double eps, const c10::optional<at::Tensor>& h,
+             const c10::optional<at::Tensor>& xout, int64_t xmt, const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets) {
   need(xf, at::kBFloat16, "xf");
   need(wf, at::kBFloat16, "wf");
   TORCH_CHECK(M >= 1 && M <= 64 && K % 32 == 0, "gemm_xf: M in 1..64, K % 32 == 0");
   const int64_t mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   TORCH_CHECK(xf.is_contiguous() && xf.numel() >= mt * 16 * K, "xf too small for M=", M, " K=", K);
   TORCH_CHECK(wf.numel() == N * K, "weight numel mismatch");
-  if (epi == 1) {
-    need(out, at::kFloat, "out");
-    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small");
-  } else {
-    need(out, at::kBFloat16, "out");
-    TORCH_CHECK(out.numel() >= (epi == 2 ? mt * 16 * (N / 2) : M * N), "bf16 out too small");
-  }
-  check(lsa_gemm_cfg(xf.data_ptr(), K, M, K, wf.data_ptr(), N, out.data_ptr(), epi, nb, splitk, waves, div, 2,
-                     cur_stream()),
+  check_out(epi, out, splitk, M, N, mt);
+  const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, h, xout, xmt, ss_out, tickets, N / 16);
+  check(lsa_gemm_ex(xf.data_ptr(), K, M, K, wf.data_ptr(), N, out.data_ptr(), epi, nb, splitk, waves, div, 2,
+                    eo.on ? &eo.e : nullptr, cur_stream()),
         "gemm_xf");
 }
 
 
 // fp8 weights, activations in the fragment-major decode layout (ops.to_xfrag), M <= 64
 void fp8_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wq, const at::Tensor& wscale, int64_t N,
-                 at::Tensor& out, int64_t epi, int64_t nb, int64_t splitk) {
+                 at::Tensor& out, int64_t epi, int64_t nb, int64_t splitk, const c10::optional<at::Tensor>& rowss,
+                 double eps, const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& xout, int64_t xmt,
+                 const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets) {
   need(xf, at::kBFloat16, "xf");
   need(wscale, at::kFloat, "wscale");
   TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
   TORCH_CHECK(M >= 1 && M <= 64 && K % 64 == 0, "fp8_gemm_xf: M in 1..64, K % 64 == 0");
   const int64_t mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   TORCH_CHECK(xf.is_contiguous() && xf.numel() >= mt * 16 * K, "xf too small");
-  if (epi == 1) {
-    need(out, at::kFloat, "out");
-    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small");
-  } else {
-    need(out, at::kBFloat16, "out");
-    TORCH_CHECK(out.numel() >= (epi == 2 ? mt * 16 * (N / 2) : M * N), "bf16 out too small");
-  }
-  check(lsa_fp8_gemm_cfg(xf.data_ptr(), K, M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(), epi, nb,
-                         splitk, 1, cur_stream()),
+  check_out(epi, out, splitk, M, N, mt);
+  const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, h, xout, xmt, ss_out, tickets, N / 16);
+  check(lsa_fp8_gemm_ex(xf.data_ptr(), K, M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(), epi, nb,
+                        splitk, 1, eo.on ? &eo.e : nullptr, cur_stream()),
         "fp8_gemm_xf");
 }
 
@@ -151,29 +215,38 @@ void gemm_t256(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor&
 }
 
 void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscale, int64_t N, at::Tensor& out,
-              int64_t epi, int64_t nb, int64_t splitk) {
+              int64_t epi, int64_t nb, int64_t splitk, const c10::optional<at::Tensor>& rowss, double eps,
+              const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& xout, int64_t xmt,
+              const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets) {
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1, "wq must be a 1-byte GPU tensor");
   need(wscale, at::kFloat, "wscale");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
   const int M = x.size(0), K = x.size(1);
   TORCH_CHECK(wq.numel() == N * K, "fp8 weight numel mismatch");
-  check(lsa_fp8_gemm(x.data_ptr(), x.stride(0), M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(), epi,
-                     nb, splitk, cur_stream()),
+  const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, h, xout, xmt, ss_out, tickets, N / 16);
+  check(lsa_fp8_gemm_ex(x.data_ptr(), x.stride(0), M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(),
+                        epi, nb, splitk, 0, eo.on ? &eo.e : nullptr, cur_stream()),
         "fp8_gemm");
 }
 
 void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t nparts, int64_t part_stride,
                  const c10::optional<at::Tensor>& ids, const c10::optional<at::Tensor>& emb,
                  const c10::optional<at::Tensor>& row_idx, bool write_h, const at::Tensor& w, double eps,
-                 at::Tensor& xn, int64_t rows, int64_t xf_mt) {
+                 at::Tensor& xn, int64_t rows, int64_t xf_mt, const c10::optional<at::Tensor>& ss_out, int64_t ss_ld,
+                 int64_t ss_nzero) {
   need(h, at::kFloat, "h");
   need(w, at::kBFloat16, "w");
   need(xn, at::kBFloat16, "xn");
   const int D = w.numel();
+  if (ss_out.has_value()) {
+    need(*ss_out, at::kFloat, "ss_out");
+    TORCH_CHECK(ss_out->numel() >= (ss_nzero + 1) * ss_ld && ss_ld >= rows, "ss_out too small");
+  }
   check(lsa_add_rmsnorm(h.data_ptr<float>(), ptr<const float>(parts), parts.has_value() ? nparts : 0, part_stride,
                         ptr<const int>(ids), ptr<const void>(emb), ptr<const int>(row_idx), write_h ? 1 : 0,
-                        w.data_ptr(), (float)eps, xn.data_ptr(), rows, D, xf_mt, cur_stream()),
+                        w.data_ptr(), (float)eps, xn.data_ptr(), rows, D, xf_mt, ptr<float>(ss_out), (int)ss_ld,
+                        (int)ss_nzero, cur_stream()),
         "add_rmsnorm");
 }
 
@@ -331,15 +404,22 @@ void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Te
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the MI355X NL->SQL / Spark-error inference engine";
   m.def("gemm", &gemm, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"),
-        py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4, py::arg("xlds") = 0);
+        py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4, py::arg("xlds") = 0,
+        py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_xf", &gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wf"), py::arg("N"), py::arg("out"),
-        py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4);
+        py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4,
+        py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_t256", &gemm_t256);
-  m.def("fp8_gemm", &fp8_gemm);
-  m.def("fp8_gemm_xf", &fp8_gemm_xf);
+  m.def("fp8_gemm", &fp8_gemm, py::arg("x"), py::arg("wq"), py::arg("wscale"), py::arg("N"), py::arg("out"),
+        py::arg("epi"), py::arg("nb"), py::arg("splitk"),
+        py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
+  m.def("fp8_gemm_xf", &fp8_gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wq"), py::arg("wscale"),
+        py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"),
+        py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
         py::arg("ids"), py::arg("emb"), py::arg("row_idx"), py::arg("write_h"), py::arg("w"), py::arg("eps"),
-        py::arg("xn"), py::arg("rows"), py::arg("xf_mt") = 0);
+        py::arg("xn"), py::arg("rows"), py::arg("xf_mt") = 0, py::arg("ss_out") = py::none(), py::arg("ss_ld") = 0,
+        py::arg("ss_nzero") = 0);
   m.def("rope_append", &rope_append);
   m.def("silu_mul", &silu_mul);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),

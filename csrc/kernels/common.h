@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lsa_epi.h"
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -95,6 +97,71 @@ __device__ __forceinline__ size_t xf_off(int m, int k, int mt) {
 }
 
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+// Decode-GEMM epilogue extensions (RMSNorm folded into the GEMMs, no norm launches):
+//  * rowss != null: X rows are the UN-normalised residual stream (the norm's gamma is folded into W at
+//    load time), so every output row m is scaled by rsqrt(rowss[m] * inv_k + eps) -- rowss[m] = sum_k x^2
+//    accumulated by the producing kernel.
+//  * EPI_RES (splitk 1): h[m][n] += y (f32 residual, row stride ldh); xout = bf16(h) (fragment-major
+//    with xmt row tiles when xmt > 0, else row-major [M][ldh]) for the next GEMM; ss_out[m] += sum over
+//    this workgroup's columns of h^2 (one device-scope float atomic per row and workgroup).
+#define EPI_RES 3
+
+__device__ __forceinline__ float epi_row_scale(const LsaEpi& ep, int m) {
+  return ep.rowss ? rsqrtf(ep.rowss[m] * ep.inv_k + ep.eps) : 1.0f;
+}
+
+//    With split-K (grid.y > 1) every split publishes its f32 partial write-through (sc1) into the
+//    [splitk][M][N] slab buffer, takes a ticket, and the last arriver of the column sums the slabs with
+//    sc1 loads and runs the epilogue (guide §6 G16 / MI355X_MICROARCH "Valid forms" table, row 1).
+#define LSA_SC1_AUX 16  // buffer cache-policy aux bit: sc1 (write-through store / L1-bypassing load)
+
+// EPI_RES for 4 consecutive columns n..n+3 of row m; returns sum of the new h^2 over them
+__device__ __forceinline__ float epi_residual4(const LsaEpi& ep, int m, int n, f32x4_t v) {
+  float* hp = ep.h + (size_t)m * ep.ldh + n;
+  float4 hv = *reinterpret_cast<const float4*>(hp);
+  hv.x += v[0]; hv.y += v[1]; hv.z += v[2]; hv.w += v[3];
+  *reinterpret_cast<float4*>(hp) = hv;
+  uint2 pk;
+  pk.x = pack2bf(hv.x, hv.y);
+  pk.y = pack2bf(hv.z, hv.w);
+  *reinterpret_cast<uint2*>(ep.xout + (ep.xmt ? xf_off(m, n, ep.xmt) : (size_t)m * ep.ldh + n)) = pk;
+  return hv.x * hv.x + hv.y * hv.y + hv.z * hv.z + hv.w * hv.w;
+}
+
+typedef __attribute__((address_space(1))) int lsa_g_i32;
+
+// Split-K residual epilogue, called by every workgroup of a column with its reduced tile available
+// through tile(m_index) -> (m, n, f32x4 partial) enumerations.  Returns true in the one workgroup that
+// must finish the column (the last to arrive); the partials are then read back by res_slab_sum.
+template <int NT>
+__device__ __forceinline__ bool res_publish_and_ticket(const LsaEpi& ep, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 partial stores
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *s_flag = __hip_atomic_fetch_add((lsa_g_i32*)(ep.tickets) + blockIdx.x, 1, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.y - 1;
+  __syncthreads();
+  if (!*s_flag) return false;
+  if (threadIdx.x == 0)
+    __hip_atomic_store((lsa_g_i32*)(ep.tickets) + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+__device__ __forceinline__ void res_store_partial(__amdgpu_buffer_rsrc_t rs, size_t elem, f32x4_t v) {
+  const u32x4_t u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(u, rs, (int)(elem * 4), 0, LSA_SC1_AUX);
+}
+
+__device__ __forceinline__ f32x4_t res_slab_sum(__amdgpu_buffer_rsrc_t rs, size_t elem, size_t slab_elems, int nsplit) {
+  f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < nsplit; ++sp) {
+    const u32x4_t u = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((elem + sp * slab_elems) * 4), 0, LSA_SC1_AUX);
+    s[0] += __uint_as_float(u[0]); s[1] += __uint_as_float(u[1]);
+    s[2] += __uint_as_float(u[2]); s[3] += __uint_as_float(u[3]);
+  }
+  return s;
+}
 
 // Orderable 32-bit key of a float (larger float -> larger unsigned key).
 __device__ __forceinline__ uint32_t float_key(float f) {

@@ -68,7 +68,7 @@ template <int MT, int NB, int EPI, int WAVES, int DIV = 1, bool XF = false>
 __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
                                                                  int KB, const uint4* __restrict__ Wf,
                                                                  void* __restrict__ out, int ldo,
-                                                                 int kb_per_split) {
+                                                                 int kb_per_split, LsaEpi ep) {
   constexpr int U = SkinnyCfg<MT, NB, DIV>::U;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -159,10 +159,14 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 
   // cross-wave reduction: red[w][tile][lane]
   __shared__ __attribute__((aligned(16))) f32x4_t red[WAVES][NB * MT][64];
+  __shared__ float ssw[16 * MT];  // EPI_RES: per-row sum of h^2 over this workgroup's columns
 #pragma unroll
   for (int i = 0; i < NB; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) red[w][i * MT + j][lane] = acc[i][j];
+  if constexpr (EPI == EPI_RES) {
+    if (threadIdx.x < 16 * MT) ssw[threadIdx.x] = 0.f;
+  }
   __syncthreads();
 
   if constexpr (EPI == EPI_SILU) {
@@ -179,9 +183,10 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       const int m = j * 16 + (l & 15);
       if (m < M) {
         const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
+        const float sc = epi_row_scale(ep, m);
         f32x4_t v;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = silu(gs[q]) * us[q];
+        for (int q = 0; q < 4; ++q) v[q] = silu(gs[q] * sc) * (us[q] * sc);
         if constexpr (XF) {  // fragment-major in -> fragment-major out (the down projection's input)
           uint2 pk;
           pk.x = pack2bf(v[0], v[1]);
@@ -194,6 +199,34 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
     }
   } else {
     const size_t slab = (size_t)blockIdx.y * M * ldo;
+    if constexpr (EPI == EPI_RES) {
+      if (gridDim.y > 1) {  // split-K: publish, ticket, the last split finishes the column
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+        for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
+          const int l = idx & 63, t = idx >> 6;
+          const int j = t % MT, i = t / MT;
+          f32x4_t s = red[0][t][l];
+#pragma unroll
+          for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
+          const int m = j * 16 + (l & 15);
+          if (m < M) res_store_partial(rs, slab + (size_t)m * ldo + (nb0 + i) * 16 + 4 * (l >> 4), s);
+        }
+        __shared__ int s_last;
+        if (!res_publish_and_ticket<64 * WAVES>(ep, &s_last)) return;
+        for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
+          const int l = idx & 63, t = idx >> 6;
+          const int j = t % MT, i = t / MT;
+          const int m = j * 16 + (l & 15);
+          if (m < M) {
+            const int n = (nb0 + i) * 16 + 4 * (l >> 4);
+            atomicAdd(&ssw[m], epi_residual4(ep, m, n, res_slab_sum(rs, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y)));
+          }
+        }
+        __syncthreads();
+        if (threadIdx.x < M) atomicAdd(ep.ss_out + threadIdx.x, ssw[threadIdx.x]);
+        return;
+      }
+    }
     for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
       const int l = idx & 63;
       const int t = idx >> 6;
@@ -202,7 +235,16 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 #pragma unroll
       for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
       const int m = j * 16 + (l & 15);
-      if (m < M) store4<EPI>(out, ldo, slab, m, (nb0 + i) * 16 + 4 * (l >> 4), s);
+      if (m < M) {
+        s *= epi_row_scale(ep, m);
+        const int n = (nb0 + i) * 16 + 4 * (l >> 4);
+        if constexpr (EPI == EPI_RES) atomicAdd(&ssw[m], epi_residual4(ep, m, n, s));
+        else store4<EPI>(out, ldo, slab, m, n, s);
+      }
+    }
+    if constexpr (EPI == EPI_RES) {
+      __syncthreads();
+      if (threadIdx.x < M) atomicAdd(ep.ss_out + threadIdx.x, ssw[threadIdx.x]);
     }
   }
 }
@@ -441,6 +483,8 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restri
 static thread_local int g_skinny_waves = 4;
 static thread_local int g_skinny_div = 4;
 
+static thread_local LsaEpi g_epi = {};
+
 template <int MT, int NB, int EPI, bool XF>
 static void launch_skinny_x(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
                             int ldo, int splitk, hipStream_t s) {
@@ -448,7 +492,7 @@ static void launch_skinny_x(const uint16_t* X, int ldx, int M, int KB, const uin
   dim3 grid(NBtot / NB, splitk);
 #define LSA_SKL(WV, DV) \
   hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF>), grid, dim3(64 * WV), 0, s, X, \
-                     ldx, M, KB, Wf, out, ldo, kbps)
+                     ldx, M, KB, Wf, out, ldo, kbps, g_epi)
   if (g_skinny_div == 2) {
     if (g_skinny_waves == 8) LSA_SKL(8, 2);
     else LSA_SKL(4, 2);
@@ -503,8 +547,22 @@ extern "C" int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, in
   return lsa_gemm_cfg(X, ldx, M, K, Wf, N, out, epi, nb, splitk, 4, 4, 0, stream);
 }
 
+extern "C" int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
+                           int splitk, int waves, int div, int xlds, const LsaEpi* ep, hipStream_t stream);
+
 extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
                             int splitk, int waves, int div, int xlds, hipStream_t stream) {
+  return lsa_gemm_ex(X, ldx, M, K, Wf, N, out, epi, nb, splitk, waves, div, xlds, nullptr, stream);
+}
+
+// ep (nullable): decode epilogue extensions (common.h LsaEpi): row scale and/or epi == EPI_RES; M <= 64 only
+extern "C" int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
+                           int splitk, int waves, int div, int xlds, const LsaEpi* ep, hipStream_t stream) {
+  g_epi = ep ? *ep : LsaEpi{};
+  if ((ep || epi == EPI_RES) && (M > 64 || (splitk > 1 && epi != EPI_F32 && epi != EPI_RES))) return -7;
+  if (epi == EPI_RES && (!ep || !ep->h || !ep->xout || !ep->ss_out || ep->ldh != N || (splitk > 1 && !ep->tickets)))
+    return -8;
+  if (ep && xlds == 1) xlds = 0;  // the LDS-staged variant has no epilogue extensions
   g_skinny_waves = (waves == 8) ? 8 : 4;
   g_skinny_div = (div == 1 || div == 2) ? div : 4;
   // xlds: 0 = row-major X, 1 = row-major X staged through LDS, 2 = fragment-major X (ops.to_xfrag)
@@ -545,12 +603,13 @@ extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf
     if (epi == EPI_SILU && nb < 2) nb = 2;
     if (NBtot % nb != 0) return -2;
     if (splitk < 1) splitk = 1;
-    if (epi != EPI_F32 && splitk != 1) return -3;
+    if (epi != EPI_F32 && epi != EPI_RES && splitk != 1) return -3;
     if (M > 32 && nb > 2) nb = 2;
     switch (epi) {
       case EPI_BF16: launch_skinny_e<EPI_BF16>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
       case EPI_F32: launch_skinny_e<EPI_F32>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
       case EPI_SILU: launch_skinny_e<EPI_SILU>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
+      case EPI_RES: launch_skinny_e<EPI_RES>(x, ldx, M, KB, w, NBtot, out, ldo, nb, splitk, stream); break;
       default: return -4;
     }
   } else {

@@ -33,7 +33,8 @@ template <int MT, int NB, int EPI, int WAVES, int U, bool XF = false>
 __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
                                                                      int KB64, const uint4* __restrict__ Wq,
                                                                      const float* __restrict__ wscale,
-                                                                     void* __restrict__ out, int ldo, int kb_per_split) {
+                                                                     void* __restrict__ out, int ldo, int kb_per_split,
+                                                                     LsaEpi ep) {
   // same work split as gemm_skinny_kernel: chunks of U k64-steps round-robin over the waves, two-deep
   // register pipeline pinned with sched_barrier(0)
   const int lane = threadIdx.x & 63;
@@ -134,10 +135,14 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
   }
 
   __shared__ __attribute__((aligned(16))) f32x4_t red[WAVES][NB * MT][64];
+  __shared__ float ssw[16 * MT];  // EPI_RES: per-row sum of h^2 over this workgroup's columns
 #pragma unroll
   for (int i = 0; i < NB; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) red[w][i * MT + j][lane] = acc[i][j];
+  if constexpr (EPI == EPI_RES) {
+    if (threadIdx.x < 16 * MT) ssw[threadIdx.x] = 0.f;
+  }
   __syncthreads();
 
   if constexpr (EPI == EPI_SILU) {
@@ -157,8 +162,9 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
         const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
         uint2 pk;
         float v[4];
+        const float sc = epi_row_scale(ep, m);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = silu(gs[q] * wscale[nrow_g + q]) * (us[q] * wscale[nrow_u + q]);
+        for (int q = 0; q < 4; ++q) v[q] = silu(gs[q] * (sc * wscale[nrow_g + q])) * (us[q] * (sc * wscale[nrow_u + q]));
         pk.x = pack2bf(v[0], v[1]);
         pk.y = pack2bf(v[2], v[3]);
         // fragment-major in -> fragment-major out (the down projection's input)
@@ -167,6 +173,38 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
     }
   } else {
     const size_t slab = (size_t)blockIdx.y * M * ldo;
+    if constexpr (EPI == EPI_RES) {
+      if (gridDim.y > 1) {  // split-K: publish (channel-scaled), ticket, the last split finishes the column
+        const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+        for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
+          const int l = idx & 63, t = idx >> 6;
+          const int j = t % MT, i = t / MT;
+          f32x4_t s = red[0][t][l];
+#pragma unroll
+          for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
+          const int m = j * 16 + (l & 15);
+          if (m >= M) continue;
+          const int n = (nb0 + i) * 16 + 4 * (l >> 4);
+          const float4 sc = *reinterpret_cast<const float4*>(wscale + n);
+          s[0] *= sc.x; s[1] *= sc.y; s[2] *= sc.z; s[3] *= sc.w;
+          res_store_partial(rsc, slab + (size_t)m * ldo + n, s);
+        }
+        __shared__ int s_last;
+        if (!res_publish_and_ticket<64 * WAVES>(ep, &s_last)) return;
+        for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
+          const int l = idx & 63, t = idx >> 6;
+          const int j = t % MT, i = t / MT;
+          const int m = j * 16 + (l & 15);
+          if (m < M) {
+            const int n = (nb0 + i) * 16 + 4 * (l >> 4);
+            atomicAdd(&ssw[m], epi_residual4(ep, m, n, res_slab_sum(rsc, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y)));
+          }
+        }
+        __syncthreads();
+        if (threadIdx.x < M) atomicAdd(ep.ss_out + threadIdx.x, ssw[threadIdx.x]);
+        return;
+      }
+    }
     for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
       const int l = idx & 63, t = idx >> 6;
       const int j = t % MT, i = t / MT;
@@ -177,8 +215,11 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
       if (m >= M) continue;
       const int n = (nb0 + i) * 16 + 4 * (l >> 4);
       const float4 sc = *reinterpret_cast<const float4*>(wscale + n);
-      s[0] *= sc.x; s[1] *= sc.y; s[2] *= sc.z; s[3] *= sc.w;
-      if constexpr (EPI == EPI_F32) {
+      const float rs = epi_row_scale(ep, m);
+      s[0] *= sc.x * rs; s[1] *= sc.y * rs; s[2] *= sc.z * rs; s[3] *= sc.w * rs;
+      if constexpr (EPI == EPI_RES) {
+        atomicAdd(&ssw[m], epi_residual4(ep, m, n, s));
+      } else if constexpr (EPI == EPI_F32) {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + slab + (size_t)m * ldo + n) =
             make_float4(s[0], s[1], s[2], s[3]);
       } else {
@@ -187,6 +228,10 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
         pk.y = pack2bf(s[2], s[3]);
         *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + (size_t)m * ldo + n) = pk;
       }
+    }
+    if constexpr (EPI == EPI_RES) {
+      __syncthreads();
+      if (threadIdx.x < M) atomicAdd(ep.ss_out + threadIdx.x, ssw[threadIdx.x]);
     }
   }
 }
@@ -220,6 +265,7 @@ __global__ __launch_bounds__(256) void fp8_dequant_kernel(const uint4* __restric
 }
 
 static thread_local int g_fp8_xfrag = 0;
+static thread_local LsaEpi g_fp8_epi = {};
 
 template <int MT, int NB, int EPI>
 static void launch_t(const uint16_t* X, int ldx, int M, int KB64, const uint4* Wq, const float* sc, int NBtot, void* out,
@@ -230,10 +276,10 @@ static void launch_t(const uint16_t* X, int ldx, int M, int KB64, const uint4* W
   const int kbps = (KB64 + splitk - 1) / splitk;
   if (g_fp8_xfrag)
     hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, 4, U, true>), dim3(NBtot / NB, splitk), dim3(256), 0, s, X,
-                       ldx, M, KB64, Wq, sc, out, ldo, kbps);
+                       ldx, M, KB64, Wq, sc, out, ldo, kbps, g_fp8_epi);
   else
     hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, 4, U, false>), dim3(NBtot / NB, splitk), dim3(256), 0, s,
-                       X, ldx, M, KB64, Wq, sc, out, ldo, kbps);
+                       X, ldx, M, KB64, Wq, sc, out, ldo, kbps, g_fp8_epi);
 }
 
 template <int EPI>
@@ -274,8 +320,21 @@ extern "C" int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq
 }
 
 // xfrag = 1: X in the fragment-major decode layout (M <= 64); a SiLU output is written in it too
+extern "C" int lsa_fp8_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N,
+                               void* out, int epi, int nb, int splitk, int xfrag, const LsaEpi* ep, hipStream_t stream);
+
 extern "C" int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N,
                                 void* out, int epi, int nb, int splitk, int xfrag, hipStream_t stream) {
+  return lsa_fp8_gemm_ex(X, ldx, M, K, Wq, wscale, N, out, epi, nb, splitk, xfrag, nullptr, stream);
+}
+
+// ep (nullable): decode epilogue extensions (common.h LsaEpi), M <= 64
+extern "C" int lsa_fp8_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N,
+                               void* out, int epi, int nb, int splitk, int xfrag, const LsaEpi* ep, hipStream_t stream) {
+  g_fp8_epi = ep ? *ep : LsaEpi{};
+  if ((ep || epi == EPI_RES) && (M > 64 || (splitk > 1 && epi != EPI_F32 && epi != EPI_RES))) return -7;
+  if (epi == EPI_RES && (!ep || !ep->h || !ep->xout || !ep->ss_out || ep->ldh != N || (splitk > 1 && !ep->tickets)))
+    return -8;
   if (K % 64 != 0 || N % 16 != 0 || M <= 0) return -1;
   if (xfrag && M > 64) return -5;
   g_fp8_xfrag = xfrag ? 1 : 0;
@@ -286,7 +345,7 @@ extern "C" int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void
     if (epi == EPI_SILU && nb < 2) nb = 2;
     if (NBtot % nb != 0) return -2;
     if (splitk < 1) splitk = 1;
-    if (epi != EPI_F32 && splitk != 1) return -3;
+    if (epi != EPI_F32 && epi != EPI_RES && splitk != 1) return -3;
     if (M > 32 && nb > 2) nb = 2;
     const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
     const uint4* w = reinterpret_cast<const uint4*>(Wq);
@@ -294,6 +353,7 @@ extern "C" int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void
       case EPI_BF16: launch_e<EPI_BF16>(x, ldx, M, KB64, w, wscale, NBtot, out, ldo, nb, splitk, stream); break;
       case EPI_F32: launch_e<EPI_F32>(x, ldx, M, KB64, w, wscale, NBtot, out, ldo, nb, splitk, stream); break;
       case EPI_SILU: launch_e<EPI_SILU>(x, ldx, M, KB64, w, wscale, NBtot, out, ldo, nb, splitk, stream); break;
+      case EPI_RES: launch_e<EPI_RES>(x, ldx, M, KB64, w, wscale, NBtot, out, ldo, nb, splitk, stream); break;
       default: return -4;
     }
     return (int)hipGetLastError();

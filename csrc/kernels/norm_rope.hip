@@ -18,7 +18,8 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
                                                            const uint16_t* __restrict__ emb,
                                                            const int* __restrict__ row_idx, int write_h,
                                                            const uint16_t* __restrict__ w, float eps,
-                                                           uint16_t* __restrict__ xn, int D, int xf_mt) {
+                                                           uint16_t* __restrict__ xn, int D, int xf_mt,
+                                                           float* __restrict__ ss_out, int ss_ld, int ss_nzero) {
   __shared__ float red[16];
   const int m = blockIdx.x;
   const int r = row_idx ? row_idx[m] : m;
@@ -74,7 +75,13 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
     }
   }
   const float tot = block_sum(ss, red);
-  const float inv = rsqrtf(tot / (float)D + eps);
+  if (ss_out) {
+    // raw mode (norm folded into the next GEMMs): xn = bf16(h) un-normalised, ss_out[m] = sum h^2, and
+    // the following ss_nzero accumulators of this row (rows ss_ld apart) are zeroed for their producers
+    if (threadIdx.x == 0) ss_out[m] = tot;
+    for (int k = threadIdx.x; k < ss_nzero; k += nt) ss_out[(size_t)(k + 1) * ss_ld + m] = 0.f;
+  }
+  const float inv = ss_out ? 1.0f : rsqrtf(tot / (float)D + eps);
 #pragma unroll
   for (int q = 0; q < VPT; ++q) {
     const int c = (threadIdx.x + q * nt) * 8;
@@ -82,7 +89,7 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
       float wf[8], o[8];
       unpack8(wq[q], wf);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = v[q][j] * inv * wf[j];
+      for (int j = 0; j < 8; ++j) o[j] = ss_out ? v[q][j] : v[q][j] * inv * wf[j];
       *reinterpret_cast<uint4*>(xn + (xf_mt ? xf_off(m, c, xf_mt) : (size_t)m * D + c)) = pack8(o);
     }
   }
@@ -91,10 +98,10 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
 template <int VPT>
 static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, const float* parts, size_t ps,
                            const int* ids, const uint16_t* e, const int* row_idx, int write_h, const uint16_t* w,
-                           float eps, uint16_t* o, int D, int xf_mt) {
+                           float eps, uint16_t* o, int D, int xf_mt, float* ss_out, int ss_ld, int ss_nzero) {
 #define LSA_RN(NP)                                                                                         \
   hipLaunchKernelGGL((add_rmsnorm_kernel<NP, VPT>), dim3(rows), dim3(nt), 0, s, h, parts, np, ps, ids, e, \
-                     row_idx, write_h, w, eps, o, D, xf_mt)
+                     row_idx, write_h, w, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero)
   switch (parts ? np : 0) {
     case 0: LSA_RN(0); break;
     case 1: LSA_RN(1); break;
@@ -110,18 +117,20 @@ static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, co
 
 extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids,
                                const void* emb, const int* row_idx, int write_h, const void* w, float eps, void* xn,
-                               int rows, int D, int xf_mt, hipStream_t s) {
+                               int rows, int D, int xf_mt, float* ss_out, int ss_ld, int ss_nzero, hipStream_t s) {
   if (D % 8 != 0 || rows <= 0) return -1;
   if (xf_mt && (D % 32 != 0 || rows > 16 * xf_mt)) return -3;
+  if (ss_out && (row_idx || ss_ld < rows || ss_nzero < 0)) return -4;
   const int vec = D / 8;
   const uint16_t* e = reinterpret_cast<const uint16_t*>(emb);
   const uint16_t* ww = reinterpret_cast<const uint16_t*>(w);
   uint16_t* o = reinterpret_cast<uint16_t*>(xn);
   if (vec <= 1024) {
     launch_rmsnorm<1>(nparts, rows, (vec + 63) / 64 * 64, s, h, parts, (size_t)part_stride, ids, e, row_idx, write_h,
-                      ww, eps, o, D, xf_mt);
+                      ww, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero);
   } else if (vec <= 4096) {
-    launch_rmsnorm<4>(nparts, rows, 1024, s, h, parts, (size_t)part_stride, ids, e, row_idx, write_h, ww, eps, o, D, xf_mt);
+    launch_rmsnorm<4>(nparts, rows, 1024, s, h, parts, (size_t)part_stride, ids, e, row_idx, write_h, ww, eps, o, D, xf_mt,
+                      ss_out, ss_ld, ss_nzero);
   } else {
     return -2;
   }

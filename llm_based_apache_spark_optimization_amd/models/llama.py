@@ -24,6 +24,13 @@ from .. import ops
 from .spec import ModelSpec, spec_from_hf_config
 
 
+# RMSNorm gammas folded into the following projections at load time (LSA_FOLD_NORMS=0 keeps them apart):
+# rmsnorm(x) * g @ W^T == rmsnorm(x) @ (W * g)^T, so wqkv / w_gate_up carry the attention / MLP norm
+# weights and the stored norm vectors are ones.  The decode path then needs no norm launch at all: the
+# GEMMs read the raw residual stream and scale their output rows by its RMS (engine/runner.py fused path).
+FOLD_NORMS = os.environ.get("LSA_FOLD_NORMS", "1") != "0"
+
+
 @dataclasses.dataclass
 class LayerWeights:
     wqkv: ops.PackedWeight
@@ -32,6 +39,7 @@ class LayerWeights:
     w_down: ops.PackedWeight
     attn_norm: torch.Tensor
     mlp_norm: torch.Tensor
+    norms_folded: bool = False
 
 
 @dataclasses.dataclass
@@ -83,10 +91,14 @@ def pack_layer(spec: ModelSpec, wq, wk, wv, wo, wg, wu, wd, an, mn, rank=0, tp=1
     wo_s = _shard_cols(wo, rank, tp)
     gu = ops.interleave_gate_up(_shard_rows(wg, rank, tp), _shard_rows(wu, rank, tp))
     wd_s = _shard_cols(wd, rank, tp)
+    an, mn = an.to(torch.bfloat16), mn.to(torch.bfloat16)
+    if FOLD_NORMS:
+        wqkv = (wqkv.float() * an.float()[None, :]).to(torch.bfloat16)
+        gu = (gu.float() * mn.float()[None, :]).to(torch.bfloat16)
+        an, mn = torch.ones_like(an), torch.ones_like(mn)
     P = ops.PackedWeight.from_dense
     return LayerWeights(P(wqkv.contiguous(), kind), P(wo_s.contiguous(), kind), P(gu.contiguous(), kind),
-                        P(wd_s.contiguous(), kind), an.to(torch.bfloat16).contiguous(),
-                        mn.to(torch.bfloat16).contiguous())
+                        P(wd_s.contiguous(), kind), an.contiguous(), mn.contiguous(), norms_folded=FOLD_NORMS)
 
 
 def init_random(spec: ModelSpec, device="cpu", seed: int = 0, kind: str = "bf16", std: float = 0.02,

@@ -25,7 +25,7 @@ from . import reference as ref
 _ext = None
 _ext_err: Optional[BaseException] = None
 
-EPI = {"bf16": 0, "f32": 1, "silu": 2}
+EPI = {"bf16": 0, "f32": 1, "silu": 2, "res": 3}
 
 
 def ext():
@@ -175,6 +175,8 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
     """(nb, splitk, waves, div) for a decode GEMM: the tuning table when it has the shape (entries
     measured with fragment-major activations carry a ':xf' suffix, fp8-weight entries ':fp8'), else
     the heuristic below (div 4, 4-wave workgroups won most measured shapes)."""
+    if epi == "res":  # the residual epilogue runs the f32-slab main loop (split-K with a last-arriver finish)
+        epi = "f32"
     if M <= 64:
         key = f"{N}x{K}:{epi}:{'s' if M <= 16 else 'm'}"
         tab = _tuning_table()
@@ -201,13 +203,64 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
 _dq_scratch: dict = {}
 
 
+def _epi_kw(rownorm, res, xmt: int) -> dict:
+    """Keyword arguments of the kernels' decode epilogue extensions (csrc/kernels/lsa_epi.h).
+
+    rownorm = (ss, eps): the input rows are the UN-normalised residual stream (RMSNorm gamma folded into
+    the weight): output row m is scaled by rsqrt(ss[m] / K + eps).
+    res = (h, xout, ss_out[, tickets]) with epi='res': h += y (f32 [M, N]); xout = bf16(h) (fragment-major
+    when the call is linear_xf, else row-major [M, N]); ss_out[m] += sum_n h[m, n]^2 (the next GEMM's
+    rownorm).  With ``tickets`` (int32, >= N/16 zeroed counters) the GEMM may split K: the splits publish
+    f32 partials into ``out`` ([splitk, M, N]) and the last to arrive finishes each column."""
+    kw = {}
+    if rownorm is not None:
+        kw["rowss"], kw["eps"] = rownorm[0], float(rownorm[1])
+    if res is not None:
+        kw["h"], kw["xout"], kw["ss_out"] = res[:3]
+        kw["xmt"] = xmt
+        if len(res) > 3 and res[3] is not None:
+            kw["tickets"] = res[3]
+    return kw
+
+
+def _res_split(res, splitk: int, out, M: int, N: int, device):
+    """(splitk, out) of a residual-epilogue call: split-K needs the ticket counters and a slab buffer."""
+    if len(res) < 4 or res[3] is None or splitk <= 1:
+        return 1, res[0]
+    if out is None:
+        out = torch.empty(splitk, M, N, device=device, dtype=torch.float32)
+    return splitk, out
+
+
+def _epi_ref(y: torch.Tensor, M: int, K: int, epi: str, rownorm, res, xf: bool):
+    """CPU semantics of the epilogue extensions on a reference result y (f32 [M, N] or bf16 silu output
+    computed from row-scaled inputs)."""
+    h, xout, ss_out = res[:3]
+    hn = h[:M].float() + y.float()
+    h[:M].copy_(hn)
+    x16 = hn.to(torch.bfloat16)
+    if xf:
+        f = to_xfrag(x16)
+        xout.view(-1)[: f.numel()].copy_(f)
+    else:
+        xout.view(-1)[: x16.numel()].copy_(x16.reshape(-1))
+    ss_out[:M] += hn.pow(2).sum(1)
+
+
 def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
            splitk: Optional[int] = None, nb: Optional[int] = None, waves: Optional[int] = None,
-           div: Optional[int] = None) -> torch.Tensor:
-    """y = x @ W^T with a fused epilogue.  epi='f32' returns [splitk, M, N] partial slabs."""
+           div: Optional[int] = None, rownorm=None, res=None, _xf: bool = False) -> torch.Tensor:
+    """y = x @ W^T with a fused epilogue.  epi='f32' returns [splitk, M, N] partial slabs.
+    rownorm / res (epi='res'): the decode epilogue extensions, see ``_epi_kw``."""
     M, K = x.shape
     assert K == w.K, (K, w.K)
+    assert (epi == "res") == (res is not None), "epi='res' needs res=(h, xout, ss_out)"
     if not _gpu(x):
+        if rownorm is not None:  # scale the rows before the product (the kernels scale the output rows)
+            x = (x.float() * torch.rsqrt(rownorm[0][:M].float() / K + rownorm[1])[:, None]).to(x.dtype)
+        if epi == "res":
+            _epi_ref(ref.linear(x, w.dense(), "f32"), M, K, epi, rownorm, res, _xf)
+            return res[0]
         y = ref.linear(x, w.dense(), epi)
         if epi == "f32":
             y = y.unsqueeze(0)
@@ -218,21 +271,25 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
     nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi, kind=w.kind)
     nb = nb0 if nb is None else nb
     if M > 64:  # prefill tile kernels: split-K (f32 slabs) only where the tile grid is small
+        assert rownorm is None and res is None, "epilogue extensions are decode-only (M <= 64)"
         splitk = (tile_splitk(M, w.N, K) if splitk is None else splitk) if epi == "f32" else 1
     splitk = sk0 if splitk is None else splitk
     waves = wv0 if waves is None else waves
     div = dv0 if div is None else div
+    if epi == "res":
+        splitk, out = _res_split(res, splitk, out, M, w.N, x.device)
     if out is None:
         if epi == "f32":
             out = torch.empty(splitk, M, w.N, device=x.device, dtype=torch.float32)
         else:
             out = torch.empty(M, w.N // 2 if epi == "silu" else w.N, device=x.device, dtype=torch.bfloat16)
     e = ext()
+    kw = _epi_kw(rownorm, res, 0)
     if w.kind == "bf16":
-        e.gemm(x, w.data, w.N, out, EPI[epi], nb, splitk, waves, div)
+        e.gemm(x, w.data, w.N, out, EPI[epi], nb, splitk, waves, div, **kw)
     elif w.kind == "fp8":
         if M <= 64:
-            e.fp8_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk)
+            e.fp8_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, **kw)
         else:
             key = (x.device, w.N * w.K)
             buf = _dq_scratch.get(x.device)
@@ -286,14 +343,15 @@ def from_xfrag(xf: torch.Tensor, M: int, K: int) -> torch.Tensor:
 
 def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
               splitk: Optional[int] = None, nb: Optional[int] = None, waves: Optional[int] = None,
-              div: Optional[int] = None) -> torch.Tensor:
+              div: Optional[int] = None, rownorm=None, res=None) -> torch.Tensor:
     """``linear`` with the activations in the fragment-major layout (``to_xfrag``), M <= 64, bf16 or fp8 weights.
     epi='silu' writes its [M, N/2] output in the fragment-major layout too (the next GEMM's input);
-    for that epilogue ``out`` is a flat buffer of at least xfrag_tiles(M) * 16 * N/2 elements."""
+    for that epilogue ``out`` is a flat buffer of at least xfrag_tiles(M) * 16 * N/2 elements.
+    epi='res' writes its bf16 copy of the residual in the fragment-major layout."""
     if not _gpu(xf) or w.kind not in ("bf16", "fp8"):
         if epi != "silu":
-            return linear(from_xfrag(xf, M, w.K), w, epi, out, splitk, nb, waves, div)
-        y = to_xfrag(linear(from_xfrag(xf, M, w.K), w, epi, None, splitk, nb, waves, div))
+            return linear(from_xfrag(xf, M, w.K), w, epi, out, splitk, nb, waves, div, rownorm, res, _xf=True)
+        y = to_xfrag(linear(from_xfrag(xf, M, w.K), w, epi, None, splitk, nb, waves, div, rownorm))
         if out is None:
             return y
         out.view(-1)[: y.numel()].copy_(y)
@@ -303,6 +361,8 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
     splitk = sk0 if splitk is None else splitk
     waves = wv0 if waves is None else waves
     div = dv0 if div is None else div
+    if epi == "res":
+        splitk, out = _res_split(res, splitk, out, M, w.N, xf.device)
     if out is None:
         if epi == "f32":
             out = torch.empty(splitk, M, w.N, device=xf.device, dtype=torch.float32)
@@ -310,10 +370,11 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
             out = torch.zeros(xfrag_tiles(M) * 16 * (w.N // 2), device=xf.device, dtype=torch.bfloat16)
         else:
             out = torch.empty(M, w.N, device=xf.device, dtype=torch.bfloat16)
+    kw = _epi_kw(rownorm, res, xfrag_tiles(M))
     if w.kind == "fp8":
-        ext().fp8_gemm_xf(xf, M, w.K, w.data, w.scale, w.N, out, EPI[epi], nb, splitk)
+        ext().fp8_gemm_xf(xf, M, w.K, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, **kw)
     else:
-        ext().gemm_xf(xf, M, w.K, w.data, w.N, out, EPI[epi], nb, splitk, waves, div)
+        ext().gemm_xf(xf, M, w.K, w.data, w.N, out, EPI[epi], nb, splitk, waves, div, **kw)
     return out
 
 
@@ -321,12 +382,29 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
 def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
                 parts: Optional[torch.Tensor] = None, ids: Optional[torch.Tensor] = None,
                 emb: Optional[torch.Tensor] = None, row_idx: Optional[torch.Tensor] = None,
-                write_h: bool = True, rows: Optional[int] = None, xf: bool = False) -> torch.Tensor:
+                write_h: bool = True, rows: Optional[int] = None, xf: bool = False,
+                ss_out: Optional[torch.Tensor] = None, ss_ld: int = 0, ss_nzero: int = 0) -> torch.Tensor:
     """h[r] (= emb[ids[r]]) (+= sum parts[:, r]); xn[m] = rmsnorm(h[row_idx[m]]) * w.
-    xf=True: xn is a flat buffer receiving the fragment-major layout (``to_xfrag``) of ``rows`` rows."""
+    xf=True: xn is a flat buffer receiving the fragment-major layout (``to_xfrag``) of ``rows`` rows.
+    ss_out (raw mode, the norm folded into the next GEMMs): xn = bf16(h) un-normalised, ss_out[m] = sum h^2,
+    and ss_out[k * ss_ld + m] = 0 for k = 1..ss_nzero (the accumulators of the later residual epilogues)."""
     if rows is None:
         assert not xf, "xf output needs rows"
         rows = xn.shape[0]
+    if ss_out is not None and not _gpu(h):
+        tmp = torch.empty(rows, w.numel(), dtype=torch.bfloat16, device=h.device)
+        ref.add_rmsnorm(h, torch.ones_like(w), eps, tmp, parts, ids, emb, row_idx, write_h)
+        hv = h[:rows].float()
+        raw = hv.to(torch.bfloat16)
+        if xf:
+            f = to_xfrag(raw)
+            xn.view(-1)[: f.numel()].copy_(f)
+        else:
+            xn[:rows].copy_(raw)
+        ss_out[:rows] = hv.pow(2).sum(1)
+        for k in range(1, ss_nzero + 1):
+            ss_out[k * ss_ld: k * ss_ld + rows] = 0
+        return xn
     if not _gpu(h):
         if not xf:
             return ref.add_rmsnorm(h, w, eps, xn, parts, ids, emb, row_idx, write_h)
@@ -338,7 +416,7 @@ def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
     nparts = parts.shape[0] if parts is not None else 0
     stride = parts.stride(0) if parts is not None else 0
     ext().add_rmsnorm(h, parts, nparts, stride, ids, emb, row_idx, write_h, w, eps, xn, rows,
-                      xfrag_tiles(rows) if xf else 0)
+                      xfrag_tiles(rows) if xf else 0, ss_out, ss_ld, ss_nzero)
     return xn
 
 

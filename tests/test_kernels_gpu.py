@@ -516,3 +516,77 @@ def test_rope_table_bound_checked_on_host(gpu):
     with pytest.raises(RuntimeError, match="rope tables"):
         ops.rope_append(parts, pos, None, bt, cos, sin, q, kc, vc, H, Hkv)
     torch.cuda.synchronize()
+
+
+# ------------------------------------------------------------------ norm-folded decode epilogues
+@pytest.mark.parametrize("kind", ["bf16", "fp8"])
+@pytest.mark.parametrize("xf", [False, True])
+@pytest.mark.parametrize("M", [1, 7, 20, 32, 64])
+def test_gemm_rownorm_and_residual_epilogues(gpu, kind, xf, M):
+    """rownorm (rows scaled by rsqrt(ss/K + eps)) on the f32-slab and SiLU epilogues, and the residual
+    epilogue (h += y, xout = bf16(h), ss_out += sum h^2) vs the fp32 PyTorch definition."""
+    if xf and M <= 16:
+        pytest.skip("fragment-major activations are the 16 < M <= 64 decode layout")
+    torch.manual_seed(M + 3 * xf)
+    d, F = 1024, 512
+    eps = 1e-5
+    h0 = torch.randn(M, d, device=gpu) * 3
+    x = h0.to(torch.bfloat16)
+    ss = h0.pow(2).sum(1)
+    wq = (torch.randn(768, d, device=gpu) / math.sqrt(d)).to(torch.bfloat16)
+    wg = (torch.randn(F, d, device=gpu) / math.sqrt(d)).to(torch.bfloat16)
+    wu = (torch.randn(F, d, device=gpu) / math.sqrt(d)).to(torch.bfloat16)
+    wo = (torch.randn(d, F, device=gpu) / math.sqrt(F)).to(torch.bfloat16)
+    pq, pgu, po = (ops.PackedWeight.from_dense(t, kind) for t in (wq, ops.interleave_gate_up(wg, wu), wo))
+    xin = ops.to_xfrag(x) if xf else x
+
+    def lin(a, w, epi, **kw):
+        return ops.linear_xf(a, M, w, epi, **kw) if xf else ops.linear(a, w, epi, **kw)
+
+    inv = torch.rsqrt(ss / d + eps)[:, None]
+    xs = x.float() * inv  # what the un-folded path feeds the GEMM (before its bf16 rounding)
+    y = lin(xin, pq, "f32", splitk=2, rownorm=(ss, eps))
+    assert _rel(y.sum(0), xs @ pq.dense().float().t()) < 2e-2
+    act = lin(xin, pgu, "silu", rownorm=(ss, eps))
+    act = ops.from_xfrag(act, M, F) if xf else act
+    gd, ud = pgu.dense().float().view(F // 16, 2, 16, d)[:, 0].reshape(F, d), pgu.dense().float().view(F // 16, 2, 16, d)[:, 1].reshape(F, d)
+    want_act = torch.nn.functional.silu(xs @ gd.t()) * (xs @ ud.t())
+    assert _rel(act, want_act) < 2e-2
+    # residual epilogue from the bf16 activations
+    a16 = want_act.to(torch.bfloat16)
+    h = torch.randn(M, d, device=gpu)
+    h_ref = h + a16.float() @ po.dense().float().t()
+    tickets = torch.zeros(d // 16, device=gpu, dtype=torch.int32)
+    for splitk in (1, 4):  # one workgroup per column, and split-K finished by the last-arriving split
+        hh = h.clone()
+        xout = torch.zeros(ops.xfrag_tiles(M) * 16 * d if xf else M * d, device=gpu, dtype=torch.bfloat16)
+        ss_out = torch.full((M,), 0.5, device=gpu)
+        lin(ops.to_xfrag(a16) if xf else a16, po, "res", splitk=splitk,
+            res=(hh, xout if xf else xout.view(M, d), ss_out, tickets))
+        torch.cuda.synchronize()
+        assert _rel(hh, h_ref) < 1e-2, splitk
+        got_x = ops.from_xfrag(xout, M, d) if xf else xout.view(M, d)
+        assert torch.equal(got_x, hh.to(torch.bfloat16)), splitk
+        assert torch.allclose(ss_out, 0.5 + hh.pow(2).sum(1), rtol=1e-4), splitk
+        assert torch.all(tickets == 0), "the last arriver must reset its column counter"
+
+
+@pytest.mark.parametrize("xf", [False, True])
+def test_add_rmsnorm_raw_mode(gpu, xf):
+    """raw mode: h = emb[ids]; x = bf16(h); ss_out[m] = sum h^2; the next nzero accumulators zeroed."""
+    B, d, V, S = 20, 512, 1000, 32
+    torch.manual_seed(5)
+    emb = torch.randn(V, d, device=gpu).to(torch.bfloat16)
+    ids = torch.randint(0, V, (B,), device=gpu, dtype=torch.int32)
+    h = torch.zeros(S, d, device=gpu)
+    xn = torch.zeros(ops.xfrag_tiles(B) * 16 * d if xf else B * d, device=gpu, dtype=torch.bfloat16)
+    ss = torch.full((4, S), 7.0, device=gpu)
+    ops.add_rmsnorm(h[:B], torch.ones(d, device=gpu, dtype=torch.bfloat16), 1e-5, xn if xf else xn.view(B, d),
+                    ids=ids, emb=emb, rows=B, xf=xf, ss_out=ss.view(-1), ss_ld=S, ss_nzero=2)
+    torch.cuda.synchronize()
+    hv = emb[ids.long()].float()
+    assert torch.equal(h[:B], hv)
+    got = ops.from_xfrag(xn, B, d) if xf else xn.view(B, d)
+    assert torch.equal(got, hv.to(torch.bfloat16))
+    assert torch.allclose(ss[0, :B], hv.pow(2).sum(1), rtol=1e-5)
+    assert torch.all(ss[1:3, :B] == 0) and torch.all(ss[3] == 7.0) and torch.all(ss[0, B:] == 7.0)
