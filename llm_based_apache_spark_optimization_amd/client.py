@@ -82,16 +82,40 @@ class Backend:
     def models(self) -> list:
         return []
 
-    def health(self) -> dict:
+    def health(self, deep: bool = False) -> dict:
         return {"ok": True}
 
 
 # -------------------------------------------------------------------------------------- engines
-class _EngineLoop:
-    """Drives one LLMEngine from a background thread; callers block on their request's event."""
+class EngineUnavailable(RuntimeError):
+    """The model's engine is down (its loop died and could not be restarted): the serving layer answers
+    503 at once instead of letting requests wait for the timeout."""
 
-    def __init__(self, engine, run_ahead: int = 16):
+
+def _fatal_device_error(e: BaseException) -> bool:
+    """A GPU fault poisons the HIP context: the engine cannot be reset in this process."""
+    from .engine.runner import TPCommError
+
+    if isinstance(e, TPCommError):  # the lockstep TP group is out of sync: never step it again
+        return True
+    msg = str(e)
+    return any(k in msg for k in ("HIP error", "hipError", "CUDA error", "illegal memory access",
+                                  "device-side assert", "Memory access fault"))
+
+
+class _EngineLoop:
+    """Drives one LLMEngine from a background thread; callers block on their request's event.
+
+    Failure handling: when a step raises, every queued / running request is failed at once
+    (``LLMEngine.abort_all``) and the loop keeps serving -- up to ``max_errors`` failures inside
+    ``error_window_s``.  A fatal device error, or too many failures, ends the loop; ``EngineService``
+    then rebuilds the engine or answers ``EngineUnavailable``."""
+
+    def __init__(self, engine, run_ahead: int = 16, max_errors: int = 3, error_window_s: float = 60.0):
         self.engine = engine
+        self.max_errors, self.error_window_s = max_errors, error_window_s
+        self._errors: list = []
+        self.restarts = 0
         engine.run_ahead = run_ahead  # serving: bound each decode run so arrivals are admitted promptly
         # each engine runs on its own HIP stream: co-served models overlap on the GPU, and one engine's
         # host syncs never wait for the other's queued kernels
@@ -107,12 +131,16 @@ class _EngineLoop:
         self._t.start()
 
     def submit(self, ids, params, stream: bool = False):
+        if not self.alive():
+            raise EngineUnavailable(f"engine {self.engine.name} is down: {self._err!r}")
         req = self.engine.add_request(ids, params, stream=stream)
         with self._cv:
             self._cv.notify()
         return req
 
     def _run(self):
+        from .utils.metrics import REGISTRY
+
         while not self._stop:
             with self._cv:
                 while not self._stop and not self.engine.has_work():
@@ -126,13 +154,20 @@ class _EngineLoop:
                 else:
                     self.engine.step()
             except BaseException as e:  # noqa: BLE001 - surface to waiting callers
-                self._err = e
-                for r in list(self.engine._reqs.values()):
-                    r.error = repr(e)
-                    r.done.set()
-                    if r.stream is not None:
-                        r.stream.put(("done", None))
-                return
+                REGISTRY.inc("lsa_engine_errors_total", 1, "engine step failures", model=self.engine.name)
+                now = time.monotonic()
+                self._errors = [t for t in self._errors if now - t < self.error_window_s] + [now]
+                fatal = _fatal_device_error(e) or len(self._errors) > self.max_errors
+                if fatal:
+                    self._err = e  # alive() turns false before any caller is released
+                try:
+                    self.engine.abort_all(repr(e))
+                except BaseException:  # noqa: BLE001
+                    self._err = e
+                    fatal = True
+                if fatal:
+                    return
+                self.restarts += 1  # the engine is empty and consistent again: keep serving
 
     def alive(self) -> bool:
         return self._t.is_alive() and self._err is None
@@ -147,17 +182,40 @@ class EngineService(Backend):
     """Named in-process engines (built lazily through ``factory``) behind the Ollama call shape."""
 
     def __init__(self, factory: Callable[[str], object], defaults: Optional[dict] = None,
-                 timeout_s: float = 300.0):
+                 timeout_s: float = 300.0, max_rebuilds: int = 2):
         self._factory = factory
         self._loops: Dict[str, _EngineLoop] = {}
         self._lock = threading.Lock()
         self.defaults = defaults or {}
         self.timeout_s = timeout_s
+        self.max_rebuilds = max_rebuilds
+        self.rebuilds: Dict[str, int] = {}
+        self._build_err: Dict[str, BaseException] = {}
 
     def loop(self, model: str) -> _EngineLoop:
+        """The model's engine loop, built on first use and rebuilt (at most ``max_rebuilds`` times) after
+        its loop died; a model that cannot be (re)built raises ``EngineUnavailable``."""
         with self._lock:
-            if model not in self._loops:
+            lp = self._loops.get(model)
+            if lp is not None and lp.alive():
+                return lp
+            if lp is not None:  # dead loop: rebuild the engine once the old one is released
+                if self.rebuilds.get(model, 0) >= self.max_rebuilds:
+                    raise EngineUnavailable(f"engine {model} is down after {self.rebuilds[model]} rebuilds: "
+                                            f"{lp._err!r}")
+                self.rebuilds[model] = self.rebuilds.get(model, 0) + 1
+                lp.close()
+                del self._loops[model]
+                lp = None
+                if torch.cuda.is_available():
+                    torch.cuda.empty_cache()
+            try:
                 self._loops[model] = _EngineLoop(self._factory(model))
+            except EngineUnavailable:
+                raise
+            except Exception as e:  # noqa: BLE001
+                self._build_err[model] = e
+                raise EngineUnavailable(f"engine {model} could not be built: {e!r}") from e
             return self._loops[model]
 
     def _submit(self, model, prompt, system, options, raw, stream=False):
@@ -203,10 +261,11 @@ class EngineService(Backend):
     def models(self) -> list:
         return sorted(self._loops)
 
-    def health(self) -> dict:
+    def health(self, deep: bool = False) -> dict:
         return {"ok": all(lp.alive() for lp in self._loops.values()),
                 "engines": {m: {"alive": lp.alive(), "running": lp.engine.sched.num_running,
                                 "waiting": lp.engine.sched.num_waiting, "kv_usage": lp.engine.sched.kv_usage,
+                                "restarts": lp.restarts, "rebuilds": self.rebuilds.get(m, 0),
                                 **lp.engine.stats} for m, lp in self._loops.items()}}
 
 

@@ -51,6 +51,9 @@ class Settings:
     # models: the first gets 45 %, the second 45 % of what is left)
     kv_memory_fraction: float = dataclasses.field(default_factory=lambda: _env("KV_MEMORY_FRACTION", 0.45, float))
     max_new_tokens: int = dataclasses.field(default_factory=lambda: _env("MAX_NEW_TOKENS", 256, int))
+    # chunked-prefill interleave: prompt tokens prefilled per engine iteration (0 = whole prompts); long
+    # /explain_error prompts then stall the running decode batch for one chunk at a time
+    prefill_chunk: int = dataclasses.field(default_factory=lambda: _env("PREFILL_CHUNK", 512, int))
     # sampling defaults: greedy (the reference sampled at Ollama defaults; pass options to match)
     temperature: float = dataclasses.field(default_factory=lambda: _env("TEMPERATURE", 0.0, float))
     top_k: int = dataclasses.field(default_factory=lambda: _env("TOP_K", 40, int))

@@ -25,6 +25,8 @@ import torch
 from ..models.templates import STOP_STRINGS, apply_stops, render
 from ..models.tokenizer import tokenizer_for
 from ..runtime import native
+from ..utils import tracing
+from ..utils.metrics import REGISTRY, TOKEN_BUCKETS
 from .runner import BLOCK, ModelRunner
 
 
@@ -81,6 +83,7 @@ class Request:
     done: threading.Event = dataclasses.field(default_factory=threading.Event)
     slot: int = -1
     gen_host: int = 0  # generated-token count as of the last device sync
+    prefilled: int = 0  # prompt tokens already in the KV cache (chunked prefill in progress when < len)
     error: Optional[str] = None
     # streaming: ("tokens", ids-so-far) after every host sync that saw new tokens, then ("done", None)
     stream: Optional[queue.Queue] = None
@@ -102,7 +105,7 @@ class GenerationResult:
 
 class LLMEngine:
     def __init__(self, runner: ModelRunner, tokenizer=None, max_prefill_tokens: int = 16384, sync_every: int = 8,
-                 name: Optional[str] = None):
+                 name: Optional[str] = None, prefill_chunk: Optional[int] = None):
         self.runner = runner
         self.spec = runner.spec
         self.name = name or self.spec.name
@@ -117,13 +120,22 @@ class LLMEngine:
         # length limit (offline batches); a server sets a bound so new arrivals are admitted promptly
         self.run_ahead: Optional[int] = None
         self.max_prefill_tokens = max_prefill_tokens
+        # chunked-prefill interleave (serving): at most this many prompt tokens are prefilled per engine
+        # iteration, so a long prompt (a 2k-token Spark error for /explain_error) is spread over several
+        # iterations with decode runs of the already-running requests in between instead of stalling them
+        # for its whole prefill.  None = prefill every admitted prompt at once (offline batches, bench.py).
+        self.prefill_chunk = prefill_chunk
+        self._prefilling: list = []  # admitted requests whose prompt is not fully in the KV cache yet
         self._ids = itertools.count(1)
         self._reqs: dict[int, Request] = {}
         self._lock = threading.RLock()
         self._slot_owner: dict[int, int] = {}
         self.load_time_s = 0.0
         self.stats = {"requests": 0, "prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0,
-                      "prefill_s": 0.0, "decode_s": 0.0}
+                      "prefill_s": 0.0, "decode_s": 0.0, "decode_device_s": 0.0, "aborted": 0}
+        # per-decode-run device timing (hipEvents around the graph replays, read after the host sync the
+        # run ends with anyway): lsa_decode_step_device_seconds{model} = GPU time per token step
+        self.device_timing = runner.on_gpu
 
     # -------------------------------------------------------------------------------- prompts
     def render(self, prompt: str, system: str = "", raw: bool = False) -> str:
@@ -163,41 +175,39 @@ class LLMEngine:
         return req
 
     def has_work(self) -> bool:
-        return self.sched.num_waiting > 0 or self.sched.num_running > 0
+        return self.sched.num_waiting > 0 or self.sched.num_running > 0 or bool(self._prefilling)
 
     def step(self) -> list[Request]:
-        """One engine iteration: admit + prefill new requests, run decode steps, retire finished."""
+        """One engine iteration: admit + prefill new requests (at most ``prefill_chunk`` prompt tokens when
+        set), run decode steps over the requests whose prompt is complete, retire finished ones."""
         r = self.runner
         with self._lock:
             admitted = self.sched.admit()
-            if admitted:
-                t0 = time.perf_counter()
-                seqs = []
-                any_sample = False
-                for rid in admitted:
-                    req = self._reqs[rid]
-                    slot = self.sched.slot(rid)
-                    req.slot, req.admitted = slot, t0
-                    self._slot_owner[slot] = rid
-                    sp = req.params
-                    seed = sp.seed if sp.seed is not None else (rid * 7919 + 17)
-                    r.set_slot(slot, self.sched.block_table(rid), sp.max_tokens, sp.temperature, sp.top_k, sp.top_p,
-                               seed, eos_on=not sp.ignore_eos, repeat_penalty=sp.repeat_penalty,
-                               repeat_last_n=sp.repeat_last_n, prompt_ids=req.prompt_ids)
-                    any_sample |= sp.needs_sampler
-                    seqs.append((slot, req.prompt_ids, 0))
-                self._prefill_packed(seqs, any_sample)
+            t0 = time.perf_counter()
+            for rid in admitted:
+                req = self._reqs[rid]
+                slot = self.sched.slot(rid)
+                req.slot, req.admitted = slot, t0
+                self._slot_owner[slot] = rid
+                sp = req.params
+                seed = sp.seed if sp.seed is not None else (rid * 7919 + 17)
+                r.set_slot(slot, self.sched.block_table(rid), sp.max_tokens, sp.temperature, sp.top_k, sp.top_p,
+                           seed, eos_on=not sp.ignore_eos, repeat_penalty=sp.repeat_penalty,
+                           repeat_last_n=sp.repeat_last_n, prompt_ids=req.prompt_ids,
+                           defer_table=self.prefill_chunk is not None)
+                self._prefilling.append(req)
+            if self._prefilling:
+                done_now = self._prefill_some()
                 t1 = time.perf_counter()
-                for rid in admitted:
-                    q = self._reqs[rid]
+                for q in done_now:
                     q.first_token = t1
                     q.gen_host = 1
                     if q.stream is not None:  # the prefill's token goes out now (one sync, streaming only)
                         q.streamed = 1
                         q.stream.put(("tokens", r.tokens_of(q.slot, 1)))
                 self.stats["prefill_s"] += t1 - t0
-                self.stats["prompt_tokens"] += sum(len(s[1]) for s in seqs)
-            running = self.sched.running()
+            pending = {q.rid for q in self._prefilling}
+            running = [rid for rid in self.sched.running() if rid not in pending]
             if not running:
                 return []
             B = r.bucket(self.sched.highest_slot + 1)
@@ -216,12 +226,23 @@ class LLMEngine:
             max_ctx = max(len(q.prompt_ids) + min(q.gen_host + n_steps, q.params.max_tokens) for q in reqs) + 1
         # the decode run needs no scheduler state: new requests may be added meanwhile
         t0 = time.perf_counter()
+        ev = None
         if n_steps:
+            if self.device_timing:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             r.decode(B, n_steps, sample, max_ctx=max_ctx)
+            if ev is not None:
+                ev[1].record()
         fin, gl, _ = r.read_rows([q.slot for q in reqs])
         with self._lock:
             self.stats["decode_s"] += time.perf_counter() - t0
             self.stats["decode_steps"] += n_steps
+            if ev is not None:
+                dev_s = ev[0].elapsed_time(ev[1]) / 1e3  # both recorded before read_rows' sync
+                self.stats["decode_device_s"] += dev_s
+                REGISTRY.observe("lsa_decode_step_device_seconds", dev_s / n_steps, "GPU time per decode step",
+                                 buckets=TOKEN_BUCKETS, model=self.name, batch=str(B))
             done = []
             now = time.perf_counter()
             for i, rid in enumerate(running):
@@ -242,31 +263,97 @@ class LLMEngine:
                     self.sched.finish(rid)
                     self.stats["generated_tokens"] += n
                     self.stats["requests"] += 1
+                    self._trace_done(req, n)
                     req.done.set()
                     if req.stream is not None:
                         req.stream.put(("done", None))
                     done.append(req)
             return done
 
+    def _trace_done(self, req: Request, n: int) -> None:
+        """Engine spans of a finished request (queue -> prefill -> decode), fed to lsa_stage_seconds and,
+        with LSA_TRACE=1, to the JSONL trace (SURVEY.md §5 tracing)."""
+        rid = f"{self.name}:{req.rid}"
+        tracing.record("engine_queue", req.admitted - req.arrival, rid, model=self.name)
+        tracing.record("engine_prefill", req.first_token - req.admitted, rid, model=self.name,
+                       prompt_tokens=len(req.prompt_ids))
+        tracing.record("engine_decode", req.finished_at - req.first_token, rid, model=self.name, tokens=n)
+
+    def abort_all(self, reason: str) -> list:
+        """Fail every queued and running request (engine recovery after a step raised): their callers are
+        released with ``error`` set, slots and KV blocks are returned, the engine is empty again."""
+        with self._lock:
+            out = []
+            now = time.perf_counter()
+            for rid, req in list(self._reqs.items()):
+                req.error = reason
+                req.finished_at = now
+                if req.slot >= 0:
+                    try:
+                        self.runner.release_slot(req.slot)
+                    except Exception:  # noqa: BLE001 - a faulted device: the engine is rebuilt anyway
+                        pass
+                self.sched.finish(rid)
+                req.done.set()
+                if req.stream is not None:
+                    req.stream.put(("done", None))
+                out.append(req)
+            self._reqs.clear()
+            self._slot_owner.clear()
+            self._prefilling.clear()
+            self.stats["aborted"] += len(out)
+            return out
+
+    def _prefill_some(self) -> list:
+        """Prefill the admitted-but-incomplete prompts FCFS within this iteration's token budget; returns the
+        requests whose prompt completed (their first token is committed)."""
+        budget = self.prefill_chunk if self.prefill_chunk else None
+        final, partial, done = [], [], []
+        any_sample = False
+        for q in list(self._prefilling):
+            rest = len(q.prompt_ids) - q.prefilled
+            take = rest if budget is None else min(rest, budget)
+            if take <= 0:
+                break
+            seg = (q.slot, q.prompt_ids[q.prefilled:q.prefilled + take], q.prefilled)
+            q.prefilled += take
+            if q.prefilled == len(q.prompt_ids):
+                final.append(seg)
+                done.append(q)
+                any_sample |= q.params.needs_sampler
+                self._prefilling.remove(q)
+            else:
+                partial.append(seg)
+            self.stats["prompt_tokens"] += take
+            if budget is not None:
+                budget -= take
+                if budget <= 0:
+                    break
+        if partial:  # KV only (no token commit); chunks of different requests pack into one launch sequence
+            self.runner.prefill_chunk(partial)
+        if final:
+            self._prefill_packed(final, any_sample)
+        return done
+
     def _prefill_packed(self, seqs, any_sample: bool) -> None:
         """Prefill in chunks of at most max_prefill_tokens tokens (long prompts split across calls)."""
         r = self.runner
         batch, tokens = [], 0
-        for slot, ids, _ in seqs:
+        for slot, ids, p0 in seqs:
             if len(ids) > self.max_prefill_tokens:  # chunked prefill of one long prompt
                 if batch:
                     r.prefill(batch, any_sample)
                     batch, tokens = [], 0
                 c = self.max_prefill_tokens
                 for s in range(0, len(ids) - c, c):
-                    r.prefill_chunk([(slot, ids[s:s + c], s)])
+                    r.prefill_chunk([(slot, ids[s:s + c], p0 + s)])
                 s = ((len(ids) - 1) // c) * c
-                r.prefill([(slot, ids[s:], s)], any_sample)
+                r.prefill([(slot, ids[s:], p0 + s)], any_sample)
                 continue
             if tokens + len(ids) > self.max_prefill_tokens and batch:
                 r.prefill(batch, any_sample)
                 batch, tokens = [], 0
-            batch.append((slot, ids, 0))
+            batch.append((slot, ids, p0))
             tokens += len(ids)
         if batch:
             r.prefill(batch, any_sample)
@@ -277,8 +364,10 @@ class LLMEngine:
 
     # -------------------------------------------------------------------------------- one-shot API
     def result(self, req: Request, template: Optional[str] = None) -> GenerationResult:
+        t0 = time.perf_counter()
         text = self.tok.decode(req.output_ids)
         text = apply_stops(text, template or self.spec.template, req.params.stop)
+        tracing.record("engine_detok", time.perf_counter() - t0, f"{self.name}:{req.rid}", model=self.name)
         ns = lambda s: int(max(0.0, s) * 1e9)  # noqa: E731
         ended_eos = bool(req.output_ids) and req.output_ids[-1] in self.runner.eos_list and not req.params.ignore_eos
         return GenerationResult(

@@ -144,10 +144,16 @@ class ModelRunner:
         # and the o / down residual epilogues into ssq[2l], ssq[2l + 1], ssq[2l + 2]
         self.fused_norm = (os.environ.get("LSA_FUSED_NORM", "1") != "0" and tps == 1
                            and all(lw.norms_folded for lw in weights.layers))
+        # ... for decode buckets up to this batch: measured on MI355X (rocprofv3 decode-step spans,
+        # profiles/rocprof_fused_norm_ab.txt) the norm-free step wins at batch 1 (3B 2k explain 1788 -> 1738 us,
+        # 7B 2.77 -> 2.71 ms) but loses at batch 32 for the 3B (2029 -> 2087 us: the residual epilogue's
+        # last-arriver tail costs more than the norm launch it replaces); the norm launches stay above it
+        self.fused_norm_max_batch = int(os.environ.get("LSA_FUSED_NORM_MAX_B", "16"))
         self.ssq = torch.zeros(2 * self.L + 2, S, **f32)
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)
         self.graphs: dict = {}
+        self._pending_bt: dict = {}  # slot -> block-table row of a prompt still being prefilled in chunks
         if self.tp is not None and self.tp.size > 1 and self.on_gpu:
             self.tp.warmup()  # communicators (RCCL + the one-shot IPC all-reduce) before any launch
 
@@ -209,7 +215,7 @@ class ModelRunner:
         return ops.decode_split_plan(B, self.Hkv, min(tier, self.max_model_len))
 
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
-        if self.fused_norm:
+        if self.fused_norm and B <= self.fused_norm_max_batch:
             return self._decode_step_fused(B, sample, plan)
         w, d = self.w, self.d
         ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
@@ -384,10 +390,18 @@ class ModelRunner:
     # ------------------------------------------------------------------------------------ slots
     def set_slot(self, slot: int, blocks: Sequence[int], limit: int, temperature: float = 0.0, top_k: int = 40,
                  top_p: float = 0.9, seed: int = 0, eos_on: bool = True, repeat_penalty: float = 1.0,
-                 repeat_last_n: int = REPEAT_WINDOW, prompt_ids: Sequence[int] = ()) -> None:
+                 repeat_last_n: int = REPEAT_WINDOW, prompt_ids: Sequence[int] = (), defer_table: bool = False) -> None:
+        """``defer_table``: the slot's block table stays out of the decode-visible table until its prompt's
+        final prefill chunk commits (chunked-prefill interleave: decode runs in between must not append
+        the idle row's k/v into the blocks the prompt is being written to)."""
         row = torch.zeros(self.max_blocks, dtype=torch.int32)
         row[: len(blocks)] = torch.tensor(list(blocks), dtype=torch.int32)
-        self.block_tables[slot].copy_(row.to(self.device, non_blocking=True))
+        if defer_table:
+            self._pending_bt[slot] = row.to(self.device, non_blocking=True)
+            self.block_tables[slot].zero_()
+        else:
+            self._pending_bt.pop(slot, None)
+            self.block_tables[slot].copy_(row.to(self.device, non_blocking=True))
         self.limit[slot] = min(int(limit), self.max_new_cap)
         self.temperature[slot] = float(temperature)
         self.top_k[slot] = int(top_k)
@@ -413,6 +427,7 @@ class ModelRunner:
         self.eos_list = ids
 
     def release_slot(self, slot: int) -> None:
+        self._pending_bt.pop(slot, None)
         self.finished[slot] = 1
         self.positions[slot] = 0
         self.gen_len[slot] = 0
@@ -459,6 +474,13 @@ class ModelRunner:
         last = dv[o:o + n]
         slot_t = torch.tensor(slots, dtype=torch.long, device=dev)
         bt = self.block_tables.index_select(0, slot_t)
+        for i, sl in enumerate(slots):  # deferred tables: prefill writes through them; the commit publishes
+            pend = self._pending_bt.get(sl)
+            if pend is not None:
+                bt[i].copy_(pend)
+                if commit:
+                    self.block_tables[sl].copy_(pend)
+                    del self._pending_bt[sl]
         work = None
         if self.on_gpu:
             work = torch.tensor(ops.prefill_work(cu), dtype=torch.int32).to(dev, non_blocking=True)

@@ -175,7 +175,14 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
     """(nb, splitk, waves, div) for a decode GEMM: the tuning table when it has the shape (entries
     measured with fragment-major activations carry a ':xf' suffix, fp8-weight entries ':fp8'), else
     the heuristic below (div 4, 4-wave workgroups won most measured shapes)."""
-    if epi == "res":  # the residual epilogue runs the f32-slab main loop (split-K with a last-arriver finish)
+    if epi == "res":  # the residual epilogue runs the f32-slab main loop (split-K with a last-arriver finish):
+        # its own measured entries (scripts/bench_res_epi.py --tune) first, else the f32 entries
+        b = 1
+        while b < M:
+            b *= 2
+        e = _tuning_table().get(f"{N}x{K}:res:b{b}" + (":fp8" if kind == "fp8" else ""))
+        if e is not None and M <= 64 and not (M > 32 and e["nb"] > 2):
+            return e["nb"], e["splitk"], e["waves"], e["div"]
         epi = "f32"
     if M <= 64:
         key = f"{N}x{K}:{epi}:{'s' if M <= 16 else 'm'}"

@@ -169,6 +169,11 @@ def _worker(conn, replica: int, devices: str, kind: str, settings_kw: dict, hear
             t = threading.Thread(target=serve, args=msg[1:], daemon=True)  # concurrency -> batching
             t.start()
             pool.append(t)
+        elif msg[0] == "health":  # the router's deep health probe: this replica's engine gauges
+            try:
+                send(("health", msg[1], backend.health()))
+            except Exception as e:  # noqa: BLE001
+                send(("health", msg[1], {"ok": False, "error": repr(e)}))
 
 
 class _Replica:
@@ -195,6 +200,7 @@ class ReplicaRouter(Backend):
         self._ids = itertools.count(1)
         self._lock = threading.Lock()
         self._waiters: dict = {}
+        self._probes: dict = {}
         self._closing = False
         ctx = mp.get_context("spawn")
         self.replicas = []
@@ -258,6 +264,13 @@ class ReplicaRouter(Backend):
                 r.ready = True
                 continue
             kind, rid, payload = msg
+            if kind == "health":
+                with self._lock:
+                    w = self._probes.get(rid)
+                if w is not None:
+                    w[1] = payload
+                    w[0].set()
+                continue
             if kind == "piece":
                 with self._lock:
                     w = self._waiters.get(rid) if rid in r.inflight else None  # a stale replica's pieces drop
@@ -383,10 +396,36 @@ class ReplicaRouter(Backend):
             with self._lock:
                 self._waiters.pop(rid, None)
 
-    def health(self) -> dict:
-        return {"ok": any(r.alive for r in self.replicas),
-                "replicas": [{"id": r.idx, "alive": r.alive, "inflight": len(r.inflight), "served": r.served}
-                             for r in self.replicas]}
+    def health(self, deep: bool = False, timeout_s: float = 1.0) -> dict:
+        """Replica liveness and load; ``deep`` also asks every live replica for its engines' health (running /
+        waiting / KV usage / restarts per model), waiting at most ``timeout_s`` in all."""
+        out = {"ok": any(r.alive for r in self.replicas),
+               "replicas": [{"id": r.idx, "alive": r.alive, "ready": r.ready, "inflight": len(r.inflight),
+                             "served": r.served} for r in self.replicas]}
+        if not deep:
+            return out
+        probes = {}
+        for r, rec in zip(self.replicas, out["replicas"]):
+            if not (r.alive and r.ready):
+                continue
+            pid = -next(self._ids)  # negative ids never collide with requests
+            w = [threading.Event(), None]
+            with self._lock:
+                self._probes[pid] = w
+            try:
+                with r.send_lock:
+                    r.conn.send(("health", pid))
+                probes[pid] = (w, rec)
+            except (OSError, EOFError, BrokenPipeError):
+                with self._lock:
+                    self._probes.pop(pid, None)
+        t_end = time.time() + timeout_s
+        for pid, (w, rec) in probes.items():
+            if w[0].wait(max(0.0, t_end - time.time())):
+                rec["health"] = w[1]
+            with self._lock:
+                self._probes.pop(pid, None)
+        return out
 
     def models(self):
         return []

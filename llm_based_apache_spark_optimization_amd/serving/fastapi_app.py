@@ -25,12 +25,13 @@ import os
 import time
 from typing import Optional
 
-from fastapi import FastAPI, HTTPException
-from fastapi.responses import PlainTextResponse, StreamingResponse
+from fastapi import FastAPI, HTTPException, Request
+from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 from pydantic import BaseModel
 
 from .. import prompts
-from ..utils.metrics import REGISTRY
+from ..client import EngineUnavailable
+from ..utils.metrics import REGISTRY, record_generation
 from ..utils.tracing import new_request_id
 from .pipeline import resolve_input
 from .service import AppContext, make_context
@@ -69,6 +70,12 @@ def create_app(ctx: Optional[AppContext] = None) -> FastAPI:
     app = FastAPI(title="MI355X NL->SQL / Spark-error service")
     app.state.ctx = ctx
     s = ctx.settings
+
+    @app.exception_handler(EngineUnavailable)
+    def engine_down(request: Request, exc: EngineUnavailable):
+        # a dead engine answers at once (SURVEY.md §5 failure detection) instead of after the request timeout
+        REGISTRY.inc("lsa_requests_total", 1, "requests", route=request.url.path.strip("/"), outcome="unavailable")
+        return JSONResponse(status_code=503, content={"error": "engine unavailable", "detail": str(exc)})
 
     @app.post("/process-data/")
     def modify_string(data: InputString):
@@ -137,9 +144,16 @@ def create_app(ctx: Optional[AppContext] = None) -> FastAPI:
     def api_generate(req: GenerateRequest):
         if req.stream:  # Ollama's NDJSON framing: response pieces as decoded, then the done chunk
             chunks = ctx.backend.generate_stream(req.model, req.prompt, req.system, req.options, req.raw)
-            return StreamingResponse((json.dumps(c.to_dict()) + "\n" for c in chunks),
-                                     media_type="application/x-ndjson")
-        return ctx.backend.generate(req.model, req.prompt, req.system, req.options, req.raw).to_dict()
+
+            def ndjson():
+                for c in chunks:
+                    if c.done:
+                        record_generation(c, "api_generate")
+                    yield json.dumps(c.to_dict()) + "\n"
+            return StreamingResponse(ndjson(), media_type="application/x-ndjson")
+        r = ctx.backend.generate(req.model, req.prompt, req.system, req.options, req.raw)
+        record_generation(r, "api_generate")
+        return r.to_dict()
 
     @app.get("/api/tags")
     def api_tags():
@@ -167,14 +181,35 @@ def create_app(ctx: Optional[AppContext] = None) -> FastAPI:
 
     @app.get("/metrics", response_class=PlainTextResponse)
     def metrics():
-        h = ctx.backend.health()
-        for m, e in (h.get("engines") or {}).items():
-            REGISTRY.set("lsa_engine_running", e.get("running", 0), "running requests", model=m)
-            REGISTRY.set("lsa_engine_waiting", e.get("waiting", 0), "queued requests", model=m)
-            REGISTRY.set("lsa_engine_kv_usage", e.get("kv_usage", 0.0), "KV cache fraction in use", model=m)
+        export_backend_gauges(ctx.backend)
         return REGISTRY.render()
 
     return app
+
+
+def export_backend_gauges(backend) -> None:
+    """Engine gauges (running / waiting / KV usage / restarts per model) and, under DP, per-replica load
+    (alive, in-flight, served) plus each replica's engine gauges (``ReplicaRouter.health(deep=True)``)."""
+    try:
+        h = backend.health(deep=True)
+    except Exception:  # noqa: BLE001 - metrics must render even when the backend is down
+        h = {}
+
+    def engines(eng: dict, **lbl):
+        for m, e in (eng or {}).items():
+            REGISTRY.set("lsa_engine_running", e.get("running", 0), "running requests", model=m, **lbl)
+            REGISTRY.set("lsa_engine_waiting", e.get("waiting", 0), "queued requests", model=m, **lbl)
+            REGISTRY.set("lsa_engine_kv_usage", e.get("kv_usage", 0.0), "KV cache fraction in use", model=m, **lbl)
+            REGISTRY.set("lsa_engine_alive", 1.0 if e.get("alive", True) else 0.0, "engine loop alive", model=m, **lbl)
+            REGISTRY.set("lsa_engine_restarts", e.get("restarts", 0) + e.get("rebuilds", 0),
+                         "engine recoveries (loop restarts + rebuilds)", model=m, **lbl)
+    engines(h.get("engines"))
+    for r in h.get("replicas") or []:
+        rid = str(r.get("id"))
+        REGISTRY.set("lsa_replica_alive", 1.0 if r.get("alive") else 0.0, "DP replica alive", replica=rid)
+        REGISTRY.set("lsa_replica_inflight", r.get("inflight", 0), "requests in flight on the replica", replica=rid)
+        REGISTRY.set("lsa_replica_served", r.get("served", 0), "requests served by the replica", replica=rid)
+        engines((r.get("health") or {}).get("engines"), replica=rid)
 
 
 def main(argv=None) -> None:  # pragma: no cover - server entry point

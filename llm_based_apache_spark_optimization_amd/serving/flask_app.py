@@ -28,6 +28,7 @@ from flask import Flask, jsonify, render_template, request, session, url_for
 from werkzeug.utils import secure_filename
 
 from .. import prompts
+from ..client import EngineUnavailable
 from ..utils.metrics import REGISTRY
 from ..utils.tracing import new_request_id
 from .pipeline import ST_UPLOAD, unique_path
@@ -42,6 +43,10 @@ def create_app(ctx: Optional[AppContext] = None) -> Flask:
     app = Flask(__name__, template_folder=os.path.join(HERE, "templates"), static_folder=os.path.join(HERE, "static"))
     app.secret_key = s.secret_key
     app.config["LSA_CTX"] = ctx
+
+    @app.errorhandler(EngineUnavailable)
+    def engine_down(exc):  # a dead engine answers at once instead of after the request timeout
+        return jsonify({"error": "engine unavailable", "detail": str(exc)}), 503
 
     @app.after_request
     def cors(resp):  # the reference enabled CORS for every origin (Flask/app.py:13)
@@ -131,6 +136,9 @@ def create_app(ctx: Optional[AppContext] = None) -> Flask:
 
     @app.route("/metrics")
     def metrics():
+        from .fastapi_app import export_backend_gauges
+
+        export_backend_gauges(ctx.backend)
         return REGISTRY.render(), 200, {"Content-Type": "text/plain; version=0.0.4"}
 
     @app.route("/health")

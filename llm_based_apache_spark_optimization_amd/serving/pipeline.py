@@ -19,7 +19,7 @@ from collections import OrderedDict
 from typing import Callable, Optional
 
 from .. import prompts
-from ..utils.metrics import REGISTRY
+from ..utils.metrics import REGISTRY, record_generation
 from ..utils.tracing import new_request_id, span
 from .executor import SQLExecutionError, write_csv
 from .history import HistoryStore
@@ -125,14 +125,14 @@ class Pipeline:
         with span("nl2sql", rid):
             res = self.backend.generate(self.settings.nl2sql_model, question,
                                         system=prompts.nl2sql_system(table_schema), options=options)
-        REGISTRY.inc("lsa_generated_tokens_total", res.eval_count, "tokens generated", model=res.model)
+        record_generation(res, "nl2sql")
         return res
 
     def explain(self, error_message: str, options: Optional[dict] = None, rid: str = ""):
         with span("explain_error", rid):
             res = self.backend.generate(self.settings.explain_model, prompts.explain_prompt(error_message),
                                         system=prompts.EXPLAIN_SYSTEM, options=options)
-        REGISTRY.inc("lsa_generated_tokens_total", res.eval_count, "tokens generated", model=res.model)
+        record_generation(res, "explain_error")
         return res
 
     # ------------------------------------------------------------------------------- full job

@@ -27,7 +27,8 @@ def engine_factory(settings: Settings, tp_factory=None):
         # two models co-serve one GPU: each engine's KV arena takes a share of the memory free at its build
         return build_engine(model, checkpoint=settings.checkpoint_dir if model == settings.nl2sql_model else None,
                             dtype=dtype, max_slots=settings.max_batch, max_model_len=settings.max_model_len,
-                            kv_memory_fraction=settings.kv_memory_fraction, warm_graphs=True, tp=tp)
+                            kv_memory_fraction=settings.kv_memory_fraction, warm_graphs=True, tp=tp,
+                            prefill_chunk=settings.prefill_chunk)
 
     return build
 

@@ -42,3 +42,14 @@ def span(stage: str, request_id: str = "", **attrs):
                 rec["error"] = err
             with _lock, open(_path, "a") as f:
                 f.write(json.dumps(rec) + "\n")
+
+
+def record(stage: str, seconds: float, request_id: str = "", **attrs) -> None:
+    """A span measured elsewhere (e.g. the engine's per-request queue / prefill / decode / detok phases,
+    known only when the request completes): same metric and JSONL record as ``span``."""
+    labels = {k: v for k, v in attrs.items() if k == "model"}
+    REGISTRY.observe("lsa_stage_seconds", max(0.0, seconds), "per-stage latency", stage=stage, **labels)
+    if ENABLED:
+        rec = {"ts": time.time(), "request_id": request_id, "stage": stage, "seconds": seconds, **attrs}
+        with _lock, open(_path, "a") as f:
+            f.write(json.dumps(rec) + "\n")

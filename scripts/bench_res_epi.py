@@ -4,7 +4,10 @@ sums of squares; no norm launch), swept over (nb, waves, div).  Also times the c
 (qkv f32 slabs, gate_up SiLU) with and without the rownorm row scale.  Weights rotate over > 600 MiB so
 they stream from HBM; us per call (median of 3 x 30).  One JSON line per (shape, M, kind).
 
-    python scripts/bench_res_epi.py [Ms] [bf16|fp8]
+    python scripts/bench_res_epi.py [Ms] [bf16|fp8] [--rowp-only]
+
+Each row-parallel line carries a ready "tune" entry (key "NxK:res:b<M>[:fp8]") when the sweep's best beats
+the f32 pick by > 3 %; scripts/merge_tuning.py folds them into ops/gemm_tuning.json.
 """
 import json
 import sys
@@ -18,8 +21,9 @@ dev = torch.device("cuda:0")
 ROWP = {"7b_o": (4096, 4096), "7b_down": (4096, 11008), "3b_o": (3072, 3072), "3b_down": (3072, 8192)}
 COLP = {"7b_qkv": (12288, 4096, "f32"), "7b_gateup": (22016, 4096, "silu"), "3b_qkv": (5120, 3072, "f32"),
         "3b_gateup": (16384, 3072, "silu")}
-Ms = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 8, 32]
-KIND = sys.argv[2] if len(sys.argv) > 2 else "bf16"
+_pos = [a for a in sys.argv[1:] if not a.startswith("--")]
+Ms = [int(a) for a in _pos[0].split(",")] if _pos else [1, 8, 32]
+KIND = _pos[1] if len(_pos) > 1 else "bf16"
 
 
 def timeit(fn, it=30):
@@ -87,11 +91,16 @@ for name, (N, K) in ROWP.items():
                         best = ((nb, sk, waves, dv), us)
         res["res_best"] = list(best[0])
         res["res_best_us"] = round(best[1], 2)
+        if best[1] < 0.97 * res["res_same_cfg_us"] and M in (1, 2, 4, 8, 16, 32, 64):
+            nb, sk, wv, dv = best[0]
+            res["tune"] = {f"{N}x{K}:res:b{M}" + (":fp8" if KIND == "fp8" else ""):
+                           {"nb": nb, "splitk": sk, "waves": wv, "div": dv, "us": round(best[1], 2),
+                            "note": f"scripts/bench_res_epi.py: f32 pick {res['res_same_cfg_us']} us"}}
         print(json.dumps(res), flush=True)
     del ws
     torch.cuda.empty_cache()
 
-for name, (N, K, epi) in COLP.items():
+for name, (N, K, epi) in ({} if "--rowp-only" in sys.argv else COLP).items():
     ws, ncopy = weights(N, K)
     for M in Ms:
         xf = 16 < M <= 64

@@ -187,3 +187,31 @@ def test_engine_service_streams_ollama_chunks():
     assert all(not c.done for c in chunks[:-1])
     assert "".join(c.response for c in chunks) == whole.response
     svc.loop("tiny-nsql").close()
+
+
+def test_chunked_prefill_interleave_matches_whole_prompt():
+    """Serving mode (prefill_chunk): a long prompt is prefilled 40 tokens per iteration while an already
+    running request keeps decoding in between; both produce exactly the tokens of whole-prompt prefill."""
+    from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build_engine
+
+    long_p = [1] + [(7 * i) % 200 + 3 for i in range(150)]
+    short_p = [1, 5, 9, 11]
+    ref = build_engine("tiny-nsql", device="cpu", max_slots=2, max_model_len=512)
+    want = [r.token_ids for r in ref.generate([short_p, long_p], SamplingParams(max_tokens=12, ignore_eos=True))]
+    eng = build_engine("tiny-nsql", device="cpu", max_slots=2, max_model_len=512, prefill_chunk=40)
+    eng.run_ahead = 2  # a server bounds each decode run (client._EngineLoop sets 16)
+    p = SamplingParams(max_tokens=12, ignore_eos=True)
+    a = eng.add_request(short_p, p)
+    eng.step()  # the short prompt completes in the first chunk and starts decoding
+    b = eng.add_request(long_p, p)
+    steps_while_prefilling = 0
+    while not b.done.is_set() or not a.done.is_set():
+        before = eng.stats["decode_steps"]
+        pending = bool(eng._prefilling) or b.prefilled < len(long_p)
+        eng.step()
+        if pending and eng.stats["decode_steps"] > before:
+            steps_while_prefilling += 1
+    assert steps_while_prefilling >= 2, "decode must interleave with the chunked prefill"
+    assert eng.result(a).token_ids == want[0]
+    assert eng.result(b).token_ids == want[1]
+    assert not eng._prefilling and not eng.runner._pending_bt
