@@ -46,6 +46,9 @@ int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
 int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
+int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
+int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
+                      void* out, int epi, int splitk, hipStream_t stream);
 int lsa_ar_alloc(size_t bytes, void** out);
 int lsa_ar_free(void* p);
 int lsa_ar_handle(void* p, char* out64);
@@ -351,6 +354,41 @@ void sample_commit(at::Tensor& logits, at::Tensor& part, at::Tensor& cand, const
         "sample_commit");
 }
 
+// per-token fp8 quantisation of bf16 rows: x8 [M, K] uint8 (e4m3fn bits), sx [M] f32 (amax / 448)
+void quant_rows_fp8(const at::Tensor& x, at::Tensor& x8, at::Tensor& sx) {
+  need(x, at::kBFloat16, "x");
+  need(sx, at::kFloat, "sx");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(x8.is_cuda() && x8.element_size() == 1 && x8.dim() == 2 && x8.size(0) >= M && x8.size(1) >= K &&
+                  x8.stride(1) == 1, "x8 must be a row-major [M, K] 1-byte tensor");
+  TORCH_CHECK(sx.numel() >= M, "sx too small");
+  check(lsa_quant_rows_fp8(x.data_ptr(), x.stride(0), M, K, x8.data_ptr(), x8.stride(0), sx.data_ptr<float>(),
+                           cur_stream()),
+        "quant_rows_fp8");
+}
+
+// W8A8 large-M linear layer on the block-scaled fp8 MFMA (kernels/gemm_fp8_tile.hip)
+void fp8_gemm_t256(const at::Tensor& x8, const at::Tensor& sx, const at::Tensor& wq, const at::Tensor& sw, int64_t N,
+                   at::Tensor& out, int64_t epi, int64_t splitk) {
+  need(sx, at::kFloat, "sx");
+  need(sw, at::kFloat, "sw");
+  TORCH_CHECK(x8.is_cuda() && x8.element_size() == 1 && x8.dim() == 2 && x8.stride(1) == 1, "x8: [M, K] bytes");
+  const int M = x8.size(0), K = x8.size(1);
+  TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
+  TORCH_CHECK(sx.numel() >= M && sw.numel() >= N, "scale sizes");
+  if (epi == 1) {
+    need(out, at::kFloat, "out");
+    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small");
+  } else {
+    need(out, at::kBFloat16, "out");
+    TORCH_CHECK(out.numel() >= M * (epi == 2 ? N / 2 : N), "bf16 out too small");
+  }
+  check(lsa_fp8_gemm_t256(x8.data_ptr(), x8.stride(0), sx.data_ptr<float>(), M, K, wq.data_ptr(), sw.data_ptr<float>(),
+                          N, out.data_ptr(), epi, splitk, cur_stream()),
+        "fp8_gemm_t256");
+}
+
 void fp8_dequant(const at::Tensor& wq, const at::Tensor& wscale, int64_t N, int64_t K, at::Tensor& wf) {
   need(wscale, at::kFloat, "wscale");
   need(wf, at::kBFloat16, "wf");
@@ -431,6 +469,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);
   m.def("fp8_dequant", &fp8_dequant);
+  m.def("quant_rows_fp8", &quant_rows_fp8);
+  m.def("fp8_gemm_t256", &fp8_gemm_t256, py::arg("x8"), py::arg("sx"), py::arg("wq"), py::arg("sw"), py::arg("N"),
+        py::arg("out"), py::arg("epi"), py::arg("splitk") = 1);
   m.def("silu_parts", [](const at::Tensor& parts, at::Tensor& out) {
     // parts: f32 [S, M, 2F] (gate/up interleaved per 16 rows) -> out bf16 [M, F] = silu(gate) * up
     need(parts, at::kFloat, "parts");

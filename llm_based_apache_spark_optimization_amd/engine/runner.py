@@ -168,7 +168,8 @@ class ModelRunner:
         if not self.on_gpu:
             return 1
         if M > 64:  # prefill: split-K on small tile grids; TP prefill reduces single slabs over RCCL
-            return 1 if (self.tp is not None and self.tp.size > 1) else ops.tile_splitk(M, N or self.d, K)
+            return 1 if (self.tp is not None and self.tp.size > 1) else ops.tile_splitk(
+                M, N or self.d, K, self.w.layers[0].wo.kind)
         if tp_reduced and self.tp is not None and self.tp.size > 1 and not self.tp.can_fold_splitk(M * self.d):
             return 1  # RCCL reduces one slab; the one-shot kernel folds split-K slabs into the all-reduce
         return ops.pick_gemm_config(M, N or self.d, K, "f32", xf=xf, kind=self.w.layers[0].wo.kind)[1]

@@ -180,11 +180,15 @@ def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[st
 
 
 @torch.no_grad()
-def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32) -> torch.Tensor:
+def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant_rows: int = 0) -> torch.Tensor:
     """fp32 causal forward of one sequence over the weights exactly as packed (``dense()`` undoes the
     fragment shuffle and the fp8 quantisation, so an fp8 model is compared against its own dequantised
     weights): logits [T, V] f32.  The numerics oracle for the engine at production shapes
-    (tests/test_prod_shapes_gpu.py); plain PyTorch, one layer's dense weights alive at a time."""
+    (tests/test_prod_shapes_gpu.py); plain PyTorch, one layer's dense weights alive at a time.
+
+    ``act_quant_rows``: fp8 models run prefill GEMMs W8A8 (ops.linear, M > 64: per-token e4m3 activations);
+    the first ``act_quant_rows`` rows (the prompt, when its prefill batch had > 64 tokens) get the same
+    per-token activation rounding before the projections, decode rows keep bf16 activations (W8A16)."""
     from ..ops import reference as ref
 
     spec, dev = w.spec, w.device
@@ -205,11 +209,22 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32) -> torch.
     def bf(x):  # the kernels hand activations between ops in bf16
         return x.to(torch.bfloat16).float()
 
+    aq = act_quant_rows if w.layers[0].wqkv.kind == "fp8" else 0
+
+    def q8(x):  # W8A8 prefill rows: per-token e4m3 with amax / 448 scales (ops.quantize_rows_fp8)
+        if aq <= 0:
+            return x
+        head = x[:aq]
+        amax = head.abs().amax(1, keepdim=True)
+        s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+        head = (head / s).to(torch.float8_e4m3fn).float() * s
+        return torch.cat([head, x[aq:]], 0)
+
     h = w.embed[ids].float()
     mask = torch.full((T, T), float("-inf"), device=dev).triu(1)
     for lw in w.layers:
         x = bf(norm(h, lw.attn_norm))
-        qkv = x @ lw.wqkv.dense().float().t()
+        qkv = q8(x) @ lw.wqkv.dense().float().t()
         q = qkv[:, : H * hd].view(T, H, hd)
         k = qkv[:, H * hd:(H + Hkv) * hd].view(T, Hkv, hd)
         v = qkv[:, (H + Hkv) * hd:].view(T, Hkv, hd)
@@ -217,10 +232,10 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32) -> torch.
         k, v = k.repeat_interleave(G, 1), v.repeat_interleave(G, 1)
         s = torch.einsum("qhd,khd->hqk", q, k) / math.sqrt(hd) + mask
         a = bf(torch.einsum("hqk,khd->qhd", s.softmax(-1), v).reshape(T, H * hd))
-        h = h + a @ lw.wo.dense().float().t()
+        h = h + q8(a) @ lw.wo.dense().float().t()
         x = bf(norm(h, lw.mlp_norm))
-        gu = (x @ lw.w_gate_up.dense().float().t()).view(T, -1, 2, 16)
+        gu = (q8(x) @ lw.w_gate_up.dense().float().t()).view(T, -1, 2, 16)
         act = bf(torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(T, -1)
-        h = h + act @ lw.w_down.dense().float().t()
+        h = h + q8(act) @ lw.w_down.dense().float().t()
     x = bf(norm(h, w.final_norm))
     return x @ w.lm_head.dense().float().t()

@@ -80,6 +80,14 @@ def interleave_gate_up(wg: torch.Tensor, wu: torch.Tensor) -> torch.Tensor:
     return torch.stack([wg.view(F // 16, 16, K), wu.view(F // 16, 16, K)], dim=1).reshape(2 * F, K)
 
 
+def pack_fp8(q: torch.Tensor) -> torch.Tensor:
+    """e4m3fn bytes [N, K] -> the fragment layout [N/16, K/64, 64 lanes, 16 B], lane = 16 g + r holding
+    W[16 nb + r][64 kb + 16 g .. + 15]."""
+    N, K = q.shape
+    assert N % 16 == 0 and K % 64 == 0, (N, K)
+    return q.view(torch.uint8).reshape(N // 16, 16, K // 64, 4, 16).permute(0, 2, 3, 1, 4).contiguous()
+
+
 def quantize_fp8(w: torch.Tensor):
     """Per-output-channel e4m3fn quantisation -> (packed uint8 [N/16, K/64, 64, 16], scale f32 [N])."""
     N, K = w.shape
@@ -87,8 +95,7 @@ def quantize_fp8(w: torch.Tensor):
     wf = w.float()
     scale = (wf.abs().amax(dim=1) / 448.0).clamp(min=1e-12)
     q = (wf / scale[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
-    packed = q.view(torch.uint8).reshape(N // 16, 16, K // 64, 4, 16).permute(0, 2, 3, 1, 4).contiguous()
-    return packed, scale
+    return pack_fp8(q), scale
 
 
 def dequantize_fp8(packed: torch.Tensor, scale: torch.Tensor, N: int, K: int) -> torch.Tensor:
@@ -279,7 +286,7 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
     nb = nb0 if nb is None else nb
     if M > 64:  # prefill tile kernels: split-K (f32 slabs) only where the tile grid is small
         assert rownorm is None and res is None, "epilogue extensions are decode-only (M <= 64)"
-        splitk = (tile_splitk(M, w.N, K) if splitk is None else splitk) if epi == "f32" else 1
+        splitk = (tile_splitk(M, w.N, K, w.kind) if splitk is None else splitk) if epi == "f32" else 1
     splitk = sk0 if splitk is None else splitk
     waves = wv0 if waves is None else waves
     div = dv0 if div is None else div
@@ -297,25 +304,60 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
     elif w.kind == "fp8":
         if M <= 64:
             e.fp8_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, **kw)
-        else:
-            key = (x.device, w.N * w.K)
+        elif K % 128 == 0 and FP8_W8A8:
+            # W8A8 on the block-scaled fp8 MFMA: per-token activation scales, no weight dequantisation
+            x8, sx = quantize_rows_fp8(x)
+            e.fp8_gemm_t256(x8, sx, w.data, w.scale, w.N, out, EPI[epi], splitk)
+        else:  # weight-only fallback: dequantise the layer into a bf16 scratch, bf16 tile GEMM
             buf = _dq_scratch.get(x.device)
             if buf is None or buf.numel() < w.N * w.K:
                 buf = torch.empty(w.N * w.K, device=x.device, dtype=torch.bfloat16)
                 _dq_scratch[x.device] = buf
             e.fp8_dequant(w.data, w.scale, w.N, w.K, buf)
             e.gemm(x, buf[: w.N * w.K], w.N, out, EPI[epi], nb, splitk, waves, div)
-            del key
     else:
         raise ValueError(f"weight kind {w.kind} on GPU")
     return out
 
 
-def tile_splitk(M: int, N: int, K: int) -> int:
+FP8_W8A8 = os.environ.get("LSA_FP8_W8A8", "1") != "0"
+
+
+def quantize_rows_fp8(x: torch.Tensor):
+    """Per-token fp8: (x8 [M, K] uint8 e4m3fn bits, sx [M] f32) with x ~= e4m3(x / sx) * sx, sx = amax / 448."""
+    M, K = x.shape
+    if not _gpu(x):
+        xf = x.float()
+        sx = (xf.abs().amax(1) / 448.0).clamp(min=1e-30)
+        sx = torch.where(xf.abs().amax(1) > 0, sx, torch.ones_like(sx))
+        q = (xf / sx[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+        return q.view(torch.uint8), sx
+    x8 = torch.empty(M, K, device=x.device, dtype=torch.uint8)
+    sx = torch.empty(M, device=x.device, dtype=torch.float32)
+    ext().quant_rows_fp8(x, x8, sx)
+    return x8, sx
+
+
+def fp8_tile_splitk(M: int, N: int, K: int) -> int:
+    """Split-K of a W8A8 prefill GEMM (f32 slab epilogue) on the 256^2 fp8 tile kernel: doubled until the
+    grid has >= 256 workgroups, at most 8 slabs and >= 4 K-tiles (512 of K) per slab."""
+    tiles = ((M + 255) // 256) * ((N // 16 + 15) // 16)
+    if tiles >= 128:
+        return 1
+    sk = 1
+    while tiles * sk < 256 and sk < 8 and (K // 128) // (sk * 2) >= 4:
+        sk *= 2
+    return sk
+
+
+def tile_splitk(M: int, N: int, K: int, kind: str = "bf16") -> int:
     """Split-K of a prefill GEMM (M > 64, f32 slab epilogue) on the 128x128 tile kernel: 1 where the
     256x256 kernel takes the shape (its grid fills >= half the CUs), else doubled until the grid has
     >= 256 workgroups, at most 8 slabs and >= 16 k-blocks (512 of K) per slab.  Without it a 128-token
-    7B prompt runs the O / down projections on 32 workgroups (N / 128 tiles) streaming all of K."""
+    7B prompt runs the O / down projections on 32 workgroups (N / 128 tiles) streaming all of K.
+    fp8 weights (W8A8 256^2 fp8 kernel): ``fp8_tile_splitk``."""
+    if kind == "fp8" and FP8_W8A8 and K % 128 == 0:
+        return fp8_tile_splitk(M, N, K)
     nbt = N // 16
     if ((M + 255) // 256) * ((nbt + 15) // 16) >= 128:
         return 1

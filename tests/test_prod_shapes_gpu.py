@@ -51,9 +51,12 @@ def test_prefill_logits_prod_shapes(gpu, model, dtype):
     r.prefill([(i, p, 0) for i, p in enumerate(prompts)])
     ours = r.logits_l[: len(prompts)].float()
     for i, p in enumerate(prompts):
-        ref = reference_forward(r.w, p)[-1]
+        ref = reference_forward(r.w, p, act_quant_rows=len(p))[-1]  # packed prefill > 64 rows: W8A8 if fp8
         rel = ((ours[i] - ref).norm() / ref.norm()).item()
-        assert rel < 2e-2, (model, dtype, i, rel)
+        # fp8: the prefill runs W8A8 (per-token e4m3 activations).  The oracle applies the same rounding, but
+        # activations that sit near an e4m3 rounding boundary round differently from the oracle's (bf16-level
+        # differences vs a 6-12 % ulp), so ~5-7 % logit error remains at 2 layers (bf16: < 1 %)
+        assert rel < (1e-1 if dtype == "fp8" else 2e-2), (model, dtype, i, rel)
     for i in range(len(prompts)):
         r.release_slot(i)
 
@@ -68,7 +71,8 @@ def test_decode_tokens_prod_shapes(gpu, model, dtype, B):
     res = eng.generate(prompts, SamplingParams(max_tokens=12, ignore_eos=True))
     worst = 0.0
     for p, out in zip(prompts, res[: min(B, 6)] if B > 1 else res):
-        lg = reference_forward(eng.runner.w, p + out.token_ids[:-1])[len(p) - 1:]
+        rows = sum(len(q) for q in prompts)  # one packed prefill: W8A8 for fp8 weights when > 64 rows
+        lg = reference_forward(eng.runner.w, p + out.token_ids[:-1], act_quant_rows=len(p) if rows > 64 else 0)[len(p) - 1:]
         chosen = lg.gather(1, torch.tensor(out.token_ids, device=lg.device).view(-1, 1)).squeeze(1)
         top = lg.max(1).values
         spread = lg.std(1)
