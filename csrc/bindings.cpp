@@ -46,6 +46,7 @@ int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
 int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
+void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
 int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
                       void* out, int epi, int splitk, hipStream_t stream);
@@ -183,7 +184,8 @@ void gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wf, i
 
 // fp8 weights, activations in the fragment-major decode layout (ops.to_xfrag), M <= 64
 void fp8_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wq, const at::Tensor& wscale, int64_t N,
-                 at::Tensor& out, int64_t epi, int64_t nb, int64_t splitk, const c10::optional<at::Tensor>& rowss,
+                 at::Tensor& out, int64_t epi, int64_t nb, int64_t splitk, int64_t waves, int64_t depth,
+                 const c10::optional<at::Tensor>& rowss,
                  double eps, const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& xout, int64_t xmt,
                  const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets) {
   need(xf, at::kBFloat16, "xf");
@@ -194,6 +196,7 @@ void fp8_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& w
   TORCH_CHECK(xf.is_contiguous() && xf.numel() >= mt * 16 * K, "xf too small");
   check_out(epi, out, splitk, M, N, mt);
   const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, h, xout, xmt, ss_out, tickets, N / 16);
+  lsa_fp8_gemm_knobs((int)waves, (int)depth);
   check(lsa_fp8_gemm_ex(xf.data_ptr(), K, M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(), epi, nb,
                         splitk, 1, eo.on ? &eo.e : nullptr, cur_stream()),
         "fp8_gemm_xf");
@@ -218,7 +221,8 @@ void gemm_t256(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor&
 }
 
 void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscale, int64_t N, at::Tensor& out,
-              int64_t epi, int64_t nb, int64_t splitk, const c10::optional<at::Tensor>& rowss, double eps,
+              int64_t epi, int64_t nb, int64_t splitk, int64_t waves, int64_t depth,
+              const c10::optional<at::Tensor>& rowss, double eps,
               const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& xout, int64_t xmt,
               const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets) {
   need(x, at::kBFloat16, "x");
@@ -228,6 +232,7 @@ void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscal
   const int M = x.size(0), K = x.size(1);
   TORCH_CHECK(wq.numel() == N * K, "fp8 weight numel mismatch");
   const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, h, xout, xmt, ss_out, tickets, N / 16);
+  lsa_fp8_gemm_knobs((int)waves, (int)depth);
   check(lsa_fp8_gemm_ex(x.data_ptr(), x.stride(0), M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(),
                         epi, nb, splitk, 0, eo.on ? &eo.e : nullptr, cur_stream()),
         "fp8_gemm");
@@ -449,10 +454,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_t256", &gemm_t256);
   m.def("fp8_gemm", &fp8_gemm, py::arg("x"), py::arg("wq"), py::arg("wscale"), py::arg("N"), py::arg("out"),
-        py::arg("epi"), py::arg("nb"), py::arg("splitk"),
+        py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("depth") = 1,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("fp8_gemm_xf", &fp8_gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wq"), py::arg("wscale"),
-        py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"),
+        py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4,
+        py::arg("depth") = 1,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
         py::arg("ids"), py::arg("emb"), py::arg("row_idx"), py::arg("write_h"), py::arg("w"), py::arg("eps"),

@@ -267,19 +267,41 @@ __global__ __launch_bounds__(256) void fp8_dequant_kernel(const uint4* __restric
 static thread_local int g_fp8_xfrag = 0;
 static thread_local LsaEpi g_fp8_epi = {};
 
+// Per-call knobs (ops.pick_gemm_config, fp8 tuning entries): waves 4 | 8 per workgroup; depth 1 | 2
+// multiplies the chunk of k64-steps each wave keeps in flight (U0 = 4 / NB fragments per chunk: the
+// shallow point; depth 2 doubles the weight bytes in flight per wave for grids with few waves per CU).
+static thread_local int g_fp8_waves = 4;
+static thread_local int g_fp8_depth = 1;
+
+template <int MT, int NB, int EPI, int WV, int U>
+static void launch_tx(const uint16_t* X, int ldx, int M, int KB64, const uint4* Wq, const float* sc, int NBtot,
+                      void* out, int ldo, int kbps, int splitk, hipStream_t s) {
+  if (g_fp8_xfrag)
+    hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, WV, U, true>), dim3(NBtot / NB, splitk), dim3(64 * WV), 0,
+                       s, X, ldx, M, KB64, Wq, sc, out, ldo, kbps, g_fp8_epi);
+  else
+    hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, WV, U, false>), dim3(NBtot / NB, splitk), dim3(64 * WV), 0,
+                       s, X, ldx, M, KB64, Wq, sc, out, ldo, kbps, g_fp8_epi);
+}
+
 template <int MT, int NB, int EPI>
 static void launch_t(const uint16_t* X, int ldx, int M, int KB64, const uint4* Wq, const float* sc, int NBtot, void* out,
                      int ldo, int splitk, hipStream_t s) {
-  // 4 waves, 4 fragments (NB * U) per chunk: the shallow-chunk / high-occupancy point that won the
-  // bf16 sweeps (each fp8 fragment feeds twice the MFMA work of a bf16 one)
+  // default: 4 waves, 4 fragments (NB * U) per chunk (the shallow-chunk / high-occupancy point that won the
+  // bf16 sweeps: each fp8 fragment feeds twice the MFMA work of a bf16 one)
   constexpr int U = (4 / NB) < 1 ? 1 : (4 / NB);
   const int kbps = (KB64 + splitk - 1) / splitk;
-  if (g_fp8_xfrag)
-    hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, 4, U, true>), dim3(NBtot / NB, splitk), dim3(256), 0, s, X,
-                       ldx, M, KB64, Wq, sc, out, ldo, kbps, g_fp8_epi);
-  else
-    hipLaunchKernelGGL((gemm_fp8_skinny_kernel<MT, NB, EPI, 4, U, false>), dim3(NBtot / NB, splitk), dim3(256), 0, s,
-                       X, ldx, M, KB64, Wq, sc, out, ldo, kbps, g_fp8_epi);
+  if constexpr (EPI == EPI_BF16) {  // not on the decode hot path: one configuration
+    launch_tx<MT, NB, EPI, 4, U>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, kbps, splitk, s);
+  } else {
+    if (g_fp8_waves == 8) {
+      if (g_fp8_depth == 2) launch_tx<MT, NB, EPI, 8, 2 * U>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, kbps, splitk, s);
+      else launch_tx<MT, NB, EPI, 8, U>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, kbps, splitk, s);
+    } else {
+      if (g_fp8_depth == 2) launch_tx<MT, NB, EPI, 4, 2 * U>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, kbps, splitk, s);
+      else launch_tx<MT, NB, EPI, 4, U>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, kbps, splitk, s);
+    }
+  }
 }
 
 template <int EPI>
@@ -322,6 +344,11 @@ extern "C" int lsa_fp8_gemm(const void* X, int ldx, int M, int K, const void* Wq
 // xfrag = 1: X in the fragment-major decode layout (M <= 64); a SiLU output is written in it too
 extern "C" int lsa_fp8_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N,
                                void* out, int epi, int nb, int splitk, int xfrag, const LsaEpi* ep, hipStream_t stream);
+
+extern "C" void lsa_fp8_gemm_knobs(int waves, int depth) {
+  g_fp8_waves = waves == 8 ? 8 : 4;
+  g_fp8_depth = depth == 2 ? 2 : 1;
+}
 
 extern "C" int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N,
                                 void* out, int epi, int nb, int splitk, int xfrag, hipStream_t stream) {

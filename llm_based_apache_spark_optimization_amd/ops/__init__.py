@@ -204,10 +204,13 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
             e = tab.get(f"{N}x{K}:{epi}:b{b}" + (":fp8" if kind == "fp8" else ":xf" if xf else ""))
         if e is None and kind == "fp8":
             e = tab.get(key + ":fp8")
+        fp8_entry = e is not None and kind == "fp8"
         if e is None and xf:
             e = tab.get(key + ":xf")
         e = e if e is not None else tab.get(key)
         if e is not None and not (M > 32 and e["nb"] > 2):
+            if kind == "fp8" and not fp8_entry:  # a bf16 entry's nb / split only; fp8 knobs at their defaults
+                return e["nb"], e["splitk"], 4, 4
             return e["nb"], e["splitk"], e["waves"], e["div"]
     nb, sk = pick_nb_splitk(M, N, K, epi)
     return nb, sk, 4, 4
@@ -215,6 +218,12 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
 
 # ----------------------------------------------------------------------------------- linear
 _dq_scratch: dict = {}
+
+
+def _fp8_depth(div) -> int:
+    """fp8 skinny GEMM chunk depth from a config tuple's 4th field: entries measured for fp8 store the
+    depth (1 | 2) there; the bf16 'div' defaults (4) mean the shallow default."""
+    return 2 if div == 2 else 1
 
 
 def _epi_kw(rownorm, res, xmt: int) -> dict:
@@ -302,8 +311,8 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
     if w.kind == "bf16":
         e.gemm(x, w.data, w.N, out, EPI[epi], nb, splitk, waves, div, **kw)
     elif w.kind == "fp8":
-        if M <= 64:
-            e.fp8_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, **kw)
+        if M <= 64:  # fp8 knobs: waves, and the tuning entry's "div" field is the chunk depth (1 | 2)
+            e.fp8_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, _fp8_depth(div), **kw)
         elif K % 128 == 0 and FP8_W8A8:
             # W8A8 on the block-scaled fp8 MFMA: per-token activation scales, no weight dequantisation
             x8, sx = quantize_rows_fp8(x)
@@ -421,7 +430,7 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
             out = torch.empty(M, w.N, device=xf.device, dtype=torch.bfloat16)
     kw = _epi_kw(rownorm, res, xfrag_tiles(M))
     if w.kind == "fp8":
-        ext().fp8_gemm_xf(xf, M, w.K, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, **kw)
+        ext().fp8_gemm_xf(xf, M, w.K, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, _fp8_depth(div), **kw)
     else:
         ext().gemm_xf(xf, M, w.K, w.data, w.N, out, EPI[epi], nb, splitk, waves, div, **kw)
     return out

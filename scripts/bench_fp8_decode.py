@@ -1,0 +1,93 @@
+"""fp8 weight-only decode GEMM sweep (W8A16 skinny kernel, csrc/kernels/gemm_fp8.hip) over (nb, splitk,
+waves, depth) at the decode batch buckets, vs the configuration ops picks today.  Weights rotate over > 600 MiB
+so they stream from HBM.  Each line carries a "tune" entry (key "NxK:epi:b<M>:fp8", the 4th config field =
+chunk depth) when the sweep beats the pick by > 3 %; scripts/merge_tuning.py folds them in.
+
+    python scripts/bench_fp8_decode.py [Ms]
+"""
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from llm_based_apache_spark_optimization_amd import ops  # noqa: E402
+
+dev = torch.device("cuda:0")
+SHAPES = {"7b_qkv": (12288, 4096, "f32"), "7b_o": (4096, 4096, "res"), "7b_gateup": (22016, 4096, "silu"),
+          "7b_down": (4096, 11008, "res"), "7b_o_f32": (4096, 4096, "f32"), "7b_down_f32": (4096, 11008, "f32"),
+          "7b_lmhead": (32000, 4096, "f32"), "3b_qkv": (5120, 3072, "f32"), "3b_gateup": (16384, 3072, "silu"),
+          "3b_o": (3072, 3072, "res"), "3b_down": (3072, 8192, "res"), "3b_o_f32": (3072, 3072, "f32"),
+          "3b_down_f32": (3072, 8192, "f32")}
+Ms = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 8, 16, 32]
+
+
+def timeit(fn, it=30):
+    for i in range(3):
+        fn(i)
+    torch.cuda.synchronize()
+    reps = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(it):
+            fn(i)
+        e1.record()
+        torch.cuda.synchronize()
+        reps.append(e0.elapsed_time(e1) * 1000 / it)
+    return sorted(reps)[1]
+
+
+for name, (N, K, epi) in SHAPES.items():
+    ncopy = max(2, (600 << 20) // (N * K) + 1)
+    ws = [ops.PackedWeight.from_dense((torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16), "fp8")
+          for _ in range(ncopy)]
+    for M in Ms:
+        xf = 16 < M <= 64
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        xin = ops.to_xfrag(x) if xf else x
+        h = torch.randn(M, N, device=dev)
+        xout = torch.zeros(ops.xfrag_tiles(M) * 16 * N if xf else M * N, device=dev, dtype=torch.bfloat16)
+        ss = torch.zeros(M, device=dev)
+        tk = torch.zeros(N // 16, device=dev, dtype=torch.int32)
+
+        def call(cfg):
+            nb, sk, waves, dv = cfg
+            if epi == "silu":
+                o = torch.empty(ops.xfrag_tiles(M) * 16 * (N // 2) if xf else M * (N // 2), device=dev,
+                                dtype=torch.bfloat16)
+                o = o if xf else o.view(M, N // 2)
+                kw = {}
+            else:
+                o = torch.empty(sk, M, N, device=dev)
+                kw = {"res": (h, xout if xf else xout.view(M, N), ss, tk)} if epi == "res" else {}
+            if xf:
+                return lambda i: ops.linear_xf(xin, M, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb, waves=waves,
+                                               div=dv, **kw)
+            return lambda i: ops.linear(xin, ws[i % ncopy], epi, out=o, splitk=sk, nb=nb, waves=waves, div=dv, **kw)
+
+        picked = ops.pick_gemm_config(M, N, K, epi, xf=xf, kind="fp8")
+        res = {"shape": name, "M": M, "epi": epi, "picked": list(picked), "picked_us": round(timeit(call(picked)), 2)}
+        best = None
+        for waves in (4, 8):
+            for depth in (1, 2):
+                for nb in (1, 2, 4):
+                    if (N // 16) % nb or (epi == "silu" and nb == 1) or (M > 32 and nb > 2):
+                        continue
+                    for sk in ((1, 2, 4, 8) if epi != "silu" else (1,)):
+                        if K // 64 // sk < 4:
+                            continue
+                        us = timeit(call((nb, sk, waves, depth)))
+                        if best is None or us < best[1]:
+                            best = ((nb, sk, waves, depth), us)
+        res["picked_us"] = round(min(res["picked_us"], timeit(call(picked))), 2)
+        res["best"], res["best_us"] = list(best[0]), round(best[1], 2)
+        res["GBps_best"] = round(N * K / best[1] / 1e3, 1)
+        if best[1] < 0.97 * res["picked_us"] and M in (1, 2, 4, 8, 16, 32, 64):
+            nb, sk, wv, dp = best[0]
+            res["tune"] = {f"{N}x{K}:{epi}:b{M}:fp8": {"nb": nb, "splitk": sk, "waves": wv, "div": dp,
+                                                         "us": round(best[1], 2),
+                                                         "note": f"scripts/bench_fp8_decode.py: pick {res['picked_us']} us (div = chunk depth)"}}
+        print(json.dumps(res), flush=True)
+    del ws
+    torch.cuda.empty_cache()
