@@ -47,6 +47,9 @@ int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const
 int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 void lsa_fp8_gemm_knobs(int waves, int depth);
+int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
+                       const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
+                       void* out, hipStream_t s);
 int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
 int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
                       void* out, int epi, int splitk, hipStream_t stream);
@@ -319,9 +322,16 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                   const at::Tensor& cu_q, const at::Tensor& ctx_lens, const at::Tensor& work, int64_t H, int64_t Hkv,
-                  double scale, at::Tensor& out) {
+                  double scale, at::Tensor& out, int64_t rows32) {
   need(q, at::kBFloat16, "q");
   need(work, at::kInt, "work");
+  if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip)
+    check(lsa_attn_prefill32(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
+                             block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
+                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), cur_stream()),
+          "attn_prefill32");
+    return;
+  }
   check(lsa_attn_prefill(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                          block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
                          work.size(0), H, Hkv, (float)scale, out.data_ptr(), cur_stream()),
@@ -471,7 +481,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("counters"), py::arg("xf_mt") = 0,
         py::arg("qkv_parts") = py::none(),
         py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4);
-  m.def("attn_prefill", &attn_prefill);
+  m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
+        py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
+        py::arg("out"), py::arg("rows32") = 0);
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);
   m.def("fp8_dequant", &fp8_dequant);

@@ -132,6 +132,27 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   // splits' first blocks too was measured: splits a short sequence does not need then cost a wasted
   // block read each, 23 -> 36 us at B = 32, ctx 200, 4 splits.)
   if (split == 0) fetch(kA, vA, 0, 63);
+  // fused RoPE: the new token's q / k / v rows (sum of the QKV projection's split-K slabs) do not depend on
+  // the context length -- their loads leave before pos[b] is read, off the prologue's dependent chain
+  float xq[8];
+  if constexpr (ROPE != 0) {
+    if (lg < G + 2) {
+      const float* row = ra.parts + (size_t)b * (H + 2 * Hkv) * D;
+      const int off = (lg < G ? (hk * G + lg) * D : (lg == G ? (H + hk) * D : (H + Hkv + hk) * D)) + li * 8;
+      const float4 a0 = *reinterpret_cast<const float4*>(row + off);
+      const float4 a1 = *reinterpret_cast<const float4*>(row + off + 4);
+      xq[0] = a0.x; xq[1] = a0.y; xq[2] = a0.z; xq[3] = a0.w; xq[4] = a1.x; xq[5] = a1.y; xq[6] = a1.z; xq[7] = a1.w;
+      const int np = ROPE > 0 ? ROPE : ra.nparts;
+#pragma unroll
+      for (int sp = 1; sp < np; ++sp) {
+        const float* r2 = row + sp * ra.part_stride + off;
+        const float4 b0 = *reinterpret_cast<const float4*>(r2);
+        const float4 b1 = *reinterpret_cast<const float4*>(r2 + 4);
+        xq[0] += b0.x; xq[1] += b0.y; xq[2] += b0.z; xq[3] += b0.w;
+        xq[4] += b1.x; xq[5] += b1.y; xq[6] += b1.z; xq[7] += b1.w;
+      }
+    }
+  }
   const int ctx = pos[b] + 1;
   const int nblk = (ctx + 63) >> 6;
   int ech, nse;
@@ -160,21 +181,8 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     // the results go through LDS to all lane groups
     static_assert(G + 2 <= NLG, "fused rope: one lane group per q head + k + v");
     if (lg < G + 2) {
-      const float* row = ra.parts + (size_t)b * (H + 2 * Hkv) * D;
       const int dd = li * 8;  // own 8 dims; the rotate-half partners live in lane li ^ 8
-      const int off = lg < G ? (hk * G + lg) * D : (lg == G ? (H + hk) * D : (H + Hkv + hk) * D);
-      float x[8];
-      const float4 a0 = *reinterpret_cast<const float4*>(row + off + dd);
-      const float4 a1 = *reinterpret_cast<const float4*>(row + off + dd + 4);
-      x[0] = a0.x; x[1] = a0.y; x[2] = a0.z; x[3] = a0.w; x[4] = a1.x; x[5] = a1.y; x[6] = a1.z; x[7] = a1.w;
-      const int np = ROPE > 0 ? ROPE : ra.nparts;
-#pragma unroll
-      for (int sp = 1; sp < np; ++sp) {
-        const float* r2 = row + sp * ra.part_stride + off + dd;
-        const float4 b0 = *reinterpret_cast<const float4*>(r2);
-        const float4 b1 = *reinterpret_cast<const float4*>(r2 + 4);
-        x[0] += b0.x; x[1] += b0.y; x[2] += b0.z; x[3] += b0.w; x[4] += b1.x; x[5] += b1.y; x[6] += b1.z; x[7] += b1.w;
-      }
+      const float* x = xq;
       float y[8];
       if (lg <= G) {  // rotate q heads and k
         const float4 c0 = *reinterpret_cast<const float4*>(ra.cos_t + (size_t)tpos * 64 + (dd & 63));
@@ -190,14 +198,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] = x[j];
       }
-      const uint4 yq = pack8(y);
-      qkv_s[lg][li] = yq;
-      // the workgroup covering position tpos appends the new token's k / v to the cache
-      if (lg >= G && blk0 < nblk && blk1 == nblk) {
-        const size_t co = (((size_t)block_tables[(size_t)b * max_blocks + (tpos >> 6)] * Hkv + hk) * 64 +
-                           (tpos & 63)) * D + dd;
-        *reinterpret_cast<uint4*>((lg == G ? ra.kc : ra.vc) + co) = yq;
-      }
+      qkv_s[lg][li] = pack8(y);
     }
     __syncthreads();
 #pragma unroll
@@ -305,6 +306,15 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     if (blk < blk1) score(kA, vA, blk);
   }
 
+  if constexpr (ROPE != 0) {
+    // the workgroup covering position tpos appends the new token's k / v to the cache: after its score loop
+    // (which substitutes them from LDS / registers where it meets tpos), off the prologue's critical path
+    if (lg >= G && lg < G + 2 && blk0 < nblk && blk1 == nblk) {
+      const size_t co = (((size_t)block_tables[(size_t)b * max_blocks + (tpos >> 6)] * Hkv + hk) * 64 +
+                         (tpos & 63)) * D + li * 8;
+      *reinterpret_cast<uint4*>((lg == G ? ra.kc : ra.vc) + co) = qkv_s[lg][li];
+    }
+  }
   // merge the 4 lane groups of each wave in registers (xor-16 / xor-32 lane exchanges), then the WV wave
   // partials through LDS: a quarter of the LDS traffic and merge loop of a lane-group-level merge
   // (7B B=32 ctx ~190: 23.6 -> 22.1 us; 7B B=1: 7.3 -> 6.4 us, rocprofv3)

@@ -483,6 +483,7 @@ class ModelRunner:
                     self.block_tables[sl].copy_(pend)
                     del self._pending_bt[sl]
         work = None
+        self._cu_host = cu  # host offsets: the prefill attention kernel choice (ops._prefill_kernel)
         if self.on_gpu:
             work = torch.tensor(ops.prefill_work(cu), dtype=torch.int32).to(dev, non_blocking=True)
 
@@ -569,7 +570,7 @@ class ModelRunner:
             ops.linear(xn, lw.wqkv, "bf16", out=qkv)
             ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
         ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
-                         work=work)
+                         work=work, cu_list=self._cu_host)
 
     def _prefill_layers_sp(self, T, ids, posd, tsd, bt, cud, ctxd, last, work, n, commit):
         """Sequence-parallel prefill under TP: rank r owns rows [r*Tl, (r+1)*Tl) of the residual stream.

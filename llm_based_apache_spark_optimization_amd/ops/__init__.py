@@ -569,11 +569,30 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     return out
 
 
+# prefill attention kernel: "32" = 32 x 32 MFMA tiles, 128 query rows per workgroup (attention_prefill32.hip);
+# "16" = the 16 x 16 kernel of attention.hip (64 rows per workgroup); "auto" = 32 when the longest packed
+# sequence has >= 512 rows (measured, scripts/bench_attn_prefill.py: 7B 2k 146 -> 119 us, 3B 2k 118 -> 115 us,
+# 8k 1051 -> 1021 us), else 16 (32 x 128-token prompts: 28 vs 31 us, twice the work items)
+PREFILL_ATTN = os.environ.get("LSA_PREFILL_ATTN", "auto")
+
+
+def _prefill_kernel(cu_q: list) -> str:
+    if PREFILL_ATTN != "auto":
+        return PREFILL_ATTN
+    longest = max((cu_q[i + 1] - cu_q[i] for i in range(len(cu_q) - 1)), default=0)
+    return "32" if longest >= 512 else "16"
+
+
+def prefill_qblock(cu_q: Optional[list] = None) -> int:
+    k = _prefill_kernel(cu_q or [0])
+    return 128 if k == "32" else ext().prefill_qblock
+
+
 def prefill_work(cu_q: list[int], qblock: Optional[int] = None) -> list[tuple[int, int]]:
-    """(seq, q_start) work items of the prefill attention kernel's query block (``ext().prefill_qblock``
+    """(seq, q_start) work items of the prefill attention kernel's query block (``prefill_qblock()``
     rows), heaviest (latest) query blocks first for causal balance."""
     if qblock is None:
-        qblock = ext().prefill_qblock
+        qblock = prefill_qblock(cu_q)
     items = []
     for s in range(len(cu_q) - 1):
         ql = cu_q[s + 1] - cu_q[s]
@@ -583,12 +602,16 @@ def prefill_work(cu_q: list[int], qblock: Optional[int] = None) -> list[tuple[in
     return items
 
 
-def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, work=None):
+def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, work=None, cu_list=None):
+    """Causal prefill attention of packed sequences (cu_q offsets) over the paged cache.  ``work`` must
+    come from ``prefill_work`` of the same offsets (``cu_list``, host copy: picks the kernel)."""
     if not _gpu(q):
         return ref.attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out)
+    cu = cu_list if cu_list is not None else cu_q.tolist()
     if work is None:
-        work = torch.tensor(prefill_work(cu_q.tolist()), dtype=torch.int32).to(q.device)
-    ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, work, H, Hkv, scale, out)
+        work = torch.tensor(prefill_work(cu), dtype=torch.int32).to(q.device)
+    ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, work, H, Hkv, scale, out,
+                       1 if _prefill_kernel(cu) == "32" else 0)
     return out
 
 

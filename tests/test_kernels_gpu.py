@@ -365,15 +365,21 @@ def test_attn_decode_fused_rope(gpu, HH, lens, nparts):
     assert _rel(o2, o1) < 1e-2
 
 
+@pytest.mark.parametrize("kernel", ["16", "32"])
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
-@pytest.mark.parametrize("case", ["fresh", "chunked"])
-def test_attn_prefill(gpu, HH, case):
+@pytest.mark.parametrize("case", ["fresh", "chunked", "long"])
+def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
+    """Both prefill attention kernels (16 x 16 MFMA, 64 rows per workgroup; 32 x 32 MFMA, 128 rows) vs the
+    fp32 reference: packed variable-length sequences, chunked continuation, multi-block causal tiles."""
+    monkeypatch.setattr(ops, "PREFILL_ATTN", kernel)
     H, Hkv = HH
     D = 128
     if case == "fresh":
         qlens, ctx = [1, 70, 130, 64], [1, 70, 130, 64]
-    else:  # chunked prefill: context already holds earlier chunks
+    elif case == "chunked":  # chunked prefill: context already holds earlier chunks
         qlens, ctx = [10, 64, 100], [200, 64, 400]
+    else:  # several 128-row query blocks and 64-key tiles per sequence, ragged ends
+        qlens, ctx = [300, 257], [300, 400]
     kc, vc, bt = _paged(ctx, Hkv, D, gpu, seed=H)
     T = sum(qlens)
     q = torch.randn(T, H, D, device=gpu).to(torch.bfloat16)
@@ -387,8 +393,10 @@ def test_attn_prefill(gpu, HH, case):
     assert _rel(out, out2) < 1e-2
 
 
-def test_attn_prefill_spike(gpu):
+@pytest.mark.parametrize("kernel", ["16", "32"])
+def test_attn_prefill_spike(gpu, kernel, monkeypatch):
     """Force the online-softmax rescale branch: one very large score late in the sequence."""
+    monkeypatch.setattr(ops, "PREFILL_ATTN", kernel)
     H, Hkv, D = 8, 8, 128
     n = 300
     kc, vc, bt = _paged([n], Hkv, D, gpu, seed=9)
