@@ -51,9 +51,11 @@ class Settings:
     # models: the first gets 45 %, the second 45 % of what is left)
     kv_memory_fraction: float = dataclasses.field(default_factory=lambda: _env("KV_MEMORY_FRACTION", 0.45, float))
     max_new_tokens: int = dataclasses.field(default_factory=lambda: _env("MAX_NEW_TOKENS", 256, int))
-    # chunked-prefill interleave: prompt tokens prefilled per engine iteration (0 = whole prompts); long
-    # /explain_error prompts then stall the running decode batch for one chunk at a time
-    prefill_chunk: int = dataclasses.field(default_factory=lambda: _env("PREFILL_CHUNK", 512, int))
+    # chunked-prefill interleave: prompt tokens prefilled per engine iteration (0 = whole prompts); longer
+    # prompts stall the running decode batch one chunk at a time.  The budget also caps prefill throughput
+    # (one chunk per decode run): 512 collapsed co-serving at 16 QPS (nl2sql p50 0.56 -> 3.4 s), 2048 does not
+    # (scripts/gpu_r2_serving_ab.sh)
+    prefill_chunk: int = dataclasses.field(default_factory=lambda: _env("PREFILL_CHUNK", 2048, int))
     # sampling defaults: greedy (the reference sampled at Ollama defaults; pass options to match)
     temperature: float = dataclasses.field(default_factory=lambda: _env("TEMPERATURE", 0.0, float))
     top_k: int = dataclasses.field(default_factory=lambda: _env("TOP_K", 40, int))
