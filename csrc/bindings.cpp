@@ -12,7 +12,7 @@ int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* 
              hipStream_t stream);
 int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
                     const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
-                    int xf_mt, float* ss_out, int ss_ld, int ss_nzero, hipStream_t s);
+                    int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, hipStream_t s);
 int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
                 int waves, int div, int xlds, const LsaEpi* ep, hipStream_t stream);
 int lsa_fp8_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
@@ -95,9 +95,9 @@ EpiOpts epi_opts(int64_t epi, int64_t M, int64_t N, int64_t K, const c10::option
                  const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets, int64_t ncols) {
   EpiOpts o;
   if (rowss.has_value()) {
-    need(*rowss, at::kFloat, "rowss");
+    need(*rowss, at::kLong, "rowss");
     TORCH_CHECK(rowss->numel() >= M, "rowss too small");
-    o.e.rowss = rowss->data_ptr<float>();
+    o.e.rowss = reinterpret_cast<const long long*>(rowss->data_ptr<int64_t>());
     o.e.inv_k = 1.0f / (float)K;
     o.e.eps = (float)eps;
     o.on = true;
@@ -106,7 +106,7 @@ EpiOpts epi_opts(int64_t epi, int64_t M, int64_t N, int64_t K, const c10::option
     TORCH_CHECK(h.has_value() && xout.has_value() && ss_out.has_value(), "residual epilogue needs h, xout, ss_out");
     need(*h, at::kFloat, "h");
     need(*xout, at::kBFloat16, "xout");
-    need(*ss_out, at::kFloat, "ss_out");
+    need(*ss_out, at::kLong, "ss_out");
     TORCH_CHECK(h->is_contiguous() && h->numel() >= M * N, "h must be a contiguous [M, N] f32 tensor");
     TORCH_CHECK(ss_out->numel() >= M, "ss_out too small");
     TORCH_CHECK(xout->numel() >= (xmt ? xmt * 16 * N : M * N), "xout too small");
@@ -114,7 +114,7 @@ EpiOpts epi_opts(int64_t epi, int64_t M, int64_t N, int64_t K, const c10::option
     o.e.ldh = (int)N;
     o.e.xout = reinterpret_cast<uint16_t*>(xout->data_ptr());
     o.e.xmt = (int)xmt;
-    o.e.ss_out = ss_out->data_ptr<float>();
+    o.e.ss_out = reinterpret_cast<long long*>(ss_out->data_ptr<int64_t>());
     if (tickets.has_value()) {
       need(*tickets, at::kInt, "tickets");
       TORCH_CHECK(tickets->numel() >= ncols, "tickets: one counter per 16-column block needed");
@@ -251,12 +251,13 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
   need(xn, at::kBFloat16, "xn");
   const int D = w.numel();
   if (ss_out.has_value()) {
-    need(*ss_out, at::kFloat, "ss_out");
+    need(*ss_out, at::kLong, "ss_out");
     TORCH_CHECK(ss_out->numel() >= (ss_nzero + 1) * ss_ld && ss_ld >= rows, "ss_out too small");
   }
   check(lsa_add_rmsnorm(h.data_ptr<float>(), ptr<const float>(parts), parts.has_value() ? nparts : 0, part_stride,
                         ptr<const int>(ids), ptr<const void>(emb), ptr<const int>(row_idx), write_h ? 1 : 0,
-                        w.data_ptr(), (float)eps, xn.data_ptr(), rows, D, xf_mt, ptr<float>(ss_out), (int)ss_ld,
+                        w.data_ptr(), (float)eps, xn.data_ptr(), rows, D, xf_mt,
+                        ss_out.has_value() ? reinterpret_cast<long long*>(ss_out->data_ptr<int64_t>()) : nullptr, (int)ss_ld,
                         (int)ss_nzero, cur_stream()),
         "add_rmsnorm");
 }

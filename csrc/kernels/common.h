@@ -107,8 +107,14 @@ __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x));
 //    this workgroup's columns of h^2 (one device-scope float atomic per row and workgroup).
 #define EPI_RES 3
 
+// Row sums of squares travel as Q24 fixed point in int64: integer atomics add exactly, so the sum (and every
+// token decoded from it) is independent of the order in which the workgroups arrive -- float atomics made
+// two identical requests in one batch diverge after a few tokens on a near-tied argmax.
+#define LSA_Q24 16777216.0f
+__device__ __forceinline__ long long ss_to_q24(float v) { return (long long)(v * LSA_Q24); }
+
 __device__ __forceinline__ float epi_row_scale(const LsaEpi& ep, int m) {
-  return ep.rowss ? rsqrtf(ep.rowss[m] * ep.inv_k + ep.eps) : 1.0f;
+  return ep.rowss ? rsqrtf((float)ep.rowss[m] * (1.0f / LSA_Q24) * ep.inv_k + ep.eps) : 1.0f;
 }
 
 //    With split-K (grid.y > 1) every split publishes its f32 partial write-through (sc1) into the

@@ -159,13 +159,13 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 
   // cross-wave reduction: red[w][tile][lane]
   __shared__ __attribute__((aligned(16))) f32x4_t red[WAVES][NB * MT][64];
-  __shared__ float ssw[16 * MT];  // EPI_RES: per-row sum of h^2 over this workgroup's columns
+  __shared__ unsigned long long ssw[16 * MT];  // EPI_RES: per-row sum of h^2 over this workgroup's columns (Q24)
 #pragma unroll
   for (int i = 0; i < NB; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) red[w][i * MT + j][lane] = acc[i][j];
   if constexpr (EPI == EPI_RES) {
-    if (threadIdx.x < 16 * MT) ssw[threadIdx.x] = 0.f;
+    if (threadIdx.x < 16 * MT) ssw[threadIdx.x] = 0ull;
   }
   __syncthreads();
 
@@ -219,11 +219,12 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
           const int m = j * 16 + (l & 15);
           if (m < M) {
             const int n = (nb0 + i) * 16 + 4 * (l >> 4);
-            atomicAdd(&ssw[m], epi_residual4(ep, m, n, res_slab_sum(rs, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y)));
+            atomicAdd(&ssw[m], (unsigned long long)ss_to_q24(
+                epi_residual4(ep, m, n, res_slab_sum(rs, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y))));
           }
         }
         __syncthreads();
-        if (threadIdx.x < M) atomicAdd(ep.ss_out + threadIdx.x, ssw[threadIdx.x]);
+        if (threadIdx.x < M) atomicAdd(reinterpret_cast<unsigned long long*>(ep.ss_out) + threadIdx.x, ssw[threadIdx.x]);
         return;
       }
     }
@@ -238,13 +239,13 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       if (m < M) {
         s *= epi_row_scale(ep, m);
         const int n = (nb0 + i) * 16 + 4 * (l >> 4);
-        if constexpr (EPI == EPI_RES) atomicAdd(&ssw[m], epi_residual4(ep, m, n, s));
+        if constexpr (EPI == EPI_RES) atomicAdd(&ssw[m], (unsigned long long)ss_to_q24(epi_residual4(ep, m, n, s)));
         else store4<EPI>(out, ldo, slab, m, n, s);
       }
     }
     if constexpr (EPI == EPI_RES) {
       __syncthreads();
-      if (threadIdx.x < M) atomicAdd(ep.ss_out + threadIdx.x, ssw[threadIdx.x]);
+      if (threadIdx.x < M) atomicAdd(reinterpret_cast<unsigned long long*>(ep.ss_out) + threadIdx.x, ssw[threadIdx.x]);
     }
   }
 }

@@ -135,13 +135,13 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
   }
 
   __shared__ __attribute__((aligned(16))) f32x4_t red[WAVES][NB * MT][64];
-  __shared__ float ssw[16 * MT];  // EPI_RES: per-row sum of h^2 over this workgroup's columns
+  __shared__ unsigned long long ssw[16 * MT];  // EPI_RES: per-row sum of h^2 over this workgroup's columns (Q24)
 #pragma unroll
   for (int i = 0; i < NB; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) red[w][i * MT + j][lane] = acc[i][j];
   if constexpr (EPI == EPI_RES) {
-    if (threadIdx.x < 16 * MT) ssw[threadIdx.x] = 0.f;
+    if (threadIdx.x < 16 * MT) ssw[threadIdx.x] = 0ull;
   }
   __syncthreads();
 
@@ -197,11 +197,12 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
           const int m = j * 16 + (l & 15);
           if (m < M) {
             const int n = (nb0 + i) * 16 + 4 * (l >> 4);
-            atomicAdd(&ssw[m], epi_residual4(ep, m, n, res_slab_sum(rsc, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y)));
+            atomicAdd(&ssw[m], (unsigned long long)ss_to_q24(
+                epi_residual4(ep, m, n, res_slab_sum(rsc, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y))));
           }
         }
         __syncthreads();
-        if (threadIdx.x < M) atomicAdd(ep.ss_out + threadIdx.x, ssw[threadIdx.x]);
+        if (threadIdx.x < M) atomicAdd(reinterpret_cast<unsigned long long*>(ep.ss_out) + threadIdx.x, ssw[threadIdx.x]);
         return;
       }
     }
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
       const float rs = epi_row_scale(ep, m);
       s[0] *= sc.x * rs; s[1] *= sc.y * rs; s[2] *= sc.z * rs; s[3] *= sc.w * rs;
       if constexpr (EPI == EPI_RES) {
-        atomicAdd(&ssw[m], epi_residual4(ep, m, n, s));
+        atomicAdd(&ssw[m], (unsigned long long)ss_to_q24(epi_residual4(ep, m, n, s)));
       } else if constexpr (EPI == EPI_F32) {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + slab + (size_t)m * ldo + n) =
             make_float4(s[0], s[1], s[2], s[3]);
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
     }
     if constexpr (EPI == EPI_RES) {
       __syncthreads();
-      if (threadIdx.x < M) atomicAdd(ep.ss_out + threadIdx.x, ssw[threadIdx.x]);
+      if (threadIdx.x < M) atomicAdd(reinterpret_cast<unsigned long long*>(ep.ss_out) + threadIdx.x, ssw[threadIdx.x]);
     }
   }
 }

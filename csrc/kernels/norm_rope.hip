@@ -19,7 +19,7 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
                                                            const int* __restrict__ row_idx, int write_h,
                                                            const uint16_t* __restrict__ w, float eps,
                                                            uint16_t* __restrict__ xn, int D, int xf_mt,
-                                                           float* __restrict__ ss_out, int ss_ld, int ss_nzero) {
+                                                           long long* __restrict__ ss_out, int ss_ld, int ss_nzero) {
   __shared__ float red[16];
   const int m = blockIdx.x;
   const int r = row_idx ? row_idx[m] : m;
@@ -78,8 +78,8 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
   if (ss_out) {
     // raw mode (norm folded into the next GEMMs): xn = bf16(h) un-normalised, ss_out[m] = sum h^2, and
     // the following ss_nzero accumulators of this row (rows ss_ld apart) are zeroed for their producers
-    if (threadIdx.x == 0) ss_out[m] = tot;
-    for (int k = threadIdx.x; k < ss_nzero; k += nt) ss_out[(size_t)(k + 1) * ss_ld + m] = 0.f;
+    if (threadIdx.x == 0) ss_out[m] = ss_to_q24(tot);
+    for (int k = threadIdx.x; k < ss_nzero; k += nt) ss_out[(size_t)(k + 1) * ss_ld + m] = 0;
   }
   const float inv = ss_out ? 1.0f : rsqrtf(tot / (float)D + eps);
 #pragma unroll
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
 template <int VPT>
 static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, const float* parts, size_t ps,
                            const int* ids, const uint16_t* e, const int* row_idx, int write_h, const uint16_t* w,
-                           float eps, uint16_t* o, int D, int xf_mt, float* ss_out, int ss_ld, int ss_nzero) {
+                           float eps, uint16_t* o, int D, int xf_mt, long long* ss_out, int ss_ld, int ss_nzero) {
 #define LSA_RN(NP)                                                                                         \
   hipLaunchKernelGGL((add_rmsnorm_kernel<NP, VPT>), dim3(rows), dim3(nt), 0, s, h, parts, np, ps, ids, e, \
                      row_idx, write_h, w, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero)
@@ -117,7 +117,7 @@ static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, co
 
 extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids,
                                const void* emb, const int* row_idx, int write_h, const void* w, float eps, void* xn,
-                               int rows, int D, int xf_mt, float* ss_out, int ss_ld, int ss_nzero, hipStream_t s) {
+                               int rows, int D, int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, hipStream_t s) {
   if (D % 8 != 0 || rows <= 0) return -1;
   if (xf_mt && (D % 32 != 0 || rows > 16 * xf_mt)) return -3;
   if (ss_out && (row_idx || ss_ld < rows || ss_nzero < 0)) return -4;

@@ -149,7 +149,7 @@ class ModelRunner:
         # 7B 2.77 -> 2.71 ms) but loses at batch 32 for the 3B (2029 -> 2087 us: the residual epilogue's
         # last-arriver tail costs more than the norm launch it replaces); the norm launches stay above it
         self.fused_norm_max_batch = int(os.environ.get("LSA_FUSED_NORM_MAX_B", "16"))
-        self.ssq = torch.zeros(2 * self.L + 2, S, **f32)
+        self.ssq = torch.zeros(2 * self.L + 2, S, dtype=torch.int64, device=dev)  # Q24 fixed point (ops.ss_q24)
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)
         self.graphs: dict = {}

@@ -226,11 +226,25 @@ def _fp8_depth(div) -> int:
     return 2 if div == 2 else 1
 
 
+SS_SCALE = float(1 << 24)
+
+
+def ss_q24(v: torch.Tensor) -> torch.Tensor:
+    """f32 sums of squares -> the kernels' int64 Q24 fixed point (truncating, like the device conversion)."""
+    return (v.float() * SS_SCALE).to(torch.int64)
+
+
+def ss_float(q: torch.Tensor) -> torch.Tensor:
+    return q.double().div(SS_SCALE).float()
+
+
 def _epi_kw(rownorm, res, xmt: int) -> dict:
     """Keyword arguments of the kernels' decode epilogue extensions (csrc/kernels/lsa_epi.h).
 
     rownorm = (ss, eps): the input rows are the UN-normalised residual stream (RMSNorm gamma folded into
-    the weight): output row m is scaled by rsqrt(ss[m] / K + eps).
+    the weight): output row m is scaled by rsqrt(ss[m] / K + eps).  Row sums of squares (``ss``, ``ss_out``)
+    are int64 Q24 fixed point (value * 2^24, ``SS_SCALE``): the kernels add them with integer atomics, so the
+    total does not depend on workgroup arrival order and batched decoding stays deterministic.
     res = (h, xout, ss_out[, tickets]) with epi='res': h += y (f32 [M, N]); xout = bf16(h) (fragment-major
     when the call is linear_xf, else row-major [M, N]); ss_out[m] += sum_n h[m, n]^2 (the next GEMM's
     rownorm).  With ``tickets`` (int32, >= N/16 zeroed counters) the GEMM may split K: the splits publish
@@ -267,7 +281,7 @@ def _epi_ref(y: torch.Tensor, M: int, K: int, epi: str, rownorm, res, xf: bool):
         xout.view(-1)[: f.numel()].copy_(f)
     else:
         xout.view(-1)[: x16.numel()].copy_(x16.reshape(-1))
-    ss_out[:M] += hn.pow(2).sum(1)
+    ss_out[:M] += ss_q24(hn.pow(2).sum(1))
 
 
 def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
@@ -280,7 +294,7 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
     assert (epi == "res") == (res is not None), "epi='res' needs res=(h, xout, ss_out)"
     if not _gpu(x):
         if rownorm is not None:  # scale the rows before the product (the kernels scale the output rows)
-            x = (x.float() * torch.rsqrt(rownorm[0][:M].float() / K + rownorm[1])[:, None]).to(x.dtype)
+            x = (x.float() * torch.rsqrt(ss_float(rownorm[0][:M]) / K + rownorm[1])[:, None]).to(x.dtype)
         if epi == "res":
             _epi_ref(ref.linear(x, w.dense(), "f32"), M, K, epi, rownorm, res, _xf)
             return res[0]
@@ -459,7 +473,7 @@ def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
             xn.view(-1)[: f.numel()].copy_(f)
         else:
             xn[:rows].copy_(raw)
-        ss_out[:rows] = hv.pow(2).sum(1)
+        ss_out[:rows] = ss_q24(hv.pow(2).sum(1))
         for k in range(1, ss_nzero + 1):
             ss_out[k * ss_ld: k * ss_ld + rows] = 0
         return xn

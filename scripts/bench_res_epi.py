@@ -57,7 +57,7 @@ for name, (N, K) in ROWP.items():
         af = ops.to_xfrag(a) if xf else a
         h = torch.randn(M, N, device=dev)
         xout = torch.zeros(ops.xfrag_tiles(M) * 16 * N if xf else M * N, device=dev, dtype=torch.bfloat16)
-        ss = torch.zeros(M, device=dev)
+        ss = torch.zeros(M, device=dev, dtype=torch.int64)
         g = torch.ones(N, device=dev, dtype=torch.bfloat16)
 
         def lin(x, w, epi, **kw):
@@ -106,7 +106,7 @@ for name, (N, K, epi) in ({} if "--rowp-only" in sys.argv else COLP).items():
         xf = 16 < M <= 64
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
         xin = ops.to_xfrag(x) if xf else x
-        ss = x.float().pow(2).sum(1)
+        ss = ops.ss_q24(x.float().pow(2).sum(1))
         nb, sk, wv, dv = ops.pick_gemm_config(M, N, K, epi, xf=xf, kind=KIND)
         o = torch.empty(sk, M, N, device=dev) if epi == "f32" else torch.empty(
             ops.xfrag_tiles(M) * 16 * (N // 2) if xf else M * N // 2, device=dev, dtype=torch.bfloat16)

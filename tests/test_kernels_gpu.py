@@ -554,9 +554,10 @@ def test_gemm_rownorm_and_residual_epilogues(gpu, kind, xf, M):
 
     inv = torch.rsqrt(ss / d + eps)[:, None]
     xs = x.float() * inv  # what the un-folded path feeds the GEMM (before its bf16 rounding)
-    y = lin(xin, pq, "f32", splitk=2, rownorm=(ss, eps))
+    ssq = ops.ss_q24(ss)  # the kernels' int64 Q24 fixed point
+    y = lin(xin, pq, "f32", splitk=2, rownorm=(ssq, eps))
     assert _rel(y.sum(0), xs @ pq.dense().float().t()) < 2e-2
-    act = lin(xin, pgu, "silu", rownorm=(ss, eps))
+    act = lin(xin, pgu, "silu", rownorm=(ssq, eps))
     act = ops.from_xfrag(act, M, F) if xf else act
     gd, ud = pgu.dense().float().view(F // 16, 2, 16, d)[:, 0].reshape(F, d), pgu.dense().float().view(F // 16, 2, 16, d)[:, 1].reshape(F, d)
     want_act = torch.nn.functional.silu(xs @ gd.t()) * (xs @ ud.t())
@@ -567,17 +568,22 @@ def test_gemm_rownorm_and_residual_epilogues(gpu, kind, xf, M):
     h_ref = h + a16.float() @ po.dense().float().t()
     tickets = torch.zeros(d // 16, device=gpu, dtype=torch.int32)
     for splitk in (1, 4):  # one workgroup per column, and split-K finished by the last-arriving split
-        hh = h.clone()
-        xout = torch.zeros(ops.xfrag_tiles(M) * 16 * d if xf else M * d, device=gpu, dtype=torch.bfloat16)
-        ss_out = torch.full((M,), 0.5, device=gpu)
-        lin(ops.to_xfrag(a16) if xf else a16, po, "res", splitk=splitk,
-            res=(hh, xout if xf else xout.view(M, d), ss_out, tickets))
-        torch.cuda.synchronize()
-        assert _rel(hh, h_ref) < 1e-2, splitk
-        got_x = ops.from_xfrag(xout, M, d) if xf else xout.view(M, d)
-        assert torch.equal(got_x, hh.to(torch.bfloat16)), splitk
-        assert torch.allclose(ss_out, 0.5 + hh.pow(2).sum(1), rtol=1e-4), splitk
-        assert torch.all(tickets == 0), "the last arriver must reset its column counter"
+        runs = []
+        for _ in range(3):
+            hh = h.clone()
+            xout = torch.zeros(ops.xfrag_tiles(M) * 16 * d if xf else M * d, device=gpu, dtype=torch.bfloat16)
+            ss_out = torch.full((M,), 1 << 23, device=gpu, dtype=torch.int64)  # 0.5 in Q24
+            lin(ops.to_xfrag(a16) if xf else a16, po, "res", splitk=splitk,
+                res=(hh, xout if xf else xout.view(M, d), ss_out, tickets))
+            torch.cuda.synchronize()
+            assert _rel(hh, h_ref) < 1e-2, splitk
+            got_x = ops.from_xfrag(xout, M, d) if xf else xout.view(M, d)
+            assert torch.equal(got_x, hh.to(torch.bfloat16)), splitk
+            assert torch.allclose(ops.ss_float(ss_out), 0.5 + hh.pow(2).sum(1), rtol=1e-4), splitk
+            assert torch.all(tickets == 0), "the last arriver must reset its column counter"
+            runs.append(ss_out)
+        # integer accumulation: bit-identical whatever order the workgroups finished in
+        assert all(torch.equal(runs[0], r) for r in runs[1:]), splitk
 
 
 @pytest.mark.parametrize("xf", [False, True])
@@ -589,7 +595,7 @@ def test_add_rmsnorm_raw_mode(gpu, xf):
     ids = torch.randint(0, V, (B,), device=gpu, dtype=torch.int32)
     h = torch.zeros(S, d, device=gpu)
     xn = torch.zeros(ops.xfrag_tiles(B) * 16 * d if xf else B * d, device=gpu, dtype=torch.bfloat16)
-    ss = torch.full((4, S), 7.0, device=gpu)
+    ss = torch.full((4, S), 7, device=gpu, dtype=torch.int64)
     ops.add_rmsnorm(h[:B], torch.ones(d, device=gpu, dtype=torch.bfloat16), 1e-5, xn if xf else xn.view(B, d),
                     ids=ids, emb=emb, rows=B, xf=xf, ss_out=ss.view(-1), ss_ld=S, ss_nzero=2)
     torch.cuda.synchronize()
@@ -597,8 +603,8 @@ def test_add_rmsnorm_raw_mode(gpu, xf):
     assert torch.equal(h[:B], hv)
     got = ops.from_xfrag(xn, B, d) if xf else xn.view(B, d)
     assert torch.equal(got, hv.to(torch.bfloat16))
-    assert torch.allclose(ss[0, :B], hv.pow(2).sum(1), rtol=1e-5)
-    assert torch.all(ss[1:3, :B] == 0) and torch.all(ss[3] == 7.0) and torch.all(ss[0, B:] == 7.0)
+    assert torch.allclose(ops.ss_float(ss[0, :B]), hv.pow(2).sum(1), rtol=1e-5)
+    assert torch.all(ss[1:3, :B] == 0) and torch.all(ss[3] == 7) and torch.all(ss[0, B:] == 7)
 
 
 # ------------------------------------------------------------------ W8A8 fp8 prefill GEMM (block-scaled MFMA)
