@@ -494,7 +494,12 @@ static void launch_skinny_x(const uint16_t* X, int ldx, int M, int KB, const uin
 #define LSA_SKL(WV, DV) \
   hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF>), grid, dim3(64 * WV), 0, s, X, \
                      ldx, M, KB, Wf, out, ldo, kbps, g_epi)
-  if (g_skinny_div == 2) {
+  if constexpr (NB >= 6) {
+    // wide n-groups (one activation fragment feeds NB weight fragments): 4 waves only, the cross-wave
+    // reduction buffer is WAVES * NB * MT KiB
+    if (g_skinny_div == 1) LSA_SKL(4, 1);
+    else LSA_SKL(4, 2);
+  } else if (g_skinny_div == 2) {
     if (g_skinny_waves == 8) LSA_SKL(8, 2);
     else LSA_SKL(4, 2);
   } else if (g_skinny_div == 4) {
@@ -529,7 +534,7 @@ static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uin
     launch_skinny_t<MTV, NBV, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);               \
     return;                                                                                      \
   }
-  LSA_SK(1, 2) LSA_SK(1, 4) LSA_SK(2, 2) LSA_SK(2, 4) LSA_SK(4, 2)
+  LSA_SK(1, 2) LSA_SK(1, 4) LSA_SK(2, 2) LSA_SK(2, 4) LSA_SK(4, 2) LSA_SK(2, 6) LSA_SK(2, 8)
   if constexpr (EPI != EPI_SILU) { LSA_SK(1, 1) LSA_SK(2, 1) LSA_SK(4, 1) }
 #undef LSA_SK
   // fallback (nb=4 with mt=4 or unsupported): nb=2 at the same row-tile count

@@ -2,6 +2,7 @@
 tuning table vs the best of a sweep over (nb, splitk, waves, div), per shape and M (us per call, weights
 rotating over > 600 MiB so they stream from HBM).  Prints one JSON line per (shape, M)."""
 import json
+import os
 import sys
 
 import torch
@@ -15,6 +16,9 @@ SHAPES = {"7b_qkv": (12288, 4096, "f32"), "7b_o": (4096, 4096, "f32"), "7b_gateu
           "3b_down": (3072, 8192, "f32"), "3b_o": (3072, 3072, "f32")}
 Ms = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else [4, 8, 16, 24, 48, 64]
 KIND = sys.argv[2] if len(sys.argv) > 2 else "bf16"  # fp8: OCP e4m3 weights (the fp8 kernel has no waves/div knobs)
+if len(sys.argv) > 3:  # shape subset
+    SHAPES = {k: v for k, v in SHAPES.items() if k in sys.argv[3].split(",")}
+NBS = tuple(int(a) for a in os.environ.get("LSA_SWEEP_NBS", "1,2,4").split(","))
 
 
 def timeit(fn, it=30):
@@ -57,8 +61,10 @@ for name, (N, K, epi) in SHAPES.items():
         res = {"shape": name, "M": M, "xf": xf, "kind": KIND, "picked": list(picked), "picked_us": round(timeit(call(picked)), 2)}
         best = None
         for waves, dv in (((4, 1), (4, 2), (4, 4), (8, 2)) if KIND == "bf16" else ((4, 4),)):
-            for nb in (1, 2, 4):
-                if (N // 16) % nb or (epi == "silu" and nb == 1) or (M > 32 and nb > 2):
+            for nb in NBS:
+                if (N // 16) % nb or (epi == "silu" and nb % 2) or (M > 32 and nb > 2):
+                    continue
+                if nb >= 6 and (waves, dv) not in ((4, 1), (4, 2)):  # wide n-groups: 4 waves, div 1 | 2 only
                     continue
                 for sk in ((1, 2, 4, 8) if epi == "f32" else (1,)):
                     if K // 32 // sk < 8:

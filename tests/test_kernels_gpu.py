@@ -60,12 +60,13 @@ def test_gemm_silu(gpu, M):
 
 @pytest.mark.parametrize("M", [1, 9, 20, 32, 48, 64])
 @pytest.mark.parametrize("epi", ["bf16", "f32", "silu"])
-@pytest.mark.parametrize("nb,waves,div", [(2, 4, 4), (4, 8, 2), (1, 4, 1)])
+@pytest.mark.parametrize("nb,waves,div", [(2, 4, 4), (4, 8, 2), (1, 4, 1), (6, 4, 2), (8, 4, 1)])
 def test_gemm_xfrag(gpu, M, epi, nb, waves, div):
-    """Fragment-major activations (ops.to_xfrag) through every epilogue and tuning knob vs fp32."""
+    """Fragment-major activations (ops.to_xfrag) through every epilogue and tuning knob vs fp32
+    (nb 6 / 8: wide n-groups, one activation fragment per 6 / 8 weight fragments)."""
     if epi == "silu" and nb == 1:
         pytest.skip("silu needs nb >= 2")
-    N, K = 1024, 2048
+    N, K = (1536 if nb >= 6 else 1024), 2048
     torch.manual_seed(M * 3 + nb)
     x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
     if epi == "silu":
