@@ -534,7 +534,7 @@ static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uin
     launch_skinny_t<MTV, NBV, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);               \
     return;                                                                                      \
   }
-  LSA_SK(1, 2) LSA_SK(1, 4) LSA_SK(2, 2) LSA_SK(2, 4) LSA_SK(4, 2) LSA_SK(2, 6) LSA_SK(2, 8)
+  LSA_SK(1, 2) LSA_SK(1, 4) LSA_SK(2, 2) LSA_SK(2, 4) LSA_SK(4, 2) LSA_SK(2, 6) LSA_SK(2, 8) LSA_SK(1, 8)
   if constexpr (EPI != EPI_SILU) { LSA_SK(1, 1) LSA_SK(2, 1) LSA_SK(4, 1) }
 #undef LSA_SK
   // fallback (nb=4 with mt=4 or unsupported): nb=2 at the same row-tile count

@@ -292,8 +292,12 @@ static void launch_t(const uint16_t* X, int ldx, int M, int KB64, const uint4* W
   // bf16 sweeps: each fp8 fragment feeds twice the MFMA work of a bf16 one)
   constexpr int U = (4 / NB) < 1 ? 1 : (4 / NB);
   const int kbps = (KB64 + splitk - 1) / splitk;
-  if constexpr (EPI == EPI_BF16) {  // not on the decode hot path: one configuration
-    launch_tx<MT, NB, EPI, 4, U>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, kbps, splitk, s);
+  if constexpr (EPI == EPI_BF16 || NB >= 6) {
+    // bf16 out: not on the decode hot path, one configuration.  Wide n-groups (NB 6 / 8: one pair of
+    // activation fragments feeds 6-8 weight fragments, the activation traffic is 2 * MT / NB of the weight
+    // bytes): 4 waves only (the reduction buffer is WAVES * NB * MT KiB), depth 1 | 2
+    if (EPI != EPI_BF16 && g_fp8_depth == 2) launch_tx<MT, NB, EPI, 4, 2 * U>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, kbps, splitk, s);
+    else launch_tx<MT, NB, EPI, 4, U>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, kbps, splitk, s);
   } else {
     if (g_fp8_waves == 8) {
       if (g_fp8_depth == 2) launch_tx<MT, NB, EPI, 8, 2 * U>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, kbps, splitk, s);
@@ -314,7 +318,7 @@ static void launch_e(const uint16_t* X, int ldx, int M, int KB64, const uint4* W
     launch_t<MTV, NBV, EPI>(X, ldx, M, KB64, Wq, sc, NBtot, out, ldo, splitk, s); \
     return;                                                                    \
   }
-  LSA_F8(1, 2) LSA_F8(1, 4) LSA_F8(2, 2) LSA_F8(2, 4) LSA_F8(4, 2)
+  LSA_F8(1, 2) LSA_F8(1, 4) LSA_F8(2, 2) LSA_F8(2, 4) LSA_F8(4, 2) LSA_F8(2, 6) LSA_F8(2, 8) LSA_F8(1, 8)
   if constexpr (EPI != EPI_SILU) { LSA_F8(1, 1) LSA_F8(2, 1) LSA_F8(4, 1) }
 #undef LSA_F8
   // fallback (unsupported nb): nb = 2 at the same row-tile count

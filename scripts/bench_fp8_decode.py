@@ -48,7 +48,7 @@ for name, (N, K, epi) in SHAPES.items():
         xin = ops.to_xfrag(x) if xf else x
         h = torch.randn(M, N, device=dev)
         xout = torch.zeros(ops.xfrag_tiles(M) * 16 * N if xf else M * N, device=dev, dtype=torch.bfloat16)
-        ss = torch.zeros(M, device=dev)
+        ss = torch.zeros(M, device=dev, dtype=torch.int64)  # Q24 row sums of squares
         tk = torch.zeros(N // 16, device=dev, dtype=torch.int32)
 
         def call(cfg):
@@ -71,8 +71,10 @@ for name, (N, K, epi) in SHAPES.items():
         best = None
         for waves in (4, 8):
             for depth in (1, 2):
-                for nb in (1, 2, 4):
-                    if (N // 16) % nb or (epi == "silu" and nb == 1) or (M > 32 and nb > 2):
+                for nb in (1, 2, 4, 6, 8):
+                    if (N // 16) % nb or (epi == "silu" and nb % 2) or (M > 32 and nb > 2):
+                        continue
+                    if nb >= 6 and (waves != 4 or (nb == 6 and not 16 < M <= 32)):  # wide n-groups: 4 waves
                         continue
                     for sk in ((1, 2, 4, 8) if epi != "silu" else (1,)):
                         if K // 64 // sk < 4:

@@ -62,7 +62,7 @@ for name, (N, K, epi) in SHAPES.items():
         best = None
         for waves, dv in (((4, 1), (4, 2), (4, 4), (8, 2)) if KIND == "bf16" else ((4, 4),)):
             for nb in NBS:
-                if (N // 16) % nb or (epi == "silu" and nb % 2) or (M > 32 and nb > 2):
+                if (N // 16) % nb or (epi == "silu" and nb % 2) or (M > 32 and nb > 2) or (nb == 6 and M <= 16):
                     continue
                 if nb >= 6 and (waves, dv) not in ((4, 1), (4, 2)):  # wide n-groups: 4 waves, div 1 | 2 only
                     continue

@@ -77,14 +77,16 @@ for name, (N, K) in ROWP.items():
                "res_same_cfg_us": round(timeit(lambda i: lin(af, ws[i % ncopy], "res", out=parts, splitk=sk0,
                                                              res=(h, xo, ss, tk))), 2)}
         best = None
-        for nb in (1, 2, 4):
-            if M > 32 and nb > 2:
+        for nb in (1, 2, 4, 6, 8):
+            if (M > 32 and nb > 2) or (N // 16) % nb or (nb == 6 and not 16 < M <= 32):
                 continue
             for sk in (1, 2, 4, 8):
                 if K // 32 // sk < 8:
                     continue
                 pb = torch.empty(sk, M, N, device=dev)
                 for waves, dv in (((4, 1), (4, 2), (4, 4), (8, 2)) if KIND == "bf16" else ((4, 4),)):
+                    if nb >= 6 and (KIND != "bf16" or (waves, dv) not in ((4, 1), (4, 2))):
+                        continue
                     us = timeit(lambda i: lin(af, ws[i % ncopy], "res", out=pb, splitk=sk, res=(h, xo, ss, tk),
                                               nb=nb, waves=waves, div=dv))
                     if best is None or us < best[1]:

@@ -88,6 +88,20 @@ def test_gemm_xfrag(gpu, M, epi, nb, waves, div):
     assert _rel(y, yr) < (1e-4 if epi == "f32" else 1e-2)
 
 
+@pytest.mark.parametrize("M", [1, 9, 16, 30])
+@pytest.mark.parametrize("nb", [6, 8])
+def test_gemm_wide_nb_rowmajor(gpu, M, nb):
+    """Wide n-groups with row-major activations (the batch <= 16 decode layout) vs fp32."""
+    N, K = 1536, 2048
+    torch.manual_seed(M + nb)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    for div in (1, 2):
+        y = ops.linear(x, pw, "f32", splitk=2, nb=nb, waves=4, div=div)
+        assert _rel(y.sum(0), x.float() @ w.float().t()) < 1e-4
+
+
 @pytest.mark.parametrize("M", [17, 32, 48, 64])
 @pytest.mark.parametrize("splitk", [1, 4, 8])
 def test_gemm_xlds_f32(gpu, M, splitk):
@@ -208,6 +222,32 @@ def test_fp8_gemm(gpu, M, epi):
         elif epi == "silu":
             yx = ops.from_xfrag(yx, M, N // 2)
         assert _rel(yx, yr) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 9, 20, 32])
+@pytest.mark.parametrize("epi", ["f32", "silu"])
+@pytest.mark.parametrize("nb,depth", [(6, 1), (8, 2), (8, 1)])
+def test_fp8_gemm_wide_nb(gpu, M, epi, nb, depth):
+    """W8A16 decode GEMM with wide n-groups (row-major and fragment-major activations) vs fp32."""
+    if nb == 6 and M <= 16:
+        pytest.skip("nb 6 is instantiated for the 17..32-row tile only")
+    N, K = 1536, 4096
+    torch.manual_seed(M + nb)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w if epi == "f32" else ops.interleave_gate_up(w[: N // 2], w[N // 2:]), "fp8")
+    wd = ops.dequantize_fp8(pw.data, pw.scale, N, K)
+    yr = ref.linear(x, wd, epi)
+    xf = 16 < M
+    xin = ops.to_xfrag(x) if xf else x
+    sk = 2 if epi == "f32" else 1
+    kw = dict(splitk=sk, nb=nb, waves=4, div=2 if depth == 2 else 4)
+    y = ops.linear_xf(xin, M, pw, epi, **kw) if xf else ops.linear(xin, pw, epi, **kw)
+    if epi == "f32":
+        y = y.sum(0)
+    elif xf:
+        y = ops.from_xfrag(y, M, N // 2)
+    assert _rel(y, yr) < 1e-2
 
 
 # ----------------------------------------------------------------------------------------- norm / rope
