@@ -49,7 +49,7 @@ int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int 
 void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                        const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
-                       void* out, hipStream_t s);
+                       void* out, int ng, hipStream_t s);
 int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
 int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
                       void* out, int epi, int splitk, hipStream_t stream);
@@ -327,9 +327,12 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& v
   need(q, at::kBFloat16, "q");
   need(work, at::kInt, "work");
   if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip)
+    // work [n_workgroups, 2 * NG]: NG (seq, q_start) items per workgroup (ops.prefill_work pairs them)
+    TORCH_CHECK(work.dim() == 2 && (work.size(1) == 2 || work.size(1) == 4) && work.is_contiguous(),
+                "attn_prefill32 work must be [n, 2] or [n, 4] int32");
     check(lsa_attn_prefill32(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                              block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
-                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), cur_stream()),
+                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 2), cur_stream()),
           "attn_prefill32");
     return;
   }

@@ -267,12 +267,12 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
 #pragma unroll
       for (int u = 1; u < TU; ++u) mx = fmaxf(mx, s[u][g]);
       const float mn = fmaxf(m[g], mx);
-      const float alpha = exp2f(m[g] - mn);
+      const float alpha = __builtin_amdgcn_exp2f(m[g] - mn);
       m[g] = mn;
       float p[TU], ps = 0.f;
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
-        p[u] = exp2f(s[u][g] - mn);
+        p[u] = __builtin_amdgcn_exp2f(s[u][g] - mn);
         ps += p[u];
       }
       l[g] = l[g] * alpha + ps;
@@ -322,7 +322,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   for (int g = 0; g < G; ++g) {
     float mo = fmaxf(m[g], __shfl_xor(m[g], 16, 64));
     mo = fmaxf(mo, __shfl_xor(mo, 32, 64));
-    const float a = exp2f(m[g] - mo);
+    const float a = __builtin_amdgcn_exp2f(m[g] - mo);
     l[g] *= a;
     l[g] += __shfl_xor(l[g], 16, 64);
     l[g] += __shfl_xor(l[g], 32, 64);
@@ -360,7 +360,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < WV; ++k) {
-      const float wgt = exp2f(sm[k][g] - M);
+      const float wgt = __builtin_amdgcn_exp2f(sm[k][g] - M);
       L += sl[k][g] * wgt;
       const float4 v = *reinterpret_cast<const float4*>(&so[k][g][d0]);
       O[0] += v.x * wgt; O[1] += v.y * wgt; O[2] += v.z * wgt; O[3] += v.w * wgt;
@@ -417,7 +417,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     const size_t pi0 = ((size_t)b * H + hk * G + g) * nsplit;
 #pragma unroll 4
     for (int sp = 0; sp < nse; ++sp) {
-      const float wgt = exp2f(cm[g * 256 + sp] - M);
+      const float wgt = __builtin_amdgcn_exp2f(cm[g * 256 + sp] - M);
       L += cl[g * 256 + sp] * wgt;
       const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs_o, (int)(((pi0 + sp) * D + d0) * 4), 0, LSA_SC1);
       O[0] += __uint_as_float(v[0]) * wgt; O[1] += __uint_as_float(v[1]) * wgt;
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mnew = fmaxf(mrow[gi], tmax);
-      const float alpha = exp2f(mrow[gi] - mnew);
+      const float alpha = __builtin_amdgcn_exp2f(mrow[gi] - mnew);
       mrow[gi] = mnew;
       float psum = 0.f;
       uint32_t pk[4][2];
@@ -607,7 +607,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
         float p[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          p[i] = exp2f(st[gi][kt][i] - mnew);
+          p[i] = __builtin_amdgcn_exp2f(st[gi][kt][i] - mnew);
           psum += p[i];
         }
         pk[kt][0] = pack2bf(p[0], p[1]);

@@ -44,73 +44,100 @@ __device__ __forceinline__ int vp_off(int r, int col) { return r * 128 + ((((col
 
 }  // namespace
 
-__global__ __launch_bounds__(256, 2) void attn_prefill32_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-                                                                const uint16_t* __restrict__ vc,
-                                                                const int* __restrict__ block_tables, int max_blocks,
-                                                                const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
-                                                                const int* __restrict__ work, int H, int Hkv,
-                                                                float scale_log2, uint16_t* __restrict__ out) {
+// NG independent 4-wave groups per workgroup (NG = 2: the host pairs a heavy causal query block with a
+// light one, ops.prefill_work, so every workgroup streams about the same number of key tiles; one pair
+// per CU instead of two heavy blocks landing on the same CU).  Each group has its own K / V image and its
+// own tile count; the groups only share the workgroup barriers (an idle group keeps passing them).
+//
+// O is accumulated TRANSPOSED, O^T += V^T P^T (A = V^T from the transposed LDS reads, B = P^T straight
+// from the S^T accumulator): the accumulator's column is then the query row = the lane, so the online-
+// softmax rescale and the final 1 / l are lane-local multiplies (no cross-lane shuffles), and each lane
+// stores 4 contiguous dims of its own row per register group.
+template <int NG>
+__global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                                                                     const uint16_t* __restrict__ vc,
+                                                                     const int* __restrict__ block_tables, int max_blocks,
+                                                                     const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
+                                                                     const int* __restrict__ work, int H, int Hkv,
+                                                                     float scale_log2, uint16_t* __restrict__ out) {
   constexpr int D = 128;
-  constexpr int QB = 128;  // query rows per workgroup
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[64 * D];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[64 * D];
+  constexpr int QB = 128;  // query rows per group
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[NG][64 * D];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[NG][64 * D];
   const int wi = blockIdx.x, h = blockIdx.y;
-  const int seq = work[2 * wi], qs = work[2 * wi + 1];
-  const int hk = h / (H / Hkv);
-  const int q0 = cu_q[seq], qlen = cu_q[seq + 1] - q0;
-  const int ctx = ctx_lens[seq];
-  const int pos0 = ctx - qlen;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3;
+  const int gi = NG == 1 ? 0 : (tid >> 8), gtid = tid & 255;
   const int r32 = lane & 31, hh = lane >> 5;
+  const int hk = h / (H / Hkv);
 
-  // Q^T fragments (B operand): lane (r, h) holds Q[row r][16 s + 8 h .. + 7] for the 8 k-steps of 16 dims
+  // tiles of every group (the loop runs to the largest; the barriers are workgroup-wide)
+  int nt_max = 0, ntiles = 0, seq = 0, qs = 0;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int sq = work[2 * (NG * wi + g)], qq0 = work[2 * (NG * wi + g) + 1];
+    int nt = 0;
+    if (sq >= 0) {
+      const int ql = cu_q[sq + 1] - cu_q[sq];
+      const int cx = ctx_lens[sq];
+      const int lr = min(qq0 + QB - 1, ql - 1);
+      nt = (min(cx, cx - ql + lr + 1) + 63) >> 6;
+    }
+    nt_max = max(nt_max, nt);
+    if (g == gi) { ntiles = nt; seq = sq; qs = qq0; }
+  }
+  const bool active = seq >= 0;
+  const int sqc = active ? seq : 0;
+  const int q0 = cu_q[sqc], qlen = cu_q[sqc + 1] - q0;
+  const int ctx = ctx_lens[sqc];
+  const int pos0 = ctx - qlen;
+
+  // Q^T fragments (B operand of S^T): lane (r, h) holds Q[row r][16 s + 8 h .. + 7] for the 8 k-steps
   const int qrow = qs + w * 32 + r32;
   const int qpos = pos0 + qrow;
   uint4 qf[8];
   {
-    const uint16_t* qp = q + ((size_t)(q0 + min(qrow, qlen - 1)) * H + h) * D + 8 * hh;
+    const uint16_t* qp = q + ((size_t)(q0 + max(0, min(qrow, qlen - 1))) * H + h) * D + 8 * hh;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const uint4*>(qp + 16 * s);
+    for (int s2 = 0; s2 < 8; ++s2) qf[s2] = *reinterpret_cast<const uint4*>(qp + 16 * s2);
   }
-  const int last_row = min(qs + QB - 1, qlen - 1);
-  const int kv_end = min(ctx, pos0 + last_row + 1);
-  const int ntiles = (kv_end + 63) >> 6;
   // keys a wave's rows can see (causal): tiles past the wave's last row are skipped by that wave
   const int wave_last = min(qs + w * 32 + 31, qlen - 1);
-  const int wave_tiles = (min(ctx, pos0 + wave_last + 1) + 63) >> 6;
+  const int wave_tiles = (active && qs + w * 32 < qlen) ? (min(ctx, pos0 + wave_last + 1) + 63) >> 6 : 0;
 
-  f32x16_t o[4];
+  f32x16_t o[4];  // O^T: register i of o[db] = dim 32 db + (i & 3) + 8 (i >> 2) + 4 hh of query row r32
 #pragma unroll
   for (int db = 0; db < 4; ++db) o[db] = f32x16_t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float mrow = LSA_NEG_P, lrow = 0.f;  // of query row r32 (identical in both lane halves)
 
-  const int* bt = block_tables + (size_t)seq * max_blocks;
+  const int* bt = block_tables + (size_t)sqc * max_blocks;
+  uint16_t* Kg = Ks[gi];
+  uint16_t* Vg = Vs[gi];
   uint4 kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3;
 #define LSA_P32_FETCH(T)                                                                 \
   {                                                                                      \
     const size_t base_ = ((size_t)bt[(T)] * Hkv + hk) * 64 * D;                          \
-    const uint4* kb_ = reinterpret_cast<const uint4*>(kc + base_) + tid;                 \
-    const uint4* vb_ = reinterpret_cast<const uint4*>(vc + base_) + tid;                 \
+    const uint4* kb_ = reinterpret_cast<const uint4*>(kc + base_) + gtid;                \
+    const uint4* vb_ = reinterpret_cast<const uint4*>(vc + base_) + gtid;                \
     kr0 = kb_[0]; kr1 = kb_[256]; kr2 = kb_[512]; kr3 = kb_[768];                        \
     vr0 = vb_[0]; vr1 = vb_[256]; vr2 = vb_[512]; vr3 = vb_[768];                        \
   }
-  LSA_P32_FETCH(0);
+  if (ntiles > 0) LSA_P32_FETCH(0);
   const int G16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-  for (int t = 0; t < ntiles; ++t) {
+  for (int t = 0; t < nt_max; ++t) {
     __syncthreads();
-    {
-      const int row = tid >> 4, ch = tid & 15;  // 16 B chunk c = tid + 256 i -> row + 16 i, chunk ch
-      *reinterpret_cast<uint4*>(&Ks[kp_off(row, ch)]) = kr0;
-      *reinterpret_cast<uint4*>(&Ks[kp_off(row + 16, ch)]) = kr1;
-      *reinterpret_cast<uint4*>(&Ks[kp_off(row + 32, ch)]) = kr2;
-      *reinterpret_cast<uint4*>(&Ks[kp_off(row + 48, ch)]) = kr3;
-      *reinterpret_cast<uint4*>(&Vs[vp_off(row, ch * 8)]) = vr0;
-      *reinterpret_cast<uint4*>(&Vs[vp_off(row + 16, ch * 8)]) = vr1;
-      *reinterpret_cast<uint4*>(&Vs[vp_off(row + 32, ch * 8)]) = vr2;
-      *reinterpret_cast<uint4*>(&Vs[vp_off(row + 48, ch * 8)]) = vr3;
+    if (t < ntiles) {
+      const int row = gtid >> 4, ch = gtid & 15;  // 16 B chunk c = gtid + 256 i -> row + 16 i, chunk ch
+      *reinterpret_cast<uint4*>(&Kg[kp_off(row, ch)]) = kr0;
+      *reinterpret_cast<uint4*>(&Kg[kp_off(row + 16, ch)]) = kr1;
+      *reinterpret_cast<uint4*>(&Kg[kp_off(row + 32, ch)]) = kr2;
+      *reinterpret_cast<uint4*>(&Kg[kp_off(row + 48, ch)]) = kr3;
+      *reinterpret_cast<uint4*>(&Vg[vp_off(row, ch * 8)]) = vr0;
+      *reinterpret_cast<uint4*>(&Vg[vp_off(row + 16, ch * 8)]) = vr1;
+      *reinterpret_cast<uint4*>(&Vg[vp_off(row + 32, ch * 8)]) = vr2;
+      *reinterpret_cast<uint4*>(&Vg[vp_off(row + 48, ch * 8)]) = vr3;
     }
     __syncthreads();
-    LSA_P32_FETCH(min(t + 1, ntiles - 1));
+    if (t + 1 < ntiles) LSA_P32_FETCH(t + 1);
     if (t >= wave_tiles) continue;  // causal: nothing this wave's rows can see (barriers stay uniform)
 
     // S^T for the two 32-key halves
@@ -119,26 +146,35 @@ __global__ __launch_bounds__(256, 2) void attn_prefill32_kernel(const uint16_t* 
     for (int kh = 0; kh < 2; ++kh) {
       st[kh] = f32x16_t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const uint4 a = *reinterpret_cast<const uint4*>(&Ks[kp_off(32 * kh + r32, 2 * s + hh)]);
-        st[kh] = mfma32x32x16(a, qf[s], st[kh]);
+      for (int s2 = 0; s2 < 8; ++s2) {
+        const uint4 a = *reinterpret_cast<const uint4*>(&Kg[kp_off(32 * kh + r32, 2 * s2 + hh)]);
+        st[kh] = mfma32x32x16(a, qf[s2], st[kh]);
       }
     }
     // mask + online softmax; register i of half kh holds key t*64 + 32 kh + (i & 3) + 8 (i >> 2) + 4 hh
     float tmax = LSA_NEG_P;
 #pragma unroll
+    for (int kh = 0; kh < 2; ++kh) st[kh] *= scale_log2;
+    // causal / context mask, only on the tiles that cross this wave's diagonal or the context end (one
+    // wave-uniform branch per tile; inside it branch-free selects -- a short-circuit per element made
+    // hipcc emit 64 exec-mask branches per tile)
+    if (t * 64 + 63 > min(pos0 + qs + w * 32, ctx - 1)) {
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = t * 64 + 32 * kh + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          const bool ok = (key <= qpos) & (key < ctx);
+          st[kh][i] = ok ? st[kh][i] : LSA_NEG_P;
+        }
+    }
+#pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = t * 64 + 32 * kh + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        float v = st[kh][i] * scale_log2;
-        v = (key > qpos || key >= ctx) ? LSA_NEG_P : v;
-        st[kh][i] = v;
-        tmax = fmaxf(tmax, v);
-      }
+      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[kh][i]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(mrow, tmax);
-    const float alpha = exp2f(mrow - mnew);
+    const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
     mrow = mnew;
     float psum = 0.f;
     uint4 pa[2][2];  // [kh][k-step s']: registers 8 s' .. 8 s' + 7 of half kh as bf16
@@ -147,7 +183,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill32_kernel(const uint16_t* 
       float p[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        p[i] = exp2f(st[kh][i] - mnew);
+        p[i] = __builtin_amdgcn_exp2f(st[kh][i] - mnew);
         psum += p[i];
       }
 #pragma unroll
@@ -160,14 +196,9 @@ __global__ __launch_bounds__(256, 2) void attn_prefill32_kernel(const uint16_t* 
     }
     psum += __shfl_xor(psum, 32, 64);
     lrow = lrow * alpha + psum;
-    // rescale O: register i of o[db] is query row (i & 3) + 8 (i >> 2) + 4 hh (alpha lives on lane = row)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float ai = __shfl(alpha, (i & 3) + 8 * (i >> 2) + 4 * hh, 64);
-#pragma unroll
-      for (int db = 0; db < 4; ++db) o[db][i] *= ai;
-    }
-    // O += P V: k-step (kh, s') covers keys 32 kh + 16 s' + 8 (j >> 2) + 4 hh + (j & 3) in element j
+    for (int db = 0; db < 4; ++db) o[db] *= alpha;  // lane-local: the accumulator column is this lane's row
+    // O^T += V^T P^T: k-step (kh, s') covers keys 32 kh + 16 s' + 8 (j >> 2) + 4 hh + (j & 3) in element j
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
@@ -176,39 +207,47 @@ __global__ __launch_bounds__(256, 2) void attn_prefill32_kernel(const uint16_t* 
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
           const int col = 32 * db + 16 * (G16 & 1) + 4 * pp;
-          const uint2 v1 = ds_read_tr16p(&Vs[vp_off(r0, col)]);
-          const uint2 v2 = ds_read_tr16p(&Vs[vp_off(r0 + 8, col)]);
-          uint4 vb;
-          vb.x = v1.x; vb.y = v1.y; vb.z = v2.x; vb.w = v2.y;
-          o[db] = mfma32x32x16(pa[kh][s2], vb, o[db]);
+          const uint2 v1 = ds_read_tr16p(&Vg[vp_off(r0, col)]);
+          const uint2 v2 = ds_read_tr16p(&Vg[vp_off(r0 + 8, col)]);
+          uint4 va;
+          va.x = v1.x; va.y = v1.y; va.z = v2.x; va.w = v2.y;
+          o[db] = mfma32x32x16(va, pa[kh][s2], o[db]);
         }
       }
   }
 #undef LSA_P32_FETCH
-  // normalise and store: register i of o[db] = O[row (i & 3) + 8 (i >> 2) + 4 hh][dim 32 db + r32]
+  // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
+  const int qr = qs + w * 32 + r32;
+  if (active && qr < qlen) {
+    const float inv = lrow > 0.f ? 1.f / lrow : 0.f;
+    uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D + 4 * hh;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int rr = (i & 3) + 8 * (i >> 2) + 4 * hh;
-    const float li = __shfl(lrow, rr, 64);
-    const float inv = li > 0.f ? 1.f / li : 0.f;
-    const int qr = qs + w * 32 + rr;
-    if (qr < qlen) {
-      uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D;
+    for (int db = 0; db < 4; ++db)
 #pragma unroll
-      for (int db = 0; db < 4; ++db) orow[32 * db + r32] = f2bf(o[db][i] * inv);
-    }
+      for (int gq = 0; gq < 4; ++gq) {
+        uint2 pk;
+        pk.x = pack2bf(o[db][4 * gq + 0] * inv, o[db][4 * gq + 1] * inv);
+        pk.y = pack2bf(o[db][4 * gq + 2] * inv, o[db][4 * gq + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + 32 * db + 8 * gq) = pk;
+      }
   }
 }
 
+// work: NG (seq, q_start) pairs per workgroup (seq < 0: that group idles), nwork workgroups
 extern "C" int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                   const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv,
-                                  float scale, void* out, hipStream_t s) {
+                                  float scale, void* out, int ng, hipStream_t s) {
   if (nwork <= 0) return 0;
   if (H % Hkv) return -1;
   dim3 grid(nwork, H);
-  hipLaunchKernelGGL(attn_prefill32_kernel, grid, dim3(256), 0, s, reinterpret_cast<const uint16_t*>(q),
-                     reinterpret_cast<const uint16_t*>(kc), reinterpret_cast<const uint16_t*>(vc), block_tables,
-                     max_blocks, cu_q, ctx_lens, work, H, Hkv, scale * 1.4426950408889634f,
-                     reinterpret_cast<uint16_t*>(out));
+  const float sl2 = scale * 1.4426950408889634f;
+#define LSA_P32_LAUNCH(NGV)                                                                                      \
+  hipLaunchKernelGGL(attn_prefill32_kernel<NGV>, grid, dim3(256 * NGV), 0, s, reinterpret_cast<const uint16_t*>(q), \
+                     reinterpret_cast<const uint16_t*>(kc), reinterpret_cast<const uint16_t*>(vc), block_tables,  \
+                     max_blocks, cu_q, ctx_lens, work, H, Hkv, sl2, reinterpret_cast<uint16_t*>(out))
+  if (ng == 2) LSA_P32_LAUNCH(2);
+  else if (ng == 1) LSA_P32_LAUNCH(1);
+  else return -2;
+#undef LSA_P32_LAUNCH
   return (int)hipGetLastError();
 }

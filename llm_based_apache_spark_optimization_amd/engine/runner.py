@@ -485,7 +485,7 @@ class ModelRunner:
         work = None
         self._cu_host = cu  # host offsets: the prefill attention kernel choice (ops._prefill_kernel)
         if self.on_gpu:
-            work = torch.tensor(ops.prefill_work(cu), dtype=torch.int32).to(dev, non_blocking=True)
+            work = torch.tensor(ops.prefill_work(cu, ctx=ctx, heads=self.H), dtype=torch.int32).to(dev, non_blocking=True)
 
         tps = self.tp.size if self.tp is not None else 1
         if self.seq_parallel and tps > 1 and T >= self.sp_min_tokens:

@@ -602,18 +602,53 @@ def prefill_qblock(cu_q: Optional[list] = None) -> int:
     return 128 if k == "32" else ext().prefill_qblock
 
 
-def prefill_work(cu_q: list[int], qblock: Optional[int] = None) -> list[tuple[int, int]]:
-    """(seq, q_start) work items of the prefill attention kernel's query block (``prefill_qblock()``
-    rows), heaviest (latest) query blocks first for causal balance."""
+def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[list[int]] = None,
+                 kernel: Optional[str] = None, heads: int = 32) -> list[tuple]:
+    """Work items of the prefill attention kernel for packed sequences (cu_q offsets; ``ctx`` = per-sequence
+    context length after this prefill, default = the chunk length, i.e. no cached prefix).
+
+    16-row kernel: (seq, q_start) per workgroup, heaviest (latest) query blocks first.
+    32-row kernel ('32'): (seq_a, q_a, seq_b, q_b) per workgroup -- two 128-row query blocks run side by
+    side as independent 4-wave groups, the k-th most expensive block (keys it attends to) with the k-th
+    cheapest, so under the causal mask every workgroup streams about the same number of key tiles
+    (seq_b = -1: the second group idles).  Otherwise (``_pair_blocks``) the items stay single: (seq, q_start)
+    per 4-wave workgroup, heaviest first."""
+    kernel = kernel or _prefill_kernel(cu_q)
     if qblock is None:
-        qblock = prefill_qblock(cu_q)
+        qblock = 128 if kernel == "32" else ext().prefill_qblock
     items = []
     for s in range(len(cu_q) - 1):
         ql = cu_q[s + 1] - cu_q[s]
+        pos0 = (ctx[s] - ql) if ctx is not None else 0
         for qs in range(0, ql, qblock):
-            items.append((s, qs))
-    items.sort(key=lambda t: -t[1])
-    return items
+            items.append((pos0 + min(qs + qblock, ql), s, qs))
+    items.sort(key=lambda t: -t[0])
+    if kernel != "32":
+        return [(s, qs) for _, s, qs in items]
+    n = len(items)
+    if not _pair_blocks(n, heads, max(cu_q[i + 1] - cu_q[i] for i in range(len(cu_q) - 1)), qblock):
+        return [(s, qs) for _, s, qs in items]
+    out = []
+    for i in range((n + 1) // 2):
+        j = n - 1 - i
+        b = (items[j][1], items[j][2]) if j > i else (-1, 0)
+        out.append((items[i][1], items[i][2]) + b)
+    return out
+
+
+# LSA_PREFILL_PAIR: auto | 1 | 0 -- heavy/light paired query blocks in the 32-row prefill kernel
+PREFILL_PAIR = os.environ.get("LSA_PREFILL_PAIR", "auto")
+
+
+def _pair_blocks(n_items: int, heads: int, longest: int, qblock: int) -> bool:
+    """Pair when every single block would be resident at once (<= 2 per CU on 256 CUs: the dispatch order
+    then fixes which blocks share a CU, and heavy ones can land together) or for very long sequences; with
+    more blocks than slots the hardware's dynamic dispatch balances them better (scripts/bench_attn_prefill.py,
+    profiles/attn_prefill_pairing_mi355x.jsonl: 7B 2k 103 -> 89 us paired, 3B 2k 97 -> 84, 3B 8k 730 -> 695;
+    4 x 1k 3B single 83 vs paired 90)."""
+    if PREFILL_PAIR != "auto":
+        return PREFILL_PAIR == "1"
+    return n_items * heads <= 512 or longest >= 32 * qblock
 
 
 def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, work=None, cu_list=None):
@@ -623,7 +658,7 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, wo
         return ref.attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out)
     cu = cu_list if cu_list is not None else cu_q.tolist()
     if work is None:
-        work = torch.tensor(prefill_work(cu), dtype=torch.int32).to(q.device)
+        work = torch.tensor(prefill_work(cu, ctx=ctx_lens.tolist(), heads=H), dtype=torch.int32).to(q.device)
     ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, work, H, Hkv, scale, out,
                        1 if _prefill_kernel(cu) == "32" else 0)
     return out

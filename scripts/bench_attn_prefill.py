@@ -40,7 +40,7 @@ def case(name, nseq, qlen, H, Hkv):
     out = torch.empty_like(q)
     cud = torch.tensor(cu, dtype=torch.int32, device=dev)
     ctx = torch.full((nseq,), qlen, dtype=torch.int32, device=dev)
-    work = torch.tensor(ops.prefill_work(cu), dtype=torch.int32, device=dev)
+    work = torch.tensor(ops.prefill_work(cu, heads=H), dtype=torch.int32, device=dev)
     us = timeit(lambda: ops.attn_prefill(q, kc, vc, bt, cud, ctx, H, Hkv, 1 / math.sqrt(128), out, work=work))
     flops = nseq * 4 * H * 128 * qlen * (qlen + 1) / 2  # causal QK^T + PV
     # numerics spot check vs torch SDPA on one sequence
@@ -49,11 +49,12 @@ def case(name, nseq, qlen, H, Hkv):
     vv = vc[bt[0].long()].transpose(0, 1).reshape(Hkv, -1, 128)[:, :qlen].float().repeat_interleave(H // Hkv, 0)
     ref = torch.nn.functional.scaled_dot_product_attention(s0, kk, vv, is_causal=True).transpose(0, 1)
     err = (out[:qlen].float() - ref).abs().max().item()
-    print(json.dumps({"case": name, "us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1), "max_err": round(err, 4)}),
-          flush=True)
+    print(json.dumps({"case": name, "kernel": ops._prefill_kernel(cu), "work": list(work.shape),
+                      "us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1), "max_err": round(err, 4)}), flush=True)
 
 
 case("3b_explain_2k", 1, 2048, 24, 8)
 case("7b_b1_2k", 1, 2048, 32, 32)
 case("7b_b32_128", 32, 128, 32, 32)
 case("3b_8k", 1, 8192, 24, 8)
+case("3b_b4_1k", 4, 1024, 24, 8)

@@ -406,13 +406,15 @@ def test_attn_decode_fused_rope(gpu, HH, lens, nparts):
     assert _rel(o2, o1) < 1e-2
 
 
-@pytest.mark.parametrize("kernel", ["16", "32"])
+@pytest.mark.parametrize("kernel", ["16", "32", "32pair"])
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
 @pytest.mark.parametrize("case", ["fresh", "chunked", "long"])
 def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
-    """Both prefill attention kernels (16 x 16 MFMA, 64 rows per workgroup; 32 x 32 MFMA, 128 rows) vs the
-    fp32 reference: packed variable-length sequences, chunked continuation, multi-block causal tiles."""
-    monkeypatch.setattr(ops, "PREFILL_ATTN", kernel)
+    """Both prefill attention kernels (16 x 16 MFMA, 64 rows per workgroup; 32 x 32 MFMA, 128 rows, single
+    or heavy/light paired query blocks per workgroup) vs the fp32 reference: packed variable-length
+    sequences, chunked continuation, multi-block causal tiles."""
+    monkeypatch.setattr(ops, "PREFILL_ATTN", kernel[:2])
+    monkeypatch.setattr(ops, "PREFILL_PAIR", "1" if kernel == "32pair" else "0")
     H, Hkv = HH
     D = 128
     if case == "fresh":
@@ -434,10 +436,11 @@ def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
     assert _rel(out, out2) < 1e-2
 
 
-@pytest.mark.parametrize("kernel", ["16", "32"])
+@pytest.mark.parametrize("kernel", ["16", "32", "32pair"])
 def test_attn_prefill_spike(gpu, kernel, monkeypatch):
     """Force the online-softmax rescale branch: one very large score late in the sequence."""
-    monkeypatch.setattr(ops, "PREFILL_ATTN", kernel)
+    monkeypatch.setattr(ops, "PREFILL_ATTN", kernel[:2])
+    monkeypatch.setattr(ops, "PREFILL_PAIR", "1" if kernel == "32pair" else "0")
     H, Hkv, D = 8, 8, 128
     n = 300
     kc, vc, bt = _paged([n], Hkv, D, gpu, seed=9)
