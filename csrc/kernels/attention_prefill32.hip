@@ -22,12 +22,29 @@
 typedef short s16x4p_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4p_t* lds_s4p_ptr;
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_u16_ptr;
 
 namespace {
 
 __device__ __forceinline__ uint2 ds_read_tr16p(const uint16_t* p) {
   s16x4p_t v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4p_ptr)(p));
   return __builtin_bit_cast(uint2, v);
+}
+
+// LDS-DMA of 16 B per lane into [lds_base + 16 * lane] (lds_base wave-uniform, in M0).  Inline asm on purpose:
+// with the builtin, hipcc cannot tell the DMA's destination buffer from the one the MFMAs are reading and
+// puts a vmcnt(0) in front of every LDS read, i.e. it serialises the prefetch with the tile it should hide
+// under.  The kernel counts these loads itself (s_waitcnt before the barrier that publishes a tile).
+__device__ __forceinline__ void dma16(const void* gsrc, unsigned lds_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_base)
+               : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(lds_u16_ptr)(p);
 }
 
 __device__ __forceinline__ f32x16_t mfma32x32x16(const uint4 a, const uint4 b, f32x16_t c) {
@@ -62,8 +79,10 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
                                                                      float scale_log2, uint16_t* __restrict__ out) {
   constexpr int D = 128;
   constexpr int QB = 128;  // query rows per group
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[NG][64 * D];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[NG][64 * D];
+  // K / V tiles, double-buffered per group, filled by LDS-DMA (global_load_lds: no staging registers, and the
+  // DMA of tile t + 1 runs under tile t's MFMAs)
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[NG][2][64 * D];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[NG][2][64 * D];
   const int wi = blockIdx.x, h = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3;
   const int gi = NG == 1 ? 0 : (tid >> 8), gtid = tid & 255;
@@ -110,112 +129,124 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   float mrow = LSA_NEG_P, lrow = 0.f;  // of query row r32 (identical in both lane halves)
 
   const int* bt = block_tables + (size_t)sqc * max_blocks;
-  uint16_t* Kg = Ks[gi];
-  uint16_t* Vg = Vs[gi];
-  uint4 kr0, kr1, kr2, kr3, vr0, vr1, vr2, vr3;
-#define LSA_P32_FETCH(T)                                                                 \
-  {                                                                                      \
-    const size_t base_ = ((size_t)bt[(T)] * Hkv + hk) * 64 * D;                          \
-    const uint4* kb_ = reinterpret_cast<const uint4*>(kc + base_) + gtid;                \
-    const uint4* vb_ = reinterpret_cast<const uint4*>(vc + base_) + gtid;                \
-    kr0 = kb_[0]; kr1 = kb_[256]; kr2 = kb_[512]; kr3 = kb_[768];                        \
-    vr0 = vb_[0]; vr1 = vb_[256]; vr2 = vb_[512]; vr3 = vb_[768];                        \
+  // LDS-DMA of one 64-key tile: 32 wave-instructions of 1 KiB (4 key rows each), 8 per wave of the group.
+  // The DMA writes lane-linearly, so the swizzled images (kp_off / vp_off) are produced by permuting the
+  // SOURCE chunk each lane fetches: lane l of instruction j fills row 4 j + (l >> 4), slot l & 15.
+  const int drow = lane >> 4, dslot = lane & 15;
+  auto dma_tile = [&](int blk, int b) {
+    const size_t base = ((size_t)blk * Hkv + hk) * 64 * D;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = w + 4 * i;
+      const int r = 4 * j + drow;
+      const uint16_t* ksrc = kc + base + r * D + ((dslot ^ (r & 15)) << 3);
+      const uint16_t* vsrc = vc + base + r * D + ((dslot ^ ((r & 3) << 2)) << 3);
+      dma16(ksrc, __builtin_amdgcn_readfirstlane(lds_addr(&Ks[gi][b][4 * j * D])));
+      dma16(vsrc, __builtin_amdgcn_readfirstlane(lds_addr(&Vs[gi][b][4 * j * D])));
+    }
+  };
+  int bnext = 0;  // block of tile t + 1 (loaded one iteration ahead: no dependent load on the DMA path)
+  if (ntiles > 0) {
+    dma_tile(bt[0], 0);
+    if (ntiles > 1) bnext = bt[1];
   }
-  if (ntiles > 0) LSA_P32_FETCH(0);
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): tile 0 has landed
+  __syncthreads();
   const int G16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
   for (int t = 0; t < nt_max; ++t) {
-    __syncthreads();
-    if (t < ntiles) {
-      const int row = gtid >> 4, ch = gtid & 15;  // 16 B chunk c = gtid + 256 i -> row + 16 i, chunk ch
-      *reinterpret_cast<uint4*>(&Kg[kp_off(row, ch)]) = kr0;
-      *reinterpret_cast<uint4*>(&Kg[kp_off(row + 16, ch)]) = kr1;
-      *reinterpret_cast<uint4*>(&Kg[kp_off(row + 32, ch)]) = kr2;
-      *reinterpret_cast<uint4*>(&Kg[kp_off(row + 48, ch)]) = kr3;
-      *reinterpret_cast<uint4*>(&Vg[vp_off(row, ch * 8)]) = vr0;
-      *reinterpret_cast<uint4*>(&Vg[vp_off(row + 16, ch * 8)]) = vr1;
-      *reinterpret_cast<uint4*>(&Vg[vp_off(row + 32, ch * 8)]) = vr2;
-      *reinterpret_cast<uint4*>(&Vg[vp_off(row + 48, ch * 8)]) = vr3;
+    int bnn = 0;
+    if (t + 1 < ntiles) {
+      dma_tile(bnext, (t + 1) & 1);  // its buffer's last readers (tile t - 1) passed the previous barrier
+      if (t + 2 < ntiles) bnn = bt[t + 2];
     }
-    __syncthreads();
-    if (t + 1 < ntiles) LSA_P32_FETCH(t + 1);
-    if (t >= wave_tiles) continue;  // causal: nothing this wave's rows can see (barriers stay uniform)
-
-    // S^T for the two 32-key halves
-    f32x16_t st[2];
+    const uint16_t* Kg = Ks[gi][t & 1];
+    const uint16_t* Vg = Vs[gi][t & 1];
+    if (t < wave_tiles) {  // causal: tiles past the wave's last row are skipped (barriers stay uniform)
+      // S^T for the two 32-key halves
+      f32x16_t st[2];
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      st[kh] = f32x16_t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int kh = 0; kh < 2; ++kh) {
+        st[kh] = f32x16_t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2) {
-        const uint4 a = *reinterpret_cast<const uint4*>(&Kg[kp_off(32 * kh + r32, 2 * s2 + hh)]);
-        st[kh] = mfma32x32x16(a, qf[s2], st[kh]);
+        for (int s2 = 0; s2 < 8; ++s2) {
+          const uint4 a = *reinterpret_cast<const uint4*>(&Kg[kp_off(32 * kh + r32, 2 * s2 + hh)]);
+          st[kh] = mfma32x32x16(a, qf[s2], st[kh]);
+        }
       }
-    }
-    // mask + online softmax; register i of half kh holds key t*64 + 32 kh + (i & 3) + 8 (i >> 2) + 4 hh
-    float tmax = LSA_NEG_P;
+      // mask + online softmax; register i of half kh holds key t*64 + 32 kh + (i & 3) + 8 (i >> 2) + 4 hh
+      float tmax = LSA_NEG_P;
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) st[kh] *= scale_log2;
-    // causal / context mask, only on the tiles that cross this wave's diagonal or the context end (one
-    // wave-uniform branch per tile; inside it branch-free selects -- a short-circuit per element made
-    // hipcc emit 64 exec-mask branches per tile)
-    if (t * 64 + 63 > min(pos0 + qs + w * 32, ctx - 1)) {
+      for (int kh = 0; kh < 2; ++kh) st[kh] *= scale_log2;
+      // causal / context mask, only on the tiles that cross this wave's diagonal or the context end (one
+      // wave-uniform branch per tile; inside it branch-free selects -- a short-circuit per element made
+      // hipcc emit 64 exec-mask branches per tile)
+      if (t * 64 + 63 > min(pos0 + qs + w * 32, ctx - 1)) {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = t * 64 + 32 * kh + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            const bool ok = (key <= qpos) & (key < ctx);
+            st[kh][i] = ok ? st[kh][i] : LSA_NEG_P;
+          }
+      }
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
+        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[kh][i]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      // online softmax; the O / l rescale runs only when some row's max grew (exact: alpha = 1 otherwise),
+      // which under the causal mask is the first few tiles of a row
+      if (__any(tmax > mrow)) {
+        const float mnew = fmaxf(mrow, tmax);
+        const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
+        mrow = mnew;
+        lrow *= alpha;
+  #pragma unroll
+        for (int db = 0; db < 4; ++db) o[db] *= alpha;  // lane-local: the accumulator column is this lane's row
+      }
+      const float mnew = mrow;
+      float psum = 0.f;
+      uint4 pa[2][2];  // [kh][k-step s']: registers 8 s' .. 8 s' + 7 of half kh as bf16
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        float p[16];
+#pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int key = t * 64 + 32 * kh + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          const bool ok = (key <= qpos) & (key < ctx);
-          st[kh][i] = ok ? st[kh][i] : LSA_NEG_P;
+          p[i] = __builtin_amdgcn_exp2f(st[kh][i] - mnew);
+          psum += p[i];
         }
-    }
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[kh][i]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(mrow, tmax);
-    const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
-    mrow = mnew;
-    float psum = 0.f;
-    uint4 pa[2][2];  // [kh][k-step s']: registers 8 s' .. 8 s' + 7 of half kh as bf16
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      float p[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        p[i] = __builtin_amdgcn_exp2f(st[kh][i] - mnew);
-        psum += p[i];
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        pa[kh][s2].x = pack2bf(p[8 * s2 + 0], p[8 * s2 + 1]);
-        pa[kh][s2].y = pack2bf(p[8 * s2 + 2], p[8 * s2 + 3]);
-        pa[kh][s2].z = pack2bf(p[8 * s2 + 4], p[8 * s2 + 5]);
-        pa[kh][s2].w = pack2bf(p[8 * s2 + 6], p[8 * s2 + 7]);
-      }
-    }
-    psum += __shfl_xor(psum, 32, 64);
-    lrow = lrow * alpha + psum;
-#pragma unroll
-    for (int db = 0; db < 4; ++db) o[db] *= alpha;  // lane-local: the accumulator column is this lane's row
-    // O^T += V^T P^T: k-step (kh, s') covers keys 32 kh + 16 s' + 8 (j >> 2) + 4 hh + (j & 3) in element j
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int r0 = 32 * kh + 16 * s2 + 4 * (G16 >> 1) + qq;  // this lane's supplied key row (j < 4)
-#pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const int col = 32 * db + 16 * (G16 & 1) + 4 * pp;
-          const uint2 v1 = ds_read_tr16p(&Vg[vp_off(r0, col)]);
-          const uint2 v2 = ds_read_tr16p(&Vg[vp_off(r0 + 8, col)]);
-          uint4 va;
-          va.x = v1.x; va.y = v1.y; va.z = v2.x; va.w = v2.y;
-          o[db] = mfma32x32x16(va, pa[kh][s2], o[db]);
+        for (int s2 = 0; s2 < 2; ++s2) {
+          pa[kh][s2].x = pack2bf(p[8 * s2 + 0], p[8 * s2 + 1]);
+          pa[kh][s2].y = pack2bf(p[8 * s2 + 2], p[8 * s2 + 3]);
+          pa[kh][s2].z = pack2bf(p[8 * s2 + 4], p[8 * s2 + 5]);
+          pa[kh][s2].w = pack2bf(p[8 * s2 + 6], p[8 * s2 + 7]);
         }
       }
+      psum += __shfl_xor(psum, 32, 64);
+      lrow += psum;
+      // O^T += V^T P^T: k-step (kh, s') covers keys 32 kh + 16 s' + 8 (j >> 2) + 4 hh + (j & 3) in element j
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int r0 = 32 * kh + 16 * s2 + 4 * (G16 >> 1) + qq;  // this lane's supplied key row (j < 4)
+#pragma unroll
+          for (int db = 0; db < 4; ++db) {
+            const int col = 32 * db + 16 * (G16 & 1) + 4 * pp;
+            const uint2 v1 = ds_read_tr16p(&Vg[vp_off(r0, col)]);
+            const uint2 v2 = ds_read_tr16p(&Vg[vp_off(r0 + 8, col)]);
+            uint4 va;
+            va.x = v1.x; va.y = v1.y; va.z = v2.x; va.w = v2.y;
+            o[db] = mfma32x32x16(va, pa[kh][s2], o[db]);
+          }
+        }
+    }
+    bnext = bnn;
+    __builtin_amdgcn_s_waitcnt(0);  // tile t + 1's DMA has landed before the barrier publishes it
+    __syncthreads();
   }
-#undef LSA_P32_FETCH
   // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
   const int qr = qs + w * 32 + r32;
   if (active && qr < qlen) {

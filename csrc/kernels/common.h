@@ -31,8 +31,13 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// ONE v_cvt_pk_bf16_f32 (RNE) for the pair; two scalar f2bf + shift + or cost 4 VALU per pair
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const bf16x2_t v = __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t);
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // 8 bf16 (one uint4) -> 8 floats
@@ -49,8 +54,6 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   r.z = pack2bf(f[4], f[5]); r.w = pack2bf(f[6], f[7]);
   return r;
 }
-
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 // dot product of 8 bf16 pairs on v_dot2c_f32_bf16 (f32 accumulate), no unpacking
 __device__ __forceinline__ float dot8_bf16(const uint4 a, const uint4 b) {

@@ -2,6 +2,7 @@
 (packed variable-length sequences over the paged cache)."""
 import json
 import math
+import os
 import sys
 
 import torch
@@ -29,6 +30,8 @@ def timeit(fn, it=20):
 
 
 def case(name, nseq, qlen, H, Hkv):
+    if os.environ.get("LSA_ATTN_CASES") and name not in os.environ["LSA_ATTN_CASES"].split(","):
+        return
     nblk = (qlen + 63) // 64
     total = nseq * nblk + 1
     kc = torch.randn(total, Hkv, 64, 128, device=dev).to(torch.bfloat16)
