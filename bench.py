@@ -40,7 +40,7 @@ REF_P50_S_LLAMA = 22.7463
 MODEL_NAMES = {"duckdb-nsql": "duckdb-nsql-7B", "llama3.2": "Llama-3.2-3B-Instruct", "mistral": "Mistral-7B-v0.3"}
 
 
-def check_numerics(eng, prompt, tokens, n=16, prefill_rows=0):
+def check_numerics(eng, prompt, tokens, n=16, prefill_rows=0, decode_batch=0):
     """Teacher-forced check of the first ``n`` generated tokens against the fp32 reference forward:
     gap = (oracle max logit - oracle logit of our token) / oracle logit std, worst over the tokens.
     fp8 weights: the prompt rows get the W8A8 prefill's per-token activation rounding in the oracle when
@@ -51,18 +51,21 @@ def check_numerics(eng, prompt, tokens, n=16, prefill_rows=0):
     toks = list(tokens[:n])
     fp8 = eng.runner.w.layers[0].wqkv.kind == "fp8"
     aq = len(prompt) if (fp8 and prefill_rows > 64 and ops.FP8_W8A8) else 0
-    lg = reference_forward(eng.runner.w, list(prompt) + toks[:-1], act_quant_rows=aq)[len(prompt) - 1:]
+    da8 = bool(decode_batch and eng.runner.a8 and decode_batch > eng.runner.a8_min_batch and eng.runner.use_xfrag(decode_batch) and not (
+        eng.runner.fused_norm and decode_batch <= eng.runner.fused_norm_max_batch))  # decode qkv / gate_up W8A8
+    lg = reference_forward(eng.runner.w, list(prompt) + toks[:-1], act_quant_rows=aq,
+                           decode_a8=da8)[len(prompt) - 1:]
     chosen = lg.gather(1, torch.tensor(toks, device=lg.device).view(-1, 1)).squeeze(1)
     gap = ((lg.max(1).values - chosen) / lg.std(1)).max().item()
     agree = int((lg.argmax(1).cpu() == torch.tensor(toks)).sum())
     del lg
-    if aq:
+    if aq or da8:
         # W8A8 prefill: every prompt activation is rounded to e4m3 (3 mantissa bits); the oracle rounds the
         # same rows, but values near a rounding boundary land on different sides in the two computations, so
         # the prompt's K/V differ by quantisation-level noise that 32 layers accumulate.  On random-init
         # weights the leading logits sit within a fraction of a std of each other, so the criterion is the
         # quantisation-level one: every chosen token within 1 std of the oracle's best, half of them its argmax
-        ok, crit = gap < 1.0 and agree >= len(toks) // 2, "W8A8 prefill: gap < 1.0 std, >= half top-1"
+        ok, crit = gap < 1.0 and agree >= len(toks) // 2, "W8A8: gap < 1.0 std, >= half top-1"
     else:
         ok, crit = gap < 0.15, "gap < 0.15 std"
     return {"tokens_checked": len(toks), "argmax_agree": agree, "max_gap_in_logit_std": round(gap, 4),
@@ -134,7 +137,8 @@ def main() -> int:
     for i in range(args.warmup):
         res = one_step()
         if i == 0 and tp == 1:
-            numerics = check_numerics(eng, prompts[0], res[0].token_ids, prefill_rows=args.batch * args.prompt_len)
+            numerics = check_numerics(eng, prompts[0], res[0].token_ids, prefill_rows=args.batch * args.prompt_len,
+                                      decode_batch=args.batch)
     eng.stats.update(decode_s=0.0, decode_steps=0, prefill_s=0.0)  # timed rounds only (no capture/warm-up)
     if world > 1:
         dist.barrier()
@@ -173,7 +177,11 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / REF_TOK_S, 2),
-            "dtype": args.dtype if args.dtype == "bf16" else "fp8 (prefill W8A8 on fp8 MFMA, decode W8A16)",
+            "dtype": args.dtype if args.dtype == "bf16" else (
+                "fp8 (prefill W8A8 on fp8 MFMA; decode qkv / gate_up W8A8 on fp8 MFMA, o / down W8A16)"
+                if eng.runner.a8 and args.batch > eng.runner.a8_min_batch and eng.runner.use_xfrag(args.batch) and not (
+                    eng.runner.fused_norm and args.batch <= eng.runner.fused_norm_max_batch)
+                else "fp8 (prefill W8A8 on fp8 MFMA, decode W8A16)"),
             "data": "synthetic prompts, random-init weights" + (" (CPU rehearsal, not a measurement)" if cpu else ""),
             "config": {
                 "model": MODEL_NAMES.get(args.model, args.model),

@@ -12,7 +12,10 @@ int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* 
              hipStream_t stream);
 int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
                     const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
-                    int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, hipStream_t s);
+                    int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, void* x8, float* sx8, hipStream_t s);
+int lsa_fp8a_gemm(const void* X8, const float* sx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
+                  int epi, int nb, int splitk, int waves, int depth, int xfo, const LsaEpi* ep, hipStream_t stream);
+int lsa_quant_xf8(const void* x, int ldx, int M, int K, int MT, void* x8, float* sx, hipStream_t s);
 int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
                 int waves, int div, int xlds, const LsaEpi* ep, hipStream_t stream);
 int lsa_fp8_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
@@ -205,6 +208,35 @@ void fp8_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& w
         "fp8_gemm_xf");
 }
 
+// W8A8 decode GEMM (kernels/gemm_fp8a.hip): x8 fp8 activations in the xf8 layout + per-row scales sx
+void fp8a_gemm(const at::Tensor& x8, const at::Tensor& sx, int64_t M, int64_t K, const at::Tensor& wq,
+               const at::Tensor& wscale, int64_t N, at::Tensor& out, int64_t epi, int64_t nb, int64_t splitk,
+               int64_t waves, int64_t depth, int64_t xfo, const c10::optional<at::Tensor>& rowss, double eps) {
+  need(sx, at::kFloat, "sx");
+  need(wscale, at::kFloat, "wscale");
+  TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
+  TORCH_CHECK(M >= 1 && M <= 64 && K % 128 == 0, "fp8a_gemm: M in 1..64, K % 128 == 0");
+  TORCH_CHECK(epi == 1 || epi == 2, "fp8a_gemm: f32 slabs or silu");
+  const int64_t mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  TORCH_CHECK(x8.is_cuda() && x8.element_size() == 1 && x8.is_contiguous() && x8.numel() >= mt * 16 * K, "x8 too small");
+  TORCH_CHECK(sx.numel() >= M, "sx too small");
+  check_out(epi, out, splitk, M, N, xfo ? mt : 0);
+  const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, c10::nullopt, c10::nullopt, 0, c10::nullopt, c10::nullopt, N / 16);
+  check(lsa_fp8a_gemm(x8.data_ptr(), sx.data_ptr<float>(), M, K, wq.data_ptr(), wscale.data_ptr<float>(), N,
+                      out.data_ptr(), epi, nb, splitk, waves, depth, xfo, eo.on ? &eo.e : nullptr, cur_stream()),
+        "fp8a_gemm");
+}
+
+void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) {
+  need(x, at::kBFloat16, "x");
+  need(sx, at::kFloat, "sx");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(x8.is_cuda() && x8.element_size() == 1 && x8.numel() >= mt * 16 * K && sx.numel() >= M, "x8 / sx too small");
+  check(lsa_quant_xf8(x.data_ptr(), x.stride(0), M, K, (int)mt, x8.data_ptr(), sx.data_ptr<float>(), cur_stream()),
+        "quant_xf8");
+}
+
 // large-M (prefill) linear layer on the 256x256 tile kernel (kernels/gemm_tile256.hip)
 void gemm_t256(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi) {
   need(x, at::kBFloat16, "x");
@@ -244,11 +276,16 @@ void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscal
 void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t nparts, int64_t part_stride,
                  const c10::optional<at::Tensor>& ids, const c10::optional<at::Tensor>& emb,
                  const c10::optional<at::Tensor>& row_idx, bool write_h, const at::Tensor& w, double eps,
-                 at::Tensor& xn, int64_t rows, int64_t xf_mt, const c10::optional<at::Tensor>& ss_out, int64_t ss_ld,
-                 int64_t ss_nzero) {
+                 const c10::optional<at::Tensor>& xn, int64_t rows, int64_t xf_mt, const c10::optional<at::Tensor>& ss_out,
+                 int64_t ss_ld, int64_t ss_nzero, const c10::optional<at::Tensor>& x8,
+                 const c10::optional<at::Tensor>& sx8) {
   need(h, at::kFloat, "h");
   need(w, at::kBFloat16, "w");
-  need(xn, at::kBFloat16, "xn");
+  if (xn.has_value()) need(*xn, at::kBFloat16, "xn");
+  if (x8.has_value()) {
+    TORCH_CHECK(x8->is_cuda() && x8->element_size() == 1 && x8->numel() >= xf_mt * 16 * w.numel(), "x8 too small");
+    TORCH_CHECK(sx8.has_value() && sx8->scalar_type() == at::kFloat && sx8->numel() >= rows, "x8 needs sx8 [rows] f32");
+  }
   const int D = w.numel();
   if (ss_out.has_value()) {
     need(*ss_out, at::kLong, "ss_out");
@@ -256,9 +293,10 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
   }
   check(lsa_add_rmsnorm(h.data_ptr<float>(), ptr<const float>(parts), parts.has_value() ? nparts : 0, part_stride,
                         ptr<const int>(ids), ptr<const void>(emb), ptr<const int>(row_idx), write_h ? 1 : 0,
-                        w.data_ptr(), (float)eps, xn.data_ptr(), rows, D, xf_mt,
+                        w.data_ptr(), (float)eps, xn.has_value() ? xn->data_ptr() : nullptr, rows, D, xf_mt,
                         ss_out.has_value() ? reinterpret_cast<long long*>(ss_out->data_ptr<int64_t>()) : nullptr, (int)ss_ld,
-                        (int)ss_nzero, cur_stream()),
+                        (int)ss_nzero, x8.has_value() ? x8->data_ptr() : nullptr,
+                        sx8.has_value() ? sx8->data_ptr<float>() : nullptr, cur_stream()),
         "add_rmsnorm");
 }
 
@@ -477,7 +515,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
         py::arg("ids"), py::arg("emb"), py::arg("row_idx"), py::arg("write_h"), py::arg("w"), py::arg("eps"),
         py::arg("xn"), py::arg("rows"), py::arg("xf_mt") = 0, py::arg("ss_out") = py::none(), py::arg("ss_ld") = 0,
-        py::arg("ss_nzero") = 0);
+        py::arg("ss_nzero") = 0, py::arg("x8") = py::none(), py::arg("sx8") = py::none());
+  m.def("fp8a_gemm", &fp8a_gemm, py::arg("x8"), py::arg("sx"), py::arg("M"), py::arg("K"), py::arg("wq"),
+        py::arg("wscale"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"),
+        py::arg("waves") = 4, py::arg("depth") = 1, py::arg("xfo") = 1, py::arg("rowss") = py::none(),
+        py::arg("eps") = 1e-5);
+  m.def("quant_xf8", &quant_xf8, py::arg("x"), py::arg("mt"), py::arg("x8"), py::arg("sx"));
   m.def("rope_append", &rope_append);
   m.def("silu_mul", &silu_mul);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),

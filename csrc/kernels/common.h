@@ -92,6 +92,36 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// block-wide max for blockDim.x <= 1024; `red` must hold >= 16 floats
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = red[0];
+  for (int i = 1; i < nw; ++i) t = fmaxf(t, red[i]);
+  __syncthreads();
+  return t;
+}
+
+// Byte offset of fp8 activation (m, k) in the W8A8 decode layout X8[k/128][mt][64 lanes][32 B]: lane (g, r)
+// holds row 16 mt + r at k = 128 s + 16 g .. +15 (bytes 0..15) and 128 s + 64 + 16 g .. +15 (bytes 16..31),
+// the k-set of the fp8 weight layout's fragment pair (2 s, 2 s + 1).  8 consecutive k from a multiple of 8
+// are contiguous.
+__device__ __forceinline__ size_t xf8_off(int m, int k, int mt) {
+  const int kc = k & 127;
+  return (((size_t)(k >> 7) * mt + (m >> 4)) * 64 + 16 * ((kc & 63) >> 4) + (m & 15)) * 32 + 16 * (kc >> 6) + (kc & 15);
+}
+
+// 8 floats * inv -> 8 OCP e4m3 bytes (v_cvt_pk_fp8_f32: round to nearest even, saturating)
+__device__ __forceinline__ uint2 pack8_fp8(const float* f, float inv) {
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0] * inv, f[1] * inv, 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2] * inv, f[3] * inv, lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4] * inv, f[5] * inv, 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6] * inv, f[7] * inv, hi, true);
+  return make_uint2((unsigned)lo, (unsigned)hi);
+}
+
 // Element offset of activation (m, k) in the fragment-major decode layout Xf[k/32][mt][64 lanes][8]
 // (lane = 16 * ((k % 32) / 8) + m % 16): one MFMA B-fragment per (k-step, 16-row tile) is 1 KiB
 // lane-linear.  8 consecutive k starting at a multiple of 8 are contiguous.

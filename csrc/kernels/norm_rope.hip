@@ -19,7 +19,8 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
                                                            const int* __restrict__ row_idx, int write_h,
                                                            const uint16_t* __restrict__ w, float eps,
                                                            uint16_t* __restrict__ xn, int D, int xf_mt,
-                                                           long long* __restrict__ ss_out, int ss_ld, int ss_nzero) {
+                                                           long long* __restrict__ ss_out, int ss_ld, int ss_nzero,
+                                                           uint8_t* __restrict__ x8, float* __restrict__ sx8) {
   __shared__ float red[16];
   const int m = blockIdx.x;
   const int r = row_idx ? row_idx[m] : m;
@@ -82,15 +83,32 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
     for (int k = threadIdx.x; k < ss_nzero; k += nt) ss_out[(size_t)(k + 1) * ss_ld + m] = 0;
   }
   const float inv = ss_out ? 1.0f : rsqrtf(tot / (float)D + eps);
+  float amax = 0.f;
 #pragma unroll
   for (int q = 0; q < VPT; ++q) {
     const int c = (threadIdx.x + q * nt) * 8;
     if (c < D) {
-      float wf[8], o[8];
+      float wf[8];
       unpack8(wq[q], wf);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = ss_out ? v[q][j] : v[q][j] * inv * wf[j];
-      *reinterpret_cast<uint4*>(xn + (xf_mt ? xf_off(m, c, xf_mt) : (size_t)m * D + c)) = pack8(o);
+      for (int j = 0; j < 8; ++j) {
+        v[q][j] = ss_out ? v[q][j] : v[q][j] * inv * wf[j];
+        amax = fmaxf(amax, fabsf(v[q][j]));
+      }
+      if (xn) *reinterpret_cast<uint4*>(xn + (xf_mt ? xf_off(m, c, xf_mt) : (size_t)m * D + c)) = pack8(v[q]);
+    }
+  }
+  if (x8) {
+    // W8A8 decode input: the row (as the GEMM will see it) in OCP e4m3 with a per-row scale amax / 448,
+    // straight into the xf8 fragment layout of the fp8-activation GEMM (gemm_fp8a.hip)
+    amax = block_max(amax, red);
+    const float sc = fmaxf(amax, 1e-30f) * (1.0f / 448.f);
+    if (threadIdx.x == 0) sx8[m] = sc;
+    const float isc = 1.0f / sc;
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int c = (threadIdx.x + q * nt) * 8;
+      if (c < D) *reinterpret_cast<uint2*>(x8 + xf8_off(m, c, xf_mt)) = pack8_fp8(v[q], isc);
     }
   }
 }
@@ -98,10 +116,11 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
 template <int VPT>
 static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, const float* parts, size_t ps,
                            const int* ids, const uint16_t* e, const int* row_idx, int write_h, const uint16_t* w,
-                           float eps, uint16_t* o, int D, int xf_mt, long long* ss_out, int ss_ld, int ss_nzero) {
+                           float eps, uint16_t* o, int D, int xf_mt, long long* ss_out, int ss_ld, int ss_nzero,
+                           uint8_t* x8, float* sx8) {
 #define LSA_RN(NP)                                                                                         \
   hipLaunchKernelGGL((add_rmsnorm_kernel<NP, VPT>), dim3(rows), dim3(nt), 0, s, h, parts, np, ps, ids, e, \
-                     row_idx, write_h, w, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero)
+                     row_idx, write_h, w, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero, x8, sx8)
   switch (parts ? np : 0) {
     case 0: LSA_RN(0); break;
     case 1: LSA_RN(1); break;
@@ -115,22 +134,28 @@ static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, co
 #undef LSA_RN
 }
 
+// x8 / sx8 (optional): also write the output rows as fp8 e4m3 in the xf8 layout of xf_mt row tiles with a
+// per-row scale (the W8A8 decode GEMM input); xn may then be null (no bf16 copy)
 extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids,
                                const void* emb, const int* row_idx, int write_h, const void* w, float eps, void* xn,
-                               int rows, int D, int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, hipStream_t s) {
+                               int rows, int D, int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, void* x8,
+                               float* sx8, hipStream_t s) {
   if (D % 8 != 0 || rows <= 0) return -1;
   if (xf_mt && (D % 32 != 0 || rows > 16 * xf_mt)) return -3;
   if (ss_out && (row_idx || ss_ld < rows || ss_nzero < 0)) return -4;
+  if (x8 && (!sx8 || !xf_mt || D % 128 != 0 || row_idx)) return -5;
+  if (!xn && !x8) return -6;
   const int vec = D / 8;
   const uint16_t* e = reinterpret_cast<const uint16_t*>(emb);
   const uint16_t* ww = reinterpret_cast<const uint16_t*>(w);
   uint16_t* o = reinterpret_cast<uint16_t*>(xn);
+  uint8_t* q8 = reinterpret_cast<uint8_t*>(x8);
   if (vec <= 1024) {
     launch_rmsnorm<1>(nparts, rows, (vec + 63) / 64 * 64, s, h, parts, (size_t)part_stride, ids, e, row_idx, write_h,
-                      ww, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero);
+                      ww, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero, q8, sx8);
   } else if (vec <= 4096) {
     launch_rmsnorm<4>(nparts, rows, 1024, s, h, parts, (size_t)part_stride, ids, e, row_idx, write_h, ww, eps, o, D, xf_mt,
-                      ss_out, ss_ld, ss_nzero);
+                      ss_out, ss_ld, ss_nzero, q8, sx8);
   } else {
     return -2;
   }

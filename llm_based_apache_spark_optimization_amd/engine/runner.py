@@ -129,6 +129,17 @@ class ModelRunner:
         self.xn_f = torch.zeros(xr * self.d, **bf)
         self.attn_f = torch.zeros(xr * self.H * self.D, **bf)
         self.act_f = torch.zeros(xr * self.ffn_l, **bf)
+        # W8A8 decode (fp8 weights, fragment-major buckets): the norm launches also write the qkv / gate_up
+        # inputs as per-row-scaled e4m3 (xf8 layout) for the fp8-MFMA GEMM (ops.linear_a8)
+        self.a8 = (ops.FP8_A8_DECODE and self.on_gpu and weights.layers[0].wqkv.kind == "fp8"
+                   and self.d % 128 == 0)
+        # ... for buckets above this batch: at 64 rows the fp8-activation GEMM is 27-30 % faster than W8A16
+        # (7B qkv 22.0 -> 16.1 us, gate_up 33.4 -> 23.5), at 32 rows it ties on qkv and the 7B b32 bench
+        # did not move (10425 vs 10357 tok/s) while the e4m3 activations cost top-1 agreement
+        # (profiles/bench_fp8a_decode_mi355x.jsonl)
+        self.a8_min_batch = int(os.environ.get("LSA_FP8_A8_MIN_B", "32"))
+        self.x8 = torch.zeros(xr * self.d if self.a8 else 1, dtype=torch.uint8, device=dev)
+        self.sx8 = torch.ones(max(S, 64), **f32)
         self.o_buf = torch.zeros(8 * S * self.d, **f32)
         self.down_buf = torch.zeros(8 * S * self.d, **f32)
         self.qkv_buf = torch.zeros(8 * S * (self.H + 2 * self.Hkv) * self.D, **f32)
@@ -225,7 +236,10 @@ class ModelRunner:
         sk_o = self._splitk(B, self.H * self.D, xf=xf)
         sk_d = self._splitk(B, self.ffn_l, xf=xf)
         nqkv = (self.H + 2 * self.Hkv) * self.D
-        sk_q = self._splitk(B, d, nqkv, tp_reduced=False, xf=xf)
+        a8 = self.a8 and xf and B > self.a8_min_batch
+        sk_q = (ops.pick_gemm_config(B, nqkv, d, "f32", xf=True, kind="fp8a")[1] if a8
+                else self._splitk(B, d, nqkv, tp_reduced=False, xf=xf))
+        q8 = dict(x8=self.x8, sx8=self.sx8) if a8 else {}
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
@@ -241,12 +255,15 @@ class ModelRunner:
             lin = ops.linear
         for l, lw in enumerate(w.layers):
             if l == 0:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf)
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf, **q8)
             else:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_red, rows=B, xf=xf)
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_red, rows=B, xf=xf, **q8)
             # QKV as f32 split-K slabs; the attention kernel sums them, applies RoPE and appends the new
             # token's k/v to the paged cache itself (no separate rope/append launch)
-            lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
+            if a8:
+                ops.linear_a8(self.x8, self.sx8, B, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
+            else:
+                lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
             kc, vc = self.kv[l, 0], self.kv[l, 1]
             if not self.fuse_rope:
                 ops.rope_append(qkv_parts, pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv)
@@ -257,8 +274,11 @@ class ModelRunner:
                             sin=self.sin if fr else None)
             lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
             o_red = self._reduce_parts(o_parts)
-            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf)
-            lin(xn, lw.w_gate_up, "silu", out=act)
+            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8)
+            if a8:
+                ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=act)
+            else:
+                lin(xn, lw.w_gate_up, "silu", out=act)
             lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
             d_red = self._reduce_parts(d_parts)
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_red, rows=B, xf=xf)

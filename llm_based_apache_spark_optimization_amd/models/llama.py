@@ -180,7 +180,8 @@ def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[st
 
 
 @torch.no_grad()
-def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant_rows: int = 0) -> torch.Tensor:
+def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant_rows: int = 0,
+                      decode_a8: bool = False) -> torch.Tensor:
     """fp32 causal forward of one sequence over the weights exactly as packed (``dense()`` undoes the
     fragment shuffle and the fp8 quantisation, so an fp8 model is compared against its own dequantised
     weights): logits [T, V] f32.  The numerics oracle for the engine at production shapes
@@ -188,7 +189,10 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
 
     ``act_quant_rows``: fp8 models run prefill GEMMs W8A8 (ops.linear, M > 64: per-token e4m3 activations);
     the first ``act_quant_rows`` rows (the prompt, when its prefill batch had > 64 tokens) get the same
-    per-token activation rounding before the projections, decode rows keep bf16 activations (W8A16)."""
+    per-token activation rounding before the projections.  Decode rows keep bf16 activations (W8A16), or with
+    ``decode_a8`` (the W8A8 decode GEMMs of fragment-major buckets, ops.linear_a8) the qkv / gate_up inputs of
+    the rows past the prompt are rounded per row to e4m3 from the f32 norm output (as add_rmsnorm's fp8
+    output does), o / down inputs stay bf16."""
     from ..ops import reference as ref
 
     spec, dev = w.spec, w.device
@@ -220,11 +224,24 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
         head = (head / s).to(torch.float8_e4m3fn).float() * s
         return torch.cat([head, x[aq:]], 0)
 
+    da8 = decode_a8 and w.layers[0].wqkv.kind == "fp8"
+
+    def e4m3_rows(x):
+        amax = x.abs().amax(1, keepdim=True)
+        s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+        return (x / s).to(torch.float8_e4m3fn).float() * s
+
+    def qin(xn):  # qkv / gate_up input from the f32 norm output
+        x = q8(bf(xn))
+        if da8 and aq < T:
+            x = torch.cat([x[:aq], e4m3_rows(xn[aq:])], 0)
+        return x
+
     h = w.embed[ids].float()
     mask = torch.full((T, T), float("-inf"), device=dev).triu(1)
     for lw in w.layers:
-        x = bf(norm(h, lw.attn_norm))
-        qkv = q8(x) @ lw.wqkv.dense().float().t()
+        x = qin(norm(h, lw.attn_norm))
+        qkv = x @ lw.wqkv.dense().float().t()
         q = qkv[:, : H * hd].view(T, H, hd)
         k = qkv[:, H * hd:(H + Hkv) * hd].view(T, Hkv, hd)
         v = qkv[:, (H + Hkv) * hd:].view(T, Hkv, hd)
@@ -233,8 +250,8 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
         s = torch.einsum("qhd,khd->hqk", q, k) / math.sqrt(hd) + mask
         a = bf(torch.einsum("hqk,khd->qhd", s.softmax(-1), v).reshape(T, H * hd))
         h = h + q8(a) @ lw.wo.dense().float().t()
-        x = bf(norm(h, lw.mlp_norm))
-        gu = (q8(x) @ lw.w_gate_up.dense().float().t()).view(T, -1, 2, 16)
+        x = qin(norm(h, lw.mlp_norm))
+        gu = (x @ lw.w_gate_up.dense().float().t()).view(T, -1, 2, 16)
         act = bf(torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(T, -1)
         h = h + q8(act) @ lw.w_down.dense().float().t()
     x = bf(norm(h, w.final_norm))

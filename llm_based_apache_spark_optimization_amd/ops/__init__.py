@@ -182,6 +182,15 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
     """(nb, splitk, waves, div) for a decode GEMM: the tuning table when it has the shape (entries
     measured with fragment-major activations carry a ':xf' suffix, fp8-weight entries ':fp8'), else
     the heuristic below (div 4, 4-wave workgroups won most measured shapes)."""
+    if kind == "fp8a":  # W8A8 decode GEMM: its own sweep entries, else the fp8 (nb, splitk) at default knobs
+        b = 1
+        while b < M:
+            b *= 2
+        e = _tuning_table().get(f"{N}x{K}:{epi}:b{b}:fp8a")
+        if e is not None:
+            return e["nb"], e["splitk"], e["waves"], e["div"]
+        nb, sk, _, _ = pick_gemm_config(M, N, K, epi, xf=xf, kind="fp8")
+        return (2 if (M > 32 and nb > 2) else nb), sk, 4, 4
     if epi == "res":  # the residual epilogue runs the f32-slab main loop (split-K with a last-arriver finish):
         # its own measured entries (scripts/bench_res_epi.py --tune) first, else the f32 entries
         b = 1
@@ -450,16 +459,109 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
     return out
 
 
+# ----------------------------------------------------------------------------------- W8A8 decode
+# LSA_FP8_A8=0 keeps the W8A16 decode GEMMs for the qkv / gate_up projections of fp8 models
+FP8_A8_DECODE = os.environ.get("LSA_FP8_A8", "1") != "0"
+
+
+def to_xf8(x8: torch.Tensor, mt: int) -> torch.Tensor:
+    """uint8 [M, K] e4m3 bytes -> the flat xf8 layout X8[K/128][mt][64 lanes][32 B] of the W8A8 decode GEMM
+    (csrc/kernels/gemm_fp8a.hip; lane 16 g + r: row 16 t + r at k = 128 s + 16 g .. +15 and 128 s + 64 + 16 g ..
+    +15), rows >= M zero."""
+    M, K = x8.shape
+    full = torch.zeros(16 * mt, K, dtype=torch.uint8, device=x8.device)
+    full[:M] = x8
+    v = full.view(mt, 16, K // 128, 2, 4, 16)  # t, r, s, h, g, e
+    return v.permute(2, 0, 4, 1, 3, 5).contiguous().view(-1)  # s, t, g, r, h, e
+
+
+def from_xf8(x8f: torch.Tensor, M: int, K: int) -> torch.Tensor:
+    mt = xfrag_tiles(M)
+    v = x8f.view(-1)[: mt * 16 * K].view(K // 128, mt, 4, 16, 2, 16)  # s, t, g, r, h, e
+    return v.permute(1, 3, 0, 4, 2, 5).reshape(16 * mt, K)[:M]
+
+
+def quantize_xf8(x: torch.Tensor, mt: Optional[int] = None, out: Optional[torch.Tensor] = None,
+                 sx: Optional[torch.Tensor] = None):
+    """(x8 flat xf8 bytes, sx [M] f32): per-row e4m3 activations (scale amax / 448) for ``linear_a8``."""
+    M, K = x.shape
+    mt = mt or xfrag_tiles(M)
+    if out is None:
+        out = torch.zeros(mt * 16 * K, dtype=torch.uint8, device=x.device)
+    if sx is None:
+        sx = torch.empty(M, dtype=torch.float32, device=x.device)
+    if not _gpu(x):
+        q, s = quantize_rows_fp8(x)
+        out.view(-1)[: mt * 16 * K].copy_(to_xf8(q, mt))
+        sx[:M].copy_(s)
+        return out, sx
+    ext().quant_xf8(x, mt, out, sx)
+    return out, sx
+
+
+def linear_a8(x8: torch.Tensor, sx: torch.Tensor, M: int, w: PackedWeight, epi: str = "f32",
+              out: Optional[torch.Tensor] = None, splitk: Optional[int] = None, nb: Optional[int] = None,
+              waves: Optional[int] = None, div: Optional[int] = None, rownorm=None, xfo: bool = True) -> torch.Tensor:
+    """W8A8 decode GEMM (M <= 64, fp8 weights): out = (x8 * sx) @ w^T with the activations in the xf8 layout
+    (``quantize_xf8`` / the fp8 output of ``add_rmsnorm``) on the fp8 MFMA.  epi 'f32' -> [splitk, M, N]
+    slabs; 'silu' -> bf16 [M, N/2] in the fragment-major layout (``xfo``) or row-major."""
+    assert epi in ("f32", "silu")
+    if not _gpu(x8):
+        xd = from_xf8(x8, M, w.K).view(torch.float8_e4m3fn).float() * sx[:M, None]
+        if rownorm is not None:
+            xd = xd * torch.rsqrt(ss_float(rownorm[0][:M]) / w.K + rownorm[1])[:, None]
+        y = xd @ w.dense().float().t()
+        if epi == "f32":
+            sk = splitk or 1
+            o = out if out is not None else torch.empty(sk, M, w.N)
+            o.view(-1)[: sk * M * w.N].zero_()
+            o.view(sk, M, w.N)[0].copy_(y)
+            return o
+        F = w.N // 2
+        y3 = y.view(M, F // 16, 2, 16)
+        act = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, F).to(torch.bfloat16)
+        act = to_xfrag(act) if xfo else act
+        if out is None:
+            return act
+        out.view(-1)[: act.numel()].copy_(act.view(-1))
+        return out
+    assert w.kind == "fp8", "linear_a8 runs fp8 weights"
+    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, w.K, epi, xf=True, kind="fp8a")
+    nb = nb0 if nb is None else nb
+    splitk = sk0 if splitk is None else splitk
+    waves = wv0 if waves is None else waves
+    div = dv0 if div is None else div
+    if out is None:
+        if epi == "f32":
+            out = torch.empty(splitk, M, w.N, device=x8.device, dtype=torch.float32)
+        else:
+            out = torch.zeros((xfrag_tiles(M) * 16 if xfo else M) * (w.N // 2), device=x8.device, dtype=torch.bfloat16)
+    kw = _epi_kw(rownorm, None, 0)
+    ext().fp8a_gemm(x8, sx, M, w.K, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, _fp8_depth(div),
+                    1 if xfo else 0, **kw)
+    return out
+
+
 # ----------------------------------------------------------------------------------- norms / rope
 def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
                 parts: Optional[torch.Tensor] = None, ids: Optional[torch.Tensor] = None,
                 emb: Optional[torch.Tensor] = None, row_idx: Optional[torch.Tensor] = None,
                 write_h: bool = True, rows: Optional[int] = None, xf: bool = False,
-                ss_out: Optional[torch.Tensor] = None, ss_ld: int = 0, ss_nzero: int = 0) -> torch.Tensor:
+                ss_out: Optional[torch.Tensor] = None, ss_ld: int = 0, ss_nzero: int = 0,
+                x8: Optional[torch.Tensor] = None, sx8: Optional[torch.Tensor] = None) -> torch.Tensor:
     """h[r] (= emb[ids[r]]) (+= sum parts[:, r]); xn[m] = rmsnorm(h[row_idx[m]]) * w.
     xf=True: xn is a flat buffer receiving the fragment-major layout (``to_xfrag``) of ``rows`` rows.
     ss_out (raw mode, the norm folded into the next GEMMs): xn = bf16(h) un-normalised, ss_out[m] = sum h^2,
-    and ss_out[k * ss_ld + m] = 0 for k = 1..ss_nzero (the accumulators of the later residual epilogues)."""
+    and ss_out[k * ss_ld + m] = 0 for k = 1..ss_nzero (the accumulators of the later residual epilogues).
+    x8 / sx8: the same rows also as per-row-scaled e4m3 in the xf8 layout (``linear_a8`` input; quantised from
+    the f32 values, before the bf16 rounding of xn)."""
+    assert x8 is None or xf, "the fp8 output rides on the fragment-major (xf) decode layout"
+    if x8 is not None and not _gpu(h):
+        add_rmsnorm(h, w, eps, xn, parts, ids, emb, row_idx, write_h, rows, xf, ss_out, ss_ld, ss_nzero)
+        n = rows if rows is not None else xn.shape[0]
+        xr = from_xfrag(xn, n, w.numel()) if xf else xn[:n]
+        quantize_xf8(xr, xfrag_tiles(n), x8, sx8)
+        return xn
     if rows is None:
         assert not xf, "xf output needs rows"
         rows = xn.shape[0]
@@ -488,7 +590,7 @@ def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
     nparts = parts.shape[0] if parts is not None else 0
     stride = parts.stride(0) if parts is not None else 0
     ext().add_rmsnorm(h, parts, nparts, stride, ids, emb, row_idx, write_h, w, eps, xn, rows,
-                      xfrag_tiles(rows) if xf else 0, ss_out, ss_ld, ss_nzero)
+                      xfrag_tiles(rows) if (xf or x8 is not None) else 0, ss_out, ss_ld, ss_nzero, x8, sx8)
     return xn
 
 

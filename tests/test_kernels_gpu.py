@@ -714,3 +714,65 @@ def test_fp8_w8a8_linear(gpu, M, epi):
         u = wd.view(F // 16, 2, 16, K)[:, 1].reshape(F, K)
         want = torch.nn.functional.silu(x.float() @ g.t()) * (x.float() @ u.t())
     assert _rel(y, want) < 4e-2
+
+
+# ------------------------------------------------------------------ W8A8 decode GEMM (fp8 activations)
+@pytest.mark.parametrize("M", [1, 9, 20, 32, 48, 64])
+def test_quant_xf8(gpu, M):
+    """GPU per-row e4m3 quantisation into the xf8 layout vs the CPU definition (one e4m3 ulp apart at most)."""
+    torch.manual_seed(M)
+    K = 512
+    x = (torch.randn(M, K, device=gpu) * 3).to(torch.bfloat16)
+    x8, sx = ops.quantize_xf8(x)
+    c8, csx = ops.quantize_xf8(x.cpu())
+    assert torch.allclose(sx.cpu(), csx, rtol=1e-6)
+    a = ops.from_xf8(x8, M, K).cpu().view(torch.float8_e4m3fn).float()
+    b = ops.from_xf8(c8, M, K).view(torch.float8_e4m3fn).float()
+    assert torch.allclose(a, b, rtol=0.13, atol=2 ** -8)
+
+
+@pytest.mark.parametrize("M", [1, 9, 20, 32, 48, 64])
+@pytest.mark.parametrize("epi", ["f32", "silu"])
+@pytest.mark.parametrize("nb", [2, 4, 6, 8])
+def test_fp8a_gemm(gpu, M, epi, nb):
+    """W8A8 decode GEMM on the fp8 MFMA vs the fp32 product of the dequantised operands (the kernel is exact
+    up to f32 accumulation order: the quantisation itself is the caller's)."""
+    if nb >= 6 and not 16 < M <= 32:
+        pytest.skip("nb 8 is instantiated for the 17..32-row tile")
+    torch.manual_seed(M + nb)
+    N, K = 1536, 1536
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w if epi == "f32" else ops.interleave_gate_up(w[: N // 2], w[N // 2:]), "fp8")
+    x8, sx = ops.quantize_xf8(x)
+    xd = ops.from_xf8(x8, M, K).view(torch.float8_e4m3fn).float() * sx[:, None]
+    yr = xd @ ops.dequantize_fp8(pw.data, pw.scale, N, K).float().t()
+    if epi == "f32":
+        for sk in (1, 3):
+            y = ops.linear_a8(x8, sx, M, pw, "f32", splitk=sk, nb=nb)
+            assert _rel(y.sum(0), yr) < 1e-4, sk
+    else:
+        y3 = yr.view(M, N // 32, 2, 16)
+        want = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, N // 2)
+        for xfo in (True, False):
+            y = ops.linear_a8(x8, sx, M, pw, "silu", nb=nb, xfo=xfo)
+            got = ops.from_xfrag(y, M, N // 2) if xfo else y.view(M, N // 2)
+            assert _rel(got, want) < 1e-2, xfo
+
+
+@pytest.mark.parametrize("M", [20, 32, 64])
+def test_add_rmsnorm_fp8_output(gpu, M):
+    """add_rmsnorm's xf8 output: the normalised rows (f32, before the bf16 rounding) as per-row e4m3."""
+    torch.manual_seed(M)
+    d = 1024
+    h = torch.randn(M, d, device=gpu) * 2
+    g = (torch.rand(d, device=gpu) + 0.5).to(torch.bfloat16)
+    want = h * torch.rsqrt(h.pow(2).mean(1, keepdim=True) + 1e-5) * g.float()
+    xn = torch.zeros(ops.xfrag_tiles(M) * 16 * d, device=gpu, dtype=torch.bfloat16)
+    x8 = torch.zeros(ops.xfrag_tiles(M) * 16 * d, device=gpu, dtype=torch.uint8)
+    sx = torch.zeros(M, device=gpu)
+    ops.add_rmsnorm(h.clone(), g, 1e-5, xn, rows=M, xf=True, x8=x8, sx8=sx)
+    assert torch.allclose(sx, want.abs().amax(1) / 448, rtol=1e-3)
+    got = ops.from_xf8(x8, M, d).view(torch.float8_e4m3fn).float() * sx[:, None]
+    assert _rel(got, want) < 4e-2
+    assert _rel(ops.from_xfrag(xn, M, d).float(), want) < 1e-2  # the bf16 copy is still written

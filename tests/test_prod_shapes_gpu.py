@@ -30,7 +30,7 @@ def _engine(gpu, model, dtype):
         torch.cuda.empty_cache()
         spec = dataclasses.replace(get_spec(model), n_layers=2, name=f"{model}-2l")
         w = init_random(spec, gpu, seed=11, kind=dtype)
-        runner = ModelRunner(w, max_slots=32, max_model_len=512, use_graphs=True)
+        runner = ModelRunner(w, max_slots=64, max_model_len=512, use_graphs=True)
         _CACHE[key] = LLMEngine(runner, name=spec.name)
     return _CACHE[key]
 
@@ -63,7 +63,7 @@ def test_prefill_logits_prod_shapes(gpu, model, dtype):
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp8"])
 @pytest.mark.parametrize("model", ["duckdb-nsql", "llama3.2"])
-@pytest.mark.parametrize("B", [1, 20, 32])
+@pytest.mark.parametrize("B", [1, 20, 32, 48])
 def test_decode_tokens_prod_shapes(gpu, model, dtype, B):
     eng = _engine(gpu, model, dtype)
     prompts = _prompts(eng.runner.V, B, 100 + B)
@@ -72,7 +72,11 @@ def test_decode_tokens_prod_shapes(gpu, model, dtype, B):
     worst = 0.0
     for p, out in zip(prompts, res[: min(B, 6)] if B > 1 else res):
         rows = sum(len(q) for q in prompts)  # one packed prefill: W8A8 for fp8 weights when > 64 rows
-        lg = reference_forward(eng.runner.w, p + out.token_ids[:-1], act_quant_rows=len(p) if rows > 64 else 0)[len(p) - 1:]
+        # fragment-major decode buckets of an fp8 model run qkv / gate_up W8A8 (ops.linear_a8)
+        a8 = eng.runner.a8 and eng.runner.bucket(B) > eng.runner.a8_min_batch and eng.runner.use_xfrag(eng.runner.bucket(B)) and not (
+            eng.runner.fused_norm and eng.runner.bucket(B) <= eng.runner.fused_norm_max_batch)
+        lg = reference_forward(eng.runner.w, p + out.token_ids[:-1], act_quant_rows=len(p) if rows > 64 else 0,
+                               decode_a8=a8)[len(p) - 1:]
         chosen = lg.gather(1, torch.tensor(out.token_ids, device=lg.device).view(-1, 1)).squeeze(1)
         top = lg.max(1).values
         spread = lg.std(1)
