@@ -323,6 +323,12 @@ void silu_mul(const at::Tensor& g, const at::Tensor& u, at::Tensor& o) {
   check(lsa_silu_mul(g.data_ptr(), u.data_ptr(), o.data_ptr(), g.numel(), cur_stream()), "silu_mul");
 }
 
+extern "C" int lsa_attn_set_stamps(void* p);
+void attn_set_stamps(const c10::optional<at::Tensor>& st) {
+  if (st.has_value()) TORCH_CHECK(st->is_cuda() && st->element_size() == 8, "stamps: int64 GPU tensor");
+  check(lsa_attn_set_stamps(st.has_value() ? st->data_ptr() : nullptr), "attn_set_stamps");
+}
+
 void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                  const at::Tensor& pos, int64_t H, int64_t Hkv, double scale, int64_t chunk_blocks, int64_t nsplit,
                  at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, at::Tensor& counters, int64_t xf_mt,
@@ -521,6 +527,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("waves") = 4, py::arg("depth") = 1, py::arg("xfo") = 1, py::arg("rowss") = py::none(),
         py::arg("eps") = 1e-5);
   m.def("quant_xf8", &quant_xf8, py::arg("x"), py::arg("mt"), py::arg("x8"), py::arg("sx"));
+  m.def("attn_set_stamps", &attn_set_stamps, py::arg("stamps") = py::none());
   m.def("rope_append", &rope_append);
   m.def("silu_mul", &silu_mul);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),

@@ -49,6 +49,12 @@ __device__ __forceinline__ void eff_split(int nblk, int chunk_blocks, int nsplit
 // split-K slabs; every workgroup rotates its own G query heads, the workgroup holding the last block
 // appends the rotated k and v to the cache, and the new token's key/value are substituted from
 // registers where the score loop meets position p (no dependency on the cache write completing).
+// timing probe (scripts/attn_stamps.py): when set, thread 0 of every decode-attention workgroup records
+// s_memrealtime (100 MHz) at 7 points of its critical path into [wg][8]; null in production
+__device__ unsigned long long* g_attn_stamps = nullptr;
+#define LSA_STAMP(K)                                                                                  \
+  if (stp && tid == 0) stp[((size_t)(split * gridDim.y + b) * gridDim.x + hk) * 8 + (K)] = __builtin_amdgcn_s_memrealtime()
+
 struct RopeArgs {
   const float* parts;  // [nparts][B][(H + 2 Hkv) * 128] f32
   size_t part_stride;
@@ -97,6 +103,8 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   const int hk = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int H = Hkv * G;
   const int tid = threadIdx.x;
+  unsigned long long* const stp = g_attn_stamps;
+  LSA_STAMP(0);
   const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(opart, 0, 0x7fffffff, 0x00020000);
   const int lg = tid >> 4, li = tid & 15, wv = tid >> 6;
   const int* bt = block_tables + (size_t)b * max_blocks;
@@ -157,6 +165,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   const int nblk = (ctx + 63) >> 6;
   int ech, nse;
   eff_split(nblk, chunk_blocks, nsplit, unsplit_max, ech, nse);
+  LSA_STAMP(1);
   if (split >= nse) return;  // whole workgroup: this sequence needs fewer splits
   const int blk0 = split * ech;
   const int blk1 = min(nblk, blk0 + ech);
@@ -201,6 +210,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
       qkv_s[lg][li] = pack8(y);
     }
     __syncthreads();
+    LSA_STAMP(2);
 #pragma unroll
     for (int g = 0; g < G; ++g) qb[g] = qkv_s[g][li];
     if constexpr (NEWREG) {
@@ -305,6 +315,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     }
     if (blk < blk1) score(kA, vA, blk);
   }
+  LSA_STAMP(3);
 
   if constexpr (ROPE != 0) {
     // the workgroup covering position tpos appends the new token's k / v to the cache: after its score loop
@@ -351,6 +362,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     }
   }
   __syncthreads();
+  LSA_STAMP(4);
   // each thread finishes 4 consecutive dims of one head
   for (int e = tid; e < G * 32; e += NT) {
     const int g = e >> 5, d0 = (e & 31) * 4;
@@ -395,33 +407,55 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   g_i32* ctr = (g_i32*)(counters) + (size_t)b * Hkv + hk;
   if (tid == 0) s_last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nse - 1;
   __syncthreads();
+  LSA_STAMP(5);
   if (!s_last) return;
   if (tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  static_assert(WV * D >= 512, "the split-combine reuses so[] as [G][256] maxima + [G][256] sums");
-  float* cm = &so[0][0][0];          // [G][256] split maxima, then weights
-  float* cl = cm + G * 256;          // [G][256] split sums
-  for (int i = tid; i < G * nse; i += NT) {
-    const int g = i / nse, sp = i - g * nse;
-    const size_t pi = ((size_t)b * H + hk * G + g) * nsplit + sp;
-    const unsigned long long ml =
-        __hip_atomic_load((g_u64*)(mlpart) + pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    cm[g * 256 + sp] = __uint_as_float((uint32_t)ml);
-    cl[g * 256 + sp] = __uint_as_float((uint32_t)(ml >> 32));
+  // the partials are spread over SS thread slices per (head, 4 dims): each slice loads its share of the nse
+  // (max, sum) words and partial vectors in one batch (one memory round trip; the maxima are merged online,
+  // log-sum-exp style) and the slices are combined through LDS.  Loading all maxima first and then the
+  // vectors nse / 4 at a time by one thread per (head, 4 dims) was the tail of the decode-attention
+  // latency chain (3B 2k explain: 3.1 us of 11.1, scripts/attn_stamps.py)
+  constexpr int NPAIR = G * 32;
+  constexpr int SS = (NT / NPAIR) >= 4 ? 4 : (NT / NPAIR);
+  __shared__ __attribute__((aligned(16))) float cpo[SS][G][D];
+  __shared__ float cpm[SS][G], cpl[SS][G];
+  if (tid < SS * NPAIR) {
+    const int pair = tid % NPAIR, slice = tid / NPAIR;
+    const int g = pair >> 5, d0 = (pair & 31) * 4;
+    const size_t pi0 = ((size_t)b * H + hk * G + g) * nsplit;
+    float M = LSA_NEG, L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int sp = slice; sp < nse; sp += SS) {
+      const unsigned long long ml =
+          __hip_atomic_load((g_u64*)(mlpart) + pi0 + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs_o, (int)(((pi0 + sp) * D + d0) * 4), 0, LSA_SC1);
+      const float mi = __uint_as_float((uint32_t)ml), li = __uint_as_float((uint32_t)(ml >> 32));
+      const float mn = fmaxf(M, mi);
+      const float a = __builtin_amdgcn_exp2f(M - mn), wgt = __builtin_amdgcn_exp2f(mi - mn);
+      M = mn;
+      L = L * a + li * wgt;
+      O[0] = O[0] * a + __uint_as_float(v[0]) * wgt; O[1] = O[1] * a + __uint_as_float(v[1]) * wgt;
+      O[2] = O[2] * a + __uint_as_float(v[2]) * wgt; O[3] = O[3] * a + __uint_as_float(v[3]) * wgt;
+    }
+    *reinterpret_cast<float4*>(&cpo[slice][g][d0]) = make_float4(O[0], O[1], O[2], O[3]);
+    if (d0 == 0) {
+      cpm[slice][g] = M;
+      cpl[slice][g] = L;
+    }
   }
   __syncthreads();
-  for (int e = tid; e < G * 32; e += NT) {
+  for (int e = tid; e < NPAIR; e += NT) {
     const int g = e >> 5, d0 = (e & 31) * 4;
     float M = LSA_NEG;
-    for (int sp = 0; sp < nse; ++sp) M = fmaxf(M, cm[g * 256 + sp]);
+#pragma unroll
+    for (int sl = 0; sl < SS; ++sl) M = fmaxf(M, cpm[sl][g]);
     float L = 0.f, O[4] = {0.f, 0.f, 0.f, 0.f};
-    const size_t pi0 = ((size_t)b * H + hk * G + g) * nsplit;
-#pragma unroll 4
-    for (int sp = 0; sp < nse; ++sp) {
-      const float wgt = __builtin_amdgcn_exp2f(cm[g * 256 + sp] - M);
-      L += cl[g * 256 + sp] * wgt;
-      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs_o, (int)(((pi0 + sp) * D + d0) * 4), 0, LSA_SC1);
-      O[0] += __uint_as_float(v[0]) * wgt; O[1] += __uint_as_float(v[1]) * wgt;
-      O[2] += __uint_as_float(v[2]) * wgt; O[3] += __uint_as_float(v[3]) * wgt;
+#pragma unroll
+    for (int sl = 0; sl < SS; ++sl) {
+      const float wgt = __builtin_amdgcn_exp2f(cpm[sl][g] - M);
+      L += cpl[sl][g] * wgt;
+      const float4 v = *reinterpret_cast<const float4*>(&cpo[sl][g][d0]);
+      O[0] += v.x * wgt; O[1] += v.y * wgt; O[2] += v.z * wgt; O[3] += v.w * wgt;
     }
     const int h = hk * G + g;
     const float inv = L > 0.f ? 1.f / L : 0.f;
@@ -430,6 +464,12 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     pk.y = pack2bf(O[2] * inv, O[3] * inv);
     *reinterpret_cast<uint2*>(out + (xf_mt ? xf_off(b, h * D + d0, xf_mt) : ((size_t)b * H + h) * D + d0)) = pk;
   }
+  LSA_STAMP(6);
+}
+
+extern "C" int lsa_attn_set_stamps(void* p) {
+  unsigned long long* v = reinterpret_cast<unsigned long long*>(p);
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), &v, sizeof(v));
 }
 
 extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
