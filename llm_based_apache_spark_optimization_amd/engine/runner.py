@@ -159,7 +159,12 @@ class ModelRunner:
         # profiles/rocprof_fused_norm_ab.txt) the norm-free step wins at batch 1 (3B 2k explain 1788 -> 1738 us,
         # 7B 2.77 -> 2.71 ms) but loses at batch 32 for the 3B (2029 -> 2087 us: the residual epilogue's
         # last-arriver tail costs more than the norm launch it replaces); the norm launches stay above it
-        self.fused_norm_max_batch = int(os.environ.get("LSA_FUSED_NORM_MAX_B", "16"))
+        # The 3B (hidden 3072) lost it again in round 2 once its o / down residual epilogues were re-measured
+        # inside the step: 192 output blocks per row-parallel GEMM leave CUs idle without split-K, and split-K
+        # adds the last-arriver tail (3B 2k explain 1.733 vs 1.708 ms per step norm-free vs norm launches,
+        # 7B b1 2.625 vs 2.69 ms) -- so the default is per hidden size
+        mb = os.environ.get("LSA_FUSED_NORM_MAX_B")
+        self.fused_norm_max_batch = int(mb) if mb is not None else (16 if self.d >= 4096 else 0)
         self.ssq = torch.zeros(2 * self.L + 2, S, dtype=torch.int64, device=dev)  # Q24 fixed point (ops.ss_q24)
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)

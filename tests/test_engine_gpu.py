@@ -24,10 +24,16 @@ def _hf(name, init=0.08, seed=0):
 
 @pytest.mark.parametrize("name", ["tiny-nsql", "tiny-llama3"])
 @pytest.mark.parametrize("graphs", [True, False])
-def test_hf_parity_gpu(gpu, name, graphs):
+@pytest.mark.parametrize("norm_free", [True, False])
+def test_hf_parity_gpu(gpu, name, graphs, norm_free):
+    """HF parity of the decode loop, with the norm-free step (gammas folded, row-scale / residual epilogues)
+    and with the norm launches (the runner's default depends on the hidden size)."""
     spec, m = _hf(name)
     w = from_hf_state_dict(spec, m.state_dict(), gpu)
-    eng = LLMEngine(ModelRunner(w, max_slots=4, max_model_len=512, use_graphs=graphs))
+    runner = ModelRunner(w, max_slots=4, max_model_len=512, use_graphs=graphs)
+    runner.fused_norm_max_batch = 16 if norm_free else 0
+    assert runner.fused_norm or not norm_free
+    eng = LLMEngine(runner)
     prompts = [[1] + list(range(5, 60)), [1] + list(range(100, 300, 3))]
     params = SamplingParams(max_tokens=12, ignore_eos=True)
     res = eng.generate(prompts, params)
@@ -98,6 +104,8 @@ def test_batched_decode_is_deterministic(gpu, batch):
     norm-folded residual epilogues accumulate row sums of squares in integer fixed point (no
     arrival-order float atomics), and every row of a tile reduces K in the same order."""
     eng = build_engine("tiny-nsql", device=str(gpu), max_slots=16, max_model_len=512)
+    eng.runner.fused_norm_max_batch = 16  # the norm-free step (the tiny model's default is the norm launches)
+    assert eng.runner.fused_norm
     prompts = [[1] + list(range(40, 90))] * batch
     params = SamplingParams(max_tokens=24, ignore_eos=True)
     a = [r.token_ids for r in eng.generate(prompts, params)]
