@@ -324,6 +324,46 @@ void silu_mul(const at::Tensor& g, const at::Tensor& u, at::Tensor& o) {
 }
 
 extern "C" int lsa_attn_set_stamps(void* p);
+extern "C" int lsa_attn_o_set_stamps(void* p);
+void attn_o_set_stamps(const c10::optional<at::Tensor>& st) {
+  if (st.has_value()) TORCH_CHECK(st->is_cuda() && st->element_size() == 8, "stamps: int64 GPU tensor");
+  check(lsa_attn_o_set_stamps(st.has_value() ? st->data_ptr() : nullptr), "attn_o_set_stamps");
+}
+extern "C" int lsa_attn_o_b1(const float* qkv_parts, int nparts, long part_stride, const float* cos_t,
+                             const float* sin_t, const int* pos, void* kc, void* vc, const int* block_table, int H,
+                             float scale, const void* Wo, int N, float* slabs, int* tickets, const LsaEpi* ep,
+                             hipStream_t s);
+
+// batch-1 attention + O projection + residual in one launch (kernels/attention_o.hip)
+void attn_o_b1(const at::Tensor& qkv_parts, const at::Tensor& cos_t, const at::Tensor& sin_t, const at::Tensor& pos,
+               at::Tensor& kc, at::Tensor& vc, const at::Tensor& block_table, int64_t H, double scale,
+               const at::Tensor& wo, int64_t N, at::Tensor& slabs, at::Tensor& tickets, at::Tensor& h,
+               at::Tensor& xout, at::Tensor& ss_out) {
+  need(qkv_parts, at::kFloat, "qkv_parts");
+  need(pos, at::kInt, "pos");
+  need(block_table, at::kInt, "block_table");
+  need(wo, at::kBFloat16, "wo");
+  need(slabs, at::kFloat, "slabs");
+  need(tickets, at::kInt, "tickets");
+  need(h, at::kFloat, "h");
+  need(xout, at::kBFloat16, "xout");
+  need(ss_out, at::kLong, "ss_out");
+  TORCH_CHECK(qkv_parts.dim() == 3 && qkv_parts.size(1) >= 1 && qkv_parts.size(2) == 3 * H * 128 &&
+                  qkv_parts.stride(2) == 1, "qkv_parts must be [S, B, 3 H 128] slabs (MHA)");
+  TORCH_CHECK(wo.numel() == N * H * 128 && slabs.numel() >= H * N && tickets.numel() >= N / 512 &&
+                  h.numel() >= N && xout.numel() >= N, "attn_o_b1 operand sizes");
+  TORCH_CHECK(cos_t.size(0) >= block_table.size(-1) * 64, "rope tables shorter than the block table");
+  LsaEpi e{};
+  e.h = h.data_ptr<float>();
+  e.ldh = N;
+  e.xout = reinterpret_cast<uint16_t*>(xout.data_ptr());
+  e.ss_out = reinterpret_cast<long long*>(ss_out.data_ptr<int64_t>());
+  check(lsa_attn_o_b1(qkv_parts.data_ptr<float>(), qkv_parts.size(0), qkv_parts.stride(0), cos_t.data_ptr<float>(),
+                      sin_t.data_ptr<float>(), pos.data_ptr<int>(), kc.data_ptr(), vc.data_ptr(),
+                      block_table.data_ptr<int>(), H, (float)scale, wo.data_ptr(), N, slabs.data_ptr<float>(),
+                      tickets.data_ptr<int>(), &e, cur_stream()),
+        "attn_o_b1");
+}
 void attn_set_stamps(const c10::optional<at::Tensor>& st) {
   if (st.has_value()) TORCH_CHECK(st->is_cuda() && st->element_size() == 8, "stamps: int64 GPU tensor");
   check(lsa_attn_set_stamps(st.has_value() ? st->data_ptr() : nullptr), "attn_set_stamps");
@@ -528,6 +568,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps") = 1e-5);
   m.def("quant_xf8", &quant_xf8, py::arg("x"), py::arg("mt"), py::arg("x8"), py::arg("sx"));
   m.def("attn_set_stamps", &attn_set_stamps, py::arg("stamps") = py::none());
+  m.def("attn_o_b1", &attn_o_b1);
+  m.def("attn_o_set_stamps", &attn_o_set_stamps, py::arg("stamps") = py::none());
   m.def("rope_append", &rope_append);
   m.def("silu_mul", &silu_mul);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),

@@ -194,6 +194,8 @@ __device__ __forceinline__ void res_store_partial(__amdgpu_buffer_rsrc_t rs, siz
 
 __device__ __forceinline__ f32x4_t res_slab_sum(__amdgpu_buffer_rsrc_t rs, size_t elem, size_t slab_elems, int nsplit) {
   f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+  // unrolled so the split loads leave together (one memory round trip, not one per split)
+#pragma unroll 8
   for (int sp = 0; sp < nsplit; ++sp) {
     const u32x4_t u = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((elem + sp * slab_elems) * 4), 0, LSA_SC1_AUX);
     s[0] += __uint_as_float(u[0]); s[1] += __uint_as_float(u[1]);

@@ -168,6 +168,11 @@ class ModelRunner:
         self.ssq = torch.zeros(2 * self.L + 2, S, dtype=torch.int64, device=dev)  # Q24 fixed point (ops.ss_q24)
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)
+        # batch-1 attention + O projection in one launch (ops.attn_o_b1): MHA, bf16 weights, contexts planned
+        # within 512 tokens (the attention is unsplit there)
+        self.attn_o = (ops.ATTN_O and self.on_gpu and tps == 1 and self.H == self.Hkv and self.D == 128
+                       and self.d % 512 == 0 and self.H % 8 == 0 and weights.layers[0].wo.kind == "bf16")
+        self.ao_slabs = torch.zeros(self.H * self.d if self.attn_o else 1, **f32)
         self.graphs: dict = {}
         self._pending_bt: dict = {}  # slot -> block-table row of a prompt still being prefilled in chunks
         if self.tp is not None and self.tp.size > 1 and self.on_gpu:
@@ -229,7 +234,8 @@ class ModelRunner:
         tier = 256
         while tier < t:
             tier *= 2
-        return ops.decode_split_plan(B, self.Hkv, min(tier, self.max_model_len))
+        tier = min(tier, self.max_model_len)
+        return tuple(ops.decode_split_plan(B, self.Hkv, tier)) + (tier,)  # the tier also keys the graph
 
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         if self.fused_norm and B <= self.fused_norm_max_batch:
@@ -322,9 +328,17 @@ class ModelRunner:
             lin = ops.linear
         ops.add_rmsnorm(h, w.layers[0].attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf,
                         ss_out=ssq.view(-1), ss_ld=S, ss_nzero=2 * self.L)
+        # batch 1, contexts planned within 512 tokens: attention + O projection + residual in one launch
+        ao = B == 1 and self.attn_o and len(plan) > 3 and plan[3] <= 512
         for l, lw in enumerate(w.layers):
             lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q, rownorm=(ssq[2 * l], self.eps))
             kc, vc = self.kv[l, 0], self.kv[l, 1]
+            if ao:
+                ops.attn_o_b1(qkv_parts, self.cos, self.sin, pos, kc, vc, bt, self.H, self.scale, lw.wo,
+                              self.ao_slabs, tk, h, xn, ssq[2 * l + 1])
+                lin(xn, lw.w_gate_up, "silu", out=act, rownorm=(ssq[2 * l + 1], self.eps))
+                lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk))
+                continue
             ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale,
                             attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
                             qkv_parts=qkv_parts, cos=self.cos, sin=self.sin)

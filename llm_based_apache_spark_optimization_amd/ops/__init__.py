@@ -685,6 +685,32 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     return out
 
 
+# batch-1 attention + O projection + residual in one launch (csrc/kernels/attention_o.hip), opt-in (LSA_ATTN_O=1):
+# correct (tests/test_kernels_gpu.py::test_attn_o_b1) but measured no faster -- 7B b1 step 2.66 vs 2.62 ms
+# (rocprofv3: 16.3 us in the captured step vs 5.9 + ~9.5 us for the two launches).  The probe
+# (scripts/attn_stamps.py --ao) shows why: the 33.5 MB weight stream contends with the K / V loads of the
+# attention it is meant to hide under (score loop 2.8 -> 5.0 us), and the cross-head reduction adds a serial
+# publish -> ticket -> sum tail of ~4 us that the GEMM launch it replaces did not have at batch 1
+ATTN_O = os.environ.get("LSA_ATTN_O", "0") == "1"
+
+
+def attn_o_b1(qkv_parts, cos, sin, pos, kc, vc, block_table, H, scale, wo: PackedWeight, slabs, tickets,
+              h, xout, ss_out) -> None:
+    """Batch-1 MHA decode: attention of the new token (RoPE + KV append fused, from the QKV split-K slabs)
+    followed by the O projection and the norm-free residual epilogue, in one launch:
+    h += o @ Wo^T; xout = bf16(h); ss_out[0] += sum h^2 (Q24).  slabs: >= H * d f32 scratch; tickets: zeroed
+    int32 counters (>= d / 512; left zeroed)."""
+    if not _gpu(pos):
+        B = pos.shape[0]
+        q = torch.empty(B, H, 128, dtype=torch.bfloat16, device=pos.device)
+        a = torch.empty_like(q)
+        attn_decode(q, kc, vc, block_table, pos, H, H, scale, a, qkv_parts=qkv_parts, cos=cos, sin=sin)
+        linear(a.view(B, -1), wo, "res", res=(h, xout, ss_out))
+        return
+    ext().attn_o_b1(qkv_parts, cos, sin, pos, kc, vc, block_table, H, scale, wo.data, wo.N, slabs, tickets,
+                    h, xout, ss_out)
+
+
 # prefill attention kernel: "32" = 32 x 32 MFMA tiles, 128 query rows per workgroup (attention_prefill32.hip);
 # "16" = the 16 x 16 kernel of attention.hip (64 rows per workgroup); "auto" = 32 when the longest packed
 # sequence has >= 512 rows (measured, scripts/bench_attn_prefill.py: 7B 2k 146 -> 119 us, 3B 2k 118 -> 115 us,

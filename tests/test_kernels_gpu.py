@@ -776,3 +776,42 @@ def test_add_rmsnorm_fp8_output(gpu, M):
     got = ops.from_xf8(x8, M, d).view(torch.float8_e4m3fn).float() * sx[:, None]
     assert _rel(got, want) < 4e-2
     assert _rel(ops.from_xfrag(xn, M, d).float(), want) < 1e-2  # the bf16 copy is still written
+
+
+# ------------------------------------------------------------------ batch-1 attention + O projection, one launch
+@pytest.mark.parametrize("ctx", [1, 64, 200, 512])
+@pytest.mark.parametrize("nparts", [1, 2])
+def test_attn_o_b1(gpu, ctx, nparts):
+    """attn_o_b1 (attention + O projection + residual epilogue fused) vs attn_decode + the residual O GEMM:
+    same h, bf16 copy and Q24 sum of squares; the K/V append lands in the cache; tickets left zeroed."""
+    from llm_based_apache_spark_optimization_amd.ops import reference as ref
+
+    H, D, d = 32, 128, 4096
+    torch.manual_seed(ctx + nparts)
+    kc, vc, bt = _paged([ctx + 64], H, D, gpu, seed=ctx)
+    cos, sin = ref.rope_tables(D, bt.shape[1] * 64, 10000.0, device=gpu)
+    pos = torch.tensor([ctx - 1], dtype=torch.int32, device=gpu)
+    parts = torch.randn(nparts, 1, 3 * H * D, device=gpu) / nparts
+    wo = ops.PackedWeight.from_dense((torch.randn(d, H * D, device=gpu) / math.sqrt(H * D)).to(torch.bfloat16))
+    h0 = torch.randn(1, d, device=gpu)
+    # reference: the two-launch path on copies of the cache
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = torch.empty(1, H, D, device=gpu, dtype=torch.bfloat16)
+    a = torch.empty_like(q)
+    ops.attn_decode(q, kc2, vc2, bt, pos, H, H, 1 / math.sqrt(D), a, qkv_parts=parts, cos=cos, sin=sin)
+    h_ref, x_ref = h0.clone(), torch.zeros(1, d, device=gpu, dtype=torch.bfloat16)
+    ss_ref = torch.zeros(1, device=gpu, dtype=torch.int64)
+    ops.linear(a.view(1, -1), wo, "res", res=(h_ref, x_ref, ss_ref))
+    # fused
+    h1, x1 = h0.clone(), torch.zeros(1, d, device=gpu, dtype=torch.bfloat16)
+    ss1 = torch.zeros(1, device=gpu, dtype=torch.int64)
+    slabs = torch.empty(H * d, device=gpu)
+    tk = torch.zeros(64, device=gpu, dtype=torch.int32)
+    ops.attn_o_b1(parts, cos, sin, pos, kc, vc, bt, H, 1 / math.sqrt(D), wo, slabs, tk, h1, x1, ss1)
+    torch.cuda.synchronize()
+    assert _rel(h1 - h0, h_ref - h0) < 2e-3
+    assert _rel(x1.float(), x_ref.float()) < 1e-2
+    assert abs(ops.ss_float(ss1).item() - ops.ss_float(ss_ref).item()) <= 1e-3 * ops.ss_float(ss_ref).item()
+    assert torch.all(tk == 0)
+    blk, slot = int(bt[0, (ctx - 1) // 64]), (ctx - 1) % 64
+    assert torch.equal(kc[blk, :, slot], kc2[blk, :, slot]) and torch.equal(vc[blk, :, slot], vc2[blk, :, slot])
