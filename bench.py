@@ -40,6 +40,15 @@ REF_P50_S_LLAMA = 22.7463
 MODEL_NAMES = {"duckdb-nsql": "duckdb-nsql-7B", "llama3.2": "Llama-3.2-3B-Instruct", "mistral": "Mistral-7B-v0.3"}
 
 
+def fp8_label(r, B):
+    """Which decode GEMMs of an fp8 model run W8A8 (fp8 activations) at batch B (engine/runner.py)."""
+    xf = r.a8 and r.use_xfrag(B) and not (r.fused_norm and B <= r.fused_norm_max_batch)
+    a8 = [name for name, on in (("qkv", xf and B > r.a8_min_batch), ("gate_up", xf and B > r.a8_mlp_min_batch)) if on]
+    if not a8:
+        return "fp8 (prefill W8A8 on fp8 MFMA, decode W8A16)"
+    return f"fp8 (prefill W8A8 on fp8 MFMA; decode {' / '.join(a8)} W8A8 on fp8 MFMA, the rest W8A16)"
+
+
 def check_numerics(eng, prompt, tokens, n=16, prefill_rows=0, decode_batch=0):
     """Teacher-forced check of the first ``n`` generated tokens against the fp32 reference forward:
     gap = (oracle max logit - oracle logit of our token) / oracle logit std, worst over the tokens.
@@ -51,15 +60,18 @@ def check_numerics(eng, prompt, tokens, n=16, prefill_rows=0, decode_batch=0):
     toks = list(tokens[:n])
     fp8 = eng.runner.w.layers[0].wqkv.kind == "fp8"
     aq = len(prompt) if (fp8 and prefill_rows > 64 and ops.FP8_W8A8) else 0
-    da8 = bool(decode_batch and eng.runner.a8 and decode_batch > eng.runner.a8_min_batch and eng.runner.use_xfrag(decode_batch) and not (
-        eng.runner.fused_norm and decode_batch <= eng.runner.fused_norm_max_batch))  # decode qkv / gate_up W8A8
-    lg = reference_forward(eng.runner.w, list(prompt) + toks[:-1], act_quant_rows=aq,
-                           decode_a8=da8)[len(prompt) - 1:]
+    r = eng.runner
+    unfused_xf = bool(decode_batch and r.a8 and r.use_xfrag(decode_batch) and not (
+        r.fused_norm and decode_batch <= r.fused_norm_max_batch))
+    da8 = unfused_xf and decode_batch > r.a8_min_batch  # decode qkv W8A8
+    da8m = unfused_xf and decode_batch > r.a8_mlp_min_batch  # decode gate_up W8A8
+    lg = reference_forward(r.w, list(prompt) + toks[:-1], act_quant_rows=aq, decode_a8=da8,
+                           decode_a8_mlp=da8m)[len(prompt) - 1:]
     chosen = lg.gather(1, torch.tensor(toks, device=lg.device).view(-1, 1)).squeeze(1)
     gap = ((lg.max(1).values - chosen) / lg.std(1)).max().item()
     agree = int((lg.argmax(1).cpu() == torch.tensor(toks)).sum())
     del lg
-    if aq or da8:
+    if aq or da8 or da8m:
         # W8A8 prefill: every prompt activation is rounded to e4m3 (3 mantissa bits); the oracle rounds the
         # same rows, but values near a rounding boundary land on different sides in the two computations, so
         # the prompt's K/V differ by quantisation-level noise that 32 layers accumulate.  On random-init
@@ -180,11 +192,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / REF_TOK_S, 2),
-            "dtype": args.dtype if args.dtype == "bf16" else (
-                "fp8 (prefill W8A8 on fp8 MFMA; decode qkv / gate_up W8A8 on fp8 MFMA, o / down W8A16)"
-                if eng.runner.a8 and args.batch > eng.runner.a8_min_batch and eng.runner.use_xfrag(args.batch) and not (
-                    eng.runner.fused_norm and args.batch <= eng.runner.fused_norm_max_batch)
-                else "fp8 (prefill W8A8 on fp8 MFMA, decode W8A16)"),
+            "dtype": args.dtype if args.dtype == "bf16" else fp8_label(eng.runner, args.batch),
             "data": "synthetic prompts, random-init weights" + (" (CPU rehearsal, not a measurement)" if cpu else ""),
             "config": {
                 "model": MODEL_NAMES.get(args.model, args.model),

@@ -138,6 +138,9 @@ class ModelRunner:
         # did not move (10425 vs 10357 tok/s) while the e4m3 activations cost top-1 agreement
         # (profiles/bench_fp8a_decode_mi355x.jsonl)
         self.a8_min_batch = int(os.environ.get("LSA_FP8_A8_MIN_B", "32"))
+        # ... and the gate_up projection from 17 rows: at 32 rows it is 13 % faster than W8A16 (7B 22.8 -> 19.8 us,
+        # profiles/bench_fp8a_decode_mi355x.jsonl) where the qkv one ties
+        self.a8_mlp_min_batch = int(os.environ.get("LSA_FP8_A8_MLP_MIN_B", "16"))
         self.x8 = torch.zeros(xr * self.d if self.a8 else 1, dtype=torch.uint8, device=dev)
         self.sx8 = torch.ones(max(S, 64), **f32)
         self.o_buf = torch.zeros(8 * S * self.d, **f32)
@@ -247,10 +250,12 @@ class ModelRunner:
         sk_o = self._splitk(B, self.H * self.D, xf=xf)
         sk_d = self._splitk(B, self.ffn_l, xf=xf)
         nqkv = (self.H + 2 * self.Hkv) * self.D
-        a8 = self.a8 and xf and B > self.a8_min_batch
+        a8 = self.a8 and xf and B > self.a8_min_batch  # qkv W8A8
+        a8m = self.a8 and xf and B > self.a8_mlp_min_batch  # gate_up W8A8
         sk_q = (ops.pick_gemm_config(B, nqkv, d, "f32", xf=True, kind="fp8a")[1] if a8
                 else self._splitk(B, d, nqkv, tp_reduced=False, xf=xf))
         q8 = dict(x8=self.x8, sx8=self.sx8) if a8 else {}
+        q8m = dict(x8=self.x8, sx8=self.sx8) if a8m else {}
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
@@ -285,8 +290,8 @@ class ModelRunner:
                             sin=self.sin if fr else None)
             lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
             o_red = self._reduce_parts(o_parts)
-            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8)
-            if a8:
+            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
+            if a8m:
                 ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=act)
             else:
                 lin(xn, lw.w_gate_up, "silu", out=act)

@@ -181,7 +181,7 @@ def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[st
 
 @torch.no_grad()
 def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant_rows: int = 0,
-                      decode_a8: bool = False) -> torch.Tensor:
+                      decode_a8: bool = False, decode_a8_mlp: Optional[bool] = None) -> torch.Tensor:
     """fp32 causal forward of one sequence over the weights exactly as packed (``dense()`` undoes the
     fragment shuffle and the fp8 quantisation, so an fp8 model is compared against its own dequantised
     weights): logits [T, V] f32.  The numerics oracle for the engine at production shapes
@@ -192,7 +192,8 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
     per-token activation rounding before the projections.  Decode rows keep bf16 activations (W8A16), or with
     ``decode_a8`` (the W8A8 decode GEMMs of fragment-major buckets, ops.linear_a8) the qkv / gate_up inputs of
     the rows past the prompt are rounded per row to e4m3 from the f32 norm output (as add_rmsnorm's fp8
-    output does), o / down inputs stay bf16."""
+    output does), o / down inputs stay bf16.  ``decode_a8_mlp`` (default: = decode_a8) sets the gate_up input
+    separately (the engine runs gate_up W8A8 from a smaller batch than qkv)."""
     from ..ops import reference as ref
 
     spec, dev = w.spec, w.device
@@ -224,23 +225,25 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
         head = (head / s).to(torch.float8_e4m3fn).float() * s
         return torch.cat([head, x[aq:]], 0)
 
-    da8 = decode_a8 and w.layers[0].wqkv.kind == "fp8"
+    fp8w = w.layers[0].wqkv.kind == "fp8"
+    da8 = decode_a8 and fp8w
+    da8m = (decode_a8 if decode_a8_mlp is None else decode_a8_mlp) and fp8w
 
     def e4m3_rows(x):
         amax = x.abs().amax(1, keepdim=True)
         s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
         return (x / s).to(torch.float8_e4m3fn).float() * s
 
-    def qin(xn):  # qkv / gate_up input from the f32 norm output
+    def qin(xn, on):  # qkv / gate_up input from the f32 norm output
         x = q8(bf(xn))
-        if da8 and aq < T:
+        if on and aq < T:
             x = torch.cat([x[:aq], e4m3_rows(xn[aq:])], 0)
         return x
 
     h = w.embed[ids].float()
     mask = torch.full((T, T), float("-inf"), device=dev).triu(1)
     for lw in w.layers:
-        x = qin(norm(h, lw.attn_norm))
+        x = qin(norm(h, lw.attn_norm), da8)
         qkv = x @ lw.wqkv.dense().float().t()
         q = qkv[:, : H * hd].view(T, H, hd)
         k = qkv[:, H * hd:(H + Hkv) * hd].view(T, Hkv, hd)
@@ -250,7 +253,7 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
         s = torch.einsum("qhd,khd->hqk", q, k) / math.sqrt(hd) + mask
         a = bf(torch.einsum("hqk,khd->qhd", s.softmax(-1), v).reshape(T, H * hd))
         h = h + q8(a) @ lw.wo.dense().float().t()
-        x = qin(norm(h, lw.mlp_norm))
+        x = qin(norm(h, lw.mlp_norm), da8m)
         gu = (x @ lw.w_gate_up.dense().float().t()).view(T, -1, 2, 16)
         act = bf(torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(T, -1)
         h = h + q8(act) @ lw.w_down.dense().float().t()
