@@ -66,7 +66,7 @@ def check_numerics(eng, prompt, tokens, n=16, prefill_rows=0, decode_batch=0):
     da8 = unfused_xf and decode_batch > r.a8_min_batch  # decode qkv W8A8
     da8m = unfused_xf and decode_batch > r.a8_mlp_min_batch  # decode gate_up W8A8
     lg = reference_forward(r.w, list(prompt) + toks[:-1], act_quant_rows=aq, decode_a8=da8,
-                           decode_a8_mlp=da8m)[len(prompt) - 1:]
+                           decode_a8_mlp=da8m, kv_fp8=r.kv_fp8)[len(prompt) - 1:]
     chosen = lg.gather(1, torch.tensor(toks, device=lg.device).view(-1, 1)).squeeze(1)
     gap = ((lg.max(1).values - chosen) / lg.std(1)).max().item()
     agree = int((lg.argmax(1).cpu() == torch.tensor(toks)).sum())
@@ -95,6 +95,8 @@ def main() -> int:
     ap.add_argument("--new-tokens", type=int, default=128)
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--kv-dtype", default=None, choices=["bf16", "fp8"],
+                    help="paged KV cache dtype (default bf16; fp8 = e4m3 rows with per-row scales, ops.KV_FP8)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="run the same bench flow on CPU over gloo (tests of the multi-rank path; not a measurement)")
@@ -133,7 +135,7 @@ def main() -> int:
     max_len = args.prompt_len + args.new_tokens + 64
     eng = build_engine(args.model, device=str(device), dtype=args.dtype, max_slots=args.batch,
                        max_model_len=max_len, seed=0, tp=tpg, use_graphs=not args.no_graphs,
-                       max_prefill_tokens=max(16384, args.batch * args.prompt_len))
+                       max_prefill_tokens=max(16384, args.batch * args.prompt_len), kv_dtype=args.kv_dtype)
     V = eng.spec.vocab_size
     g = torch.Generator().manual_seed(1234 + replica)
     prompts = [[eng.spec.bos_id if eng.spec.bos_id < V else 1]
@@ -192,7 +194,8 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / REF_TOK_S, 2),
-            "dtype": args.dtype if args.dtype == "bf16" else fp8_label(eng.runner, args.batch),
+            "dtype": (args.dtype if args.dtype == "bf16" else fp8_label(eng.runner, args.batch))
+            + ("; fp8 e4m3 KV cache" if eng.runner.kv_fp8 else ""),
             "data": "synthetic prompts, random-init weights" + (" (CPU rehearsal, not a measurement)" if cpu else ""),
             "config": {
                 "model": MODEL_NAMES.get(args.model, args.model),

@@ -21,14 +21,16 @@ int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf, int N, voi
 int lsa_fp8_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                     int epi, int nb, int splitk, int xfrag, const LsaEpi* ep, hipStream_t stream);
 int lsa_rope_append(const void* qkv, const float* qkv_parts, int nparts, long part_stride, const int* pos, const int* tok_seq, const int* block_tables, int max_blocks,
-                    const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int T, int H, int Hkv,
-                    hipStream_t s);
+                    const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, float* ks, float* vs, int T,
+                    int H, int Hkv, hipStream_t s);
 int lsa_silu_mul(const void* g, const void* u, void* o, long n, hipStream_t s);
 int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                     const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit, int unsplit_max,
                     void* out, float* opart, float* mlpart, int* counters, int xf_mt, const float* qkv_parts, int nparts,
                     long part_stride,
-                    const float* cos_t, const float* sin_t, hipStream_t s);
+                    const float* cos_t, const float* sin_t, const float* ks, const float* vs, hipStream_t s);
+int lsa_kv8_dequant(const void* kc, const void* vc, const float* ks, const float* vs, const int* block_tables,
+                    int max_blocks, const int* ctx_lens, int nseq, int Hkv, int mb, void* ko, void* vo, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                      const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
                      void* out, hipStream_t s);
@@ -78,6 +80,24 @@ void check(int rc, const char* what) { TORCH_CHECK(rc == 0, "lsa kernel '", what
 void need(const at::Tensor& t, at::ScalarType dt, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+
+// paged KV cache operands: bf16 [nblk, Hkv, 64, 128], or fp8 (uint8 e4m3 bytes, same shape) with f32
+// per-(token, kv-head) scales [nblk, Hkv, 64]
+void check_cache(const at::Tensor& kc, const at::Tensor& vc, const c10::optional<at::Tensor>& ks,
+                 const c10::optional<at::Tensor>& vs) {
+  TORCH_CHECK(ks.has_value() == vs.has_value(), "fp8 cache needs both K and V scales");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(2) == 64 && kc.size(3) == 128 && kc.sizes() == vc.sizes() &&
+                  kc.is_contiguous() && vc.is_contiguous(), "cache must be contiguous [nblk, Hkv, 64, 128]");
+  const at::ScalarType dt = ks.has_value() ? at::kByte : at::kBFloat16;
+  need(kc, dt, "kc");
+  need(vc, dt, "vc");
+  if (ks.has_value()) {
+    need(*ks, at::kFloat, "ks");
+    need(*vs, at::kFloat, "vs");
+    TORCH_CHECK(ks->numel() == kc.numel() / 128 && vs->numel() == kc.numel() / 128 && ks->is_contiguous() &&
+                    vs->is_contiguous(), "fp8 cache scales must be contiguous [nblk, Hkv, 64]");
+  }
 }
 
 template <typename T>
@@ -302,8 +322,10 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
 
 void rope_append(const at::Tensor& qkv, const at::Tensor& pos, const c10::optional<at::Tensor>& tok_seq,
                  const at::Tensor& block_tables, const at::Tensor& cos_t, const at::Tensor& sin_t, at::Tensor& q_out,
-                 at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv) {
+                 at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv, const c10::optional<at::Tensor>& ks,
+                 const c10::optional<at::Tensor>& vs) {
   need(pos, at::kInt, "pos");
+  check_cache(kc, vc, ks, vs);
   need(block_tables, at::kInt, "block_tables");
   // qkv: bf16 [T, n] or f32 split-K slabs [S, T, n]
   const bool parts = qkv.scalar_type() == at::kFloat;
@@ -314,7 +336,7 @@ void rope_append(const at::Tensor& qkv, const at::Tensor& pos, const c10::option
   check(lsa_rope_append(parts ? nullptr : qkv.data_ptr(), parts ? qkv.data_ptr<float>() : nullptr,
                         parts ? qkv.size(0) : 0, parts ? qkv.stride(0) : 0, pos.data_ptr<int>(), ptr<const int>(tok_seq), block_tables.data_ptr<int>(),
                         block_tables.size(1), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), q_out.data_ptr(),
-                        kc.data_ptr(), vc.data_ptr(), T, H, Hkv, cur_stream()),
+                        kc.data_ptr(), vc.data_ptr(), ptr<float>(ks), ptr<float>(vs), T, H, Hkv, cur_stream()),
         "rope_append");
 }
 
@@ -373,8 +395,10 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                  const at::Tensor& pos, int64_t H, int64_t Hkv, double scale, int64_t chunk_blocks, int64_t nsplit,
                  at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, at::Tensor& counters, int64_t xf_mt,
                  const c10::optional<at::Tensor>& qkv_parts, const c10::optional<at::Tensor>& cos_t,
-                 const c10::optional<at::Tensor>& sin_t, int64_t unsplit_max) {
+                 const c10::optional<at::Tensor>& sin_t, int64_t unsplit_max, const c10::optional<at::Tensor>& ks,
+                 const c10::optional<at::Tensor>& vs) {
   need(q, at::kBFloat16, "q");
+  check_cache(kc, vc, ks, vs);
   need(pos, at::kInt, "pos");
   const int B = pos.size(0);
   need(opart, at::kFloat, "opart");
@@ -401,8 +425,27 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                         (int)unsplit_max, out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), counters.data_ptr<int>(), xf_mt,
                         ptr<const float>(qkv_parts), qkv_parts.has_value() ? qkv_parts->size(0) : 0,
                         qkv_parts.has_value() ? qkv_parts->stride(0) : 0, ptr<const float>(cos_t),
-                        ptr<const float>(sin_t), cur_stream()),
+                        ptr<const float>(sin_t), ptr<const float>(ks), ptr<const float>(vs), cur_stream()),
         "attn_decode");
+}
+
+// fp8 cache blocks of a prefill batch -> compact bf16 scratch [nseq * mb, Hkv, 64, 128] (kernels/kv8.hip)
+void kv8_dequant(const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& ks, const at::Tensor& vs,
+                 const at::Tensor& block_tables, const at::Tensor& ctx_lens, int64_t mb, at::Tensor& ko, at::Tensor& vo) {
+  check_cache(kc, vc, ks, vs);
+  need(block_tables, at::kInt, "block_tables");
+  need(ctx_lens, at::kInt, "ctx_lens");
+  need(ko, at::kBFloat16, "ko");
+  need(vo, at::kBFloat16, "vo");
+  const int64_t nseq = ctx_lens.numel(), Hkv = kc.size(1);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= nseq && block_tables.is_contiguous(),
+              "block_tables must be a contiguous [nseq, max_blocks] table");
+  TORCH_CHECK(mb <= block_tables.size(1), "mb exceeds the block table width");
+  TORCH_CHECK(ko.numel() >= nseq * mb * Hkv * 64 * 128 && vo.numel() >= nseq * mb * Hkv * 64 * 128, "kv8 scratch too small");
+  check(lsa_kv8_dequant(kc.data_ptr(), vc.data_ptr(), ks.data_ptr<float>(), vs.data_ptr<float>(),
+                        block_tables.data_ptr<int>(), block_tables.size(1), ctx_lens.data_ptr<int>(), nseq, Hkv, mb,
+                        ko.data_ptr(), vo.data_ptr(), cur_stream()),
+        "kv8_dequant");
 }
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
@@ -570,13 +613,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_stamps", &attn_set_stamps, py::arg("stamps") = py::none());
   m.def("attn_o_b1", &attn_o_b1);
   m.def("attn_o_set_stamps", &attn_o_set_stamps, py::arg("stamps") = py::none());
-  m.def("rope_append", &rope_append);
+  m.def("rope_append", &rope_append, py::arg("qkv"), py::arg("pos"), py::arg("tok_seq"), py::arg("block_tables"),
+        py::arg("cos"), py::arg("sin"), py::arg("q_out"), py::arg("kc"), py::arg("vc"), py::arg("H"), py::arg("Hkv"),
+        py::arg("ks") = py::none(), py::arg("vs") = py::none());
+  m.def("kv8_dequant", &kv8_dequant);
   m.def("silu_mul", &silu_mul);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("pos"), py::arg("H"), py::arg("Hkv"), py::arg("scale"), py::arg("chunk_blocks"), py::arg("nsplit"),
         py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("counters"), py::arg("xf_mt") = 0,
         py::arg("qkv_parts") = py::none(),
-        py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4);
+        py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4,
+        py::arg("ks") = py::none(), py::arg("vs") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
         py::arg("out"), py::arg("rows32") = 0);

@@ -63,7 +63,13 @@ struct RopeArgs {
   const float* sin_t;
   uint16_t* kc;        // cache (writable aliases of the kernel's kc / vc)
   uint16_t* vc;
+  float* ks;           // fp8 cache: per-(token, kv-head) scales (writable aliases of ksc / vsc)
+  float* vs;
 };
+
+// K / V register image of one 8-dim lane slice: 8 bf16 (uint4) or, fp8 cache, 8 e4m3 bytes (uint2)
+template <bool KV8> struct KvLane { typedef uint4 T; };
+template <> struct KvLane<true> { typedef uint2 T; };
 
 // WV = waves per workgroup: 8 for G <= 3 (two keys per lane group per block -> half the K/V registers,
 // so four 4-wave-equivalents fit per CU and a B x Hkv = 1024 grid runs in whole rounds; G = 3: half the
@@ -84,10 +90,16 @@ struct RopeArgs {
 #ifndef LSA_ATTN_DOT2_G
 #define LSA_ATTN_DOT2_G 99
 #endif
-template <int G, int ROPE, int WV>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime slab count
+//
+// KV8: fp8 cache (ops.KV_FP8) -- kc / vc hold e4m3 bytes [blocks, Hkv, 64, 128] and ksc / vsc the per-(token,
+// kv-head) f32 scales [blocks, Hkv, 64].  Same lane map with 8-byte K / V loads (half the HBM bytes of the
+// memory-bound score loop); a K slice is widened to bf16 exactly (v_cvt_scalef32_pk_bf16_fp8) for the same dot2
+// products and its scale multiplies the reduced score; a V slice goes to f32 with its scale folded into p.
+template <int G, int ROPE, int WV, bool KV8 = false>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime
 __global__ __launch_bounds__(64 * WV)
 __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc,
+                                                          const float* __restrict__ ksc, const float* __restrict__ vsc,
                                                           const int* __restrict__ block_tables, int max_blocks,
                                                           const int* __restrict__ pos, int Hkv, float scale_log2,
                                                           int chunk_blocks, int nsplit, int unsplit_max,
@@ -109,19 +121,32 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   const int lg = tid >> 4, li = tid & 15, wv = tid >> 6;
   const int* bt = block_tables + (size_t)b * max_blocks;
   // K/V of block blk+1 are in flight while block blk is scored (two register sets, static names)
-  uint4 kA[TU], vA[TU], kB[TU], vB[TU];
+  typedef typename KvLane<KV8>::T KT;
+  KT kA[TU], vA[TU], kB[TU], vB[TU];
+  float ksA[TU], vsA[TU], ksB[TU], vsB[TU];  // KV8 only: the keys' / values' row scales
   // keys past the context in the last block re-read the last valid row (a cache hit, not HBM traffic);
   // they are masked in the score
   // G >= LSA_ATTN_BUF_G: one buffer resource per (block, kv-head) slab, built in SGPRs from the uniform
   // block-table entry, the lanes carry 32-bit offsets (3B: 10.3 -> 9.8 us at B = 32); G = 1 keeps 64-bit
   // global loads (buffer loads measured 20.7 -> 22.4 us for the 7B at B = 32)
   constexpr bool BUF = G >= LSA_ATTN_BUF_G;
-  auto fetch = [&](uint4 (&kr)[TU], uint4 (&vr)[TU], int blk, int last_tok) {
-    const size_t base = ((size_t)__builtin_amdgcn_readfirstlane(bt[blk]) * Hkv + hk) * 64 * D;
+  auto fetch = [&](KT (&kr)[TU], KT (&vr)[TU], float (&ksr)[TU], float (&vsr)[TU], int blk, int last_tok) {
+    const size_t rowb = ((size_t)__builtin_amdgcn_readfirstlane(bt[blk]) * Hkv + hk) * 64;
+    const size_t base = rowb * D;
 #pragma unroll
     for (int u = 0; u < TU; ++u) {
       const int tok = min(wv * TW + u * 4 + (lg & 3), last_tok);
-      if constexpr (BUF) {
+      if constexpr (KV8) {
+        const uint8_t* k8 = reinterpret_cast<const uint8_t*>(kc) + base + tok * D + li * 8;
+        const uint8_t* v8 = reinterpret_cast<const uint8_t*>(vc) + base + tok * D + li * 8;
+        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t a = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(k8));
+        const u32x2_t c = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(v8));
+        kr[u] = make_uint2(a[0], a[1]);
+        vr[u] = make_uint2(c[0], c[1]);
+        ksr[u] = ksc[rowb + tok];
+        vsr[u] = vsc[rowb + tok];
+      } else if constexpr (BUF) {
         const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)(kc + base), 0, 64 * D * 2, 0x00020000);
         const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(vc + base), 0, 64 * D * 2, 0x00020000);
         const int off = (tok * D + li * 8) * 2;
@@ -139,7 +164,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   // block): its first K/V fetch leaves before the context length is even known.  (Speculating the other
   // splits' first blocks too was measured: splits a short sequence does not need then cost a wasted
   // block read each, 23 -> 36 us at B = 32, ctx 200, 4 splits.)
-  if (split == 0) fetch(kA, vA, 0, 63);
+  if (split == 0) fetch(kA, vA, ksA, vsA, 0, 63);
   // fused RoPE: the new token's q / k / v rows (sum of the QKV projection's split-K slabs) do not depend on
   // the context length -- their loads leave before pos[b] is read, off the prologue's dependent chain
   float xq[8];
@@ -171,7 +196,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   const int blk1 = min(nblk, blk0 + ech);
 
   // the first K/V block is in flight while the query (and, fused, RoPE) is prepared
-  if (split != 0 && blk0 < blk1) fetch(kA, vA, blk0, ctx - 1 - blk0 * 64);
+  if (split != 0 && blk0 < blk1) fetch(kA, vA, ksA, vsA, blk0, ctx - 1 - blk0 * 64);
   __builtin_amdgcn_sched_barrier(0);
 
   const int tpos = ctx - 1;  // position of the new token
@@ -183,6 +208,8 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   // of a branch around an LDS read)
   constexpr bool NEWREG = G >= LSA_ATTN_NEWREG_G;
   __shared__ uint4 qkv_s[G + 2][16];
+  __shared__ uint2 new8_s[KV8 ? 2 : 1][16];  // KV8: the new token's e4m3 key / value row and its scales
+  __shared__ float newsc_s[2];
   uint4 knew = make_uint4(0, 0, 0, 0), vnew = make_uint4(0, 0, 0, 0);
   if constexpr (ROPE != 0) {
     // lane group j < G builds query head j, group G the new key, group G + 1 the new value (each lane
@@ -208,6 +235,19 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
         for (int j = 0; j < 8; ++j) y[j] = x[j];
       }
       qkv_s[lg][li] = pack8(y);
+      if constexpr (KV8) {  // the new key / value row quantised like every cached row (16-lane amax)
+        if (lg >= G) {
+          float a = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a = fmaxf(a, fabsf(y[j]));
+          a = fmaxf(a, __shfl_xor(a, 8, 64));
+          a = fmaxf(a, __shfl_xor(a, 4, 64));
+          a = fmaxf(a, __shfl_xor(a, 2, 64));
+          a = fmaxf(a, __shfl_xor(a, 1, 64));
+          new8_s[lg - G][li] = pack8_fp8(y, kv8_inv(a));
+          if (li == 0) newsc_s[lg - G] = a * LSA_KV8_RMAX;
+        }
+      }
     }
     __syncthreads();
     LSA_STAMP(2);
@@ -242,15 +282,30 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
   }
 
-  auto score = [&](const uint4 (&kr)[TU], const uint4 (&vr)[TU], int blk) {
+  auto score = [&](const KT (&kr)[TU], const KT (&vr)[TU], const float (&ksr)[TU], const float (&vsr)[TU], int blk) {
     float s[TU][G];
 #pragma unroll
     for (int u = 0; u < TU; ++u) {
-      uint4 kq = kr[u];
+      uint4 kq;
+      float ksu = 1.f;
       const int tp = blk * 64 + wv * TW + u * 4 + (lg & 3);
       const bool valid = tp < ctx;
-      if constexpr (ROPE != 0) {
-        if (tp == tpos) kq = NEWREG ? knew : qkv_s[G][li];
+      if constexpr (KV8) {
+        uint2 k8 = kr[u];
+        ksu = ksr[u];
+        if constexpr (ROPE != 0) {
+          if (tp == tpos) {
+            k8 = new8_s[0][li];
+            ksu = newsc_s[0];
+          }
+        }
+        kq = fp8x8_to_bf16x8(k8);
+        if constexpr (DOT2) ksu *= scale_log2;  // (else q was pre-scaled)
+      } else {
+        kq = kr[u];
+        if constexpr (ROPE != 0) {
+          if (tp == tpos) kq = NEWREG ? knew : qkv_s[G][li];
+        }
       }
       float kf[8];
       if constexpr (!DOT2) unpack8(kq, kf);
@@ -268,7 +323,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
         d += __shfl_xor(d, 4, 64);
         d += __shfl_xor(d, 2, 64);
         d += __shfl_xor(d, 1, 64);
-        s[u][g] = valid ? (DOT2 ? d * scale_log2 : d) : LSA_NEG;
+        s[u][g] = valid ? (KV8 ? d * ksu : (DOT2 ? d * scale_log2 : d)) : LSA_NEG;
       }
     }
 #pragma unroll
@@ -290,30 +345,43 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
       for (int j = 0; j < 8; ++j) o[g][j] *= alpha;
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
-        uint4 vq = vr[u];
-        if constexpr (ROPE != 0) {
-          if (blk * 64 + wv * TW + u * 4 + (lg & 3) == tpos) vq = NEWREG ? vnew : qkv_s[G + 1][li];
+        float vf[8], pu = p[u];
+        if constexpr (KV8) {
+          uint2 v8 = vr[u];
+          float vsu = vsr[u];
+          if constexpr (ROPE != 0) {
+            if (blk * 64 + wv * TW + u * 4 + (lg & 3) == tpos) {
+              v8 = new8_s[1][li];
+              vsu = newsc_s[1];
+            }
+          }
+          fp8x8_to_f32(v8, vf);
+          pu *= vsu;
+        } else {
+          uint4 vq = vr[u];
+          if constexpr (ROPE != 0) {
+            if (blk * 64 + wv * TW + u * 4 + (lg & 3) == tpos) vq = NEWREG ? vnew : qkv_s[G + 1][li];
+          }
+          unpack8(vq, vf);
         }
-        float vf[8];
-        unpack8(vq, vf);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[g][j] = fmaf(p[u], vf[j], o[g][j]);
+        for (int j = 0; j < 8; ++j) o[g][j] = fmaf(pu, vf[j], o[g][j]);
       }
     }
   };
   if (blk0 < blk1) {
     int blk = blk0;
     for (; blk + 1 < blk1; blk += 2) {
-      fetch(kB, vB, blk + 1, ctx - 1 - (blk + 1) * 64);
+      fetch(kB, vB, ksB, vsB, blk + 1, ctx - 1 - (blk + 1) * 64);
       __builtin_amdgcn_sched_barrier(0);
-      score(kA, vA, blk);
+      score(kA, vA, ksA, vsA, blk);
       __builtin_amdgcn_sched_barrier(0);
-      fetch(kA, vA, min(blk + 2, blk1 - 1), ctx - 1 - min(blk + 2, blk1 - 1) * 64);
+      fetch(kA, vA, ksA, vsA, min(blk + 2, blk1 - 1), ctx - 1 - min(blk + 2, blk1 - 1) * 64);
       __builtin_amdgcn_sched_barrier(0);
-      score(kB, vB, blk + 1);
+      score(kB, vB, ksB, vsB, blk + 1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (blk < blk1) score(kA, vA, blk);
+    if (blk < blk1) score(kA, vA, ksA, vsA, blk);
   }
   LSA_STAMP(3);
 
@@ -321,9 +389,14 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     // the workgroup covering position tpos appends the new token's k / v to the cache: after its score loop
     // (which substitutes them from LDS / registers where it meets tpos), off the prologue's critical path
     if (lg >= G && lg < G + 2 && blk0 < nblk && blk1 == nblk) {
-      const size_t co = (((size_t)block_tables[(size_t)b * max_blocks + (tpos >> 6)] * Hkv + hk) * 64 +
-                         (tpos & 63)) * D + li * 8;
-      *reinterpret_cast<uint4*>((lg == G ? ra.kc : ra.vc) + co) = qkv_s[lg][li];
+      const size_t row = ((size_t)block_tables[(size_t)b * max_blocks + (tpos >> 6)] * Hkv + hk) * 64 + (tpos & 63);
+      if constexpr (KV8) {
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(lg == G ? ra.kc : ra.vc) + row * D + li * 8) =
+            new8_s[lg - G][li];
+        if (li == 0) (lg == G ? ra.ks : ra.vs)[row] = newsc_s[lg - G];
+      } else {
+        *reinterpret_cast<uint4*>((lg == G ? ra.kc : ra.vc) + row * D + li * 8) = qkv_s[lg][li];
+      }
     }
   }
   // merge the 4 lane groups of each wave in registers (xor-16 / xor-32 lane exchanges), then the WV wave
@@ -476,10 +549,12 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
                                const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit,
                                int unsplit_max, void* out, float* opart, float* mlpart, int* counters, int xf_mt,
                                const float* qkv_parts, int nparts,
-                               long part_stride, const float* cos_t, const float* sin_t, hipStream_t s) {
+                               long part_stride, const float* cos_t, const float* sin_t, const float* ks,
+                               const float* vs, hipStream_t s) {
   if (H % Hkv) return -1;
   if (xf_mt && B > 16 * xf_mt) return -4;
   if (nsplit > 256) return -3;
+  if ((ks == nullptr) != (vs == nullptr)) return -5;
   const int G = H / Hkv;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid(Hkv, B, nsplit);
@@ -488,11 +563,18 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
   const uint16_t* vv = reinterpret_cast<const uint16_t*>(vc);
   uint16_t* oo = reinterpret_cast<uint16_t*>(out);
   const RopeArgs ra{qkv_parts, (size_t)part_stride, nparts, cos_t, sin_t, const_cast<uint16_t*>(kk),
-                    const_cast<uint16_t*>(vv)};
-#define LSA_ADK(GV, RP)                                                                                      \
-  hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4)>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, qq, kk, \
-                     vv, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart, counters,  \
-                     xf_mt, ra)
+                    const_cast<uint16_t*>(vv), const_cast<float*>(ks), const_cast<float*>(vs)};
+#define LSA_ADK(GV, RP)                                                                                               \
+  do {                                                                                                                 \
+    if (ks)                                                                                                            \
+      hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4), true>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, \
+                         qq, kk, vv, ks, vs, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max,  \
+                         oo, opart, mlpart, counters, xf_mt, ra);                                                      \
+    else                                                                                                               \
+      hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4)>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, qq,   \
+                         kk, vv, ks, vs, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max,   \
+                         oo, opart, mlpart, counters, xf_mt, ra);                                                      \
+  } while (0)
 #define LSA_AD(GV)                                  \
   case GV:                                          \
     if (!qkv_parts) LSA_ADK(GV, 0);                 \

@@ -122,6 +122,28 @@ __device__ __forceinline__ uint2 pack8_fp8(const float* f, float inv) {
   return make_uint2((unsigned)lo, (unsigned)hi);
 }
 
+// 8 OCP e4m3 bytes -> 8 bf16 (v_cvt_scalef32_pk_bf16_fp8 at unit scale; exact: every e4m3 value is a bf16 value)
+__device__ __forceinline__ uint4 fp8x8_to_bf16x8(const uint2 q) {
+  uint4 r;
+  r.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q.x, 1.0f, false));
+  r.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q.x, 1.0f, true));
+  r.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q.y, 1.0f, false));
+  r.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q.y, 1.0f, true));
+  return r;
+}
+
+// 8 OCP e4m3 bytes -> 8 floats (v_cvt_pk_f32_fp8)
+__device__ __forceinline__ void fp8x8_to_f32(const uint2 q, float* f) {
+  const f32x2_t a = __builtin_amdgcn_cvt_pk_f32_fp8((int)q.x, false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)q.x, true);
+  const f32x2_t c = __builtin_amdgcn_cvt_pk_f32_fp8((int)q.y, false), d = __builtin_amdgcn_cvt_pk_f32_fp8((int)q.y, true);
+  f[0] = a[0]; f[1] = a[1]; f[2] = b[0]; f[3] = b[1]; f[4] = c[0]; f[5] = c[1]; f[6] = d[0]; f[7] = d[1];
+}
+
+// fp8 KV cache (ops.KV_FP8): every (token, kv-head) row of 128 values is stored as e4m3(x * 448 / amax) with the
+// f32 scale amax / 448 beside it (ops/reference.py quant_kv_rows is the host twin of these two formulas)
+#define LSA_KV8_RMAX (1.0f / 448.0f)
+__device__ __forceinline__ float kv8_inv(float amax) { return amax > 0.f ? 448.0f / amax : 0.f; }
+
 // Element offset of activation (m, k) in the fragment-major decode layout Xf[k/32][mt][64 lanes][8]
 // (lane = 16 * ((k % 32) / 8) + m % 16): one MFMA B-fragment per (k-step, 16-row tile) is 1 KiB
 // lane-linear.  8 consecutive k starting at a multiple of 8 are contiguous.

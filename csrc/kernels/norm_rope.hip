@@ -168,14 +168,18 @@ extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long pa
 // block_tables[seq * max_blocks + pos / 64], slot pos % 64.  cos/sin: [max_pos, 64] f32.
 // One workgroup per token; each thread rotates 4 (d, d+64) pairs (8 B loads of both halves).
 // ------------------------------------------------------------------------------------------------
-template <int NP>  // NP = 0: bf16 qkv rows; NP > 0: that many f32 split-K slabs; NP < 0: runtime count
+// KV8: fp8 cache -- kc / vc are e4m3 bytes and every (token, kv-head) row is stored as e4m3(x * 448 / amax)
+// with amax / 448 in ks / vs [nblk, Hkv, 64] (common.h kv8_inv); the 16 threads of a head (aligned lanes)
+// reduce the row's amax with xor shuffles.
+template <int NP, bool KV8 = false>  // NP = 0: bf16 qkv rows; NP > 0: that many f32 split-K slabs; NP < 0: runtime
 __global__ __launch_bounds__(1024) void rope_append_kernel(const uint16_t* __restrict__ qkv, const float* __restrict__ qkv_parts,
                                                           int nparts, size_t part_stride, const int* __restrict__ pos,
                                                           const int* __restrict__ tok_seq,
                                                           const int* __restrict__ block_tables, int max_blocks,
                                                           const float* __restrict__ cos_t,
                                                           const float* __restrict__ sin_t, uint16_t* __restrict__ q_out,
-                                                          uint16_t* __restrict__ kc, uint16_t* __restrict__ vc, int H,
+                                                          uint16_t* __restrict__ kc, uint16_t* __restrict__ vc,
+                                                          float* __restrict__ ks, float* __restrict__ vs, int H,
                                                           int Hkv) {
   constexpr int D = 128;
   const int t = blockIdx.x;
@@ -226,6 +230,26 @@ __global__ __launch_bounds__(1024) void rope_append_kernel(const uint16_t* __res
       y0[j] = x0[j] * cc[j] - x1[j] * sn[j];
       y1[j] = x1[j] * cc[j] + x0[j] * sn[j];
     }
+    if (KV8 && hd >= H) {  // (uniform over the 16 lanes of a head)
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a = fmaxf(a, fmaxf(fabsf(y0[j]), fabsf(y1[j])));
+      a = fmaxf(a, __shfl_xor(a, 8, 64));
+      a = fmaxf(a, __shfl_xor(a, 4, 64));
+      a = fmaxf(a, __shfl_xor(a, 2, 64));
+      a = fmaxf(a, __shfl_xor(a, 1, 64));
+      const float inv = kv8_inv(a);
+      const size_t r8 = ((size_t)blk * Hkv + (hd - H)) * 64 + off;
+      uint8_t* dst8 = reinterpret_cast<uint8_t*>(kc) + r8 * D;
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(y0[0] * inv, y0[1] * inv, 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(y0[2] * inv, y0[3] * inv, lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(y1[0] * inv, y1[1] * inv, 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(y1[2] * inv, y1[3] * inv, hi, true);
+      *reinterpret_cast<int*>(dst8 + d0) = lo;
+      *reinterpret_cast<int*>(dst8 + d0 + 64) = hi;
+      if (d0 == 0) ks[r8] = a * LSA_KV8_RMAX;
+      continue;
+    }
     uint2 olo, ohi;
     olo.x = pack2bf(y0[0], y0[1]); olo.y = pack2bf(y0[2], y0[3]);
     ohi.x = pack2bf(y1[0], y1[1]); ohi.y = pack2bf(y1[2], y1[3]);
@@ -241,6 +265,26 @@ __global__ __launch_bounds__(1024) void rope_append_kernel(const uint16_t* __res
   // v copy: Hkv * 16 chunks of 8 bf16
   for (int it = threadIdx.x; it < Hkv * 16; it += blockDim.x) {
     const int hv = it >> 4, c = (it & 15) * 8;
+    if constexpr (KV8) {
+      float f[8];
+      if constexpr (NP != 0) {
+        load4((H + Hkv + hv) * D + c, f);
+        load4((H + Hkv + hv) * D + c + 4, f + 4);
+      } else {
+        unpack8(*reinterpret_cast<const uint4*>(row + (H + Hkv + hv) * D + c), f);
+      }
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a = fmaxf(a, fabsf(f[j]));
+      a = fmaxf(a, __shfl_xor(a, 8, 64));
+      a = fmaxf(a, __shfl_xor(a, 4, 64));
+      a = fmaxf(a, __shfl_xor(a, 2, 64));
+      a = fmaxf(a, __shfl_xor(a, 1, 64));
+      const size_t r8 = ((size_t)blk * Hkv + hv) * 64 + off;
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(vc) + r8 * D + c) = pack8_fp8(f, kv8_inv(a));
+      if (c == 0) vs[r8] = a * LSA_KV8_RMAX;
+      continue;
+    }
     uint4 v;
     if constexpr (NP != 0) {
       float f[8];
@@ -256,8 +300,9 @@ __global__ __launch_bounds__(1024) void rope_append_kernel(const uint16_t* __res
 
 extern "C" int lsa_rope_append(const void* qkv, const float* qkv_parts, int nparts, long part_stride, const int* pos, const int* tok_seq, const int* block_tables,
                                int max_blocks, const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc,
-                               int T, int H, int Hkv, hipStream_t s) {
+                               float* ks, float* vs, int T, int H, int Hkv, hipStream_t s) {
   if (T <= 0) return 0;
+  if ((ks == nullptr) != (vs == nullptr)) return -5;
   // one rotation item per thread where possible (the decode case is latency-bound)
   const int items = (H + Hkv) * 16;
   const int nt = items >= 1024 ? 1024 : (items + 63) / 64 * 64;
@@ -265,9 +310,17 @@ extern "C" int lsa_rope_append(const void* qkv, const float* qkv_parts, int npar
   uint16_t* qo = reinterpret_cast<uint16_t*>(q_out);
   uint16_t* k16 = reinterpret_cast<uint16_t*>(kc);
   uint16_t* v16 = reinterpret_cast<uint16_t*>(vc);
-#define LSA_RA(NP)                                                                                              \
-  hipLaunchKernelGGL(rope_append_kernel<NP>, dim3(T), dim3(nt), 0, s, q16, qkv_parts, nparts, (size_t)part_stride, \
-                     pos, tok_seq, block_tables, max_blocks, cos_t, sin_t, qo, k16, v16, H, Hkv)
+#define LSA_RA(NP)                                                                                                   \
+  do {                                                                                                                \
+    if (ks)                                                                                                           \
+      hipLaunchKernelGGL((rope_append_kernel<NP, true>), dim3(T), dim3(nt), 0, s, q16, qkv_parts, nparts,             \
+                         (size_t)part_stride, pos, tok_seq, block_tables, max_blocks, cos_t, sin_t, qo, k16, v16, ks, vs, \
+                         H, Hkv);                                                                                     \
+    else                                                                                                              \
+      hipLaunchKernelGGL((rope_append_kernel<NP>), dim3(T), dim3(nt), 0, s, q16, qkv_parts, nparts,                   \
+                         (size_t)part_stride, pos, tok_seq, block_tables, max_blocks, cos_t, sin_t, qo, k16, v16, ks, vs, \
+                         H, Hkv);                                                                                     \
+  } while (0)
   switch (qkv_parts ? nparts : 0) {
     case 0: LSA_RA(0); break;
     case 1: LSA_RA(1); break;

@@ -43,6 +43,8 @@ class Settings:
     checkpoint_dir: Optional[str] = dataclasses.field(default_factory=lambda: _env("CHECKPOINT_DIR", None))
     dtype: str = dataclasses.field(default_factory=lambda: _env("DTYPE", "bf16"))
     explain_dtype: str = dataclasses.field(default_factory=lambda: _env("EXPLAIN_DTYPE", "bf16"))
+    # paged KV cache dtype of every engine: "bf16" | "fp8" (e4m3 rows + per-row scales, ops.KV_FP8)
+    kv_dtype: str = dataclasses.field(default_factory=lambda: _env("KV_DTYPE", "bf16"))
     tp: int = dataclasses.field(default_factory=lambda: _env("TP", 1, int))
     dp: int = dataclasses.field(default_factory=lambda: _env("DP", 1, int))
     max_batch: int = dataclasses.field(default_factory=lambda: _env("MAX_BATCH", 32, int))

@@ -42,8 +42,13 @@ class ModelRunner:
     def __init__(self, weights: LlamaWeights, max_slots: int = 32, max_model_len: int = 4096,
                  num_kv_blocks: Optional[int] = None, kv_memory_fraction: float = 0.85,
                  max_new_cap: Optional[int] = None, tp=None, use_graphs: bool = True, steps_per_graph: int = 1,
-                 fuse_rope: Optional[bool] = None, seq_parallel: Optional[bool] = None, sp_min_tokens: Optional[int] = None):
+                 fuse_rope: Optional[bool] = None, seq_parallel: Optional[bool] = None, sp_min_tokens: Optional[int] = None,
+                 kv_dtype: Optional[str] = None):
         self.w = weights
+        # paged KV cache dtype: "bf16" or "fp8" (e4m3 rows with per-(token, kv-head) scales, ops.KV_FP8)
+        kv_dtype = kv_dtype or ("fp8" if ops.KV_FP8 else "bf16")
+        assert kv_dtype in ("bf16", "fp8"), kv_dtype
+        self.kv_fp8 = kv_dtype == "fp8"
         # Megatron sequence parallelism for TP prefill (SURVEY.md §2.6 P-SP): reduce-scatter the row-parallel
         # outputs, residual + RMSNorm on T/tp rows, all-gather the bf16 normalised activations
         self.seq_parallel = (os.environ.get("LSA_SEQ_PARALLEL", "1") != "0") if seq_parallel is None else seq_parallel
@@ -74,8 +79,8 @@ class ModelRunner:
         self.steps_per_graph = steps_per_graph
         dev = self.device
 
-        # ---------------- KV cache: [L, 2, blocks, Hkv, 64, D] bf16
-        per_block = self.L * 2 * self.Hkv * BLOCK * self.D * 2
+        # ---------------- KV cache: [L, 2, blocks, Hkv, 64, D] bf16, or e4m3 bytes + [L, 2, blocks, Hkv, 64] f32 scales
+        per_block = self.L * 2 * self.Hkv * BLOCK * ((self.D + 4) if self.kv_fp8 else self.D * 2)
         want = max_slots * self.max_blocks + 1
         if num_kv_blocks is None:
             if self.on_gpu:
@@ -85,8 +90,10 @@ class ModelRunner:
             else:
                 num_kv_blocks = want
         self.num_kv_blocks = int(num_kv_blocks)
-        self.kv = torch.zeros(self.L, 2, self.num_kv_blocks, self.Hkv, BLOCK, self.D, dtype=torch.bfloat16,
-                              device=dev)
+        self.kv = torch.zeros(self.L, 2, self.num_kv_blocks, self.Hkv, BLOCK, self.D,
+                              dtype=torch.uint8 if self.kv_fp8 else torch.bfloat16, device=dev)
+        self.kv_scale = (torch.zeros(self.L, 2, self.num_kv_blocks, self.Hkv, BLOCK, dtype=torch.float32, device=dev)
+                         if self.kv_fp8 else None)
         # one row per position the block tables can address (the kernels check this bound on the host)
         cos, sin = ref.rope_tables(self.D, self.max_blocks * BLOCK, spec.rope_theta, spec.rope_scaling, device=dev)
         self.cos, self.sin = cos.contiguous(), sin.contiguous()
@@ -174,7 +181,8 @@ class ModelRunner:
         # batch-1 attention + O projection in one launch (ops.attn_o_b1): MHA, bf16 weights, contexts planned
         # within 512 tokens (the attention is unsplit there)
         self.attn_o = (ops.ATTN_O and self.on_gpu and tps == 1 and self.H == self.Hkv and self.D == 128
-                       and self.d % 512 == 0 and self.H % 8 == 0 and weights.layers[0].wo.kind == "bf16")
+                       and self.d % 512 == 0 and self.H % 8 == 0 and weights.layers[0].wo.kind == "bf16"
+                       and not self.kv_fp8)
         self.ao_slabs = torch.zeros(self.H * self.d if self.attn_o else 1, **f32)
         self.graphs: dict = {}
         self._pending_bt: dict = {}  # slot -> block-table row of a prompt still being prefilled in chunks
@@ -182,6 +190,10 @@ class ModelRunner:
             self.tp.warmup()  # communicators (RCCL + the one-shot IPC all-reduce) before any launch
 
     # ------------------------------------------------------------------------------------ helpers
+    def _kv_scales(self, l: int):
+        """(ks, vs) scale tensors of layer l's fp8 cache, None for a bf16 cache."""
+        return (self.kv_scale[l, 0], self.kv_scale[l, 1]) if self.kv_fp8 else None
+
     def _reduce_parts(self, parts: torch.Tensor) -> torch.Tensor:
         """TP all-reduce of a row-parallel GEMM's split-K slabs; returns what the next add_rmsnorm sums."""
         if self.tp is None or self.tp.size == 1:
@@ -282,12 +294,13 @@ class ModelRunner:
                 lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
             kc, vc = self.kv[l, 0], self.kv[l, 1]
             if not self.fuse_rope:
-                ops.rope_append(qkv_parts, pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv)
+                ops.rope_append(qkv_parts, pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv,
+                                kv_scales=self._kv_scales(l))
             fr = self.fuse_rope
             ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale,
                             attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
                             qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
-                            sin=self.sin if fr else None)
+                            sin=self.sin if fr else None, kv_scales=self._kv_scales(l))
             lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
             o_red = self._reduce_parts(o_parts)
             ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
@@ -346,7 +359,7 @@ class ModelRunner:
                 continue
             ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale,
                             attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
-                            qkv_parts=qkv_parts, cos=self.cos, sin=self.sin)
+                            qkv_parts=qkv_parts, cos=self.cos, sin=self.sin, kv_scales=self._kv_scales(l))
             lin(attn, lw.wo, "res", out=o_parts, splitk=sk_o, res=(h, xn, ssq[2 * l + 1], tk))
             lin(xn, lw.w_gate_up, "silu", out=act, rownorm=(ssq[2 * l + 1], self.eps))
             lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk))
@@ -528,6 +541,8 @@ class ModelRunner:
                     del self._pending_bt[sl]
         work = None
         self._cu_host = cu  # host offsets: the prefill attention kernel choice (ops._prefill_kernel)
+        # fp8 cache: the bf16 scratch every layer's prefill attention widens its blocks into (ops.kv8_scratch)
+        self._kv8_scratch = ops.kv8_scratch(ctx, self.Hkv, dev) if (self.kv_fp8 and self.on_gpu) else None
         if self.on_gpu:
             work = torch.tensor(ops.prefill_work(cu, ctx=ctx, heads=self.H), dtype=torch.int32).to(dev, non_blocking=True)
 
@@ -606,15 +621,16 @@ class ModelRunner:
 
     def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T):
         kc, vc = self.kv[l, 0], self.kv[l, 1]
+        kvs = self._kv_scales(l)
         sk_q = self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D)
         if sk_q > 1:  # small tile grid: f32 split-K slabs, summed by rope_append while it rotates
             parts = ops.linear(xn, lw.wqkv, "f32", splitk=sk_q)
-            ops.rope_append(parts, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
+            ops.rope_append(parts, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)
         else:
             ops.linear(xn, lw.wqkv, "bf16", out=qkv)
-            ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
+            ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)
         ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
-                         work=work, cu_list=self._cu_host)
+                         work=work, cu_list=self._cu_host, kv_scales=kvs, kv8_scratch_=self._kv8_scratch)
 
     def _prefill_layers_sp(self, T, ids, posd, tsd, bt, cud, ctxd, last, work, n, commit):
         """Sequence-parallel prefill under TP: rank r owns rows [r*Tl, (r+1)*Tl) of the residual stream.

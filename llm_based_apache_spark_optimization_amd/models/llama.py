@@ -181,7 +181,8 @@ def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[st
 
 @torch.no_grad()
 def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant_rows: int = 0,
-                      decode_a8: bool = False, decode_a8_mlp: Optional[bool] = None) -> torch.Tensor:
+                      decode_a8: bool = False, decode_a8_mlp: Optional[bool] = None,
+                      kv_fp8: bool = False) -> torch.Tensor:
     """fp32 causal forward of one sequence over the weights exactly as packed (``dense()`` undoes the
     fragment shuffle and the fp8 quantisation, so an fp8 model is compared against its own dequantised
     weights): logits [T, V] f32.  The numerics oracle for the engine at production shapes
@@ -193,7 +194,9 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
     ``decode_a8`` (the W8A8 decode GEMMs of fragment-major buckets, ops.linear_a8) the qkv / gate_up inputs of
     the rows past the prompt are rounded per row to e4m3 from the f32 norm output (as add_rmsnorm's fp8
     output does), o / down inputs stay bf16.  ``decode_a8_mlp`` (default: = decode_a8) sets the gate_up input
-    separately (the engine runs gate_up W8A8 from a smaller batch than qkv)."""
+    separately (the engine runs gate_up W8A8 from a smaller batch than qkv).  ``kv_fp8``: the engine's fp8 KV
+    cache (ops.KV_FP8) -- every rotated key and value row is rounded per (token, kv-head) to e4m3 with its
+    amax / 448 scale (ops.reference.quant_kv_rows) before attention."""
     from ..ops import reference as ref
 
     spec, dev = w.spec, w.device
@@ -248,7 +251,10 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
         q = qkv[:, : H * hd].view(T, H, hd)
         k = qkv[:, H * hd:(H + Hkv) * hd].view(T, Hkv, hd)
         v = qkv[:, (H + Hkv) * hd:].view(T, Hkv, hd)
-        q, k, v = bf(rope(q)), bf(rope(k)), bf(v)
+        if kv_fp8:
+            q, k, v = bf(rope(q)), ref.dequant_kv_rows(*ref.quant_kv_rows(rope(k))), ref.dequant_kv_rows(*ref.quant_kv_rows(v))
+        else:
+            q, k, v = bf(rope(q)), bf(rope(k)), bf(v)
         k, v = k.repeat_interleave(G, 1), v.repeat_interleave(G, 1)
         s = torch.einsum("qhd,khd->hqk", q, k) / math.sqrt(hd) + mask
         a = bf(torch.einsum("hqk,khd->qhd", s.softmax(-1), v).reshape(T, H * hd))

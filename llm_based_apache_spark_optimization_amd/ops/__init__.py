@@ -594,10 +594,13 @@ def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
     return xn
 
 
-def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv):
+def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, kv_scales=None):
+    """RoPE of q / k and the paged-cache append of k / v.  kv_scales = (ks, vs): fp8 cache (``KV_FP8``), kc / vc
+    are uint8 e4m3 bytes and every (token, kv-head) row is stored with its own f32 scale."""
     if not _gpu(qkv):
-        return ref.rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
-    ext().rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
+        return ref.rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, kv_scales)
+    ks, vs = kv_scales if kv_scales is not None else (None, None)
+    ext().rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, ks, vs)
 
 
 def silu_parts(parts: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -623,6 +626,25 @@ def silu_mul(g: torch.Tensor, u: torch.Tensor, out: Optional[torch.Tensor] = Non
 
 
 # ----------------------------------------------------------------------------------- attention
+# fp8 KV cache (LSA_KV_FP8=1 or ModelRunner(kv_dtype="fp8")): the paged cache holds e4m3 bytes with one f32 scale
+# per (token, kv-head) row of 128 values (amax / 448) -- half the bytes of the memory-bound decode attention and
+# twice the tokens per GiB of cache.  Decode attention reads the bytes directly; prefill widens the blocks it
+# attends to into a bf16 scratch per layer (kv8_dequant).  Off by default: it is a lossy cache (relative error
+# ~2^-4 per element), checked against the oracle's own fp8-cache emulation (models.llama.reference_forward kv_fp8).
+KV_FP8 = os.environ.get("LSA_KV_FP8", "0") == "1"
+
+
+def kv8_scratch(ctx: list[int], Hkv: int, device) -> tuple:
+    """(ko, vo, table) for ``attn_prefill``'s fp8 path: compact bf16 scratch of every block the sequences with
+    contexts ``ctx`` attend to (sequence i's block j at i * mb + j) and the matching [n, mb] block table."""
+    mb = max(1, max((c + 63) // 64 for c in ctx))
+    n = len(ctx)
+    ko = torch.empty(n * mb, Hkv, 64, 128, dtype=torch.bfloat16, device=device)
+    vo = torch.empty_like(ko)
+    table = torch.arange(n * mb, dtype=torch.int32, device=device).view(n, mb)
+    return ko, vo, table
+
+
 def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int, int]:
     """(chunk_blocks, nsplit, unsplit_max) grid plan of split-KV decode for contexts up to max_ctx.  The
     kernel picks each sequence's own split from its length (csrc/kernels/attention.hip eff_split):
@@ -658,19 +680,20 @@ def decode_workspace(B: int, H: int, Hkv: int, nsplit: int, device) -> tuple:
 
 
 def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None, xf=False,
-                qkv_parts=None, cos=None, sin=None):
+                qkv_parts=None, cos=None, sin=None, kv_scales=None):
     """q [B,H,128] vs paged cache, context = pos + 1.  workspace = decode_workspace(...) for split-KV.
     xf=True: out is a flat buffer receiving the fragment-major layout of the [B, H*128] output.
     qkv_parts ([S, B, (H+2Hkv)*128] f32 split-K slabs of the QKV projection) + cos/sin: RoPE and the
-    KV-cache append of the new token are fused in (``q`` is then only a [B, H, 128] scratch buffer)."""
+    KV-cache append of the new token are fused in (``q`` is then only a [B, H, 128] scratch buffer).
+    kv_scales = (ks, vs): fp8 cache (see ``KV_FP8``)."""
     B = pos.shape[0]
     if not _gpu(pos):
         if qkv_parts is not None:
-            ref.rope_append(qkv_parts, pos, None, block_tables, cos, sin, q, kc, vc, H, Hkv)
+            ref.rope_append(qkv_parts, pos, None, block_tables, cos, sin, q, kc, vc, H, Hkv, kv_scales)
         if not xf:
-            return ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out)
+            return ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, kv_scales)
         tmp = torch.empty(B, H, q.shape[-1], dtype=torch.bfloat16, device=q.device)
-        ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, tmp)
+        ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, tmp, kv_scales)
         f = to_xfrag(tmp.view(B, -1))
         out.view(-1)[: f.numel()].copy_(f)
         return out
@@ -680,8 +703,9 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     if workspace is None:
         workspace = decode_workspace(B, H, Hkv, nsplit, q.device)
     opart, mlpart, counters = workspace
+    ks, vs = kv_scales if kv_scales is not None else (None, None)
     ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart, counters,
-                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max)
+                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs)
     return out
 
 
@@ -779,11 +803,18 @@ def _pair_blocks(n_items: int, heads: int, longest: int, qblock: int) -> bool:
     return n_items * heads <= 512 or longest >= 32 * qblock
 
 
-def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, work=None, cu_list=None):
+def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, work=None, cu_list=None,
+                 kv_scales=None, kv8_scratch_=None):
     """Causal prefill attention of packed sequences (cu_q offsets) over the paged cache.  ``work`` must
-    come from ``prefill_work`` of the same offsets (``cu_list``, host copy: picks the kernel)."""
+    come from ``prefill_work`` of the same offsets (``cu_list``, host copy: picks the kernel).
+    kv_scales = (ks, vs): fp8 cache -- the attended blocks are widened into ``kv8_scratch_`` (= kv8_scratch(ctx,
+    ...), built from the host context list; made here when not given) and the bf16 kernels run on that."""
     if not _gpu(q):
-        return ref.attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out)
+        return ref.attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, kv_scales)
+    if kv_scales is not None:
+        ko, vo, table = kv8_scratch_ if kv8_scratch_ is not None else kv8_scratch(ctx_lens.tolist(), Hkv, q.device)
+        ext().kv8_dequant(kc, vc, kv_scales[0], kv_scales[1], block_tables, ctx_lens, table.shape[1], ko, vo)
+        kc, vc, block_tables = ko, vo, table
     cu = cu_list if cu_list is not None else cu_q.tolist()
     if work is None:
         work = torch.tensor(prefill_work(cu, ctx=ctx_lens.tolist(), heads=H), dtype=torch.int32).to(q.device)

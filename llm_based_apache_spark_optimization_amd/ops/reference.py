@@ -69,7 +69,25 @@ def _slots(pos, tok_seq, block_tables):
     return blk, p % BLOCK
 
 
-def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv):
+# fp8 KV cache rows (csrc/kernels/common.h kv8_inv / LSA_KV8_RMAX): e4m3(x * (448 / amax)) with scale amax * (1/448)
+KV8_RMAX = torch.tensor(1.0 / 448.0, dtype=torch.float32)
+
+
+def quant_kv_rows(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """x f32 [..., 128] -> (e4m3 bytes as uint8 [..., 128], f32 scales [...]) per row of 128 values."""
+    x = x.float()
+    a = x.abs().amax(-1)
+    inv = torch.where(a > 0, torch.tensor(448.0, dtype=torch.float32, device=x.device) / a.clamp_min(1e-38),
+                      torch.zeros_like(a))
+    q = (x * inv.unsqueeze(-1)).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q, a * KV8_RMAX.to(x.device)
+
+
+def dequant_kv_rows(q: torch.Tensor, sc: torch.Tensor) -> torch.Tensor:
+    return q.view(torch.float8_e4m3fn).float() * sc.float().unsqueeze(-1)
+
+
+def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, kv_scales=None):
     if qkv.dtype == torch.float32 and qkv.dim() == 3:  # f32 split-K slabs [S, T, n]
         qkv = qkv.sum(0)
     T = qkv.shape[0]
@@ -83,31 +101,44 @@ def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H,
     rot = torch.cat([lo * c - hi * s, hi * c + lo * s], dim=-1)
     q_out.copy_(rot[:, :H].to(torch.bfloat16).view_as(q_out))
     blk, off = _slots(pos, tok_seq, block_tables)
+    if kv_scales is not None:  # fp8 cache: quantise each (token, kv-head) row
+        ks, vs = kv_scales
+        k8, ksc = quant_kv_rows(rot[:, H:])
+        v8, vsc = quant_kv_rows(x[:, H + Hkv:])
+        kc[blk, :, off] = k8
+        vc[blk, :, off] = v8
+        ks[blk, :, off] = ksc
+        vs[blk, :, off] = vsc
+        return
     kc[blk, :, off] = rot[:, H:].to(kc.dtype)
     vc[blk, :, off] = x[:, H + Hkv:].to(vc.dtype)
 
 
-def _gather_kv(cache, table_row, n):
+def _gather_kv(cache, table_row, n, scales=None):
     nb = (n + BLOCK - 1) // BLOCK
     blocks = cache[table_row[:nb].long()]  # [nb, Hkv, 64, D]
+    if scales is not None:
+        blocks = dequant_kv_rows(blocks, scales[table_row[:nb].long()])
     return blocks.permute(1, 0, 2, 3).reshape(cache.shape[1], nb * BLOCK, cache.shape[3])[:, :n]
 
 
-def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out):
+def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, kv_scales=None):
     B = pos.shape[0]
     G = H // Hkv
+    ks, vs = kv_scales if kv_scales is not None else (None, None)
     for b in range(B):
         n = int(pos[b]) + 1
-        k = _gather_kv(kc, block_tables[b], n).float().repeat_interleave(G, 0)
-        v = _gather_kv(vc, block_tables[b], n).float().repeat_interleave(G, 0)
+        k = _gather_kv(kc, block_tables[b], n, ks).float().repeat_interleave(G, 0)
+        v = _gather_kv(vc, block_tables[b], n, vs).float().repeat_interleave(G, 0)
         s = torch.einsum("hd,hnd->hn", q[b].float(), k) * scale
         o = torch.einsum("hn,hnd->hd", s.softmax(-1), v)
         out[b] = o.to(out.dtype).view_as(out[b])
     return out
 
 
-def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out):
+def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, kv_scales=None):
     G = H // Hkv
+    ks, vs = kv_scales if kv_scales is not None else (None, None)
     cu = cu_q.tolist()
     for sq in range(len(cu) - 1):
         q0, q1 = cu[sq], cu[sq + 1]
@@ -115,8 +146,8 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out):
         if ql == 0:
             continue
         n = int(ctx_lens[sq])
-        k = _gather_kv(kc, block_tables[sq], n).float().repeat_interleave(G, 0)
-        v = _gather_kv(vc, block_tables[sq], n).float().repeat_interleave(G, 0)
+        k = _gather_kv(kc, block_tables[sq], n, ks).float().repeat_interleave(G, 0)
+        v = _gather_kv(vc, block_tables[sq], n, vs).float().repeat_interleave(G, 0)
         qq = q[q0:q1].float().transpose(0, 1)  # [H, ql, D]
         s = torch.einsum("hqd,hnd->hqn", qq, k) * scale
         qpos = torch.arange(n - ql, n, device=q.device).view(ql, 1)

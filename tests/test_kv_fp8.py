@@ -1,0 +1,97 @@
+"""fp8 KV cache (ops.KV_FP8) on CPU: the row quantiser's error bound, the reference ops over an e4m3 cache, and
+the whole engine with kv_dtype="fp8" against the oracle's own fp8-cache emulation (models.llama.reference_forward
+kv_fp8=True) -- the tolerance test the fp8 cache ships behind.  The HIP kernels are checked against these same
+reference ops in tests/test_kv_fp8_gpu.py."""
+import math
+
+import torch
+
+from llm_based_apache_spark_optimization_amd.config import Settings
+from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build_engine
+from llm_based_apache_spark_optimization_amd.models.llama import reference_forward
+from llm_based_apache_spark_optimization_amd.ops import reference as ref
+
+
+def test_quant_kv_rows_error_bound():
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(64, 8, 128, generator=g) * torch.logspace(-3, 2, 64).view(64, 1, 1)
+    x[3, 2] = 0.0  # an all-zero row: scale 0, bytes 0, exact
+    q, sc = ref.quant_kv_rows(x)
+    assert q.dtype == torch.uint8 and q.shape == x.shape and sc.shape == x.shape[:-1]
+    y = ref.dequant_kv_rows(q, sc)
+    amax = x.abs().amax(-1, keepdim=True)
+    # e4m3: 3 mantissa bits -> |err| <= 2^-4 |x| for normal codes, and <= half the subnormal step (2^-10 of the
+    # row's 448-scaled range) below them
+    bound = torch.maximum(x.abs() * 2.0 ** -4, amax / 448 * 2.0 ** -10) * 1.0001
+    assert ((y - x).abs() <= bound).all()
+    assert torch.equal(y[3, 2], torch.zeros(128)) and sc[3, 2] == 0
+    # the row maximum maps to 448 exactly (no saturation loss at the top of the range)
+    assert torch.allclose(y.abs().amax(-1), x.abs().amax(-1), rtol=1e-6)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+def test_reference_ops_fp8_cache_track_bf16():
+    """rope_append into an fp8 cache, then decode / prefill attention over it, stay within e4m3 noise of the
+    same ops over a bf16 cache."""
+    H, Hkv, D, nblk = 8, 2, 128, 5
+    g = torch.Generator().manual_seed(1)
+    cos, sin = ref.rope_tables(D, 512, 10000.0)
+    T = 150
+    qkv = torch.randn(T, (H + 2 * Hkv) * D, generator=g).to(torch.bfloat16)
+    pos = torch.arange(T, dtype=torch.int32)
+    tok_seq = torch.zeros(T, dtype=torch.int32)
+    bt = torch.tensor([[3, 1, 4]], dtype=torch.int32)
+    kb = torch.zeros(nblk, Hkv, 64, D, dtype=torch.bfloat16)
+    vb = torch.zeros_like(kb)
+    k8 = torch.zeros(nblk, Hkv, 64, D, dtype=torch.uint8)
+    v8 = torch.zeros_like(k8)
+    ks = torch.zeros(nblk, Hkv, 64)
+    vs = torch.zeros_like(ks)
+    q = torch.empty(T, H, D, dtype=torch.bfloat16)
+    q2 = torch.empty_like(q)
+    ref.rope_append(qkv, pos, tok_seq, bt, cos, sin, q, kb, vb, H, Hkv)
+    ref.rope_append(qkv, pos, tok_seq, bt, cos, sin, q2, k8, v8, H, Hkv, kv_scales=(ks, vs))
+    assert torch.equal(q, q2)
+    deq = ref.dequant_kv_rows(k8[1], ks[1])
+    assert _rel(deq, kb[1]) < 0.04 and ks[2].abs().sum() == 0  # block 2 is not in the table
+    cu = torch.tensor([0, T], dtype=torch.int32)
+    cl = torch.tensor([T], dtype=torch.int32)
+    o_b = torch.empty(T, H, D, dtype=torch.bfloat16)
+    o_8 = torch.empty_like(o_b)
+    ref.attn_prefill(q, kb, vb, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), o_b)
+    ref.attn_prefill(q, k8, v8, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), o_8, kv_scales=(ks, vs))
+    assert _rel(o_8, o_b) < 0.05
+    d_b = torch.empty(1, H, D, dtype=torch.bfloat16)
+    d_8 = torch.empty_like(d_b)
+    p = torch.tensor([T - 1], dtype=torch.int32)
+    ref.attn_decode(q[-1:], kb, vb, bt, p, H, Hkv, 1 / math.sqrt(D), d_b)
+    ref.attn_decode(q[-1:], k8, v8, bt, p, H, Hkv, 1 / math.sqrt(D), d_8, kv_scales=(ks, vs))
+    assert _rel(d_8, d_b) < 0.05
+    assert _rel(d_8[0], o_8[-1]) < 1e-2  # decode of the last row == the prefill's last row (same cache)
+
+
+def test_engine_kv_fp8_matches_oracle():
+    """Greedy decoding with the fp8 cache: every chosen token is within bf16 noise of the fp8-cache oracle's
+    argmax (teacher-forced), and the cache really is e4m3 (half the bytes per block)."""
+    eng = build_engine("tiny-nsql", device="cpu", max_slots=2, max_model_len=256, kv_dtype="fp8")
+    r = eng.runner
+    assert r.kv_fp8 and r.kv.dtype == torch.uint8 and r.kv_scale.shape == r.kv.shape[:-1]
+    prompts = [[1] + list(range(5, 45)), [1, 9, 8, 7, 6]]
+    res = eng.generate(prompts, SamplingParams(max_tokens=10, ignore_eos=True))
+    for p, out in zip(prompts, res):
+        lg = reference_forward(r.w, p + out.token_ids[:-1], kv_fp8=True)[len(p) - 1:]
+        chosen = lg.gather(1, torch.tensor(out.token_ids).view(-1, 1)).squeeze(1)
+        gap = ((lg.max(1).values - chosen) / lg.std(1)).max().item()
+        assert gap < 0.15, gap
+    bf = build_engine("tiny-nsql", device="cpu", max_slots=2, max_model_len=256)
+    assert bf.runner.kv.dtype == torch.bfloat16 and bf.runner.kv_scale is None
+
+
+def test_settings_kv_dtype(monkeypatch):
+    monkeypatch.setenv("LSA_KV_DTYPE", "fp8")
+    assert Settings().kv_dtype == "fp8"
+    monkeypatch.delenv("LSA_KV_DTYPE")
+    assert Settings().kv_dtype == "bf16"
