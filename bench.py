@@ -71,7 +71,13 @@ def check_numerics(eng, prompt, tokens, n=16, prefill_rows=0, decode_batch=0):
     gap = ((lg.max(1).values - chosen) / lg.std(1)).max().item()
     agree = int((lg.argmax(1).cpu() == torch.tensor(toks)).sum())
     del lg
-    if aq or da8 or da8m:
+    if r.kv_fp8:
+        # fp8 KV cache: every cached key / value row is rounded to e4m3 in the engine and in the oracle, from
+        # values that differ at the bf16 level, so rows near a rounding boundary differ by a full e4m3 step; over
+        # 32 layers on random-init weights (leading logits within a fraction of a std) that flips near-ties.
+        # Per-layer parity at the strict criterion is pinned by tests/test_kv_fp8_gpu.py (2-layer prod shapes)
+        ok, crit = gap < 1.0, "fp8 KV cache: gap < 1.0 std (quantisation-level; top-1 agreement reported)"
+    elif aq or da8 or da8m:
         # W8A8 prefill: every prompt activation is rounded to e4m3 (3 mantissa bits); the oracle rounds the
         # same rows, but values near a rounding boundary land on different sides in the two computations, so
         # the prompt's K/V differ by quantisation-level noise that 32 layers accumulate.  On random-init

@@ -67,10 +67,6 @@ struct RopeArgs {
   float* vs;
 };
 
-// K / V register image of one 8-dim lane slice: 8 bf16 (uint4) or, fp8 cache, 8 e4m3 bytes (uint2)
-template <bool KV8> struct KvLane { typedef uint4 T; };
-template <> struct KvLane<true> { typedef uint2 T; };
-
 // WV = waves per workgroup: 8 for G <= 3 (two keys per lane group per block -> half the K/V registers,
 // so four 4-wave-equivalents fit per CU and a B x Hkv = 1024 grid runs in whole rounds; G = 3: half the
 // per-wave score work on the latency-bound small grids, 3B B=32 ctx 200 11.1 -> 10.0 us), else 4 (the
@@ -80,6 +76,9 @@ template <> struct KvLane<true> { typedef uint2 T; };
 // the 7B B x Hkv = 1024 workgroups run in 1.33 rounds instead of two (7B B=32 ctx 200: 23.4 -> 21.0 us).
 #ifndef LSA_ATTN_WPE
 #define LSA_ATTN_WPE 6
+#endif
+#ifndef LSA_ATTN_WPE8
+#define LSA_ATTN_WPE8 6  // fp8 cache, G = 1 (8 = 64 VGPRs, one grid round at B x Hkv = 1024: spills, 7B b32 ctx 200 17.6 -> 18.2 us)
 #endif
 #ifndef LSA_ATTN_BUF_G
 #define LSA_ATTN_BUF_G 2
@@ -91,13 +90,14 @@ template <> struct KvLane<true> { typedef uint2 T; };
 #define LSA_ATTN_DOT2_G 99
 #endif
 //
-// KV8: fp8 cache (ops.KV_FP8) -- kc / vc hold e4m3 bytes [blocks, Hkv, 64, 128] and ksc / vsc the per-(token,
-// kv-head) f32 scales [blocks, Hkv, 64].  Same lane map with 8-byte K / V loads (half the HBM bytes of the
-// memory-bound score loop); a K slice is widened to bf16 exactly (v_cvt_scalef32_pk_bf16_fp8) for the same dot2
-// products and its scale multiplies the reduced score; a V slice goes to f32 with its scale folded into p.
+// KV8: fp8 cache (ops.KV_FP8) -- kc / vc hold e4m3 bytes, 8 KiB per (block, kv-head) tile in the token-pair
+// order of common.h kv8_off, and ksc / vsc the per-(token, kv-head) f32 scales [blocks, Hkv, 64].  Same 16-lane
+// groups of 8 dims, but one 16-byte load per lane now carries two keys (half the load instructions and half
+// the HBM bytes of the bf16 cache); a K slice is widened to bf16 exactly (v_cvt_scalef32_pk_bf16_fp8) for the
+// same dot2 products and its scale multiplies the reduced score; a V slice goes to f32 with its scale in p.
 template <int G, int ROPE, int WV, bool KV8 = false>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime
 __global__ __launch_bounds__(64 * WV)
-__attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+__attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (KV8 ? LSA_ATTN_WPE8 : LSA_ATTN_WPE) : 1))) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc,
                                                           const float* __restrict__ ksc, const float* __restrict__ vsc,
                                                           const int* __restrict__ block_tables, int max_blocks,
@@ -121,32 +121,33 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
   const int lg = tid >> 4, li = tid & 15, wv = tid >> 6;
   const int* bt = block_tables + (size_t)b * max_blocks;
   // K/V of block blk+1 are in flight while block blk is scored (two register sets, static names)
-  typedef typename KvLane<KV8>::T KT;
-  KT kA[TU], vA[TU], kB[TU], vB[TU];
-  float ksA[TU], vsA[TU], ksB[TU], vsB[TU];  // KV8 only: the keys' / values' row scales
+  // KV8: one 16-byte load carries the lane's 8 dims of a token PAIR (kv8_off), so NL = TU / 2 loads per block
+  constexpr int NL = KV8 ? TU / 2 : TU;
+  static_assert(!KV8 || TU % 2 == 0, "KV8 pairs keys");
+  uint4 kA[NL], vA[NL], kB[NL], vB[NL];
+  float2 ksA[NL], vsA[NL], ksB[NL], vsB[NL];  // KV8 only: the pair's key / value row scales
   // keys past the context in the last block re-read the last valid row (a cache hit, not HBM traffic);
   // they are masked in the score
   // G >= LSA_ATTN_BUF_G: one buffer resource per (block, kv-head) slab, built in SGPRs from the uniform
   // block-table entry, the lanes carry 32-bit offsets (3B: 10.3 -> 9.8 us at B = 32); G = 1 keeps 64-bit
   // global loads (buffer loads measured 20.7 -> 22.4 us for the 7B at B = 32)
   constexpr bool BUF = G >= LSA_ATTN_BUF_G;
-  auto fetch = [&](KT (&kr)[TU], KT (&vr)[TU], float (&ksr)[TU], float (&vsr)[TU], int blk, int last_tok) {
+  auto fetch = [&](uint4 (&kr)[NL], uint4 (&vr)[NL], float2 (&ksr)[NL], float2 (&vsr)[NL], int blk, int last_tok) {
     const size_t rowb = ((size_t)__builtin_amdgcn_readfirstlane(bt[blk]) * Hkv + hk) * 64;
     const size_t base = rowb * D;
 #pragma unroll
-    for (int u = 0; u < TU; ++u) {
+    for (int u = 0; u < NL; ++u) {
+      if constexpr (KV8) {  // pair pr = tokens 2 pr, 2 pr + 1 (clamped like single keys)
+        const int pr = min(wv * (TW / 2) + u * 4 + (lg & 3), last_tok >> 1);
+        const size_t off = base + kv8_off(2 * pr, li * 8);
+        kr[u] = ldg_nt(reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(kc) + off));
+        vr[u] = ldg_nt(reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(vc) + off));
+        ksr[u] = *reinterpret_cast<const float2*>(ksc + rowb + 2 * pr);
+        vsr[u] = *reinterpret_cast<const float2*>(vsc + rowb + 2 * pr);
+        continue;
+      }
       const int tok = min(wv * TW + u * 4 + (lg & 3), last_tok);
-      if constexpr (KV8) {
-        const uint8_t* k8 = reinterpret_cast<const uint8_t*>(kc) + base + tok * D + li * 8;
-        const uint8_t* v8 = reinterpret_cast<const uint8_t*>(vc) + base + tok * D + li * 8;
-        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-        const u32x2_t a = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(k8));
-        const u32x2_t c = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(v8));
-        kr[u] = make_uint2(a[0], a[1]);
-        vr[u] = make_uint2(c[0], c[1]);
-        ksr[u] = ksc[rowb + tok];
-        vsr[u] = vsc[rowb + tok];
-      } else if constexpr (BUF) {
+      if constexpr (BUF) {
         const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)(kc + base), 0, 64 * D * 2, 0x00020000);
         const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(vc + base), 0, 64 * D * 2, 0x00020000);
         const int off = (tok * D + li * 8) * 2;
@@ -282,17 +283,23 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
   }
 
-  auto score = [&](const KT (&kr)[TU], const KT (&vr)[TU], const float (&ksr)[TU], const float (&vsr)[TU], int blk) {
+  // key slot u of this lane group -> its position (KV8: slot u is half u & 1 of load u / 2's token pair)
+  auto slot_pos = [&](int blk, int u) {
+    return KV8 ? blk * 64 + 2 * (wv * (TW / 2) + (u >> 1) * 4 + (lg & 3)) + (u & 1) : blk * 64 + wv * TW + u * 4 + (lg & 3);
+  };
+  auto score = [&](const uint4 (&kr)[NL], const uint4 (&vr)[NL], const float2 (&ksr)[NL], const float2 (&vsr)[NL],
+                   int blk) {
     float s[TU][G];
 #pragma unroll
     for (int u = 0; u < TU; ++u) {
       uint4 kq;
       float ksu = 1.f;
-      const int tp = blk * 64 + wv * TW + u * 4 + (lg & 3);
+      const int tp = slot_pos(blk, u);
       const bool valid = tp < ctx;
       if constexpr (KV8) {
-        uint2 k8 = kr[u];
-        ksu = ksr[u];
+        const uint4 kp = kr[u >> 1];
+        uint2 k8 = (u & 1) ? make_uint2(kp.z, kp.w) : make_uint2(kp.x, kp.y);
+        ksu = (u & 1) ? ksr[u >> 1].y : ksr[u >> 1].x;
         if constexpr (ROPE != 0) {
           if (tp == tpos) {
             k8 = new8_s[0][li];
@@ -347,10 +354,11 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
       for (int u = 0; u < TU; ++u) {
         float vf[8], pu = p[u];
         if constexpr (KV8) {
-          uint2 v8 = vr[u];
-          float vsu = vsr[u];
+          const uint4 vp = vr[u >> 1];
+          uint2 v8 = (u & 1) ? make_uint2(vp.z, vp.w) : make_uint2(vp.x, vp.y);
+          float vsu = (u & 1) ? vsr[u >> 1].y : vsr[u >> 1].x;
           if constexpr (ROPE != 0) {
-            if (blk * 64 + wv * TW + u * 4 + (lg & 3) == tpos) {
+            if (slot_pos(blk, u) == tpos) {
               v8 = new8_s[1][li];
               vsu = newsc_s[1];
             }
@@ -391,8 +399,8 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? LSA_ATTN_WPE : 1))) void 
     if (lg >= G && lg < G + 2 && blk0 < nblk && blk1 == nblk) {
       const size_t row = ((size_t)block_tables[(size_t)b * max_blocks + (tpos >> 6)] * Hkv + hk) * 64 + (tpos & 63);
       if constexpr (KV8) {
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(lg == G ? ra.kc : ra.vc) + row * D + li * 8) =
-            new8_s[lg - G][li];
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(lg == G ? ra.kc : ra.vc) + (row - (tpos & 63)) * D +
+                                  kv8_off(tpos & 63, li * 8)) = new8_s[lg - G][li];
         if (li == 0) (lg == G ? ra.ks : ra.vs)[row] = newsc_s[lg - G];
       } else {
         *reinterpret_cast<uint4*>((lg == G ? ra.kc : ra.vc) + row * D + li * 8) = qkv_s[lg][li];

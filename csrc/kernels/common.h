@@ -142,6 +142,10 @@ __device__ __forceinline__ void fp8x8_to_f32(const uint2 q, float* f) {
 // fp8 KV cache (ops.KV_FP8): every (token, kv-head) row of 128 values is stored as e4m3(x * 448 / amax) with the
 // f32 scale amax / 448 beside it (ops/reference.py quant_kv_rows is the host twin of these two formulas)
 #define LSA_KV8_RMAX (1.0f / 448.0f)
+// Byte offset of (token t, dim d) inside one fp8 (block, kv-head) tile of 64 x 128 bytes: tokens are stored in
+// pairs, the 8-byte chunk d / 8 of tokens 2p and 2p + 1 side by side, so one 16-byte lane load carries its 8 dims
+// of two keys (ops/reference.py kv8_physical is the host twin)
+__device__ __forceinline__ int kv8_off(int t, int d) { return (((t >> 1) * 16 + (d >> 3)) * 2 + (t & 1)) * 8 + (d & 7); }
 __device__ __forceinline__ float kv8_inv(float amax) { return amax > 0.f ? 448.0f / amax : 0.f; }
 
 // Element offset of activation (m, k) in the fragment-major decode layout Xf[k/32][mt][64 lanes][8]

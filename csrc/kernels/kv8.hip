@@ -1,6 +1,7 @@
 // fp8 KV cache (ops.KV_FP8) support kernels.
 //
-// The cache stores every (token, kv-head) row of 128 values as e4m3 bytes with one f32 scale (written by
+// The cache stores every (token, kv-head) row of 128 values as e4m3 bytes (token-pair order, common.h kv8_off)
+// with one f32 scale (written by
 // rope_append_kernel<.., KV8> / attn_decode_kernel<.., KV8>).  Decode attention reads the bytes directly
 // (attention.hip).  Prefill attention is compute-bound MFMA work on bf16 LDS tiles, so the blocks a prefill batch
 // attends to are widened once per layer into a compact bf16 scratch (lsa_kv8_dequant) and the unchanged prefill
@@ -8,8 +9,9 @@
 // value, ~3 % of a 2k-token prefill layer's attention time.
 #include "common.h"
 
-// grid (mb, nseq * Hkv, 2): block j of sequence seq, kv head hk, K (z = 0) or V (z = 1); 256 threads, each one
-// quarter row (32 values) of the 64 x 128 tile.  Blocks at or past the sequence's context are skipped.
+// grid (mb, nseq * Hkv, 2): block j of sequence seq, kv head hk, K (z = 0) or V (z = 1); 256 threads, each two
+// 16-byte units of the tile (token pair p, 8-dim chunk ch: common.h kv8_off) -> 8 bf16 of tokens 2p and 2p + 1.
+// Blocks at or past the sequence's context are skipped.
 __global__ __launch_bounds__(256) void kv8_dequant_kernel(const uint8_t* __restrict__ kc, const uint8_t* __restrict__ vc,
                                                           const float* __restrict__ ks, const float* __restrict__ vs,
                                                           const int* __restrict__ block_tables, int max_blocks,
@@ -20,20 +22,23 @@ __global__ __launch_bounds__(256) void kv8_dequant_kernel(const uint8_t* __restr
   const bool isv = blockIdx.z != 0;
   const size_t src = ((size_t)block_tables[(size_t)seq * max_blocks + j] * Hkv + hk) * 64;
   const size_t dst = ((size_t)(seq * mb + j) * Hkv + hk) * 64;
-  const int row = threadIdx.x >> 2, c = (threadIdx.x & 3) * 32;
-  const uint8_t* s8 = (isv ? vc : kc) + (src + row) * 128 + c;
-  const float sc = (isv ? vs : ks)[src + row];
-  const uint4 a = *reinterpret_cast<const uint4*>(s8);
-  const uint4 b = *reinterpret_cast<const uint4*>(s8 + 16);
-  const uint2 part[4] = {make_uint2(a.x, a.y), make_uint2(a.z, a.w), make_uint2(b.x, b.y), make_uint2(b.z, b.w)};
-  uint16_t* o = (isv ? vo : ko) + (dst + row) * 128 + c;
+  const uint8_t* tile = (isv ? vc : kc) + src * 128;
+  const float* sc = (isv ? vs : ks) + src;
+  uint16_t* o = (isv ? vo : ko) + dst * 128;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 2; ++i) {
+    const int unit = threadIdx.x + 256 * i, p = unit >> 4, ch = unit & 15;
+    const uint4 q = *reinterpret_cast<const uint4*>(tile + unit * 16);  // == kv8_off(2 p, 8 ch)
+    const float2 s2 = *reinterpret_cast<const float2*>(sc + 2 * p);
     float f[8];
-    fp8x8_to_f32(part[i], f);
+    fp8x8_to_f32(make_uint2(q.x, q.y), f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] *= sc;
-    *reinterpret_cast<uint4*>(o + 8 * i) = pack8(f);
+    for (int e = 0; e < 8; ++e) f[e] *= s2.x;
+    *reinterpret_cast<uint4*>(o + (2 * p) * 128 + 8 * ch) = pack8(f);
+    fp8x8_to_f32(make_uint2(q.z, q.w), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] *= s2.y;
+    *reinterpret_cast<uint4*>(o + (2 * p + 1) * 128 + 8 * ch) = pack8(f);
   }
 }
 

@@ -240,13 +240,13 @@ __global__ __launch_bounds__(1024) void rope_append_kernel(const uint16_t* __res
       a = fmaxf(a, __shfl_xor(a, 1, 64));
       const float inv = kv8_inv(a);
       const size_t r8 = ((size_t)blk * Hkv + (hd - H)) * 64 + off;
-      uint8_t* dst8 = reinterpret_cast<uint8_t*>(kc) + r8 * D;
+      uint8_t* tile = reinterpret_cast<uint8_t*>(kc) + (r8 - off) * D;  // token-pair order (common.h kv8_off)
       int lo = __builtin_amdgcn_cvt_pk_fp8_f32(y0[0] * inv, y0[1] * inv, 0, false);
       lo = __builtin_amdgcn_cvt_pk_fp8_f32(y0[2] * inv, y0[3] * inv, lo, true);
       int hi = __builtin_amdgcn_cvt_pk_fp8_f32(y1[0] * inv, y1[1] * inv, 0, false);
       hi = __builtin_amdgcn_cvt_pk_fp8_f32(y1[2] * inv, y1[3] * inv, hi, true);
-      *reinterpret_cast<int*>(dst8 + d0) = lo;
-      *reinterpret_cast<int*>(dst8 + d0 + 64) = hi;
+      *reinterpret_cast<int*>(tile + kv8_off(off, d0)) = lo;
+      *reinterpret_cast<int*>(tile + kv8_off(off, d0 + 64)) = hi;
       if (d0 == 0) ks[r8] = a * LSA_KV8_RMAX;
       continue;
     }
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(1024) void rope_append_kernel(const uint16_t* __res
       a = fmaxf(a, __shfl_xor(a, 2, 64));
       a = fmaxf(a, __shfl_xor(a, 1, 64));
       const size_t r8 = ((size_t)blk * Hkv + hv) * 64 + off;
-      *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(vc) + r8 * D + c) = pack8_fp8(f, kv8_inv(a));
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(vc) + (r8 - off) * D + kv8_off(off, c)) = pack8_fp8(f, kv8_inv(a));
       if (c == 0) vs[r8] = a * LSA_KV8_RMAX;
       continue;
     }

@@ -87,6 +87,21 @@ def dequant_kv_rows(q: torch.Tensor, sc: torch.Tensor) -> torch.Tensor:
     return q.view(torch.float8_e4m3fn).float() * sc.float().unsqueeze(-1)
 
 
+# The fp8 cache tensors keep the [.., 64 tokens, 128] shape but store each (block, kv-head) tile in token-pair order
+# (csrc/kernels/common.h kv8_off): the 8-byte chunk c of tokens 2p and 2p + 1 side by side, so one 16-byte lane load
+# in decode attention carries two keys.  Scales stay in token order.
+def kv8_physical(logical: torch.Tensor) -> torch.Tensor:
+    """token-order e4m3 bytes [..., 64, 128] -> the cache's token-pair order (same shape)."""
+    sh = logical.shape
+    return logical.reshape(*sh[:-2], 32, 2, 16, 8).transpose(-3, -2).reshape(sh)
+
+
+def kv8_logical(physical: torch.Tensor) -> torch.Tensor:
+    """the cache's token-pair order [..., 64, 128] -> token-order e4m3 bytes (same shape)."""
+    sh = physical.shape
+    return physical.reshape(*sh[:-2], 32, 16, 2, 8).transpose(-3, -2).reshape(sh)
+
+
 def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, kv_scales=None):
     if qkv.dtype == torch.float32 and qkv.dim() == 3:  # f32 split-K slabs [S, T, n]
         qkv = qkv.sum(0)
@@ -105,8 +120,12 @@ def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H,
         ks, vs = kv_scales
         k8, ksc = quant_kv_rows(rot[:, H:])
         v8, vsc = quant_kv_rows(x[:, H + Hkv:])
-        kc[blk, :, off] = k8
-        vc[blk, :, off] = v8
+        ub = blk.unique()
+        idx = torch.searchsorted(ub, blk)
+        for cache, rows in ((kc, k8), (vc, v8)):
+            tiles = kv8_logical(cache[ub])
+            tiles[idx, :, off] = rows
+            cache[ub] = kv8_physical(tiles)
         ks[blk, :, off] = ksc
         vs[blk, :, off] = vsc
         return
@@ -118,7 +137,7 @@ def _gather_kv(cache, table_row, n, scales=None):
     nb = (n + BLOCK - 1) // BLOCK
     blocks = cache[table_row[:nb].long()]  # [nb, Hkv, 64, D]
     if scales is not None:
-        blocks = dequant_kv_rows(blocks, scales[table_row[:nb].long()])
+        blocks = dequant_kv_rows(kv8_logical(blocks), scales[table_row[:nb].long()])
     return blocks.permute(1, 0, 2, 3).reshape(cache.shape[1], nb * BLOCK, cache.shape[3])[:, :n]
 
 

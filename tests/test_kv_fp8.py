@@ -33,6 +33,17 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
+def test_kv8_layout_roundtrip():
+    x = torch.randint(0, 255, (3, 2, 64, 128), dtype=torch.uint8)
+    p = ref.kv8_physical(x)
+    assert torch.equal(ref.kv8_logical(p), x)
+    # token 2p / 2p + 1, 8-dim chunk c: 16 contiguous bytes at ((p * 16 + c) * 16) of the tile
+    flat = p.reshape(3, 2, -1)
+    for t, d in ((0, 0), (1, 0), (5, 17), (62, 120), (63, 127)):
+        off = (((t >> 1) * 16 + (d >> 3)) * 2 + (t & 1)) * 8 + (d & 7)
+        assert flat[1, 1, off] == x[1, 1, t, d]
+
+
 def test_reference_ops_fp8_cache_track_bf16():
     """rope_append into an fp8 cache, then decode / prefill attention over it, stay within e4m3 noise of the
     same ops over a bf16 cache."""
@@ -55,7 +66,7 @@ def test_reference_ops_fp8_cache_track_bf16():
     ref.rope_append(qkv, pos, tok_seq, bt, cos, sin, q, kb, vb, H, Hkv)
     ref.rope_append(qkv, pos, tok_seq, bt, cos, sin, q2, k8, v8, H, Hkv, kv_scales=(ks, vs))
     assert torch.equal(q, q2)
-    deq = ref.dequant_kv_rows(k8[1], ks[1])
+    deq = ref.dequant_kv_rows(ref.kv8_logical(k8[1]), ks[1])
     assert _rel(deq, kb[1]) < 0.04 and ks[2].abs().sum() == 0  # block 2 is not in the table
     cu = torch.tensor([0, T], dtype=torch.int32)
     cl = torch.tensor([T], dtype=torch.int32)

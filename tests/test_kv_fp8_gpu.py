@@ -35,6 +35,7 @@ def _paged8(kv_lens, Hkv, device, seed=0):
     mag = torch.logspace(-1, 1, total).view(total, 1, 1, 1)  # per-block magnitudes: the scales matter
     k8, ks = ref.quant_kv_rows(torch.randn(total, Hkv, 64, 128, generator=g) * mag)
     v8, vs = ref.quant_kv_rows(torch.randn(total, Hkv, 64, 128, generator=g) * mag)
+    k8, v8 = ref.kv8_physical(k8), ref.kv8_physical(v8)  # the cache's token-pair byte order
     return k8.to(device), v8.to(device), ks.to(device), vs.to(device), bt.to(device)
 
 
@@ -43,7 +44,7 @@ def _deq_close(k8a, ksa, k8b, ksb):
     rounding, bytes equal except for rare 1-code flips."""
     assert torch.allclose(ksa, ksb, rtol=1e-5, atol=0)
     assert (k8a != k8b).float().mean().item() < 0.01
-    assert _rel(ref.dequant_kv_rows(k8a, ksa), ref.dequant_kv_rows(k8b, ksb)) < 1e-2
+    assert _rel(ref.dequant_kv_rows(ref.kv8_logical(k8a), ksa), ref.dequant_kv_rows(ref.kv8_logical(k8b), ksb)) < 1e-2
 
 
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
@@ -145,8 +146,8 @@ def test_kv8_dequant_exact(gpu):
         for j in range((n + 63) // 64):
             b = int(bt[s, j])
             i = int(table[s, j])
-            assert torch.equal(ko[i], ref.dequant_kv_rows(k8[b], ks[b]).to(torch.bfloat16))
-            assert torch.equal(vo[i], ref.dequant_kv_rows(v8[b], vs[b]).to(torch.bfloat16))
+            assert torch.equal(ko[i], ref.dequant_kv_rows(ref.kv8_logical(k8[b]), ks[b]).to(torch.bfloat16))
+            assert torch.equal(vo[i], ref.dequant_kv_rows(ref.kv8_logical(v8[b]), vs[b]).to(torch.bfloat16))
 
 
 @pytest.mark.parametrize("kernel", ["16", "32", "32pair"])
