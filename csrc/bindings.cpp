@@ -54,7 +54,7 @@ int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int 
 void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                        const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
-                       void* out, int ng, hipStream_t s);
+                       void* out, int ng, float* part, float* part_ml, const int* combine, int ncomb, hipStream_t s);
 int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
 int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
                       void* out, int epi, int splitk, hipStream_t stream);
@@ -450,16 +450,30 @@ void kv8_dequant(const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& k
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                   const at::Tensor& cu_q, const at::Tensor& ctx_lens, const at::Tensor& work, int64_t H, int64_t Hkv,
-                  double scale, at::Tensor& out, int64_t rows32) {
+                  double scale, at::Tensor& out, int64_t rows32, const c10::optional<at::Tensor>& part,
+                  const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& combine, int64_t n_pslots) {
   need(q, at::kBFloat16, "q");
   need(work, at::kInt, "work");
   if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip)
-    // work [n_workgroups, 2 * NG]: NG (seq, q_start) items per workgroup (ops.prefill_work pairs them)
-    TORCH_CHECK(work.dim() == 2 && (work.size(1) == 2 || work.size(1) == 4) && work.is_contiguous(),
-                "attn_prefill32 work must be [n, 2] or [n, 4] int32");
+    // work [n_workgroups, 5 * NG]: NG (seq, q_start, t0, t1, pslot) items per workgroup (ops.prefill_plan)
+    TORCH_CHECK(work.dim() == 2 && (work.size(1) == 5 || work.size(1) == 10) && work.is_contiguous(),
+                "attn_prefill32 work must be [n, 5] or [n, 10] int32");
+    int ncomb = 0;
+    if (combine.has_value() && combine->numel() > 0) {  // KV-split heavy blocks: partial slots + merge items
+      TORCH_CHECK(part.has_value() && part_ml.has_value(), "split prefill needs the partial workspace");
+      need(*combine, at::kInt, "combine");
+      need(*part, at::kFloat, "part");
+      need(*part_ml, at::kFloat, "part_ml");
+      TORCH_CHECK(combine->dim() == 2 && combine->size(1) == 4 && combine->is_contiguous(), "combine must be [n, 4]");
+      TORCH_CHECK(part->numel() >= n_pslots * H * 128 * 128 && part_ml->numel() >= n_pslots * H * 128 * 2,
+                  "prefill partial workspace too small for ", n_pslots, " slots");
+      ncomb = (int)combine->size(0);
+    }
     check(lsa_attn_prefill32(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                              block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
-                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 2), cur_stream()),
+                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 5),
+                             ncomb ? part->data_ptr<float>() : nullptr, ncomb ? part_ml->data_ptr<float>() : nullptr,
+                             ncomb ? combine->data_ptr<int>() : nullptr, ncomb, cur_stream()),
           "attn_prefill32");
     return;
   }
@@ -626,7 +640,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ks") = py::none(), py::arg("vs") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
-        py::arg("out"), py::arg("rows32") = 0);
+        py::arg("out"), py::arg("rows32") = 0, py::arg("part") = py::none(), py::arg("part_ml") = py::none(),
+        py::arg("combine") = py::none(), py::arg("n_pslots") = 0);
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);
   m.def("fp8_dequant", &fp8_dequant);

@@ -66,6 +66,12 @@ __device__ __forceinline__ int vp_off(int r, int col) { return r * 128 + ((((col
 // per CU instead of two heavy blocks landing on the same CU).  Each group has its own K / V image and its
 // own tile count; the groups only share the workgroup barriers (an idle group keeps passing them).
 //
+// Work item of a group: (seq, q_start, t0, t1, pslot) -- the key tiles [t0, t1) of one 128-row query block.
+// pslot < 0: the whole causal range, normalised output written directly.  pslot >= 0: one KV split of a heavy
+// block (ops.prefill_plan cuts blocks whose causal range exceeds the plan's tile budget, so the heaviest block
+// no longer sets the kernel's critical path); the group writes its unnormalised O and (m, l) per row to
+// partial slot pslot and attn_prefill_combine_kernel merges the splits.
+//
 // O is accumulated TRANSPOSED, O^T += V^T P^T (A = V^T from the transposed LDS reads, B = P^T straight
 // from the S^T accumulator): the accumulator's column is then the query row = the lane, so the online-
 // softmax rescale and the final 1 / l are lane-local multiplies (no cross-lane shuffles), and each lane
@@ -76,9 +82,9 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
                                                                      const int* __restrict__ block_tables, int max_blocks,
                                                                      const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
                                                                      const int* __restrict__ work, int H, int Hkv,
-                                                                     float scale_log2, uint16_t* __restrict__ out) {
+                                                                     float scale_log2, uint16_t* __restrict__ out,
+                                                                     float* __restrict__ part, float* __restrict__ part_ml) {
   constexpr int D = 128;
-  constexpr int QB = 128;  // query rows per group
   // K / V tiles, double-buffered per group, filled by LDS-DMA (global_load_lds: no staging registers, and the
   // DMA of tile t + 1 runs under tile t's MFMAs)
   __shared__ __attribute__((aligned(16))) uint16_t Ks[NG][2][64 * D];
@@ -90,19 +96,14 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   const int hk = h / (H / Hkv);
 
   // tiles of every group (the loop runs to the largest; the barriers are workgroup-wide)
-  int nt_max = 0, ntiles = 0, seq = 0, qs = 0;
+  int nt_max = 0, ntiles = 0, seq = 0, qs = 0, t0 = 0, t1 = 0, pslot = -1;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    const int sq = work[2 * (NG * wi + g)], qq0 = work[2 * (NG * wi + g) + 1];
-    int nt = 0;
-    if (sq >= 0) {
-      const int ql = cu_q[sq + 1] - cu_q[sq];
-      const int cx = ctx_lens[sq];
-      const int lr = min(qq0 + QB - 1, ql - 1);
-      nt = (min(cx, cx - ql + lr + 1) + 63) >> 6;
-    }
+    const int* wk = work + 5 * (NG * wi + g);
+    const int sq = wk[0];
+    const int nt = sq >= 0 ? wk[3] - wk[2] : 0;
     nt_max = max(nt_max, nt);
-    if (g == gi) { ntiles = nt; seq = sq; qs = qq0; }
+    if (g == gi) { ntiles = nt; seq = sq; qs = wk[1]; t0 = wk[2]; t1 = wk[3]; pslot = wk[4]; }
   }
   const bool active = seq >= 0;
   const int sqc = active ? seq : 0;
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   // keys a wave's rows can see (causal): tiles past the wave's last row are skipped by that wave
   const int wave_last = min(qs + w * 32 + 31, qlen - 1);
-  const int wave_tiles = (active && qs + w * 32 < qlen) ? (min(ctx, pos0 + wave_last + 1) + 63) >> 6 : 0;
+  const int wave_tiles = (active && qs + w * 32 < qlen) ? min(t1, (min(ctx, pos0 + wave_last + 1) + 63) >> 6) : 0;
 
   f32x16_t o[4];  // O^T: register i of o[db] = dim 32 db + (i & 3) + 8 (i >> 2) + 4 hh of query row r32
 #pragma unroll
@@ -147,20 +148,21 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   };
   int bnext = 0;  // block of tile t + 1 (loaded one iteration ahead: no dependent load on the DMA path)
   if (ntiles > 0) {
-    dma_tile(bt[0], 0);
-    if (ntiles > 1) bnext = bt[1];
+    dma_tile(bt[t0], 0);
+    if (ntiles > 1) bnext = bt[t0 + 1];
   }
   __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): tile 0 has landed
   __syncthreads();
   const int G16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-  for (int t = 0; t < nt_max; ++t) {
+  for (int tt = 0; tt < nt_max; ++tt) {
+    const int t = t0 + tt;  // absolute key tile
     int bnn = 0;
-    if (t + 1 < ntiles) {
-      dma_tile(bnext, (t + 1) & 1);  // its buffer's last readers (tile t - 1) passed the previous barrier
-      if (t + 2 < ntiles) bnn = bt[t + 2];
+    if (tt + 1 < ntiles) {
+      dma_tile(bnext, (tt + 1) & 1);  // its buffer's last readers (tile t - 1) passed the previous barrier
+      if (tt + 2 < ntiles) bnn = bt[t + 2];
     }
-    const uint16_t* Kg = Ks[gi][t & 1];
-    const uint16_t* Vg = Vs[gi][t & 1];
+    const uint16_t* Kg = Ks[gi][tt & 1];
+    const uint16_t* Vg = Vs[gi][tt & 1];
     if (t < wave_tiles) {  // causal: tiles past the wave's last row are skipped (barriers stay uniform)
       // S^T for the two 32-key halves
       f32x16_t st[2];
@@ -249,7 +251,19 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
   const int qr = qs + w * 32 + r32;
-  if (active && qr < qlen) {
+  if (pslot >= 0) {  // one KV split: unnormalised O^T rows + (m, l), f32 (no workspace: nothing to write)
+    if (active && qr < qlen && part != nullptr) {
+      const size_t pr = ((size_t)pslot * H + h) * 128 + w * 32 + r32;
+      float* prow = part + pr * D + 4 * hh;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+          *reinterpret_cast<float4*>(prow + 32 * db + 8 * gq) =
+              make_float4(o[db][4 * gq + 0], o[db][4 * gq + 1], o[db][4 * gq + 2], o[db][4 * gq + 3]);
+      if (hh == 0) *reinterpret_cast<float2*>(part_ml + 2 * pr) = make_float2(mrow, lrow);
+    }
+  } else if (active && qr < qlen) {
     const float inv = lrow > 0.f ? 1.f / lrow : 0.f;
     uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D + 4 * hh;
 #pragma unroll
@@ -264,21 +278,69 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
 }
 
-// work: NG (seq, q_start) pairs per workgroup (seq < 0: that group idles), nwork workgroups
+// Merge of the KV splits of the heavy query blocks: item c = (seq, q_start, pslot0, nsplit), grid (items, H),
+// 256 threads = 128 rows x 2 halves of 64 dims; log-sum-exp over the splits' (m, l), O = sum w_i O_i / sum w_i.
+__global__ __launch_bounds__(256) void attn_prefill_combine_kernel(const float* __restrict__ part,
+                                                                   const float* __restrict__ part_ml,
+                                                                   const int* __restrict__ items,
+                                                                   const int* __restrict__ cu_q, int H,
+                                                                   uint16_t* __restrict__ out) {
+  constexpr int D = 128;
+  const int* it = items + 4 * blockIdx.x;
+  const int seq = it[0], qs = it[1], p0 = it[2], ns = it[3];
+  const int h = blockIdx.y;
+  const int row = threadIdx.x >> 1, c0 = (threadIdx.x & 1) * 64;
+  const int q0 = cu_q[seq], qlen = cu_q[seq + 1] - q0;
+  if (qs + row >= qlen) return;
+  float M = LSA_NEG_P;
+  for (int i = 0; i < ns; ++i) M = fmaxf(M, part_ml[2 * (((size_t)(p0 + i) * H + h) * 128 + row)]);
+  float L = 0.f, acc[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) acc[j] = 0.f;
+  for (int i = 0; i < ns; ++i) {
+    const size_t pr = ((size_t)(p0 + i) * H + h) * 128 + row;
+    const float2 ml = *reinterpret_cast<const float2*>(part_ml + 2 * pr);
+    const float wgt = __builtin_amdgcn_exp2f(ml.x - M);
+    L += ml.y * wgt;
+    const float* src = part + pr * D + c0;
+#pragma unroll
+    for (int j = 0; j < 64; j += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(src + j);
+      acc[j] += v.x * wgt; acc[j + 1] += v.y * wgt; acc[j + 2] += v.z * wgt; acc[j + 3] += v.w * wgt;
+    }
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  uint16_t* orow = out + ((size_t)(q0 + qs + row) * H + h) * D + c0;
+#pragma unroll
+  for (int j = 0; j < 64; j += 8) {
+    uint4 pk;
+    pk.x = pack2bf(acc[j] * inv, acc[j + 1] * inv); pk.y = pack2bf(acc[j + 2] * inv, acc[j + 3] * inv);
+    pk.z = pack2bf(acc[j + 4] * inv, acc[j + 5] * inv); pk.w = pack2bf(acc[j + 6] * inv, acc[j + 7] * inv);
+    *reinterpret_cast<uint4*>(orow + j) = pk;
+  }
+}
+
+// work: NG (seq, q_start, t0, t1, pslot) items per workgroup (seq < 0: that group idles), nwork workgroups;
+// combine: ncomb (seq, q_start, pslot0, nsplit) merges after the main launch (part / part_ml: the split partials)
 extern "C" int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                   const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv,
-                                  float scale, void* out, int ng, hipStream_t s) {
+                                  float scale, void* out, int ng, float* part, float* part_ml, const int* combine,
+                                  int ncomb, hipStream_t s) {
   if (nwork <= 0) return 0;
   if (H % Hkv) return -1;
+  if (ncomb > 0 && (!part || !part_ml || !combine)) return -3;
   dim3 grid(nwork, H);
   const float sl2 = scale * 1.4426950408889634f;
 #define LSA_P32_LAUNCH(NGV)                                                                                      \
   hipLaunchKernelGGL(attn_prefill32_kernel<NGV>, grid, dim3(256 * NGV), 0, s, reinterpret_cast<const uint16_t*>(q), \
                      reinterpret_cast<const uint16_t*>(kc), reinterpret_cast<const uint16_t*>(vc), block_tables,  \
-                     max_blocks, cu_q, ctx_lens, work, H, Hkv, sl2, reinterpret_cast<uint16_t*>(out))
+                     max_blocks, cu_q, ctx_lens, work, H, Hkv, sl2, reinterpret_cast<uint16_t*>(out), part, part_ml)
   if (ng == 2) LSA_P32_LAUNCH(2);
   else if (ng == 1) LSA_P32_LAUNCH(1);
   else return -2;
 #undef LSA_P32_LAUNCH
+  if (ncomb > 0)
+    hipLaunchKernelGGL(attn_prefill_combine_kernel, dim3(ncomb, H), dim3(256), 0, s, part, part_ml, combine, cu_q, H,
+                       reinterpret_cast<uint16_t*>(out));
   return (int)hipGetLastError();
 }

@@ -544,7 +544,7 @@ class ModelRunner:
         # fp8 cache: the bf16 scratch every layer's prefill attention widens its blocks into (ops.kv8_scratch)
         self._kv8_scratch = ops.kv8_scratch(ctx, self.Hkv, dev) if (self.kv_fp8 and self.on_gpu) else None
         if self.on_gpu:
-            work = torch.tensor(ops.prefill_work(cu, ctx=ctx, heads=self.H), dtype=torch.int32).to(dev, non_blocking=True)
+            work = ops.prefill_plan(cu, ctx=ctx, heads=self.H, device=dev)
 
         tps = self.tp.size if self.tp is not None else 1
         if self.seq_parallel and tps > 1 and T >= self.sp_min_tokens:

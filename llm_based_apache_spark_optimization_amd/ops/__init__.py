@@ -16,7 +16,7 @@ import importlib
 import importlib.util
 import json
 import os
-from typing import Optional
+from typing import NamedTuple, Optional
 
 import torch
 
@@ -760,11 +760,26 @@ def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[li
     context length after this prefill, default = the chunk length, i.e. no cached prefix).
 
     16-row kernel: (seq, q_start) per workgroup, heaviest (latest) query blocks first.
-    32-row kernel ('32'): (seq_a, q_a, seq_b, q_b) per workgroup -- two 128-row query blocks run side by
-    side as independent 4-wave groups, the k-th most expensive block (keys it attends to) with the k-th
-    cheapest, so under the causal mask every workgroup streams about the same number of key tiles
-    (seq_b = -1: the second group idles).  Otherwise (``_pair_blocks``) the items stay single: (seq, q_start)
-    per 4-wave workgroup, heaviest first."""
+    32-row kernel ('32'): NG items (seq, q_start, t0, t1, pslot) per workgroup -- the key tiles [t0, t1) of a
+    128-row query block; see ``prefill_plan`` for the KV splits (pslot >= 0) and the heavy/light pairing."""
+    return prefill_plan_items(cu_q, qblock, ctx, kernel, heads)[0]
+
+
+# LSA_PREFILL_SPLIT: key tiles per work item of the 32-row prefill kernel before a heavy query block's causal
+# range is cut into KV splits (merged by attn_prefill_combine_kernel): "auto" (the plan's even share of the chip,
+# >= 8 tiles), a number, or 0 (never split)
+PREFILL_SPLIT = os.environ.get("LSA_PREFILL_SPLIT", "auto")
+
+
+def _split_tiles(total_tiles: int) -> int:
+    if PREFILL_SPLIT == "auto":
+        return max(8, -(-total_tiles // 512))
+    return int(PREFILL_SPLIT) or (1 << 30)
+
+
+def prefill_plan_items(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[list[int]] = None,
+                       kernel: Optional[str] = None, heads: int = 32):
+    """(work rows, combine rows, n_pslots) of ``prefill_plan``, as Python lists."""
     kernel = kernel or _prefill_kernel(cu_q)
     if qblock is None:
         qblock = 128 if kernel == "32" else ext().prefill_qblock
@@ -773,19 +788,58 @@ def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[li
         ql = cu_q[s + 1] - cu_q[s]
         pos0 = (ctx[s] - ql) if ctx is not None else 0
         for qs in range(0, ql, qblock):
-            items.append((pos0 + min(qs + qblock, ql), s, qs))
+            items.append(((pos0 + min(qs + qblock, ql) + 63) // 64, s, qs))
     items.sort(key=lambda t: -t[0])
     if kernel != "32":
-        return [(s, qs) for _, s, qs in items]
-    n = len(items)
-    if not _pair_blocks(n, heads, max(cu_q[i + 1] - cu_q[i] for i in range(len(cu_q) - 1)), qblock):
-        return [(s, qs) for _, s, qs in items]
+        return [(s, qs) for _, s, qs in items], [], 0
+    # KV splits: a block whose causal range exceeds the tile budget is cut into nearly equal pieces of key tiles
+    # (partial O + (m, l) per piece into its own slot, merged afterwards) so the heaviest block no longer sets the
+    # critical path: the 2k prompts ran 192 paired workgroups on 256 CUs with the last block's 32 tiles in series
+    budget = _split_tiles(sum(t for t, _, _ in items) * heads)
+    units, combine, np_ = [], [], 0
+    for nt, s, qs in items:
+        if nt <= budget:
+            units.append((nt, s, qs, 0, nt, -1))
+            continue
+        k = -(-nt // budget)
+        size = -(-nt // k)
+        for j in range(k):
+            t0, t1 = j * size, min(nt, (j + 1) * size)
+            units.append((t1 - t0, s, qs, t0, t1, np_ + j))
+        combine.append((s, qs, np_, k))
+        np_ += k
+    units.sort(key=lambda u: -u[0])
+    n = len(units)
+    longest = max(cu_q[i + 1] - cu_q[i] for i in range(len(cu_q) - 1))
+    if not _pair_blocks(n, heads, longest, qblock):
+        return [u[1:] for u in units], combine, np_
     out = []
     for i in range((n + 1) // 2):
         j = n - 1 - i
-        b = (items[j][1], items[j][2]) if j > i else (-1, 0)
-        out.append((items[i][1], items[i][2]) + b)
-    return out
+        b = units[j][1:] if j > i else (-1, 0, 0, 0, -1)
+        out.append(units[i][1:] + b)
+    return out, combine, np_
+
+
+class PrefillPlan(NamedTuple):
+    """Device-side plan of one prefill attention call (``prefill_plan``)."""
+    kernel: str
+    work: torch.Tensor               # int32 [n_workgroups, 2 | 5 * NG]
+    combine: Optional[torch.Tensor]  # int32 [n, 4] (seq, q_start, pslot0, nsplit) merges, or None
+    n_pslots: int
+
+
+def prefill_plan(cu_q: list[int], ctx: Optional[list[int]] = None, heads: int = 32, device=None,
+                 kernel: Optional[str] = None) -> PrefillPlan:
+    """Work items (+ KV-split merges) of the prefill attention kernel for packed sequences, on ``device``."""
+    kernel = kernel or _prefill_kernel(cu_q)
+    work, combine, np_ = prefill_plan_items(cu_q, ctx=ctx, kernel=kernel, heads=heads)
+    w = torch.tensor(work, dtype=torch.int32)
+    c = torch.tensor(combine, dtype=torch.int32) if combine else None
+    if device is not None:
+        w = w.to(device, non_blocking=True)
+        c = c.to(device, non_blocking=True) if c is not None else None
+    return PrefillPlan(kernel, w, c, np_)
 
 
 # LSA_PREFILL_PAIR: auto | 1 | 0 -- heavy/light paired query blocks in the 32-row prefill kernel
@@ -805,8 +859,8 @@ def _pair_blocks(n_items: int, heads: int, longest: int, qblock: int) -> bool:
 
 def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, work=None, cu_list=None,
                  kv_scales=None, kv8_scratch_=None):
-    """Causal prefill attention of packed sequences (cu_q offsets) over the paged cache.  ``work`` must
-    come from ``prefill_work`` of the same offsets (``cu_list``, host copy: picks the kernel).
+    """Causal prefill attention of packed sequences (cu_q offsets) over the paged cache.  ``work``: the
+    ``prefill_plan`` of the same offsets (or None: planned here from ``cu_list`` / the device offsets).
     kv_scales = (ks, vs): fp8 cache -- the attended blocks are widened into ``kv8_scratch_`` (= kv8_scratch(ctx,
     ...), built from the host context list; made here when not given) and the bf16 kernels run on that."""
     if not _gpu(q):
@@ -816,10 +870,16 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, wo
         ext().kv8_dequant(kc, vc, kv_scales[0], kv_scales[1], block_tables, ctx_lens, table.shape[1], ko, vo)
         kc, vc, block_tables = ko, vo, table
     cu = cu_list if cu_list is not None else cu_q.tolist()
-    if work is None:
-        work = torch.tensor(prefill_work(cu, ctx=ctx_lens.tolist(), heads=H), dtype=torch.int32).to(q.device)
-    ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, work, H, Hkv, scale, out,
-                       1 if _prefill_kernel(cu) == "32" else 0)
+    plan = work if isinstance(work, PrefillPlan) else None
+    if plan is None:
+        plan = (prefill_plan(cu, ctx=ctx_lens.tolist(), heads=H, device=q.device) if work is None
+                else PrefillPlan(_prefill_kernel(cu), work, None, 0))
+    part = part_ml = None
+    if plan.combine is not None:  # KV-split heavy blocks: partial slots for the merge
+        part = torch.empty(plan.n_pslots * H * 128 * 128, dtype=torch.float32, device=q.device)
+        part_ml = torch.empty(plan.n_pslots * H * 128 * 2, dtype=torch.float32, device=q.device)
+    ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out,
+                       1 if plan.kernel == "32" else 0, part, part_ml, plan.combine, plan.n_pslots)
     return out
 
 

@@ -43,7 +43,7 @@ def case(name, nseq, qlen, H, Hkv):
     out = torch.empty_like(q)
     cud = torch.tensor(cu, dtype=torch.int32, device=dev)
     ctx = torch.full((nseq,), qlen, dtype=torch.int32, device=dev)
-    work = torch.tensor(ops.prefill_work(cu, heads=H), dtype=torch.int32, device=dev)
+    work = ops.prefill_plan(cu, heads=H, device=dev)
     us = timeit(lambda: ops.attn_prefill(q, kc, vc, bt, cud, ctx, H, Hkv, 1 / math.sqrt(128), out, work=work))
     flops = nseq * 4 * H * 128 * qlen * (qlen + 1) / 2  # causal QK^T + PV
     # numerics spot check vs torch SDPA on one sequence
@@ -52,7 +52,8 @@ def case(name, nseq, qlen, H, Hkv):
     vv = vc[bt[0].long()].transpose(0, 1).reshape(Hkv, -1, 128)[:, :qlen].float().repeat_interleave(H // Hkv, 0)
     ref = torch.nn.functional.scaled_dot_product_attention(s0, kk, vv, is_causal=True).transpose(0, 1)
     err = (out[:qlen].float() - ref).abs().max().item()
-    print(json.dumps({"case": name, "kernel": ops._prefill_kernel(cu), "work": list(work.shape),
+    print(json.dumps({"case": name, "kernel": work.kernel, "work": list(work.work.shape), "split_slots": work.n_pslots,
+                      "split_tiles": os.environ.get("LSA_PREFILL_SPLIT", "auto"),
                       "us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1), "max_err": round(err, 4)}), flush=True)
 
 

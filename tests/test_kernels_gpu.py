@@ -436,6 +436,32 @@ def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
     assert _rel(out, out2) < 1e-2
 
 
+@pytest.mark.parametrize("split", ["2", "3", "5"])
+@pytest.mark.parametrize("pair", ["0", "1"])
+@pytest.mark.parametrize("case", ["fresh", "chunked", "long"])
+def test_attn_prefill_kv_split(gpu, case, pair, split, monkeypatch):
+    """32-row kernel with the heavy query blocks' causal key ranges cut into KV splits (ops.prefill_plan:
+    partial O + (m, l) per split, attn_prefill_combine_kernel merge) vs the fp32 reference."""
+    monkeypatch.setattr(ops, "PREFILL_ATTN", "32")
+    monkeypatch.setattr(ops, "PREFILL_PAIR", pair)
+    monkeypatch.setattr(ops, "PREFILL_SPLIT", split)
+    H, Hkv, D = 24, 8, 128
+    qlens, ctx = {"fresh": ([1, 70, 130, 600], [1, 70, 130, 600]), "chunked": ([10, 200, 100], [700, 264, 400]),
+                  "long": ([1000, 257], [1000, 900])}[case]
+    kc, vc, bt = _paged(ctx, Hkv, D, gpu, seed=3)
+    T = sum(qlens)
+    q = torch.randn(T, H, D, device=gpu).to(torch.bfloat16)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0).tolist()), device=gpu, dtype=torch.int32)
+    cl = torch.tensor(ctx, device=gpu, dtype=torch.int32)
+    plan = ops.prefill_plan(cu.tolist(), ctx=ctx, heads=H, device=gpu)
+    assert plan.n_pslots > 0 and plan.combine is not None  # the split path is what runs
+    out = torch.empty(T, H, D, device=gpu, dtype=torch.bfloat16)
+    out2 = torch.empty_like(out)
+    ops.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), out, work=plan)
+    ref.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), out2)
+    assert _rel(out, out2) < 1e-2
+
+
 @pytest.mark.parametrize("kernel", ["16", "32", "32pair"])
 def test_attn_prefill_spike(gpu, kernel, monkeypatch):
     """Force the online-softmax rescale branch: one very large score late in the sequence."""
