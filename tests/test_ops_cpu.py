@@ -58,3 +58,46 @@ def test_norm_and_attention_xf_cpu():
     of = torch.zeros(16 * H * Dh, dtype=torch.bfloat16)
     ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, 0.1, of, xf=True)
     assert torch.equal(ops.from_xfrag(of, 2, H * Dh), o.view(2, -1))
+
+
+def _check_plan(cu, ctx, heads, monkeypatch, split):
+    monkeypatch.setattr(ops, "PREFILL_SPLIT", split)
+    work, combine, npl = ops.prefill_plan_items(cu, ctx=ctx, kernel="32", heads=heads)
+    units = [tuple(w[i:i + 5]) for w in work for i in range(0, len(w), 5) if w[i] >= 0]
+    cover = {}
+    for s, qs, t0, t1, ps in units:
+        assert 0 <= t0 < t1
+        cover.setdefault((s, qs), []).append((t0, t1, ps))
+    merges = {(s, qs): (p0, k) for s, qs, p0, k in combine}
+    slots = []
+    for s in range(len(cu) - 1):
+        ql, pos0 = cu[s + 1] - cu[s], ctx[s] - (cu[s + 1] - cu[s])
+        for qs in range(0, ql, 128):
+            nt = (pos0 + min(qs + 128, ql) + 63) // 64
+            pieces = sorted(cover.pop((s, qs)))
+            assert pieces[0][0] == 0 and pieces[-1][1] == nt  # every causal key tile exactly once
+            assert all(a[1] == b[0] for a, b in zip(pieces, pieces[1:]))
+            if len(pieces) == 1:
+                assert pieces[0][2] == -1 and (s, qs) not in merges
+            else:
+                p0, k = merges.pop((s, qs))
+                assert k == len(pieces) and sorted(p[2] for p in pieces) == list(range(p0, p0 + k))
+                slots += [p[2] for p in pieces]
+    assert not cover and not merges and sorted(slots) == list(range(npl))
+    return units, npl
+
+
+def test_prefill_plan_kv_splits_cover_causal_ranges(monkeypatch):
+    """ops.prefill_plan for the 32-row kernel: each query block's causal key tiles are covered exactly once by
+    its pieces, split blocks get consecutive partial slots and one merge row, unsplit blocks write directly."""
+    monkeypatch.setattr(ops, "PREFILL_PAIR", "auto")
+    # 2k prompt (3B heads): the auto budget splits the heavy half of the blocks
+    units, npl = _check_plan([0, 2048], [2048], 24, monkeypatch, "auto")
+    assert npl > 0 and max(t1 - t0 for _, _, t0, t1, _ in units) <= ops._split_tiles(272 * 24)
+    # chunked continuation and several sequences, forced small budget; and splitting off
+    _check_plan([0, 10, 210, 310], [700, 264, 400], 32, monkeypatch, "3")
+    _, npl = _check_plan([0, 2048], [2048], 24, monkeypatch, "0")
+    assert npl == 0
+    # an 8k prompt already has more blocks than slots: no splits under auto
+    _, npl = _check_plan([0, 8192], [8192], 24, monkeypatch, "auto")
+    assert npl == 0
