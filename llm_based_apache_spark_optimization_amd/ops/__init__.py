@@ -767,8 +767,11 @@ def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[li
 
 # LSA_PREFILL_SPLIT: key tiles per work item of the 32-row prefill kernel before a heavy query block's causal
 # range is cut into KV splits (merged by attn_prefill_combine_kernel): "auto" (the plan's even share of the chip,
-# >= 8 tiles), a number, or 0 (never split)
-PREFILL_SPLIT = os.environ.get("LSA_PREFILL_SPLIT", "auto")
+# >= 8 tiles), a number, or 0 (never split, the default).  Measured on MI355X (profiles/attn_prefill_kv_split_
+# mi355x.jsonl, scripts/gpu_psplit.sh): every budget is slower than no split -- 3B 2k 75.1 us unsplit vs 84.5
+# (auto) .. 113 (4 tiles), 7B 2k 81.0 vs 98.1 .. 134, 3B 8k 577 vs 577 .. 1530 -- the partial-O stores, the merge
+# launch and the extra K/V passes of the pieces cost more than the heavy/light pairing leaves on the critical path
+PREFILL_SPLIT = os.environ.get("LSA_PREFILL_SPLIT", "0")
 
 
 def _split_tiles(total_tiles: int) -> int:
