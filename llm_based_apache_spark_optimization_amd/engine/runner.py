@@ -76,7 +76,9 @@ class ModelRunner:
         self.max_new_cap = max_new_cap or self.max_model_len
         self.on_gpu = self.device.type == "cuda"
         self.use_graphs = use_graphs and self.on_gpu
-        self.steps_per_graph = steps_per_graph
+        # decode steps per captured graph (runs replay the k-step graph, then single steps for the rest):
+        # fewer graph boundaries per generated token; LSA_STEPS_PER_GRAPH overrides
+        self.steps_per_graph = max(1, int(os.environ.get("LSA_STEPS_PER_GRAPH", steps_per_graph)))
         dev = self.device
 
         # ---------------- KV cache: [L, 2, blocks, Hkv, 64, D] bf16, or e4m3 bytes + [L, 2, blocks, Hkv, 64] f32 scales
@@ -384,9 +386,10 @@ class ModelRunner:
             b *= 2
         return min(b, self.max_slots) if n <= self.max_slots else self.max_slots
 
-    def capture(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
+    def capture(self, B: int, sample: bool, plan: Optional[tuple] = None, k: int = 1) -> None:
+        """Capture the k-step decode graph of (bucket, sampling mode, plan)."""
         plan = tuple(plan or self.ctx_plan(B))
-        key = (B, sample, plan)
+        key = (B, sample, plan) if k == 1 else (B, sample, plan, k)
         if key in self.graphs:
             return
         if self.tp is not None and self.tp.size > 1:
@@ -397,7 +400,7 @@ class ModelRunner:
         with torch.cuda.stream(s):
             # state must not change during capture: kernels are recorded, not executed
             with torch.cuda.graph(g, stream=s):
-                for _ in range(self.steps_per_graph):
+                for _ in range(k):
                     self._decode_step(B, sample, plan)
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graphs[key] = g
@@ -429,6 +432,8 @@ class ModelRunner:
             for sm in sample_modes:
                 for p in self.plans(b):
                     self.capture(b, sm, p)
+                    if self.steps_per_graph > 1:
+                        self.capture(b, sm, p, self.steps_per_graph)
         torch.cuda.synchronize(self.device)
 
     def decode(self, B: int, steps: int, sample: bool = False, max_ctx: Optional[int] = None) -> None:
@@ -439,11 +444,18 @@ class ModelRunner:
             for _ in range(steps):
                 self._decode_step(B, sample, plan)
             return
-        self.capture(B, sample, plan)
-        g = self.graphs[(B, sample, plan)]
-        n = (steps + self.steps_per_graph - 1) // self.steps_per_graph
-        for _ in range(n):
-            g.replay()
+        k = self.steps_per_graph
+        full, rest = divmod(steps, k) if k > 1 else (0, steps)
+        if full:
+            self.capture(B, sample, plan, k)
+            g = self.graphs[(B, sample, plan, k)]
+            for _ in range(full):
+                g.replay()
+        if rest:
+            self.capture(B, sample, plan)
+            g = self.graphs[(B, sample, plan)]
+            for _ in range(rest):
+                g.replay()
 
     # ------------------------------------------------------------------------------------ slots
     def set_slot(self, slot: int, blocks: Sequence[int], limit: int, temperature: float = 0.0, top_k: int = 40,
