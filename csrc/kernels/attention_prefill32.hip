@@ -70,7 +70,8 @@ __device__ __forceinline__ int vp_off(int r, int col) { return r * 128 + ((((col
 // pslot < 0: the whole causal range, normalised output written directly.  pslot >= 0: one KV split of a heavy
 // block (ops.prefill_plan cuts blocks whose causal range exceeds the plan's tile budget, so the heaviest block
 // no longer sets the kernel's critical path); the group writes its unnormalised O and (m, l) per row to
-// partial slot pslot and attn_prefill_combine_kernel merges the splits.
+// partial slot pslot and attn_prefill_combine_kernel merges the splits.  pslot == -2 (NG = 2, both groups): the
+// two groups hold the same block, each a part of its key tiles, merged through LDS at the end (no combine launch).
 //
 // O is accumulated TRANSPOSED, O^T += V^T P^T (A = V^T from the transposed LDS reads, B = P^T straight
 // from the S^T accumulator): the accumulator's column is then the query row = the lane, so the online-
@@ -251,6 +252,46 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
   const int qr = qs + w * 32 + r32;
+  if constexpr (NG == 2) {
+    // pslot == -2 in group 0's item: both groups hold the SAME query block, split over its key tiles (group 0
+    // the unmasked first part, group 1 the rest with the diagonal); group 1's unnormalised O^T and (m, l) go
+    // through LDS (the K / V images are free: the loop's last barrier follows every group's last LDS read and
+    // DMA) and group 0 merges and stores -- the heaviest block's critical path halves without a merge launch
+    if (work[5 * (NG * wi) + 4] == -2) {
+      float* xo = reinterpret_cast<float*>(&Ks[0][0][0]);  // 256 threads x 64 floats = the 64 KiB of Ks
+      float* xml = reinterpret_cast<float*>(&Vs[0][0][0]);
+      if (gi == 1) {
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq)
+            *reinterpret_cast<float4*>(xo + ((db * 4 + gq) * 256 + gtid) * 4) =
+                make_float4(o[db][4 * gq + 0], o[db][4 * gq + 1], o[db][4 * gq + 2], o[db][4 * gq + 3]);
+        *reinterpret_cast<float2*>(xml + 2 * gtid) = make_float2(mrow, lrow);
+      }
+      __syncthreads();
+      if (gi == 0 && active && qr < qlen) {
+        const float2 ml1 = *reinterpret_cast<const float2*>(xml + 2 * gtid);
+        const float mm = fmaxf(mrow, ml1.x);
+        const float a0 = __builtin_amdgcn_exp2f(mrow - mm), a1 = __builtin_amdgcn_exp2f(ml1.x - mm);
+        const float L = lrow * a0 + ml1.y * a1;
+        const float inv = L > 0.f ? 1.f / L : 0.f;
+        const float w0 = a0 * inv, w1 = a1 * inv;
+        uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D + 4 * hh;
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const float4 v = *reinterpret_cast<const float4*>(xo + ((db * 4 + gq) * 256 + gtid) * 4);
+            uint2 pk;
+            pk.x = pack2bf(o[db][4 * gq + 0] * w0 + v.x * w1, o[db][4 * gq + 1] * w0 + v.y * w1);
+            pk.y = pack2bf(o[db][4 * gq + 2] * w0 + v.z * w1, o[db][4 * gq + 3] * w0 + v.w * w1);
+            *reinterpret_cast<uint2*>(orow + 32 * db + 8 * gq) = pk;
+          }
+      }
+      return;
+    }
+  }
   if (pslot >= 0) {  // one KV split: unnormalised O^T rows + (m, l), f32 (no workspace: nothing to write)
     if (active && qr < qlen && part != nullptr) {
       const size_t pr = ((size_t)pslot * H + h) * 128 + w * 32 + r32;

@@ -813,6 +813,17 @@ def prefill_plan_items(cu_q: list[int], qblock: Optional[int] = None, ctx: Optio
         np_ += k
     units.sort(key=lambda u: -u[0])
     n = len(units)
+    if not combine and _halve_blocks(n, heads):
+        # both 4-wave groups of a workgroup on ONE query block, its key tiles split in two (pslot -2: the kernel
+        # merges group 1's partial into group 0 through LDS), heaviest blocks first
+        out = []
+        for nt, s, qs, _, _, _ in units:
+            if nt >= 2:
+                mid = (nt + 1) // 2
+                out.append((s, qs, 0, mid, -2, s, qs, mid, nt, -2))
+            else:
+                out.append((s, qs, 0, nt, -1, -1, 0, 0, 0, -1))
+        return out, combine, np_
     longest = max(cu_q[i + 1] - cu_q[i] for i in range(len(cu_q) - 1))
     if not _pair_blocks(n, heads, longest, qblock):
         return [u[1:] for u in units], combine, np_
@@ -847,6 +858,22 @@ def prefill_plan(cu_q: list[int], ctx: Optional[list[int]] = None, heads: int = 
 
 # LSA_PREFILL_PAIR: auto | 1 | 0 -- heavy/light paired query blocks in the 32-row prefill kernel
 PREFILL_PAIR = os.environ.get("LSA_PREFILL_PAIR", "auto")
+
+
+# LSA_PREFILL_HALVES: auto | 1 | 0 (default) -- one query block per workgroup, its key tiles split over the two
+# 4-wave groups and merged in LDS (attention_prefill32.hip, pslot -2).  Correct (tests/test_kernels_gpu.py
+# test_attn_prefill_halves) but measured slower (profiles/attn_prefill_halves_mi355x.jsonl: 3B 2k 73.3 -> 98.6 us,
+# 7B 2k 80.2 -> 102.3 us): two waves per SIMD on one block take ~2x the per-tile time of one (the CU is
+# throughput-bound in the tile loop, not latency-bound), and 2x the workgroups at one per CU need 1.5 rounds
+PREFILL_HALVES = os.environ.get("LSA_PREFILL_HALVES", "0")
+
+
+def _halve_blocks(n_items: int, heads: int) -> bool:
+    """Halve every block over two wave groups when all blocks are resident at once (one workgroup per CU at
+    128 KiB of LDS): the critical path is then the heaviest block, which the halves shorten."""
+    if PREFILL_HALVES != "auto":
+        return PREFILL_HALVES == "1"
+    return n_items * heads <= 512
 
 
 def _pair_blocks(n_items: int, heads: int, longest: int, qblock: int) -> bool:

@@ -462,6 +462,30 @@ def test_attn_prefill_kv_split(gpu, case, pair, split, monkeypatch):
     assert _rel(out, out2) < 1e-2
 
 
+@pytest.mark.parametrize("case", ["fresh", "chunked", "long", "2k"])
+def test_attn_prefill_halves(gpu, case, monkeypatch):
+    """32-row kernel with each query block's key tiles split over the workgroup's two wave groups and merged
+    in LDS (pslot -2) vs the fp32 reference; includes 1-tile blocks (no split) and idle waves past qlen."""
+    monkeypatch.setattr(ops, "PREFILL_ATTN", "32")
+    monkeypatch.setattr(ops, "PREFILL_SPLIT", "0")
+    monkeypatch.setattr(ops, "PREFILL_HALVES", "1")
+    H, Hkv, D = 24, 8, 128
+    qlens, ctx = {"fresh": ([1, 70, 130, 600], [1, 70, 130, 600]), "chunked": ([10, 200, 100], [700, 264, 400]),
+                  "long": ([1000, 257], [1000, 900]), "2k": ([2048], [2048])}[case]
+    kc, vc, bt = _paged(ctx, Hkv, D, gpu, seed=5)
+    T = sum(qlens)
+    q = torch.randn(T, H, D, device=gpu).to(torch.bfloat16)
+    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0).tolist()), device=gpu, dtype=torch.int32)
+    cl = torch.tensor(ctx, device=gpu, dtype=torch.int32)
+    plan = ops.prefill_plan(cu.tolist(), ctx=ctx, heads=H, device=gpu)
+    assert plan.kernel == "32" and plan.combine is None and int((plan.work[:, 4] == -2).sum()) > 0
+    out = torch.empty(T, H, D, device=gpu, dtype=torch.bfloat16)
+    out2 = torch.empty_like(out)
+    ops.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), out, work=plan)
+    ref.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), out2)
+    assert _rel(out, out2) < 1e-2
+
+
 @pytest.mark.parametrize("kernel", ["16", "32", "32pair"])
 def test_attn_prefill_spike(gpu, kernel, monkeypatch):
     """Force the online-softmax rescale branch: one very large score late in the sequence."""

@@ -69,6 +69,9 @@ def _check_plan(cu, ctx, heads, monkeypatch, split):
         assert 0 <= t0 < t1
         cover.setdefault((s, qs), []).append((t0, t1, ps))
     merges = {(s, qs): (p0, k) for s, qs, p0, k in combine}
+    for w in work:  # in-workgroup halves: both groups of the row on one block, nowhere else
+        if len(w) == 10 and w[4] == -2:
+            assert w[9] == -2 and (w[0], w[1]) == (w[5], w[6]) and w[3] == w[7]
     slots = []
     for s in range(len(cu) - 1):
         ql, pos0 = cu[s + 1] - cu[s], ctx[s] - (cu[s + 1] - cu[s])
@@ -79,6 +82,8 @@ def _check_plan(cu, ctx, heads, monkeypatch, split):
             assert all(a[1] == b[0] for a, b in zip(pieces, pieces[1:]))
             if len(pieces) == 1:
                 assert pieces[0][2] == -1 and (s, qs) not in merges
+            elif pieces[0][2] == -2:
+                assert len(pieces) == 2 and pieces[1][2] == -2 and (s, qs) not in merges
             else:
                 p0, k = merges.pop((s, qs))
                 assert k == len(pieces) and sorted(p[2] for p in pieces) == list(range(p0, p0 + k))
@@ -96,8 +101,14 @@ def test_prefill_plan_kv_splits_cover_causal_ranges(monkeypatch):
     assert npl > 0 and max(t1 - t0 for _, _, t0, t1, _ in units) <= ops._split_tiles(272 * 24)
     # chunked continuation and several sequences, forced small budget; and splitting off
     _check_plan([0, 10, 210, 310], [700, 264, 400], 32, monkeypatch, "3")
+    monkeypatch.setattr(ops, "PREFILL_HALVES", "0")
     _, npl = _check_plan([0, 2048], [2048], 24, monkeypatch, "0")
     assert npl == 0
+    # in-workgroup halves (no splits): every block of >= 2 tiles is one workgroup row of two halves
+    monkeypatch.setattr(ops, "PREFILL_HALVES", "auto")  # (opt-in: the default is "0")
+    units, npl = _check_plan([0, 2048], [2048], 24, monkeypatch, "0")
+    assert npl == 0 and len(units) == 32 and all(ps == -2 for *_, ps in units)
+    _check_plan([0, 10, 210, 310], [700, 264, 400], 32, monkeypatch, "0")
     # an 8k prompt already has more blocks than slots: no splits under auto
     _, npl = _check_plan([0, 8192], [8192], 24, monkeypatch, "auto")
     assert npl == 0
