@@ -22,6 +22,7 @@
 typedef short s16x4p_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4p_t* lds_s4p_ptr;
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef float f32x2p_t __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void* lds_u16_ptr;
 
 namespace {
@@ -40,6 +41,15 @@ __device__ __forceinline__ void dma16(const void* gsrc, unsigned lds_base) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(gsrc), "s"(lds_base)
+               : "memory");
+}
+// the same DMA from a wave-uniform base (SGPR pair) + a 32-bit per-lane byte offset (saddr form): no 64-bit
+// per-lane address arithmetic on the tile loop's VALU
+__device__ __forceinline__ void dma16s(const void* gbase, unsigned voff, unsigned lds_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(gbase), "s"(lds_base)
                : "memory");
 }
 
@@ -91,8 +101,10 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   __shared__ __attribute__((aligned(16))) uint16_t Ks[NG][2][64 * D];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[NG][2][64 * D];
   const int wi = blockIdx.x, h = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3;
-  const int gi = NG == 1 ? 0 : (tid >> 8), gtid = tid & 255;
+  // wave and group ids are wave-uniform: readfirstlane lets hipcc keep every per-group work field, block id
+  // and DMA base in SGPRs (selected by a VGPR id, the whole tile loop's address math ran on the VALU)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
+  const int gi = NG == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 8), gtid = tid & 255;
   const int r32 = lane & 31, hh = lane >> 5;
   const int hk = h / (H / Hkv);
 
@@ -135,22 +147,29 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   // The DMA writes lane-linearly, so the swizzled images (kp_off / vp_off) are produced by permuting the
   // SOURCE chunk each lane fetches: lane l of instruction j fills row 4 j + (l >> 4), slot l & 15.
   const int drow = lane >> 4, dslot = lane & 15;
+  // per-lane byte offsets inside a (block, kv-head) tile (loop-invariant) and the LDS images' wave bases
+  unsigned koff[4], voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * (w + 4 * i) + drow;
+    koff[i] = (unsigned)(r * D + ((dslot ^ (r & 15)) << 3)) * 2u;
+    voff[i] = (unsigned)(r * D + ((dslot ^ ((r & 3) << 2)) << 3)) * 2u;
+  }
+  const unsigned kl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Ks[gi][0][4 * w * D]));
+  const unsigned vl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Vs[gi][0][4 * w * D]));
   auto dma_tile = [&](int blk, int b) {
     const size_t base = ((size_t)blk * Hkv + hk) * 64 * D;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int j = w + 4 * i;
-      const int r = 4 * j + drow;
-      const uint16_t* ksrc = kc + base + r * D + ((dslot ^ (r & 15)) << 3);
-      const uint16_t* vsrc = vc + base + r * D + ((dslot ^ ((r & 3) << 2)) << 3);
-      dma16(ksrc, __builtin_amdgcn_readfirstlane(lds_addr(&Ks[gi][b][4 * j * D])));
-      dma16(vsrc, __builtin_amdgcn_readfirstlane(lds_addr(&Vs[gi][b][4 * j * D])));
+      const unsigned lo = (unsigned)(b * 64 * D + 16 * i * D) * 2u;  // buffer b, rows 4 (w + 4 i) ..
+      dma16s(kc + base, koff[i], kl0 + lo);
+      dma16s(vc + base, voff[i], vl0 + lo);
     }
   };
   int bnext = 0;  // block of tile t + 1 (loaded one iteration ahead: no dependent load on the DMA path)
   if (ntiles > 0) {
-    dma_tile(bt[t0], 0);
-    if (ntiles > 1) bnext = bt[t0 + 1];
+    dma_tile(__builtin_amdgcn_readfirstlane(bt[t0]), 0);
+    if (ntiles > 1) bnext = __builtin_amdgcn_readfirstlane(bt[t0 + 1]);
   }
   __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): tile 0 has landed
   __syncthreads();
@@ -160,7 +179,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
     int bnn = 0;
     if (tt + 1 < ntiles) {
       dma_tile(bnext, (tt + 1) & 1);  // its buffer's last readers (tile t - 1) passed the previous barrier
-      if (tt + 2 < ntiles) bnn = bt[t + 2];
+      if (tt + 2 < ntiles) bnn = __builtin_amdgcn_readfirstlane(bt[t + 2]);
     }
     const uint16_t* Kg = Ks[gi][tt & 1];
     const uint16_t* Vg = Vs[gi][tt & 1];
@@ -176,10 +195,10 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
           st[kh] = mfma32x32x16(a, qf[s2], st[kh]);
         }
       }
-      // mask + online softmax; register i of half kh holds key t*64 + 32 kh + (i & 3) + 8 (i >> 2) + 4 hh
-      float tmax = LSA_NEG_P;
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) st[kh] *= scale_log2;
+      // mask + online softmax; register i of half kh holds key t*64 + 32 kh + (i & 3) + 8 (i >> 2) + 4 hh.
+      // Raw scores: the scale is folded into one packed FMA per key pair in the exponent (v_pk_fma_f32), the
+      // row max is taken over raw scores and scaled once, masked keys are -inf (exp2 -> 0 whatever the row
+      // max; mrow starts finite, so a row with no visible key yet keeps p = 0, l = 0)
       // causal / context mask, only on the tiles that cross this wave's diagonal or the context end (one
       // wave-uniform branch per tile; inside it branch-free selects -- a short-circuit per element made
       // hipcc emit 64 exec-mask branches per tile)
@@ -190,14 +209,15 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
           for (int i = 0; i < 16; ++i) {
             const int key = t * 64 + 32 * kh + (i & 3) + 8 * (i >> 2) + 4 * hh;
             const bool ok = (key <= qpos) & (key < ctx);
-            st[kh][i] = ok ? st[kh][i] : LSA_NEG_P;
+            st[kh][i] = ok ? st[kh][i] : -__builtin_inff();
           }
       }
+      float tmax = -__builtin_inff();
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[kh][i]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;
       // online softmax; the O / l rescale runs only when some row's max grew (exact: alpha = 1 otherwise),
       // which under the causal mask is the first few tiles of a row
       if (__any(tmax > mrow)) {
@@ -208,16 +228,18 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   #pragma unroll
         for (int db = 0; db < 4; ++db) o[db] *= alpha;  // lane-local: the accumulator column is this lane's row
       }
-      const float mnew = mrow;
-      float psum = 0.f;
+      const f32x2p_t sc2 = {scale_log2, scale_log2}, mn2 = {-mrow, -mrow};
+      f32x2p_t ps2 = {0.f, 0.f};
       uint4 pa[2][2];  // [kh][k-step s']: registers 8 s' .. 8 s' + 7 of half kh as bf16
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
         float p[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          p[i] = __builtin_amdgcn_exp2f(st[kh][i] - mnew);
-          psum += p[i];
+        for (int i = 0; i < 16; i += 2) {
+          const f32x2p_t x = __builtin_elementwise_fma(f32x2p_t{st[kh][i], st[kh][i + 1]}, sc2, mn2);
+          p[i] = __builtin_amdgcn_exp2f(x.x);
+          p[i + 1] = __builtin_amdgcn_exp2f(x.y);
+          ps2 += f32x2p_t{p[i], p[i + 1]};
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -227,6 +249,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
           pa[kh][s2].w = pack2bf(p[8 * s2 + 6], p[8 * s2 + 7]);
         }
       }
+      float psum = ps2.x + ps2.y;
       psum += __shfl_xor(psum, 32, 64);
       lrow += psum;
       // O^T += V^T P^T: k-step (kh, s') covers keys 32 kh + 16 s' + 8 (j >> 2) + 4 hh + (j & 3) in element j
