@@ -18,6 +18,10 @@
 #include "common.h"
 
 #define LSA_NEG_P (-1.0e30f)
+#ifndef LSA_P32_VREG
+#define LSA_P32_VREG 0  // 1: V by VGPR staging + ds_write, K by LDS-DMA -- measured slower (3B 2k 70.2 -> 72.8 us,
+                        // profiles/attn_prefill_vreg_ab_mi355x.jsonl): the DMA fill rate is not what bounds the loop
+#endif
 
 typedef short s16x4p_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4p_t* lds_s4p_ptr;
@@ -157,13 +161,30 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   const unsigned kl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Ks[gi][0][4 * w * D]));
   const unsigned vl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Vs[gi][0][4 * w * D]));
+  // LSA_P32_VREG: V tiles travel global -> VGPRs -> ds_write (staged across the tile's compute) while K keeps
+  // the LDS-DMA path, so the per-CU DMA fill rate carries half the bytes per tile
+  // (four named registers, not an array: hipcc's promote-alloca would move an array into the free LDS)
+  uint4 vst0, vst1, vst2, vst3;
+  auto vst = [&](int i) -> uint4& { return i == 0 ? vst0 : (i == 1 ? vst1 : (i == 2 ? vst2 : vst3)); };
   auto dma_tile = [&](int blk, int b) {
     const size_t base = ((size_t)blk * Hkv + hk) * 64 * D;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const unsigned lo = (unsigned)(b * 64 * D + 16 * i * D) * 2u;  // buffer b, rows 4 (w + 4 i) ..
       dma16s(kc + base, koff[i], kl0 + lo);
-      dma16s(vc + base, voff[i], vl0 + lo);
+      if constexpr (LSA_P32_VREG)
+        vst(i) = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(vc + base) + voff[i]);
+      else
+        dma16s(vc + base, voff[i], vl0 + lo);
+    }
+  };
+  auto vwrite = [&](int b) {  // the staged V rows to the image slots the DMA would have filled
+    if constexpr (LSA_P32_VREG) {
+      // compiler fence: hipcc otherwise hoists these stores up to their loads (a vmcnt(0) per load at the tile
+      // start, serialising the staging it should hide)
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(&Vs[gi][b][4 * (w + 4 * i) * D + lane * 8]) = vst(i);
     }
   };
   int bnext = 0;  // block of tile t + 1 (loaded one iteration ahead: no dependent load on the DMA path)
@@ -172,6 +193,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
     if (ntiles > 1) bnext = __builtin_amdgcn_readfirstlane(bt[t0 + 1]);
   }
   __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): tile 0 has landed
+  if (ntiles > 0) vwrite(0);
   __syncthreads();
   const int G16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
   for (int tt = 0; tt < nt_max; ++tt) {
@@ -271,6 +293,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
     }
     bnext = bnn;
     __builtin_amdgcn_s_waitcnt(0);  // tile t + 1's DMA has landed before the barrier publishes it
+    if (tt + 1 < ntiles) vwrite((tt + 1) & 1);
     __syncthreads();
   }
   // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
