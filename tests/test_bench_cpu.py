@@ -36,7 +36,8 @@ def _run(nproc: int, extra=()):
     return lines[0]
 
 
-@pytest.mark.parametrize("nproc,extra,par,batch", [(1, (), "dp1", 3), (2, (), "dp2", 6), (2, ("--tp", "2"), "tp2dp1", 3)])
+@pytest.mark.parametrize("nproc,extra,par,batch", [(1, (), "dp1", 3), (2, (), "dp2", 6), (2, ("--tp", "2"), "tp2dp1", 3),
+                                                 (4, ("--tp", "2"), "tp2dp2", 6)])
 def test_bench_contract_cpu(nproc, extra, par, batch):
     d = _run(nproc, extra)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
