@@ -18,9 +18,10 @@
 #include "common.h"
 
 #define LSA_NEG_P (-1.0e30f)
-#ifndef LSA_P32_VREG
-#define LSA_P32_VREG 0  // 1: V by VGPR staging + ds_write, K by LDS-DMA -- measured slower (3B 2k 70.2 -> 72.8 us,
-                        // profiles/attn_prefill_vreg_ab_mi355x.jsonl): the DMA fill rate is not what bounds the loop
+#ifndef LSA_P32_NBUF1
+#define LSA_P32_NBUF1 2  // K / V tile buffers of the single-group (NG = 1) kernel: the DMA runs NBUF - 1 tiles
+                         // ahead.  4 (128 KiB, 3 tiles ahead) measured slower: one workgroup per CU instead of two
+                         // (3B 2k single 86.5 -> 127.7 us, 4 x 1k 78.3 -> 109.2; profiles/attn_prefill_nbuf_ab_mi355x.jsonl)
 #endif
 
 typedef short s16x4p_t __attribute__((ext_vector_type(4)));
@@ -55,6 +56,16 @@ __device__ __forceinline__ void dma16s(const void* gbase, unsigned voff, unsigne
                : "=&s"(keep)
                : "v"(voff), "s"(gbase), "s"(lds_base)
                : "memory");
+}
+
+// wait until at most k later tiles' DMAs (8 wave-instructions each: 4 K + 4 V rows groups) are in flight (k is
+// wave-uniform; vmcnt counts this wave's vector-memory instructions in issue order), and for this wave's LDS reads
+// The builtin (not inline asm), so hipcc's own wait tracking sees it.  simm16 on gfx9: vmcnt[3:0] bits 3:0,
+// expcnt bits 6:4 (7 = no wait), lgkmcnt bits 11:8, vmcnt[5:4] bits 15:14.
+__device__ __forceinline__ void wait_dma_tiles(int k) {
+  if (k <= 0) __builtin_amdgcn_s_waitcnt(0x0070);       // vmcnt(0) lgkmcnt(0)
+  else if (k == 1) __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) lgkmcnt(0)
+  else __builtin_amdgcn_s_waitcnt(0x4070);              // vmcnt(16) lgkmcnt(0)
 }
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
@@ -100,10 +111,11 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
                                                                      float scale_log2, uint16_t* __restrict__ out,
                                                                      float* __restrict__ part, float* __restrict__ part_ml) {
   constexpr int D = 128;
-  // K / V tiles, double-buffered per group, filled by LDS-DMA (global_load_lds: no staging registers, and the
-  // DMA of tile t + 1 runs under tile t's MFMAs)
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[NG][2][64 * D];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[NG][2][64 * D];
+  // K / V tiles, NB buffers per group, filled by LDS-DMA (global_load_lds: no staging registers, and the DMAs of
+  // the next NB - 1 tiles run under tile t's MFMAs)
+  constexpr int NB = NG == 1 ? LSA_P32_NBUF1 : 2;  // tile buffers per group (NG = 2: 2 x 2 x 32 KiB fills the LDS)
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[NG][NB][64 * D];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[NG][NB][64 * D];
   const int wi = blockIdx.x, h = blockIdx.y;
   // wave and group ids are wave-uniform: readfirstlane lets hipcc keep every per-group work field, block id
   // and DMA base in SGPRs (selected by a VGPR id, the whole tile loop's address math ran on the VALU)
@@ -161,50 +173,36 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   const unsigned kl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Ks[gi][0][4 * w * D]));
   const unsigned vl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Vs[gi][0][4 * w * D]));
-  // LSA_P32_VREG: V tiles travel global -> VGPRs -> ds_write (staged across the tile's compute) while K keeps
-  // the LDS-DMA path, so the per-CU DMA fill rate carries half the bytes per tile
-  // (four named registers, not an array: hipcc's promote-alloca would move an array into the free LDS)
-  uint4 vst0, vst1, vst2, vst3;
-  auto vst = [&](int i) -> uint4& { return i == 0 ? vst0 : (i == 1 ? vst1 : (i == 2 ? vst2 : vst3)); };
   auto dma_tile = [&](int blk, int b) {
     const size_t base = ((size_t)blk * Hkv + hk) * 64 * D;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const unsigned lo = (unsigned)(b * 64 * D + 16 * i * D) * 2u;  // buffer b, rows 4 (w + 4 i) ..
       dma16s(kc + base, koff[i], kl0 + lo);
-      if constexpr (LSA_P32_VREG)
-        vst(i) = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(vc + base) + voff[i]);
-      else
-        dma16s(vc + base, voff[i], vl0 + lo);
+      dma16s(vc + base, voff[i], vl0 + lo);
     }
   };
-  auto vwrite = [&](int b) {  // the staged V rows to the image slots the DMA would have filled
-    if constexpr (LSA_P32_VREG) {
-      // compiler fence: hipcc otherwise hoists these stores up to their loads (a vmcnt(0) per load at the tile
-      // start, serialising the staging it should hide)
-      asm volatile("" ::: "memory");
+  // the DMA runs NB - 1 tiles ahead: the prologue issues tiles 0 .. NB - 2, iteration tt issues tile tt + NB - 1
+  // into the buffer tile tt - 1 left (its readers passed the previous barrier)
+  int bnext = 0;  // block of the next tile to issue (loaded one iteration ahead: no dependent load on the DMA path)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(&Vs[gi][b][4 * (w + 4 * i) * D + lane * 8]) = vst(i);
-    }
-  };
-  int bnext = 0;  // block of tile t + 1 (loaded one iteration ahead: no dependent load on the DMA path)
-  if (ntiles > 0) {
-    dma_tile(__builtin_amdgcn_readfirstlane(bt[t0]), 0);
-    if (ntiles > 1) bnext = __builtin_amdgcn_readfirstlane(bt[t0 + 1]);
-  }
-  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): tile 0 has landed
-  if (ntiles > 0) vwrite(0);
+  for (int p = 0; p < NB - 1; ++p)
+    if (p < ntiles) dma_tile(__builtin_amdgcn_readfirstlane(bt[t0 + p]), p);
+  if (NB - 1 < ntiles) bnext = __builtin_amdgcn_readfirstlane(bt[t0 + NB - 1]);
+  // everything issued so far has landed (the Q fragments too, so hipcc's own wait tracking starts the loop with
+  // no outstanding loads and inserts no vmcnt waits of its own in front of the K reads)
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   const int G16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
   for (int tt = 0; tt < nt_max; ++tt) {
     const int t = t0 + tt;  // absolute key tile
     int bnn = 0;
-    if (tt + 1 < ntiles) {
-      dma_tile(bnext, (tt + 1) & 1);  // its buffer's last readers (tile t - 1) passed the previous barrier
-      if (tt + 2 < ntiles) bnn = __builtin_amdgcn_readfirstlane(bt[t + 2]);
+    if (tt + NB - 1 < ntiles) {
+      dma_tile(bnext, (tt + NB - 1) % NB);  // its buffer's last readers (tile t - 1) passed the previous barrier
+      if (tt + NB < ntiles) bnn = __builtin_amdgcn_readfirstlane(bt[t + NB]);
     }
-    const uint16_t* Kg = Ks[gi][tt & 1];
-    const uint16_t* Vg = Vs[gi][tt & 1];
+    const uint16_t* Kg = Ks[gi][tt % NB];
+    const uint16_t* Vg = Vs[gi][tt % NB];
     if (t < wave_tiles) {  // causal: tiles past the wave's last row are skipped (barriers stay uniform)
       // S^T for the two 32-key halves
       f32x16_t st[2];
@@ -292,8 +290,8 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
         }
     }
     bnext = bnn;
-    __builtin_amdgcn_s_waitcnt(0);  // tile t + 1's DMA has landed before the barrier publishes it
-    if (tt + 1 < ntiles) vwrite((tt + 1) & 1);
+    // tile t + 1's DMA has landed before the barrier publishes it; the tiles issued after it may stay in flight
+    wait_dma_tiles(min(ntiles - 1, tt + NB - 1) - (tt + 1));
     __syncthreads();
   }
   // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
