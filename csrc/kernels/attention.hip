@@ -80,6 +80,9 @@ struct RopeArgs {
 #ifndef LSA_ATTN_WPE8
 #define LSA_ATTN_WPE8 6  // fp8 cache, G = 1 (8 = 64 VGPRs, one grid round at B x Hkv = 1024: spills, 7B b32 ctx 200 17.6 -> 18.2 us)
 #endif
+#ifndef LSA_ATTN_SB_MIN_WG
+#define LSA_ATTN_SB_MIN_WG 512  // grids of at least this many workgroups run the single-buffered G = 1 kernel (SB)
+#endif
 #ifndef LSA_ATTN_BUF_G
 #define LSA_ATTN_BUF_G 2
 #endif
@@ -95,9 +98,15 @@ struct RopeArgs {
 // groups of 8 dims, but one 16-byte load per lane now carries two keys (half the load instructions and half
 // the HBM bytes of the bf16 cache); a K slice is widened to bf16 exactly (v_cvt_scalef32_pk_bf16_fp8) for the
 // same dot2 products and its scale multiplies the reduced score; a V slice goes to f32 with its scale in p.
-template <int G, int ROPE, int WV, bool KV8 = false>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime
+//
+// SB (G = 1, bf16 cache, large grids): ONE K/V register set -- each wave waits for its own block, and the 56-VGPR
+// kernel runs 8 waves per SIMD (four 8-wave workgroups per CU), so the 7B's B x Hkv = 1024 workgroups at batch 32
+// fill the chip in one grid round and the waves of a CU hide each other's load latency: 7B b32 ctx 200
+// 22.1 -> 18.6 us, decode step 3.60 -> 3.50 ms (profiles/attn_decode_sb_ab_mi355x.jsonl).  Small grids keep the
+// two-set pipeline (7B b1: 6.8 vs 7.1 us).
+template <int G, int ROPE, int WV, bool KV8 = false, bool SB = false>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime
 __global__ __launch_bounds__(64 * WV)
-__attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (KV8 ? LSA_ATTN_WPE8 : LSA_ATTN_WPE) : 1))) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+__attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (KV8 ? LSA_ATTN_WPE8 : (SB ? 8 : LSA_ATTN_WPE)) : 1))) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc,
                                                           const float* __restrict__ ksc, const float* __restrict__ vsc,
                                                           const int* __restrict__ block_tables, int max_blocks,
@@ -377,7 +386,16 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (KV8 ? LSA_ATTN_WPE8 : LS
       }
     }
   };
-  if (blk0 < blk1) {
+  static_assert(!SB || (G == 1 && !KV8), "SB: G = 1, bf16 cache");
+  if constexpr (SB) {
+    // single register set: each wave waits for its block, the 32 waves of a CU overlap each other's loads
+    for (int blk = blk0; blk < blk1; ++blk) {
+      if (blk != blk0) fetch(kA, vA, ksA, vsA, blk, ctx - 1 - blk * 64);
+      __builtin_amdgcn_sched_barrier(0);
+      score(kA, vA, ksA, vsA, blk);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else if (blk0 < blk1) {
     int blk = blk0;
     for (; blk + 1 < blk1; blk += 2) {
       fetch(kB, vB, ksB, vsB, blk + 1, ctx - 1 - (blk + 1) * 64);
@@ -578,6 +596,11 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
       hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4), true>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, \
                          qq, kk, vv, ks, vs, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max,  \
                          oo, opart, mlpart, counters, xf_mt, ra);                                                      \
+    else if (GV == 1 && (long)grid.x * grid.y * grid.z >= LSA_ATTN_SB_MIN_WG)                                          \
+      hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4), false, GV == 1>), grid,                      \
+                         dim3(GV <= 3 ? 512 : 256), 0, s, qq, kk, vv, ks, vs,                                          \
+                         block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart, \
+                         counters, xf_mt, ra);                                                                         \
     else                                                                                                               \
       hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4)>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, qq,   \
                          kk, vv, ks, vs, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max,   \

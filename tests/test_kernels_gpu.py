@@ -406,6 +406,31 @@ def test_attn_decode_fused_rope(gpu, HH, lens, nparts):
     assert _rel(o2, o1) < 1e-2
 
 
+@pytest.mark.parametrize("B", [2, 16, 20])
+def test_attn_decode_g1_single_buffer_grids(gpu, B):
+    """G = 1 (7B MHA) decode attention with fused RoPE / KV append on both sides of the single-buffer grid
+    threshold (B x 32 heads >= 512 workgroups: one K/V register set at 8 waves / SIMD; below it the two-set
+    pipeline) vs the fp32 reference over the rope_append-written cache."""
+    H = Hkv = 32
+    D = 128
+    lens = [(37 * i) % 300 + 1 for i in range(B)]
+    kc, vc, bt = _paged(lens, Hkv, D, gpu, seed=11)
+    pos = torch.tensor([n - 1 for n in lens], device=gpu, dtype=torch.int32)
+    cos, sin = ref.rope_tables(D, 4096, 500000.0, device=gpu)
+    parts = torch.randn(2, B, (H + 2 * Hkv) * D, device=gpu)
+    scale = 1 / math.sqrt(D)
+    k1, v1 = kc.clone(), vc.clone()
+    q1 = torch.empty(B, H, D, device=gpu, dtype=torch.bfloat16)
+    ops.rope_append(parts, pos, None, bt, cos, sin, q1, k1, v1, H, Hkv)
+    o_ref = torch.empty(B, H, D, device=gpu, dtype=torch.bfloat16)
+    ref.attn_decode(q1, k1, v1, bt, pos, H, Hkv, scale, o_ref)
+    o = torch.empty_like(o_ref)
+    ops.attn_decode(torch.empty_like(q1), kc, vc, bt, pos, H, Hkv, scale, o, qkv_parts=parts, cos=cos, sin=sin)
+    torch.cuda.synchronize()
+    assert _rel(o, o_ref) < 1e-2
+    assert torch.equal(vc, v1)
+
+
 @pytest.mark.parametrize("kernel", ["16", "32", "32pair"])
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
 @pytest.mark.parametrize("case", ["fresh", "chunked", "long"])
