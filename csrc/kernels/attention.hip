@@ -80,6 +80,9 @@ struct RopeArgs {
 #ifndef LSA_ATTN_WPE8
 #define LSA_ATTN_WPE8 6  // fp8 cache, G = 1 (8 = 64 VGPRs, one grid round at B x Hkv = 1024: spills, 7B b32 ctx 200 17.6 -> 18.2 us)
 #endif
+#ifndef LSA_ATTN_SB8
+#define LSA_ATTN_SB8 1  // the single-buffered G = 1 kernel for the fp8 KV cache too
+#endif
 #ifndef LSA_ATTN_SB_MIN_WG
 #define LSA_ATTN_SB_MIN_WG 512  // grids of at least this many workgroups run the single-buffered G = 1 kernel (SB)
 #endif
@@ -106,7 +109,7 @@ struct RopeArgs {
 // two-set pipeline (7B b1: 6.8 vs 7.1 us).
 template <int G, int ROPE, int WV, bool KV8 = false, bool SB = false>  // ROPE: 0 = q given; > 0 = that many QKV slabs; < 0 = runtime
 __global__ __launch_bounds__(64 * WV)
-__attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (KV8 ? LSA_ATTN_WPE8 : (SB ? 8 : LSA_ATTN_WPE)) : 1))) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+__attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN_WPE8 : LSA_ATTN_WPE)) : 1))) void attn_decode_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc,
                                                           const float* __restrict__ ksc, const float* __restrict__ vsc,
                                                           const int* __restrict__ block_tables, int max_blocks,
@@ -386,7 +389,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (KV8 ? LSA_ATTN_WPE8 : (S
       }
     }
   };
-  static_assert(!SB || (G == 1 && !KV8), "SB: G = 1, bf16 cache");
+  static_assert(!SB || G == 1, "SB: G = 1");
   if constexpr (SB) {
     // single register set: each wave waits for its block, the 32 waves of a CU overlap each other's loads
     for (int blk = blk0; blk < blk1; ++blk) {
@@ -592,7 +595,11 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
                     const_cast<uint16_t*>(vv), const_cast<float*>(ks), const_cast<float*>(vs)};
 #define LSA_ADK(GV, RP)                                                                                               \
   do {                                                                                                                 \
-    if (ks)                                                                                                            \
+    if (ks && GV == 1 && LSA_ATTN_SB8 && (long)grid.x * grid.y * grid.z >= LSA_ATTN_SB_MIN_WG)                         \
+      hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4), true, GV == 1>), grid,                       \
+                         dim3(GV <= 3 ? 512 : 256), 0, s, qq, kk, vv, ks, vs, block_tables, max_blocks, pos, Hkv, sl2, \
+                         chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart, counters, xf_mt, ra);                   \
+    else if (ks)                                                                                                       \
       hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4), true>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, \
                          qq, kk, vv, ks, vs, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max,  \
                          oo, opart, mlpart, counters, xf_mt, ra);                                                      \
