@@ -40,6 +40,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "long":  # larger grids at longer contex
                   "7b_b4_ctx1024": (4, 32, 32, 1024, 4), "3b_b1_ctx2100": (1, 24, 8, 2100, 8),
                   "3b_b16_ctx1024": (16, 24, 8, 1024, 4), "3b_b2_ctx2048": (2, 24, 8, 2048, 8),
                   "3b_b1_ctx8192": (1, 24, 8, 8192, 8), "7b_b1_ctx200": (1, 32, 32, 200, 4)})
+if len(sys.argv) > 1 and sys.argv[1] == "grid":  # 7B (G = 1) around the single-buffer grid threshold
+    cases = {f"7b_b{B}_ctx{c}": (B, 32, 32, c, 2) for B in (8, 16, 24, 32, 64) for c in (200, 512)}
 cos, sin = ref.rope_tables(128, 64 * max((c[3] + 63) // 64 for c in cases.values()), 500000.0, device=dev)
 for name, (B, H, Hkv, ctx, nparts) in cases.items():
     nblk = (ctx + 63) // 64
