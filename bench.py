@@ -12,9 +12,16 @@ downloaded), bf16 (or ``--dtype fp8`` weights).
     torchrun --nproc-per-node 8 bench.py --gpus 8     # 8 DP replicas of one GPU each (dp8)
     torchrun --nproc-per-node 8 bench.py --gpus 8 --tp 2   # BASELINE config 4: 4 replicas x TP2 (tp2dp4)
 
-Before the timed region one request of the first warm-up round is checked against the plain fp32
-PyTorch forward over the same weights (``models.llama.reference_forward``, teacher-forced: every chosen
-token must be within bf16 noise of the oracle's argmax); the result is reported as ``numerics``.
+Before the timed region the decode path is checked at the benchmark's batch (``eval/numerics.py``): the batch
+is decoded greedily for 64 steps with each step's logits recorded, and two of its sequences are fed, with the
+engine's own tokens, through the plain fp32 PyTorch forward over the same (for TP: the unsharded) weights
+(``models.llama.reference_forward``, emulating fp8 quantisation where the engine quantises); mean KL, top-1 and
+top-5 agreement over the 64 positions are reported as ``numerics``.
+
+One-GPU runs then also time, untimed by the headline (after its region), BASELINE config 2 (the same model at
+batch 1: ``p50_e2e_latency_s_b1``, ``decode_device_ms_per_step_b1``) and config 3 (Llama-3.2-3B /explain_error
+with a 2k-token prompt, batch 1: ``explain_2k_p50_e2e_latency_s``, ``explain_2k_device_ms_per_step``), each with
+its own teacher-forced numerics check (``--no-extras`` skips them).
 
 Prints ONE JSON line on rank 0.  ``value`` = whole-job output tokens/s (sum over replicas, timed by
 the slowest rank); ``vs_baseline`` = value / 4.0 tok/s, the only throughput figure BASELINE.md
@@ -24,6 +31,7 @@ derives for the reference (its measured numbers are latencies: ``vs_baseline_p50
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import statistics
@@ -49,45 +57,72 @@ def fp8_label(r, B):
     return f"fp8 (prefill W8A8 on fp8 MFMA; decode {' / '.join(a8)} W8A8 on fp8 MFMA, the rest W8A16)"
 
 
-def check_numerics(eng, prompt, tokens, n=16, prefill_rows=0, decode_batch=0):
-    """Teacher-forced check of the first ``n`` generated tokens against the fp32 reference forward:
-    gap = (oracle max logit - oracle logit of our token) / oracle logit std, worst over the tokens.
-    fp8 weights: the prompt rows get the W8A8 prefill's per-token activation rounding in the oracle when
-    the packed prefill had > 64 rows (``prefill_rows``), as the engine's kernels do."""
-    from llm_based_apache_spark_optimization_amd import ops
-    from llm_based_apache_spark_optimization_amd.models.llama import reference_forward
+def numerics_check(eng, prompts, n_steps, rank0: bool, tp: int, model: str, dtype: str, device):
+    """Teacher-forced check of the decode path at the benchmark's batch (eval/numerics.py): every rank runs the
+    recording decode (TP ranks in lockstep), global rank 0 compares rows against the fp32 oracle over the
+    UNSHARDED weights (TP engines hold one shard: the oracle regenerates the full seeded weights)."""
+    from llm_based_apache_spark_optimization_amd.eval import numerics as nm
 
-    toks = list(tokens[:n])
-    fp8 = eng.runner.w.layers[0].wqkv.kind == "fp8"
-    aq = len(prompt) if (fp8 and prefill_rows > 64 and ops.FP8_W8A8) else 0
-    r = eng.runner
-    unfused_xf = bool(decode_batch and r.a8 and r.use_xfrag(decode_batch) and not (
-        r.fused_norm and decode_batch <= r.fused_norm_max_batch))
-    da8 = unfused_xf and decode_batch > r.a8_min_batch  # decode qkv W8A8
-    da8m = unfused_xf and decode_batch > r.a8_mlp_min_batch  # decode gate_up W8A8
-    lg = reference_forward(r.w, list(prompt) + toks[:-1], act_quant_rows=aq, decode_a8=da8,
-                           decode_a8_mlp=da8m, kv_fp8=r.kv_fp8)[len(prompt) - 1:]
-    chosen = lg.gather(1, torch.tensor(toks, device=lg.device).view(-1, 1)).squeeze(1)
-    gap = ((lg.max(1).values - chosen) / lg.std(1)).max().item()
-    agree = int((lg.argmax(1).cpu() == torch.tensor(toks)).sum())
-    del lg
-    if r.kv_fp8:
-        # fp8 KV cache: every cached key / value row is rounded to e4m3 in the engine and in the oracle, from
-        # values that differ at the bf16 level, so rows near a rounding boundary differ by a full e4m3 step; over
-        # 32 layers on random-init weights (leading logits within a fraction of a std) that flips near-ties.
-        # Per-layer parity at the strict criterion is pinned by tests/test_kv_fp8_gpu.py (2-layer prod shapes)
-        ok, crit = gap < 1.0, "fp8 KV cache: gap < 1.0 std (quantisation-level; top-1 agreement reported)"
-    elif aq or da8 or da8m:
-        # W8A8 prefill: every prompt activation is rounded to e4m3 (3 mantissa bits); the oracle rounds the
-        # same rows, but values near a rounding boundary land on different sides in the two computations, so
-        # the prompt's K/V differ by quantisation-level noise that 32 layers accumulate.  On random-init
-        # weights the leading logits sit within a fraction of a std of each other, so the criterion is the
-        # quantisation-level one: every chosen token within 1 std of the oracle's best, half of them its argmax
-        ok, crit = gap < 1.0 and agree >= len(toks) // 2, "W8A8: gap < 1.0 std, >= half top-1"
-    else:
-        ok, crit = gap < 0.15, "gap < 0.15 std"
-    return {"tokens_checked": len(toks), "argmax_agree": agree, "max_gap_in_logit_std": round(gap, 4),
-            "ok": ok, "criterion": crit}
+    toks, elog = nm.record_decode_logits(eng, prompts, n_steps)
+    if not rank0:
+        return None
+    weights = None
+    if tp > 1:
+        from llm_based_apache_spark_optimization_amd.models import get_spec
+        from llm_based_apache_spark_optimization_amd.models.llama import init_random
+
+        weights = init_random(get_spec(model), device, seed=0, kind=dtype)
+    res = nm.check_recorded(eng, prompts, toks, elog, n_steps, check_rows=(0, len(prompts) - 1), weights=weights)
+    del weights, elog
+    return res
+
+
+def _timed_rounds(eng, prompts, params, n: int):
+    """n untimed-by-the-headline rounds: (p50 e2e latency s, GPU ms per decode step)."""
+    import statistics as st
+
+    eng.generate(prompts, params)  # warm (graphs of this bucket captured)
+    eng.stats.update(decode_s=0.0, decode_steps=0, prefill_s=0.0, decode_device_s=0.0)
+    lat = []
+    for _ in range(n):
+        t = time.perf_counter()
+        res = eng.generate(prompts, params)
+        lat.append(time.perf_counter() - t)
+        assert all(r.eval_count == params.max_tokens for r in res)
+    return st.median(lat), 1000.0 * eng.stats["decode_device_s"] / max(1, eng.stats["decode_steps"])
+
+
+def batch1_round(eng, prompt, args) -> dict:
+    """BASELINE config 2 on the same engine: one request, ``--new-tokens`` greedy tokens (the reference's own
+    per-request shape, Model_Evaluation_&_Comparision.py:113-119)."""
+    from llm_based_apache_spark_optimization_amd.engine import SamplingParams
+
+    num = numerics_check(eng, [prompt], min(64, args.new_tokens - 1), True, 1, args.model, args.dtype, None)
+    p50, dev = _timed_rounds(eng, [prompt], SamplingParams(max_tokens=args.new_tokens, temperature=0.0,
+                                                           ignore_eos=True), 5)
+    return {"p50_e2e_latency_s_b1": round(p50, 4), "decode_device_ms_per_step_b1": round(dev, 3),
+            "vs_baseline_p50_latency_b1": round(REF_P50_S / p50, 2), "numerics_b1": num}
+
+
+def explain_round(device, prompt_len: int = 2048, new_tokens: int = 128) -> dict:
+    """BASELINE config 3: Llama-3.2-3B-Instruct /explain_error, a ``prompt_len``-token synthetic Spark stack
+    trace, batch 1, bf16 (Flask/app.py:153-164)."""
+    from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build_engine
+
+    eng = build_engine("llama3.2", device=str(device), dtype="bf16", max_slots=2,
+                       max_model_len=prompt_len + new_tokens + 64, seed=0)
+    g = torch.Generator().manual_seed(4321)
+    prompt = [eng.spec.bos_id] + torch.randint(3, eng.spec.vocab_size, (prompt_len - 1,), generator=g).tolist()
+    num = numerics_check(eng, [prompt], 64, True, 1, "llama3.2", "bf16", None)
+    p50, dev = _timed_rounds(eng, [prompt], SamplingParams(max_tokens=new_tokens, temperature=0.0, ignore_eos=True), 3)
+    out = {"explain_2k_p50_e2e_latency_s": round(p50, 4), "explain_2k_device_ms_per_step": round(dev, 3),
+           "vs_baseline_p50_latency_explain": round(REF_P50_S_LLAMA / p50, 2), "numerics_explain_2k": num,
+           "explain_2k_config": {"model": MODEL_NAMES["llama3.2"], "prompt_len": prompt_len, "new_tokens": new_tokens,
+                                 "batch": 1, "dtype": "bf16"}}
+    del eng
+    gc.collect()
+    torch.cuda.empty_cache()
+    return out
 
 
 def main() -> int:
@@ -106,6 +141,9 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="run the same bench flow on CPU over gloo (tests of the multi-rank path; not a measurement)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the untimed BASELINE config 2 (batch 1) / config 3 (3B 2k explain) rounds after the "
+                         "timed region (they run on one-GPU-per-replica GPU benches by default)")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -153,12 +191,10 @@ def main() -> int:
         assert all(r.eval_count == args.new_tokens for r in res), [r.eval_count for r in res]
         return res
 
-    numerics = None
+    # numerics before the warm-up: a teacher-forced decode of the same batch, >= 64 steps when the run has them
+    numerics = numerics_check(eng, prompts, min(64, args.new_tokens - 1), rank == 0, tp, args.model, args.dtype, device)
     for i in range(args.warmup):
-        res = one_step()
-        if i == 0 and tp == 1:
-            numerics = check_numerics(eng, prompts[0], res[0].token_ids, prefill_rows=args.batch * args.prompt_len,
-                                      decode_batch=args.batch)
+        one_step()
     eng.stats.update(decode_s=0.0, decode_steps=0, prefill_s=0.0, decode_device_s=0.0)  # timed rounds only
     if world > 1:
         dist.barrier()
@@ -186,6 +222,19 @@ def main() -> int:
     # host-side decode_s also waits for: its first sync lands after the asynchronously launched prefill)
     decode_ms_tok = 1000.0 * eng.stats["decode_s"] / max(1, eng.stats["decode_steps"])
     decode_dev_ms = 1000.0 * eng.stats["decode_device_s"] / max(1, eng.stats["decode_steps"])
+    extras = {}
+    if world == 1 and not cpu and not args.no_extras:
+        extras.update(batch1_round(eng, prompts[0], args))
+        dtype_label = (args.dtype if args.dtype == "bf16" else fp8_label(eng.runner, args.batch)) \
+            + ("; fp8 e4m3 KV cache" if eng.runner.kv_fp8 else "")
+        del eng
+        gc.collect()
+        torch.cuda.empty_cache()
+        extras.update(explain_round(device))
+        eng = None
+    else:
+        dtype_label = (args.dtype if args.dtype == "bf16" else fp8_label(eng.runner, args.batch)) \
+            + ("; fp8 e4m3 KV cache" if eng.runner.kv_fp8 else "")
     if rank == 0:
         ref_p50 = REF_P50_S_LLAMA if args.model.startswith("llama") else REF_P50_S
         par = f"dp{dp}" if tp == 1 else f"tp{tp}dp{dp}"
@@ -200,8 +249,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / REF_TOK_S, 2),
-            "dtype": (args.dtype if args.dtype == "bf16" else fp8_label(eng.runner, args.batch))
-            + ("; fp8 e4m3 KV cache" if eng.runner.kv_fp8 else ""),
+            "dtype": dtype_label,
             "data": "synthetic prompts, random-init weights" + (" (CPU rehearsal, not a measurement)" if cpu else ""),
             "config": {
                 "model": MODEL_NAMES.get(args.model, args.model),
@@ -218,6 +266,7 @@ def main() -> int:
             "decode_device_ms_per_step": round(decode_dev_ms, 3),
             "per_gpu_tokens_per_sec": round(value / world, 2),
             "numerics": numerics,
+            **extras,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

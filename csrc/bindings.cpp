@@ -54,7 +54,7 @@ int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int 
 void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                        const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
-                       void* out, int ng, float* part, float* part_ml, const int* combine, int ncomb, hipStream_t s);
+                       void* out, int ng, hipStream_t s);
 int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
 int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
                       void* out, int epi, int splitk, hipStream_t stream);
@@ -346,46 +346,6 @@ void silu_mul(const at::Tensor& g, const at::Tensor& u, at::Tensor& o) {
 }
 
 extern "C" int lsa_attn_set_stamps(void* p);
-extern "C" int lsa_attn_o_set_stamps(void* p);
-void attn_o_set_stamps(const c10::optional<at::Tensor>& st) {
-  if (st.has_value()) TORCH_CHECK(st->is_cuda() && st->element_size() == 8, "stamps: int64 GPU tensor");
-  check(lsa_attn_o_set_stamps(st.has_value() ? st->data_ptr() : nullptr), "attn_o_set_stamps");
-}
-extern "C" int lsa_attn_o_b1(const float* qkv_parts, int nparts, long part_stride, const float* cos_t,
-                             const float* sin_t, const int* pos, void* kc, void* vc, const int* block_table, int H,
-                             float scale, const void* Wo, int N, float* slabs, int* tickets, const LsaEpi* ep,
-                             hipStream_t s);
-
-// batch-1 attention + O projection + residual in one launch (kernels/attention_o.hip)
-void attn_o_b1(const at::Tensor& qkv_parts, const at::Tensor& cos_t, const at::Tensor& sin_t, const at::Tensor& pos,
-               at::Tensor& kc, at::Tensor& vc, const at::Tensor& block_table, int64_t H, double scale,
-               const at::Tensor& wo, int64_t N, at::Tensor& slabs, at::Tensor& tickets, at::Tensor& h,
-               at::Tensor& xout, at::Tensor& ss_out) {
-  need(qkv_parts, at::kFloat, "qkv_parts");
-  need(pos, at::kInt, "pos");
-  need(block_table, at::kInt, "block_table");
-  need(wo, at::kBFloat16, "wo");
-  need(slabs, at::kFloat, "slabs");
-  need(tickets, at::kInt, "tickets");
-  need(h, at::kFloat, "h");
-  need(xout, at::kBFloat16, "xout");
-  need(ss_out, at::kLong, "ss_out");
-  TORCH_CHECK(qkv_parts.dim() == 3 && qkv_parts.size(1) >= 1 && qkv_parts.size(2) == 3 * H * 128 &&
-                  qkv_parts.stride(2) == 1, "qkv_parts must be [S, B, 3 H 128] slabs (MHA)");
-  TORCH_CHECK(wo.numel() == N * H * 128 && slabs.numel() >= H * N && tickets.numel() >= N / 512 &&
-                  h.numel() >= N && xout.numel() >= N, "attn_o_b1 operand sizes");
-  TORCH_CHECK(cos_t.size(0) >= block_table.size(-1) * 64, "rope tables shorter than the block table");
-  LsaEpi e{};
-  e.h = h.data_ptr<float>();
-  e.ldh = N;
-  e.xout = reinterpret_cast<uint16_t*>(xout.data_ptr());
-  e.ss_out = reinterpret_cast<long long*>(ss_out.data_ptr<int64_t>());
-  check(lsa_attn_o_b1(qkv_parts.data_ptr<float>(), qkv_parts.size(0), qkv_parts.stride(0), cos_t.data_ptr<float>(),
-                      sin_t.data_ptr<float>(), pos.data_ptr<int>(), kc.data_ptr(), vc.data_ptr(),
-                      block_table.data_ptr<int>(), H, (float)scale, wo.data_ptr(), N, slabs.data_ptr<float>(),
-                      tickets.data_ptr<int>(), &e, cur_stream()),
-        "attn_o_b1");
-}
 void attn_set_stamps(const c10::optional<at::Tensor>& st) {
   if (st.has_value()) TORCH_CHECK(st->is_cuda() && st->element_size() == 8, "stamps: int64 GPU tensor");
   check(lsa_attn_set_stamps(st.has_value() ? st->data_ptr() : nullptr), "attn_set_stamps");
@@ -450,30 +410,16 @@ void kv8_dequant(const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& k
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                   const at::Tensor& cu_q, const at::Tensor& ctx_lens, const at::Tensor& work, int64_t H, int64_t Hkv,
-                  double scale, at::Tensor& out, int64_t rows32, const c10::optional<at::Tensor>& part,
-                  const c10::optional<at::Tensor>& part_ml, const c10::optional<at::Tensor>& combine, int64_t n_pslots) {
+                  double scale, at::Tensor& out, int64_t rows32) {
   need(q, at::kBFloat16, "q");
   need(work, at::kInt, "work");
   if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip)
-    // work [n_workgroups, 5 * NG]: NG (seq, q_start, t0, t1, pslot) items per workgroup (ops.prefill_plan)
-    TORCH_CHECK(work.dim() == 2 && (work.size(1) == 5 || work.size(1) == 10) && work.is_contiguous(),
-                "attn_prefill32 work must be [n, 5] or [n, 10] int32");
-    int ncomb = 0;
-    if (combine.has_value() && combine->numel() > 0) {  // KV-split heavy blocks: partial slots + merge items
-      TORCH_CHECK(part.has_value() && part_ml.has_value(), "split prefill needs the partial workspace");
-      need(*combine, at::kInt, "combine");
-      need(*part, at::kFloat, "part");
-      need(*part_ml, at::kFloat, "part_ml");
-      TORCH_CHECK(combine->dim() == 2 && combine->size(1) == 4 && combine->is_contiguous(), "combine must be [n, 4]");
-      TORCH_CHECK(part->numel() >= n_pslots * H * 128 * 128 && part_ml->numel() >= n_pslots * H * 128 * 2,
-                  "prefill partial workspace too small for ", n_pslots, " slots");
-      ncomb = (int)combine->size(0);
-    }
+    // work [n_workgroups, 4 * NG]: NG (seq, q_start, t0, t1) items per workgroup (ops.prefill_plan)
+    TORCH_CHECK(work.dim() == 2 && (work.size(1) == 4 || work.size(1) == 8) && work.is_contiguous(),
+                "attn_prefill32 work must be [n, 4] or [n, 8] int32");
     check(lsa_attn_prefill32(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                              block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
-                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 5),
-                             ncomb ? part->data_ptr<float>() : nullptr, ncomb ? part_ml->data_ptr<float>() : nullptr,
-                             ncomb ? combine->data_ptr<int>() : nullptr, ncomb, cur_stream()),
+                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 4), cur_stream()),
           "attn_prefill32");
     return;
   }
@@ -625,8 +571,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps") = 1e-5);
   m.def("quant_xf8", &quant_xf8, py::arg("x"), py::arg("mt"), py::arg("x8"), py::arg("sx"));
   m.def("attn_set_stamps", &attn_set_stamps, py::arg("stamps") = py::none());
-  m.def("attn_o_b1", &attn_o_b1);
-  m.def("attn_o_set_stamps", &attn_o_set_stamps, py::arg("stamps") = py::none());
   m.def("rope_append", &rope_append, py::arg("qkv"), py::arg("pos"), py::arg("tok_seq"), py::arg("block_tables"),
         py::arg("cos"), py::arg("sin"), py::arg("q_out"), py::arg("kc"), py::arg("vc"), py::arg("H"), py::arg("Hkv"),
         py::arg("ks") = py::none(), py::arg("vs") = py::none());
@@ -640,8 +584,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ks") = py::none(), py::arg("vs") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
-        py::arg("out"), py::arg("rows32") = 0, py::arg("part") = py::none(), py::arg("part_ml") = py::none(),
-        py::arg("combine") = py::none(), py::arg("n_pslots") = 0);
+        py::arg("out"), py::arg("rows32") = 0);
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);
   m.def("fp8_dequant", &fp8_dequant);

@@ -11,6 +11,7 @@
 // the peers with hipIpcOpenMemHandle):
 //   [0,      8 KiB)  flags[AR_MAX_BLOCKS][AR_MAX_WORLD]  u32, written by peers (epoch numbers)
 //   [8 KiB, 9 KiB)   epoch[AR_MAX_BLOCKS]                u32, this rank's per-block call counter
+//   [9 KiB, +4)      abort                               u32, set by ANY rank whose wait timed out
 //   [16 KiB, ...)    recv[2 parities][world][maxb]       pushed payloads
 // Uncached memory keeps remote pushes coherent with the receiver's reads (no stale L2 lines of a slot
 // from two calls ago).  The epoch lives on the device, so the launch has fixed arguments and replays
@@ -20,7 +21,10 @@
 //   * pushing into parity p at epoch ep is safe: reaching ep means the peer raised ep-1, which it
 //     does only after finishing ep-2 (the previous user of parity p).
 // Every wait is bounded by a wall-clock timeout that sets *err and drains the grid, so a missing
-// peer can never leave waves spinning on the GPU.
+// peer can never leave waves spinning on the GPU.  A rank that times out also raises the abort word in
+// every peer's region; every later call on every rank reads its own abort word first and then poisons its
+// result and sets its *err too, so the leader of a TP replica learns of a FOLLOWER's timeout at its next
+// host sync (engine/runner.py read_rows) instead of committing tokens computed from the follower's NaNs.
 #include "common.h"
 #include <cstring>
 
@@ -28,6 +32,7 @@
 #define AR_MAX_BLOCKS 256
 #define AR_FLAGS_OFF 0
 #define AR_EPOCH_OFF 8192
+#define AR_ABORT_OFF 9216
 #define AR_DATA_OFF 16384
 #define AR_THREADS 256
 
@@ -56,7 +61,9 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
   __shared__ int s_timeout;
   if (tid == 0) {
     s_ep = my_epoch[b] + 1u;
-    s_timeout = 0;
+    // a peer (or this rank) timed out in an earlier call: the group is out of step for good
+    s_timeout = ld_relaxed_sys(reinterpret_cast<const uint32_t*>(mine + AR_ABORT_OFF)) != 0u;
+    if (s_timeout) atomicExch(err, 1);
   }
   __syncthreads();
   const uint32_t ep = s_ep;
@@ -95,6 +102,8 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
       if (wall_clock64() - t0 > timeout_ticks) {
         atomicExch(err, 1);
         s_timeout = 1;
+        for (int p = 0; p < W; ++p)  // tell every rank (this one included) that the group is broken
+          st_release_sys(reinterpret_cast<uint32_t*>(regions[p] + AR_ABORT_OFF), 1u);
         break;
       }
     }

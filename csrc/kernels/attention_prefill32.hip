@@ -91,12 +91,10 @@ __device__ __forceinline__ int vp_off(int r, int col) { return r * 128 + ((((col
 // per CU instead of two heavy blocks landing on the same CU).  Each group has its own K / V image and its
 // own tile count; the groups only share the workgroup barriers (an idle group keeps passing them).
 //
-// Work item of a group: (seq, q_start, t0, t1, pslot) -- the key tiles [t0, t1) of one 128-row query block.
-// pslot < 0: the whole causal range, normalised output written directly.  pslot >= 0: one KV split of a heavy
-// block (ops.prefill_plan cuts blocks whose causal range exceeds the plan's tile budget, so the heaviest block
-// no longer sets the kernel's critical path); the group writes its unnormalised O and (m, l) per row to
-// partial slot pslot and attn_prefill_combine_kernel merges the splits.  pslot == -2 (NG = 2, both groups): the
-// two groups hold the same block, each a part of its key tiles, merged through LDS at the end (no combine launch).
+// Work item of a group: (seq, q_start, t0, t1) -- the key tiles [t0, t1) of one 128-row query block (the
+// whole causal range: t0 = 0; cutting heavy blocks into KV splits with a merge launch, or into two halves
+// merged in LDS, were both measured slower and removed: profiles/attn_prefill_kv_split_mi355x.jsonl,
+// profiles/attn_prefill_halves_mi355x.jsonl).
 //
 // O is accumulated TRANSPOSED, O^T += V^T P^T (A = V^T from the transposed LDS reads, B = P^T straight
 // from the S^T accumulator): the accumulator's column is then the query row = the lane, so the online-
@@ -108,8 +106,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
                                                                      const int* __restrict__ block_tables, int max_blocks,
                                                                      const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
                                                                      const int* __restrict__ work, int H, int Hkv,
-                                                                     float scale_log2, uint16_t* __restrict__ out,
-                                                                     float* __restrict__ part, float* __restrict__ part_ml) {
+                                                                     float scale_log2, uint16_t* __restrict__ out) {
   constexpr int D = 128;
   // K / V tiles, NB buffers per group, filled by LDS-DMA (global_load_lds: no staging registers, and the DMAs of
   // the next NB - 1 tiles run under tile t's MFMAs)
@@ -120,19 +117,19 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   // wave and group ids are wave-uniform: readfirstlane lets hipcc keep every per-group work field, block id
   // and DMA base in SGPRs (selected by a VGPR id, the whole tile loop's address math ran on the VALU)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
-  const int gi = NG == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 8), gtid = tid & 255;
+  const int gi = NG == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 8);
   const int r32 = lane & 31, hh = lane >> 5;
   const int hk = h / (H / Hkv);
 
   // tiles of every group (the loop runs to the largest; the barriers are workgroup-wide)
-  int nt_max = 0, ntiles = 0, seq = 0, qs = 0, t0 = 0, t1 = 0, pslot = -1;
+  int nt_max = 0, ntiles = 0, seq = 0, qs = 0, t0 = 0, t1 = 0;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    const int* wk = work + 5 * (NG * wi + g);
+    const int* wk = work + 4 * (NG * wi + g);
     const int sq = wk[0];
     const int nt = sq >= 0 ? wk[3] - wk[2] : 0;
     nt_max = max(nt_max, nt);
-    if (g == gi) { ntiles = nt; seq = sq; qs = wk[1]; t0 = wk[2]; t1 = wk[3]; pslot = wk[4]; }
+    if (g == gi) { ntiles = nt; seq = sq; qs = wk[1]; t0 = wk[2]; t1 = wk[3]; }
   }
   const bool active = seq >= 0;
   const int sqc = active ? seq : 0;
@@ -296,59 +293,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
   const int qr = qs + w * 32 + r32;
-  if constexpr (NG == 2) {
-    // pslot == -2 in group 0's item: both groups hold the SAME query block, split over its key tiles (group 0
-    // the unmasked first part, group 1 the rest with the diagonal); group 1's unnormalised O^T and (m, l) go
-    // through LDS (the K / V images are free: the loop's last barrier follows every group's last LDS read and
-    // DMA) and group 0 merges and stores -- the heaviest block's critical path halves without a merge launch
-    if (work[5 * (NG * wi) + 4] == -2) {
-      float* xo = reinterpret_cast<float*>(&Ks[0][0][0]);  // 256 threads x 64 floats = the 64 KiB of Ks
-      float* xml = reinterpret_cast<float*>(&Vs[0][0][0]);
-      if (gi == 1) {
-#pragma unroll
-        for (int db = 0; db < 4; ++db)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq)
-            *reinterpret_cast<float4*>(xo + ((db * 4 + gq) * 256 + gtid) * 4) =
-                make_float4(o[db][4 * gq + 0], o[db][4 * gq + 1], o[db][4 * gq + 2], o[db][4 * gq + 3]);
-        *reinterpret_cast<float2*>(xml + 2 * gtid) = make_float2(mrow, lrow);
-      }
-      __syncthreads();
-      if (gi == 0 && active && qr < qlen) {
-        const float2 ml1 = *reinterpret_cast<const float2*>(xml + 2 * gtid);
-        const float mm = fmaxf(mrow, ml1.x);
-        const float a0 = __builtin_amdgcn_exp2f(mrow - mm), a1 = __builtin_amdgcn_exp2f(ml1.x - mm);
-        const float L = lrow * a0 + ml1.y * a1;
-        const float inv = L > 0.f ? 1.f / L : 0.f;
-        const float w0 = a0 * inv, w1 = a1 * inv;
-        uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D + 4 * hh;
-#pragma unroll
-        for (int db = 0; db < 4; ++db)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            const float4 v = *reinterpret_cast<const float4*>(xo + ((db * 4 + gq) * 256 + gtid) * 4);
-            uint2 pk;
-            pk.x = pack2bf(o[db][4 * gq + 0] * w0 + v.x * w1, o[db][4 * gq + 1] * w0 + v.y * w1);
-            pk.y = pack2bf(o[db][4 * gq + 2] * w0 + v.z * w1, o[db][4 * gq + 3] * w0 + v.w * w1);
-            *reinterpret_cast<uint2*>(orow + 32 * db + 8 * gq) = pk;
-          }
-      }
-      return;
-    }
-  }
-  if (pslot >= 0) {  // one KV split: unnormalised O^T rows + (m, l), f32 (no workspace: nothing to write)
-    if (active && qr < qlen && part != nullptr) {
-      const size_t pr = ((size_t)pslot * H + h) * 128 + w * 32 + r32;
-      float* prow = part + pr * D + 4 * hh;
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq)
-          *reinterpret_cast<float4*>(prow + 32 * db + 8 * gq) =
-              make_float4(o[db][4 * gq + 0], o[db][4 * gq + 1], o[db][4 * gq + 2], o[db][4 * gq + 3]);
-      if (hh == 0) *reinterpret_cast<float2*>(part_ml + 2 * pr) = make_float2(mrow, lrow);
-    }
-  } else if (active && qr < qlen) {
+  if (active && qr < qlen) {
     const float inv = lrow > 0.f ? 1.f / lrow : 0.f;
     uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D + 4 * hh;
 #pragma unroll
@@ -363,69 +308,21 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
 }
 
-// Merge of the KV splits of the heavy query blocks: item c = (seq, q_start, pslot0, nsplit), grid (items, H),
-// 256 threads = 128 rows x 2 halves of 64 dims; log-sum-exp over the splits' (m, l), O = sum w_i O_i / sum w_i.
-__global__ __launch_bounds__(256) void attn_prefill_combine_kernel(const float* __restrict__ part,
-                                                                   const float* __restrict__ part_ml,
-                                                                   const int* __restrict__ items,
-                                                                   const int* __restrict__ cu_q, int H,
-                                                                   uint16_t* __restrict__ out) {
-  constexpr int D = 128;
-  const int* it = items + 4 * blockIdx.x;
-  const int seq = it[0], qs = it[1], p0 = it[2], ns = it[3];
-  const int h = blockIdx.y;
-  const int row = threadIdx.x >> 1, c0 = (threadIdx.x & 1) * 64;
-  const int q0 = cu_q[seq], qlen = cu_q[seq + 1] - q0;
-  if (qs + row >= qlen) return;
-  float M = LSA_NEG_P;
-  for (int i = 0; i < ns; ++i) M = fmaxf(M, part_ml[2 * (((size_t)(p0 + i) * H + h) * 128 + row)]);
-  float L = 0.f, acc[64];
-#pragma unroll
-  for (int j = 0; j < 64; ++j) acc[j] = 0.f;
-  for (int i = 0; i < ns; ++i) {
-    const size_t pr = ((size_t)(p0 + i) * H + h) * 128 + row;
-    const float2 ml = *reinterpret_cast<const float2*>(part_ml + 2 * pr);
-    const float wgt = __builtin_amdgcn_exp2f(ml.x - M);
-    L += ml.y * wgt;
-    const float* src = part + pr * D + c0;
-#pragma unroll
-    for (int j = 0; j < 64; j += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(src + j);
-      acc[j] += v.x * wgt; acc[j + 1] += v.y * wgt; acc[j + 2] += v.z * wgt; acc[j + 3] += v.w * wgt;
-    }
-  }
-  const float inv = L > 0.f ? 1.f / L : 0.f;
-  uint16_t* orow = out + ((size_t)(q0 + qs + row) * H + h) * D + c0;
-#pragma unroll
-  for (int j = 0; j < 64; j += 8) {
-    uint4 pk;
-    pk.x = pack2bf(acc[j] * inv, acc[j + 1] * inv); pk.y = pack2bf(acc[j + 2] * inv, acc[j + 3] * inv);
-    pk.z = pack2bf(acc[j + 4] * inv, acc[j + 5] * inv); pk.w = pack2bf(acc[j + 6] * inv, acc[j + 7] * inv);
-    *reinterpret_cast<uint4*>(orow + j) = pk;
-  }
-}
-
-// work: NG (seq, q_start, t0, t1, pslot) items per workgroup (seq < 0: that group idles), nwork workgroups;
-// combine: ncomb (seq, q_start, pslot0, nsplit) merges after the main launch (part / part_ml: the split partials)
+// work: NG (seq, q_start, t0, t1) items per workgroup (seq < 0: that group idles), nwork workgroups
 extern "C" int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                   const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv,
-                                  float scale, void* out, int ng, float* part, float* part_ml, const int* combine,
-                                  int ncomb, hipStream_t s) {
+                                  float scale, void* out, int ng, hipStream_t s) {
   if (nwork <= 0) return 0;
   if (H % Hkv) return -1;
-  if (ncomb > 0 && (!part || !part_ml || !combine)) return -3;
   dim3 grid(nwork, H);
   const float sl2 = scale * 1.4426950408889634f;
 #define LSA_P32_LAUNCH(NGV)                                                                                      \
   hipLaunchKernelGGL(attn_prefill32_kernel<NGV>, grid, dim3(256 * NGV), 0, s, reinterpret_cast<const uint16_t*>(q), \
                      reinterpret_cast<const uint16_t*>(kc), reinterpret_cast<const uint16_t*>(vc), block_tables,  \
-                     max_blocks, cu_q, ctx_lens, work, H, Hkv, sl2, reinterpret_cast<uint16_t*>(out), part, part_ml)
+                     max_blocks, cu_q, ctx_lens, work, H, Hkv, sl2, reinterpret_cast<uint16_t*>(out))
   if (ng == 2) LSA_P32_LAUNCH(2);
   else if (ng == 1) LSA_P32_LAUNCH(1);
   else return -2;
 #undef LSA_P32_LAUNCH
-  if (ncomb > 0)
-    hipLaunchKernelGGL(attn_prefill_combine_kernel, dim3(ncomb, H), dim3(256), 0, s, part, part_ml, combine, cu_q, H,
-                       reinterpret_cast<uint16_t*>(out));
   return (int)hipGetLastError();
 }

@@ -220,7 +220,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
           if (m < M) {
             const int n = (nb0 + i) * 16 + 4 * (l >> 4);
             atomicAdd(&ssw[m], (unsigned long long)ss_to_q24(
-                epi_residual4(ep, m, n, res_slab_sum(rs, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y))));
+                epi_residual4(ep, m, n, res_slab_sum(rs, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y) *
+                                        epi_row_scale(ep, m))));
           }
         }
         __syncthreads();

@@ -109,11 +109,18 @@ class _EngineLoop:
     Failure handling: when a step raises, every queued / running request is failed at once
     (``LLMEngine.abort_all``) and the loop keeps serving -- up to ``max_errors`` failures inside
     ``error_window_s``.  A fatal device error, or too many failures, ends the loop; ``EngineService``
-    then rebuilds the engine or answers ``EngineUnavailable``."""
+    then rebuilds the engine or answers ``EngineUnavailable``.
 
-    def __init__(self, engine, run_ahead: int = 16, max_errors: int = 3, error_window_s: float = 60.0):
+    ``every_error_fatal`` (the leader of a lockstep TP replica, parallel/lockstep.py): any step exception
+    ends the loop, because a failure after a mirrored call left the followers inside collectives the leader
+    never joins; ``on_fatal(e)`` then runs before any request is released (the TP leader exits, so the
+    router re-dispatches its in-flight requests and terminates the followers)."""
+
+    def __init__(self, engine, run_ahead: int = 16, max_errors: int = 3, error_window_s: float = 60.0,
+                 every_error_fatal: bool = False, on_fatal: Optional[Callable[[BaseException], None]] = None):
         self.engine = engine
         self.max_errors, self.error_window_s = max_errors, error_window_s
+        self.every_error_fatal, self.on_fatal = every_error_fatal, on_fatal
         self._errors: list = []
         self.restarts = 0
         engine.run_ahead = run_ahead  # serving: bound each decode run so arrivals are admitted promptly
@@ -157,9 +164,12 @@ class _EngineLoop:
                 REGISTRY.inc("lsa_engine_errors_total", 1, "engine step failures", model=self.engine.name)
                 now = time.monotonic()
                 self._errors = [t for t in self._errors if now - t < self.error_window_s] + [now]
-                fatal = _fatal_device_error(e) or len(self._errors) > self.max_errors
+                fatal = (self.every_error_fatal or _fatal_device_error(e)
+                         or len(self._errors) > self.max_errors)
                 if fatal:
                     self._err = e  # alive() turns false before any caller is released
+                    if self.on_fatal is not None:
+                        self.on_fatal(e)
                 try:
                     self.engine.abort_all(repr(e))
                 except BaseException:  # noqa: BLE001
@@ -182,8 +192,10 @@ class EngineService(Backend):
     """Named in-process engines (built lazily through ``factory``) behind the Ollama call shape."""
 
     def __init__(self, factory: Callable[[str], object], defaults: Optional[dict] = None,
-                 timeout_s: float = 300.0, max_rebuilds: int = 2):
+                 timeout_s: float = 300.0, max_rebuilds: int = 2, every_error_fatal: bool = False,
+                 on_fatal: Optional[Callable[[BaseException], None]] = None):
         self._factory = factory
+        self._loop_kw = dict(every_error_fatal=every_error_fatal, on_fatal=on_fatal)
         self._loops: Dict[str, _EngineLoop] = {}
         self._lock = threading.Lock()
         self.defaults = defaults or {}
@@ -210,7 +222,7 @@ class EngineService(Backend):
                 if torch.cuda.is_available():
                     torch.cuda.empty_cache()
             try:
-                self._loops[model] = _EngineLoop(self._factory(model))
+                self._loops[model] = _EngineLoop(self._factory(model), **self._loop_kw)
             except EngineUnavailable:
                 raise
             except Exception as e:  # noqa: BLE001
@@ -223,7 +235,9 @@ class EngineService(Backend):
         eng = lp.engine
         opts = dict(self.defaults)
         opts.update(options or {})
-        params = SamplingParams.from_ollama_options(opts, default_max=int(opts.get("num_predict", 256)))
+        # no num_predict (the reference's option-less calls): generate until EOS / the context window, as
+        # Ollama does; the engine bounds it by num_ctx and its own max_new_cap
+        params = SamplingParams.from_ollama_options(opts)
         ids = eng.encode(eng.render(prompt, system, raw))
         if params.num_ctx is not None:
             ids = eng.fit_context(ids, params.num_ctx, params.num_keep)

@@ -52,7 +52,12 @@ class Settings:
     # share of the free GPU memory each engine's paged KV arena takes when it is built (two co-served
     # models: the first gets 45 %, the second 45 % of what is left)
     kv_memory_fraction: float = dataclasses.field(default_factory=lambda: _env("KV_MEMORY_FRACTION", 0.45, float))
-    max_new_tokens: int = dataclasses.field(default_factory=lambda: _env("MAX_NEW_TOKENS", 256, int))
+    # default num_predict of a request that sets none: -1 = Ollama's default, generate until EOS or the context
+    # window (the reference's option-less ollama.generate calls, FastAPI/app.py:85-90,105-109)
+    max_new_tokens: int = dataclasses.field(default_factory=lambda: _env("MAX_NEW_TOKENS", -1, int))
+    # server safety cap on generated tokens per request (0 = the model context window); far above any
+    # typical NL->SQL or explanation answer, it only bounds a model that never emits EOS
+    max_new_cap: int = dataclasses.field(default_factory=lambda: _env("MAX_NEW_CAP", 0, int))
     # chunked-prefill interleave: prompt tokens prefilled per engine iteration (0 = whole prompts); longer
     # prompts stall the running decode batch one chunk at a time.  The budget also caps prefill throughput
     # (one chunk per decode run): 512 collapsed co-serving at 16 QPS (nl2sql p50 0.56 -> 3.4 s), 2048 does not

@@ -30,6 +30,9 @@ from ..utils.metrics import REGISTRY, TOKEN_BUCKETS
 from .runner import BLOCK, ModelRunner
 
 
+UNLIMITED = 1 << 30  # max_tokens of a request without num_predict: EOS / context window end it
+
+
 @dataclasses.dataclass
 class SamplingParams:
     """Ollama-compatible options (temperature 0 = greedy, as the benchmark configs require)."""
@@ -54,11 +57,13 @@ class SamplingParams:
         return self.temperature > 0 or self.repeat_penalty != 1.0
 
     @staticmethod
-    def from_ollama_options(opts: Optional[dict], default_max: int = 128) -> "SamplingParams":
+    def from_ollama_options(opts: Optional[dict], default_max: int = UNLIMITED) -> "SamplingParams":
+        """Ollama option dict -> params.  ``num_predict`` absent, None or negative = Ollama's default: generate
+        until EOS or the context window (``LLMEngine.add_request`` bounds it by num_ctx / max_new_cap)."""
         opts = opts or {}
         n = opts.get("num_predict", default_max)
-        if n is None or n < 0:
-            n = default_max
+        if n is None or int(n) < 0:
+            n = default_max if default_max is not None and default_max >= 0 else UNLIMITED
         stop = opts.get("stop") or ()
         # ignore_eos: benchmark extension (fixed-length outputs from random-init weights), not an Ollama option
         return SamplingParams(max_tokens=int(n), temperature=float(opts.get("temperature", 0.0)),

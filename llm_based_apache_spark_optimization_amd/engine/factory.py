@@ -17,8 +17,9 @@ def build_engine(model: str, device: Optional[str] = None, checkpoint: Optional[
                  use_graphs: bool = True, sync_every: int = 8, num_kv_blocks: Optional[int] = None,
                  max_prefill_tokens: int = 16384, kv_memory_fraction: float = 0.85,
                  warm_graphs: bool = False, prefill_chunk: Optional[int] = None,
-                 kv_dtype: Optional[str] = None) -> LLMEngine:
-    """kv_dtype: paged KV cache dtype, "bf16" | "fp8" (None: LSA_KV_FP8, default bf16)."""
+                 kv_dtype: Optional[str] = None, max_new_cap: Optional[int] = None) -> LLMEngine:
+    """kv_dtype: paged KV cache dtype, "bf16" | "fp8" (None: LSA_KV_FP8, default bf16).
+    max_new_cap: generated-token cap per request (None: the context window)."""
     if device is None:
         device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
     t0 = time.perf_counter()
@@ -31,7 +32,8 @@ def build_engine(model: str, device: Optional[str] = None, checkpoint: Optional[
         w = init_random(spec, device, seed=seed, kind=dtype, tp_rank=tpr, tp_size=tps)
         tok = tokenizer_for(spec)
     runner = ModelRunner(w, max_slots=max_slots, max_model_len=max_model_len, tp=tp, use_graphs=use_graphs,
-                         num_kv_blocks=num_kv_blocks, kv_memory_fraction=kv_memory_fraction, kv_dtype=kv_dtype)
+                         num_kv_blocks=num_kv_blocks, kv_memory_fraction=kv_memory_fraction, kv_dtype=kv_dtype,
+                         max_new_cap=max_new_cap)
     eng = LLMEngine(runner, tok, sync_every=sync_every, max_prefill_tokens=max_prefill_tokens, name=model,
                     prefill_chunk=prefill_chunk or None)
     if torch.device(device).type == "cuda":

@@ -41,7 +41,7 @@ class TPCommError(RuntimeError):
 class ModelRunner:
     def __init__(self, weights: LlamaWeights, max_slots: int = 32, max_model_len: int = 4096,
                  num_kv_blocks: Optional[int] = None, kv_memory_fraction: float = 0.85,
-                 max_new_cap: Optional[int] = None, tp=None, use_graphs: bool = True, steps_per_graph: int = 1,
+                 max_new_cap: Optional[int] = None, tp=None, use_graphs: bool = True,
                  fuse_rope: Optional[bool] = None, seq_parallel: Optional[bool] = None, sp_min_tokens: Optional[int] = None,
                  kv_dtype: Optional[str] = None):
         self.w = weights
@@ -76,9 +76,6 @@ class ModelRunner:
         self.max_new_cap = max_new_cap or self.max_model_len
         self.on_gpu = self.device.type == "cuda"
         self.use_graphs = use_graphs and self.on_gpu
-        # decode steps per captured graph (runs replay the k-step graph, then single steps for the rest):
-        # fewer graph boundaries per generated token; LSA_STEPS_PER_GRAPH overrides
-        self.steps_per_graph = max(1, int(os.environ.get("LSA_STEPS_PER_GRAPH", steps_per_graph)))
         dev = self.device
 
         # ---------------- KV cache: [L, 2, blocks, Hkv, 64, D] bf16, or e4m3 bytes + [L, 2, blocks, Hkv, 64] f32 scales
@@ -91,6 +88,11 @@ class ModelRunner:
                 num_kv_blocks = max(2, min(want, budget // per_block))
             else:
                 num_kv_blocks = want
+        if tp is not None and tp.size > 1:
+            # every rank's arena must hold every block id the leader's scheduler hands out: ranks that size
+            # their arenas from their own free memory (shared GPUs, a rebuild beside a not-yet-freed engine)
+            # agree on the smallest
+            num_kv_blocks = tp.min_int(num_kv_blocks)
         self.num_kv_blocks = int(num_kv_blocks)
         self.kv = torch.zeros(self.L, 2, self.num_kv_blocks, self.Hkv, BLOCK, self.D,
                               dtype=torch.uint8 if self.kv_fp8 else torch.bfloat16, device=dev)
@@ -180,16 +182,12 @@ class ModelRunner:
         self.ssq = torch.zeros(2 * self.L + 2, S, dtype=torch.int64, device=dev)  # Q24 fixed point (ops.ss_q24)
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)
-        # batch-1 attention + O projection in one launch (ops.attn_o_b1): MHA, bf16 weights, contexts planned
-        # within 512 tokens (the attention is unsplit there)
-        self.attn_o = (ops.ATTN_O and self.on_gpu and tps == 1 and self.H == self.Hkv and self.D == 128
-                       and self.d % 512 == 0 and self.H % 8 == 0 and weights.layers[0].wo.kind == "bf16"
-                       and not self.kv_fp8)
-        self.ao_slabs = torch.zeros(self.H * self.d if self.attn_o else 1, **f32)
         self.graphs: dict = {}
         self._pending_bt: dict = {}  # slot -> block-table row of a prompt still being prefilled in chunks
         if self.tp is not None and self.tp.size > 1 and self.on_gpu:
             self.tp.warmup()  # communicators (RCCL + the one-shot IPC all-reduce) before any launch
+            if not self.tp.capturable():  # gloo without the IPC kernel (test boxes): eager decode steps
+                self.use_graphs = False
 
     # ------------------------------------------------------------------------------------ helpers
     def _kv_scales(self, l: int):
@@ -252,7 +250,7 @@ class ModelRunner:
         while tier < t:
             tier *= 2
         tier = min(tier, self.max_model_len)
-        return tuple(ops.decode_split_plan(B, self.Hkv, tier)) + (tier,)  # the tier also keys the graph
+        return tuple(ops.decode_split_plan(B, self.Hkv, tier))
 
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         if self.fused_norm and B <= self.fused_norm_max_batch:
@@ -348,17 +346,9 @@ class ModelRunner:
             lin = ops.linear
         ops.add_rmsnorm(h, w.layers[0].attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf,
                         ss_out=ssq.view(-1), ss_ld=S, ss_nzero=2 * self.L)
-        # batch 1, contexts planned within 512 tokens: attention + O projection + residual in one launch
-        ao = B == 1 and self.attn_o and len(plan) > 3 and plan[3] <= 512
         for l, lw in enumerate(w.layers):
             lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q, rownorm=(ssq[2 * l], self.eps))
             kc, vc = self.kv[l, 0], self.kv[l, 1]
-            if ao:
-                ops.attn_o_b1(qkv_parts, self.cos, self.sin, pos, kc, vc, bt, self.H, self.scale, lw.wo,
-                              self.ao_slabs, tk, h, xn, ssq[2 * l + 1])
-                lin(xn, lw.w_gate_up, "silu", out=act, rownorm=(ssq[2 * l + 1], self.eps))
-                lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk))
-                continue
             ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale,
                             attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
                             qkv_parts=qkv_parts, cos=self.cos, sin=self.sin, kv_scales=self._kv_scales(l))
@@ -386,10 +376,11 @@ class ModelRunner:
             b *= 2
         return min(b, self.max_slots) if n <= self.max_slots else self.max_slots
 
-    def capture(self, B: int, sample: bool, plan: Optional[tuple] = None, k: int = 1) -> None:
-        """Capture the k-step decode graph of (bucket, sampling mode, plan)."""
+    def capture(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
+        """Capture the decode-step graph of (bucket, sampling mode, split plan).  (Several steps per graph were
+        measured no faster -- no idle time at graph boundaries, profiles/decode_b32_normfree_spg_ab_mi355x.txt.)"""
         plan = tuple(plan or self.ctx_plan(B))
-        key = (B, sample, plan) if k == 1 else (B, sample, plan, k)
+        key = (B, sample, plan)
         if key in self.graphs:
             return
         if self.tp is not None and self.tp.size > 1:
@@ -400,8 +391,7 @@ class ModelRunner:
         with torch.cuda.stream(s):
             # state must not change during capture: kernels are recorded, not executed
             with torch.cuda.graph(g, stream=s):
-                for _ in range(k):
-                    self._decode_step(B, sample, plan)
+                self._decode_step(B, sample, plan)
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graphs[key] = g
 
@@ -432,8 +422,6 @@ class ModelRunner:
             for sm in sample_modes:
                 for p in self.plans(b):
                     self.capture(b, sm, p)
-                    if self.steps_per_graph > 1:
-                        self.capture(b, sm, p, self.steps_per_graph)
         torch.cuda.synchronize(self.device)
 
     def decode(self, B: int, steps: int, sample: bool = False, max_ctx: Optional[int] = None) -> None:
@@ -444,18 +432,10 @@ class ModelRunner:
             for _ in range(steps):
                 self._decode_step(B, sample, plan)
             return
-        k = self.steps_per_graph
-        full, rest = divmod(steps, k) if k > 1 else (0, steps)
-        if full:
-            self.capture(B, sample, plan, k)
-            g = self.graphs[(B, sample, plan, k)]
-            for _ in range(full):
-                g.replay()
-        if rest:
-            self.capture(B, sample, plan)
-            g = self.graphs[(B, sample, plan)]
-            for _ in range(rest):
-                g.replay()
+        self.capture(B, sample, plan)
+        g = self.graphs[(B, sample, plan)]
+        for _ in range(steps):
+            g.replay()
 
     # ------------------------------------------------------------------------------------ slots
     def set_slot(self, slot: int, blocks: Sequence[int], limit: int, temperature: float = 0.0, top_k: int = 40,

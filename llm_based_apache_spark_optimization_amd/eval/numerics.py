@@ -1,0 +1,125 @@
+"""Teacher-forced numerics check of the engine's DECODE path against the plain fp32 PyTorch forward.
+
+The engine decodes a batch greedily with its captured graphs; the logits of every step (the decode kernels'
+own lm_head output, rows of the batch bucket the benchmark times) are recorded.  The oracle
+(``models.llama.reference_forward``) is then fed each sequence's prompt plus the engine's own tokens
+(teacher forcing), so position j of both predicts the same token j.  Per position:
+
+* KL(oracle || engine) of the two next-token distributions (nats),
+* top-1 agreement (argmax of the engine's logits vs the oracle's),
+* top-5 overlap (|top5(engine) n top5(oracle)| / 5).
+
+Statistics are taken over >= 64 positions per checked sequence.  fp8 models are compared with an oracle that
+emulates the engine's quantisation (its dequantised weights, the same per-token e4m3 activation rounding for
+W8A8 GEMMs, the e4m3 KV rows of an fp8 cache), so the thresholds measure kernels and layouts, not the
+quantiser -- and a wrong scale or a scrambled cache layout moves the distributions far past them
+(tests/test_numerics_gpu.py injects both and requires the check to fail).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+# (mean KL nats, top-5 overlap, top-1 agreement) a healthy engine stays within, per numerics class.
+# Calibrated on MI355X at the benchmark shapes (profiles/numerics_calibration_mi355x.jsonl): the healthy
+# engine sits an order of magnitude inside each bound, the injected faults (one layer's weight scale x1.25,
+# two swapped cached tokens) several times outside.
+THRESHOLDS = {
+    "bf16": (2e-3, 0.9, 0.9),
+    "w8a16": (2e-2, 0.8, 0.6),
+    "w8a8": (5e-2, 0.7, 0.5),
+}
+
+
+def record_decode_logits(eng, prompts: Sequence[Sequence[int]], n_steps: int):
+    """Greedy-decode ``prompts`` as ONE batch (bucket of len(prompts)), one decode step per engine iteration,
+    recording the decode step's logits.  Returns (tokens [P][n_steps + 1], logits [P, n_steps, V] f32) where
+    logits[i, j - 1] are the engine's logits that chose token j (j = 1 .. n_steps; token 0 comes from prefill)."""
+    from ..engine import SamplingParams
+
+    r = eng.runner
+    old = eng.run_ahead
+    eng.run_ahead = 1
+    try:
+        params = SamplingParams(max_tokens=n_steps + 1, temperature=0.0, ignore_eos=True)
+        reqs = [eng.add_request(list(p), params) for p in prompts]
+        out = torch.zeros(len(prompts), n_steps, r.V, dtype=torch.float32, device=r.device)
+        while not all(q.done.is_set() for q in reqs):
+            eng.step()
+            for i, q in enumerate(reqs):
+                j = (len(q.output_ids) if q.done.is_set() else q.gen_host) - 1  # token the last step chose
+                if 1 <= j <= n_steps and q.slot >= 0:
+                    out[i, j - 1].copy_(r.logits[q.slot].float())
+        return [q.output_ids for q in reqs], out
+    finally:
+        eng.run_ahead = old
+
+
+def compare(engine_logits: torch.Tensor, oracle_logits: torch.Tensor) -> dict:
+    """Per-position KL(oracle || engine), top-1 agreement and top-5 overlap over [n, V] logits."""
+    e = engine_logits.float()
+    o = oracle_logits.float().to(e.device)
+    lo, le = torch.log_softmax(o, -1), torch.log_softmax(e, -1)
+    kl = (lo.exp() * (lo - le)).sum(-1)
+    top1 = (e.argmax(-1) == o.argmax(-1)).float()
+    t5e, t5o = e.topk(5, -1).indices, o.topk(5, -1).indices
+    top5 = (t5e.unsqueeze(-1) == t5o.unsqueeze(-2)).any(-1).float().mean(-1)
+    return {"kl": kl, "top1": top1, "top5": top5}
+
+
+def numerics_class(runner, decode_batch: int) -> str:
+    """Which threshold row applies to the decode path at ``decode_batch`` (see engine/runner.py)."""
+    if runner.w.layers[0].wqkv.kind != "fp8":
+        return "bf16"
+    xf = runner.a8 and runner.use_xfrag(decode_batch) and not (
+        runner.fused_norm and decode_batch <= runner.fused_norm_max_batch)
+    a8 = xf and (decode_batch > runner.a8_min_batch or decode_batch > runner.a8_mlp_min_batch)
+    return "w8a8" if a8 or runner.kv_fp8 else "w8a16"
+
+
+def teacher_forced_check(eng, prompts: Sequence[Sequence[int]], n_steps: int = 64, check_rows: Sequence[int] = (0,),
+                         weights=None, prefill_rows: Optional[int] = None) -> dict:
+    """Decode ``prompts`` as one batch for ``n_steps`` steps, compare rows ``check_rows`` against the oracle."""
+    toks, elog = record_decode_logits(eng, prompts, n_steps)
+    return check_recorded(eng, prompts, toks, elog, n_steps, check_rows, weights, prefill_rows)
+
+
+def check_recorded(eng, prompts, toks, elog, n_steps: int, check_rows: Sequence[int] = (0,), weights=None,
+                   prefill_rows: Optional[int] = None) -> dict:
+    """Compare recorded decode logits (``record_decode_logits``) of rows ``check_rows`` with the oracle.
+
+    ``weights``: the unsharded weights for the oracle (TP engines hold one shard; default the engine's own).
+    ``prefill_rows``: rows of the packed prefill (fp8: > 64 -> W8A8 prefill, emulated by the oracle)."""
+    from .. import ops
+    from ..models.llama import reference_forward
+
+    r = eng.runner
+    B = r.bucket(len(prompts))
+    w = weights if weights is not None else r.w
+    fp8 = w.layers[0].wqkv.kind == "fp8"
+    rows = prefill_rows if prefill_rows is not None else sum(len(p) for p in prompts)
+    unfused_xf = bool(r.a8 and r.use_xfrag(B) and not (r.fused_norm and B <= r.fused_norm_max_batch))
+    da8 = unfused_xf and B > r.a8_min_batch
+    da8m = unfused_xf and B > r.a8_mlp_min_batch
+    kls, t1s, t5s = [], [], []
+    for i in sorted(set(check_rows)):
+        p = list(prompts[i])
+        aq = len(p) if (fp8 and rows > 64 and ops.FP8_W8A8) else 0
+        lg = reference_forward(w, p + list(toks[i][:n_steps]), act_quant_rows=aq, decode_a8=da8, decode_a8_mlp=da8m,
+                               kv_fp8=r.kv_fp8)
+        c = compare(elog[i], lg[len(p):len(p) + n_steps])
+        kls.append(c["kl"])
+        t1s.append(c["top1"])
+        t5s.append(c["top5"])
+        del lg
+    kl, t1, t5 = torch.cat(kls), torch.cat(t1s), torch.cat(t5s)
+    cls = numerics_class(r, B)
+    kl_max, t5_min, t1_min = THRESHOLDS[cls]
+    res = {"tokens_checked": int(kl.numel()), "decode_batch": len(prompts), "class": cls,
+           "mean_kl": round(float(kl.mean()), 6), "max_kl": round(float(kl.max()), 6),
+           "top1_agree": round(float(t1.mean()), 4), "top5_overlap": round(float(t5.mean()), 4)}
+    res["ok"] = bool(res["mean_kl"] < kl_max and res["top5_overlap"] >= t5_min and res["top1_agree"] >= t1_min)
+    res["criterion"] = (f"{cls}: teacher-forced over {n_steps} decode steps: mean KL(oracle||engine) < {kl_max}, "
+                        f"top-5 overlap >= {t5_min}, top-1 agreement >= {t1_min}")
+    return res

@@ -709,32 +709,6 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     return out
 
 
-# batch-1 attention + O projection + residual in one launch (csrc/kernels/attention_o.hip), opt-in (LSA_ATTN_O=1):
-# correct (tests/test_kernels_gpu.py::test_attn_o_b1) but measured no faster -- 7B b1 step 2.66 vs 2.62 ms
-# (rocprofv3: 16.3 us in the captured step vs 5.9 + ~9.5 us for the two launches).  The probe
-# (scripts/attn_stamps.py --ao) shows why: the 33.5 MB weight stream contends with the K / V loads of the
-# attention it is meant to hide under (score loop 2.8 -> 5.0 us), and the cross-head reduction adds a serial
-# publish -> ticket -> sum tail of ~4 us that the GEMM launch it replaces did not have at batch 1
-ATTN_O = os.environ.get("LSA_ATTN_O", "0") == "1"
-
-
-def attn_o_b1(qkv_parts, cos, sin, pos, kc, vc, block_table, H, scale, wo: PackedWeight, slabs, tickets,
-              h, xout, ss_out) -> None:
-    """Batch-1 MHA decode: attention of the new token (RoPE + KV append fused, from the QKV split-K slabs)
-    followed by the O projection and the norm-free residual epilogue, in one launch:
-    h += o @ Wo^T; xout = bf16(h); ss_out[0] += sum h^2 (Q24).  slabs: >= H * d f32 scratch; tickets: zeroed
-    int32 counters (>= d / 512; left zeroed)."""
-    if not _gpu(pos):
-        B = pos.shape[0]
-        q = torch.empty(B, H, 128, dtype=torch.bfloat16, device=pos.device)
-        a = torch.empty_like(q)
-        attn_decode(q, kc, vc, block_table, pos, H, H, scale, a, qkv_parts=qkv_parts, cos=cos, sin=sin)
-        linear(a.view(B, -1), wo, "res", res=(h, xout, ss_out))
-        return
-    ext().attn_o_b1(qkv_parts, cos, sin, pos, kc, vc, block_table, H, scale, wo.data, wo.N, slabs, tickets,
-                    h, xout, ss_out)
-
-
 # prefill attention kernel: "32" = 32 x 32 MFMA tiles, 128 query rows per workgroup (attention_prefill32.hip);
 # "16" = the 16 x 16 kernel of attention.hip (64 rows per workgroup); "auto" = 32 when the longest packed
 # sequence has >= 512 rows (measured, scripts/bench_attn_prefill.py: 7B 2k 146 -> 119 us, 3B 2k 118 -> 115 us,
@@ -760,29 +734,11 @@ def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[li
     context length after this prefill, default = the chunk length, i.e. no cached prefix).
 
     16-row kernel: (seq, q_start) per workgroup, heaviest (latest) query blocks first.
-    32-row kernel ('32'): NG items (seq, q_start, t0, t1, pslot) per workgroup -- the key tiles [t0, t1) of a
-    128-row query block; see ``prefill_plan`` for the KV splits (pslot >= 0) and the heavy/light pairing."""
-    return prefill_plan_items(cu_q, qblock, ctx, kernel, heads)[0]
-
-
-# LSA_PREFILL_SPLIT: key tiles per work item of the 32-row prefill kernel before a heavy query block's causal
-# range is cut into KV splits (merged by attn_prefill_combine_kernel): "auto" (the plan's even share of the chip,
-# >= 8 tiles), a number, or 0 (never split, the default).  Measured on MI355X (profiles/attn_prefill_kv_split_
-# mi355x.jsonl, scripts/gpu_psplit.sh): every budget is slower than no split -- 3B 2k 75.1 us unsplit vs 84.5
-# (auto) .. 113 (4 tiles), 7B 2k 81.0 vs 98.1 .. 134, 3B 8k 577 vs 577 .. 1530 -- the partial-O stores, the merge
-# launch and the extra K/V passes of the pieces cost more than the heavy/light pairing leaves on the critical path
-PREFILL_SPLIT = os.environ.get("LSA_PREFILL_SPLIT", "0")
-
-
-def _split_tiles(total_tiles: int) -> int:
-    if PREFILL_SPLIT == "auto":
-        return max(8, -(-total_tiles // 512))
-    return int(PREFILL_SPLIT) or (1 << 30)
-
-
-def prefill_plan_items(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[list[int]] = None,
-                       kernel: Optional[str] = None, heads: int = 32):
-    """(work rows, combine rows, n_pslots) of ``prefill_plan``, as Python lists."""
+    32-row kernel ('32'): NG items (seq, q_start, t0, t1) per workgroup -- the key tiles [t0, t1) = the whole
+    causal range of a 128-row query block; NG = 2 pairs a heavy block with a light one (``_pair_blocks``).
+    (Cutting heavy blocks into KV splits merged by a second launch, or into two halves merged in LDS, were
+    both built and measured slower -- profiles/attn_prefill_kv_split_mi355x.jsonl,
+    profiles/attn_prefill_halves_mi355x.jsonl -- and removed.)"""
     kernel = kernel or _prefill_kernel(cu_q)
     if qblock is None:
         qblock = 128 if kernel == "32" else ext().prefill_qblock
@@ -794,86 +750,38 @@ def prefill_plan_items(cu_q: list[int], qblock: Optional[int] = None, ctx: Optio
             items.append(((pos0 + min(qs + qblock, ql) + 63) // 64, s, qs))
     items.sort(key=lambda t: -t[0])
     if kernel != "32":
-        return [(s, qs) for _, s, qs in items], [], 0
-    # KV splits: a block whose causal range exceeds the tile budget is cut into nearly equal pieces of key tiles
-    # (partial O + (m, l) per piece into its own slot, merged afterwards) so the heaviest block no longer sets the
-    # critical path: the 2k prompts ran 192 paired workgroups on 256 CUs with the last block's 32 tiles in series
-    budget = _split_tiles(sum(t for t, _, _ in items) * heads)
-    units, combine, np_ = [], [], 0
-    for nt, s, qs in items:
-        if nt <= budget:
-            units.append((nt, s, qs, 0, nt, -1))
-            continue
-        k = -(-nt // budget)
-        size = -(-nt // k)
-        for j in range(k):
-            t0, t1 = j * size, min(nt, (j + 1) * size)
-            units.append((t1 - t0, s, qs, t0, t1, np_ + j))
-        combine.append((s, qs, np_, k))
-        np_ += k
-    units.sort(key=lambda u: -u[0])
+        return [(s, qs) for _, s, qs in items]
+    units = [(s, qs, 0, nt) for nt, s, qs in items]
     n = len(units)
-    if not combine and _halve_blocks(n, heads):
-        # both 4-wave groups of a workgroup on ONE query block, its key tiles split in two (pslot -2: the kernel
-        # merges group 1's partial into group 0 through LDS), heaviest blocks first
-        out = []
-        for nt, s, qs, _, _, _ in units:
-            if nt >= 2:
-                mid = (nt + 1) // 2
-                out.append((s, qs, 0, mid, -2, s, qs, mid, nt, -2))
-            else:
-                out.append((s, qs, 0, nt, -1, -1, 0, 0, 0, -1))
-        return out, combine, np_
     longest = max(cu_q[i + 1] - cu_q[i] for i in range(len(cu_q) - 1))
     if not _pair_blocks(n, heads, longest, qblock):
-        return [u[1:] for u in units], combine, np_
+        return units
     out = []
     for i in range((n + 1) // 2):
         j = n - 1 - i
-        b = units[j][1:] if j > i else (-1, 0, 0, 0, -1)
-        out.append(units[i][1:] + b)
-    return out, combine, np_
+        b = units[j] if j > i else (-1, 0, 0, 0)
+        out.append(units[i] + b)
+    return out
 
 
 class PrefillPlan(NamedTuple):
     """Device-side plan of one prefill attention call (``prefill_plan``)."""
     kernel: str
-    work: torch.Tensor               # int32 [n_workgroups, 2 | 5 * NG]
-    combine: Optional[torch.Tensor]  # int32 [n, 4] (seq, q_start, pslot0, nsplit) merges, or None
-    n_pslots: int
+    work: torch.Tensor  # int32 [n_workgroups, 2 | 4 * NG]
 
 
 def prefill_plan(cu_q: list[int], ctx: Optional[list[int]] = None, heads: int = 32, device=None,
                  kernel: Optional[str] = None) -> PrefillPlan:
-    """Work items (+ KV-split merges) of the prefill attention kernel for packed sequences, on ``device``."""
+    """Work items of the prefill attention kernel for packed sequences, on ``device``."""
     kernel = kernel or _prefill_kernel(cu_q)
-    work, combine, np_ = prefill_plan_items(cu_q, ctx=ctx, kernel=kernel, heads=heads)
-    w = torch.tensor(work, dtype=torch.int32)
-    c = torch.tensor(combine, dtype=torch.int32) if combine else None
+    w = torch.tensor(prefill_work(cu_q, ctx=ctx, kernel=kernel, heads=heads), dtype=torch.int32)
     if device is not None:
         w = w.to(device, non_blocking=True)
-        c = c.to(device, non_blocking=True) if c is not None else None
-    return PrefillPlan(kernel, w, c, np_)
+    return PrefillPlan(kernel, w)
 
 
 # LSA_PREFILL_PAIR: auto | 1 | 0 -- heavy/light paired query blocks in the 32-row prefill kernel
 PREFILL_PAIR = os.environ.get("LSA_PREFILL_PAIR", "auto")
-
-
-# LSA_PREFILL_HALVES: auto | 1 | 0 (default) -- one query block per workgroup, its key tiles split over the two
-# 4-wave groups and merged in LDS (attention_prefill32.hip, pslot -2).  Correct (tests/test_kernels_gpu.py
-# test_attn_prefill_halves) but measured slower (profiles/attn_prefill_halves_mi355x.jsonl: 3B 2k 73.3 -> 98.6 us,
-# 7B 2k 80.2 -> 102.3 us): two waves per SIMD on one block take ~2x the per-tile time of one (the CU is
-# throughput-bound in the tile loop, not latency-bound), and 2x the workgroups at one per CU need 1.5 rounds
-PREFILL_HALVES = os.environ.get("LSA_PREFILL_HALVES", "0")
-
-
-def _halve_blocks(n_items: int, heads: int) -> bool:
-    """Halve every block over two wave groups when all blocks are resident at once (one workgroup per CU at
-    128 KiB of LDS): the critical path is then the heaviest block, which the halves shorten."""
-    if PREFILL_HALVES != "auto":
-        return PREFILL_HALVES == "1"
-    return n_items * heads <= 512
 
 
 def _pair_blocks(n_items: int, heads: int, longest: int, qblock: int) -> bool:
@@ -903,13 +811,9 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, wo
     plan = work if isinstance(work, PrefillPlan) else None
     if plan is None:
         plan = (prefill_plan(cu, ctx=ctx_lens.tolist(), heads=H, device=q.device) if work is None
-                else PrefillPlan(_prefill_kernel(cu), work, None, 0))
-    part = part_ml = None
-    if plan.combine is not None:  # KV-split heavy blocks: partial slots for the merge
-        part = torch.empty(plan.n_pslots * H * 128 * 128, dtype=torch.float32, device=q.device)
-        part_ml = torch.empty(plan.n_pslots * H * 128 * 2, dtype=torch.float32, device=q.device)
+                else PrefillPlan(_prefill_kernel(cu), work))
     ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out,
-                       1 if plan.kernel == "32" else 0, part, part_ml, plan.combine, plan.n_pslots)
+                       1 if plan.kernel == "32" else 0)
     return out
 
 

@@ -15,6 +15,7 @@ single-GPU tests over gloo.
 """
 from __future__ import annotations
 
+import logging
 import os
 from typing import Optional
 
@@ -23,8 +24,86 @@ import torch.distributed as dist
 
 from .. import ops
 
+log = logging.getLogger(__name__)
+
 DEFAULT_MAX_BYTES = 8 << 20  # B=64 x d=4096 f32 all-reduces; B=32 x 64128 vocab-parallel logit gathers (3B, TP2)
 DEFAULT_TIMEOUT_S = 60.0
+
+
+class IpcUnavailable(RuntimeError):
+    """The IPC regions could not be allocated, exported or mapped on some rank of the group; every rank
+    then keeps RCCL for all of its collectives (the decision is collective, so the ranks never disagree
+    on which path a call takes)."""
+
+
+def _peer_reachable(mine: Optional[int], peer: Optional[int]) -> bool:
+    """hipDeviceCanAccessPeer between two GPUs this process can see (TP ranks of a router replica see the
+    replica's whole GPU list); ranks sharing one GPU, or a peer outside this process's view, pass here and
+    are settled by the mapping itself."""
+    if mine is None or peer is None or mine == peer:
+        return True
+    try:
+        n = torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        return True
+    if not (0 <= mine < n and 0 <= peer < n):
+        return True
+    return bool(torch.cuda.can_device_access_peer(mine, peer))
+
+
+def open_regions(group, rank: int, world: int, ext, nbytes: int,
+                 device_index: Optional[int] = None) -> tuple[int, list, list]:
+    """Allocate this rank's region, exchange IPC handles and map every peer's region.
+
+    Collective over ``group`` and all-or-nothing: a failure on ANY rank (allocation, handle export, peer
+    mapping -- e.g. ``hipIpcOpenMemHandle`` refused because the peer GPU is not reachable) makes every rank
+    release what it mapped and raise ``IpcUnavailable``.  Returns (own base, [region ptr per rank], [opened
+    peer ptrs])."""
+    base, handle, why = 0, None, ""
+    try:
+        base = ext.ar_alloc(nbytes)
+        handle = ext.ar_handle(base)
+    except Exception as e:  # noqa: BLE001 - reported collectively below
+        why = f"rank {rank}: region export failed: {e}"
+    recs: list = [None] * world
+    dist.all_gather_object(recs, (handle, device_index), group=group)
+    handles = [h for h, _ in recs]
+    opened, ptrs = [], []
+    if not why:
+        unreachable = [r for r, (_, di) in enumerate(recs) if r != rank and not _peer_reachable(device_index, di)]
+        if unreachable:
+            why = f"rank {rank}: no peer access to the GPUs of ranks {unreachable}"
+    if not why and all(h is not None for h in handles):
+        try:
+            for r, h in enumerate(handles):
+                if r == rank:
+                    ptrs.append(base)
+                    continue
+                if os.environ.get("LSA_TEST_FAIL_AR_OPEN") == str(rank):  # fault injection (tests)
+                    raise RuntimeError("injected ar_open failure")
+                p = ext.ar_open(h)
+                opened.append(p)
+                ptrs.append(p)
+        except Exception as e:  # noqa: BLE001
+            why = f"rank {rank}: peer mapping failed: {e}"
+    elif not why:
+        why = "a peer could not export its region"
+    verdicts: list = [None] * world
+    dist.all_gather_object(verdicts, why, group=group)
+    bad = [v for v in verdicts if v]
+    if bad:
+        for p in opened:
+            try:
+                ext.ar_close(p)
+            except Exception:  # noqa: BLE001
+                pass
+        if base:
+            try:
+                ext.ar_free(base)
+            except Exception:  # noqa: BLE001
+                pass
+        raise IpcUnavailable("; ".join(bad))
+    return base, ptrs, opened
 
 
 class IpcAllReduce:
@@ -39,19 +118,9 @@ class IpcAllReduce:
         self.max_bytes = int(max_bytes)
         self.nblocks = int(nblocks)
         with torch.cuda.device(device):
-            self._base = ext.ar_alloc(ext.ar_header_bytes + 2 * world * self.max_bytes)
-            handle = ext.ar_handle(self._base)
-            handles: list = [None] * world
-            dist.all_gather_object(handles, handle, group=group)
-            self._opened = []
-            ptrs = []
-            for r, h in enumerate(handles):
-                if r == rank:
-                    ptrs.append(self._base)
-                else:
-                    p = ext.ar_open(h)
-                    self._opened.append(p)
-                    ptrs.append(p)
+            self._base, ptrs, self._opened = open_regions(group, rank, world, ext,
+                                                          ext.ar_header_bytes + 2 * world * self.max_bytes,
+                                                          device_index=device.index)
             self.regions = torch.tensor(ptrs, dtype=torch.int64, device=device)
             self.err = torch.zeros(1, dtype=torch.int32, device=device)
             self.timeout_ticks = int(timeout_s * ext.ar_wallclock_khz() * 1000)
@@ -102,11 +171,18 @@ class IpcAllReduce:
 
 
 def maybe_ipc_allreduce(group, rank: int, world: int, device: torch.device) -> Optional[IpcAllReduce]:
-    """The one-shot all-reduce for a GPU TP group, unless disabled (``LSA_CUSTOM_AR=0``) or unavailable."""
+    """The one-shot all-reduce for a GPU TP group, unless disabled (``LSA_CUSTOM_AR=0``) or unavailable.
+
+    Unavailable includes a failure on any rank to map its peers' regions (``IpcUnavailable``): the group
+    then degrades to RCCL for every collective instead of the replica dying in ``TPGroup.warmup``."""
     if device.type != "cuda" or world < 2 or os.environ.get("LSA_CUSTOM_AR", "1") == "0":
         return None
     if world > ops.ext().ar_max_world:
         return None
-    return IpcAllReduce(group, rank, world, device,
-                        max_bytes=int(os.environ.get("LSA_CUSTOM_AR_MAX_BYTES", DEFAULT_MAX_BYTES)),
-                        timeout_s=float(os.environ.get("LSA_CUSTOM_AR_TIMEOUT_S", DEFAULT_TIMEOUT_S)))
+    try:
+        return IpcAllReduce(group, rank, world, device,
+                            max_bytes=int(os.environ.get("LSA_CUSTOM_AR_MAX_BYTES", DEFAULT_MAX_BYTES)),
+                            timeout_s=float(os.environ.get("LSA_CUSTOM_AR_TIMEOUT_S", DEFAULT_TIMEOUT_S)))
+    except IpcUnavailable as e:
+        log.warning("one-shot IPC all-reduce unavailable, TP group falls back to RCCL: %s", e)
+        return None

@@ -19,7 +19,9 @@ communicator and IPC all-reduce region) and its own HIP stream on every rank.
 from __future__ import annotations
 
 import contextlib
+import gc
 import logging
+import os
 import threading
 from typing import Callable, Optional
 
@@ -91,8 +93,12 @@ def lockstep_factory(build: Callable[[str], object], chan: Optional[LeaderChanne
     return make
 
 
-def follow(conn, build: Callable[[str], object]) -> None:
-    """Follower loop: build engines and replay the leader's runner calls until told to stop."""
+def follow(conn, build: Callable[[str], object], exit_on_error: bool = True) -> None:
+    """Follower loop: build engines and replay the leader's runner calls until told to stop.
+
+    A replayed call that raises leaves this rank out of step with the leader (which ran or will run the
+    same call's collectives): the follower exits non-zero (``exit_on_error``), the router sees the TP group
+    lose a rank and terminates the whole replica instead of pairing later collectives wrongly."""
     engines: dict = {}
     streams: dict = {}
     while True:
@@ -105,7 +111,17 @@ def follow(conn, build: Callable[[str], object]) -> None:
             return
         if kind == "build":
             model = msg[1]
-            eng = build(model)
+            if model in engines:  # rebuild: free the old engine's weights / KV arena before the new one sizes its arena
+                engines.pop(model)
+                streams.pop(model, None)
+                gc.collect()
+                if torch.cuda.is_available():
+                    torch.cuda.empty_cache()
+            try:
+                eng = build(model)
+            except BaseException as e:  # noqa: BLE001
+                _die(e, f"build {model}", exit_on_error)
+                raise
             engines[model] = eng
             dev = getattr(eng.runner, "device", None)
             if dev is not None and torch.device(dev).type == "cuda":
@@ -117,7 +133,17 @@ def follow(conn, build: Callable[[str], object]) -> None:
             _, model, name, args, kwargs = msg
             s = streams.get(model)
             ctx = torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
-            with ctx:
-                getattr(engines[model].runner, name)(*args, **kwargs)
+            try:
+                with ctx:
+                    getattr(engines[model].runner, name)(*args, **kwargs)
+            except BaseException as e:  # noqa: BLE001
+                _die(e, name, exit_on_error)
+                raise
             continue
         log.warning("follower: unknown message %r", kind)
+
+
+def _die(e: BaseException, what: str, exit_on_error: bool) -> None:
+    log.error("TP follower: %s failed (%r); leaving the replica", what, e)
+    if exit_on_error:
+        os._exit(71)

@@ -55,20 +55,29 @@ def _visible_gpus() -> int:
         return 0
 
 
+def _tp_local_device(tp_rank: int, shared_device: bool) -> int:
+    """Index of this TP rank's GPU in its own view: every rank of a replica sees the replica's whole GPU
+    list (as torchrun ranks do) and owns entry ``tp_rank``, so peers are visible devices and
+    ``hipDeviceCanAccessPeer`` can be checked before the IPC all-reduce maps them; ranks sharing one GPU
+    (test boxes) see only that GPU."""
+    return 0 if shared_device else tp_rank
+
+
 def _init_tp_rank(tp_rank: int, tp_size: int, port: int, shared_device: bool) -> None:
     """torch.distributed world = this replica's TP ranks (one process per GPU; RCCL when every rank
     owns its own GPU, gloo when ranks share one device (test boxes) or there is no GPU)."""
     import torch
     import torch.distributed as dist
 
+    local = _tp_local_device(tp_rank, shared_device)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(tp_rank),
-                      WORLD_SIZE=str(tp_size), LOCAL_RANK="0")
+                      WORLD_SIZE=str(tp_size), LOCAL_RANK=str(local))
     if torch.cuda.is_available() and not shared_device:
-        torch.cuda.set_device(0)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         if torch.cuda.is_available():
-            torch.cuda.set_device(0)
+            torch.cuda.set_device(local)
         dist.init_process_group("gloo")
 
 
@@ -83,7 +92,7 @@ def _tp_engine_factory(settings, tp_rank: int, tp_size: int):
 
     def tp_for_model():
         g = dist.new_group(list(range(tp_size)))
-        dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
         return TPGroup(g, tp_rank, tp_size, dev)
 
     return engine_factory(settings, tp_factory=tp_for_model)
@@ -95,7 +104,8 @@ def _worker(conn, replica: int, devices: str, kind: str, settings_kw: dict, hear
 
     TP replicas (tp_size > 1): rank 0 is the leader (``conn`` = router pipe, ``peers`` = pipes to its
     followers); ranks > 0 are followers (``conn`` = pipe from the leader) that mirror its runner calls
-    (parallel/lockstep.py)."""
+    (parallel/lockstep.py).  ``devices``: this process's HIP_VISIBLE_DEVICES -- a TP rank gets its
+    replica's whole GPU list and selects entry ``tp_rank`` (``_tp_local_device``)."""
     if devices:
         os.environ["HIP_VISIBLE_DEVICES"] = devices  # before any HIP call in this process
     from ..config import Settings
@@ -113,8 +123,17 @@ def _worker(conn, replica: int, devices: str, kind: str, settings_kw: dict, hear
             return
         chan = lockstep.LeaderChannel(peers or [])
         defaults = {"temperature": s.temperature, "top_k": s.top_k, "top_p": s.top_p, "num_predict": s.max_new_tokens}
+
+        def die(e: BaseException) -> None:
+            # any failed step leaves the lockstep group out of step (followers may sit in collectives the
+            # leader never joins): never step it again -- exit, so the router re-dispatches the in-flight
+            # requests to live replicas and terminates this replica's followers
+            log.error("TP replica %d leader: engine step failed (%r); exiting", replica, e)
+            os._exit(70)
+
         backend = EngineService(lockstep.lockstep_factory(build, chan), defaults=defaults,
-                                timeout_s=s.request_timeout_s)
+                                timeout_s=s.request_timeout_s, max_rebuilds=0, every_error_fatal=True,
+                                on_fatal=die)
     elif kind == "fake":
         backend = FakeBackend()
     else:
@@ -221,14 +240,15 @@ class ReplicaRouter(Backend):
             port = _free_port()
             shared = len(set(dev)) < len(dev)  # ranks sharing one GPU (test boxes): gloo, not RCCL
             lead_ends, followers = [], []
+            vis = (lambda j: dev[j]) if shared else (lambda j: ",".join(dev))
             for j in range(1, self.tp):
                 lc, fc = ctx.Pipe()
                 lead_ends.append(lc)
-                fp = ctx.Process(target=_worker, args=(fc, i, dev[j], kind, settings_kw or {}, heartbeat_s, j,
+                fp = ctx.Process(target=_worker, args=(fc, i, vis(j), kind, settings_kw or {}, heartbeat_s, j,
                                                        self.tp, port, None, shared), daemon=True)
                 fp.start()
                 followers.append(fp)
-            p = ctx.Process(target=_worker, args=(b, i, dev[0], kind, settings_kw or {}, heartbeat_s, 0, self.tp,
+            p = ctx.Process(target=_worker, args=(b, i, vis(0), kind, settings_kw or {}, heartbeat_s, 0, self.tp,
                                                   port, lead_ends, shared), daemon=True)
             p.start()
             self.replicas.append(_Replica(i, p, a, followers))

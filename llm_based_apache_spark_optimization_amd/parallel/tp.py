@@ -60,6 +60,18 @@ class TPGroup:
             return
         dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group)
 
+    def capturable(self) -> bool:
+        """Whether the decode step's collectives can be captured in a hipGraph: the one-shot IPC kernel or
+        RCCL can; gloo (ranks sharing one GPU on test boxes, after an IPC fallback) cannot."""
+        return self.car is not None or dist.get_backend(self.group) == "nccl"
+
+    def min_int(self, x: int) -> int:
+        """Minimum of ``x`` over the group (host value; collective)."""
+        on_dev = dist.get_backend(self.group) == "nccl"
+        t = torch.tensor([int(x)], dtype=torch.int64, device=self.device if on_dev else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return int(t.item())
+
     def warmup(self) -> None:
         """Initialise the communicators outside graph capture (collective over the group)."""
         if not self._warm:

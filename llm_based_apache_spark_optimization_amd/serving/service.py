@@ -28,7 +28,8 @@ def engine_factory(settings: Settings, tp_factory=None):
         return build_engine(model, checkpoint=settings.checkpoint_dir if model == settings.nl2sql_model else None,
                             dtype=dtype, max_slots=settings.max_batch, max_model_len=settings.max_model_len,
                             kv_memory_fraction=settings.kv_memory_fraction, warm_graphs=True, tp=tp,
-                            prefill_chunk=settings.prefill_chunk, kv_dtype=settings.kv_dtype)
+                            prefill_chunk=settings.prefill_chunk, kv_dtype=settings.kv_dtype,
+                            max_new_cap=settings.max_new_cap or None)
 
     return build
 

@@ -58,39 +58,3 @@ for name, (B, H, Hkv, ctx, nparts) in cases.items():
             d = (b[ok] - a[ok]) / 100.0
             res[ph] = [round(float(d.median()), 2), round(float(d.max()), 2), int(ok.sum())]
     print(json.dumps(res), flush=True)
-
-# --ao: the fused batch-1 attention + O projection kernel (csrc/kernels/attention_o.hip)
-if "--ao" in sys.argv:
-    H, D, d, ctx = 32, 128, 4096, 200
-    nblk = (ctx + 63) // 64
-    kc = torch.randn(nblk * 8 + 1, H, 64, D, device=dev).to(torch.bfloat16)
-    vc = torch.randn_like(kc)
-    bt = (torch.randperm(nblk * 8, device=dev)[:nblk].int() + 1).view(1, nblk)
-    pos = torch.tensor([ctx - 1], dtype=torch.int32, device=dev)
-    parts = torch.randn(2, 1, 3 * H * D, device=dev)
-    wo = ops.PackedWeight.from_dense((torch.randn(d, H * D, device=dev) * 0.02).to(torch.bfloat16))
-    h = torch.zeros(1, d, device=dev)
-    x = torch.zeros(1, d, device=dev, dtype=torch.bfloat16)
-    ss = torch.zeros(1, device=dev, dtype=torch.int64)
-    slabs = torch.empty(H * d, device=dev)
-    tk = torch.zeros(64, device=dev, dtype=torch.int32)
-    for _ in range(5):
-        ops.attn_o_b1(parts, cos, sin, pos, kc, vc, bt, H, 1 / math.sqrt(D), wo, slabs, tk, h, x, ss)
-    torch.cuda.synchronize()
-    st = torch.zeros(H * (d // 512) * 8, dtype=torch.int64, device=dev)
-    ops.ext().attn_o_set_stamps(st)
-    ops.attn_o_b1(parts, cos, sin, pos, kc, vc, bt, H, 1 / math.sqrt(D), wo, slabs, tk, h, x, ss)
-    torch.cuda.synchronize()
-    ops.ext().attn_o_set_stamps(None)
-    s = st.view(-1, 8).cpu().double()
-    t0 = s[:, 0].min()
-    names = ["start->rope", "rope->scored", "scored->merged", "merged->ticket", "ticket->end"]
-    res = {"case": "attn_o_b1_7b_ctx200", "start_spread_us": round(float((s[:, 0].max() - t0) / 100), 2),
-           "last_end_us": round(float((s.max(1).values.max() - t0) / 100), 2)}
-    for k, ph in enumerate(names):
-        a, b = s[:, k], s[:, k + 1]
-        ok = (a > 0) & (b > 0)
-        if ok.any():
-            dd = (b[ok] - a[ok]) / 100.0
-            res[ph] = [round(float(dd.median()), 2), round(float(dd.max()), 2), int(ok.sum())]
-    print(json.dumps(res), flush=True)

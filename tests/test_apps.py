@@ -204,3 +204,36 @@ def test_run_client_against_app(api, ctx):
     assert c.generate("duckdb-nsql", "Select 10 records", "T (int)")["response"].startswith("SELECT")
     with pytest.raises(ValueError):
         c.process_data("", "")  # the notebook's empty payload is rejected client-side
+
+
+def test_explain_error_without_num_predict_is_not_truncated(tmp_path):
+    """The reference's option-less ollama.generate call (FastAPI/app.py:105-109) generates until EOS or the
+    context window; a served /explain_error without num_predict must not stop at a fixed cap (it used to
+    be cut at 256 tokens).  Tiny Llama-3 engine on CPU with EOS disabled: the answer runs to the window."""
+    from fastapi.testclient import TestClient
+
+    from llm_based_apache_spark_optimization_amd.client import EngineService
+    from llm_based_apache_spark_optimization_amd.engine import build_engine
+    from llm_based_apache_spark_optimization_amd.serving.fastapi_app import create_app
+
+    s = Settings(input_dir=str(tmp_path / "in"), output_dir=str(tmp_path / "out"),
+                 history_dsn="sqlite:///" + str(tmp_path / "h.db"), engine="hip", secret_key="test",
+                 explain_model="tiny-llama3", nl2sql_model="tiny-nsql")
+    assert s.max_new_tokens < 0  # the service default is Ollama's: no num_predict
+
+    def factory(model):
+        eng = build_engine(model, device="cpu", max_slots=2, max_model_len=1024)
+        eng.runner.set_eos([-1])  # random weights: never stop early, so the length is the window's
+        return eng
+
+    svc = EngineService(factory, defaults={"temperature": 0.0, "num_predict": s.max_new_tokens})
+    try:
+        api = TestClient(create_app(make_context(s, backend=svc)))
+        r = api.post("/explain_error", json={"error_message": "[UNRESOLVED_COLUMN.WITH_SUGGESTION] A column "
+                                                               "with name `Locaton` cannot be resolved."})
+        assert r.status_code == 200, r.text
+        body = r.json()
+        assert body["eval_count"] > 256
+        assert body["eval_count"] + body["prompt_eval_count"] == 1024  # stopped by the context window only
+    finally:
+        svc.loop("tiny-llama3").close()

@@ -186,3 +186,120 @@ def test_engine_ar_timeout_raises(gpu):
         [p.kill() for p in ps if p.is_alive()]
     assert got[0][0][0] == "good" and got[1][0][0] == "good" and got[0][0][1] == got[1][0][1], got
     assert got[0][1][0] == "raised", got
+
+
+def _spawn(target, world, limit):
+    import torch.multiprocessing as tmp
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in ps]
+    got, t0 = {}, time.time()
+    try:
+        while len(got) < world:
+            assert time.time() - t0 < limit, "workers timed out"
+            assert not any(p.exitcode not in (None, 0) for p in ps), [p.exitcode for p in ps]
+            try:
+                r, out = q.get(timeout=2)
+                got[r] = out
+            except queue.Empty:
+                pass
+    finally:
+        [p.join(timeout=30) for p in ps]
+        [p.kill() for p in ps if p.is_alive()]
+    return got
+
+
+def _follower_timeout_worker(rank, world, port, q):
+    """Rank 1 (a follower) times out waiting for rank 0; rank 0's NEXT call must see the abort word rank 1
+    raised in its region: poisoned (NaN) result and err set, so the leader's host sync raises."""
+    import os
+
+    import torch.distributed as dist
+
+    from llm_based_apache_spark_optimization_amd.parallel.custom_ar import IpcAllReduce
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    out = {}
+    try:
+        car = IpcAllReduce(dist.group.WORLD, rank, world, dev, max_bytes=1 << 20, timeout_s=0.5)
+        t = torch.ones(4096, device=dev)
+        car(t)
+        torch.cuda.synchronize(dev)
+        out["good"] = bool(torch.all(t == world).item())
+        dist.barrier()
+        if rank == 1:
+            t = torch.ones(4096, device=dev)
+            car(t)  # rank 0 is asleep: times out after 0.5 s
+            torch.cuda.synchronize(dev)
+            out["err"] = int(car.err.item())
+            dist.barrier()
+        else:
+            dist.barrier()  # rank 1's call has timed out and raised the abort word
+            t = torch.ones(4096, device=dev)
+            car(t)  # rank 1's flag for this epoch is up: no wait, but the abort word is set
+            torch.cuda.synchronize(dev)
+            out["err"] = int(car.err.item())
+            out["nan"] = bool(torch.isnan(t).all().item())
+        dist.barrier()
+    except Exception as e:  # noqa: BLE001
+        out["exc"] = repr(e)
+    q.put((rank, out))
+
+
+def test_follower_timeout_poisons_the_leader(gpu):
+    got = _spawn(_follower_timeout_worker, 2, 90)
+    assert got[0].get("good") and got[1].get("good"), got
+    assert got[1]["err"] == 1, got
+    assert got[0]["err"] == 1 and got[0]["nan"], got
+
+
+def _fallback_worker(rank, world, port, q):
+    """TP=2 tiny engine with rank 1's peer mapping forced to fail: both ranks fall back to the plain
+    collectives (no IPC all-reduce) and generate the same tokens as the IPC path."""
+    import os
+
+    import torch.distributed as dist
+
+    from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build_engine
+    from llm_based_apache_spark_optimization_amd.parallel import TPGroup
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    out = {}
+    try:
+        sp = SamplingParams(max_tokens=12, ignore_eos=True)
+        prompts = [[1, 5, 6, 7, 8], [1] + list(range(20, 90))]
+        os.environ["LSA_TEST_FAIL_AR_OPEN"] = "1"
+        tp = TPGroup(dist.group.WORLD, rank, world, dev)
+        eng = build_engine("tiny-nsql", device=str(dev), max_slots=2, max_model_len=256, tp=tp)
+        out["fallback_car"] = tp.car is None
+        out["fallback"] = [r.token_ids for r in eng.generate(prompts, sp)]
+        del eng
+        os.environ.pop("LSA_TEST_FAIL_AR_OPEN")
+        tp2 = TPGroup(dist.new_group([0, 1]), rank, world, dev)
+        eng2 = build_engine("tiny-nsql", device=str(dev), max_slots=2, max_model_len=256, tp=tp2)
+        out["ipc_car"] = tp2.car is not None
+        out["ipc"] = [r.token_ids for r in eng2.generate(prompts, sp)]
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+    except Exception as e:  # noqa: BLE001
+        out["exc"] = repr(e)
+    q.put((rank, out))
+
+
+def test_ar_open_failure_falls_back_with_identical_tokens(gpu):
+    got = _spawn(_fallback_worker, 2, 150)
+    for r in (0, 1):
+        assert "exc" not in got[r], got
+        assert got[r]["fallback_car"] and got[r]["ipc_car"], got
+    assert got[0]["fallback"] == got[0]["ipc"] == got[1]["fallback"], got

@@ -114,26 +114,6 @@ def test_batched_decode_is_deterministic(gpu, batch):
     assert a == b
 
 
-def test_multi_step_graphs_match_single_step(gpu, monkeypatch):
-    """Decode runs replay a k-step graph, then single-step graphs for the rest: same tokens as one step per
-    graph, for length limits that are not multiples of k and with EOS checks (sync_every not a multiple)."""
-    prompts = [[1] + list(range(3, 3 + n)) for n in (5, 70, 9)]
-    lens = [13, 7, 21]
-    outs = []
-    for k in ("1", "4"):
-        monkeypatch.setenv("LSA_STEPS_PER_GRAPH", k)
-        eng = build_engine("tiny-nsql", device=str(gpu), max_slots=4, max_model_len=256, sync_every=6)
-        assert eng.runner.steps_per_graph == int(k)
-        reqs = [eng.add_request(p, SamplingParams(max_tokens=n, ignore_eos=True)) for p, n in zip(prompts, lens)]
-        eng.run_until_done(reqs)
-        eos = reqs[2].output_ids[9]
-        eng.runner.set_eos([eos])
-        r2 = eng.generate([prompts[2]], SamplingParams(max_tokens=21))[0]
-        outs.append(([q.output_ids for q in reqs], r2.token_ids))
-        assert [len(q.output_ids) for q in reqs] == lens
-    assert outs[0] == outs[1]
-
-
 def test_eos_stops(gpu):
     eng = build_engine("tiny-nsql", device=str(gpu), max_slots=2, max_model_len=256)
     r = eng.generate([[1, 5, 6, 7]], SamplingParams(max_tokens=20, ignore_eos=True))[0]

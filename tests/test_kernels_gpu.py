@@ -461,56 +461,6 @@ def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
     assert _rel(out, out2) < 1e-2
 
 
-@pytest.mark.parametrize("split", ["2", "3", "5"])
-@pytest.mark.parametrize("pair", ["0", "1"])
-@pytest.mark.parametrize("case", ["fresh", "chunked", "long"])
-def test_attn_prefill_kv_split(gpu, case, pair, split, monkeypatch):
-    """32-row kernel with the heavy query blocks' causal key ranges cut into KV splits (ops.prefill_plan:
-    partial O + (m, l) per split, attn_prefill_combine_kernel merge) vs the fp32 reference."""
-    monkeypatch.setattr(ops, "PREFILL_ATTN", "32")
-    monkeypatch.setattr(ops, "PREFILL_PAIR", pair)
-    monkeypatch.setattr(ops, "PREFILL_SPLIT", split)
-    H, Hkv, D = 24, 8, 128
-    qlens, ctx = {"fresh": ([1, 70, 130, 600], [1, 70, 130, 600]), "chunked": ([10, 200, 100], [700, 264, 400]),
-                  "long": ([1000, 257], [1000, 900])}[case]
-    kc, vc, bt = _paged(ctx, Hkv, D, gpu, seed=3)
-    T = sum(qlens)
-    q = torch.randn(T, H, D, device=gpu).to(torch.bfloat16)
-    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0).tolist()), device=gpu, dtype=torch.int32)
-    cl = torch.tensor(ctx, device=gpu, dtype=torch.int32)
-    plan = ops.prefill_plan(cu.tolist(), ctx=ctx, heads=H, device=gpu)
-    assert plan.n_pslots > 0 and plan.combine is not None  # the split path is what runs
-    out = torch.empty(T, H, D, device=gpu, dtype=torch.bfloat16)
-    out2 = torch.empty_like(out)
-    ops.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), out, work=plan)
-    ref.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), out2)
-    assert _rel(out, out2) < 1e-2
-
-
-@pytest.mark.parametrize("case", ["fresh", "chunked", "long", "2k"])
-def test_attn_prefill_halves(gpu, case, monkeypatch):
-    """32-row kernel with each query block's key tiles split over the workgroup's two wave groups and merged
-    in LDS (pslot -2) vs the fp32 reference; includes 1-tile blocks (no split) and idle waves past qlen."""
-    monkeypatch.setattr(ops, "PREFILL_ATTN", "32")
-    monkeypatch.setattr(ops, "PREFILL_SPLIT", "0")
-    monkeypatch.setattr(ops, "PREFILL_HALVES", "1")
-    H, Hkv, D = 24, 8, 128
-    qlens, ctx = {"fresh": ([1, 70, 130, 600], [1, 70, 130, 600]), "chunked": ([10, 200, 100], [700, 264, 400]),
-                  "long": ([1000, 257], [1000, 900]), "2k": ([2048], [2048])}[case]
-    kc, vc, bt = _paged(ctx, Hkv, D, gpu, seed=5)
-    T = sum(qlens)
-    q = torch.randn(T, H, D, device=gpu).to(torch.bfloat16)
-    cu = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0).tolist()), device=gpu, dtype=torch.int32)
-    cl = torch.tensor(ctx, device=gpu, dtype=torch.int32)
-    plan = ops.prefill_plan(cu.tolist(), ctx=ctx, heads=H, device=gpu)
-    assert plan.kernel == "32" and plan.combine is None and int((plan.work[:, 4] == -2).sum()) > 0
-    out = torch.empty(T, H, D, device=gpu, dtype=torch.bfloat16)
-    out2 = torch.empty_like(out)
-    ops.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), out, work=plan)
-    ref.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, 1 / math.sqrt(D), out2)
-    assert _rel(out, out2) < 1e-2
-
-
 @pytest.mark.parametrize("kernel", ["16", "32", "32pair"])
 def test_attn_prefill_spike(gpu, kernel, monkeypatch):
     """Force the online-softmax rescale branch: one very large score late in the sequence."""
@@ -852,41 +802,3 @@ def test_add_rmsnorm_fp8_output(gpu, M):
     assert _rel(got, want) < 4e-2
     assert _rel(ops.from_xfrag(xn, M, d).float(), want) < 1e-2  # the bf16 copy is still written
 
-
-# ------------------------------------------------------------------ batch-1 attention + O projection, one launch
-@pytest.mark.parametrize("ctx", [1, 64, 200, 512])
-@pytest.mark.parametrize("nparts", [1, 2])
-def test_attn_o_b1(gpu, ctx, nparts):
-    """attn_o_b1 (attention + O projection + residual epilogue fused) vs attn_decode + the residual O GEMM:
-    same h, bf16 copy and Q24 sum of squares; the K/V append lands in the cache; tickets left zeroed."""
-    from llm_based_apache_spark_optimization_amd.ops import reference as ref
-
-    H, D, d = 32, 128, 4096
-    torch.manual_seed(ctx + nparts)
-    kc, vc, bt = _paged([ctx + 64], H, D, gpu, seed=ctx)
-    cos, sin = ref.rope_tables(D, bt.shape[1] * 64, 10000.0, device=gpu)
-    pos = torch.tensor([ctx - 1], dtype=torch.int32, device=gpu)
-    parts = torch.randn(nparts, 1, 3 * H * D, device=gpu) / nparts
-    wo = ops.PackedWeight.from_dense((torch.randn(d, H * D, device=gpu) / math.sqrt(H * D)).to(torch.bfloat16))
-    h0 = torch.randn(1, d, device=gpu)
-    # reference: the two-launch path on copies of the cache
-    kc2, vc2 = kc.clone(), vc.clone()
-    q = torch.empty(1, H, D, device=gpu, dtype=torch.bfloat16)
-    a = torch.empty_like(q)
-    ops.attn_decode(q, kc2, vc2, bt, pos, H, H, 1 / math.sqrt(D), a, qkv_parts=parts, cos=cos, sin=sin)
-    h_ref, x_ref = h0.clone(), torch.zeros(1, d, device=gpu, dtype=torch.bfloat16)
-    ss_ref = torch.zeros(1, device=gpu, dtype=torch.int64)
-    ops.linear(a.view(1, -1), wo, "res", res=(h_ref, x_ref, ss_ref))
-    # fused
-    h1, x1 = h0.clone(), torch.zeros(1, d, device=gpu, dtype=torch.bfloat16)
-    ss1 = torch.zeros(1, device=gpu, dtype=torch.int64)
-    slabs = torch.empty(H * d, device=gpu)
-    tk = torch.zeros(64, device=gpu, dtype=torch.int32)
-    ops.attn_o_b1(parts, cos, sin, pos, kc, vc, bt, H, 1 / math.sqrt(D), wo, slabs, tk, h1, x1, ss1)
-    torch.cuda.synchronize()
-    assert _rel(h1 - h0, h_ref - h0) < 2e-3
-    assert _rel(x1.float(), x_ref.float()) < 1e-2
-    assert abs(ops.ss_float(ss1).item() - ops.ss_float(ss_ref).item()) <= 1e-3 * ops.ss_float(ss_ref).item()
-    assert torch.all(tk == 0)
-    blk, slot = int(bt[0, (ctx - 1) // 64]), (ctx - 1) % 64
-    assert torch.equal(kc[blk, :, slot], kc2[blk, :, slot]) and torch.equal(vc[blk, :, slot], vc2[blk, :, slot])

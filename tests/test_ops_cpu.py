@@ -60,55 +60,31 @@ def test_norm_and_attention_xf_cpu():
     assert torch.equal(ops.from_xfrag(of, 2, H * Dh), o.view(2, -1))
 
 
-def _check_plan(cu, ctx, heads, monkeypatch, split):
-    monkeypatch.setattr(ops, "PREFILL_SPLIT", split)
-    work, combine, npl = ops.prefill_plan_items(cu, ctx=ctx, kernel="32", heads=heads)
-    units = [tuple(w[i:i + 5]) for w in work for i in range(0, len(w), 5) if w[i] >= 0]
+def _check_plan(cu, ctx, heads, pair, monkeypatch):
+    monkeypatch.setattr(ops, "PREFILL_PAIR", pair)
+    work = ops.prefill_work(cu, ctx=ctx, kernel="32", heads=heads)
+    assert all(len(w) in (4, 8) for w in work)
+    units = [tuple(w[i:i + 4]) for w in work for i in range(0, len(w), 4) if w[i] >= 0]
     cover = {}
-    for s, qs, t0, t1, ps in units:
-        assert 0 <= t0 < t1
-        cover.setdefault((s, qs), []).append((t0, t1, ps))
-    merges = {(s, qs): (p0, k) for s, qs, p0, k in combine}
-    for w in work:  # in-workgroup halves: both groups of the row on one block, nowhere else
-        if len(w) == 10 and w[4] == -2:
-            assert w[9] == -2 and (w[0], w[1]) == (w[5], w[6]) and w[3] == w[7]
-    slots = []
+    for s, qs, t0, t1 in units:
+        assert (s, qs) not in cover  # one work item per query block
+        cover[(s, qs)] = (t0, t1)
     for s in range(len(cu) - 1):
         ql, pos0 = cu[s + 1] - cu[s], ctx[s] - (cu[s + 1] - cu[s])
         for qs in range(0, ql, 128):
             nt = (pos0 + min(qs + 128, ql) + 63) // 64
-            pieces = sorted(cover.pop((s, qs)))
-            assert pieces[0][0] == 0 and pieces[-1][1] == nt  # every causal key tile exactly once
-            assert all(a[1] == b[0] for a, b in zip(pieces, pieces[1:]))
-            if len(pieces) == 1:
-                assert pieces[0][2] == -1 and (s, qs) not in merges
-            elif pieces[0][2] == -2:
-                assert len(pieces) == 2 and pieces[1][2] == -2 and (s, qs) not in merges
-            else:
-                p0, k = merges.pop((s, qs))
-                assert k == len(pieces) and sorted(p[2] for p in pieces) == list(range(p0, p0 + k))
-                slots += [p[2] for p in pieces]
-    assert not cover and not merges and sorted(slots) == list(range(npl))
-    return units, npl
+            assert cover.pop((s, qs)) == (0, nt)  # the whole causal key range
+    assert not cover
+    return work
 
 
-def test_prefill_plan_kv_splits_cover_causal_ranges(monkeypatch):
-    """ops.prefill_plan for the 32-row kernel: each query block's causal key tiles are covered exactly once by
-    its pieces, split blocks get consecutive partial slots and one merge row, unsplit blocks write directly."""
-    monkeypatch.setattr(ops, "PREFILL_PAIR", "auto")
-    # 2k prompt (3B heads): the auto budget splits the heavy half of the blocks
-    units, npl = _check_plan([0, 2048], [2048], 24, monkeypatch, "auto")
-    assert npl > 0 and max(t1 - t0 for _, _, t0, t1, _ in units) <= ops._split_tiles(272 * 24)
-    # chunked continuation and several sequences, forced small budget; and splitting off
-    _check_plan([0, 10, 210, 310], [700, 264, 400], 32, monkeypatch, "3")
-    monkeypatch.setattr(ops, "PREFILL_HALVES", "0")
-    _, npl = _check_plan([0, 2048], [2048], 24, monkeypatch, "0")
-    assert npl == 0
-    # in-workgroup halves (no splits): every block of >= 2 tiles is one workgroup row of two halves
-    monkeypatch.setattr(ops, "PREFILL_HALVES", "auto")  # (opt-in: the default is "0")
-    units, npl = _check_plan([0, 2048], [2048], 24, monkeypatch, "0")
-    assert npl == 0 and len(units) == 32 and all(ps == -2 for *_, ps in units)
-    _check_plan([0, 10, 210, 310], [700, 264, 400], 32, monkeypatch, "0")
-    # an 8k prompt already has more blocks than slots: no splits under auto
-    _, npl = _check_plan([0, 8192], [8192], 24, monkeypatch, "auto")
-    assert npl == 0
+def test_prefill_plan_covers_causal_ranges(monkeypatch):
+    """ops.prefill_work for the 32-row kernel: every query block is one work item over all its causal key
+    tiles; paired rows hold a heavy and a light block (heaviest first), unpaired rows one block."""
+    w = _check_plan([0, 2048], [2048], 24, "auto", monkeypatch)
+    assert len(w) == 8 and all(len(r) == 8 for r in w)  # 16 blocks x 24 heads <= 512 slots: paired
+    assert [r[3] for r in w] == sorted([r[3] for r in w], reverse=True)
+    _check_plan([0, 10, 210, 310], [700, 264, 400], 32, "1", monkeypatch)
+    w = _check_plan([0, 10, 210, 310], [700, 264, 400], 32, "0", monkeypatch)
+    assert all(len(r) == 4 for r in w)
+    _check_plan([0, 8192], [8192], 24, "auto", monkeypatch)
