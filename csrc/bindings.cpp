@@ -1,9 +1,16 @@
 // pybind11 / torch bindings of the gfx950 kernels (csrc/kernels/*.hip).
 // Every op launches on the current HIP stream so it can be captured into a hipGraph
 // (torch.cuda.CUDAGraph) and ordered with RCCL collectives issued by torch.distributed.
+#ifdef LSA_BINDINGS_SELFTEST
+// host-only build of the argument validation (csrc/tests/bindings_selftest.cpp, under ASan / UBSan on the CPU):
+// CPU tensors stand in for device tensors, the launchers are stubs, no Python module
+#include <ATen/ATen.h>
+#include <hip/hip_runtime_api.h>
+#else
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
+#endif
 
 #include "kernels/lsa_epi.h"
 
@@ -73,12 +80,18 @@ int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int ran
 
 namespace {
 
+#ifdef LSA_BINDINGS_SELFTEST
+hipStream_t cur_stream() { return nullptr; }
+bool on_dev(const at::Tensor& t) { return t.defined(); }
+#else
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+bool on_dev(const at::Tensor& t) { return t.is_cuda(); }
+#endif
 
 void check(int rc, const char* what) { TORCH_CHECK(rc == 0, "lsa kernel '", what, "' failed: rc=", rc); }
 
 void need(const at::Tensor& t, at::ScalarType dt, const char* name) {
-  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(on_dev(t), name, " must be a GPU tensor");
   TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
 }
 
@@ -216,7 +229,7 @@ void fp8_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& w
                  const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets) {
   need(xf, at::kBFloat16, "xf");
   need(wscale, at::kFloat, "wscale");
-  TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
+  TORCH_CHECK(on_dev(wq) && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
   TORCH_CHECK(M >= 1 && M <= 64 && K % 64 == 0, "fp8_gemm_xf: M in 1..64, K % 64 == 0");
   const int64_t mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   TORCH_CHECK(xf.is_contiguous() && xf.numel() >= mt * 16 * K, "xf too small");
@@ -234,11 +247,11 @@ void fp8a_gemm(const at::Tensor& x8, const at::Tensor& sx, int64_t M, int64_t K,
                int64_t waves, int64_t depth, int64_t xfo, const c10::optional<at::Tensor>& rowss, double eps) {
   need(sx, at::kFloat, "sx");
   need(wscale, at::kFloat, "wscale");
-  TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
+  TORCH_CHECK(on_dev(wq) && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
   TORCH_CHECK(M >= 1 && M <= 64 && K % 128 == 0, "fp8a_gemm: M in 1..64, K % 128 == 0");
   TORCH_CHECK(epi == 1 || epi == 2, "fp8a_gemm: f32 slabs or silu");
   const int64_t mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  TORCH_CHECK(x8.is_cuda() && x8.element_size() == 1 && x8.is_contiguous() && x8.numel() >= mt * 16 * K, "x8 too small");
+  TORCH_CHECK(on_dev(x8) && x8.element_size() == 1 && x8.is_contiguous() && x8.numel() >= mt * 16 * K, "x8 too small");
   TORCH_CHECK(sx.numel() >= M, "sx too small");
   check_out(epi, out, splitk, M, N, xfo ? mt : 0);
   const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, c10::nullopt, c10::nullopt, 0, c10::nullopt, c10::nullopt, N / 16);
@@ -252,7 +265,7 @@ void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) 
   need(sx, at::kFloat, "sx");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
   const int M = x.size(0), K = x.size(1);
-  TORCH_CHECK(x8.is_cuda() && x8.element_size() == 1 && x8.numel() >= mt * 16 * K && sx.numel() >= M, "x8 / sx too small");
+  TORCH_CHECK(on_dev(x8) && x8.element_size() == 1 && x8.numel() >= mt * 16 * K && sx.numel() >= M, "x8 / sx too small");
   check(lsa_quant_xf8(x.data_ptr(), x.stride(0), M, K, (int)mt, x8.data_ptr(), sx.data_ptr<float>(), cur_stream()),
         "quant_xf8");
 }
@@ -281,7 +294,7 @@ void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscal
               const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& xout, int64_t xmt,
               const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets) {
   need(x, at::kBFloat16, "x");
-  TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1, "wq must be a 1-byte GPU tensor");
+  TORCH_CHECK(on_dev(wq) && wq.element_size() == 1, "wq must be a 1-byte GPU tensor");
   need(wscale, at::kFloat, "wscale");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
   const int M = x.size(0), K = x.size(1);
@@ -303,7 +316,7 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
   need(w, at::kBFloat16, "w");
   if (xn.has_value()) need(*xn, at::kBFloat16, "xn");
   if (x8.has_value()) {
-    TORCH_CHECK(x8->is_cuda() && x8->element_size() == 1 && x8->numel() >= xf_mt * 16 * w.numel(), "x8 too small");
+    TORCH_CHECK(on_dev(*x8) && x8->element_size() == 1 && x8->numel() >= xf_mt * 16 * w.numel(), "x8 too small");
     TORCH_CHECK(sx8.has_value() && sx8->scalar_type() == at::kFloat && sx8->numel() >= rows, "x8 needs sx8 [rows] f32");
   }
   const int D = w.numel();
@@ -327,10 +340,15 @@ void rope_append(const at::Tensor& qkv, const at::Tensor& pos, const c10::option
   need(pos, at::kInt, "pos");
   check_cache(kc, vc, ks, vs);
   need(block_tables, at::kInt, "block_tables");
+  need(cos_t, at::kFloat, "cos");
+  need(sin_t, at::kFloat, "sin");
+  need(q_out, at::kBFloat16, "q_out");
   // qkv: bf16 [T, n] or f32 split-K slabs [S, T, n]
   const bool parts = qkv.scalar_type() == at::kFloat;
   TORCH_CHECK(parts || qkv.scalar_type() == at::kBFloat16, "qkv must be bf16 or f32 slabs");
   const int T = parts ? qkv.size(1) : qkv.size(0);
+  TORCH_CHECK(qkv.size(qkv.dim() - 1) == (H + 2 * Hkv) * 128 && pos.numel() >= T && q_out.numel() >= (int64_t)T * H * 128,
+              "rope_append: qkv [.., T, (H + 2 Hkv) * 128], pos [T], q_out [T, H, 128]");
   TORCH_CHECK(cos_t.size(0) >= block_tables.size(1) * 64 && sin_t.size(0) >= block_tables.size(1) * 64,
               "rope tables have fewer rows than the block tables address (", block_tables.size(1) * 64, ")");
   check(lsa_rope_append(parts ? nullptr : qkv.data_ptr(), parts ? qkv.data_ptr<float>() : nullptr,
@@ -342,12 +360,16 @@ void rope_append(const at::Tensor& qkv, const at::Tensor& pos, const c10::option
 
 void silu_mul(const at::Tensor& g, const at::Tensor& u, at::Tensor& o) {
   need(g, at::kBFloat16, "g");
+  need(u, at::kBFloat16, "u");
+  need(o, at::kBFloat16, "o");
+  TORCH_CHECK(u.numel() == g.numel() && o.numel() >= g.numel() && g.is_contiguous() && u.is_contiguous() &&
+                  o.is_contiguous(), "silu_mul: contiguous g, u of equal size and o at least as large");
   check(lsa_silu_mul(g.data_ptr(), u.data_ptr(), o.data_ptr(), g.numel(), cur_stream()), "silu_mul");
 }
 
 extern "C" int lsa_attn_set_stamps(void* p);
 void attn_set_stamps(const c10::optional<at::Tensor>& st) {
-  if (st.has_value()) TORCH_CHECK(st->is_cuda() && st->element_size() == 8, "stamps: int64 GPU tensor");
+  if (st.has_value()) TORCH_CHECK(on_dev(*st) && st->element_size() == 8, "stamps: int64 GPU tensor");
   check(lsa_attn_set_stamps(st.has_value() ? st->data_ptr() : nullptr), "attn_set_stamps");
 }
 
@@ -360,7 +382,13 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
   need(q, at::kBFloat16, "q");
   check_cache(kc, vc, ks, vs);
   need(pos, at::kInt, "pos");
+  need(block_tables, at::kInt, "block_tables");
   const int B = pos.size(0);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.is_contiguous(),
+              "block_tables [>= B, max_blocks]");
+  TORCH_CHECK(H > 0 && Hkv > 0 && H % Hkv == 0 && kc.size(1) == Hkv, "heads: H % Hkv == 0, cache has Hkv heads");
+  need(out, at::kBFloat16, "out");
+  TORCH_CHECK(out.numel() >= (xf_mt ? xf_mt * 16 : B) * H * 128, "attn_decode out too small");
   need(opart, at::kFloat, "opart");
   need(mlpart, at::kFloat, "mlpart");
   need(counters, at::kInt, "counters");
@@ -413,6 +441,13 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& v
                   double scale, at::Tensor& out, int64_t rows32) {
   need(q, at::kBFloat16, "q");
   need(work, at::kInt, "work");
+  need(cu_q, at::kInt, "cu_q");
+  need(ctx_lens, at::kInt, "ctx_lens");
+  need(block_tables, at::kInt, "block_tables");
+  need(out, at::kBFloat16, "out");
+  TORCH_CHECK(q.dim() == 3 && q.size(1) == H && q.size(2) == 128 && out.sizes() == q.sizes(), "q / out [T, H, 128]");
+  TORCH_CHECK(cu_q.numel() == ctx_lens.numel() + 1 && block_tables.size(0) >= ctx_lens.numel(),
+              "cu_q [nseq + 1], ctx_lens [nseq], block_tables [>= nseq, max_blocks]");
   if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip)
     // work [n_workgroups, 4 * NG]: NG (seq, q_start, t0, t1) items per workgroup (ops.prefill_plan)
     TORCH_CHECK(work.dim() == 2 && (work.size(1) == 4 || work.size(1) == 8) && work.is_contiguous(),
@@ -429,11 +464,29 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& v
         "attn_prefill");
 }
 
+// decode-state operands of the commit kernels: [B] int32 rows, out_tokens [B, max_new]
+void check_state(int64_t B, const at::Tensor& out_tokens, const at::Tensor& gen_len, const at::Tensor& input_ids,
+                 const at::Tensor& positions, const at::Tensor& finished, const at::Tensor& eos,
+                 const at::Tensor& limit, const at::Tensor& eos_on) {
+  for (const at::Tensor* t : {&gen_len, &input_ids, &positions, &finished, &limit, &eos_on}) {
+    need(*t, at::kInt, "decode state");
+    TORCH_CHECK(t->numel() >= B && t->is_contiguous(), "decode state rows: numel < B");
+  }
+  need(out_tokens, at::kInt, "out_tokens");
+  TORCH_CHECK(out_tokens.dim() == 2 && out_tokens.size(0) >= B && out_tokens.is_contiguous(), "out_tokens [B, max_new]");
+  need(eos, at::kInt, "eos");
+  TORCH_CHECK(eos.numel() >= 1, "eos: at least one id (-1 = none)");
+}
+
 void argmax_commit(const at::Tensor& logits, at::Tensor& part, at::Tensor& out_tokens, at::Tensor& gen_len,
                    at::Tensor& input_ids, at::Tensor& positions, at::Tensor& finished, const at::Tensor& eos,
                    const at::Tensor& limit, const at::Tensor& eos_on) {
   need(logits, at::kFloat, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits: contiguous [B, V]");
   const int B = logits.size(0), V = logits.size(1);
+  check_state(B, out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on);
+  need(part, at::kLong, "part");
+  TORCH_CHECK(part.numel() >= (int64_t)B * ((V + 4095) / 4096), "argmax partials too small");
   check(lsa_argmax_commit(logits.data_ptr<float>(), B, V, reinterpret_cast<unsigned long long*>(part.data_ptr()),
                           out_tokens.data_ptr<int>(), out_tokens.size(1), gen_len.data_ptr<int>(),
                           input_ids.data_ptr<int>(), positions.data_ptr<int>(), finished.data_ptr<int>(),
@@ -448,7 +501,24 @@ void sample_commit(at::Tensor& logits, at::Tensor& part, at::Tensor& cand, const
                    at::Tensor& input_ids, at::Tensor& positions, at::Tensor& finished, const at::Tensor& eos,
                    const at::Tensor& limit, const at::Tensor& eos_on) {
   need(logits, at::kFloat, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits: contiguous [B, V]");
   const int B = logits.size(0), V = logits.size(1);
+  check_state(B, out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on);
+  need(part, at::kLong, "part");
+  need(cand, at::kLong, "cand");
+  TORCH_CHECK(part.numel() >= (int64_t)B * ((V + 4095) / 4096) && cand.numel() >= (int64_t)B * ((V + 2047) / 2048) * 64,
+              "sampling workspace too small");
+  need(temperature, at::kFloat, "temperature");
+  need(top_p, at::kFloat, "top_p");
+  need(top_k, at::kInt, "top_k");
+  need(seeds, at::kLong, "seeds");
+  TORCH_CHECK(temperature.numel() >= B && top_p.numel() >= B && top_k.numel() >= B && seeds.numel() >= B,
+              "sampling parameters: one per row");
+  if (hist.has_value()) {
+    need(*hist, at::kInt, "hist");
+    TORCH_CHECK(hist->dim() == 2 && hist->size(0) >= B && hist->is_contiguous(), "hist [B, W]");
+    TORCH_CHECK(penalty.has_value() && penalty->numel() >= B, "repetition penalty: one per row");
+  }
   const int window = hist.has_value() ? hist->size(1) : 0;
   check(lsa_sample_commit(logits.data_ptr<float>(), B, V, reinterpret_cast<unsigned long long*>(part.data_ptr()),
                           reinterpret_cast<unsigned long long*>(cand.data_ptr()), ptr<int>(hist), window,
@@ -466,7 +536,7 @@ void quant_rows_fp8(const at::Tensor& x, at::Tensor& x8, at::Tensor& sx) {
   need(sx, at::kFloat, "sx");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
   const int M = x.size(0), K = x.size(1);
-  TORCH_CHECK(x8.is_cuda() && x8.element_size() == 1 && x8.dim() == 2 && x8.size(0) >= M && x8.size(1) >= K &&
+  TORCH_CHECK(on_dev(x8) && x8.element_size() == 1 && x8.dim() == 2 && x8.size(0) >= M && x8.size(1) >= K &&
                   x8.stride(1) == 1, "x8 must be a row-major [M, K] 1-byte tensor");
   TORCH_CHECK(sx.numel() >= M, "sx too small");
   check(lsa_quant_rows_fp8(x.data_ptr(), x.stride(0), M, K, x8.data_ptr(), x8.stride(0), sx.data_ptr<float>(),
@@ -479,9 +549,9 @@ void fp8_gemm_t256(const at::Tensor& x8, const at::Tensor& sx, const at::Tensor&
                    at::Tensor& out, int64_t epi, int64_t splitk) {
   need(sx, at::kFloat, "sx");
   need(sw, at::kFloat, "sw");
-  TORCH_CHECK(x8.is_cuda() && x8.element_size() == 1 && x8.dim() == 2 && x8.stride(1) == 1, "x8: [M, K] bytes");
+  TORCH_CHECK(on_dev(x8) && x8.element_size() == 1 && x8.dim() == 2 && x8.stride(1) == 1, "x8: [M, K] bytes");
   const int M = x8.size(0), K = x8.size(1);
-  TORCH_CHECK(wq.is_cuda() && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
+  TORCH_CHECK(on_dev(wq) && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
   TORCH_CHECK(sx.numel() >= M && sw.numel() >= N, "scale sizes");
   if (epi == 1) {
     need(out, at::kFloat, "out");
@@ -509,11 +579,13 @@ int64_t ar_alloc(int64_t bytes) {
   return reinterpret_cast<int64_t>(p);
 }
 
+#ifndef LSA_BINDINGS_SELFTEST
 py::bytes ar_handle(int64_t p) {
   char h[64];
   check(lsa_ar_handle(reinterpret_cast<void*>(p), h), "ar_handle");
   return py::bytes(h, 64);
 }
+#endif
 
 int64_t ar_open(const std::string& h) {
   TORCH_CHECK(h.size() == 64, "IPC handle must be 64 bytes");
@@ -528,6 +600,8 @@ void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Te
   need(data, at::kFloat, "data");
   need(regions, at::kLong, "regions");
   need(err, at::kInt, "err");
+  TORCH_CHECK(regions.numel() >= 2 && regions.numel() <= 8 && rank >= 0 && rank < regions.numel(),
+              "all-reduce: 2..8 regions and 0 <= rank < world");
   TORCH_CHECK(nslab >= 1 && data.numel() % nslab == 0, "all-reduce: numel must split into nslab slabs");
   const int64_t n = data.numel() / nslab;
   TORCH_CHECK(data.is_contiguous() && n % 4 == 0, "all-reduce data: contiguous, slab numel % 4 == 0");
@@ -545,6 +619,7 @@ void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Te
 
 }  // namespace
 
+#ifndef LSA_BINDINGS_SELFTEST
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the MI355X NL->SQL / Spark-error inference engine";
   m.def("gemm", &gemm, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"),
@@ -616,3 +691,4 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("prefill_qblock") = lsa_prefill_qblock();
   m.attr("arch") = "gfx950";
 }
+#endif  // LSA_BINDINGS_SELFTEST

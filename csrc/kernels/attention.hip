@@ -86,6 +86,9 @@ struct RopeArgs {
 #ifndef LSA_ATTN_SB_MIN_WG
 #define LSA_ATTN_SB_MIN_WG 512  // grids of at least this many workgroups run the single-buffered G = 1 kernel (SB)
 #endif
+#ifndef LSA_ATTN_SPEC_MAX_WG
+#define LSA_ATTN_SPEC_MAX_WG 512  // grids up to this many workgroups speculate every split's first block (below)
+#endif
 #ifndef LSA_ATTN_BUF_G
 #define LSA_ATTN_BUF_G 2
 #endif
@@ -177,7 +180,15 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
   // block): its first K/V fetch leaves before the context length is even known.  (Speculating the other
   // splits' first blocks too was measured: splits a short sequence does not need then cost a wasted
   // block read each, 23 -> 36 us at B = 32, ctx 200, 4 splits.)
+  // Small grids (the latency-bound batch-1 shapes, <= LSA_ATTN_SPEC_MAX_WG workgroups): every other split
+  // speculates that its range starts at split * chunk_blocks -- exact whenever the context is longer than the
+  // unsplit threshold, because the host plan has nsplit * chunk_blocks >= every context the captured graph
+  // serves -- so its first K/V fetch also leaves before pos[b] is read (one dependent round trip off the
+  // chain, 3B 2k explain: start->ctx 1.2 us); a mismatch (a short context) re-fetches below.
+  const int spec_blk = (split != 0 && (int)(gridDim.x * gridDim.y * gridDim.z) <= LSA_ATTN_SPEC_MAX_WG &&
+                        split * chunk_blocks < max_blocks) ? split * chunk_blocks : -1;
   if (split == 0) fetch(kA, vA, ksA, vsA, 0, 63);
+  else if (spec_blk >= 0) fetch(kA, vA, ksA, vsA, spec_blk, 63);
   // fused RoPE: the new token's q / k / v rows (sum of the QKV projection's split-K slabs) do not depend on
   // the context length -- their loads leave before pos[b] is read, off the prologue's dependent chain
   float xq[8];
@@ -209,7 +220,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
   const int blk1 = min(nblk, blk0 + ech);
 
   // the first K/V block is in flight while the query (and, fused, RoPE) is prepared
-  if (split != 0 && blk0 < blk1) fetch(kA, vA, ksA, vsA, blk0, ctx - 1 - blk0 * 64);
+  if (split != 0 && blk0 < blk1 && blk0 != spec_blk) fetch(kA, vA, ksA, vsA, blk0, ctx - 1 - blk0 * 64);
   __builtin_amdgcn_sched_barrier(0);
 
   const int tpos = ctx - 1;  // position of the new token

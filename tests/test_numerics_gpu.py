@@ -1,0 +1,87 @@
+"""The bench's decode numerics check (eval/numerics.py) must be able to FAIL.
+
+A 4-layer duckdb-nsql-7B-shaped engine (production hidden / head / ffn / vocab dims, random init) decodes a
+batch for 64 steps; the teacher-forced comparison against the fp32 oracle passes at HEAD and fails when a
+fault is injected into the ENGINE only (the oracle keeps the true weights / cache semantics):
+
+* one layer's down-projection weight scale x1.25 (fp8) / weights x1.25 (bf16): a wrong dequantisation scale;
+* a swapped token pair in the K cache layout (keys of positions 2k and 2k + 1 exchanged in the first block of
+  every layer after prefill, values left in place): a KV layout bug.
+"""
+import dataclasses
+
+import pytest
+import torch
+
+from llm_based_apache_spark_optimization_amd.engine import LLMEngine, ModelRunner
+from llm_based_apache_spark_optimization_amd.eval import numerics as nm
+from llm_based_apache_spark_optimization_amd.models import get_spec
+from llm_based_apache_spark_optimization_amd.models.llama import init_random
+
+pytestmark = pytest.mark.gpu
+
+SPEC = dataclasses.replace(get_spec("duckdb-nsql"), n_layers=4, name="duckdb-nsql-4l")
+
+
+def _engine(gpu, dtype, kv):
+    w = init_random(SPEC, gpu, seed=5, kind=dtype)
+    r = ModelRunner(w, max_slots=32, max_model_len=512, use_graphs=True, num_kv_blocks=32 * 8 + 1, kv_dtype=kv)
+    return LLMEngine(r, name=SPEC.name)
+
+
+def _prompts(n, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    return [[1] + torch.randint(3, 30000, (100 + 7 * i,), generator=g).tolist() for i in range(n)]
+
+
+def _check(eng, B, weights=None):
+    return nm.teacher_forced_check(eng, _prompts(B), 64, check_rows=(0, B - 1), weights=weights)
+
+
+@pytest.mark.parametrize("dtype,kv", [("bf16", "bf16"), ("fp8", "bf16"), ("fp8", "fp8")])
+@pytest.mark.parametrize("B", [4, 32])
+def test_numerics_check_passes_and_catches_faults(gpu, dtype, kv, B):
+    eng = _engine(gpu, dtype, kv)
+    good = _check(eng, B)
+    assert good["ok"] and good["tokens_checked"] >= 128, good
+
+    # fault 1: a wrong weight scale in one layer of the engine (the oracle gets a fresh copy of the true weights)
+    truth = init_random(SPEC, gpu, seed=5, kind=dtype)
+    lw = eng.runner.w.layers[1].w_down
+    saved = (lw.scale.clone() if lw.scale is not None else lw.data.clone())
+    if lw.scale is not None:
+        lw.scale.mul_(1.25)
+    else:
+        lw.data.copy_((lw.data.float() * 1.25).to(lw.data.dtype))
+    eng.runner.graphs.clear()  # graphs hold pointers, not values: recapture is not needed, but keep it clean
+    bad_scale = _check(eng, B, weights=truth)
+    if lw.scale is not None:
+        lw.scale.copy_(saved)
+    else:
+        lw.data.copy_(saved)
+    assert not bad_scale["ok"], (good, bad_scale)
+
+    # fault 2: keys of a token pair swapped in the cache layout (every layer, first block of every sequence)
+    r = eng.runner
+    orig = r.prefill
+
+    def prefill_swapping(seqs, *a, **k):
+        orig(seqs, *a, **k)
+        for slot, _, _ in seqs:
+            blk = int(r.block_tables[slot, 0])
+            for l in range(r.L):
+                kc = r.kv[l, 0, blk]  # [Hkv, 64, D] (bytes for the fp8 cache: token-pair interleaved rows)
+                ev, od = kc[:, 0:32:2].clone(), kc[:, 1:32:2].clone()
+                kc[:, 0:32:2], kc[:, 1:32:2] = od, ev
+                if r.kv_fp8:  # the per-token scales move with their rows
+                    ks = r.kv_scale[l, 0, blk]
+                    e2, o2 = ks[:, 0:32:2].clone(), ks[:, 1:32:2].clone()
+                    ks[:, 0:32:2], ks[:, 1:32:2] = o2, e2
+
+    r.prefill = prefill_swapping
+    try:
+        bad_kv = _check(eng, B, weights=truth)
+    finally:
+        del r.prefill
+    assert not bad_kv["ok"], (good, bad_kv)
+    print({"good": good, "bad_scale": bad_scale, "bad_kv": bad_kv})
