@@ -89,11 +89,17 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 
   const uint16_t* xp[MT];
   bool xvalid[MT];
+  // row-major X: rows >= M are read through a buffer resource at an offset past its range, so the hardware
+  // returns zeros without a memory request (at batch 1 the 15 padding rows of the 16-row MFMA tile were 15/16
+  // of the activation loads, every one re-reading row 0's lines)
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, XF ? 0 : M * ldx * 2, 0x00020000);
+  uint32_t xoff[MT];
 #pragma unroll
   for (int j = 0; j < MT; ++j) {
     const int m = j * 16 + r;
     xvalid[j] = m < M;
     xp[j] = XF ? X + ((size_t)j * 64 + lane) * 8 : X + (size_t)(xvalid[j] ? m : 0) * ldx + 8 * g;
+    xoff[j] = xvalid[j] ? (uint32_t)(((size_t)m * ldx + 8 * g) * 2) : 0x80000000u;
   }
   const uint4* wp[NB];
 #pragma unroll
@@ -114,8 +120,14 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
     for (int u = 0; u < U; ++u) {
       const int kk = min(kb + u, kbB - 1);
 #pragma unroll
-      for (int j = 0; j < MT; ++j)
-        xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)(LSA_XSAME ? (kk & 1) : kk) * (XF ? MT * 512 : 32));
+      for (int j = 0; j < MT; ++j) {
+        if constexpr (XF) {
+          xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)(LSA_XSAME ? (kk & 1) : kk) * MT * 512);
+        } else {
+          const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff[j] + (uint32_t)kk * 64u, 0, 0);
+          xr[u][j] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+      }
     }
   };
   auto load = [&](uint4 (&wr)[U][NB], uint4 (&xr)[U][MT], int c) {

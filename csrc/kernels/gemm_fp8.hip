@@ -55,12 +55,16 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
     for (int j = 0; j < MT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const uint16_t* xp[MT];
   bool xvalid[MT];
+  // row-major X: padding rows (>= M) read zeros from past the buffer range, no memory request (gemm.hip)
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, XF ? 0 : M * ldx * 2, 0x00020000);
+  uint32_t xoff[MT];
 #pragma unroll
   for (int j = 0; j < MT; ++j) {
     const int m = j * 16 + r;
     xvalid[j] = m < M;
     xp[j] = XF ? X + (((size_t)(g >> 1) * MT + j) * 64 + 32 * (g & 1) + r) * 8
                : X + (size_t)(xvalid[j] ? m : 0) * ldx + 16 * g;
+    xoff[j] = xvalid[j] ? (uint32_t)(((size_t)m * ldx + 16 * g) * 2) : 0x80000000u;
   }
   const uint4* wp[NB];
 #pragma unroll
@@ -84,9 +88,11 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp8_skinny_kernel(const uint1
           xr[u][j][0] = px[0];
           xr[u][j][1] = px[16];
         } else {
-          const uint4* px = reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * 64);
-          xr[u][j][0] = px[0];
-          xr[u][j][1] = px[1];
+          const uint32_t o = xoff[j] + (uint32_t)kk * 128u;
+          const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(xrs, o, 0, 0);
+          const u32x4_t b = __builtin_amdgcn_raw_buffer_load_b128(xrs, o + 16u, 0, 0);
+          xr[u][j][0] = make_uint4(a[0], a[1], a[2], a[3]);
+          xr[u][j][1] = make_uint4(b[0], b[1], b[2], b[3]);
         }
       }
     }

@@ -180,8 +180,20 @@ class ModelRunner:
         mb = os.environ.get("LSA_FUSED_NORM_MAX_B")
         self.fused_norm_max_batch = int(mb) if mb is not None else (16 if self.d >= 4096 else 0)
         self.ssq = torch.zeros(2 * self.L + 2, S, dtype=torch.int64, device=dev)  # Q24 fixed point (ops.ss_q24)
+        # buckets above fused_norm_max_batch: the MLP half only norm-free (o projection with the residual epilogue,
+        # gate_up row-scaled by its sums of squares; the attention-side norm launch stays).  bf16 / W8A16 weights
+        # (the W8A8 gate_up input is quantised by the norm launch)
+        self.mlp_res = (os.environ.get("LSA_MLP_RES", "0") != "0" and tps == 1
+                        and all(lw.norms_folded for lw in weights.layers))
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)
+        # one persistent launch per layer for the post-attention block (ops.decode_block: o -> residual -> gate_up ->
+        # down -> residual -> next qkv) at decode batches <= 64: TP = 1, bf16 weights, folded norms (LSA_DECODE_BLOCK)
+        self.block_decode = (os.environ.get("LSA_DECODE_BLOCK", "0") != "0" and tps == 1 and self.d % 32 == 0
+                             and weights.layers[0].wqkv.kind in ("bf16", "dense")
+                             and all(lw.norms_folded for lw in weights.layers))
+        self.blk_cnt = torch.zeros(self.L, ops.DECODE_BLOCK_CNT_INTS, dtype=torch.int32, device=dev)  # per layer
+        self.blk_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graphs: dict = {}
         self._pending_bt: dict = {}  # slot -> block-table row of a prompt still being prefilled in chunks
         if self.tp is not None and self.tp.size > 1 and self.on_gpu:
@@ -253,6 +265,8 @@ class ModelRunner:
         return tuple(ops.decode_split_plan(B, self.Hkv, tier))
 
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
+        if self.block_decode and B <= 64:
+            return self._decode_step_block(B, sample, plan)
         if self.fused_norm and B <= self.fused_norm_max_batch:
             return self._decode_step_fused(B, sample, plan)
         w, d = self.w, self.d
@@ -268,6 +282,9 @@ class ModelRunner:
                 else self._splitk(B, d, nqkv, tp_reduced=False, xf=xf))
         q8 = dict(x8=self.x8, sx8=self.sx8) if a8 else {}
         q8m = dict(x8=self.x8, sx8=self.sx8) if a8m else {}
+        mres = self.mlp_res and not a8m
+        if mres:
+            sk_o = ops.pick_gemm_config(B, d, self.H * self.D, "res", xf=xf, kind=w.layers[0].wo.kind)[1]
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
@@ -282,7 +299,10 @@ class ModelRunner:
             xn, attn, act = self.xn[:B], self.attn[:B], self.act[:B]
             lin = ops.linear
         for l, lw in enumerate(w.layers):
-            if l == 0:
+            if l == 0 and mres:  # the embedding launch also zeroes the MLP-side row sums of every layer
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf,
+                                ss_out=self.ssq.view(-1), ss_ld=self.max_slots, ss_nzero=2 * self.L, **q8)
+            elif l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf, **q8)
             else:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_red, rows=B, xf=xf, **q8)
@@ -301,13 +321,18 @@ class ModelRunner:
                             attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
                             qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
                             sin=self.sin if fr else None, kv_scales=self._kv_scales(l))
-            lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
-            o_red = self._reduce_parts(o_parts)
-            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
-            if a8m:
-                ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=act)
+            if mres:
+                lin(attn, lw.wo, "res", out=o_parts, splitk=sk_o,
+                    res=(h, xn, self.ssq[2 * l + 1], self.res_tickets))
+                lin(xn, lw.w_gate_up, "silu", out=act, rownorm=(self.ssq[2 * l + 1], self.eps))
             else:
-                lin(xn, lw.w_gate_up, "silu", out=act)
+                lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
+                o_red = self._reduce_parts(o_parts)
+                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
+                if a8m:
+                    ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=act)
+                else:
+                    lin(xn, lw.w_gate_up, "silu", out=act)
             lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
             d_red = self._reduce_parts(d_parts)
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_red, rows=B, xf=xf)
@@ -331,6 +356,9 @@ class ModelRunner:
         sk_o = self._splitk(B, self.H * self.D, xf=xf)
         sk_d = self._splitk(B, self.ffn_l, xf=xf)
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
+        mres = self.mlp_res and not a8m
+        if mres:
+            sk_o = ops.pick_gemm_config(B, d, self.H * self.D, "res", xf=xf, kind=w.layers[0].wo.kind)[1]
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
         plan = plan or ops.decode_split_plan(B, self.Hkv, self.max_model_len)
@@ -357,6 +385,37 @@ class ModelRunner:
             lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk))
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, rows=B, xf=xf, write_h=False)
         self._decode_tail(B, sample, xn, xf)
+
+    def _decode_step_block(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
+        """Decode step with the post-attention block of every layer in ONE persistent launch (ops.decode_block):
+
+          embed (+ row sums of squares) -> qkv[0] (row-scaled, f32) -> per layer:
+            attn_decode (RoPE + KV append from the f32 qkv, fragment-major output)
+            -> decode_block (o + residual -> gate_up -> down + residual -> qkv[l + 1])
+          -> final RMSNorm -> lm_head -> token commit
+
+        2 launches per layer instead of 5-7; every activation in the fragment-major layout (any bucket <= 64)."""
+        w, L = self.w, self.L
+        ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
+        h = self.h[:B]
+        nqkv = (self.H + 2 * self.Hkv) * self.D
+        qkv = self.qkv_buf[: B * nqkv].view(1, B, nqkv)  # one f32 slab, rewritten by every block's last phase
+        plan = plan or ops.decode_split_plan(B, self.Hkv, self.max_model_len)
+        ssq, S = self.ssq, self.max_slots
+        xn, attn, act = self.xn_f, self.attn_f, self.act_f
+        self.blk_cnt.zero_()  # one memset node per step: every layer's claim / done counters
+        ops.add_rmsnorm(h, w.layers[0].attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=True,
+                        ss_out=ssq.view(-1), ss_ld=S, ss_nzero=2 * L)
+        ops.linear_xf(xn, B, w.layers[0].wqkv, "f32", out=qkv, splitk=1, rownorm=(ssq[0], self.eps))
+        for l, lw in enumerate(w.layers):
+            ops.attn_decode(self.q[:B], self.kv[l, 0], self.kv[l, 1], bt, pos, self.H, self.Hkv, self.scale, attn,
+                            workspace=self.attn_ws, plan=plan, xf=True, qkv_parts=qkv, cos=self.cos,
+                            sin=self.sin, kv_scales=self._kv_scales(l))
+            nxt = w.layers[l + 1].wqkv if l + 1 < L else None
+            ops.decode_block(attn, lw.wo, h, xn, ssq[2 * l + 1], ssq[2 * l + 2], lw.w_gate_up, act, lw.w_down, nxt,
+                             qkv, B, self.eps, self.blk_cnt[l], self.blk_err)
+        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, rows=B, xf=True, write_h=False)
+        self._decode_tail(B, sample, xn, True)
 
     def _decode_tail(self, B: int, sample: bool, xn, xf: bool) -> None:
         logits = self._lm_head(xn, B, xf)
@@ -678,10 +737,14 @@ class ModelRunner:
         car = getattr(self.tp, "car", None) if self.tp is not None else None
         if car is not None:
             parts.append(car.err)  # one-shot all-reduce timeout flag, read in the same transfer
+        if self.block_decode:
+            parts.append(self.blk_err)  # persistent decode block: a phase wait that timed out
         host = torch.cat(parts).cpu()
         if car is not None and int(host[2 * n]):
             raise TPCommError("tensor-parallel all-reduce: a peer did not arrive within the timeout; "
                               "this replica's outputs since the last sync are invalid")
+        if self.block_decode and int(host[-1]):
+            raise RuntimeError("decode block: a phase wait timed out; the outputs since the last sync are invalid")
         return host[:n], host[n:2 * n], idx
 
     def tokens_of(self, slot: int, n: int) -> list[int]:

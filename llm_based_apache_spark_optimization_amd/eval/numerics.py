@@ -17,18 +17,30 @@ quantiser -- and a wrong scale or a scrambled cache layout moves the distributio
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Optional, Sequence
 
 import torch
 
-# (mean KL nats, top-5 overlap, top-1 agreement) a healthy engine stays within, per numerics class.
-# Calibrated on MI355X at the benchmark shapes (profiles/numerics_calibration_mi355x.jsonl): the healthy
-# engine sits an order of magnitude inside each bound, the injected faults (one layer's weight scale x1.25,
-# two swapped cached tokens) several times outside.
+# (mean KL nats PER LAYER, top-5 overlap, top-1 agreement) a healthy engine stays within, per numerics class;
+# the KL bound is n_layers x the first entry.  Calibrated on MI355X (profiles/numerics_calibration_mi355x.jsonl,
+# scripts/numerics_calibrate.py: duckdb-nsql-7B shape, random init, 4 and 32 layers, batch 4 and 32):
+#
+#   class   healthy KL / layer      one layer's scale x1.25: KL / layer   swapped cached keys: KL / layer
+#   bf16    1.6e-5 .. 2.6e-5         4.8e-3 .. 5.3e-3                      1.9e-2 .. 5.9e-2
+#   w8a16   2.8e-4 .. 7.2e-4         5.3e-3 .. 5.6e-3                      2.6e-2 .. 5.7e-2
+#   w8a8    4.6e-4 .. 2.1e-3         5.6e-3 .. 6.7e-3                      1.9e-2 .. 7.8e-2
+#
+# Both the healthy noise and a fault's KL grow ~linearly with depth, so the bound scales with n_layers.  The fp8
+# classes' healthy noise is dominated by per-token e4m3 activation rounding that the oracle emulates but cannot
+# reproduce bit-exactly (a bf16-level difference flips a rounding: one e4m3 ulp, ~6 %), compounded over a
+# random-init network; the fp8 bounds sit 1.6-2.8x above the worst healthy row and 1.6-2.7x below the scale
+# fault (bf16: ~10x above, ~19x below).
+# Top-5 / top-1 floors are gross-failure guards (at 32 random layers healthy fp8 top-1 is only ~0.4-0.7).
 THRESHOLDS = {
-    "bf16": (2e-3, 0.9, 0.9),
-    "w8a16": (2e-2, 0.8, 0.6),
-    "w8a8": (5e-2, 0.7, 0.5),
+    "bf16": (2.5e-4, 0.85, 0.8),
+    "w8a16": (2.0e-3, 0.5, 0.4),
+    "w8a8": (3.5e-3, 0.4, 0.3),
 }
 
 
@@ -115,11 +127,56 @@ def check_recorded(eng, prompts, toks, elog, n_steps: int, check_rows: Sequence[
         del lg
     kl, t1, t5 = torch.cat(kls), torch.cat(t1s), torch.cat(t5s)
     cls = numerics_class(r, B)
-    kl_max, t5_min, t1_min = THRESHOLDS[cls]
+    kl_layer, t5_min, t1_min = THRESHOLDS[cls]
+    kl_max = round(kl_layer * len(r.w.layers), 6)
     res = {"tokens_checked": int(kl.numel()), "decode_batch": len(prompts), "class": cls,
            "mean_kl": round(float(kl.mean()), 6), "max_kl": round(float(kl.max()), 6),
            "top1_agree": round(float(t1.mean()), 4), "top5_overlap": round(float(t5.mean()), 4)}
     res["ok"] = bool(res["mean_kl"] < kl_max and res["top5_overlap"] >= t5_min and res["top1_agree"] >= t1_min)
-    res["criterion"] = (f"{cls}: teacher-forced over {n_steps} decode steps: mean KL(oracle||engine) < {kl_max}, "
+    res["criterion"] = (f"{cls}: teacher-forced over {n_steps} decode steps: mean KL(oracle||engine) < {kl_max} "
+                        f"({kl_layer} x {len(r.w.layers)} layers), "
                         f"top-5 overlap >= {t5_min}, top-1 agreement >= {t1_min}")
     return res
+
+
+# ---- fault injection (tests/test_numerics_gpu.py, scripts/numerics_calibrate.py): the check must catch these
+@contextlib.contextmanager
+def scale_fault(eng, layer: int = 1, factor: float = 1.25):
+    """One layer's down-projection dequantisation scale (fp8) / weights (bf16) x ``factor`` in the ENGINE."""
+    lw = eng.runner.w.layers[layer].w_down
+    saved = lw.scale.clone() if lw.scale is not None else lw.data.clone()
+    if lw.scale is not None:
+        lw.scale.mul_(factor)
+    else:
+        lw.data.copy_((lw.data.float() * factor).to(lw.data.dtype))
+    try:
+        yield
+    finally:
+        (lw.scale if lw.scale is not None else lw.data).copy_(saved)
+
+
+@contextlib.contextmanager
+def kv_swap_fault(eng):
+    """Keys of positions 2k and 2k + 1 exchanged in the first cache block of every sequence and layer after
+    prefill (values left in place): a KV layout bug."""
+    r = eng.runner
+    orig = r.prefill
+
+    def prefill_swapping(seqs, *a, **k):
+        orig(seqs, *a, **k)
+        for slot, _, _ in seqs:
+            blk = int(r.block_tables[slot, 0])
+            for l in range(r.L):
+                kc = r.kv[l, 0, blk]  # [Hkv, 64, D] (bytes for the fp8 cache)
+                ev, od = kc[:, 0:32:2].clone(), kc[:, 1:32:2].clone()
+                kc[:, 0:32:2], kc[:, 1:32:2] = od, ev
+                if r.kv_fp8:  # the per-token scales move with their rows
+                    ks = r.kv_scale[l, 0, blk]
+                    e2, o2 = ks[:, 0:32:2].clone(), ks[:, 1:32:2].clone()
+                    ks[:, 0:32:2], ks[:, 1:32:2] = o2, e2
+
+    r.prefill = prefill_swapping
+    try:
+        yield
+    finally:
+        del r.prefill

@@ -402,6 +402,75 @@ def tile_splitk(M: int, N: int, K: int, kind: str = "bf16") -> int:
     return sk
 
 
+# Persistent post-attention decode block (csrc/kernels/decode_block.hip): n-blocks per work item of each phase,
+# (nbo, nbg, nbd, nbq); LSA_DECODE_BLOCK_CFG="nbo,nbg,nbd,nbq" overrides (tuning: scripts/bench_decode_block.py)
+DECODE_BLOCK_DEFAULT = (1, 2, 1, 1)
+DECODE_BLOCK_CNT_INTS = 256  # per-layer claim / done counter block (8 lines of 128 B; kernel's DB_CNT_INTS)
+
+
+def decode_block_cfg(B: int) -> tuple:
+    env = os.environ.get("LSA_DECODE_BLOCK_CFG")
+    if env:
+        return tuple(int(v) for v in env.split(","))
+    return DECODE_BLOCK_DEFAULT
+
+
+def decode_block_grid(B: int, device) -> int:
+    """Workgroups of the persistent block: LSA_DECODE_BLOCK_NWG, else one per CU (the work is claimed
+    dynamically, so any grid size is correct; two resident workgroups per CU need <= 128 VGPRs)."""
+    env = int(os.environ.get("LSA_DECODE_BLOCK_NWG", "0"))
+    return env or num_cus(device)
+
+
+_NUM_CUS: dict = {}
+
+
+def num_cus(device) -> int:
+    idx = torch.device(device).index or 0
+    if idx not in _NUM_CUS:
+        _NUM_CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return _NUM_CUS[idx]
+
+
+def decode_block(attn_xf, wo: "PackedWeight", h, x_xf, ss1, ss2, wgu: "PackedWeight", act_xf, wd: "PackedWeight",
+                 wq: Optional["PackedWeight"], qout, B: int, eps: float, cnt, err, cfg: Optional[tuple] = None,
+                 timeout_s: float = 2.0, nwg: Optional[int] = None) -> None:
+    """One layer's post-attention block in ONE persistent launch (TP = 1, bf16 weights, B <= 64, fragment-major
+    activations): o projection + residual (h += o, x = bf16(h), ss1 += sum h^2) -> gate_up (row-scaled by ss1,
+    SiLU * up -> act) -> down + residual (h, x, ss2) -> [next layer's qkv, row-scaled by ss2, into ``qout``
+    f32 [B, nq] (a one-slab ``qkv_parts`` for the fused-RoPE attention)].  ``cnt`` (int32,
+    >= DECODE_BLOCK_CNT_INTS) must be zero at the launch (the runner zeroes every layer's counters with one memset
+    per step); ss1 / ss2 must be zero."""
+    nbo, nbg, nbd, nbq = cfg or decode_block_cfg(B)
+    d, ffn = wo.N, wd.K
+    if not _gpu(h):
+        a = from_xfrag(attn_xf, B, wo.K)
+        hn = h[:B].float() + ref.linear(a, wo.dense(), "f32")
+        h[:B].copy_(hn)
+        x16 = hn.to(torch.bfloat16)
+        x_xf.view(-1)[: xfrag_tiles(B) * 16 * d].copy_(to_xfrag(x16))
+        ss1[:B] += ss_q24(hn.pow(2).sum(1))
+        rs1 = torch.rsqrt(ss_float(ss1[:B]) / d + eps)[:, None]
+        gu = ref.linear(x16, wgu.dense(), "f32") * rs1
+        g, u = gu.view(B, -1, 2, 16)[:, :, 0].reshape(B, -1), gu.view(B, -1, 2, 16)[:, :, 1].reshape(B, -1)
+        act = (torch.nn.functional.silu(g) * u).to(torch.bfloat16)
+        act_xf.view(-1)[: xfrag_tiles(B) * 16 * ffn].copy_(to_xfrag(act))
+        hn = h[:B].float() + ref.linear(act, wd.dense(), "f32")
+        h[:B].copy_(hn)
+        x16 = hn.to(torch.bfloat16)
+        x_xf.view(-1)[: xfrag_tiles(B) * 16 * d].copy_(to_xfrag(x16))
+        ss2[:B] += ss_q24(hn.pow(2).sum(1))
+        if wq is not None:
+            rs2 = torch.rsqrt(ss_float(ss2[:B]) / d + eps)[:, None]
+            qout.view(-1)[: B * wq.N].view(B, wq.N).copy_(ref.linear(x16, wq.dense(), "f32") * rs2)
+        return
+    assert wo.kind == wgu.kind == wd.kind == "bf16" and (wq is None or wq.kind == "bf16"), "decode_block: bf16 weights"
+    ticks = int(timeout_s * ext().ar_wallclock_khz() * 1000)
+    ext().decode_block(attn_xf, wo.data, h, x_xf, ss1, ss2, wgu.data, act_xf, wd.data,
+                       wq.data if wq is not None else None, qout, B, ffn, wq.N if wq is not None else 0, float(eps),
+                       cnt, err, ticks, nwg or decode_block_grid(B, h.device), nbo, nbg, nbd, nbq)
+
+
 def xfrag_tiles(M: int) -> int:
     """Row tiles (16 rows each) of the fragment-major activation layout for M rows (decode: M <= 64)."""
     return 1 if M <= 16 else (2 if M <= 32 else 4)

@@ -1,0 +1,52 @@
+"""Calibration data for eval/numerics.py THRESHOLDS: the teacher-forced statistics of a healthy engine and of
+the two injected faults (one layer's down scale x1.25, swapped cached keys) per numerics class, at the test's
+4-layer duckdb-nsql-7B shape and at full depth.  One JSON line per (model, dtype, kv, batch, case).
+
+    python scripts/numerics_calibrate.py [n_layers ...]      (GPU; default 4 32)
+"""
+import dataclasses
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from llm_based_apache_spark_optimization_amd.engine import LLMEngine, ModelRunner  # noqa: E402
+from llm_based_apache_spark_optimization_amd.eval import numerics as nm  # noqa: E402
+from llm_based_apache_spark_optimization_amd.models import get_spec  # noqa: E402
+from llm_based_apache_spark_optimization_amd.models.llama import init_random  # noqa: E402
+
+
+def prompts(n, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    return [[1] + torch.randint(3, 30000, (100 + 7 * i,), generator=g).tolist() for i in range(n)]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    layers = [int(v) for v in sys.argv[1:]] or [4, 32]
+    for nl in layers:
+        spec = dataclasses.replace(get_spec("duckdb-nsql"), n_layers=nl, name=f"duckdb-nsql-{nl}l")
+        for dtype, kv in (("bf16", "bf16"), ("fp8", "bf16"), ("fp8", "fp8")):
+            for B in (4, 32):
+                w = init_random(spec, dev, seed=5, kind=dtype)
+                r = ModelRunner(w, max_slots=32, max_model_len=512, use_graphs=True, num_kv_blocks=32 * 8 + 1,
+                                kv_dtype=kv)
+                eng = LLMEngine(r, name=spec.name)
+                ps = prompts(B)
+                rows = (0, B - 1)
+                out = {"good": nm.teacher_forced_check(eng, ps, 64, check_rows=rows)}
+                truth = init_random(spec, dev, seed=5, kind=dtype)
+                with nm.scale_fault(eng, 1, 1.25):
+                    out["bad_scale"] = nm.teacher_forced_check(eng, ps, 64, check_rows=rows, weights=truth)
+                with nm.kv_swap_fault(eng):
+                    out["bad_kv"] = nm.teacher_forced_check(eng, ps, 64, check_rows=rows, weights=truth)
+                for case, res in out.items():
+                    res.pop("criterion", None)
+                    print(json.dumps({"layers": nl, "dtype": dtype, "kv": kv, "B": B, "case": case, **res}), flush=True)
+                del eng, r, w, truth
+                torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

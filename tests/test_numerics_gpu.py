@@ -47,41 +47,12 @@ def test_numerics_check_passes_and_catches_faults(gpu, dtype, kv, B):
 
     # fault 1: a wrong weight scale in one layer of the engine (the oracle gets a fresh copy of the true weights)
     truth = init_random(SPEC, gpu, seed=5, kind=dtype)
-    lw = eng.runner.w.layers[1].w_down
-    saved = (lw.scale.clone() if lw.scale is not None else lw.data.clone())
-    if lw.scale is not None:
-        lw.scale.mul_(1.25)
-    else:
-        lw.data.copy_((lw.data.float() * 1.25).to(lw.data.dtype))
-    eng.runner.graphs.clear()  # graphs hold pointers, not values: recapture is not needed, but keep it clean
-    bad_scale = _check(eng, B, weights=truth)
-    if lw.scale is not None:
-        lw.scale.copy_(saved)
-    else:
-        lw.data.copy_(saved)
+    with nm.scale_fault(eng, 1, 1.25):
+        bad_scale = _check(eng, B, weights=truth)
     assert not bad_scale["ok"], (good, bad_scale)
 
     # fault 2: keys of a token pair swapped in the cache layout (every layer, first block of every sequence)
-    r = eng.runner
-    orig = r.prefill
-
-    def prefill_swapping(seqs, *a, **k):
-        orig(seqs, *a, **k)
-        for slot, _, _ in seqs:
-            blk = int(r.block_tables[slot, 0])
-            for l in range(r.L):
-                kc = r.kv[l, 0, blk]  # [Hkv, 64, D] (bytes for the fp8 cache: token-pair interleaved rows)
-                ev, od = kc[:, 0:32:2].clone(), kc[:, 1:32:2].clone()
-                kc[:, 0:32:2], kc[:, 1:32:2] = od, ev
-                if r.kv_fp8:  # the per-token scales move with their rows
-                    ks = r.kv_scale[l, 0, blk]
-                    e2, o2 = ks[:, 0:32:2].clone(), ks[:, 1:32:2].clone()
-                    ks[:, 0:32:2], ks[:, 1:32:2] = o2, e2
-
-    r.prefill = prefill_swapping
-    try:
+    with nm.kv_swap_fault(eng):
         bad_kv = _check(eng, B, weights=truth)
-    finally:
-        del r.prefill
     assert not bad_kv["ok"], (good, bad_kv)
     print({"good": good, "bad_scale": bad_scale, "bad_kv": bad_kv})
