@@ -12,15 +12,16 @@
 // boundary, ramp-up and tail (profiles/roofline_b32_decode.md).  Here the weight stream runs through the seams:
 //   * every work item is a group of NB 16-column n-blocks over the FULL k range (no split-K: o and down finish
 //     their columns' residual in the epilogue, no slab round trip, no residual phase);
-//   * a workgroup claims its NEXT item while computing the current one (the claim's round trip hides behind
-//     the k-loop) and issues the next item's first weight chunks before the current item's epilogue;
-//   * at a phase seam it claims its first item of the next phase and issues its weights BEFORE it waits for the
-//     current phase to complete (weights never depend on activations: MI355X_MICROARCH.md 'prefetch-credit');
-//   * a workgroup publishes its phase work once (one add of its item count), not per item.
+//   * workgroup i owns item i of every phase (no claim at a seam); the remaining items are claimed dynamically,
+//     a workgroup claiming its NEXT item while computing the current one (the round trip hides behind the
+//     k-loop) and issuing the next item's first weight chunks before the current item's epilogue;
+//   * at a phase seam it issues its first item of the next phase's weights BEFORE it waits for the current phase
+//     to complete (weights never depend on activations: MI355X_MICROARCH.md 'prefetch-credit');
+//   * a workgroup publishes its phase work once (one add of its item count to its XCD's done slot), not per item.
 //
-// Work distribution is dynamic (claim counters), so a workgroup that is not resident never holds work: the launch
-// completes with any number of resident workgroups (no grid barrier, no residency assumption).  Every wait is
-// bounded: on timeout the kernel sets *err and returns.
+// The grid is clamped to the co-resident capacity (occupancy x CUs), so every statically owned item belongs to a
+// workgroup that is resident, or becomes resident as soon as another stream's kernels drain (they never wait on
+// this one): no grid barrier, no deadlock.  Every wait is bounded: on timeout the kernel sets *err and returns.
 //
 // Hand-offs follow MI355X_MICROARCH.md 'Valid forms' row 1: every byte another workgroup reads inside the launch
 // (h, the bf16 activations x / act) is stored write-through (sc1) and loaded with sc1 loads; each storing wave
@@ -36,8 +37,10 @@
 #define DB_WAVES 8
 #define DB_SC1 16   // buffer aux: sc1 (write-through store / L1-bypassing load)
 #define DB_LINE 32  // ints per counter line (128 B)
-// per-layer counter block: phase p's claim counter at cnt[2p * DB_LINE], its done counter at cnt[(2p + 1) * DB_LINE]
-#define DB_CNT_INTS (8 * DB_LINE)
+#define DB_SLOTS 8  // done counters per phase: one per XCD (workgroup i runs on XCD i % 8)
+// per-layer counter block, one 128-B line each: phase p's claim counter at line 9p, its done slots at lines
+// 9p + 1 .. 9p + 8
+#define DB_CNT_INTS (4 * (1 + DB_SLOTS) * DB_LINE)
 
 namespace {
 
@@ -62,6 +65,7 @@ struct DbArgs {
   int* cnt;              // DB_CNT_INTS, zeroed before the launch
   int* err;
   long long timeout_ticks;
+  long long* stamps;     // optional [nwg][16] wall-clock stamps of the phase boundaries (scripts/bench_decode_block.py)
 };
 
 __device__ __forceinline__ u32x4_t ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
@@ -70,52 +74,54 @@ __device__ __forceinline__ u32x4_t ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ db_g_i32* ctr(const DbArgs& a, int p, int done) {
-  return (db_g_i32*)a.cnt + (2 * p + done) * DB_LINE;
+__device__ __forceinline__ db_g_i32* claim_ctr(const DbArgs& a, int p) {
+  return (db_g_i32*)a.cnt + p * (1 + DB_SLOTS) * DB_LINE;
 }
+__device__ __forceinline__ db_g_i32* done_ctr(const DbArgs& a, int p, int slot) {
+  return (db_g_i32*)a.cnt + (p * (1 + DB_SLOTS) + 1 + slot) * DB_LINE;
+}
+// dynamic items start after the static ones: workgroup i owns item i of every phase, the rest are claimed
 __device__ __forceinline__ int claim_issue(const DbArgs& a, int p) {
-  return __hip_atomic_fetch_add(ctr(a, p, 0), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (int)gridDim.x + __hip_atomic_fetch_add(claim_ctr(a, p), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// entry claim (blocking, workgroup-uniform)
-__device__ __forceinline__ int claim_now(const DbArgs& a, int p, int* s_item) {
-  if (threadIdx.x == 0) *s_item = claim_issue(a, p);
-  __syncthreads();
-  return *s_item;
-}
-
-// end of phase p: every storing wave drains its write-through stores, one lane adds the workgroup's item count
-// to the done counter; the claim of the first item of phase pn (< 0: none) rides on the same drain.
-__device__ __forceinline__ int publish_and_claim(const DbArgs& a, int p, int ndone, int pn, int* s_item) {
-  int t = 0;
-  if (threadIdx.x == 0 && pn >= 0) t = claim_issue(a, pn);
+// end of phase p: every storing wave drains its write-through stores, then one lane adds the workgroup's item
+// count to its XCD's done slot (8 slots: no 256-way same-address atomic storm at a seam)
+__device__ __forceinline__ void publish(const DbArgs& a, int p, int ndone) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every wave drained its stores and has read the last *s_item
-  if (threadIdx.x == 0) {
-    if (ndone) __hip_atomic_fetch_add(ctr(a, p, 1), ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *s_item = t;
-  }
   __syncthreads();
-  return *s_item;
+  if (threadIdx.x == 0 && ndone)
+    __hip_atomic_fetch_add(done_ctr(a, p, blockIdx.x % DB_SLOTS), ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// wait until phase p has n items done (bounded); false on timeout (err set)
+// wait until phase p has n items done (bounded); false on timeout (err set).  Lanes 0-7 of wave 0 poll one slot
+// each; the sum is broadcast from lane 0 so the loop stays wave-uniform.
 __device__ __forceinline__ bool wait_done(const DbArgs& a, int p, int n, int* s_flag) {
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
     int ok = 1;
     const long long t0 = wall_clock64();
-    while (__hip_atomic_load(ctr(a, p, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+    while (true) {
+      int v = l < DB_SLOTS ? __hip_atomic_load(done_ctr(a, p, l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (__shfl(v, 0, 64) >= n) break;
       __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > a.timeout_ticks) {
-        __hip_atomic_store((db_g_i32*)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (l == 0) __hip_atomic_store((db_g_i32*)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
       }
     }
-    *s_flag = ok;
+    if (l == 0) *s_flag = ok;
   }
   __syncthreads();
   return *s_flag != 0;
+}
+
+__device__ __forceinline__ void stamp(const DbArgs& a, int k, long long v = -1) {
+  if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 16 + k] = v < 0 ? wall_clock64() : v;
 }
 
 __device__ __forceinline__ float row_scale(const long long* ss, int m, float inv_d, float eps) {
@@ -124,41 +130,43 @@ __device__ __forceinline__ float row_scale(const long long* ss, int m, float inv
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// One GEMM work item: NB n-blocks (16 columns each) x all KB k-blocks, 8 waves splitting the k range in chunks
-// of U k-blocks dealt round-robin (each wave streams its chunks with a two-deep register pipeline, as
-// gemm.hip's skinny kernel).  load_w() issues the first two chunks' weights (the prefetch), run() continues.
+// One GEMM work item: NB n-blocks (16 columns each) x all KB k-blocks.  Wave w owns the contiguous k-blocks
+// [w KB / 8, (w + 1) KB / 8) (balanced to one k-block for any KB) and streams them in chunks of U k-blocks with a
+// two-deep register pipeline.  load_w() issues the first two chunks' weights (the prefetch), run() continues.
+// Chunks past the wave's range re-read its last k-block (an L2 hit) and are masked.
+// (A D-deep register ring was measured slower: 7B b32 110 -> 123 us per block, scripts/bench_decode_block.py.)
 // ------------------------------------------------------------------------------------------------------------
 template <int MT, int NB, int U>
 struct GemmItem {
   const uint4* wp[NB];
-  int KB, nch, n_it, last_c;
+  int kb0, kb1, n_it;
   uint4 wA[U][NB], wB[U][NB];
 
-  __device__ __forceinline__ void setup(const uint4* W, int kb_total, int nb0, int w, int lane) {
+  __device__ __forceinline__ void setup(const uint4* W, int KB, int nb0, int w, int lane) {
 #pragma unroll
-    for (int i = 0; i < NB; ++i) wp[i] = W + (size_t)(nb0 + i) * kb_total * 64 + lane;
-    KB = kb_total;
-    nch = (KB + U - 1) / U;
-    n_it = nch > w ? (nch - w + DB_WAVES - 1) / DB_WAVES : 0;
-    last_c = w + DB_WAVES * (n_it - 1);
+    for (int i = 0; i < NB; ++i) wp[i] = W + (size_t)(nb0 + i) * KB * 64 + lane;
+    kb0 = (w * KB) / DB_WAVES;
+    kb1 = ((w + 1) * KB) / DB_WAVES;
+    n_it = (kb1 - kb0 + U - 1) / U;
   }
+  __device__ __forceinline__ int kblk(int c, int u) const { return min(kb0 + c * U + u, kb1 - 1); }
   __device__ __forceinline__ void wload(uint4 (&wr)[U][NB], int c) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int kk = min(c * U + u, KB - 1);
+      const int kk = kblk(c, u);
 #pragma unroll
       for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
     }
   }
-  __device__ __forceinline__ void load_w(int w) {
-    if (n_it > 0) wload(wA, w);
-    if (n_it > 1) wload(wB, w + DB_WAVES);
+  __device__ __forceinline__ void load_w(int) {
+    if (n_it > 0) wload(wA, 0);
+    if (n_it > 1) wload(wB, 1);
   }
   // activations: xf layout, sc1 loads (handed off inside the launch)
   __device__ __forceinline__ void xload(uint4 (&xr)[U][MT], __amdgpu_buffer_rsrc_t xr_rs, int c, int lane) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int kk = min(c * U + u, KB - 1);
+      const int kk = kblk(c, u);
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         const u32x4_t v = ld_sc1(xr_rs, (uint32_t)((((size_t)kk * MT + j) * 64 + lane) * 16));
@@ -169,7 +177,7 @@ struct GemmItem {
   __device__ __forceinline__ void comp(f32x4_t (&acc)[NB][MT], const uint4 (&wr)[U][NB], const uint4 (&xr)[U][MT], int c) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool live = (c * U + u) < KB;
+      const bool live = kb0 + c * U + u < kb1;
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         uint4 xv = xr[u][j];
@@ -179,30 +187,30 @@ struct GemmItem {
       }
     }
   }
-  __device__ __forceinline__ void run(f32x4_t (&acc)[NB][MT], __amdgpu_buffer_rsrc_t xr_rs, int w, int lane) {
+  __device__ __forceinline__ void run(f32x4_t (&acc)[NB][MT], __amdgpu_buffer_rsrc_t xr_rs, int, int lane) {
 #pragma unroll
     for (int i = 0; i < NB; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     if (n_it <= 0) return;
     uint4 xA[U][MT], xB[U][MT];
-    xload(xA, xr_rs, w, lane);
+    xload(xA, xr_rs, 0, lane);
     int i = 0;
     for (; i + 1 < n_it; i += 2) {
-      xload(xB, xr_rs, w + DB_WAVES * (i + 1), lane);
+      xload(xB, xr_rs, i + 1, lane);
       __builtin_amdgcn_sched_barrier(0);
-      comp(acc, wA, xA, w + DB_WAVES * i);
+      comp(acc, wA, xA, i);
       __builtin_amdgcn_sched_barrier(0);
-      const int c2 = min(w + DB_WAVES * (i + 2), last_c);  // clamped: the tail re-reads a cached chunk
+      const int c2 = min(i + 2, n_it - 1);  // clamped: the tail re-reads a cached chunk
       wload(wA, c2);
       xload(xA, xr_rs, c2, lane);
       __builtin_amdgcn_sched_barrier(0);
-      comp(acc, wB, xB, w + DB_WAVES * (i + 1));
+      comp(acc, wB, xB, i + 1);
       __builtin_amdgcn_sched_barrier(0);
-      if (i + 3 < n_it) wload(wB, w + DB_WAVES * (i + 3));
+      if (i + 3 < n_it) wload(wB, i + 3);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (i < n_it) comp(acc, wA, xA, w + DB_WAVES * i);
+    if (i < n_it) comp(acc, wA, xA, i);
   }
 };
 
@@ -275,15 +283,19 @@ __device__ __forceinline__ void residual_epi(const DbArgs& a, const f32x4_t* red
   }
 }
 
+// k-blocks per chunk for MT row tiles x NB n-blocks: as deep as the VGPRs allow without spilling (two chunks of
+// weights + two of activations per wave; one workgroup per CU leaves 256 VGPRs per wave)
+constexpr int db_chunk(int mt, int nb) {
+  return nb == 1 ? (mt == 1 ? 8 : (mt == 2 ? 6 : 4)) : (nb == 2 ? (mt == 4 ? 2 : 4) : (mt == 4 ? 1 : 2));
+}
+
 }  // namespace
 
 // NBx: n-blocks per work item of each phase (NBG counts gate + up blocks: even); MT: 16-row tiles (B <= 16 MT)
 template <int MT, int NBO, int NBG, int NBD, int NBQ>
 __global__ __launch_bounds__(DB_THREADS) void decode_block_kernel(DbArgs a) {
   constexpr int NBMAX = (NBO > NBG ? NBO : NBG) > (NBD > NBQ ? NBD : NBQ) ? (NBO > NBG ? NBO : NBG) : (NBD > NBQ ? NBD : NBQ);
-  // k-blocks per chunk: two chunks in flight per wave = 2 * U * NB KiB of weights; activations 2 * U * MT
-  constexpr int UO = (NBO == 1 && MT <= 2) ? 4 : 2, UG = NBG >= 4 ? 1 : 2;
-  constexpr int UD = (NBD == 1 && MT <= 2) ? 4 : 2, UQ = (NBQ == 1 && MT <= 2) ? 4 : 2;
+  constexpr int UO = db_chunk(MT, NBO), UG = db_chunk(MT, NBG), UD = db_chunk(MT, NBD), UQ = db_chunk(MT, NBQ);
   __shared__ __attribute__((aligned(16))) f32x4_t red[DB_WAVES * NBMAX * MT * 64];
   __shared__ int s_item, s_flag;
   const int lane = threadIdx.x & 63;
@@ -295,25 +307,31 @@ __global__ __launch_bounds__(DB_THREADS) void decode_block_kernel(DbArgs a) {
 
   // ---------------- PO: o projection + residual (ss1)
   int ndone;
+  stamp(a, 0);
   {
     GemmItem<MT, NBO, UO> g;
-    const int it = claim_now(a, 0, &s_item);
+    const int it = blockIdx.x < nO ? (int)blockIdx.x : nO;
+    stamp(a, 1);
     if (it < nO) {
       g.setup(a.wo, KBo, it * NBO, w, lane);
       g.load_w(w);
     }
     ndone = gemm_phase<MT, NBO, UO>(a, 0, nO, a.wo, KBo, rsrc(a.attn), g, it, red, &s_item, w, lane,
                                     [&](int nb0, const f32x4_t* r) { residual_epi<NBO, MT>(a, r, nb0, a.ss1); });
+    stamp(a, 2);
+    stamp(a, 9, ndone);
   }
   // ---------------- PG: gate_up (rows scaled by ss1, SiLU * up -> act); first item's weights before the seam
   {
     GemmItem<MT, NBG, UG> g;
-    const int it = publish_and_claim(a, 0, ndone, 1, &s_item);
+    publish(a, 0, ndone);
+    const int it = blockIdx.x < nG ? (int)blockIdx.x : nG;
     if (it < nG) {
       g.setup(a.wgu, KBg, it * NBG, w, lane);
       g.load_w(w);
     }
     if (!wait_done(a, 0, nO, &s_flag)) return;
+    stamp(a, 3);
     const __amdgpu_buffer_rsrc_t ra = rsrc(a.act);
     ndone = gemm_phase<MT, NBG, UG>(a, 1, nG, a.wgu, KBg, rsrc(a.x), g, it, red, &s_item, w, lane,
                                     [&](int nb0, const f32x4_t* r) {
@@ -331,31 +349,39 @@ __global__ __launch_bounds__(DB_THREADS) void decode_block_kernel(DbArgs a) {
         __builtin_amdgcn_raw_buffer_store_b64(pk, ra, (int)(xf_off(m, n, MT) * 2), 0, DB_SC1);
       }
     });
+    stamp(a, 4);
+    stamp(a, 10, ndone);
   }
   // ---------------- PD: down + residual (ss2)
   {
     GemmItem<MT, NBD, UD> g;
-    const int it = publish_and_claim(a, 1, ndone, 2, &s_item);
+    publish(a, 1, ndone);
+    const int it = blockIdx.x < nD ? (int)blockIdx.x : nD;
     if (it < nD) {
       g.setup(a.wd, KBd, it * NBD, w, lane);
       g.load_w(w);
     }
     if (!wait_done(a, 1, nG, &s_flag)) return;
+    stamp(a, 5);
     ndone = gemm_phase<MT, NBD, UD>(a, 2, nD, a.wd, KBd, rsrc(a.act), g, it, red, &s_item, w, lane,
                                     [&](int nb0, const f32x4_t* r) { residual_epi<NBD, MT>(a, r, nb0, a.ss2); });
+    stamp(a, 6);
+    stamp(a, 11, ndone);
   }
   if (!nQ) return;
   // ---------------- PQ: next layer's qkv (rows scaled by ss2) -> f32 [B][nq] for the fused-RoPE attention
   {
     GemmItem<MT, NBQ, UQ> g;
-    const int it = publish_and_claim(a, 2, ndone, 3, &s_item);
+    publish(a, 2, ndone);
+    const int it = blockIdx.x < nQ ? (int)blockIdx.x : nQ;
     if (it < nQ) {
       g.setup(a.wq, KBq, it * NBQ, w, lane);
       g.load_w(w);
     }
     if (!wait_done(a, 2, nD, &s_flag)) return;
+    stamp(a, 7);
     const __amdgpu_buffer_rsrc_t rq = rsrc(a.qout);
-    gemm_phase<MT, NBQ, UQ>(a, 3, nQ, a.wq, KBq, rsrc(a.x), g, it, red, &s_item, w, lane,
+    ndone = gemm_phase<MT, NBQ, UQ>(a, 3, nQ, a.wq, KBq, rsrc(a.x), g, it, red, &s_item, w, lane,
                             [&](int nb0, const f32x4_t* r) {
       for (int idx = threadIdx.x; idx < NBQ * MT * 64; idx += DB_THREADS) {
         const int l = idx & 63, t = idx >> 6;
@@ -368,25 +394,38 @@ __global__ __launch_bounds__(DB_THREADS) void decode_block_kernel(DbArgs a) {
         __builtin_amdgcn_raw_buffer_store_b128(u, rq, (int)(((size_t)m * a.nq + n) * 4), 0, 0);
       }
     });
+    stamp(a, 8);
+    stamp(a, 12, ndone);
   }
 }
 
 extern "C" int lsa_decode_block_cnt_ints() { return DB_CNT_INTS; }
 
+// co-resident workgroups of a kernel on this device: occupancy per CU x CUs
+static int db_capacity(const void* kernel) {
+  int per_cu = 0, dev = 0, ncu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, DB_THREADS, 0) != hipSuccess) per_cu = 1;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    ncu = 1;
+  return (per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
+}
+
 extern "C" int lsa_decode_block(const void* attn, const void* wo, float* h, void* x, long long* ss1, long long* ss2,
                                 const void* wgu, void* act, const void* wd, const void* wq, float* qout, int B, int d,
                                 int hd, int ffn, int nq, float eps, int* cnt, int* err, long long timeout_ticks,
-                                int nwg, int nbo, int nbg, int nbd, int nbq, hipStream_t s) {
+                                int nwg, int nbo, int nbg, int nbd, int nbq, long long* stamps, hipStream_t s) {
   if (B < 1 || B > 64 || d % 32 || hd % 32 || ffn % 32 || (wq && nq % 16) || nwg < 1) return -1;
   if ((d / 16) % nbo || (2 * ffn / 16) % nbg || nbg % 2 || (d / 16) % nbd || (wq && (nq / 16) % nbq)) return -3;
   const int mt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
   DbArgs a{reinterpret_cast<const uint16_t*>(attn), reinterpret_cast<const uint4*>(wo), h,
            reinterpret_cast<uint16_t*>(x), ss1, ss2, reinterpret_cast<const uint4*>(wgu),
            reinterpret_cast<uint16_t*>(act), reinterpret_cast<const uint4*>(wd), reinterpret_cast<const uint4*>(wq),
-           qout, B, d, hd, ffn, nq, eps, cnt, err, timeout_ticks};
+           qout, B, d, hd, ffn, nq, eps, cnt, err, timeout_ticks, stamps};
 #define DB_L(MTV, O, G, D_, Q)                                                                              \
   if (mt == MTV && nbo == O && nbg == G && nbd == D_ && nbq == Q) {                                          \
-    hipLaunchKernelGGL((decode_block_kernel<MTV, O, G, D_, Q>), dim3(nwg), dim3(DB_THREADS), 0, s, a);       \
+    static const int cap = db_capacity(reinterpret_cast<const void*>(decode_block_kernel<MTV, O, G, D_, Q>)); \
+    hipLaunchKernelGGL((decode_block_kernel<MTV, O, G, D_, Q>), dim3(nwg < cap ? nwg : cap), dim3(DB_THREADS), \
+                       0, s, a);                                                                            \
     return (int)hipGetLastError();                                                                          \
   }
 #define DB_MT(MTV) DB_L(MTV, 1, 2, 1, 1) DB_L(MTV, 1, 2, 1, 2) DB_L(MTV, 2, 2, 2, 2) DB_L(MTV, 1, 4, 1, 1)

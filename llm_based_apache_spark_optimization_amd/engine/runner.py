@@ -353,12 +353,11 @@ class ModelRunner:
         xf = self.use_xfrag(B)
         nqkv = (self.H + 2 * self.Hkv) * self.D
         sk_q = self._splitk(B, d, nqkv, tp_reduced=False, xf=xf)
-        sk_o = self._splitk(B, self.H * self.D, xf=xf)
-        sk_d = self._splitk(B, self.ffn_l, xf=xf)
+        # the residual-epilogue GEMMs run their own tuned split (ops/gemm_tuning.json "res" entries; the
+        # f32 pick where none is tuned)
+        sk_o = ops.pick_gemm_config(B, d, self.H * self.D, "res", xf=xf, kind=w.layers[0].wo.kind)[1]
+        sk_d = ops.pick_gemm_config(B, d, self.ffn_l, "res", xf=xf, kind=w.layers[0].w_down.kind)[1]
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
-        mres = self.mlp_res and not a8m
-        if mres:
-            sk_o = ops.pick_gemm_config(B, d, self.H * self.D, "res", xf=xf, kind=w.layers[0].wo.kind)[1]
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
         plan = plan or ops.decode_split_plan(B, self.Hkv, self.max_model_len)

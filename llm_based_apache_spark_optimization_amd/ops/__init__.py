@@ -405,7 +405,7 @@ def tile_splitk(M: int, N: int, K: int, kind: str = "bf16") -> int:
 # Persistent post-attention decode block (csrc/kernels/decode_block.hip): n-blocks per work item of each phase,
 # (nbo, nbg, nbd, nbq); LSA_DECODE_BLOCK_CFG="nbo,nbg,nbd,nbq" overrides (tuning: scripts/bench_decode_block.py)
 DECODE_BLOCK_DEFAULT = (1, 2, 1, 1)
-DECODE_BLOCK_CNT_INTS = 256  # per-layer claim / done counter block (8 lines of 128 B; kernel's DB_CNT_INTS)
+DECODE_BLOCK_CNT_INTS = 1152  # per-layer claim / done counter block (36 lines of 128 B; kernel's DB_CNT_INTS)
 
 
 def decode_block_cfg(B: int) -> tuple:
@@ -434,13 +434,15 @@ def num_cus(device) -> int:
 
 def decode_block(attn_xf, wo: "PackedWeight", h, x_xf, ss1, ss2, wgu: "PackedWeight", act_xf, wd: "PackedWeight",
                  wq: Optional["PackedWeight"], qout, B: int, eps: float, cnt, err, cfg: Optional[tuple] = None,
-                 timeout_s: float = 2.0, nwg: Optional[int] = None) -> None:
+                 timeout_s: float = 2.0, nwg: Optional[int] = None, stamps=None) -> None:
     """One layer's post-attention block in ONE persistent launch (TP = 1, bf16 weights, B <= 64, fragment-major
     activations): o projection + residual (h += o, x = bf16(h), ss1 += sum h^2) -> gate_up (row-scaled by ss1,
     SiLU * up -> act) -> down + residual (h, x, ss2) -> [next layer's qkv, row-scaled by ss2, into ``qout``
     f32 [B, nq] (a one-slab ``qkv_parts`` for the fused-RoPE attention)].  ``cnt`` (int32,
     >= DECODE_BLOCK_CNT_INTS) must be zero at the launch (the runner zeroes every layer's counters with one memset
-    per step); ss1 / ss2 must be zero."""
+    per step); ss1 / ss2 must be zero.  ``stamps`` (int64 [nwg, 16]): per-workgroup wall-clock stamps of the
+    phase boundaries (0 start, 1 claimed, 2 o done, 3 o complete, 4 gate_up done, 5 complete, 6 down done,
+    7 complete, 8 qkv done; 9-12 items per phase)."""
     nbo, nbg, nbd, nbq = cfg or decode_block_cfg(B)
     d, ffn = wo.N, wd.K
     if not _gpu(h):
@@ -468,7 +470,7 @@ def decode_block(attn_xf, wo: "PackedWeight", h, x_xf, ss1, ss2, wgu: "PackedWei
     ticks = int(timeout_s * ext().ar_wallclock_khz() * 1000)
     ext().decode_block(attn_xf, wo.data, h, x_xf, ss1, ss2, wgu.data, act_xf, wd.data,
                        wq.data if wq is not None else None, qout, B, ffn, wq.N if wq is not None else 0, float(eps),
-                       cnt, err, ticks, nwg or decode_block_grid(B, h.device), nbo, nbg, nbd, nbq)
+                       cnt, err, ticks, nwg or decode_block_grid(B, h.device), nbo, nbg, nbd, nbq, stamps)
 
 
 def xfrag_tiles(M: int) -> int:

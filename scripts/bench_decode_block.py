@@ -2,7 +2,10 @@
 stream's effective bandwidth, over a sweep of tile plans and grid sizes.  Weights rotate over 4 layer copies
 (> MALL) so they stream from HBM.  One JSON line per (shape, B, cfg, nwg).
 
-    python scripts/bench_decode_block.py [Bs] [cfg;cfg..] [nwg,nwg..]
+    python scripts/bench_decode_block.py [Bs] [cfg;cfg..] [nwg,nwg..] [--stamps]
+
+--stamps: also one stamped launch per point (after 3 unstamped ones): per phase boundary the min / median / max
+over workgroups of the wall-clock time since the earliest workgroup start (us).
       cfg = nbo,nbg,nbd,nbq      ("-": ops.decode_block_cfg(B))
 """
 import json
@@ -15,9 +18,12 @@ from llm_based_apache_spark_optimization_amd import ops  # noqa: E402
 
 dev = torch.device("cuda:0")
 SHAPES = {"7b": (4096, 4096, 11008, 12288), "3b": (3072, 3072, 8192, 5120)}
-Bs = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 8, 32, 64]
-CFGS = [tuple(int(x) for x in c.split(",")) for c in sys.argv[2].split(";")] if len(sys.argv) > 2 and sys.argv[2] != "-" else [None]
-NWGS = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]
+_pos = [a for a in sys.argv[1:] if not a.startswith("--")]
+Bs = [int(v) for v in _pos[0].split(",")] if len(_pos) > 0 else [1, 8, 32, 64]
+CFGS = [tuple(int(x) for x in c.split(",")) for c in _pos[1].split(";")] if len(_pos) > 1 and _pos[1] != "-" else [None]
+NWGS = [int(v) for v in _pos[2].split(",")] if len(_pos) > 2 else [0]
+STAMPS = "--stamps" in sys.argv
+NAMES = ["start", "claimed", "o_done", "o_complete", "gu_done", "gu_complete", "down_done", "down_complete", "qkv_done"]
 
 
 def main():
@@ -67,6 +73,24 @@ def main():
                                "TBps": round(wbytes / us / 1e6, 2), "err": int(err[0])}
                     except Exception as e:  # noqa: BLE001 - an unsupported plan is a result, not a crash
                         rec = {"shape": name, "B": B, "cfg": list(c), "nwg": n, "error": str(e)[:200]}
+                    if STAMPS and "us" in rec:
+                        st = torch.zeros(n, 16, device=dev, dtype=torch.long)
+                        cnt.zero_(); ss.zero_()
+                        for i in range(3):
+                            run(i)
+                        wo, wgu, wd, wq = layers[3]
+                        ops.decode_block(attn, wo, h, x, ss[0], ss[1], wgu, act, wd, wq, qout, B, 1e-5, cnt[3], err,
+                                         cfg=c, nwg=n, stamps=st)
+                        torch.cuda.synchronize()
+                        st = st.cpu()
+                        st = st[st[:, 0] > 0]  # the launcher clamps the grid to the co-resident capacity
+                        khz = ops.ext().ar_wallclock_khz()
+                        t0 = int(st[:, 0].min())
+                        us = (st[:, :9] - t0).double() * 1000.0 / khz
+                        rec["stamps_us"] = {k: [round(float(us[:, i].min()), 1), round(float(us[:, i].median()), 1),
+                                                round(float(us[:, i].max()), 1)] for i, k in enumerate(NAMES)}
+                        rec["items"] = {k: [int(st[:, 9 + i].min()), int(st[:, 9 + i].max())]
+                                        for i, k in enumerate(["o", "gu", "down", "qkv"])}
                     print(json.dumps(rec), flush=True)
                     if int(err[0]):
                         return

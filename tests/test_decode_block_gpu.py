@@ -95,7 +95,7 @@ def test_decode_block_reproducible(gpu):
     for nwg in (1, None, 300):
         b = _bufs(32, gpu, 4)
         _run(b, wg, 32, nwg=nwg)
-        outs.append((b["h"].clone(), b["ss2"].clone(), b["qout"].clone()))
+        outs.append((b["h"].clone(), b["ss2"].clone(), _q(b, 32).clone()))
     for o in outs[1:]:
         assert all(torch.equal(a, c) for a, c in zip(outs[0], o))
 
