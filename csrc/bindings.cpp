@@ -80,7 +80,7 @@ int lsa_decode_block_cnt_ints();
 int lsa_decode_block(const void* attn, const void* wo, float* h, void* x, long long* ss1, long long* ss2, const void* wgu,
                      void* act, const void* wd, const void* wq, float* qout, int B, int d, int hd, int ffn, int nq,
                      float eps, int* cnt, int* err, long long timeout_ticks, int nwg, int nbo, int nbg, int nbd, int nbq,
-                     long long* stamps, hipStream_t s);
+                     int cw, long long* stamps, hipStream_t s);
 }
 
 namespace {
@@ -628,7 +628,8 @@ void decode_block(const at::Tensor& attn, const at::Tensor& wo, at::Tensor& h, a
                   at::Tensor& ss2, const at::Tensor& wgu, at::Tensor& act, const at::Tensor& wd,
                   const c10::optional<at::Tensor>& wq, const c10::optional<at::Tensor>& qout, int64_t B, int64_t ffn,
                   int64_t nq, double eps, at::Tensor& cnt, at::Tensor& err, int64_t timeout_ticks, int64_t nwg,
-                  int64_t nbo, int64_t nbg, int64_t nbd, int64_t nbq, const c10::optional<at::Tensor>& stamps) {
+                  int64_t nbo, int64_t nbg, int64_t nbd, int64_t nbq, int64_t cw,
+                  const c10::optional<at::Tensor>& stamps) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&attn, &wo, &x, &wgu, &act, &wd})
     need(*t, at::kBFloat16, "decode_block bf16 operand");
   need(h, at::kFloat, "h");
@@ -647,6 +648,7 @@ void decode_block(const at::Tensor& attn, const at::Tensor& wo, at::Tensor& h, a
   TORCH_CHECK(ss1.numel() >= B && ss2.numel() >= B && err.numel() >= 1, "decode_block: row sums / err too small");
   TORCH_CHECK(cnt.is_contiguous() && cnt.numel() >= lsa_decode_block_cnt_ints(), "decode_block: counter block too small");
   TORCH_CHECK(nwg >= 1 && nwg <= 65536, "decode_block: 1..65536 workgroups");
+  TORCH_CHECK(cw == 4 || cw == 8, "decode_block: 4 or 8 consumer waves");
   if (wq.has_value()) {
     need(*wq, at::kBFloat16, "wq");
     TORCH_CHECK(qout.has_value(), "next-layer qkv needs its output buffer");
@@ -663,7 +665,7 @@ void decode_block(const at::Tensor& attn, const at::Tensor& wo, at::Tensor& h, a
                          wd.data_ptr(), wq.has_value() ? wq->data_ptr() : nullptr,
                          wq.has_value() ? qout->data_ptr<float>() : nullptr, B, d, hd, ffn, wq.has_value() ? nq : 0,
                          (float)eps, cnt.data_ptr<int>(), err.data_ptr<int>(), timeout_ticks, nwg, nbo, nbg, nbd, nbq,
-                         stamps.has_value() ? reinterpret_cast<long long*>(stamps->data_ptr<int64_t>()) : nullptr,
+                         (int)cw, stamps.has_value() ? reinterpret_cast<long long*>(stamps->data_ptr<int64_t>()) : nullptr,
                          cur_stream()),
         "decode_block");
 }
@@ -728,7 +730,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_block", &decode_block, py::arg("attn"), py::arg("wo"), py::arg("h"), py::arg("x"), py::arg("ss1"),
         py::arg("ss2"), py::arg("wgu"), py::arg("act"), py::arg("wd"), py::arg("wq"), py::arg("qout"), py::arg("B"),
         py::arg("ffn"), py::arg("nq"), py::arg("eps"), py::arg("cnt"), py::arg("err"), py::arg("timeout_ticks"),
-        py::arg("nwg"), py::arg("nbo"), py::arg("nbg"), py::arg("nbd"), py::arg("nbq"), py::arg("stamps") = py::none());
+        py::arg("nwg"), py::arg("nbo"), py::arg("nbg"), py::arg("nbd"), py::arg("nbq"), py::arg("cw") = 4,
+        py::arg("stamps") = py::none());
   m.def("decode_block_cnt_ints", []() { return lsa_decode_block_cnt_ints(); });
   m.def("ar_alloc", &ar_alloc);
   m.def("ar_free", [](int64_t p) { check(lsa_ar_free(reinterpret_cast<void*>(p)), "ar_free"); });

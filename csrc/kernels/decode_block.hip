@@ -1,4 +1,5 @@
-// Persistent post-attention decode block (TP = 1, decode batch <= 64, fragment-major activations), gfx950.
+// Persistent post-attention decode block on an LDS-DMA weight ring (TP = 1, decode batch <= 64,
+// fragment-major activations), gfx950.
 //
 // ONE launch per layer runs, in order,
 //   PO  o projection + residual   attn (xf) @ Wo: h += o; x = bf16(h) (xf); ss1[m] += sum h^2
@@ -8,44 +9,62 @@
 // in place of six launches (o GEMM, add_rmsnorm, gate_up, down, add_rmsnorm, next qkv); the RMSNorm gammas are
 // folded into Wgu / Wqkv at load time (models/llama.py), so a norm is a row scale in the consumer's epilogue.
 //
-// Why one launch: at decode batch <= 64 each projection is a 2-30 us weight stream that pays ~2-3 us of launch
-// boundary, ramp-up and tail (profiles/roofline_b32_decode.md).  Here the weight stream runs through the seams:
-//   * every work item is a group of NB 16-column n-blocks over the FULL k range (no split-K: o and down finish
-//     their columns' residual in the epilogue, no slab round trip, no residual phase);
-//   * workgroup i owns item i of every phase (no claim at a seam); the remaining items are claimed dynamically,
-//     a workgroup claiming its NEXT item while computing the current one (the round trip hides behind the
-//     k-loop) and issuing the next item's first weight chunks before the current item's epilogue;
-//   * at a phase seam it issues its first item of the next phase's weights BEFORE it waits for the current phase
-//     to complete (weights never depend on activations: MI355X_MICROARCH.md 'prefetch-credit');
-//   * a workgroup publishes its phase work once (one add of its item count to its XCD's done slot), not per item.
-//
+// Engine (MI355X_MICROARCH.md price list: ldsdma-fill, prefetch-credit, ring-gemm; one workgroup per CU):
+//   * ONE loader wave per CU streams this CU's weights for ALL four phases, in consumption order, into a ring of
+//     DB_RING 16 KiB LDS slots with global_load_lds (nt: read once per step), DB_INFLIGHT slots in flight, and
+//     publishes a slot (an LDS FULL word) behind a counted vmcnt.  Weights never depend on activations, so the
+//     loader never waits for a phase hand-off: while this CU's consumers wait for the previous phase to complete
+//     on every CU, its loader keeps filling the ring with the next phase's weights (the seam is hidden behind the
+//     ring's ~5 us of stream).  It only waits for ring slots its consumers have not released yet (FREE words).
+//   * C consumer waves split every slot's k-blocks (wave c takes k-blocks c, c + C, ..): per k-block one
+//     ds_read_b128 per n-block, then the slot is released, then MT MFMA 16x16x32 per n-block against the
+//     activation fragments the wave prefetched from L2 (sc1 loads) one slot ahead.  Partial sums of the C waves
+//     meet in LDS at the end of each work item for the epilogue.
+//   * Work is assigned statically: workgroup i owns items i, i + grid, .. of every phase (an item = NB 16-column
+//     n-blocks over the full k range), so loader and consumers walk the same schedule with no claims.
+//   * Phase hand-off (MI355X_MICROARCH.md 'Valid forms' row 1): every byte another workgroup reads inside the
+//     launch (h, the bf16 activations x / act) is stored write-through (sc1) and loaded with sc1 loads; each
+//     consumer wave drains its stores (s_waitcnt vmcnt(0)) and adds to an LDS counter, the wave whose add is last
+//     adds the workgroup's item count to its XCD's done slot (agent scope); consumer wave 0 polls the 8 slots
+//     (relaxed agent loads, s_sleep between polls) and then sets an LDS word the other consumer waves wait for.
+//   * No __syncthreads after the prologue (the loader runs ahead of every consumer barrier): consumer waves meet
+//     through LDS counters.  The loader's own LDS traffic is inline asm, so the compiler never drains its
+//     LDS-DMA queue (vmcnt(0)) in front of a flag access.
 // The grid is clamped to the co-resident capacity (occupancy x CUs), so every statically owned item belongs to a
 // workgroup that is resident, or becomes resident as soon as another stream's kernels drain (they never wait on
-// this one): no grid barrier, no deadlock.  Every wait is bounded: on timeout the kernel sets *err and returns.
+// this one): no grid barrier, no deadlock.  Every wait is bounded: on timeout the kernel sets *err, raises an LDS
+// abort word that releases the other waves, and returns.  Row sums of squares are int64 Q24 agent-scope atomics
+// (exact and order-independent: batched decoding stays bit-reproducible; every item reduces its k range in a
+// fixed order whichever workgroup runs it).
 //
-// Hand-offs follow MI355X_MICROARCH.md 'Valid forms' row 1: every byte another workgroup reads inside the launch
-// (h, the bf16 activations x / act) is stored write-through (sc1) and loaded with sc1 loads; each storing wave
-// drains its stores (s_waitcnt vmcnt(0)), the workgroup barrier follows, then one lane adds to the phase's done
-// counter (agent scope); a consumer polls that counter from one lane (relaxed agent loads, s_sleep between
-// polls), then joins a workgroup barrier before any wave loads.  Claim and done counters sit on their own 128-B
-// lines.  Row sums of squares are int64 Q24 agent-scope atomics (exact and order-independent, as in the
-// residual GEMM epilogue: batched decoding stays bit-reproducible; every item reduces its k range in a fixed
-// order whichever workgroup runs it).
+// Measured on MI355X (profiles/r3/decode_block_ring_mi355x.jsonl, scripts/bench_decode_block.py --stamps): 7B per
+// block 86.8 us at batch 1 and 105 us at batch 32 (the register-streaming v2 with dynamic claims: 98 / 111 us), i.e.
+// still slower than the launch chain it replaces (bench 7B b32 7,089 vs 8,103 tok/s), so it stays opt-in
+// (LSA_DECODE_BLOCK=1).  The stamps say why: every in-launch phase hand-off costs 4-6 us after the last
+// producer's item (store drain ~2 us under the weight stream + counter + poll), more than the ring's ~4.5 us of
+// prefetch credit, and gate_up's 688 items leave a third of the CUs one item (~10 us) short; a kernel boundary
+// costs ~1.7 us.  Pausing the loader during the poll did not shorten the hand-off (86.8 vs 87.6 us).
 #include "common.h"
 
-#define DB_THREADS 512
-#define DB_WAVES 8
-#define DB_SC1 16   // buffer aux: sc1 (write-through store / L1-bypassing load)
-#define DB_LINE 32  // ints per counter line (128 B)
-#define DB_SLOTS 8  // done counters per phase: one per XCD (workgroup i runs on XCD i % 8)
-// per-layer counter block, one 128-B line each: phase p's claim counter at line 9p, its done slots at lines
-// 9p + 1 .. 9p + 8
+#ifndef DB_RING
+#define DB_RING 7       // 16 KiB weight slots (the guide: >= 3 more than the slots in flight)
+#endif
+#ifndef DB_HOLD
+#define DB_HOLD 1       // pause the loader while consumer wave 0 polls a phase hand-off
+#endif
+#define DB_INFLIGHT 3   // slots the loader keeps in flight: 48 LDS-DMA ops <= the 63 vmcnt can count
+#define DB_SC1 16       // buffer aux: sc1 (write-through store / L1-bypassing load)
+#define DB_NT 2         // LDS-DMA aux: nt (weights streamed once per step)
+#define DB_LINE 32      // ints per counter line (128 B)
+#define DB_SLOTS 8      // done counters per phase: one per XCD (workgroup i runs on XCD i % 8)
+// per-layer counter block, one 128-B line each: phase p's done slots at lines 9p + 1 .. 9p + 8 (line 9p unused)
 #define DB_CNT_INTS (4 * (1 + DB_SLOTS) * DB_LINE)
 
 namespace {
 
 typedef __attribute__((address_space(1))) int db_g_i32;
 typedef __attribute__((address_space(1))) long long db_g_i64;
+typedef __attribute__((address_space(3))) void* db_lds_t;
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 struct DbArgs {
@@ -68,56 +87,76 @@ struct DbArgs {
   long long* stamps;     // optional [nwg][16] wall-clock stamps of the phase boundaries (scripts/bench_decode_block.py)
 };
 
+// LDS control words (zeroed in the prologue)
+struct DbCtl {
+  int full[DB_RING];   // slot r holds its (full[r])-th use: the loader's publication
+  int free_[DB_RING];  // consumer releases of slot r (C per use)
+  int cb;              // consumer barrier arrivals (2 per consumer wave per work item)
+  int pub;             // consumer waves done with their phase's stores
+  int ready;           // phases handed off (set by consumer wave 0 after its poll)
+  int hold;            // consumer wave 0 polls a hand-off: the loader keeps its DMA queue empty meanwhile
+  int abort;           // a bounded wait timed out: every wave returns
+};
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(db_lds_t)p; }
+// LDS flag accesses as inline asm: invisible to the waitcnt pass, so no vmcnt(0) drain of the LDS-DMA queue
+__device__ __forceinline__ int lds_ld(const int* p) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ void lds_st(int* p, int v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_inc1(int* p, int lane) {  // one lane adds 1
+  if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(lds_addr(p)), "v"(1) : "memory");
+}
+
+// one 1 KiB wave-instruction of LDS-DMA (16 B per lane, nt); a non-template wrapper (the builtin inside a
+// template trips hipcc's host pass)
+__device__ __forceinline__ void glds_nt(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds(g, (db_lds_t)l, 16, 0, DB_NT);
+}
+
 __device__ __forceinline__ u32x4_t ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, DB_SC1);
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
 }
-__device__ __forceinline__ db_g_i32* claim_ctr(const DbArgs& a, int p) {
-  return (db_g_i32*)a.cnt + p * (1 + DB_SLOTS) * DB_LINE;
-}
 __device__ __forceinline__ db_g_i32* done_ctr(const DbArgs& a, int p, int slot) {
   return (db_g_i32*)a.cnt + (p * (1 + DB_SLOTS) + 1 + slot) * DB_LINE;
 }
-// dynamic items start after the static ones: workgroup i owns item i of every phase, the rest are claimed
-__device__ __forceinline__ int claim_issue(const DbArgs& a, int p) {
-  return (int)gridDim.x + __hip_atomic_fetch_add(claim_ctr(a, p), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
-// end of phase p: every storing wave drains its write-through stores, then one lane adds the workgroup's item
-// count to its XCD's done slot (8 slots: no 256-way same-address atomic storm at a seam)
-__device__ __forceinline__ void publish(const DbArgs& a, int p, int ndone) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0 && ndone)
-    __hip_atomic_fetch_add(done_ctr(a, p, blockIdx.x % DB_SLOTS), ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// wait until phase p has n items done (bounded); false on timeout (err set).  Lanes 0-7 of wave 0 poll one slot
-// each; the sum is broadcast from lane 0 so the loop stays wave-uniform.
-__device__ __forceinline__ bool wait_done(const DbArgs& a, int p, int n, int* s_flag) {
-  if (threadIdx.x < 64) {
-    const int l = threadIdx.x;
-    int ok = 1;
-    const long long t0 = wall_clock64();
-    while (true) {
-      int v = l < DB_SLOTS ? __hip_atomic_load(done_ctr(a, p, l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      if (__shfl(v, 0, 64) >= n) break;
-      __builtin_amdgcn_s_sleep(2);
-      if (wall_clock64() - t0 > a.timeout_ticks) {
-        if (l == 0) __hip_atomic_store((db_g_i32*)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
+// bounded LDS spin until *p >= v; false (abort raised, err set) on timeout or when another wave aborted
+__device__ __forceinline__ bool spin_ge(const DbArgs& a, DbCtl* ctl, const int* p, int v) {
+  if (lds_ld(p) >= v) return true;
+  const long long t0 = wall_clock64();
+  while (true) {
+    __builtin_amdgcn_s_sleep(1);
+    if (lds_ld(p) >= v) return true;
+    if (lds_ld(&ctl->abort)) return false;
+    if (wall_clock64() - t0 > a.timeout_ticks) {
+      __hip_atomic_store((db_g_i32*)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lds_st(&ctl->abort, 1);
+      return false;
     }
-    if (l == 0) *s_flag = ok;
   }
-  __syncthreads();
-  return *s_flag != 0;
+}
+
+// bounded LDS spin until *p == 0
+__device__ __forceinline__ bool spin_le0(const DbArgs& a, DbCtl* ctl, const int* p) {
+  const long long t0 = wall_clock64();
+  while (lds_ld(p) > 0) {
+    __builtin_amdgcn_s_sleep(1);
+    if (lds_ld(&ctl->abort)) return false;
+    if (wall_clock64() - t0 > a.timeout_ticks) {
+      __hip_atomic_store((db_g_i32*)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lds_st(&ctl->abort, 1);
+      return false;
+    }
+  }
+  return true;
 }
 
 __device__ __forceinline__ void stamp(const DbArgs& a, int k, long long v = -1) {
@@ -130,141 +169,174 @@ __device__ __forceinline__ float row_scale(const long long* ss, int m, float inv
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// One GEMM work item: NB n-blocks (16 columns each) x all KB k-blocks.  Wave w owns the contiguous k-blocks
-// [w KB / 8, (w + 1) KB / 8) (balanced to one k-block for any KB) and streams them in chunks of U k-blocks with a
-// two-deep register pipeline.  load_w() issues the first two chunks' weights (the prefetch), run() continues.
-// Chunks past the wave's range re-read its last k-block (an L2 hit) and are masked.
-// (A D-deep register ring was measured slower: 7B b32 110 -> 123 us per block, scripts/bench_decode_block.py.)
+// Loader: this workgroup's items of one phase, slot by slot.  Slot = NB n-blocks x KS = 16 / NB k-blocks, 16
+// fragments of 1 KiB in [n-block][k-block] order; k-blocks past KB re-read the last one (an L2 hit; the
+// consumers mask them).  q counts slots over the whole launch, pub the published ones.
+// (Measured and not kept, scripts/bench_decode_block.py, 7B batch 1: one flat schedule over all phases with
+// division-free cursors 87.6 -> 102.7 us per block; the same plus 4-byte "touch" reads of the next 8 slots into
+// L2 / Infinity Cache while the ring is full 110.9 us -- the touches queue in front of the hand-off polls.)
 // ------------------------------------------------------------------------------------------------------------
-template <int MT, int NB, int U>
-struct GemmItem {
-  const uint4* wp[NB];
-  int kb0, kb1, n_it;
-  uint4 wA[U][NB], wB[U][NB];
-
-  __device__ __forceinline__ void setup(const uint4* W, int KB, int nb0, int w, int lane) {
+template <int NB, int C>
+__device__ __forceinline__ bool db_load_phase(const DbArgs& a, DbCtl* ctl, uint4* ring, const uint4* W, int KB,
+                                              int n_items, int& q, int& pub, int lane) {
+  constexpr int KS = 16 / NB;
+  const int nsl = (KB + KS - 1) / KS;
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const uint4* wi[NB];
 #pragma unroll
-    for (int i = 0; i < NB; ++i) wp[i] = W + (size_t)(nb0 + i) * KB * 64 + lane;
-    kb0 = (w * KB) / DB_WAVES;
-    kb1 = ((w + 1) * KB) / DB_WAVES;
-    n_it = (kb1 - kb0 + U - 1) / U;
-  }
-  __device__ __forceinline__ int kblk(int c, int u) const { return min(kb0 + c * U + u, kb1 - 1); }
-  __device__ __forceinline__ void wload(uint4 (&wr)[U][NB], int c) {
+    for (int i = 0; i < NB; ++i) wi[i] = W + (size_t)(item * NB + i) * KB * 64 + lane;
+    for (int s = 0; s < nsl; ++s, ++q) {
+      const int r = q % DB_RING;
+      if (q - pub >= DB_INFLIGHT) {  // the oldest slot in flight has landed once <= DB_INFLIGHT - 1 remain
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        lds_st(&ctl->full[pub % DB_RING], pub / DB_RING + 1);
+        ++pub;
+      }
+      if (q >= DB_RING) {
+        const int need = (q / DB_RING) * C;  // every consumer released the slot's previous use
+        if (lds_ld(&ctl->free_[r]) < need) {
+          // the consumers are behind: publish everything in flight, then wait for the slot
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          for (; pub < q; ++pub) lds_st(&ctl->full[pub % DB_RING], pub / DB_RING + 1);
+          if (!spin_ge(a, ctl, &ctl->free_[r], need)) return false;
+        }
+      }
+#if DB_HOLD
+      if (lds_ld(&ctl->hold)) {
+        // a hand-off poll is in flight on this CU: its loads (and the activation loads right after it) would
+        // queue behind this wave's LDS-DMA (MI355X_MICROARCH.md gather-pass / handoff-1to1), so drain and pause
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (; pub < q; ++pub) lds_st(&ctl->full[pub % DB_RING], pub / DB_RING + 1);
+        if (!spin_le0(a, ctl, &ctl->hold)) return false;
+      }
+#endif
+      uint4* dst = ring + r * 1024;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = kblk(c, u);
-#pragma unroll
-      for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
-    }
-  }
-  __device__ __forceinline__ void load_w(int) {
-    if (n_it > 0) wload(wA, 0);
-    if (n_it > 1) wload(wB, 1);
-  }
-  // activations: xf layout, sc1 loads (handed off inside the launch)
-  __device__ __forceinline__ void xload(uint4 (&xr)[U][MT], __amdgpu_buffer_rsrc_t xr_rs, int c, int lane) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = kblk(c, u);
-#pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const u32x4_t v = ld_sc1(xr_rs, (uint32_t)((((size_t)kk * MT + j) * 64 + lane) * 16));
-        xr[u][j] = make_uint4(v[0], v[1], v[2], v[3]);
+      for (int f = 0; f < 16; ++f) {
+        const int i = f / KS, kk = f % KS;
+        const int kb = min(s * KS + kk, KB - 1);
+        glds_nt(wi[i] + (size_t)kb * 64, dst + f * 64);
       }
     }
   }
-  __device__ __forceinline__ void comp(f32x4_t (&acc)[NB][MT], const uint4 (&wr)[U][NB], const uint4 (&xr)[U][MT], int c) {
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Consumers: this workgroup's items of one phase.  Wave c (of C) reads fragments (i, c + C kw) of every slot
+// (KW = KS / C k-blocks x NB n-blocks), prefetches the next slot's activation fragments (sc1, L2) one slot ahead,
+// and at the end of an item the C partial accumulators meet in LDS (red) for the epilogue epi(nb0, red).
+// e counts items over the launch (consumer-barrier generations).  Returns false on abort.
+// ------------------------------------------------------------------------------------------------------------
+template <int MT, int NB, int C, typename Epi>
+__device__ __forceinline__ bool db_consume_phase(const DbArgs& a, DbCtl* ctl, const uint4* ring, f32x4_t* red,
+                                                 const void* xin, int KB, int n_items, int& q, int& e, int& ndone,
+                                                 int c, int lane, Epi epi) {
+  constexpr int KS = 16 / NB, KW = KS / C;
+  static_assert(KW >= 1 && KS % C == 0, "a slot's k-blocks split evenly over the consumer waves");
+  const int nsl = (KB + KS - 1) / KS;
+  const __amdgpu_buffer_rsrc_t rx = rsrc(xin);
+  auto xload = [&](uint4 (&xr)[KW][MT], int s) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool live = kb0 + c * U + u < kb1;
+    for (int kw = 0; kw < KW; ++kw) {
+      const int kb = min(s * KS + kw * C + c, KB - 1);  // masked at use (a select here would wait for the load)
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
-        uint4 xv = xr[u][j];
+        const u32x4_t v = ld_sc1(rx, (uint32_t)((((size_t)kb * MT + j) * 64 + lane) * 16));
+        xr[kw][j] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+  auto step = [&](f32x4_t (&acc)[NB][MT], const uint4 (&xr)[KW][MT], int s) -> bool {
+    const int r = q % DB_RING;
+    if (!spin_ge(a, ctl, &ctl->full[r], q / DB_RING + 1)) return false;
+    const uint4* slot = ring + r * 1024;
+    uint4 w[NB][KW];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int kw = 0; kw < KW; ++kw) w[i][kw] = slot[(i * KS + kw * C + c) * 64 + lane];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_inc1(&ctl->free_[r], lane);  // the slot's fragments are in registers: the loader may refill it
+    ++q;
+#pragma unroll
+    for (int kw = 0; kw < KW; ++kw) {
+      const bool live = s * KS + kw * C + c < KB;
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        uint4 xv = xr[kw][j];
         xv.x = live ? xv.x : 0u; xv.y = live ? xv.y : 0u; xv.z = live ? xv.z : 0u; xv.w = live ? xv.w : 0u;
 #pragma unroll
-        for (int i = 0; i < NB; ++i) acc[i][j] = mfma16x16x32(wr[u][i], xv, acc[i][j]);
+        for (int i = 0; i < NB; ++i) acc[i][j] = mfma16x16x32(w[i][kw], xv, acc[i][j]);
       }
     }
-  }
-  __device__ __forceinline__ void run(f32x4_t (&acc)[NB][MT], __amdgpu_buffer_rsrc_t xr_rs, int, int lane) {
+    return true;
+  };
+
+  uint4 xa[KW][MT], xb[KW][MT];
+  bool first = true;
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+    f32x4_t acc[NB][MT];
 #pragma unroll
     for (int i = 0; i < NB; ++i)
 #pragma unroll
       for (int j = 0; j < MT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    if (n_it <= 0) return;
-    uint4 xA[U][MT], xB[U][MT];
-    xload(xA, xr_rs, 0, lane);
-    int i = 0;
-    for (; i + 1 < n_it; i += 2) {
-      xload(xB, xr_rs, i + 1, lane);
-      __builtin_amdgcn_sched_barrier(0);
-      comp(acc, wA, xA, i);
-      __builtin_amdgcn_sched_barrier(0);
-      const int c2 = min(i + 2, n_it - 1);  // clamped: the tail re-reads a cached chunk
-      wload(wA, c2);
-      xload(xA, xr_rs, c2, lane);
-      __builtin_amdgcn_sched_barrier(0);
-      comp(acc, wB, xB, i + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      if (i + 3 < n_it) wload(wB, i + 3);
-      __builtin_amdgcn_sched_barrier(0);
+    if (first) xload(xa, 0);
+    first = false;
+    const bool more = item + (int)gridDim.x < n_items;  // the next item starts at slot 0 (the same k-blocks)
+    int s = 0;
+    for (; s + 1 < nsl; s += 2) {
+      xload(xb, s + 1);
+      if (!step(acc, xa, s)) return false;
+      if (s + 2 < nsl || more) xload(xa, s + 2 < nsl ? s + 2 : 0);
+      if (!step(acc, xb, s + 1)) return false;
     }
-    if (i < n_it) comp(acc, wA, xA, i);
-  }
-};
-
-template <int NB, int MT>
-__device__ __forceinline__ f32x4_t lds_sum(const f32x4_t* red, int t, int l) {
-  f32x4_t s = red[t * 64 + l];
+    if (s < nsl) {  // odd slot count: the tail runs from xa, the next item's first slot lands in xb
+      if (more) xload(xb, 0);
+      if (!step(acc, xa, s)) return false;
 #pragma unroll
-  for (int ww = 1; ww < DB_WAVES; ++ww) s += red[(ww * NB * MT + t) * 64 + l];
-  return s;
-}
-
-// One GEMM phase: run items until the claim counter is exhausted.  `item` is this workgroup's first item (its
-// weights already issued by g.load_w); returns the number of items this workgroup completed.
-template <int MT, int NB, int U, typename Epi>
-__device__ __forceinline__ int gemm_phase(const DbArgs& a, int p, int n, const uint4* W, int KB,
-                                          __amdgpu_buffer_rsrc_t xr, GemmItem<MT, NB, U>& g, int item,
-                                          f32x4_t* red, int* s_item, int w, int lane, Epi epi) {
-  int done = 0;
-  while (item < n) {
-    int tk = 0;
-    if (threadIdx.x == 0) tk = claim_issue(a, p);  // next item: the round trip hides behind the k-loop
-    f32x4_t acc[NB][MT];
-    g.run(acc, xr, w, lane);
-    __syncthreads();  // the previous item's epilogue is done reading red
+      for (int kw = 0; kw < KW; ++kw)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) xa[kw][j] = xb[kw][j];
+    }
+    // partial sums -> LDS once every consumer is done reading the previous item's (barrier generation 2e)
+    if (e > 0 && !spin_ge(a, ctl, &ctl->cb, 2 * C * e)) return false;
 #pragma unroll
     for (int i = 0; i < NB; ++i)
 #pragma unroll
-      for (int j = 0; j < MT; ++j) red[((w * NB + i) * MT + j) * 64 + lane] = acc[i][j];
-    if (threadIdx.x == 0) *s_item = tk;
-    __syncthreads();
-    const int nxt = *s_item;
-    if (nxt < n) {  // the next item's weights stream while this one's epilogue runs
-      g.setup(W, KB, nxt * NB, w, lane);
-      g.load_w(w);
-    }
+      for (int j = 0; j < MT; ++j) red[((c * NB + i) * MT + j) * 64 + lane] = acc[i][j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_inc1(&ctl->cb, lane);
+    if (!spin_ge(a, ctl, &ctl->cb, 2 * C * e + C)) return false;
     epi(item * NB, red);
-    ++done;
-    item = nxt;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_inc1(&ctl->cb, lane);
+    ++e;
+    ++ndone;
   }
-  return done;
+  return true;
+}
+
+template <int NB, int MT, int C>
+__device__ __forceinline__ f32x4_t lds_sum(const f32x4_t* red, int t, int l) {
+  f32x4_t s = red[t * 64 + l];
+#pragma unroll
+  for (int ww = 1; ww < C; ++ww) s += red[(ww * NB * MT + t) * 64 + l];
+  return s;
 }
 
 // residual epilogue of o / down for n-blocks nb0 .. nb0 + NB - 1: h += y; x = bf16(h) (xf); ss[m] += sum h^2
-template <int NB, int MT>
+template <int NB, int MT, int C>
 __device__ __forceinline__ void residual_epi(const DbArgs& a, const f32x4_t* red, int nb0, long long* ss) {
   const __amdgpu_buffer_rsrc_t rh = rsrc(a.h), rx = rsrc(a.x);
-  for (int idx = threadIdx.x; idx < NB * MT * 64; idx += DB_THREADS) {
+  for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * C) {
     const int l = idx & 63, t = idx >> 6;
     const int j = t % MT, i = t / MT;
     const int m = j * 16 + (l & 15);
     const int n = (nb0 + i) * 16 + 4 * (l >> 4);
     float hs = 0.f;
     if (m < a.B) {
-      const f32x4_t s = lds_sum<NB, MT>(red, t, l);
+      const f32x4_t s = lds_sum<NB, MT, C>(red, t, l);
       const uint32_t ho = (uint32_t)(((size_t)m * a.d + n) * 4);
       const u32x4_t hv = ld_sc1(rh, ho);
       const float v0 = __uint_as_float(hv[0]) + s[0], v1 = __uint_as_float(hv[1]) + s[1];
@@ -283,128 +355,156 @@ __device__ __forceinline__ void residual_epi(const DbArgs& a, const f32x4_t* red
   }
 }
 
-// k-blocks per chunk for MT row tiles x NB n-blocks: as deep as the VGPRs allow without spilling (two chunks of
-// weights + two of activations per wave; one workgroup per CU leaves 256 VGPRs per wave)
-constexpr int db_chunk(int mt, int nb) {
-  return nb == 1 ? (mt == 1 ? 8 : (mt == 2 ? 6 : 4)) : (nb == 2 ? (mt == 4 ? 2 : 4) : (mt == 4 ? 1 : 2));
+// end of phase p: every consumer wave drains its write-through stores, adds to the LDS counter; the wave whose add
+// is last adds the workgroup's item count to its XCD's done slot (8 slots: no 256-way same-address storm)
+template <int C>
+__device__ __forceinline__ void publish(const DbArgs& a, DbCtl* ctl, int p, int ndone, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (p == 0) stamp(a, 13);  // wave 0's stores of the o phase drained
+  if (lane == 0) {
+    const int old = __hip_atomic_fetch_add(&ctl->pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (old == C * (p + 1) - 1 && ndone)
+      __hip_atomic_fetch_add(done_ctr(a, p, blockIdx.x % DB_SLOTS), ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// wait until phase p has n items done on every CU: consumer wave 0 polls the 8 slots (lanes 0-7, the sum
+// broadcast from lane 0 so the loop stays wave-uniform), then sets ready; the other consumer waves wait for it
+__device__ __forceinline__ bool wait_phase(const DbArgs& a, DbCtl* ctl, int p, int n, int c, int lane) {
+  if (c != 0) return spin_ge(a, ctl, &ctl->ready, p + 1);
+  if (DB_HOLD) lds_st(&ctl->hold, 1);
+  const long long t0 = wall_clock64();
+  while (true) {
+    int v = lane < DB_SLOTS ? __hip_atomic_load(done_ctr(a, p, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    if (__shfl(v, 0, 64) >= n) break;
+    if (lds_ld(&ctl->abort)) return false;
+    if (wall_clock64() - t0 > a.timeout_ticks) {
+      if (lane == 0) __hip_atomic_store((db_g_i32*)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lds_st(&ctl->abort, 1);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  lds_st(&ctl->ready, p + 1);
+  if (DB_HOLD) lds_st(&ctl->hold, 0);
+  return true;
 }
 
 }  // namespace
 
-// NBx: n-blocks per work item of each phase (NBG counts gate + up blocks: even); MT: 16-row tiles (B <= 16 MT)
-template <int MT, int NBO, int NBG, int NBD, int NBQ>
-__global__ __launch_bounds__(DB_THREADS) void decode_block_kernel(DbArgs a) {
+// NBx: n-blocks per work item of each phase (NBG counts gate + up blocks: even); MT: 16-row tiles (B <= 16 MT);
+// C: consumer waves (+ 1 loader wave)
+template <int MT, int NBO, int NBG, int NBD, int NBQ, int C>
+__global__ __launch_bounds__(64 * (C + 1)) void decode_block_kernel(DbArgs a) {
   constexpr int NBMAX = (NBO > NBG ? NBO : NBG) > (NBD > NBQ ? NBD : NBQ) ? (NBO > NBG ? NBO : NBG) : (NBD > NBQ ? NBD : NBQ);
-  constexpr int UO = db_chunk(MT, NBO), UG = db_chunk(MT, NBG), UD = db_chunk(MT, NBD), UQ = db_chunk(MT, NBQ);
-  __shared__ __attribute__((aligned(16))) f32x4_t red[DB_WAVES * NBMAX * MT * 64];
-  __shared__ int s_item, s_flag;
+  constexpr int RED = C * NBMAX * MT * 64;  // f32x4 partial sums of one item
+  // ONE __shared__ object: ring | red | control words
+  __shared__ __attribute__((aligned(16))) uint4 smem[DB_RING * 1024 + RED + 8];
+  static_assert(sizeof(DbCtl) <= 8 * 16, "control words");
+  uint4* ring = smem;
+  f32x4_t* red = reinterpret_cast<f32x4_t*>(smem + DB_RING * 1024);
+  DbCtl* ctl = reinterpret_cast<DbCtl*>(smem + DB_RING * 1024 + RED);
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  stamp(a, 0);
+  if (threadIdx.x < sizeof(DbCtl) / 4) reinterpret_cast<int*>(ctl)[threadIdx.x] = 0;
+  __syncthreads();  // the only workgroup barrier: the loader runs ahead of the consumers from here on
+  stamp(a, 1);
   const float inv_d = 1.0f / (float)a.d;
   const int KBo = a.hd / 32, KBg = a.d / 32, KBd = a.ffn / 32, KBq = a.d / 32;
   const int nO = a.d / 16 / NBO, nG = (2 * a.ffn / 16) / NBG, nD = a.d / 16 / NBD;
   const int nQ = a.wq ? (a.nq / 16) / NBQ : 0;
 
-  // ---------------- PO: o projection + residual (ss1)
-  int ndone;
-  stamp(a, 0);
-  {
-    GemmItem<MT, NBO, UO> g;
-    const int it = blockIdx.x < nO ? (int)blockIdx.x : nO;
-    stamp(a, 1);
-    if (it < nO) {
-      g.setup(a.wo, KBo, it * NBO, w, lane);
-      g.load_w(w);
-    }
-    ndone = gemm_phase<MT, NBO, UO>(a, 0, nO, a.wo, KBo, rsrc(a.attn), g, it, red, &s_item, w, lane,
-                                    [&](int nb0, const f32x4_t* r) { residual_epi<NBO, MT>(a, r, nb0, a.ss1); });
-    stamp(a, 2);
-    stamp(a, 9, ndone);
+  if (wv == C) {  // ---------------- the loader wave: the whole launch's weight stream
+    int q = 0, pub = 0;
+    const bool ok = db_load_phase<NBO, C>(a, ctl, ring, a.wo, KBo, nO, q, pub, lane) &&
+                    db_load_phase<NBG, C>(a, ctl, ring, a.wgu, KBg, nG, q, pub, lane) &&
+                    db_load_phase<NBD, C>(a, ctl, ring, a.wd, KBd, nD, q, pub, lane) &&
+                    (nQ == 0 || db_load_phase<NBQ, C>(a, ctl, ring, a.wq, KBq, nQ, q, pub, lane));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the wave
+    if (ok)
+      for (; pub < q; ++pub) lds_st(&ctl->full[pub % DB_RING], pub / DB_RING + 1);
+    return;
   }
-  // ---------------- PG: gate_up (rows scaled by ss1, SiLU * up -> act); first item's weights before the seam
-  {
-    GemmItem<MT, NBG, UG> g;
-    publish(a, 0, ndone);
-    const int it = blockIdx.x < nG ? (int)blockIdx.x : nG;
-    if (it < nG) {
-      g.setup(a.wgu, KBg, it * NBG, w, lane);
-      g.load_w(w);
-    }
-    if (!wait_done(a, 0, nO, &s_flag)) return;
-    stamp(a, 3);
-    const __amdgpu_buffer_rsrc_t ra = rsrc(a.act);
-    ndone = gemm_phase<MT, NBG, UG>(a, 1, nG, a.wgu, KBg, rsrc(a.x), g, it, red, &s_item, w, lane,
+
+  // ---------------- consumer waves
+  const int c = wv;
+  int q = 0, e = 0, nd = 0;
+  // PO: o projection + residual (ss1)
+  if (!db_consume_phase<MT, NBO, C>(a, ctl, ring, red, a.attn, KBo, nO, q, e, nd, c, lane,
+                                    [&](int nb0, const f32x4_t* r) { residual_epi<NBO, MT, C>(a, r, nb0, a.ss1); }))
+    return;
+  stamp(a, 2);
+  stamp(a, 9, nd);
+  publish<C>(a, ctl, 0, nd, lane);
+  if (!wait_phase(a, ctl, 0, nO, c, lane)) return;
+  stamp(a, 3);
+  // PG: gate_up (rows scaled by ss1, SiLU * up -> act)
+  nd = 0;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(a.act);
+  if (!db_consume_phase<MT, NBG, C>(a, ctl, ring, red, a.x, KBg, nG, q, e, nd, c, lane,
                                     [&](int nb0, const f32x4_t* r) {
-      for (int idx = threadIdx.x; idx < (NBG / 2) * MT * 64; idx += DB_THREADS) {
-        const int l = idx & 63, t = idx >> 6;
-        const int j = t % MT, pr = t / MT;
-        const int m = j * 16 + (l & 15);
-        if (m >= a.B) continue;
-        const f32x4_t gs = lds_sum<NBG, MT>(r, (2 * pr) * MT + j, l);
-        const f32x4_t us = lds_sum<NBG, MT>(r, (2 * pr + 1) * MT + j, l);
-        const float sc = row_scale(a.ss1, m, inv_d, a.eps);
-        const int n = ((nb0 + 2 * pr) >> 1) * 16 + 4 * (l >> 4);
-        const u32x2_t pk = {pack2bf(silu(gs[0] * sc) * (us[0] * sc), silu(gs[1] * sc) * (us[1] * sc)),
-                            pack2bf(silu(gs[2] * sc) * (us[2] * sc), silu(gs[3] * sc) * (us[3] * sc))};
-        __builtin_amdgcn_raw_buffer_store_b64(pk, ra, (int)(xf_off(m, n, MT) * 2), 0, DB_SC1);
-      }
-    });
-    stamp(a, 4);
-    stamp(a, 10, ndone);
-  }
-  // ---------------- PD: down + residual (ss2)
-  {
-    GemmItem<MT, NBD, UD> g;
-    publish(a, 1, ndone);
-    const int it = blockIdx.x < nD ? (int)blockIdx.x : nD;
-    if (it < nD) {
-      g.setup(a.wd, KBd, it * NBD, w, lane);
-      g.load_w(w);
+    for (int idx = threadIdx.x; idx < (NBG / 2) * MT * 64; idx += 64 * C) {
+      const int l = idx & 63, t = idx >> 6;
+      const int j = t % MT, pr = t / MT;
+      const int m = j * 16 + (l & 15);
+      if (m >= a.B) continue;
+      const f32x4_t gs = lds_sum<NBG, MT, C>(r, (2 * pr) * MT + j, l);
+      const f32x4_t us = lds_sum<NBG, MT, C>(r, (2 * pr + 1) * MT + j, l);
+      const float sc = row_scale(a.ss1, m, inv_d, a.eps);
+      const int n = ((nb0 + 2 * pr) >> 1) * 16 + 4 * (l >> 4);
+      const u32x2_t pk = {pack2bf(silu(gs[0] * sc) * (us[0] * sc), silu(gs[1] * sc) * (us[1] * sc)),
+                          pack2bf(silu(gs[2] * sc) * (us[2] * sc), silu(gs[3] * sc) * (us[3] * sc))};
+      __builtin_amdgcn_raw_buffer_store_b64(pk, ra, (int)(xf_off(m, n, MT) * 2), 0, DB_SC1);
     }
-    if (!wait_done(a, 1, nG, &s_flag)) return;
-    stamp(a, 5);
-    ndone = gemm_phase<MT, NBD, UD>(a, 2, nD, a.wd, KBd, rsrc(a.act), g, it, red, &s_item, w, lane,
-                                    [&](int nb0, const f32x4_t* r) { residual_epi<NBD, MT>(a, r, nb0, a.ss2); });
-    stamp(a, 6);
-    stamp(a, 11, ndone);
-  }
+  }))
+    return;
+  stamp(a, 4);
+  stamp(a, 10, nd);
+  publish<C>(a, ctl, 1, nd, lane);
+  if (!wait_phase(a, ctl, 1, nG, c, lane)) return;
+  stamp(a, 5);
+  // PD: down + residual (ss2)
+  nd = 0;
+  if (!db_consume_phase<MT, NBD, C>(a, ctl, ring, red, a.act, KBd, nD, q, e, nd, c, lane,
+                                    [&](int nb0, const f32x4_t* r) { residual_epi<NBD, MT, C>(a, r, nb0, a.ss2); }))
+    return;
+  stamp(a, 6);
+  stamp(a, 11, nd);
   if (!nQ) return;
-  // ---------------- PQ: next layer's qkv (rows scaled by ss2) -> f32 [B][nq] for the fused-RoPE attention
-  {
-    GemmItem<MT, NBQ, UQ> g;
-    publish(a, 2, ndone);
-    const int it = blockIdx.x < nQ ? (int)blockIdx.x : nQ;
-    if (it < nQ) {
-      g.setup(a.wq, KBq, it * NBQ, w, lane);
-      g.load_w(w);
+  publish<C>(a, ctl, 2, nd, lane);
+  if (!wait_phase(a, ctl, 2, nD, c, lane)) return;
+  stamp(a, 7);
+  // PQ: next layer's qkv (rows scaled by ss2) -> f32 [B][nq] for the fused-RoPE attention
+  nd = 0;
+  const __amdgpu_buffer_rsrc_t rq = rsrc(a.qout);
+  if (!db_consume_phase<MT, NBQ, C>(a, ctl, ring, red, a.x, KBq, nQ, q, e, nd, c, lane,
+                                    [&](int nb0, const f32x4_t* r) {
+    for (int idx = threadIdx.x; idx < NBQ * MT * 64; idx += 64 * C) {
+      const int l = idx & 63, t = idx >> 6;
+      const int j = t % MT, i = t / MT;
+      const int m = j * 16 + (l & 15);
+      if (m >= a.B) continue;
+      const f32x4_t s = lds_sum<NBQ, MT, C>(r, t, l) * row_scale(a.ss2, m, inv_d, a.eps);
+      const int n = (nb0 + i) * 16 + 4 * (l >> 4);
+      const u32x4_t u = {__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]), __float_as_uint(s[3])};
+      __builtin_amdgcn_raw_buffer_store_b128(u, rq, (int)(((size_t)m * a.nq + n) * 4), 0, 0);
     }
-    if (!wait_done(a, 2, nD, &s_flag)) return;
-    stamp(a, 7);
-    const __amdgpu_buffer_rsrc_t rq = rsrc(a.qout);
-    ndone = gemm_phase<MT, NBQ, UQ>(a, 3, nQ, a.wq, KBq, rsrc(a.x), g, it, red, &s_item, w, lane,
-                            [&](int nb0, const f32x4_t* r) {
-      for (int idx = threadIdx.x; idx < NBQ * MT * 64; idx += DB_THREADS) {
-        const int l = idx & 63, t = idx >> 6;
-        const int j = t % MT, i = t / MT;
-        const int m = j * 16 + (l & 15);
-        if (m >= a.B) continue;
-        const f32x4_t s = lds_sum<NBQ, MT>(r, t, l) * row_scale(a.ss2, m, inv_d, a.eps);
-        const int n = (nb0 + i) * 16 + 4 * (l >> 4);
-        const u32x4_t u = {__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]), __float_as_uint(s[3])};
-        __builtin_amdgcn_raw_buffer_store_b128(u, rq, (int)(((size_t)m * a.nq + n) * 4), 0, 0);
-      }
-    });
-    stamp(a, 8);
-    stamp(a, 12, ndone);
-  }
+  }))
+    return;
+  stamp(a, 8);
+  stamp(a, 12, nd);
 }
 
 extern "C" int lsa_decode_block_cnt_ints() { return DB_CNT_INTS; }
 
 // co-resident workgroups of a kernel on this device: occupancy per CU x CUs
-static int db_capacity(const void* kernel) {
+static int db_capacity(const void* kernel, int threads) {
   int per_cu = 0, dev = 0, ncu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, DB_THREADS, 0) != hipSuccess) per_cu = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess) per_cu = 1;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 1;
   return (per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
@@ -413,7 +513,7 @@ static int db_capacity(const void* kernel) {
 extern "C" int lsa_decode_block(const void* attn, const void* wo, float* h, void* x, long long* ss1, long long* ss2,
                                 const void* wgu, void* act, const void* wd, const void* wq, float* qout, int B, int d,
                                 int hd, int ffn, int nq, float eps, int* cnt, int* err, long long timeout_ticks,
-                                int nwg, int nbo, int nbg, int nbd, int nbq, long long* stamps, hipStream_t s) {
+                                int nwg, int nbo, int nbg, int nbd, int nbq, int cw, long long* stamps, hipStream_t s) {
   if (B < 1 || B > 64 || d % 32 || hd % 32 || ffn % 32 || (wq && nq % 16) || nwg < 1) return -1;
   if ((d / 16) % nbo || (2 * ffn / 16) % nbg || nbg % 2 || (d / 16) % nbd || (wq && (nq / 16) % nbq)) return -3;
   const int mt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
@@ -421,16 +521,16 @@ extern "C" int lsa_decode_block(const void* attn, const void* wo, float* h, void
            reinterpret_cast<uint16_t*>(x), ss1, ss2, reinterpret_cast<const uint4*>(wgu),
            reinterpret_cast<uint16_t*>(act), reinterpret_cast<const uint4*>(wd), reinterpret_cast<const uint4*>(wq),
            qout, B, d, hd, ffn, nq, eps, cnt, err, timeout_ticks, stamps};
-#define DB_L(MTV, O, G, D_, Q)                                                                              \
-  if (mt == MTV && nbo == O && nbg == G && nbd == D_ && nbq == Q) {                                          \
-    static const int cap = db_capacity(reinterpret_cast<const void*>(decode_block_kernel<MTV, O, G, D_, Q>)); \
-    hipLaunchKernelGGL((decode_block_kernel<MTV, O, G, D_, Q>), dim3(nwg < cap ? nwg : cap), dim3(DB_THREADS), \
-                       0, s, a);                                                                            \
-    return (int)hipGetLastError();                                                                          \
+#define DB_L(MTV, O, G, D_, Q, CW)                                                                                \
+  if (mt == MTV && nbo == O && nbg == G && nbd == D_ && nbq == Q && cw == CW) {                                     \
+    static const int cap = db_capacity(reinterpret_cast<const void*>(decode_block_kernel<MTV, O, G, D_, Q, CW>), \
+                                       64 * (CW + 1));                                                            \
+    hipLaunchKernelGGL((decode_block_kernel<MTV, O, G, D_, Q, CW>), dim3(nwg < cap ? nwg : cap),                 \
+                       dim3(64 * (CW + 1)), 0, s, a);                                                             \
+    return (int)hipGetLastError();                                                                                \
   }
-#define DB_MT(MTV) DB_L(MTV, 1, 2, 1, 1) DB_L(MTV, 1, 2, 1, 2) DB_L(MTV, 2, 2, 2, 2) DB_L(MTV, 1, 4, 1, 1)
-  DB_MT(1) DB_MT(2) DB_MT(4)
-#undef DB_MT
+  DB_L(1, 1, 2, 1, 1, 4) DB_L(2, 1, 2, 1, 1, 4) DB_L(4, 1, 2, 1, 1, 4)
+  DB_L(1, 1, 2, 1, 1, 8) DB_L(2, 1, 2, 1, 1, 8)
 #undef DB_L
   return -4;
 }

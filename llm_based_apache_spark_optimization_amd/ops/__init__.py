@@ -402,22 +402,24 @@ def tile_splitk(M: int, N: int, K: int, kind: str = "bf16") -> int:
     return sk
 
 
-# Persistent post-attention decode block (csrc/kernels/decode_block.hip): n-blocks per work item of each phase,
-# (nbo, nbg, nbd, nbq); LSA_DECODE_BLOCK_CFG="nbo,nbg,nbd,nbq" overrides (tuning: scripts/bench_decode_block.py)
-DECODE_BLOCK_DEFAULT = (1, 2, 1, 1)
+# Persistent post-attention decode block (csrc/kernels/decode_block.hip): n-blocks per work item of each phase and
+# consumer waves per workgroup, (nbo, nbg, nbd, nbq, cw); LSA_DECODE_BLOCK_CFG="nbo,nbg,nbd,nbq[,cw]" overrides
+# (tuning: scripts/bench_decode_block.py)
+DECODE_BLOCK_DEFAULT = (1, 2, 1, 1, 4)
 DECODE_BLOCK_CNT_INTS = 1152  # per-layer claim / done counter block (36 lines of 128 B; kernel's DB_CNT_INTS)
 
 
 def decode_block_cfg(B: int) -> tuple:
     env = os.environ.get("LSA_DECODE_BLOCK_CFG")
     if env:
-        return tuple(int(v) for v in env.split(","))
+        c = tuple(int(v) for v in env.split(","))
+        return c + DECODE_BLOCK_DEFAULT[len(c):]
     return DECODE_BLOCK_DEFAULT
 
 
 def decode_block_grid(B: int, device) -> int:
-    """Workgroups of the persistent block: LSA_DECODE_BLOCK_NWG, else one per CU (the work is claimed
-    dynamically, so any grid size is correct; two resident workgroups per CU need <= 128 VGPRs)."""
+    """Workgroups of the persistent block: LSA_DECODE_BLOCK_NWG, else one per CU (every workgroup owns items
+    i, i + grid, .. of each phase, so any grid size is correct; the ring's LDS admits one workgroup per CU)."""
     env = int(os.environ.get("LSA_DECODE_BLOCK_NWG", "0"))
     return env or num_cus(device)
 
@@ -441,9 +443,9 @@ def decode_block(attn_xf, wo: "PackedWeight", h, x_xf, ss1, ss2, wgu: "PackedWei
     f32 [B, nq] (a one-slab ``qkv_parts`` for the fused-RoPE attention)].  ``cnt`` (int32,
     >= DECODE_BLOCK_CNT_INTS) must be zero at the launch (the runner zeroes every layer's counters with one memset
     per step); ss1 / ss2 must be zero.  ``stamps`` (int64 [nwg, 16]): per-workgroup wall-clock stamps of the
-    phase boundaries (0 start, 1 claimed, 2 o done, 3 o complete, 4 gate_up done, 5 complete, 6 down done,
+    phase boundaries (0 start, 1 prologue done, 2 o done, 3 o complete, 4 gate_up done, 5 complete, 6 down done,
     7 complete, 8 qkv done; 9-12 items per phase)."""
-    nbo, nbg, nbd, nbq = cfg or decode_block_cfg(B)
+    nbo, nbg, nbd, nbq, cw = (tuple(cfg) + DECODE_BLOCK_DEFAULT[len(cfg):]) if cfg else decode_block_cfg(B)
     d, ffn = wo.N, wd.K
     if not _gpu(h):
         a = from_xfrag(attn_xf, B, wo.K)
@@ -470,7 +472,7 @@ def decode_block(attn_xf, wo: "PackedWeight", h, x_xf, ss1, ss2, wgu: "PackedWei
     ticks = int(timeout_s * ext().ar_wallclock_khz() * 1000)
     ext().decode_block(attn_xf, wo.data, h, x_xf, ss1, ss2, wgu.data, act_xf, wd.data,
                        wq.data if wq is not None else None, qout, B, ffn, wq.N if wq is not None else 0, float(eps),
-                       cnt, err, ticks, nwg or decode_block_grid(B, h.device), nbo, nbg, nbd, nbq, stamps)
+                       cnt, err, ticks, nwg or decode_block_grid(B, h.device), nbo, nbg, nbd, nbq, cw, stamps)
 
 
 def xfrag_tiles(M: int) -> int:

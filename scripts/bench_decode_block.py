@@ -23,7 +23,7 @@ Bs = [int(v) for v in _pos[0].split(",")] if len(_pos) > 0 else [1, 8, 32, 64]
 CFGS = [tuple(int(x) for x in c.split(",")) for c in _pos[1].split(";")] if len(_pos) > 1 and _pos[1] != "-" else [None]
 NWGS = [int(v) for v in _pos[2].split(",")] if len(_pos) > 2 else [0]
 STAMPS = "--stamps" in sys.argv
-NAMES = ["start", "claimed", "o_done", "o_complete", "gu_done", "gu_complete", "down_done", "down_complete", "qkv_done"]
+NAMES = ["start", "prologue", "o_done", "o_complete", "gu_done", "gu_complete", "down_done", "down_complete", "qkv_done"]
 
 
 def main():
@@ -89,6 +89,9 @@ def main():
                         us = (st[:, :9] - t0).double() * 1000.0 / khz
                         rec["stamps_us"] = {k: [round(float(us[:, i].min()), 1), round(float(us[:, i].median()), 1),
                                                 round(float(us[:, i].max()), 1)] for i, k in enumerate(NAMES)}
+                        rec["o_drained_us"] = [round(float(v), 1) for v in
+                                               ((st[:, 13] - t0).double() * 1000.0 / khz).quantile(
+                                                   torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64)).tolist()]
                         rec["items"] = {k: [int(st[:, 9 + i].min()), int(st[:, 9 + i].max())]
                                         for i, k in enumerate(["o", "gu", "down", "qkv"])}
                     print(json.dumps(rec), flush=True)

@@ -1,8 +1,9 @@
 """Persistent post-attention decode block (csrc/kernels/decode_block.hip) against its fp32 PyTorch reference
 (ops.decode_block's CPU path), and the block decode step (LSA_DECODE_BLOCK=1) against the default decode path.
 
-The kernel distributes work dynamically (claim counters per phase), so the same launch must be correct with
-ONE workgroup (it runs every item of every phase itself), with a few, and with more workgroups than CUs."""
+Workgroup i owns items i, i + grid, .. of every phase and its loader wave streams exactly those items' weights,
+so the same launch must be correct with ONE workgroup (it runs every item of every phase itself), with a few, and
+with more workgroups than CUs (clamped to the co-resident capacity)."""
 import dataclasses
 
 import pytest
@@ -17,7 +18,7 @@ from llm_based_apache_spark_optimization_amd.models.llama import init_random
 pytestmark = pytest.mark.gpu
 
 D, HD, FFN, NQ = 1024, 1024, 2816, 1536
-CFGS = [(1, 2, 1, 1), (1, 2, 1, 2), (2, 2, 2, 2), (1, 4, 1, 1)]
+CFGS = [(1, 2, 1, 1, 4), (1, 2, 1, 1, 8)]  # (nbo, nbg, nbd, nbq, consumer waves)
 
 
 def _weights(dev):
@@ -56,6 +57,8 @@ def test_decode_block_matches_reference(gpu, B):
     ref = _bufs(B, "cpu", B)
     _run(ref, wc, B)
     for cfg in CFGS:
+        if cfg[4] == 8 and B > 32:
+            continue  # 8 consumer waves: 16-row tiles <= 2 (register budget)
         for nwg in (1, 7, None, 1024):
             b = _bufs(B, gpu, B)
             _run(b, wg, B, cfg=cfg, nwg=nwg)
@@ -89,7 +92,7 @@ def test_decode_block_last_layer_has_no_qkv_phase(gpu):
 
 
 def test_decode_block_reproducible(gpu):
-    """Dynamic claiming changes which workgroup computes an item, never the summation order inside it."""
+    """The grid size changes which workgroup computes an item, never the summation order inside it."""
     wg, _ = _weights(gpu)
     outs = []
     for nwg in (1, None, 300):
