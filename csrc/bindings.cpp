@@ -77,6 +77,8 @@ int lsa_ar_header_bytes();
 int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
                int nblocks, long long timeout_ticks, int* err, int nslab, long slab_stride, hipStream_t s);
 int lsa_decode_block_cnt_ints();
+int lsa_res_gemm(const void* X, const void* W, float* h, void* xout, long long* ss, int B, int N, int K, int* err,
+                 long long timeout_ticks, int nwg, int cw, long long* stamps, hipStream_t s);
 int lsa_decode_block(const void* attn, const void* wo, float* h, void* x, long long* ss1, long long* ss2, const void* wgu,
                      void* act, const void* wd, const void* wq, float* qout, int B, int d, int hd, int ffn, int nq,
                      float eps, int* cnt, int* err, long long timeout_ticks, int nwg, int nbo, int nbg, int nbd, int nbq,
@@ -670,6 +672,37 @@ void decode_block(const at::Tensor& attn, const at::Tensor& wo, at::Tensor& h, a
         "decode_block");
 }
 
+// one residual GEMM on the decode block's ring engine (kernels/decode_block.hip lsa_res_gemm):
+// h[:B] += X @ W^T, xout = bf16(h) fragment-major, ss[:B] += row sums of h^2 (Q24)
+void res_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& h, at::Tensor& xout, at::Tensor& ss, int64_t B,
+              at::Tensor& err, int64_t timeout_ticks, int64_t nwg, int64_t cw, const c10::optional<at::Tensor>& stamps) {
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "w");
+  need(xout, at::kBFloat16, "xout");
+  need(h, at::kFloat, "h");
+  need(ss, at::kLong, "ss");
+  need(err, at::kInt, "err");
+  TORCH_CHECK(B >= 1 && B <= 64, "res_gemm: batch 1..64");
+  TORCH_CHECK(h.dim() == 2 && h.size(0) >= B && h.is_contiguous(), "h [>= B, N] f32");
+  const int64_t N = h.size(1), mt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
+  TORCH_CHECK(N % 16 == 0 && N > 0 && w.numel() % N == 0, "res_gemm: w [N, K], N % 16 == 0");
+  const int64_t K = w.numel() / N;
+  TORCH_CHECK(K % 32 == 0, "res_gemm: K % 32 == 0");
+  TORCH_CHECK(x.is_contiguous() && x.numel() >= mt * 16 * K, "res_gemm: fragment-major x too small");
+  TORCH_CHECK(xout.is_contiguous() && xout.numel() >= mt * 16 * N, "res_gemm: fragment-major xout too small");
+  TORCH_CHECK(ss.numel() >= B && err.numel() >= 1, "res_gemm: row sums / err too small");
+  TORCH_CHECK(nwg >= 1 && nwg <= 65536 && (cw == 4 || cw == 8), "res_gemm: grid / consumer waves");
+  if (stamps.has_value()) {
+    need(*stamps, at::kLong, "stamps");
+    TORCH_CHECK(stamps->is_contiguous() && stamps->numel() >= nwg * 16, "res_gemm: stamps [nwg, 16] int64");
+  }
+  check(lsa_res_gemm(x.data_ptr(), w.data_ptr(), h.data_ptr<float>(), xout.data_ptr(),
+                     reinterpret_cast<long long*>(ss.data_ptr<int64_t>()), B, N, K, err.data_ptr<int>(), timeout_ticks,
+                     nwg, cw, stamps.has_value() ? reinterpret_cast<long long*>(stamps->data_ptr<int64_t>()) : nullptr,
+                     cur_stream()),
+        "res_gemm");
+}
+
 }  // namespace
 
 #ifndef LSA_BINDINGS_SELFTEST
@@ -732,6 +765,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ffn"), py::arg("nq"), py::arg("eps"), py::arg("cnt"), py::arg("err"), py::arg("timeout_ticks"),
         py::arg("nwg"), py::arg("nbo"), py::arg("nbg"), py::arg("nbd"), py::arg("nbq"), py::arg("cw") = 4,
         py::arg("stamps") = py::none());
+  m.def("res_gemm", &res_gemm, py::arg("x"), py::arg("w"), py::arg("h"), py::arg("xout"), py::arg("ss"), py::arg("B"),
+        py::arg("err"), py::arg("timeout_ticks"), py::arg("nwg"), py::arg("cw") = 4, py::arg("stamps") = py::none());
   m.def("decode_block_cnt_ints", []() { return lsa_decode_block_cnt_ints(); });
   m.def("ar_alloc", &ar_alloc);
   m.def("ar_free", [](int64_t p) { check(lsa_ar_free(reinterpret_cast<void*>(p)), "ar_free"); });

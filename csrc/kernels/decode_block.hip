@@ -85,6 +85,7 @@ struct DbArgs {
   int* err;
   long long timeout_ticks;
   long long* stamps;     // optional [nwg][16] wall-clock stamps of the phase boundaries (scripts/bench_decode_block.py)
+  int mode;              // 0: the whole block; 1: PO alone = one residual GEMM h += X @ W (lsa_res_gemm)
 };
 
 // LDS control words (zeroed in the prologue)
@@ -420,10 +421,10 @@ __global__ __launch_bounds__(64 * (C + 1)) void decode_block_kernel(DbArgs a) {
 
   if (wv == C) {  // ---------------- the loader wave: the whole launch's weight stream
     int q = 0, pub = 0;
-    const bool ok = db_load_phase<NBO, C>(a, ctl, ring, a.wo, KBo, nO, q, pub, lane) &&
+    const bool ok = db_load_phase<NBO, C>(a, ctl, ring, a.wo, KBo, nO, q, pub, lane) && (a.mode == 1 ||
                     db_load_phase<NBG, C>(a, ctl, ring, a.wgu, KBg, nG, q, pub, lane) &&
                     db_load_phase<NBD, C>(a, ctl, ring, a.wd, KBd, nD, q, pub, lane) &&
-                    (nQ == 0 || db_load_phase<NBQ, C>(a, ctl, ring, a.wq, KBq, nQ, q, pub, lane));
+                    (nQ == 0 || db_load_phase<NBQ, C>(a, ctl, ring, a.wq, KBq, nQ, q, pub, lane)));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the wave
     if (ok)
       for (; pub < q; ++pub) lds_st(&ctl->full[pub % DB_RING], pub / DB_RING + 1);
@@ -439,6 +440,7 @@ __global__ __launch_bounds__(64 * (C + 1)) void decode_block_kernel(DbArgs a) {
     return;
   stamp(a, 2);
   stamp(a, 9, nd);
+  if (a.mode == 1) return;
   publish<C>(a, ctl, 0, nd, lane);
   if (!wait_phase(a, ctl, 0, nO, c, lane)) return;
   stamp(a, 3);
@@ -510,17 +512,37 @@ static int db_capacity(const void* kernel, int threads) {
   return (per_cu > 0 ? per_cu : 1) * (ncu > 0 ? ncu : 1);
 }
 
+static int db_launch(const DbArgs& a, int nwg, int nbo, int nbg, int nbd, int nbq, int cw, hipStream_t s);
+
 extern "C" int lsa_decode_block(const void* attn, const void* wo, float* h, void* x, long long* ss1, long long* ss2,
                                 const void* wgu, void* act, const void* wd, const void* wq, float* qout, int B, int d,
                                 int hd, int ffn, int nq, float eps, int* cnt, int* err, long long timeout_ticks,
                                 int nwg, int nbo, int nbg, int nbd, int nbq, int cw, long long* stamps, hipStream_t s) {
   if (B < 1 || B > 64 || d % 32 || hd % 32 || ffn % 32 || (wq && nq % 16) || nwg < 1) return -1;
   if ((d / 16) % nbo || (2 * ffn / 16) % nbg || nbg % 2 || (d / 16) % nbd || (wq && (nq / 16) % nbq)) return -3;
-  const int mt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
   DbArgs a{reinterpret_cast<const uint16_t*>(attn), reinterpret_cast<const uint4*>(wo), h,
            reinterpret_cast<uint16_t*>(x), ss1, ss2, reinterpret_cast<const uint4*>(wgu),
            reinterpret_cast<uint16_t*>(act), reinterpret_cast<const uint4*>(wd), reinterpret_cast<const uint4*>(wq),
-           qout, B, d, hd, ffn, nq, eps, cnt, err, timeout_ticks, stamps};
+           qout, B, d, hd, ffn, nq, eps, cnt, err, timeout_ticks, stamps, 0};
+  return db_launch(a, nwg, nbo, nbg, nbd, nbq, cw, s);
+}
+
+// One residual GEMM on the ring engine (the block's PO phase alone): h[B][N] += X @ W^T, xout = bf16(h)
+// (fragment-major, MT row tiles), ss[m] += sum_n h^2 (Q24) -- no split-K slabs, no arrival tickets, no norm
+// launch: every workgroup owns whole 16-column n-blocks over the full K, streamed by its loader wave.
+// X: fragment-major [K / 32][MT][64][8] bf16; W: fragment-major [N / 16][K / 32][64].
+extern "C" int lsa_res_gemm(const void* X, const void* W, float* h, void* xout, long long* ss, int B, int N, int K,
+                            int* err, long long timeout_ticks, int nwg, int cw, long long* stamps, hipStream_t s) {
+  if (B < 1 || B > 64 || N % 16 || K % 32 || nwg < 1) return -1;
+  DbArgs a{reinterpret_cast<const uint16_t*>(X), reinterpret_cast<const uint4*>(W), h,
+           reinterpret_cast<uint16_t*>(xout), ss, ss, reinterpret_cast<const uint4*>(W),
+           reinterpret_cast<uint16_t*>(xout), reinterpret_cast<const uint4*>(W), nullptr,
+           nullptr, B, N, K, 32, 0, 0.f, nullptr, err, timeout_ticks, stamps, 1};
+  return db_launch(a, nwg, 1, 2, 1, 1, cw, s);
+}
+
+static int db_launch(const DbArgs& a, int nwg, int nbo, int nbg, int nbd, int nbq, int cw, hipStream_t s) {
+  const int mt = a.B <= 16 ? 1 : (a.B <= 32 ? 2 : 4);
 #define DB_L(MTV, O, G, D_, Q, CW)                                                                                \
   if (mt == MTV && nbo == O && nbg == G && nbd == D_ && nbq == Q && cw == CW) {                                     \
     static const int cap = db_capacity(reinterpret_cast<const void*>(decode_block_kernel<MTV, O, G, D_, Q, CW>), \

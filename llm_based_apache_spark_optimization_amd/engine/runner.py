@@ -177,6 +177,10 @@ class ModelRunner:
         # inside the step: 192 output blocks per row-parallel GEMM leave CUs idle without split-K, and split-K
         # adds the last-arriver tail (3B 2k explain 1.733 vs 1.708 ms per step norm-free vs norm launches,
         # 7B b1 2.625 vs 2.69 ms) -- so the default is per hidden size
+        # (o / down as non-split residual GEMMs on the decode block's ring engine, ops.res_gemm, in the norm-free
+        # step at batch 32 measured slower than the split-K GEMMs + norm launches: 7B 3.77 vs 3.49 ms per step,
+        # profiles/r3/res_ring_ab_mi355x.txt -- a standalone full-K stream cannot ramp 128-352 KB per CU fast
+        # enough with <= 63 KB of LDS-DMA in flight per loader wave; not wired in)
         mb = os.environ.get("LSA_FUSED_NORM_MAX_B")
         self.fused_norm_max_batch = int(mb) if mb is not None else (16 if self.d >= 4096 else 0)
         self.ssq = torch.zeros(2 * self.L + 2, S, dtype=torch.int64, device=dev)  # Q24 fixed point (ops.ss_q24)

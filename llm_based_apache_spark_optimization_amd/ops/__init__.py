@@ -475,6 +475,25 @@ def decode_block(attn_xf, wo: "PackedWeight", h, x_xf, ss1, ss2, wgu: "PackedWei
                        cnt, err, ticks, nwg or decode_block_grid(B, h.device), nbo, nbg, nbd, nbq, cw, stamps)
 
 
+def res_gemm(x_xf, w: "PackedWeight", h, xout_xf, ss, B: int, err, timeout_s: float = 2.0, nwg: Optional[int] = None,
+             cw: int = 4, stamps=None) -> None:
+    """Residual row-parallel projection on the decode block's LDS-DMA ring engine (csrc/kernels/decode_block.hip
+    lsa_res_gemm; TP = 1, bf16 weights, B <= 64): h[:B] += x @ W^T (f32), xout = bf16(h) in the fragment-major
+    layout, ss[:B] += row sums of h^2 (Q24).  Every workgroup owns whole 16-column n-blocks over the full K (no
+    split-K slabs, no arrival tickets), streamed into LDS by its own loader wave -- the norm-free decode step's o /
+    down projection without the slab round trip of the split-K residual epilogue."""
+    N, K = w.N, w.K
+    if not _gpu(h):
+        hn = h[:B].float() + ref.linear(from_xfrag(x_xf, B, K), w.dense(), "f32")
+        h[:B].copy_(hn)
+        xout_xf.view(-1)[: xfrag_tiles(B) * 16 * N].copy_(to_xfrag(hn.to(torch.bfloat16)))
+        ss[:B] += ss_q24(hn.pow(2).sum(1))
+        return
+    assert w.kind == "bf16", "res_gemm: bf16 weights"
+    ticks = int(timeout_s * ext().ar_wallclock_khz() * 1000)
+    ext().res_gemm(x_xf, w.data, h, xout_xf, ss, B, err, ticks, nwg or num_cus(h.device), cw, stamps)
+
+
 def xfrag_tiles(M: int) -> int:
     """Row tiles (16 rows each) of the fragment-major activation layout for M rows (decode: M <= 64)."""
     return 1 if M <= 16 else (2 if M <= 32 else 4)

@@ -138,3 +138,33 @@ def test_block_decode_numerics(gpu, monkeypatch, B):
     res = nm.teacher_forced_check(eng, prompts, 64, check_rows=(0, B - 1))
     print(res)
     assert res["ok"], res
+
+
+@pytest.mark.parametrize("B", [1, 16, 20, 32, 33, 64])
+def test_res_gemm_matches_reference(gpu, B):
+    """ops.res_gemm (one residual GEMM on the ring engine, the block's PO phase alone) against its fp32 reference,
+    for the o (K = HD) and down (K = FFN) shapes, with one workgroup, a few, and one per CU."""
+    wg, wc = _weights(gpu)
+    for wname, K in (("wo", HD), ("wd", FFN)):
+        g = torch.Generator().manual_seed(B + K)
+        xin = torch.randn(B, K, generator=g).to(torch.bfloat16)
+        xf = torch.zeros(64 * K, dtype=torch.bfloat16)
+        xf[: ops.xfrag_tiles(B) * 16 * K] = ops.to_xfrag(xin)
+        h0 = torch.zeros(64, D)
+        h0[:B] = torch.randn(B, D, generator=g) * 3
+        ref = {"h": h0.clone(), "x": torch.zeros(64 * D, dtype=torch.bfloat16), "ss": torch.zeros(64, dtype=torch.long)}
+        ops.res_gemm(xf, wc[wname], ref["h"], ref["x"], ref["ss"], B, torch.zeros(1, dtype=torch.int32))
+        for nwg in (1, 7, None):
+            h, x = h0.clone().to(gpu), torch.zeros(64 * D, dtype=torch.bfloat16, device=gpu)
+            ss, err = torch.zeros(64, dtype=torch.long, device=gpu), torch.zeros(1, dtype=torch.int32, device=gpu)
+            ops.res_gemm(xf.to(gpu), wg[wname], h, x, ss, B, err, nwg=nwg)
+            torch.cuda.synchronize()
+            tag = (B, wname, nwg)
+            assert int(err[0]) == 0, tag
+            hg, hr = h[:B].cpu(), ref["h"][:B]
+            assert ((hg - hr).norm() / hr.norm()) < 2e-3, tag
+            assert torch.equal(h[B:].cpu(), ref["h"][B:]), tag
+            assert torch.allclose(ops.ss_float(ss[:B].cpu()), ops.ss_float(ref["ss"][:B]), rtol=2e-3), tag
+            xg = ops.from_xfrag(x, B, D).float().cpu()
+            assert ((xg - hr).norm() / hr.norm()) < 1e-2, tag
+
