@@ -57,6 +57,8 @@ int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, vo
 int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
 int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, hipStream_t stream);
+int lsa_gemm_t256x(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int xf_tiles,
+                   hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
@@ -293,6 +295,26 @@ void gemm_t256(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor&
   }
   check(lsa_gemm_t256(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, cur_stream()),
         "gemm_t256");
+}
+
+// the 256^2 tile GEMM over fragment-major X (xf: [K / 32][xf_tiles][64][8] bf16, rows >= M zero or ignored)
+void gemm_t256_xf(const at::Tensor& xf, int64_t xf_tiles, int64_t M, const at::Tensor& wf, int64_t N, at::Tensor& out,
+                  int64_t epi) {
+  need(xf, at::kBFloat16, "xf");
+  need(wf, at::kBFloat16, "wf");
+  TORCH_CHECK(N > 0 && wf.numel() % N == 0, "weight numel mismatch");
+  const int64_t K = wf.numel() / N;
+  TORCH_CHECK(M > 0 && xf_tiles * 16 >= M && xf.is_contiguous() && xf.numel() >= xf_tiles * 16 * K,
+              "fragment-major x too small");
+  if (epi == 1) {
+    need(out, at::kFloat, "out");
+    TORCH_CHECK(out.numel() >= M * N, "f32 out too small");
+  } else {
+    need(out, at::kBFloat16, "out");
+    TORCH_CHECK(out.numel() >= M * (epi == 2 ? N / 2 : N), "bf16 out too small");
+  }
+  check(lsa_gemm_t256x(xf.data_ptr(), 0, M, K, wf.data_ptr(), N, out.data_ptr(), epi, xf_tiles, cur_stream()),
+        "gemm_t256_xf");
 }
 
 void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscale, int64_t N, at::Tensor& out,
@@ -715,6 +737,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_t256", &gemm_t256);
+  m.def("gemm_t256_xf", &gemm_t256_xf);
   m.def("fp8_gemm", &fp8_gemm, py::arg("x"), py::arg("wq"), py::arg("wscale"), py::arg("N"), py::arg("out"),
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("depth") = 1,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());

@@ -69,7 +69,9 @@ __device__ __forceinline__ void store_out(void* out, int ldo, int m, int n, cons
 // Every restage comes >= 2 phases after the last read of that half (WAR); every read comes a phase after
 // the wait that retired it (RAW) - cdna_hip_programming.md §5, 8-phase template rules.  Tiles past the
 // end are staged from clamped addresses (never read) so the counted wait stays exact.
-template <int EPI>
+// XF: X is fragment-major too, Xf[K / 32][mtt][64 lanes][8] (ops.to_xfrag layout with mtt 16-row tiles): every
+// X staging DMA then reads one contiguous 1 KiB fragment (8 full 128-B lines) instead of 16 rows x 64 B
+template <int EPI, bool XF = false>
 __global__ __launch_bounds__(512) void gemm_t256_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                                         const uint4* __restrict__ Wf, int NBtot,
                                                         void* __restrict__ out, int ldo, int ntm) {
@@ -101,8 +103,13 @@ __global__ __launch_bounds__(512) void gemm_t256_kernel(const uint16_t* __restri
       const char* g;
       if (h < 2) {  // X half h (qm = h): fragment (wr * 4 + i) * 2 + ks
         const int wi = f >> 1, wr = wi >> 2, i = wi & 3;
-        const int row = min(mbase + wr * 128 + h * 64 + i * 16 + r16, M - 1);
-        g = reinterpret_cast<const char*>(X + (size_t)row * ldx + kstep * 32 + c16);
+        if constexpr (XF) {  // ldx = row tiles of the fragment-major X
+          const int rt = min((mbase + wr * 128 + h * 64 + i * 16) >> 4, ldx - 1);
+          g = reinterpret_cast<const char*>(X + (((size_t)kstep * ldx + rt) * 64 + lane) * 8);
+        } else {
+          const int row = min(mbase + wr * 128 + h * 64 + i * 16 + r16, M - 1);
+          g = reinterpret_cast<const char*>(X + (size_t)row * ldx + kstep * 32 + c16);
+        }
       } else {      // W half h - 2 (qn): fragment (wc * 2 + j) * 2 + ks -> n-block wc * 4 + qn * 2 + j
         const int wj = f >> 1, wc = wj >> 1, j = wj & 1;
         const int nb = min(nbase + wc * 4 + (h - 2) * 2 + j, NBtot - 1);
@@ -213,6 +220,33 @@ __global__ __launch_bounds__(512) void gemm_t256_kernel(const uint16_t* __restri
 }
 
 // M > 64 linear layer on the 256^2 tile (K % 32 == 0, N % 16 == 0; EPI_SILU needs N % 32 == 0)
+// xf_tiles > 0: X is fragment-major with that many 16-row tiles (>= ceil(M / 16))
+extern "C" int lsa_gemm_t256x(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi,
+                              int xf_tiles, hipStream_t stream) {
+  if (K % 32 != 0 || N % 16 != 0 || M <= 0 || (xf_tiles > 0 && xf_tiles * 16 < M)) return -1;
+  const int KB = K / 32, NBtot = N / 16;
+  const int ntm = (M + 255) / 256, ntn = (NBtot + 15) / 16;
+  const int ldo = epi == EPI_SILU ? N / 2 : N;
+  const dim3 grid(ntm * ntn);
+  const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
+  const uint4* w = reinterpret_cast<const uint4*>(Wf);
+  if (xf_tiles <= 0) return -5;
+  switch (epi) {
+    case EPI_BF16:
+      hipLaunchKernelGGL((gemm_t256_kernel<EPI_BF16, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm);
+      break;
+    case EPI_F32:
+      hipLaunchKernelGGL((gemm_t256_kernel<EPI_F32, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm);
+      break;
+    case EPI_SILU:
+      hipLaunchKernelGGL((gemm_t256_kernel<EPI_SILU, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm);
+      break;
+    default:
+      return -4;
+  }
+  return (int)hipGetLastError();
+}
+
 extern "C" int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi,
                              hipStream_t stream) {
   if (K % 32 != 0 || N % 16 != 0 || M <= 0) return -1;

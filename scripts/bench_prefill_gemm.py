@@ -50,8 +50,13 @@ for name, (M, N, K, epi) in shapes.items():
         ref = (torch.nn.functional.silu(r3[:, :, 0]) * r3[:, :, 1]).reshape(M, N // 2)
     res = {"shape": name, "M": M, "N": N, "K": K, "epi": epi}
     flops = 2.0 * M * N * K
+    mtt = (M + 255) // 256 * 16  # fragment-major X over whole 256-row tiles
+    xp = torch.zeros(mtt * 16, K, device=dev, dtype=torch.bfloat16)
+    xp[:M] = x
+    xf = xp.view(mtt, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).contiguous().view(-1)
     for kname, fn in (("tile128", lambda: e.gemm(x, pw.data, N, out, EPI[epi], 1, 1, 4, 4, 0)),
-                      ("tile256", lambda: e.gemm_t256(x, pw.data, N, out, EPI[epi]))):
+                      ("tile256", lambda: e.gemm_t256(x, pw.data, N, out, EPI[epi])),
+                      ("tile256_xf", lambda: e.gemm_t256_xf(xf, mtt, M, pw.data, N, out, EPI[epi]))):
         fn()
         torch.cuda.synchronize()
         err = ((out.float() - ref).norm() / ref.norm()).item()
