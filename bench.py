@@ -50,6 +50,9 @@ MODEL_NAMES = {"duckdb-nsql": "duckdb-nsql-7B", "llama3.2": "Llama-3.2-3B-Instru
 
 def fp8_label(r, B):
     """Which decode GEMMs of an fp8 model run W8A8 (fp8 activations) at batch B (engine/runner.py)."""
+    if r.w.layers[0].wqkv.kind == "mxfp4":
+        return ("mxfp4 weights (e2m1 + E8M0 per 32, decode W4A16: dequantised to bf16 in registers, bf16 MFMA; "
+                "prefill on the dequantised bf16 layer), bf16 activations")
     xf = r.a8 and r.use_xfrag(B) and not (r.fused_norm and B <= r.fused_norm_max_batch)
     a8 = [name for name, on in (("qkv", xf and B > r.a8_min_batch), ("gate_up", xf and B > r.a8_mlp_min_batch)) if on]
     if not a8:
@@ -135,7 +138,9 @@ def main() -> int:
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--new-tokens", type=int, default=128)
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "mxfp4"],
+                    help="weights: bf16 | fp8 (e4m3, per-channel scales) | mxfp4 (OCP MX e2m1 + E8M0 block scales, the "
+                         "4-bit weight class of the reference's Ollama tags; W4A16 decode)")
     ap.add_argument("--kv-dtype", default=None, choices=["bf16", "fp8"],
                     help="paged KV cache dtype (default bf16; fp8 = e4m3 rows with per-row scales, ops.KV_FP8)")
     ap.add_argument("--no-graphs", action="store_true")

@@ -79,6 +79,9 @@ int lsa_ar_header_bytes();
 int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
                int nblocks, long long timeout_ticks, int* err, int nslab, long slab_stride, hipStream_t s);
 int lsa_decode_block_cnt_ints();
+int lsa_fp4_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const void* S, int N, void* out, int epi,
+                    int nb, int splitk, int waves, int xfrag, const LsaEpi* ep, hipStream_t stream);
+int lsa_fp4_dequant(const void* Wq, const void* S, int N, int K, void* Wf, hipStream_t s);
 int lsa_res_gemm(const void* X, const void* W, float* h, void* xout, long long* ss, int B, int N, int K, int* err,
                  long long timeout_ticks, int nwg, int cw, long long* stamps, hipStream_t s);
 int lsa_decode_block(const void* attn, const void* wo, float* h, void* x, long long* ss1, long long* ss2, const void* wgu,
@@ -333,6 +336,56 @@ void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscal
   check(lsa_fp8_gemm_ex(x.data_ptr(), x.stride(0), M, K, wq.data_ptr(), wscale.data_ptr<float>(), N, out.data_ptr(),
                         epi, nb, splitk, 0, eo.on ? &eo.e : nullptr, cur_stream()),
         "fp8_gemm");
+}
+
+// MXFP4 weights (kernels/gemm_fp4.hip, ops.pack_mxfp4): wq [N/16, K/128, 64, 16] e2m1 nibbles, sw [N/16, KB4, 64, 4]
+// E8M0 block scales (KB4 = ceil(K / 512))
+void check_fp4(const at::Tensor& wq, const at::Tensor& sw, int64_t N, int64_t K) {
+  TORCH_CHECK(N % 16 == 0 && K % 128 == 0, "mxfp4: N % 16 == 0, K % 128 == 0");
+  TORCH_CHECK(on_dev(wq) && wq.element_size() == 1 && wq.is_contiguous() && wq.numel() == N * K / 2,
+              "wq must be N*K/2 contiguous e2m1 bytes");
+  TORCH_CHECK(on_dev(sw) && sw.element_size() == 1 && sw.is_contiguous() && sw.numel() == (N / 16) * ((K / 128 + 3) / 4) * 256,
+              "sw must be the [N/16, ceil(K/512), 64, 4] E8M0 scale bytes");
+}
+
+void fp4_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& sw, int64_t N, at::Tensor& out, int64_t epi,
+              int64_t nb, int64_t splitk, int64_t waves, const c10::optional<at::Tensor>& rowss, double eps,
+              const c10::optional<at::Tensor>& h, const c10::optional<at::Tensor>& xout, int64_t xmt,
+              const c10::optional<at::Tensor>& ss_out, const c10::optional<at::Tensor>& tickets) {
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(M >= 1 && M <= 64, "fp4_gemm: decode rows 1..64 (prefill dequantises, fp4_dequant)");
+  check_fp4(wq, sw, N, K);
+  check_out(epi, out, splitk, M, N, 0);
+  const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, h, xout, xmt, ss_out, tickets, N / 16);
+  check(lsa_fp4_gemm_ex(x.data_ptr(), x.stride(0), M, K, wq.data_ptr(), sw.data_ptr(), N, out.data_ptr(), epi, nb, splitk,
+                        waves, 0, eo.on ? &eo.e : nullptr, cur_stream()),
+        "fp4_gemm");
+}
+
+void fp4_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& wq, const at::Tensor& sw, int64_t N,
+                 at::Tensor& out, int64_t epi, int64_t nb, int64_t splitk, int64_t waves,
+                 const c10::optional<at::Tensor>& rowss, double eps, const c10::optional<at::Tensor>& h,
+                 const c10::optional<at::Tensor>& xout, int64_t xmt, const c10::optional<at::Tensor>& ss_out,
+                 const c10::optional<at::Tensor>& tickets) {
+  need(xf, at::kBFloat16, "xf");
+  TORCH_CHECK(M >= 1 && M <= 64, "fp4_gemm_xf: M in 1..64");
+  check_fp4(wq, sw, N, K);
+  const int64_t mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  TORCH_CHECK(xf.is_contiguous() && xf.numel() >= mt * 16 * K, "xf too small");
+  check_out(epi, out, splitk, M, N, mt);
+  const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, h, xout, xmt, ss_out, tickets, N / 16);
+  check(lsa_fp4_gemm_ex(xf.data_ptr(), K, M, K, wq.data_ptr(), sw.data_ptr(), N, out.data_ptr(), epi, nb, splitk, waves,
+                        1, eo.on ? &eo.e : nullptr, cur_stream()),
+        "fp4_gemm_xf");
+}
+
+void fp4_dequant(const at::Tensor& wq, const at::Tensor& sw, int64_t N, int64_t K, at::Tensor& wf) {
+  check_fp4(wq, sw, N, K);
+  need(wf, at::kBFloat16, "wf");
+  TORCH_CHECK(wf.is_contiguous() && wf.numel() >= N * K, "fp4_dequant: output too small");
+  check(lsa_fp4_dequant(wq.data_ptr(), sw.data_ptr(), N, K, wf.data_ptr(), cur_stream()), "fp4_dequant");
 }
 
 void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t nparts, int64_t part_stride,
@@ -737,6 +790,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_t256", &gemm_t256);
+  m.def("fp4_gemm", &fp4_gemm, py::arg("x"), py::arg("wq"), py::arg("sw"), py::arg("N"), py::arg("out"), py::arg("epi"),
+        py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("rowss") = py::none(), py::arg("eps") = 1e-5,
+        py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(),
+        py::arg("tickets") = py::none());
+  m.def("fp4_gemm_xf", &fp4_gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wq"), py::arg("sw"),
+        py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4,
+        py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(),
+        py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
+  m.def("fp4_dequant", &fp4_dequant);
   m.def("gemm_t256_xf", &gemm_t256_xf);
   m.def("fp8_gemm", &fp8_gemm, py::arg("x"), py::arg("wq"), py::arg("wscale"), py::arg("N"), py::arg("out"),
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("depth") = 1,

@@ -229,7 +229,7 @@ class ModelRunner:
     def use_xfrag(self, B: int) -> bool:
         """Fragment-major activations pay off once a decode batch spans >1 row tile (B > 16):
         measured 8-20 % faster GEMMs at B = 32 (scripts/bench_xf.py); bf16 and fp8 weights."""
-        return self.on_gpu and 16 < B <= 64 and self.w.layers[0].wqkv.kind in ("bf16", "fp8")
+        return self.on_gpu and 16 < B <= 64 and self.w.layers[0].wqkv.kind in ("bf16", "fp8", "mxfp4")
 
     def _lm_head(self, xn: torch.Tensor, M: int, xf: bool = False) -> torch.Tensor:
         """logits [M, V] (f32) for the normalised rows xn [M, d] (fragment-major when xf)."""

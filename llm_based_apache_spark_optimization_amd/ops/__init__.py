@@ -103,13 +103,62 @@ def dequantize_fp8(packed: torch.Tensor, scale: torch.Tensor, N: int, K: int) ->
     return q.view(torch.float8_e4m3fn).float() * scale[:, None]
 
 
+# MXFP4 (OCP MX): e2m1 elements, one E8M0 power-of-two scale per 32 consecutive k (csrc/kernels/gemm_fp4.hip)
+FP4_VALUES = (0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0)
+_FP4_EDGES = (0.25, 0.75, 1.25, 1.75, 2.5, 3.5, 5.0)  # midpoints of the e2m1 magnitude grid
+
+
+def quantize_mxfp4(w: torch.Tensor):
+    """[N, K] -> (e2m1 codes uint8 [N, K] (sign in bit 3), E8M0 scale bytes uint8 [N, K/32]): per 32-element block
+    scale 2^(floor(log2 amax) - 2) (e2m1 emax = 2, OCP MX), elements rounded to the e2m1 grid, saturated at 6."""
+    N, K = w.shape
+    assert K % 32 == 0, K
+    wf = w.float().view(N, K // 32, 32)
+    amax = wf.abs().amax(-1)
+    e = (torch.floor(torch.log2(amax.clamp(min=2.0 ** -125))) - 2).clamp(-126, 127)
+    e = torch.where(amax > 0, e, torch.full_like(e, -127))
+    v = wf / torch.exp2(e.clamp(min=-126))[..., None]
+    mag = torch.bucketize(v.abs().clamp(max=6.0), torch.tensor(_FP4_EDGES, device=w.device))
+    codes = (mag | ((v < 0).to(mag.dtype) << 3)).to(torch.uint8).view(N, K)
+    return codes, (e + 127).to(torch.uint8)
+
+
+def pack_mxfp4(codes: torch.Tensor, sbytes: torch.Tensor):
+    """codes [N, K], scale bytes [N, K/32] -> the gemm_fp4 layouts: Wq [N/16, K/128, 64 lanes, 16 B] (lane = 16 g + r
+    holds W[16 nb + r][128 kb + 32 g .. + 31], element 2i in the low nibble of byte i) and S [N/16, ceil(K/512), 64, 4]
+    (the lane's scale byte of four consecutive 128-k steps in one word)."""
+    N, K = codes.shape
+    assert N % 16 == 0 and K % 128 == 0, (N, K)
+    c = codes.view(N, K // 2, 2)
+    packed = (c[..., 0] | (c[..., 1] << 4)).contiguous()
+    wq = packed.view(N // 16, 16, K // 128, 4, 16).permute(0, 2, 3, 1, 4).reshape(N // 16, K // 128, 64, 16)
+    kb = K // 128
+    kb4 = (kb + 3) // 4
+    sl = sbytes.view(N // 16, 16, kb, 4).permute(0, 2, 3, 1).reshape(N // 16, kb, 64)
+    sp = torch.zeros(N // 16, kb4 * 4, 64, dtype=torch.uint8, device=codes.device)
+    sp[:, :kb] = sl
+    return wq, sp.view(N // 16, kb4, 4, 64).permute(0, 1, 3, 2).contiguous()
+
+
+def dequantize_mxfp4(wq: torch.Tensor, sw: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    """The exact f32 values the gemm_fp4 kernels multiply with (e2m1 value x 2^(e - 127))."""
+    kb = K // 128
+    packed = wq.reshape(N // 16, kb, 4, 16, 16).permute(0, 3, 1, 2, 4).reshape(N, K // 2)
+    codes = torch.stack([packed & 15, packed >> 4], dim=-1).view(N, K).long()
+    vals = torch.tensor(FP4_VALUES, device=wq.device)[codes & 7] * (1.0 - 2.0 * (codes >> 3).float())
+    sb = sw.reshape(N // 16, -1, 64, 4).permute(0, 1, 3, 2).reshape(N // 16, -1, 64)[:, :kb]
+    sb = sb.reshape(N // 16, kb, 4, 16).permute(0, 3, 1, 2).reshape(N, K // 32).float()
+    scale = torch.where(sb > 0, torch.exp2(sb - 127.0), torch.zeros_like(sb))
+    return (vals.view(N, K // 32, 32) * scale[..., None]).view(N, K)
+
+
 @dataclasses.dataclass
 class PackedWeight:
     """A linear layer's weight in the layout its kernel streams."""
 
     N: int
     K: int
-    kind: str  # "dense" (CPU reference) | "bf16" (fragment layout) | "fp8"
+    kind: str  # "dense" (CPU reference) | "bf16" (fragment layout) | "fp8" | "mxfp4"
     data: torch.Tensor
     scale: Optional[torch.Tensor] = None
 
@@ -121,6 +170,9 @@ class PackedWeight:
         if kind == "fp8":
             q, s = quantize_fp8(w)
             return PackedWeight(N, K, "fp8", q, s.contiguous())
+        if kind == "mxfp4":
+            wq, sw = pack_mxfp4(*quantize_mxfp4(w))
+            return PackedWeight(N, K, "mxfp4", wq, sw)
         return PackedWeight(N, K, "bf16", shuffle_weight(w.to(torch.bfloat16)))
 
     def dense(self) -> torch.Tensor:
@@ -128,11 +180,14 @@ class PackedWeight:
             return self.data
         if self.kind == "bf16":
             return unshuffle_weight(self.data, self.N, self.K)
+        if self.kind == "mxfp4":
+            return dequantize_mxfp4(self.data, self.scale, self.N, self.K).to(torch.bfloat16)
         return dequantize_fp8(self.data, self.scale, self.N, self.K).to(torch.bfloat16)
 
     @property
     def nbytes(self) -> int:
-        return self.data.numel() * self.data.element_size()
+        return self.data.numel() * self.data.element_size() + (
+            self.scale.numel() * self.scale.element_size() if self.scale is not None else 0)
 
 
 def pick_nb_splitk(M: int, N: int, K: int, epi: str) -> tuple[int, int]:
@@ -182,6 +237,25 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
     """(nb, splitk, waves, div) for a decode GEMM: the tuning table when it has the shape (entries
     measured with fragment-major activations carry a ':xf' suffix, fp8-weight entries ':fp8'), else
     the heuristic below (div 4, 4-wave workgroups won most measured shapes)."""
+    if kind == "mxfp4":  # W4A16 decode GEMM (gemm_fp4.hip): its own sweep entries (scripts/bench_fp4_decode.py)
+        b = 1
+        while b < M:
+            b *= 2
+        e = _tuning_table().get(f"{N}x{K}:{epi}:b{b}:fp4") or _tuning_table().get(
+            f"{N}x{K}:{'f32' if epi == 'res' else epi}:b{b}:fp4")
+        if e is not None and M <= 64:
+            return e["nb"], e["splitk"], e["waves"], 4
+        nbt = N // 16
+        nb = 2 if M <= 16 else (8 if M <= 32 else 2)
+        while nb > 1 and nbt % nb:
+            nb //= 2
+        if epi == "silu":
+            nb = max(nb, 2)
+        sk, target = 1, (512 if M <= 16 else 256)
+        if epi in ("f32", "res"):
+            while (nbt // nb) * sk < target and sk < 8 and K // (128 * sk * 2) >= 4:
+                sk *= 2
+        return nb, sk, 4, 4
     if kind == "fp8a":  # W8A8 decode GEMM: its own sweep entries, else the fp8 (nb, splitk) at default knobs
         b = 1
         while b < M:
@@ -347,12 +421,31 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
                 _dq_scratch[x.device] = buf
             e.fp8_dequant(w.data, w.scale, w.N, w.K, buf)
             e.gemm(x, buf[: w.N * w.K], w.N, out, EPI[epi], nb, splitk, waves, div)
+    elif w.kind == "mxfp4":
+        if M <= 64:  # W4A16 decode GEMM, e2m1 -> bf16 in registers (v_cvt_scalef32_pk_bf16_fp4)
+            e.fp4_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, **kw)
+        else:  # prefill: dequantise the layer into a bf16 fragment-layout scratch, bf16 tile GEMM
+            e.gemm(x, _dequant_scratch(w, x.device), w.N, out, EPI[epi], nb, splitk, waves, div)
     else:
         raise ValueError(f"weight kind {w.kind} on GPU")
     return out
 
 
 FP8_W8A8 = os.environ.get("LSA_FP8_W8A8", "1") != "0"
+
+
+def _dequant_scratch(w: PackedWeight, device) -> torch.Tensor:
+    """One layer's weight dequantised to the bf16 fragment layout in a per-device scratch (prefill of quantised
+    models: one pass over 0.5-1 byte per weight, then the bf16 tile GEMM)."""
+    buf = _dq_scratch.get(device)
+    if buf is None or buf.numel() < w.N * w.K:
+        buf = torch.empty(w.N * w.K, device=device, dtype=torch.bfloat16)
+        _dq_scratch[device] = buf
+    if w.kind == "mxfp4":
+        ext().fp4_dequant(w.data, w.scale, w.N, w.K, buf)
+    else:
+        ext().fp8_dequant(w.data, w.scale, w.N, w.K, buf)
+    return buf[: w.N * w.K]
 
 
 def quantize_rows_fp8(x: torch.Tensor):
@@ -521,7 +614,7 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
     epi='silu' writes its [M, N/2] output in the fragment-major layout too (the next GEMM's input);
     for that epilogue ``out`` is a flat buffer of at least xfrag_tiles(M) * 16 * N/2 elements.
     epi='res' writes its bf16 copy of the residual in the fragment-major layout."""
-    if not _gpu(xf) or w.kind not in ("bf16", "fp8"):
+    if not _gpu(xf) or w.kind not in ("bf16", "fp8", "mxfp4"):
         if epi != "silu":
             return linear(from_xfrag(xf, M, w.K), w, epi, out, splitk, nb, waves, div, rownorm, res, _xf=True)
         y = to_xfrag(linear(from_xfrag(xf, M, w.K), w, epi, None, splitk, nb, waves, div, rownorm))
@@ -546,6 +639,8 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
     kw = _epi_kw(rownorm, res, xfrag_tiles(M))
     if w.kind == "fp8":
         ext().fp8_gemm_xf(xf, M, w.K, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, _fp8_depth(div), **kw)
+    elif w.kind == "mxfp4":
+        ext().fp4_gemm_xf(xf, M, w.K, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, **kw)
     else:
         ext().gemm_xf(xf, M, w.K, w.data, w.N, out, EPI[epi], nb, splitk, waves, div, **kw)
     return out
