@@ -89,6 +89,12 @@ struct RopeArgs {
 #ifndef LSA_ATTN_SPEC_MAX_WG
 #define LSA_ATTN_SPEC_MAX_WG 512  // grids up to this many workgroups speculate every split's first block (below)
 #endif
+#ifndef LSA_ATTN_WV23
+#define LSA_ATTN_WV23 4  // waves per workgroup for G = 2, 3 on small grids (below)
+#endif
+#ifndef LSA_ATTN_SMALL23_WG
+#define LSA_ATTN_SMALL23_WG 256
+#endif
 #ifndef LSA_ATTN_BUF_G
 #define LSA_ATTN_BUF_G 2
 #endif
@@ -604,25 +610,34 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
   uint16_t* oo = reinterpret_cast<uint16_t*>(out);
   const RopeArgs ra{qkv_parts, (size_t)part_stride, nparts, cos_t, sin_t, const_cast<uint16_t*>(kk),
                     const_cast<uint16_t*>(vv), const_cast<float*>(ks), const_cast<float*>(vs)};
+#define LSA_ADL(GV, RP, WV, KV8, SB)                                                                              \
+  hipLaunchKernelGGL((attn_decode_kernel<GV, RP, WV, KV8, SB>), grid, dim3(64 * (WV)), 0, s, qq, kk, vv, ks, vs,     \
+                     block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart,  \
+                     counters, xf_mt, ra)
+  // waves per workgroup: 8 for G = 1 (single-buffered at >= LSA_ATTN_SB_MIN_WG workgroups); for G = 2, 3 four on
+  // grids of <= LSA_ATTN_SMALL23_WG workgroups (3B batch 1, 2k context: 11.34 -> 10.74 us -- half the cross-wave
+  // merge, profiles/r3/attn_decode_wv23_ab_mi355x.jsonl) and eight above (3B batch 32: 10.54 vs 11.33 us); else 4
+  const long nwg = (long)grid.x * grid.y * grid.z;
+  const bool sb = nwg >= LSA_ATTN_SB_MIN_WG, small23 = nwg <= LSA_ATTN_SMALL23_WG;
 #define LSA_ADK(GV, RP)                                                                                               \
   do {                                                                                                                 \
-    if (ks && GV == 1 && LSA_ATTN_SB8 && (long)grid.x * grid.y * grid.z >= LSA_ATTN_SB_MIN_WG)                         \
-      hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4), true, GV == 1>), grid,                       \
-                         dim3(GV <= 3 ? 512 : 256), 0, s, qq, kk, vv, ks, vs, block_tables, max_blocks, pos, Hkv, sl2, \
-                         chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart, counters, xf_mt, ra);                   \
-    else if (ks)                                                                                                       \
-      hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4), true>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, \
-                         qq, kk, vv, ks, vs, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max,  \
-                         oo, opart, mlpart, counters, xf_mt, ra);                                                      \
-    else if (GV == 1 && (long)grid.x * grid.y * grid.z >= LSA_ATTN_SB_MIN_WG)                                          \
-      hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4), false, GV == 1>), grid,                      \
-                         dim3(GV <= 3 ? 512 : 256), 0, s, qq, kk, vv, ks, vs,                                          \
-                         block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart, \
-                         counters, xf_mt, ra);                                                                         \
-    else                                                                                                               \
-      hipLaunchKernelGGL((attn_decode_kernel<GV, RP, (GV <= 3 ? 8 : 4)>), grid, dim3(GV <= 3 ? 512 : 256), 0, s, qq,   \
-                         kk, vv, ks, vs, block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max,   \
-                         oo, opart, mlpart, counters, xf_mt, ra);                                                      \
+    if constexpr (GV == 1) {                                                                                           \
+      if (ks && LSA_ATTN_SB8 && sb) LSA_ADL(GV, RP, 8, true, true);                                                    \
+      else if (ks) LSA_ADL(GV, RP, 8, true, false);                                                                    \
+      else if (sb) LSA_ADL(GV, RP, 8, false, true);                                                                    \
+      else LSA_ADL(GV, RP, 8, false, false);                                                                           \
+    } else if constexpr (GV <= 3) {                                                                                    \
+      if (small23) {                                                                                                   \
+        if (ks) LSA_ADL(GV, RP, LSA_ATTN_WV23, true, false);                                                           \
+        else LSA_ADL(GV, RP, LSA_ATTN_WV23, false, false);                                                             \
+      } else {                                                                                                         \
+        if (ks) LSA_ADL(GV, RP, 8, true, false);                                                                       \
+        else LSA_ADL(GV, RP, 8, false, false);                                                                         \
+      }                                                                                                                \
+    } else {                                                                                                           \
+      if (ks) LSA_ADL(GV, RP, 4, true, false);                                                                         \
+      else LSA_ADL(GV, RP, 4, false, false);                                                                           \
+    }                                                                                                                  \
   } while (0)
 #define LSA_AD(GV)                                  \
   case GV:                                          \
@@ -637,6 +652,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
     LSA_AD(1) LSA_AD(2) LSA_AD(3) LSA_AD(4) LSA_AD(8)
     default: return -2;
   }
+#undef LSA_ADL
 #undef LSA_ADK
 #undef LSA_AD
   return (int)hipGetLastError();

@@ -283,9 +283,10 @@ static void launch_fe(const uint16_t* X, int ldx, int M, int KB128, const uint4*
   // 4 x MT / NB of the weight bytes) one step per chunk (registers)
 #define LSA_F4(MTV, NBV)                                                                                           \
   if (mt == MTV && nb == NBV) {                                                                                    \
-    constexpr int UV = NBV >= 8 ? 1 : 2;                                                                           \
-    if (waves == 8) launch_fx<MTV, NBV, EPI, 8, UV>(X, ldx, M, KB128, Wq, S, NBtot, out, ldo, kbps, splitk, s);   \
-    else launch_fx<MTV, NBV, EPI, 4, UV>(X, ldx, M, KB128, Wq, S, NBtot, out, ldo, kbps, splitk, s);              \
+    constexpr int U4 = NBV >= 8 ? 1 : 2; /* 4 at one row tile measured slower at batch 1 (7B 1.57 -> 1.69 ms) */ \
+    constexpr int U8 = (MTV >= 4 || NBV >= 4) ? 1 : U4; /* 8 waves: 256 VGPRs per wave, no spills */             \
+    if (waves == 8) launch_fx<MTV, NBV, EPI, 8, U8>(X, ldx, M, KB128, Wq, S, NBtot, out, ldo, kbps, splitk, s);   \
+    else launch_fx<MTV, NBV, EPI, 4, U4>(X, ldx, M, KB128, Wq, S, NBtot, out, ldo, kbps, splitk, s);              \
     return;                                                                                                        \
   }
   LSA_F4(1, 2) LSA_F4(1, 4) LSA_F4(2, 2) LSA_F4(2, 4) LSA_F4(4, 2) LSA_F4(1, 8) LSA_F4(2, 8)

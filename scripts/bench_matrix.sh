@@ -9,3 +9,5 @@ run 3b_explain_2k --model llama3.2 --batch 1 --prompt-len 2048 --new-tokens 128 
 run 7b_b32_fp8 --dtype fp8 --steps 3 --warmup 1
 run 3b_b32_bf16 --model llama3.2 --steps 3 --warmup 1
 run 7b_b1_fp8 --dtype fp8 --batch 1 --steps 3 --warmup 1
+run 7b_b32_mxfp4 --dtype mxfp4 --steps 3 --warmup 1
+run 7b_b1_mxfp4 --dtype mxfp4 --batch 1 --steps 3 --warmup 1
