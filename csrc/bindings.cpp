@@ -20,6 +20,8 @@ int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* 
 int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
                     const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
                     int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, void* x8, float* sx8, hipStream_t s);
+int lsa_res_add_ss(float* h, const float* parts, int nparts, long part_stride, void* xn, int rows, int D, int xf_mt,
+                   long long* ss_out, hipStream_t s);
 int lsa_fp8a_gemm(const void* X8, const float* sx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                   int epi, int nb, int splitk, int waves, int depth, int xfo, const LsaEpi* ep, hipStream_t stream);
 int lsa_quant_xf8(const void* x, int ldx, int M, int K, int MT, void* x8, float* sx, hipStream_t s);
@@ -415,6 +417,29 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
         "add_rmsnorm");
 }
 
+// wide raw residual add of the folded-norm decode step: h += sum parts; xn = bf16(h); ss_out[m] += sum h^2 (Q24)
+void res_add_ss(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t nparts, int64_t part_stride,
+                at::Tensor& xn, int64_t rows, int64_t D, int64_t xf_mt, at::Tensor& ss_out) {
+  need(h, at::kFloat, "h");
+  need(xn, at::kBFloat16, "xn");
+  need(ss_out, at::kLong, "ss_out");
+  TORCH_CHECK(rows > 0 && D > 0 && D % 8 == 0, "res_add_ss: bad rows / D");
+  TORCH_CHECK(h.is_contiguous() && h.numel() >= rows * D, "res_add_ss: h too small");
+  TORCH_CHECK(xn.is_contiguous() && xn.numel() >= (xf_mt > 0 ? xf_mt * 16 : rows) * D, "res_add_ss: xn too small");
+  TORCH_CHECK(xf_mt <= 0 || (D % 32 == 0 && rows <= 16 * xf_mt), "res_add_ss: xf tiles");
+  TORCH_CHECK(ss_out.is_contiguous() && ss_out.numel() >= rows, "res_add_ss: ss_out too small");
+  if (parts.has_value() && nparts > 0) {
+    need(*parts, at::kFloat, "parts");
+    TORCH_CHECK(part_stride >= rows * D && parts->numel() >= (nparts - 1) * part_stride + rows * D,
+                "res_add_ss: parts too small");
+  }
+  check(lsa_res_add_ss(h.data_ptr<float>(), parts.has_value() && nparts > 0 ? parts->data_ptr<float>() : nullptr,
+                       parts.has_value() ? (int)nparts : 0, part_stride, xn.data_ptr(), (int)rows, (int)D,
+                       (int)(xf_mt > 0 ? xf_mt : 0), reinterpret_cast<long long*>(ss_out.data_ptr<int64_t>()),
+                       cur_stream()),
+        "res_add_ss");
+}
+
 void rope_append(const at::Tensor& qkv, const at::Tensor& pos, const c10::optional<at::Tensor>& tok_seq,
                  const at::Tensor& block_tables, const at::Tensor& cos_t, const at::Tensor& sin_t, at::Tensor& q_out,
                  at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv, const c10::optional<at::Tensor>& ks,
@@ -807,6 +832,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4,
         py::arg("depth") = 1,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
+  m.def("res_add_ss", &res_add_ss, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
+        py::arg("xn"), py::arg("rows"), py::arg("D"), py::arg("xf_mt"), py::arg("ss_out"));
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
         py::arg("ids"), py::arg("emb"), py::arg("row_idx"), py::arg("write_h"), py::arg("w"), py::arg("eps"),
         py::arg("xn"), py::arg("rows"), py::arg("xf_mt") = 0, py::arg("ss_out") = py::none(), py::arg("ss_ld") = 0,

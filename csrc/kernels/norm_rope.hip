@@ -163,6 +163,83 @@ extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long pa
 }
 
 // ------------------------------------------------------------------------------------------------
+// Wide raw residual add (decode step with the RMSNorm gammas folded into the next GEMMs, which scale their
+// output rows by rsqrt(ss / D + eps)):  h[m] += sum_s parts[s][m];  xn[m] = bf16(h[m]) (fragment-major when
+// xf_mt);  ss_out[m] += sum_c h[m][c]^2 (Q24 int64 atomics, so the total does not depend on arrival order).
+// ss_out must be zero on entry (the step's embedding launch zeroes every layer's accumulator).
+// One WAVE per 512-column slice of a row: grid (D / 512, rows) of one-wave workgroups (7B batch 32: 256; 3B
+// batch 1: 6), every lane's slab loads issued before the first add, a shuffle reduction and one atomic per
+// wave -- no block-wide reduction, a single dependent memory round trip.  Replaces add_rmsnorm's one
+// 512-thread workgroup per row (whose LDS reduction and per-row serial chain are the decode-step norm cost).
+template <int NP>
+__global__ __launch_bounds__(64) void res_add_ss_kernel(float* __restrict__ h, const float* __restrict__ parts,
+                                                        int nparts, size_t part_stride, uint16_t* __restrict__ xn,
+                                                        int D, int xf_mt, long long* __restrict__ ss_out) {
+  const int m = blockIdx.y;
+  const int c = (blockIdx.x * 64 + threadIdx.x) * 8;
+  float ss = 0.f;
+  if (c < D) {
+    float* hr = h + (size_t)m * D + c;
+    const float* p = parts + (size_t)m * D + c;
+    float v[8];
+    {
+      const float4 a = *reinterpret_cast<const float4*>(hr);
+      const float4 b = *reinterpret_cast<const float4*>(hr + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+    if constexpr (NP > 0) {
+      float4 t[NP][2];
+#pragma unroll
+      for (int s = 0; s < NP; ++s) {
+        t[s][0] = *reinterpret_cast<const float4*>(p + s * part_stride);
+        t[s][1] = *reinterpret_cast<const float4*>(p + s * part_stride + 4);
+      }
+#pragma unroll
+      for (int s = 0; s < NP; ++s) {
+        v[0] += t[s][0].x; v[1] += t[s][0].y; v[2] += t[s][0].z; v[3] += t[s][0].w;
+        v[4] += t[s][1].x; v[5] += t[s][1].y; v[6] += t[s][1].z; v[7] += t[s][1].w;
+      }
+    } else {
+      for (int s = 0; s < nparts; ++s) {
+        const float4 a = *reinterpret_cast<const float4*>(p + s * part_stride);
+        const float4 b = *reinterpret_cast<const float4*>(p + s * part_stride + 4);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+    }
+    *reinterpret_cast<float4*>(hr) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(hr + 4) = make_float4(v[4], v[5], v[6], v[7]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+    *reinterpret_cast<uint4*>(xn + (xf_mt ? xf_off(m, c, xf_mt) : (size_t)m * D + c)) = pack8(v);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if (threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ss_out) + m, (unsigned long long)ss_to_q24(ss));
+}
+
+extern "C" int lsa_res_add_ss(float* h, const float* parts, int nparts, long part_stride, void* xn, int rows, int D,
+                              int xf_mt, long long* ss_out, hipStream_t s) {
+  if (D % 8 != 0 || rows <= 0 || nparts < 0 || !ss_out || !xn) return -1;
+  if (xf_mt && (D % 32 != 0 || rows > 16 * xf_mt)) return -3;
+  const dim3 grid((D / 8 + 63) / 64, rows);
+  uint16_t* o = reinterpret_cast<uint16_t*>(xn);
+#define LSA_RS(NP) \
+  hipLaunchKernelGGL((res_add_ss_kernel<NP>), grid, dim3(64), 0, s, h, parts, nparts, (size_t)part_stride, o, D, xf_mt, ss_out)
+  switch (parts ? nparts : 0) {
+    case 0: LSA_RS(0); break;
+    case 1: LSA_RS(1); break;
+    case 2: LSA_RS(2); break;
+    case 3: LSA_RS(3); break;
+    case 4: LSA_RS(4); break;
+    case 6: LSA_RS(6); break;
+    case 8: LSA_RS(8); break;
+    default: LSA_RS(-1); break;
+  }
+#undef LSA_RS
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // RoPE + paged KV append.  qkv: [T, (H + 2*Hkv) * 128]; q_out: [T, H, 128];
 // cache: [nblk, Hkv, 64, 128]; token t of sequence seq(t) at position pos(t) goes to
 // block_tables[seq * max_blocks + pos / 64], slot pos % 64.  cos/sin: [max_pos, 64] f32.

@@ -191,6 +191,13 @@ class ModelRunner:
                         and all(lw.norms_folded for lw in weights.layers))
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)
+        # buckets that keep the norm launches (above fused_norm_max_batch): the norms as WIDE raw residual adds
+        # (ops.res_add_ss: one wave per 512-column slice, Q24 row sums of squares by integer atomics) with the RMS
+        # scaling moved into the qkv / gate_up GEMMs (rownorm; gammas folded into their weights) instead of one
+        # 512-thread workgroup per row with a block reduction.  TP = 1; not with W8A8 inputs (their e4m3
+        # quantisation needs the whole-row amax in the norm launch) or the MLP residual epilogue
+        self.wide_norm = (os.environ.get("LSA_WIDE_NORM", "1") != "0" and tps == 1
+                          and all(lw.norms_folded for lw in weights.layers))
         # one persistent launch per layer for the post-attention block (ops.decode_block: o -> residual -> gate_up ->
         # down -> residual -> next qkv) at decode batches <= 64: TP = 1, bf16 weights, folded norms (LSA_DECODE_BLOCK)
         self.block_decode = (os.environ.get("LSA_DECODE_BLOCK", "0") != "0" and tps == 1 and self.d % 32 == 0
@@ -287,6 +294,10 @@ class ModelRunner:
         q8 = dict(x8=self.x8, sx8=self.sx8) if a8 else {}
         q8m = dict(x8=self.x8, sx8=self.sx8) if a8m else {}
         mres = self.mlp_res and not a8m
+        wn = self.wide_norm and not (a8 or a8m or mres)
+        ssq = self.ssq
+        rn_a = (lambda l: dict(rownorm=(ssq[2 * l], self.eps))) if wn else (lambda l: {})
+        rn_m = (lambda l: dict(rownorm=(ssq[2 * l + 1], self.eps))) if wn else (lambda l: {})
         if mres:
             sk_o = ops.pick_gemm_config(B, d, self.H * self.D, "res", xf=xf, kind=w.layers[0].wo.kind)[1]
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
@@ -303,7 +314,12 @@ class ModelRunner:
             xn, attn, act = self.xn[:B], self.attn[:B], self.act[:B]
             lin = ops.linear
         for l, lw in enumerate(w.layers):
-            if l == 0 and mres:  # the embedding launch also zeroes the MLP-side row sums of every layer
+            if l == 0 and wn:  # raw embedding rows + their sums of squares; zeroes every later accumulator
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf,
+                                ss_out=ssq.view(-1), ss_ld=self.max_slots, ss_nzero=2 * self.L)
+            elif wn:
+                ops.res_add_ss(h, d_red, xn, B, ssq[2 * l], xf=xf)
+            elif l == 0 and mres:  # the embedding launch also zeroes the MLP-side row sums of every layer
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf,
                                 ss_out=self.ssq.view(-1), ss_ld=self.max_slots, ss_nzero=2 * self.L, **q8)
             elif l == 0:
@@ -315,7 +331,7 @@ class ModelRunner:
             if a8:
                 ops.linear_a8(self.x8, self.sx8, B, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
             else:
-                lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
+                lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q, **rn_a(l))
             kc, vc = self.kv[l, 0], self.kv[l, 1]
             if not self.fuse_rope:
                 ops.rope_append(qkv_parts, pos, None, bt, self.cos, self.sin, self.q[:B], kc, vc, self.H, self.Hkv,
@@ -332,11 +348,14 @@ class ModelRunner:
             else:
                 lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
                 o_red = self._reduce_parts(o_parts)
-                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
+                if wn:
+                    ops.res_add_ss(h, o_red, xn, B, ssq[2 * l + 1], xf=xf)
+                else:
+                    ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
                 if a8m:
                     ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=act)
                 else:
-                    lin(xn, lw.w_gate_up, "silu", out=act)
+                    lin(xn, lw.w_gate_up, "silu", out=act, **rn_m(l))
             lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
             d_red = self._reduce_parts(d_parts)
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_red, rows=B, xf=xf)

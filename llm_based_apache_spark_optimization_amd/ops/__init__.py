@@ -781,6 +781,32 @@ def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
     return xn
 
 
+def res_add_ss(h: torch.Tensor, parts: Optional[torch.Tensor], xn: torch.Tensor, rows: int, ss_out: torch.Tensor,
+               xf: bool = False) -> torch.Tensor:
+    """Residual add of the folded-norm decode step (the RMSNorm gammas live in the next GEMM's weight, which scales
+    its output rows by rsqrt(ss / d + eps), ``linear(..., rownorm=(ss_out, eps))``):
+    h[:rows] += sum_s parts[s];  xn = bf16(h) (fragment-major when xf);  ss_out[:rows] += sum h^2 (Q24 int64).
+    ss_out must be zero on entry.  One wave per 512-column slice on the GPU (norm_rope.hip res_add_ss_kernel)."""
+    D = h.shape[1]
+    if not _gpu(h):
+        hv = h[:rows].float()
+        if parts is not None:
+            hv = hv + parts[:, :rows].float().sum(0)
+        h[:rows].copy_(hv)
+        x16 = hv.to(torch.bfloat16)
+        if xf:
+            f = to_xfrag(x16)
+            xn.view(-1)[: f.numel()].copy_(f)
+        else:
+            xn[:rows].copy_(x16)
+        ss_out[:rows] += ss_q24(hv.pow(2).sum(1))
+        return xn
+    nparts = parts.shape[0] if parts is not None else 0
+    stride = parts.stride(0) if parts is not None else 0
+    ext().res_add_ss(h, parts, nparts, stride, xn, rows, D, xfrag_tiles(rows) if xf else 0, ss_out)
+    return xn
+
+
 def rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, kv_scales=None):
     """RoPE of q / k and the paged-cache append of k / v.  kv_scales = (ks, vs): fp8 cache (``KV_FP8``), kc / vc
     are uint8 e4m3 bytes and every (token, kv-head) row is stored with its own f32 scale."""

@@ -33,3 +33,32 @@ if spans:
 if between:
     print(f"between steps (commit end -> next step's first kernel): median {statistics.median(between):.1f} us, "
           f"mean {statistics.mean(between):.1f} us over {len(between)} boundaries")
+
+# round level: idle stretches > 20 us anywhere in the trace (host work between a round's decode run and the next
+# round's prefill, prefill host preparation, result read-back), with the kernels on either side
+idle = []
+for a, b in zip(rows, rows[1:]):
+    g = (b[0] - a[1]) / 1e3
+    if g > 20:
+        idle.append((g, a[2][:48], b[2][:48]))
+if idle:
+    tot = sum(g for g, _, _ in idle)
+    print(f"idle stretches > 20 us: {len(idle)}, total {tot / 1e3:.2f} ms over a {(rows[-1][1] - rows[0][0]) / 1e6:.1f} ms trace")
+    by = {}
+    for g, a, b in idle:
+        k = (a, b)
+        c, s = by.get(k, (0, 0.0))
+        by[k] = (c + 1, s + g)
+    for (a, b), (c, s) in sorted(by.items(), key=lambda kv: -kv[1][1])[:12]:
+        print(f"  {c:4d} x {s / c:9.1f} us  after {a}  before {b}")
+# prefill segments: runs of tile-GEMM / prefill-attention kernels (M > 64 paths) between decode runs
+seg, segs = [], []
+for r in rows:
+    if "t256" in r[2] or "prefill" in r[2] or "rope_append" in r[2]:
+        seg.append(r)
+    elif seg and "commit_kernel" in r[2]:
+        segs.append((seg[0][0], r[1], sum(e - s for s, e, _ in seg)))
+        seg = []
+if segs:
+    print(f"prefill segments {len(segs)}: span median {statistics.median([(b - a) / 1e3 for a, b, _ in segs]):.0f} us, "
+          f"tile/attention kernel time median {statistics.median([k / 1e3 for _, _, k in segs]):.0f} us")

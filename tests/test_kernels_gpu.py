@@ -676,6 +676,35 @@ def test_add_rmsnorm_raw_mode(gpu, xf):
     assert torch.all(ss[1:3, :B] == 0) and torch.all(ss[3] == 7) and torch.all(ss[0, B:] == 7)
 
 
+@pytest.mark.parametrize("case", [(1, 3072, 4, False), (32, 4096, 2, True), (20, 4096, 3, True), (5, 2560, 0, False),
+                                  (64, 4096, 5, True)])
+def test_res_add_ss(gpu, case):
+    """Wide raw residual add (ops.res_add_ss) vs the fp32 PyTorch definition: h += sum of the split-K slabs,
+    x = bf16(h) (row-major or fragment-major), ss += sum h^2 in Q24 on top of what the accumulator holds; rows
+    past B and the slab padding untouched; bitwise identical across repeats (integer atomics)."""
+    B, d, S, xf = case
+    torch.manual_seed(B * d + S)
+    Sl = 64
+    h = torch.randn(Sl, d, device=gpu) * 4
+    parts = torch.randn(max(S, 1), B, d, device=gpu) if S else None
+    runs = []
+    for _ in range(2):
+        hh = h.clone()
+        xn = torch.zeros(ops.xfrag_tiles(B) * 16 * d if xf else B * d, device=gpu, dtype=torch.bfloat16)
+        ss = torch.full((Sl,), 1 << 23, device=gpu, dtype=torch.int64)  # 0.5 in Q24
+        ops.res_add_ss(hh[:B], parts, xn if xf else xn.view(B, d), B, ss, xf=xf)
+        torch.cuda.synchronize()
+        hv = h[:B] + (parts.sum(0) if parts is not None else 0)
+        assert torch.allclose(hh[:B], hv, atol=1e-5, rtol=1e-6)
+        assert torch.equal(hh[B:], h[B:])
+        got = ops.from_xfrag(xn, B, d) if xf else xn.view(B, d)
+        assert torch.equal(got, hh[:B].to(torch.bfloat16))
+        assert torch.allclose(ops.ss_float(ss[:B]), 0.5 + hv.pow(2).sum(1), rtol=1e-5)
+        assert torch.all(ss[B:] == 1 << 23)
+        runs.append(ss)
+    assert torch.equal(runs[0], runs[1])
+
+
 # ------------------------------------------------------------------ W8A8 fp8 prefill GEMM (block-scaled MFMA)
 def test_fp8_tile_gemm_exact_integers(gpu):
     """Small integers are exact in e4m3 and in every partial sum: the 16x16x128 f8f6f4 MFMA tile GEMM must
