@@ -189,6 +189,7 @@ class LLMEngine:
         with self._lock:
             admitted = self.sched.admit()
             t0 = time.perf_counter()
+            entries = []
             for rid in admitted:
                 req = self._reqs[rid]
                 slot = self.sched.slot(rid)
@@ -196,11 +197,13 @@ class LLMEngine:
                 self._slot_owner[slot] = rid
                 sp = req.params
                 seed = sp.seed if sp.seed is not None else (rid * 7919 + 17)
-                r.set_slot(slot, self.sched.block_table(rid), sp.max_tokens, sp.temperature, sp.top_k, sp.top_p,
-                           seed, eos_on=not sp.ignore_eos, repeat_penalty=sp.repeat_penalty,
-                           repeat_last_n=sp.repeat_last_n, prompt_ids=req.prompt_ids,
-                           defer_table=self.prefill_chunk is not None)
+                entries.append(dict(slot=slot, blocks=self.sched.block_table(rid), limit=sp.max_tokens,
+                                    temperature=sp.temperature, top_k=sp.top_k, top_p=sp.top_p, seed=seed,
+                                    eos_on=not sp.ignore_eos, repeat_penalty=sp.repeat_penalty,
+                                    repeat_last_n=sp.repeat_last_n, prompt_ids=req.prompt_ids,
+                                    defer_table=self.prefill_chunk is not None))
                 self._prefilling.append(req)
+            r.set_slots(entries)  # one batched host -> device transfer for every admitted request
             if self._prefilling:
                 done_now = self._prefill_some()
                 t1 = time.perf_counter()
@@ -250,6 +253,11 @@ class LLMEngine:
                                  buckets=TOKEN_BUCKETS, model=self.name, batch=str(B))
             done = []
             now = time.perf_counter()
+            # generated tokens of every finished row in one device -> host transfer
+            fin_rows = [(self._reqs[rid].slot, min(int(gl[i]), self._reqs[rid].params.max_tokens))
+                        for i, rid in enumerate(running) if int(fin[i])]
+            fin_toks = dict(zip([s for s, _ in fin_rows], r.tokens_of_many([s for s, _ in fin_rows],
+                                                                           [n for _, n in fin_rows])))
             for i, rid in enumerate(running):
                 self._reqs[rid].gen_host = int(gl[i])
                 q = self._reqs[rid]
@@ -261,7 +269,7 @@ class LLMEngine:
                 if int(fin[i]):
                     req = self._reqs.pop(rid)
                     n = min(int(gl[i]), req.params.max_tokens)
-                    req.output_ids = r.tokens_of(req.slot, n)
+                    req.output_ids = fin_toks[req.slot]
                     req.finished_at = now
                     r.release_slot(req.slot)
                     self._slot_owner.pop(req.slot, None)

@@ -203,6 +203,14 @@ class ModelRunner:
         self.block_decode = (os.environ.get("LSA_DECODE_BLOCK", "0") != "0" and tps == 1 and self.d % 32 == 0
                              and weights.layers[0].wqkv.kind in ("bf16", "dense")
                              and all(lw.norms_folded for lw in weights.layers))
+        # decode buckets up to this batch: the residual add + RMSNorm run in the PROLOGUE of the qkv / gate_up GEMMs
+        # (ops.linear_pre, csrc/kernels/gemm_pre.hip) -- 5 launches per layer, no norm launch and no split-K
+        # last-arriver tail (the residual stream ping-pongs between h and h2).  TP = 1, bf16 weights, folded norms
+        pm = os.environ.get("LSA_PRE_MAX_B")
+        self.pre_max_batch = (int(pm) if pm is not None else 0) if (
+            tps == 1 and weights.layers[0].wqkv.kind in ("bf16", "dense")
+            and all(lw.norms_folded for lw in weights.layers)) else 0
+        self.h2 = torch.zeros(S, self.d, **f32) if self.pre_max_batch else None
         self.blk_cnt = torch.zeros(self.L, ops.DECODE_BLOCK_CNT_INTS, dtype=torch.int32, device=dev)  # per layer
         self.blk_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graphs: dict = {}
@@ -278,6 +286,8 @@ class ModelRunner:
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         if self.block_decode and B <= 64:
             return self._decode_step_block(B, sample, plan)
+        if B <= min(self.pre_max_batch, 4):
+            return self._decode_step_pre(B, sample, plan)
         if self.fused_norm and B <= self.fused_norm_max_batch:
             return self._decode_step_fused(B, sample, plan)
         w, d = self.w, self.d
@@ -408,6 +418,42 @@ class ModelRunner:
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, rows=B, xf=xf, write_h=False)
         self._decode_tail(B, sample, xn, xf)
 
+    def _decode_step_pre(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
+        """Decode step for B <= 4 with the residual adds + RMSNorms inside the consuming GEMMs (5 launches per layer):
+
+          embed -> per layer:
+            qkv = linear_pre(h + down slabs -> h2, rms-scaled)  (f32 split-K slabs)
+            -> attn_decode (RoPE + KV append)  -> o (f32 split-K slabs)
+            -> gate_up = linear_pre(h2 + o slabs -> h, rms-scaled, SiLU*up)  -> down (f32 split-K slabs)
+          -> final RMSNorm (h + down slabs) -> lm_head -> token commit
+
+        Every qkv / gate_up workgroup rebuilds its activation rows from the f32 residual and the previous projection's
+        slabs itself (<= 64 KiB per workgroup at B <= 4), so no launch sits between two projections."""
+        w, d = self.w, self.d
+        ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
+        h, h2 = self.h[:B], self.h2[:B]
+        nqkv = (self.H + 2 * self.Hkv) * self.D
+        sk_q = ops.pre_config(B, nqkv, d, "f32")[1] if self.on_gpu else 1
+        sk_o = self._splitk(B, self.H * self.D)
+        sk_d = self._splitk(B, self.ffn_l)
+        qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
+        o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
+        d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
+        plan = plan or ops.decode_split_plan(B, self.Hkv, self.max_model_len)
+        attn, act = self.attn[:B], self.act[:B]
+        # the embedding rows into h (xn / norm output unused: layer 0's qkv prologue reads h itself)
+        ops.add_rmsnorm(h, w.layers[0].attn_norm, self.eps, self.xn[:B], ids=ids, emb=w.embed, rows=B)
+        for l, lw in enumerate(w.layers):
+            ops.linear_pre(h, d_parts if l else None, lw.wqkv, "f32", qkv_parts, B, self.eps, hout=h2, splitk=sk_q)
+            ops.attn_decode(self.q[:B], self.kv[l, 0], self.kv[l, 1], bt, pos, self.H, self.Hkv, self.scale,
+                            attn.view(B, self.H, self.D), workspace=self.attn_ws, plan=plan, qkv_parts=qkv_parts,
+                            cos=self.cos, sin=self.sin, kv_scales=self._kv_scales(l))
+            ops.linear(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
+            ops.linear_pre(h2, o_parts, lw.w_gate_up, "silu", act, B, self.eps, hout=h)
+            ops.linear(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
+        ops.add_rmsnorm(h, w.final_norm, self.eps, self.xn[:B], parts=d_parts, rows=B, write_h=False)
+        self._decode_tail(B, sample, self.xn[:B], False)
+
     def _decode_step_block(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         """Decode step with the post-attention block of every layer in ONE persistent launch (ops.decode_block):
 
@@ -525,27 +571,65 @@ class ModelRunner:
         """``defer_table``: the slot's block table stays out of the decode-visible table until its prompt's
         final prefill chunk commits (chunked-prefill interleave: decode runs in between must not append
         the idle row's k/v into the blocks the prompt is being written to)."""
-        row = torch.zeros(self.max_blocks, dtype=torch.int32)
-        row[: len(blocks)] = torch.tensor(list(blocks), dtype=torch.int32)
-        if defer_table:
-            self._pending_bt[slot] = row.to(self.device, non_blocking=True)
-            self.block_tables[slot].zero_()
-        else:
-            self._pending_bt.pop(slot, None)
-            self.block_tables[slot].copy_(row.to(self.device, non_blocking=True))
-        self.limit[slot] = min(int(limit), self.max_new_cap)
-        self.temperature[slot] = float(temperature)
-        self.top_k[slot] = int(top_k)
-        self.top_p[slot] = float(top_p)
-        self.seeds[slot] = int(seed)
-        self.eos_on[slot] = 1 if eos_on else 0
-        self.penalty[slot] = float(repeat_penalty)
-        self.last_n[slot] = max(0, min(int(repeat_last_n), REPEAT_WINDOW))
-        if repeat_penalty != 1.0:  # seed the ring with the prompt's last tokens (token at p -> column p % W)
-            ring = torch.full((REPEAT_WINDOW,), -1, dtype=torch.int32)
-            for p in range(max(0, len(prompt_ids) - REPEAT_WINDOW), len(prompt_ids)):
-                ring[p % REPEAT_WINDOW] = int(prompt_ids[p])
-            self.hist[slot].copy_(ring.to(self.device, non_blocking=True))
+        self.set_slots([dict(slot=slot, blocks=blocks, limit=limit, temperature=temperature, top_k=top_k, top_p=top_p,
+                             seed=seed, eos_on=eos_on, repeat_penalty=repeat_penalty, repeat_last_n=repeat_last_n,
+                             prompt_ids=prompt_ids, defer_table=defer_table)])
+
+    def set_slots(self, entries: Sequence[dict]) -> None:
+        """``set_slot`` for every admitted request at once (keyword dicts of set_slot's arguments): the per-slot
+        parameters travel host -> device in ONE pinned int32 + one f32 + one int64 transfer and land with one
+        index_copy per state tensor, instead of ~11 tiny copies / fills per slot (a 32-request bench round's
+        admission was ~350 small launches of host time with the GPU idle)."""
+        if not entries:
+            return
+        n, W, mb = len(entries), REPEAT_WINDOW, self.max_blocks
+        ints = torch.zeros(n, mb + 5, dtype=torch.int32)  # block-table row | limit top_k eos_on last_n visible
+        flts = torch.zeros(n, 3, dtype=torch.float32)     # temperature top_p penalty
+        seeds = torch.zeros(n, dtype=torch.int64)
+        hist = None
+        for i, e in enumerate(entries):
+            blocks = list(e["blocks"])
+            ints[i, : len(blocks)] = torch.tensor(blocks, dtype=torch.int32)
+            last_n = max(0, min(int(e.get("repeat_last_n", REPEAT_WINDOW)), W))
+            ints[i, mb:] = torch.tensor([min(int(e["limit"]), self.max_new_cap), int(e.get("top_k", 40)),
+                                         1 if e.get("eos_on", True) else 0, last_n,
+                                         0 if e.get("defer_table", False) else 1], dtype=torch.int32)
+            flts[i] = torch.tensor([float(e.get("temperature", 0.0)), float(e.get("top_p", 0.9)),
+                                    float(e.get("repeat_penalty", 1.0))])
+            seeds[i] = int(e.get("seed", 0))
+            if float(e.get("repeat_penalty", 1.0)) != 1.0:  # seed the ring with the prompt's last tokens (p -> p % W)
+                if hist is None:
+                    hist = torch.full((n, W), -1, dtype=torch.int32)
+                ids = list(e.get("prompt_ids", ()))
+                for p in range(max(0, len(ids) - W), len(ids)):
+                    hist[i, p % W] = int(ids[p])
+        if self.on_gpu:
+            ints, flts, seeds = ints.pin_memory(), flts.pin_memory(), seeds.pin_memory()
+        dv = ints.to(self.device, non_blocking=True)
+        fv = flts.to(self.device, non_blocking=True)
+        sv = seeds.to(self.device, non_blocking=True)
+        slots = [int(e["slot"]) for e in entries]
+        idx = torch.tensor(slots, dtype=torch.long).to(self.device, non_blocking=True)
+        visible = ints[:, mb + 4].tolist()
+        for i, sl in enumerate(slots):
+            if visible[i]:
+                self._pending_bt.pop(sl, None)
+            else:
+                self._pending_bt[sl] = dv[i, :mb].clone()
+        self.block_tables.index_copy_(0, idx, dv[:, :mb] * dv[:, mb + 4:mb + 5])  # deferred rows stay zero
+        self.limit.index_copy_(0, idx, dv[:, mb])
+        self.top_k.index_copy_(0, idx, dv[:, mb + 1])
+        self.eos_on.index_copy_(0, idx, dv[:, mb + 2])
+        self.last_n.index_copy_(0, idx, dv[:, mb + 3])
+        self.temperature.index_copy_(0, idx, fv[:, 0])
+        self.top_p.index_copy_(0, idx, fv[:, 1])
+        self.penalty.index_copy_(0, idx, fv[:, 2])
+        self.seeds.index_copy_(0, idx, sv)
+        if hist is not None:
+            hv = hist.pin_memory() if self.on_gpu else hist
+            hsel = torch.tensor([i for i, e in enumerate(entries) if float(e.get("repeat_penalty", 1.0)) != 1.0],
+                                dtype=torch.long)
+            self.hist.index_copy_(0, idx[hsel.to(self.device)], hv[hsel].to(self.device, non_blocking=True))
 
     def set_eos(self, ids: Sequence[int]) -> None:
         """Replace the stop-token set (same length keeps captured graphs valid; otherwise recapture)."""
@@ -771,3 +855,12 @@ class ModelRunner:
 
     def tokens_of(self, slot: int, n: int) -> list[int]:
         return self.out_tokens[slot, :n].tolist()
+
+    def tokens_of_many(self, slots: Sequence[int], ns: Sequence[int]) -> list[list[int]]:
+        """``tokens_of`` for several rows in one device -> host transfer."""
+        if not slots:
+            return []
+        m = max(ns)
+        idx = torch.tensor(list(slots), dtype=torch.long, device=self.device)
+        rows = self.out_tokens[:, :m].index_select(0, idx).cpu().tolist()
+        return [r[:k] for r, k in zip(rows, ns)]
