@@ -20,8 +20,6 @@ int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* 
 int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
                     const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
                     int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, void* x8, float* sx8, hipStream_t s);
-int lsa_gemm_pre(const float* h, const float* parts, int np, long pstride, float* hout, int M, int K, const void* Wf,
-                 int N, void* out, int epi, int nb, int splitk, int waves, int div, float eps, hipStream_t stream);
 int lsa_res_add_ss(float* h, const float* parts, int nparts, long part_stride, void* xn, int rows, int D, int xf_mt,
                    long long* ss_out, hipStream_t s);
 int lsa_fp8a_gemm(const void* X8, const float* sx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
@@ -417,43 +415,6 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
                         (int)ss_nzero, x8.has_value() ? x8->data_ptr() : nullptr,
                         sx8.has_value() ? sx8->data_ptr<float>() : nullptr, cur_stream()),
         "add_rmsnorm");
-}
-
-// decode GEMM with the residual add + RMSNorm in its activation prologue (gemm_pre.hip): x = h + sum parts,
-// hout = x, out = rms-scaled bf16(x) @ W^T (gammas folded into W); M <= 4
-void gemm_pre(const at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t nparts, int64_t part_stride,
-              const c10::optional<at::Tensor>& hout, int64_t M, const at::Tensor& wf, int64_t N, at::Tensor& out,
-              int64_t epi, int64_t nb, int64_t splitk, int64_t waves, int64_t div, double eps) {
-  need(h, at::kFloat, "h");
-  need(wf, at::kBFloat16, "wf");
-  TORCH_CHECK(M >= 1 && M <= 4, "gemm_pre: M must be 1..4");
-  TORCH_CHECK(h.dim() == 2 && h.is_contiguous() && h.size(0) >= M, "gemm_pre: h must be contiguous [>= M, K]");
-  const int64_t K = h.size(1);
-  TORCH_CHECK(K % 32 == 0 && N % 16 == 0 && wf.numel() == N * K, "gemm_pre: weight is not [N, K] fragment-major");
-  if (parts.has_value() && nparts > 0) {
-    need(*parts, at::kFloat, "parts");
-    TORCH_CHECK(nparts <= 8 && part_stride >= M * K && parts->numel() >= (nparts - 1) * part_stride + M * K,
-                "gemm_pre: parts too small");
-  }
-  if (hout.has_value()) {
-    need(*hout, at::kFloat, "hout");
-    TORCH_CHECK(hout->is_contiguous() && hout->numel() >= M * K && hout->data_ptr() != h.data_ptr(),
-                "gemm_pre: hout must hold M x K and not alias h");
-  }
-  TORCH_CHECK(splitk >= 1 && (epi == 1 || splitk == 1), "gemm_pre: only the f32 epilogue splits K");
-  const int64_t ncol = epi == 2 ? N / 2 : N;
-  if (epi == 1) {
-    need(out, at::kFloat, "out");
-    TORCH_CHECK(out.is_contiguous() && out.numel() >= splitk * M * N, "gemm_pre: out too small for the slabs");
-  } else {
-    need(out, at::kBFloat16, "out");
-    TORCH_CHECK(out.is_contiguous() && out.numel() >= M * ncol, "gemm_pre: out too small");
-  }
-  check(lsa_gemm_pre(h.data_ptr<float>(), parts.has_value() && nparts > 0 ? parts->data_ptr<float>() : nullptr,
-                     parts.has_value() ? (int)nparts : 0, part_stride,
-                     hout.has_value() ? hout->data_ptr<float>() : nullptr, (int)M, (int)K, wf.data_ptr(), (int)N,
-                     out.data_ptr(), (int)epi, (int)nb, (int)splitk, (int)waves, (int)div, (float)eps, cur_stream()),
-        "gemm_pre");
 }
 
 // wide raw residual add of the folded-norm decode step: h += sum parts; xn = bf16(h); ss_out[m] += sum h^2 (Q24)
@@ -871,9 +832,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4,
         py::arg("depth") = 1,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
-  m.def("gemm_pre", &gemm_pre, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
-        py::arg("hout"), py::arg("M"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"),
-        py::arg("splitk"), py::arg("waves"), py::arg("div"), py::arg("eps"));
   m.def("res_add_ss", &res_add_ss, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
         py::arg("xn"), py::arg("rows"), py::arg("D"), py::arg("xf_mt"), py::arg("ss_out"));
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),

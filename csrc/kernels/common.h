@@ -194,6 +194,22 @@ __device__ __forceinline__ float epi_residual4(const LsaEpi& ep, int m, int n, f
   return hv.x * hv.x + hv.y * hv.y + hv.z * hv.z + hv.w * hv.w;
 }
 
+// n-block range of a skinny decode-GEMM workgroup (gemm.hip, gemm_fp4.hip): NB blocks each when NB divides the
+// column count NBtot; otherwise (a ragged grid of ceil(NBtot / NB) workgroups) the column units -- P = 2 for the
+// interleaved gate/up pairs of a SiLU epilogue -- are dealt as evenly as possible, cnt <= NB (7B gate_up at 32 rows:
+// 688 pairs as 2-3 per workgroup on 230 CUs instead of 4 on 172).  Blocks i >= cnt re-load the workgroup's last block
+// (an L2 hit, no branch in the weight stream) and are never stored.
+template <int NB, int P>
+__device__ __forceinline__ void skinny_nblocks(int NBtot, int& nb0, int& cnt) {
+  nb0 = blockIdx.x * NB;
+  cnt = NB;
+  if (NBtot % NB) {
+    const int units = NBtot / P, G = gridDim.x, base = units / G, rem = units % G, b = blockIdx.x;
+    nb0 = (b * base + min(b, rem)) * P;
+    cnt = (base + (b < rem ? 1 : 0)) * P;
+  }
+}
+
 typedef __attribute__((address_space(1))) int lsa_g_i32;
 
 // Split-K residual epilogue, called by every workgroup of a column with its reduced tile available

@@ -73,7 +73,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int nb0 = blockIdx.x * NB;
+  int nb0, cnt;  // this workgroup's n-blocks (ragged grids: common.h skinny_nblocks)
+  skinny_nblocks<NB, EPI == EPI_SILU ? 2 : 1>(EPI == EPI_SILU ? ldo / 8 : ldo / 16, nb0, cnt);
   const int kbA = blockIdx.y * kb_per_split;
   const int kbB = min(KB, kbA + kb_per_split);
   const int nk = kbB - kbA;
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
   }
   const uint4* wp[NB];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) wp[i] = Wf + (size_t)(nb0 + i) * KB * 64 + lane;
+  for (int i = 0; i < NB; ++i) wp[i] = Wf + (size_t)(nb0 + min(i, cnt - 1)) * KB * 64 + lane;
 
   auto wload = [&](uint4 (&wr)[U][NB], int c) {
     const int kb = kbA + c * U;
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
         us += red[ww][(2 * p + 1) * MT + j][l];
       }
       const int m = j * 16 + (l & 15);
-      if (m < M) {
+      if (m < M && 2 * p < cnt) {
         const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
         const float sc = epi_row_scale(ep, m);
         f32x4_t v;
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 #pragma unroll
           for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
           const int m = j * 16 + (l & 15);
-          if (m < M) res_store_partial(rs, slab + (size_t)m * ldo + (nb0 + i) * 16 + 4 * (l >> 4), s);
+          if (m < M && i < cnt) res_store_partial(rs, slab + (size_t)m * ldo + (nb0 + i) * 16 + 4 * (l >> 4), s);
         }
         __shared__ int s_last;
         if (!res_publish_and_ticket<64 * WAVES>(ep, &s_last)) return;
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
           const int l = idx & 63, t = idx >> 6;
           const int j = t % MT, i = t / MT;
           const int m = j * 16 + (l & 15);
-          if (m < M) {
+          if (m < M && i < cnt) {
             const int n = (nb0 + i) * 16 + 4 * (l >> 4);
             atomicAdd(&ssw[m], (unsigned long long)ss_to_q24(
                 epi_residual4(ep, m, n, res_slab_sum(rs, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y) *
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 #pragma unroll
       for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
       const int m = j * 16 + (l & 15);
-      if (m < M) {
+      if (m < M && i < cnt) {
         s *= epi_row_scale(ep, m);
         const int n = (nb0 + i) * 16 + 4 * (l >> 4);
         if constexpr (EPI == EPI_RES) atomicAdd(&ssw[m], (unsigned long long)ss_to_q24(epi_residual4(ep, m, n, s)));
@@ -503,7 +504,7 @@ template <int MT, int NB, int EPI, bool XF>
 static void launch_skinny_x(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
                             int ldo, int splitk, hipStream_t s) {
   const int kbps = (KB + splitk - 1) / splitk;
-  dim3 grid(NBtot / NB, splitk);
+  dim3 grid((NBtot + NB - 1) / NB, splitk);  // ragged when NB does not divide NBtot (kernel deals the blocks)
 #define LSA_SKL(WV, DV) \
   hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF>), grid, dim3(64 * WV), 0, s, X, \
                      ldx, M, KB, Wf, out, ldo, kbps, g_epi)
@@ -630,7 +631,10 @@ extern "C" int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf,
   if (M <= 64) {
     if (nb <= 0) nb = 1;
     if (epi == EPI_SILU && nb < 2) nb = 2;
-    if (NBtot % nb != 0) return -2;
+    // a ragged grid (nb not dividing the n-blocks) needs >= 1 column unit per workgroup; SiLU units are pairs
+    if (NBtot % nb != 0 && (epi == EPI_SILU ? (nb % 2 || NBtot % 2 || NBtot / 2 < (NBtot + nb - 1) / nb)
+                                              : NBtot < (NBtot + nb - 1) / nb))
+      return -2;
     if (splitk < 1) splitk = 1;
     if (epi != EPI_F32 && epi != EPI_RES && splitk != 1) return -3;
     if (M > 32 && nb > 2) nb = 2;

@@ -48,7 +48,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp4_skinny_kernel(const uint1
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int nb0 = blockIdx.x * NB;
+  int nb0, cnt;  // this workgroup's n-blocks (ragged grids: common.h skinny_nblocks)
+  skinny_nblocks<NB, EPI == EPI_SILU ? 2 : 1>(EPI == EPI_SILU ? ldo / 8 : ldo / 16, nb0, cnt);
   const int kbA = blockIdx.y * kb_per_split;
   const int kbB = min(KB128, kbA + kb_per_split);
   const int nk = kbB - kbA;
@@ -77,8 +78,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp4_skinny_kernel(const uint1
   const uint32_t* sp[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    wp[i] = Wq + (size_t)(nb0 + i) * KB128 * 64 + lane;
-    sp[i] = Sw + (size_t)(nb0 + i) * KB4 * 64 + lane;
+    wp[i] = Wq + (size_t)(nb0 + min(i, cnt - 1)) * KB128 * 64 + lane;
+    sp[i] = Sw + (size_t)(nb0 + min(i, cnt - 1)) * KB4 * 64 + lane;
   }
 
   auto load = [&](uint4 (&wr)[U][NB], uint32_t (&sr)[U][NB], uint4 (&xr)[U][MT][4], int c) {
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp4_skinny_kernel(const uint1
         us += red[ww][(2 * p + 1) * MT + j][l];
       }
       const int m = j * 16 + (l & 15);
-      if (m < M) {
+      if (m < M && 2 * p < cnt) {
         const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
         const float sc = epi_row_scale(ep, m);
         float v[4];
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp4_skinny_kernel(const uint1
 #pragma unroll
           for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
           const int m = j * 16 + (l & 15);
-          if (m < M) res_store_partial(rsc, slab + (size_t)m * ldo + (nb0 + i) * 16 + 4 * (l >> 4), s);
+          if (m < M && i < cnt) res_store_partial(rsc, slab + (size_t)m * ldo + (nb0 + i) * 16 + 4 * (l >> 4), s);
         }
         __shared__ int s_last;
         if (!res_publish_and_ticket<64 * WAVES>(ep, &s_last)) return;
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp4_skinny_kernel(const uint1
           const int l = idx & 63, t = idx >> 6;
           const int j = t % MT, i = t / MT;
           const int m = j * 16 + (l & 15);
-          if (m < M) {
+          if (m < M && i < cnt) {
             const int n = (nb0 + i) * 16 + 4 * (l >> 4);
             atomicAdd(&ssw[m], (unsigned long long)ss_to_q24(
                 epi_residual4(ep, m, n, res_slab_sum(rsc, (size_t)m * ldo + n, (size_t)M * ldo, gridDim.y) *
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_fp4_skinny_kernel(const uint1
 #pragma unroll
       for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
       const int m = j * 16 + (l & 15);
-      if (m >= M) continue;
+      if (m >= M || i >= cnt) continue;
       const int n = (nb0 + i) * 16 + 4 * (l >> 4);
       s *= epi_row_scale(ep, m);
       if constexpr (EPI == EPI_RES) {
@@ -266,10 +267,10 @@ template <int MT, int NB, int EPI, int WV, int U>
 static void launch_fx(const uint16_t* X, int ldx, int M, int KB128, const uint4* Wq, const uint32_t* S, int NBtot,
                       void* out, int ldo, int kbps, int splitk, hipStream_t s) {
   if (g_fp4_xfrag)
-    hipLaunchKernelGGL((gemm_fp4_skinny_kernel<MT, NB, EPI, WV, U, true>), dim3(NBtot / NB, splitk), dim3(64 * WV), 0,
+    hipLaunchKernelGGL((gemm_fp4_skinny_kernel<MT, NB, EPI, WV, U, true>), dim3((NBtot + NB - 1) / NB, splitk), dim3(64 * WV), 0,
                        s, X, ldx, M, KB128, Wq, S, out, ldo, kbps, g_fp4_epi);
   else
-    hipLaunchKernelGGL((gemm_fp4_skinny_kernel<MT, NB, EPI, WV, U, false>), dim3(NBtot / NB, splitk), dim3(64 * WV), 0,
+    hipLaunchKernelGGL((gemm_fp4_skinny_kernel<MT, NB, EPI, WV, U, false>), dim3((NBtot + NB - 1) / NB, splitk), dim3(64 * WV), 0,
                        s, X, ldx, M, KB128, Wq, S, out, ldo, kbps, g_fp4_epi);
 }
 
@@ -289,7 +290,7 @@ static void launch_fe(const uint16_t* X, int ldx, int M, int KB128, const uint4*
     else launch_fx<MTV, NBV, EPI, 4, U4>(X, ldx, M, KB128, Wq, S, NBtot, out, ldo, kbps, splitk, s);              \
     return;                                                                                                        \
   }
-  LSA_F4(1, 2) LSA_F4(1, 4) LSA_F4(2, 2) LSA_F4(2, 4) LSA_F4(4, 2) LSA_F4(1, 8) LSA_F4(2, 8)
+  LSA_F4(1, 2) LSA_F4(1, 4) LSA_F4(2, 2) LSA_F4(2, 4) LSA_F4(4, 2) LSA_F4(1, 8) LSA_F4(2, 8) LSA_F4(2, 6)
   if constexpr (EPI != EPI_SILU) { LSA_F4(1, 1) LSA_F4(2, 1) LSA_F4(4, 1) }
 #undef LSA_F4
   // unsupported nb: nb = 2 at the same row-tile count
@@ -323,7 +324,10 @@ extern "C" int lsa_fp4_gemm_ex(const void* X, int ldx, int M, int K, const void*
   const int ldo = (epi == EPI_SILU) ? N / 2 : N;
   if (nb <= 0) nb = 1;
   if (epi == EPI_SILU && nb < 2) nb = 2;
-  if (NBtot % nb != 0) return -2;
+  // a ragged grid (nb not dividing the n-blocks) needs >= 1 column unit per workgroup; SiLU units are pairs
+  if (NBtot % nb != 0 && (epi == EPI_SILU ? (nb % 2 || NBtot % 2 || NBtot / 2 < (NBtot + nb - 1) / nb)
+                                            : NBtot < (NBtot + nb - 1) / nb))
+    return -2;
   if (splitk < 1) splitk = 1;
   if (epi != EPI_F32 && epi != EPI_RES && splitk != 1) return -3;
   if (M > 32 && nb > 2) nb = 2;

@@ -45,7 +45,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r = lane & 15;
-  const int nb0 = blockIdx.x * NB;
+  int nb0, cnt;  // this workgroup's n-blocks (ragged grids: common.h skinny_nblocks)
+  skinny_nblocks<NB, EPI == EPI_SILU ? 2 : 1>(EPI == EPI_SILU ? ldo / 8 : ldo / 16, nb0, cnt);
   const int kbA = blockIdx.y * kb_per_split;
   const int kbB = min(KB128, kbA + kb_per_split);
   const int nk = kbB - kbA;
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
   for (int j = 0; j < MT; ++j) xvalid[j] = j * 16 + r < M;
   const uint4* wp[NB];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) wp[i] = Wq + (size_t)(nb0 + i) * (2 * KB128) * 64 + lane;
+  for (int i = 0; i < NB; ++i) wp[i] = Wq + (size_t)(nb0 + min(i, cnt - 1)) * (2 * KB128) * 64 + lane;
   const uint4* xp = X8 + 2 * lane;
 
   auto load = [&](uint4 (&wr)[U][NB][2], uint4 (&xr)[U][MT][2], int c) {
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
         us += red[ww][(2 * p + 1) * MT + j][l];
       }
       const int m = j * 16 + (l & 15);
-      if (m < M) {
+      if (m < M && 2 * p < cnt) {
         const int nrow_g = (nb0 + 2 * p) * 16 + 4 * (l >> 4);
         const int nrow_u = nrow_g + 16;
         const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
 #pragma unroll
       for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
       const int m = j * 16 + (l & 15);
-      if (m >= M) continue;
+      if (m >= M || i >= cnt) continue;
       const int n = (nb0 + i) * 16 + 4 * (l >> 4);
       const float4 sc = *reinterpret_cast<const float4*>(wscale + n);
       const float rs = sx[m] * epi_row_scale(ep, m);
@@ -180,10 +181,10 @@ static void launch_a8_x(const uint4* X8, const float* sx, int M, int KB128, cons
                         void* out, int ldo, int splitk, hipStream_t s) {
   const int kbps = (KB128 + splitk - 1) / splitk;
   if (g_a8_xfo)
-    hipLaunchKernelGGL((gemm_a8_skinny_kernel<MT, NB, EPI, WV, U, true>), dim3(NBtot / NB, splitk), dim3(64 * WV), 0, s,
+    hipLaunchKernelGGL((gemm_a8_skinny_kernel<MT, NB, EPI, WV, U, true>), dim3((NBtot + NB - 1) / NB, splitk), dim3(64 * WV), 0, s,
                        X8, sx, M, KB128, Wq, sc, out, ldo, kbps, g_a8_epi);
   else
-    hipLaunchKernelGGL((gemm_a8_skinny_kernel<MT, NB, EPI, WV, U, false>), dim3(NBtot / NB, splitk), dim3(64 * WV), 0, s,
+    hipLaunchKernelGGL((gemm_a8_skinny_kernel<MT, NB, EPI, WV, U, false>), dim3((NBtot + NB - 1) / NB, splitk), dim3(64 * WV), 0, s,
                        X8, sx, M, KB128, Wq, sc, out, ldo, kbps, g_a8_epi);
 }
 
@@ -237,7 +238,10 @@ extern "C" int lsa_fp8a_gemm(const void* X8, const float* sx, int M, int K, cons
   if (nb <= 0) nb = 2;
   if (epi == EPI_SILU && nb < 2) nb = 2;
   if (M > 32 && nb > 2) nb = 2;
-  if (NBtot % nb != 0) return -2;
+  // a ragged grid (nb not dividing the n-blocks) needs >= 1 column unit per workgroup; SiLU units are pairs
+  if (NBtot % nb != 0 && (epi == EPI_SILU ? (nb % 2 || NBtot % 2 || NBtot / 2 < (NBtot + nb - 1) / nb)
+                                            : NBtot < (NBtot + nb - 1) / nb))
+    return -2;
   if (splitk < 1) splitk = 1;
   if (epi == EPI_SILU && splitk != 1) return -3;
   if ((KB128 + ((KB128 + splitk - 1) / splitk) - 1) / ((KB128 + splitk - 1) / splitk) != splitk) return -3;

@@ -203,14 +203,6 @@ class ModelRunner:
         self.block_decode = (os.environ.get("LSA_DECODE_BLOCK", "0") != "0" and tps == 1 and self.d % 32 == 0
                              and weights.layers[0].wqkv.kind in ("bf16", "dense")
                              and all(lw.norms_folded for lw in weights.layers))
-        # decode buckets up to this batch: the residual add + RMSNorm run in the PROLOGUE of the qkv / gate_up GEMMs
-        # (ops.linear_pre, csrc/kernels/gemm_pre.hip) -- 5 launches per layer, no norm launch and no split-K
-        # last-arriver tail (the residual stream ping-pongs between h and h2).  TP = 1, bf16 weights, folded norms
-        pm = os.environ.get("LSA_PRE_MAX_B")
-        self.pre_max_batch = (int(pm) if pm is not None else 0) if (
-            tps == 1 and weights.layers[0].wqkv.kind in ("bf16", "dense")
-            and all(lw.norms_folded for lw in weights.layers)) else 0
-        self.h2 = torch.zeros(S, self.d, **f32) if self.pre_max_batch else None
         self.blk_cnt = torch.zeros(self.L, ops.DECODE_BLOCK_CNT_INTS, dtype=torch.int32, device=dev)  # per layer
         self.blk_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graphs: dict = {}
@@ -286,8 +278,6 @@ class ModelRunner:
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         if self.block_decode and B <= 64:
             return self._decode_step_block(B, sample, plan)
-        if B <= min(self.pre_max_batch, 4):
-            return self._decode_step_pre(B, sample, plan)
         if self.fused_norm and B <= self.fused_norm_max_batch:
             return self._decode_step_fused(B, sample, plan)
         w, d = self.w, self.d
@@ -417,42 +407,6 @@ class ModelRunner:
             lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk))
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, rows=B, xf=xf, write_h=False)
         self._decode_tail(B, sample, xn, xf)
-
-    def _decode_step_pre(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
-        """Decode step for B <= 4 with the residual adds + RMSNorms inside the consuming GEMMs (5 launches per layer):
-
-          embed -> per layer:
-            qkv = linear_pre(h + down slabs -> h2, rms-scaled)  (f32 split-K slabs)
-            -> attn_decode (RoPE + KV append)  -> o (f32 split-K slabs)
-            -> gate_up = linear_pre(h2 + o slabs -> h, rms-scaled, SiLU*up)  -> down (f32 split-K slabs)
-          -> final RMSNorm (h + down slabs) -> lm_head -> token commit
-
-        Every qkv / gate_up workgroup rebuilds its activation rows from the f32 residual and the previous projection's
-        slabs itself (<= 64 KiB per workgroup at B <= 4), so no launch sits between two projections."""
-        w, d = self.w, self.d
-        ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
-        h, h2 = self.h[:B], self.h2[:B]
-        nqkv = (self.H + 2 * self.Hkv) * self.D
-        sk_q = ops.pre_config(B, nqkv, d, "f32")[1] if self.on_gpu else 1
-        sk_o = self._splitk(B, self.H * self.D)
-        sk_d = self._splitk(B, self.ffn_l)
-        qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
-        o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
-        d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
-        plan = plan or ops.decode_split_plan(B, self.Hkv, self.max_model_len)
-        attn, act = self.attn[:B], self.act[:B]
-        # the embedding rows into h (xn / norm output unused: layer 0's qkv prologue reads h itself)
-        ops.add_rmsnorm(h, w.layers[0].attn_norm, self.eps, self.xn[:B], ids=ids, emb=w.embed, rows=B)
-        for l, lw in enumerate(w.layers):
-            ops.linear_pre(h, d_parts if l else None, lw.wqkv, "f32", qkv_parts, B, self.eps, hout=h2, splitk=sk_q)
-            ops.attn_decode(self.q[:B], self.kv[l, 0], self.kv[l, 1], bt, pos, self.H, self.Hkv, self.scale,
-                            attn.view(B, self.H, self.D), workspace=self.attn_ws, plan=plan, qkv_parts=qkv_parts,
-                            cos=self.cos, sin=self.sin, kv_scales=self._kv_scales(l))
-            ops.linear(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
-            ops.linear_pre(h2, o_parts, lw.w_gate_up, "silu", act, B, self.eps, hout=h)
-            ops.linear(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
-        ops.add_rmsnorm(h, w.final_norm, self.eps, self.xn[:B], parts=d_parts, rows=B, write_h=False)
-        self._decode_tail(B, sample, self.xn[:B], False)
 
     def _decode_step_block(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         """Decode step with the post-attention block of every layer in ONE persistent launch (ops.decode_block):

@@ -781,54 +781,6 @@ def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
     return xn
 
 
-PRE_NB = {"f32": (1, 2, 4), "bf16": (1, 2), "silu": (2, 4, 8)}  # n-block widths gemm_pre.hip instantiates
-
-
-def pre_config(M: int, N: int, K: int, epi: str) -> tuple[int, int, int, int]:
-    """(nb, splitk, waves, div) of a prologue-add GEMM: the decode tuning-table pick for the same shape, clamped to
-    the instantiated widths (waves 4 | 8)."""
-    nb, sk, wv, dv = pick_gemm_config(M, N, K, epi)
-    allowed = PRE_NB[epi]
-    nb = max([b for b in allowed if b <= nb and (N // 16) % b == 0] or [allowed[0]])
-    return nb, (sk if epi == "f32" else 1), (8 if wv >= 8 else 4), dv
-
-
-def linear_pre(h: torch.Tensor, parts: Optional[torch.Tensor], w: PackedWeight, epi: str, out: torch.Tensor,
-               M: int, eps: float, hout: Optional[torch.Tensor] = None, splitk: Optional[int] = None) -> torch.Tensor:
-    """Decode projection with the residual add + RMSNorm in its prologue (csrc/kernels/gemm_pre.hip, M <= 4):
-    x = h[:M] + sum_s parts[s];  hout[:M] = x;  out = rsqrt(mean(x^2) + eps) * (bf16(x) @ W^T) with the norm gamma
-    folded into W.  epi 'f32' writes [splitk, M, N] slabs (each scaled by the full-row RMS), 'silu' the bf16
-    silu(gate) * up, 'bf16' a bf16 row block."""
-    K = h.shape[1]
-    assert K == w.K and 1 <= M <= 4
-    if not _gpu(h):
-        x = h[:M].float()
-        if parts is not None:
-            x = x + parts[:, :M].float().sum(0)
-        if hout is not None:
-            hout[:M].copy_(x)
-        sc = torch.rsqrt(x.pow(2).mean(1, keepdim=True) + eps)
-        y = ref.linear(x.to(torch.bfloat16), w.dense(), "f32").float() * sc
-        if epi == "silu":
-            y3 = y.view(M, w.N // 32, 2, 16)
-            res = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, w.N // 2).to(torch.bfloat16)
-            out.view(-1)[: res.numel()].copy_(res.reshape(-1))
-        elif epi == "f32":
-            sk = splitk or 1
-            out.view(-1)[: sk * M * w.N].zero_()
-            out.view(-1)[: M * w.N].copy_(y.reshape(-1))  # slab 0 carries the product, the rest are zero
-        else:
-            out.view(-1)[: M * w.N].copy_(y.to(torch.bfloat16).reshape(-1))
-        return out
-    assert w.kind == "bf16", "the prologue-add GEMM streams bf16 fragment-major weights"
-    nb, sk, wv, dv = pre_config(M, w.N, K, epi)
-    sk = sk if splitk is None else splitk
-    nparts = parts.shape[0] if parts is not None else 0
-    stride = parts.stride(0) if parts is not None else 0
-    ext().gemm_pre(h, parts, nparts, stride, hout, M, w.data, w.N, out, EPI[epi], nb, sk, wv, dv, float(eps))
-    return out
-
-
 def res_add_ss(h: torch.Tensor, parts: Optional[torch.Tensor], xn: torch.Tensor, rows: int, ss_out: torch.Tensor,
                xf: bool = False) -> torch.Tensor:
     """Residual add of the folded-norm decode step (the RMSNorm gammas live in the next GEMM's weight, which scales

@@ -676,43 +676,6 @@ def test_add_rmsnorm_raw_mode(gpu, xf):
     assert torch.all(ss[1:3, :B] == 0) and torch.all(ss[3] == 7) and torch.all(ss[0, B:] == 7)
 
 
-@pytest.mark.parametrize("case", [(1, 3072, 5120, "f32", 2, 2), (1, 4096, 22016, "silu", 4, 1), (3, 3072, 16384, "silu", 0, 1),
-                                  (4, 4096, 12288, "f32", 8, 3), (2, 2048, 1024, "bf16", 1, 1), (1, 3072, 3072, "f32", 1, 1)])
-def test_linear_pre(gpu, case):
-    """Prologue-add decode GEMM (ops.linear_pre, gemm_pre.hip) vs the fp32 definition: x = h + sum slabs,
-    hout = x, y = rsqrt(mean(x^2) + eps) * (bf16(x) @ W^T) (bf16 / f32 slabs / SiLU(gate)*up), h left untouched,
-    slabs summing to y, bitwise repeatable."""
-    M, K, N, epi, S, sk = case
-    torch.manual_seed(M * K + N)
-    Sl = 8
-    h = torch.randn(Sl, K, device=gpu) * 3
-    parts = torch.randn(S, M, K, device=gpu) if S else None
-    wd = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
-    pw = ops.PackedWeight.from_dense(wd)
-    x = h[:M] + (parts.sum(0) if parts is not None else 0)
-    sc = torch.rsqrt(x.pow(2).mean(1, keepdim=True) + 1e-5)
-    yr = (x.to(torch.bfloat16).float() @ wd.float().t()) * sc
-    if epi == "silu":
-        y3 = yr.view(M, N // 32, 2, 16)
-        yr = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, N // 2)
-    outs = []
-    for _ in range(2):
-        hb = h.clone()
-        hout = torch.full((Sl, K), 7.0, device=gpu)
-        if epi == "f32":
-            out = torch.zeros(sk, M, N, device=gpu)
-        else:
-            out = torch.zeros(M, N // 2 if epi == "silu" else N, device=gpu, dtype=torch.bfloat16)
-        ops.linear_pre(hb, parts, pw, epi, out, M, 1e-5, hout=hout, splitk=sk if epi == "f32" else None)
-        torch.cuda.synchronize()
-        assert torch.equal(hb, h)
-        assert torch.allclose(hout[:M], x, atol=1e-5) and torch.all(hout[M:] == 7.0)
-        got = out.sum(0) if epi == "f32" else out.float()
-        assert _rel(got, yr) < 1e-2, (epi, _rel(got, yr))
-        outs.append(out.clone())
-    assert torch.equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("case", [(1, 3072, 4, False), (32, 4096, 2, True), (20, 4096, 3, True), (5, 2560, 0, False),
                                   (64, 4096, 5, True)])
 def test_res_add_ss(gpu, case):
