@@ -215,7 +215,7 @@ def pick_nb_splitk(M: int, N: int, K: int, epi: str) -> tuple[int, int]:
 
 
 # ----------------------------------------------------------------------------------- tuning
-_TUNING_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
+_TUNING_PATH = os.environ.get("LSA_GEMM_TUNING") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _tuning: Optional[dict] = None
 
 

@@ -13,7 +13,8 @@ from llm_based_apache_spark_optimization_amd import ops  # noqa: E402
 
 dev = torch.device("cuda:0")
 SHAPES = {"7b_gateup": (22016, 4096, "silu"), "7b_qkv": (12288, 4096, "f32"), "7b_head": (32000, 4096, "f32"),
-          "3b_gateup": (16384, 3072, "silu"), "3b_qkv": (5120, 3072, "f32")}
+          "3b_gateup": (16384, 3072, "silu"), "3b_qkv": (5120, 3072, "f32"), "7b_down": (4096, 11008, "f32"),
+          "7b_o": (4096, 4096, "f32"), "3b_down": (3072, 8192, "f32"), "3b_o": (3072, 3072, "f32")}
 Ms = [int(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 32]
 if len(sys.argv) > 2:
     SHAPES = {k: v for k, v in SHAPES.items() if k in sys.argv[2].split(",")}
@@ -53,7 +54,7 @@ for name, (N, K, epi) in SHAPES.items():
         cands = {tuple(pick)}
         for nb in (4, 6, 8):
             for dv in ((1, 2) if KIND == "bf16" else (4,) if KIND == "mxfp4" else (2, 4)):
-                for sk in ((1,) if epi == "silu" else (1, 2)):
+                for sk in ((1,) if epi == "silu" else (1, 2, 4, 8)):
                     for wv in ((4,) if KIND == "bf16" else (4, 8)):  # (fp8a: div 2 = depth 2, 4 = depth 1)
                         cands.add((nb, sk, wv, dv))
         for nb, sk, wv, dv in sorted(cands):
