@@ -52,14 +52,14 @@ for name, (N, K, epi) in SHAPES.items():
         pick = ops.pick_gemm_config(M, N, K, epi, xf=True, kind=KIND) if KIND == "fp8a" else \
             ops.pick_gemm_config(M, N, K, epi, xf=xf, kind=KIND)
         cands = {tuple(pick)}
-        for nb in (4, 6, 8):
+        for nb in ((4, 6, 8) if KIND == "bf16" else (1, 2, 4, 6, 8)):
             for dv in ((1, 2) if KIND == "bf16" else (4,) if KIND == "mxfp4" else (2, 4)):
                 for sk in ((1,) if epi == "silu" else (1, 2, 4, 8)):
                     for wv in ((4,) if KIND == "bf16" else (4, 8)):  # (fp8a: div 2 = depth 2, 4 = depth 1)
                         cands.add((nb, sk, wv, dv))
         for nb, sk, wv, dv in sorted(cands):
-            if (epi == "silu" and nb % 2) or (M > 32 and nb > 2):
-                continue
+            if (epi == "silu" and nb % 2) or (M > 32 and nb > 2) or (nb == 6 and M <= 16):
+                continue  # (nb 6 is instantiated for two row tiles only; one row tile would fall back to nb 2)
             if epi == "silu":
                 out = torch.empty(ops.xfrag_tiles(M) * 16 * (N // 2) if xf else M * N // 2, device=dev,
                                   dtype=torch.bfloat16)
