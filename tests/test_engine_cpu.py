@@ -215,3 +215,24 @@ def test_chunked_prefill_interleave_matches_whole_prompt():
     assert eng.result(a).token_ids == want[0]
     assert eng.result(b).token_ids == want[1]
     assert not eng._prefilling and not eng.runner._pending_bt
+
+
+def test_set_slots_batched_equals_per_slot():
+    """Batched admission (ModelRunner.set_slots: one transfer + one index_copy per state tensor) leaves exactly the
+    device state that per-slot set_slot calls leave, including deferred block tables and repetition-penalty rings."""
+    entries = [dict(slot=0, blocks=[3, 4], limit=7, temperature=0.0, top_k=40, top_p=0.9, seed=11, eos_on=True),
+               dict(slot=2, blocks=[5], limit=99, temperature=0.7, top_k=5, top_p=0.5, seed=12, eos_on=False,
+                    repeat_penalty=1.2, repeat_last_n=8, prompt_ids=list(range(100, 180))),
+               dict(slot=3, blocks=[6, 7, 8], limit=3, temperature=1.0, top_k=1, top_p=1.0, seed=13, eos_on=True,
+                    defer_table=True)]
+    engs = [build_engine("tiny-nsql", device="cpu", max_slots=4, max_model_len=512) for _ in range(2)]
+    a, b = engs[0].runner, engs[1].runner
+    for e in entries:
+        a.set_slot(**e)
+    b.set_slots(entries)
+    for name in ("block_tables", "limit", "top_k", "eos_on", "last_n", "temperature", "top_p", "penalty", "seeds",
+                 "hist"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert set(a._pending_bt) == set(b._pending_bt) == {3}
+    assert torch.equal(a._pending_bt[3], b._pending_bt[3])
+    assert b.block_tables[3].abs().sum() == 0 and b._pending_bt[3][:3].tolist() == [6, 7, 8]

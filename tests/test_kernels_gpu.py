@@ -831,3 +831,47 @@ def test_add_rmsnorm_fp8_output(gpu, M):
     assert _rel(got, want) < 4e-2
     assert _rel(ops.from_xfrag(xn, M, d).float(), want) < 1e-2  # the bf16 copy is still written
 
+
+
+@pytest.mark.parametrize("kind", ["bf16", "mxfp4", "fp8a"])
+@pytest.mark.parametrize("M", [1, 9, 32])
+@pytest.mark.parametrize("nb", [4, 6, 8])
+def test_gemm_ragged_grid(gpu, kind, M, nb):
+    """Ragged decode-GEMM grids (common.h skinny_nblocks): 172 n-blocks (86 gate/up pairs; the 7B gate_up's 1376 / 8)
+    are not a multiple of nb = 6 or 8, so ceil(172 / nb) workgroups share them 1-2 blocks / pairs apart (nb 4: the
+    divisible grid); every column written exactly once, vs fp32, for the bf16, MXFP4 and W8A8 decode kernels (f32
+    split-K slabs and the SiLU epilogue)."""
+    if kind == "fp8a" and M <= 16:
+        pytest.skip("W8A8 decode runs the fragment-major buckets above 16 rows")
+    if nb == 6 and M <= 16:
+        pytest.skip("nb 6 is instantiated for the two-row-tile kernels")
+    N, K = 16 * 172, 1024
+    torch.manual_seed(M * 31 + nb)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+    wkind = "fp8" if kind == "fp8a" else kind
+    pw = ops.PackedWeight.from_dense(w, wkind)
+    # the exact weights the kernel multiplies (fp8: e4m3 x f32 channel scale, not rounded to bf16)
+    wd = ops.dequantize_fp8(pw.data, pw.scale, N, K).float() if wkind == "fp8" else pw.dense().float()
+    xf = 16 < M <= 64
+    if kind == "fp8a":
+        x8, sx = ops.quantize_xf8(x)
+        xe = ops.from_xf8(x8, M, K).view(torch.float8_e4m3fn).float() * sx[:, None]
+    else:
+        xe = x.float()
+    yr = xe @ wd.t()
+    y3 = yr.view(M, N // 32, 2, 16)
+    want_silu = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, N // 2)
+    for epi in ("f32", "silu"):
+        sk = 2 if epi == "f32" else 1
+        if kind == "fp8a":
+            y = ops.linear_a8(x8, sx, M, pw, epi, splitk=sk, nb=nb, xfo=True)
+        elif xf:
+            y = ops.linear_xf(ops.to_xfrag(x), M, pw, epi, splitk=sk, nb=nb)
+        else:
+            y = ops.linear(x, pw, epi, splitk=sk, nb=nb)
+        if epi == "f32":
+            assert y.shape[0] == sk and _rel(y.sum(0), yr) < 1e-4, (kind, epi)
+        else:
+            got = ops.from_xfrag(y, M, N // 2) if (xf or kind == "fp8a") else y.view(M, N // 2)
+            assert _rel(got, want_silu) < 1e-2, (kind, epi)
