@@ -115,6 +115,12 @@ int main() {
     expect_reject("add_rmsnorm ss too small", [&] { add_rmsnorm(h, none, 0, 0, none, none, none, true, w, 1e-5, xn, 4, 0, ss, 4, 3, none, none); });
     auto x8 = T({8}, U8), sx8 = T({4}, F32);
     expect_reject("add_rmsnorm x8 too small", [&] { add_rmsnorm(h, none, 0, 0, none, none, none, true, w, 1e-5, xn, 4, 1, none, 0, 0, x8, sx8); });
+    auto hr = T({4, 1024}, F32), pr = T({2, 4, 1024}, F32), xr = T({4, 1024}, BF), ss1 = T({4}, I64);
+    auto ss_small = T({3}, I64), xr_small = T({3, 1024}, BF);
+    expect_ok("res_add_ss", [&] { res_add_ss(hr, pr, 2, 4 * 1024, xr, 4, 1024, 0, ss1); });
+    expect_reject("res_add_ss ss too small", [&] { res_add_ss(hr, pr, 2, 4 * 1024, xr, 4, 1024, 0, ss_small); });
+    expect_reject("res_add_ss xn too small", [&] { res_add_ss(hr, pr, 2, 4 * 1024, xr_small, 4, 1024, 0, ss1); });
+    expect_reject("res_add_ss parts too small", [&] { res_add_ss(hr, pr, 3, 4 * 1024, xr, 4, 1024, 0, ss1); });
     auto g = T({1000}, BF), u = T({1000}, BF), o = T({1000}, BF), us = T({999}, BF);
     expect_ok("silu_mul", [&] { silu_mul(g, u, o); });
     expect_reject("silu_mul size mismatch", [&] { silu_mul(g, us, o); });
