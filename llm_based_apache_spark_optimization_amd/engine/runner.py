@@ -294,10 +294,14 @@ class ModelRunner:
         q8 = dict(x8=self.x8, sx8=self.sx8) if a8 else {}
         q8m = dict(x8=self.x8, sx8=self.sx8) if a8m else {}
         mres = self.mlp_res and not a8m
-        wn = self.wide_norm and not (a8 or a8m or mres)
+        # attention side: a wide residual add + qkv row scale unless qkv runs W8A8 (its e4m3 input comes from the norm
+        # launch); MLP side: the o projection's residual epilogue (mres), else a wide add unless gate_up runs W8A8
+        wna = self.wide_norm and not a8
+        wnm = self.wide_norm and not a8m and not mres
+        raw0 = wna or mres  # the embedding launch writes raw rows + row sums and zeroes every later accumulator
         ssq = self.ssq
-        rn_a = (lambda l: dict(rownorm=(ssq[2 * l], self.eps))) if wn else (lambda l: {})
-        rn_m = (lambda l: dict(rownorm=(ssq[2 * l + 1], self.eps))) if wn else (lambda l: {})
+        rn_a = lambda l: dict(rownorm=(ssq[2 * l], self.eps)) if (wna or (l == 0 and raw0)) else {}  # noqa: E731
+        rn_m = lambda l: dict(rownorm=(ssq[2 * l + 1], self.eps)) if wnm else {}  # noqa: E731
         if mres:
             sk_o = ops.pick_gemm_config(B, d, self.H * self.D, "res", xf=xf, kind=w.layers[0].wo.kind)[1]
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
@@ -314,16 +318,13 @@ class ModelRunner:
             xn, attn, act = self.xn[:B], self.attn[:B], self.act[:B]
             lin = ops.linear
         for l, lw in enumerate(w.layers):
-            if l == 0 and wn:  # raw embedding rows + their sums of squares; zeroes every later accumulator
+            if l == 0 and raw0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf,
-                                ss_out=ssq.view(-1), ss_ld=self.max_slots, ss_nzero=2 * self.L)
-            elif wn:
-                ops.res_add_ss(h, d_red, xn, B, ssq[2 * l], xf=xf)
-            elif l == 0 and mres:  # the embedding launch also zeroes the MLP-side row sums of every layer
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf,
-                                ss_out=self.ssq.view(-1), ss_ld=self.max_slots, ss_nzero=2 * self.L, **q8)
+                                ss_out=ssq.view(-1), ss_ld=self.max_slots, ss_nzero=2 * self.L, **q8)
             elif l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf, **q8)
+            elif wna:
+                ops.res_add_ss(h, d_red, xn, B, ssq[2 * l], xf=xf)
             else:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_red, rows=B, xf=xf, **q8)
             # QKV as f32 split-K slabs; the attention kernel sums them, applies RoPE and appends the new
@@ -342,13 +343,12 @@ class ModelRunner:
                             qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
                             sin=self.sin if fr else None, kv_scales=self._kv_scales(l))
             if mres:
-                lin(attn, lw.wo, "res", out=o_parts, splitk=sk_o,
-                    res=(h, xn, self.ssq[2 * l + 1], self.res_tickets))
-                lin(xn, lw.w_gate_up, "silu", out=act, rownorm=(self.ssq[2 * l + 1], self.eps))
+                lin(attn, lw.wo, "res", out=o_parts, splitk=sk_o, res=(h, xn, ssq[2 * l + 1], self.res_tickets))
+                lin(xn, lw.w_gate_up, "silu", out=act, rownorm=(ssq[2 * l + 1], self.eps))
             else:
                 lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
                 o_red = self._reduce_parts(o_parts)
-                if wn:
+                if wnm:
                     ops.res_add_ss(h, o_red, xn, B, ssq[2 * l + 1], xf=xf)
                 else:
                     ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
