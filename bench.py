@@ -118,7 +118,14 @@ def explain_round(device, prompt_len: int = 2048, new_tokens: int = 128) -> dict
     prompt = [eng.spec.bos_id] + torch.randint(3, eng.spec.vocab_size, (prompt_len - 1,), generator=g).tolist()
     num = numerics_check(eng, [prompt], 64, True, 1, "llama3.2", "bf16", None)
     p50, dev = _timed_rounds(eng, [prompt], SamplingParams(max_tokens=new_tokens, temperature=0.0, ignore_eos=True), 3)
+    # time to first token: a one-token request (2k-token prefill + first-token commit + the host read-back)
+    ttft = []
+    for _ in range(3):
+        t = time.perf_counter()
+        eng.generate([prompt], SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))
+        ttft.append(time.perf_counter() - t)
     out = {"explain_2k_p50_e2e_latency_s": round(p50, 4), "explain_2k_device_ms_per_step": round(dev, 3),
+           "explain_2k_ttft_s": round(sorted(ttft)[1], 4),
            "vs_baseline_p50_latency_explain": round(REF_P50_S_LLAMA / p50, 2), "numerics_explain_2k": num,
            "explain_2k_config": {"model": MODEL_NAMES["llama3.2"], "prompt_len": prompt_len, "new_tokens": new_tokens,
                                  "batch": 1, "dtype": "bf16"}}

@@ -58,7 +58,8 @@ int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, vo
                  int waves, int div, int xlds, hipStream_t stream);
 int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
-int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, hipStream_t stream);
+int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int splitk,
+                  hipStream_t stream);
 int lsa_gemm_t256x(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int xf_tiles,
                    hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
@@ -285,20 +286,21 @@ void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) 
 }
 
 // large-M (prefill) linear layer on the 256x256 tile kernel (kernels/gemm_tile256.hip)
-void gemm_t256(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi) {
+void gemm_t256(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, int64_t splitk) {
   need(x, at::kBFloat16, "x");
   need(wf, at::kBFloat16, "wf");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
   const int M = x.size(0), K = x.size(1);
   TORCH_CHECK(wf.numel() == N * K, "weight numel mismatch");
+  TORCH_CHECK(splitk >= 1 && (splitk == 1 || epi == 1), "gemm_t256: only the f32 epilogue splits K");
   if (epi == 1) {
     need(out, at::kFloat, "out");
-    TORCH_CHECK(out.numel() >= M * N, "f32 out too small");
+    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small for the slabs");
   } else {
     need(out, at::kBFloat16, "out");
     TORCH_CHECK(out.numel() >= M * (epi == 2 ? N / 2 : N), "bf16 out too small");
   }
-  check(lsa_gemm_t256(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, cur_stream()),
+  check(lsa_gemm_t256(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, (int)splitk, cur_stream()),
         "gemm_t256");
 }
 
@@ -814,7 +816,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_xf", &gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wf"), py::arg("N"), py::arg("out"),
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
-  m.def("gemm_t256", &gemm_t256);
+  m.def("gemm_t256", &gemm_t256, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"),
+        py::arg("splitk") = 1);
   m.def("fp4_gemm", &fp4_gemm, py::arg("x"), py::arg("wq"), py::arg("sw"), py::arg("N"), py::arg("out"), py::arg("epi"),
         py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("rowss") = py::none(), py::arg("eps") = 1e-5,
         py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(),

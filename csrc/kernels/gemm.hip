@@ -570,7 +570,7 @@ static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uin
 extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
                             int splitk, int waves, int div, int xlds, hipStream_t stream);
 extern "C" int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi,
-                             hipStream_t stream);
+                             int splitk, hipStream_t stream);
 
 extern "C" int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
                         int splitk, hipStream_t stream) {
@@ -651,7 +651,9 @@ extern "C" int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf,
     // the 256^2 8-phase kernel (gemm_tile256.hip) once its grid fills half the CUs; measured 1.2-1.34 PF
     // vs 0.73-0.86 PF for the 128^2 tile at the 7B/3B prefill shapes (scripts/bench_prefill_gemm.py)
     if (splitk == 1 && ((M + 255) / 256) * ((NBtot + 15) / 16) >= 128 && (epi != EPI_SILU || NBtot % 2 == 0))
-      return lsa_gemm_t256(X, ldx, M, K, Wf, N, out, epi, stream);
+      return lsa_gemm_t256(X, ldx, M, K, Wf, N, out, epi, 1, stream);
+    // from 1024 rows a small 256^2 grid splits K instead of falling back to the 128^2 tile (ops.tile_splitk)
+    if (splitk > 1 && epi == EPI_F32 && M >= 1024) return lsa_gemm_t256(X, ldx, M, K, Wf, N, out, epi, splitk, stream);
     const int kbps = (KB + splitk - 1) / splitk;
     if ((KB + kbps - 1) / kbps != splitk) return -3;  // every slab must own >= 1 k-block (no unwritten slab)
     dim3 grid((NBtot + 7) / 8, (M + 127) / 128, splitk);

@@ -74,7 +74,7 @@ __device__ __forceinline__ void store_out(void* out, int ldo, int m, int n, cons
 template <int EPI, bool XF = false>
 __global__ __launch_bounds__(512) void gemm_t256_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                                         const uint4* __restrict__ Wf, int NBtot,
-                                                        void* __restrict__ out, int ldo, int ntm) {
+                                                        void* __restrict__ out, int ldo, int ntm, int kts) {
   __shared__ __attribute__((aligned(16))) uint4 lds[2][4][16][64];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;  // 0..7
@@ -83,17 +83,24 @@ __global__ __launch_bounds__(512) void gemm_t256_kernel(const uint16_t* __restri
   // XCD-aware bijective remap (consecutive ids go round-robin over the 8 XCDs)
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7;
   const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int wgid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  // split-K (EPI_F32 only, kts > 0): workgroup = (output tile, K split); split s covers K-tiles [s*kts, (s+1)*kts)
+  // and writes f32 slab s (the consumer sums the slabs)
+  const int ntiles = ntm * ((NBtot + 15) >> 4);
+  const int split = kts > 0 ? wgid0 / ntiles : 0;
+  const int wgid = kts > 0 ? wgid0 - split * ntiles : wgid0;
   const int tm = wgid % ntm, tn = wgid / ntm;
   const int mbase = tm * 256, nbase = tn * 16;  // first row / first n-block
 
-  const int T = (KB + 1) >> 1;
+  const int T = (KB + 1) >> 1;  // K-tiles of the whole product
+  const int kt0 = kts > 0 ? split * kts : 0;
+  const int Tl = kts > 0 ? min(T, kt0 + kts) - kt0 : T;  // this workgroup's K-tiles (>= 1: host-checked)
   const bool odd_tail = KB & 1;  // the last K-tile has one k-step (its second fragments re-read the first)
   const int r16 = lane & 15, c16 = 8 * (lane >> 4);
   // stage half h of K-tile t (clamped to the last tile) into buffer t & 1: this wave moves fragments
   // 2w and 2w + 1 of the half, one global_load_lds (1 KiB) each
   auto stage = [&](int h, int t) {
-    const int tc = min(t, T - 1);
+    const int tc = kt0 + min(t, Tl - 1);  // global K-tile (clamped to this split's last)
     const int buf = t & 1;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -180,9 +187,9 @@ __global__ __launch_bounds__(512) void gemm_t256_kernel(const uint16_t* __restri
   // ping-pong: the second M wave group runs one barrier behind, so one group's MFMA section overlaps the
   // other's fragment reads + prefetch issue (the >= 2-phase WAR/RAW slack above covers the offset)
   if (wm == 1) __builtin_amdgcn_s_barrier();
-  for (int t = 0; t < T; ++t) {
+  for (int t = 0; t < Tl; ++t) {
     const int b = t & 1;
-    const int nks = (odd_tail && t == T - 1) ? 1 : 2;
+    const int nks = (odd_tail && kt0 + t == T - 1) ? 1 : 2;
     LSA_PHASE((read_x(b, 0), read_w(b, 0)), 1, t + 1, (void)0, 0, 0);
     LSA_PHASE(read_w(b, 1), 2, t + 1, (void)0, 0, 1);
     LSA_PHASE(read_x(b, 1), 0, t + 2, (void)0, 1, 1);
@@ -213,7 +220,9 @@ __global__ __launch_bounds__(512) void gemm_t256_kernel(const uint16_t* __restri
       for (int j = 0; j < 4; ++j) {
         const int nb = nbase + wn * 4 + j;
         if (nb >= NBtot) continue;
-        store_out<EPI>(out, ldo, m, nb * 16 + 4 * g, acc[i][j]);
+        store_out<EPI>(EPI == EPI_F32 ? reinterpret_cast<void*>(reinterpret_cast<float*>(out) + (size_t)split * M * ldo)
+                                      : out,
+                       ldo, m, nb * 16 + 4 * g, acc[i][j]);
       }
     }
   }
@@ -233,13 +242,13 @@ extern "C" int lsa_gemm_t256x(const void* X, int ldx, int M, int K, const void* 
   if (xf_tiles <= 0) return -5;
   switch (epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL((gemm_t256_kernel<EPI_BF16, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm);
+      hipLaunchKernelGGL((gemm_t256_kernel<EPI_BF16, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm, 0);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL((gemm_t256_kernel<EPI_F32, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm);
+      hipLaunchKernelGGL((gemm_t256_kernel<EPI_F32, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm, 0);
       break;
     case EPI_SILU:
-      hipLaunchKernelGGL((gemm_t256_kernel<EPI_SILU, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm);
+      hipLaunchKernelGGL((gemm_t256_kernel<EPI_SILU, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm, 0);
       break;
     default:
       return -4;
@@ -247,24 +256,31 @@ extern "C" int lsa_gemm_t256x(const void* X, int ldx, int M, int K, const void* 
   return (int)hipGetLastError();
 }
 
+// splitk > 1 (EPI_F32 only): the K range is cut into splitk pieces of ceil(K-tiles / splitk) 64-deep tiles, one
+// workgroup per (output tile, piece), f32 slab per piece in out[splitk][M][N] -- fills the chip when the 256^2 tile
+// grid alone would not (3B 2k prefill o / down: 96 tiles -> x3)
 extern "C" int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi,
-                             hipStream_t stream) {
+                             int splitk, hipStream_t stream) {
   if (K % 32 != 0 || N % 16 != 0 || M <= 0) return -1;
   const int KB = K / 32, NBtot = N / 16;
   const int ntm = (M + 255) / 256, ntn = (NBtot + 15) / 16;
   const int ldo = epi == EPI_SILU ? N / 2 : N;
-  const dim3 grid(ntm * ntn);
+  if (splitk < 1) splitk = 1;
+  if (splitk > 1 && epi != EPI_F32) return -3;
+  const int T = (KB + 1) / 2, kts = splitk > 1 ? (T + splitk - 1) / splitk : 0;
+  if (splitk > 1 && (T + kts - 1) / kts != splitk) return -3;  // every piece owns >= 1 K-tile
+  const dim3 grid(ntm * ntn * splitk);
   const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
   const uint4* w = reinterpret_cast<const uint4*>(Wf);
   switch (epi) {
     case EPI_BF16:
-      hipLaunchKernelGGL(gemm_t256_kernel<EPI_BF16>, grid, dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, ntm);
+      hipLaunchKernelGGL(gemm_t256_kernel<EPI_BF16>, grid, dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, ntm, 0);
       break;
     case EPI_F32:
-      hipLaunchKernelGGL(gemm_t256_kernel<EPI_F32>, grid, dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, ntm);
+      hipLaunchKernelGGL(gemm_t256_kernel<EPI_F32>, grid, dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, ntm, kts);
       break;
     case EPI_SILU:
-      hipLaunchKernelGGL(gemm_t256_kernel<EPI_SILU>, grid, dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, ntm);
+      hipLaunchKernelGGL(gemm_t256_kernel<EPI_SILU>, grid, dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, ntm, 0);
       break;
     default:
       return -4;

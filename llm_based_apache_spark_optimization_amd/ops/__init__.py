@@ -432,6 +432,9 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
 
 
 FP8_W8A8 = os.environ.get("LSA_FP8_W8A8", "1") != "0"
+# prefill GEMMs of >= 1024 rows whose 256^2 tile grid under-fills the chip split K on that kernel (LSA_T256_SPLIT=0:
+# the 128^2 tile kernel with split-K, as before round 3)
+T256_SPLIT = os.environ.get("LSA_T256_SPLIT", "1") != "0"
 
 
 def _dequant_scratch(w: PackedWeight, device) -> torch.Tensor:
@@ -484,7 +487,17 @@ def tile_splitk(M: int, N: int, K: int, kind: str = "bf16") -> int:
     if kind == "fp8" and FP8_W8A8 and K % 128 == 0:
         return fp8_tile_splitk(M, N, K)
     nbt = N // 16
-    if ((M + 255) // 256) * ((nbt + 15) // 16) >= 128:
+    t256 = ((M + 255) // 256) * ((nbt + 15) // 16)
+    if M >= 1024 and t256 < 256 and T256_SPLIT:
+        # the 256^2 kernel with K split over sk pieces (f32 slabs): the sk in 2..4 whose grid rounds over 256 CUs,
+        # ceil(t256 * sk / 256) / sk, are shortest, each piece >= 4 K-tiles of 64 (3B 2k prefill o / down: 96 tiles,
+        # sk 2; qkv 160 tiles, sk 3)
+        best = (1.0, 1)
+        for sk in (2, 3, 4):
+            if (K // 64) // sk >= 4:
+                best = min(best, (-(-t256 * sk // 256) / sk, sk))
+        return best[1]
+    if t256 >= 128:
         return 1
     tiles = ((nbt + 7) // 8) * ((M + 127) // 128)
     target = int(os.environ.get("LSA_TILE_SPLIT_TARGET", "256"))

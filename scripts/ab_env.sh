@@ -16,7 +16,8 @@ for r in $(seq 1 $rounds); do
     python - "$s" "$log" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-keys = ["value", "decode_device_ms_per_step", "decode_device_ms_per_step_b1", "explain_2k_device_ms_per_step"]
+keys = ["value", "p50_e2e_latency_s", "decode_device_ms_per_step", "decode_device_ms_per_step_b1",
+        "explain_2k_device_ms_per_step", "explain_2k_p50_e2e_latency_s", "explain_2k_ttft_s"]
 print(f"[{sys.argv[1]}]", {k: d.get(k) for k in keys if k in d}, "numerics_ok", (d.get("numerics") or {}).get("ok"))
 PY
     i=$((i+1))

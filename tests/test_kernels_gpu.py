@@ -156,6 +156,26 @@ def test_gemm_tile(gpu, M, NK, epi):
         assert _rel(y, yr) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1024, 2048, 1100])
+@pytest.mark.parametrize("NK", [(3072, 3072), (5120, 3072), (3072, 8192), (1024, 1376)])
+@pytest.mark.parametrize("sk", [2, 3, 4])
+def test_gemm_tile256_splitk(gpu, M, NK, sk):
+    """The 256^2 kernel with K split into sk pieces (f32 slabs summing to the product; odd K/32 in the last piece), and
+    the prefill dispatch (ops.linear, ops.tile_splitk) that picks it for >= 1024 rows on small tile grids."""
+    N, K = NK
+    torch.manual_seed(M + N + K + sk)
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    yr = x.float() @ w.float().t()
+    out = torch.full((sk, M, N), float("nan"), device=gpu)
+    ops.ext().gemm_t256(x, pw.data, N, out, 1, sk)
+    assert not torch.isnan(out).any()  # every slab element written
+    assert _rel(out.sum(0), yr) < 1e-4
+    y = ops.linear(x, pw, "f32")  # dispatch: the tile_splitk pick
+    assert y.shape[0] == ops.tile_splitk(M, N, K) and _rel(y.sum(0), yr) < 1e-4
+
+
 @pytest.mark.parametrize("M", [65, 256, 300, 777])
 @pytest.mark.parametrize("NK", [(800, 4096), (1024, 1376), (4096, 512), (256, 96)])
 @pytest.mark.parametrize("epi", ["bf16", "f32", "silu"])
