@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import sys
 import os
 import random
 import socket
@@ -149,7 +150,11 @@ def run(args) -> dict:
                 cl.post("/" + route, json=body).raise_for_status()
             warm_s = time.perf_counter() - t0
 
-            phases = [_phase(cl, args, float(q), rng, make_request) for q in str(args.qps).split(",")]
+            phases = []
+            for q in str(args.qps).split(","):
+                phases.append(_phase(cl, args, float(q), rng, make_request))
+                # progress on stderr (long multi-phase runs stay visibly alive)
+                print(f"phase qps={q}: {phases[-1].get('output_tokens_per_sec')} tok/s", file=sys.stderr, flush=True)
     for p in phases:
         p.update(warmup_s=round(warm_s, 2), models={"nl2sql": f"duckdb-nsql-7B ({args.nl2sql_dtype})",
                                                     "explain_error": f"Llama-3.2-3B-Instruct ({args.explain_dtype})"},
