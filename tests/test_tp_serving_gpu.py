@@ -44,6 +44,9 @@ def test_tp2_replica_behind_fastapi(gpu, tmp_path):
             d = r.json()
             assert d["eval_count"] == 8
             got.append(d["sql_query"])
+        # bf16 shards sum in a different order than the TP=1 GEMMs, so a near-tied greedy argmax of the random-init
+        # model may flip in one answer; the sharded math itself is pinned at logit level (KL < 1e-6 against the
+        # unsharded fp32 oracle) by tests/test_engine_cpu.py::test_tensor_parallel_matches_single
         assert sum(a == b for a, b in zip(got, want)) >= len(QUESTIONS) - 1, (got, want)
         assert router.health()["ok"]
     finally:
