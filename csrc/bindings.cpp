@@ -81,16 +81,9 @@ int lsa_ar_wallclock_khz(int* out);
 int lsa_ar_header_bytes();
 int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
                int nblocks, long long timeout_ticks, int* err, int nslab, long slab_stride, hipStream_t s);
-int lsa_decode_block_cnt_ints();
 int lsa_fp4_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const void* S, int N, void* out, int epi,
                     int nb, int splitk, int waves, int xfrag, const LsaEpi* ep, hipStream_t stream);
 int lsa_fp4_dequant(const void* Wq, const void* S, int N, int K, void* Wf, hipStream_t s);
-int lsa_res_gemm(const void* X, const void* W, float* h, void* xout, long long* ss, int B, int N, int K, int* err,
-                 long long timeout_ticks, int nwg, int cw, long long* stamps, hipStream_t s);
-int lsa_decode_block(const void* attn, const void* wo, float* h, void* x, long long* ss1, long long* ss2, const void* wgu,
-                     void* act, const void* wd, const void* wq, float* qout, int B, int d, int hd, int ffn, int nq,
-                     float eps, int* cnt, int* err, long long timeout_ticks, int nwg, int nbo, int nbg, int nbd, int nbq,
-                     int cw, long long* stamps, hipStream_t s);
 }
 
 namespace {
@@ -726,85 +719,6 @@ void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Te
         "ar_run");
 }
 
-// persistent post-attention decode block (kernels/decode_block.hip): o + residual -> gate_up -> down + residual
-// [-> next layer's qkv], one launch; cnt [>= lsa_decode_block_cnt_ints()] int32 zeroed before every launch
-void decode_block(const at::Tensor& attn, const at::Tensor& wo, at::Tensor& h, at::Tensor& x, at::Tensor& ss1,
-                  at::Tensor& ss2, const at::Tensor& wgu, at::Tensor& act, const at::Tensor& wd,
-                  const c10::optional<at::Tensor>& wq, const c10::optional<at::Tensor>& qout, int64_t B, int64_t ffn,
-                  int64_t nq, double eps, at::Tensor& cnt, at::Tensor& err, int64_t timeout_ticks, int64_t nwg,
-                  int64_t nbo, int64_t nbg, int64_t nbd, int64_t nbq, int64_t cw,
-                  const c10::optional<at::Tensor>& stamps) {
-  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&attn, &wo, &x, &wgu, &act, &wd})
-    need(*t, at::kBFloat16, "decode_block bf16 operand");
-  need(h, at::kFloat, "h");
-  need(ss1, at::kLong, "ss1");
-  need(ss2, at::kLong, "ss2");
-  need(cnt, at::kInt, "cnt");
-  need(err, at::kInt, "err");
-  TORCH_CHECK(B >= 1 && B <= 64, "decode_block: batch 1..64");
-  TORCH_CHECK(h.dim() == 2 && h.size(0) >= B && h.is_contiguous(), "h [>= B, d] f32");
-  const int64_t d = h.size(1), mt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
-  TORCH_CHECK(d > 0 && wo.numel() % d == 0, "wo [d, hd]");
-  const int64_t hd = wo.numel() / d;
-  TORCH_CHECK(attn.numel() >= mt * 16 * hd && x.numel() >= mt * 16 * d && act.numel() >= mt * 16 * ffn,
-              "decode_block: fragment-major activations too small");
-  TORCH_CHECK(wgu.numel() == 2 * ffn * d && wd.numel() == d * ffn, "decode_block: MLP weight sizes");
-  TORCH_CHECK(ss1.numel() >= B && ss2.numel() >= B && err.numel() >= 1, "decode_block: row sums / err too small");
-  TORCH_CHECK(cnt.is_contiguous() && cnt.numel() >= lsa_decode_block_cnt_ints(), "decode_block: counter block too small");
-  TORCH_CHECK(nwg >= 1 && nwg <= 65536, "decode_block: 1..65536 workgroups");
-  TORCH_CHECK(cw == 4 || cw == 8, "decode_block: 4 or 8 consumer waves");
-  if (wq.has_value()) {
-    need(*wq, at::kBFloat16, "wq");
-    TORCH_CHECK(qout.has_value(), "next-layer qkv needs its output buffer");
-    need(*qout, at::kFloat, "qout");
-    TORCH_CHECK(wq->numel() == nq * d && qout->numel() >= B * nq, "decode_block: qkv sizes");
-  }
-  if (stamps.has_value()) {
-    need(*stamps, at::kLong, "stamps");
-    TORCH_CHECK(stamps->is_contiguous() && stamps->numel() >= nwg * 16, "decode_block: stamps [nwg, 16] int64");
-  }
-  check(lsa_decode_block(attn.data_ptr(), wo.data_ptr(), h.data_ptr<float>(), x.data_ptr(),
-                         reinterpret_cast<long long*>(ss1.data_ptr<int64_t>()),
-                         reinterpret_cast<long long*>(ss2.data_ptr<int64_t>()), wgu.data_ptr(), act.data_ptr(),
-                         wd.data_ptr(), wq.has_value() ? wq->data_ptr() : nullptr,
-                         wq.has_value() ? qout->data_ptr<float>() : nullptr, B, d, hd, ffn, wq.has_value() ? nq : 0,
-                         (float)eps, cnt.data_ptr<int>(), err.data_ptr<int>(), timeout_ticks, nwg, nbo, nbg, nbd, nbq,
-                         (int)cw, stamps.has_value() ? reinterpret_cast<long long*>(stamps->data_ptr<int64_t>()) : nullptr,
-                         cur_stream()),
-        "decode_block");
-}
-
-// one residual GEMM on the decode block's ring engine (kernels/decode_block.hip lsa_res_gemm):
-// h[:B] += X @ W^T, xout = bf16(h) fragment-major, ss[:B] += row sums of h^2 (Q24)
-void res_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& h, at::Tensor& xout, at::Tensor& ss, int64_t B,
-              at::Tensor& err, int64_t timeout_ticks, int64_t nwg, int64_t cw, const c10::optional<at::Tensor>& stamps) {
-  need(x, at::kBFloat16, "x");
-  need(w, at::kBFloat16, "w");
-  need(xout, at::kBFloat16, "xout");
-  need(h, at::kFloat, "h");
-  need(ss, at::kLong, "ss");
-  need(err, at::kInt, "err");
-  TORCH_CHECK(B >= 1 && B <= 64, "res_gemm: batch 1..64");
-  TORCH_CHECK(h.dim() == 2 && h.size(0) >= B && h.is_contiguous(), "h [>= B, N] f32");
-  const int64_t N = h.size(1), mt = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
-  TORCH_CHECK(N % 16 == 0 && N > 0 && w.numel() % N == 0, "res_gemm: w [N, K], N % 16 == 0");
-  const int64_t K = w.numel() / N;
-  TORCH_CHECK(K % 32 == 0, "res_gemm: K % 32 == 0");
-  TORCH_CHECK(x.is_contiguous() && x.numel() >= mt * 16 * K, "res_gemm: fragment-major x too small");
-  TORCH_CHECK(xout.is_contiguous() && xout.numel() >= mt * 16 * N, "res_gemm: fragment-major xout too small");
-  TORCH_CHECK(ss.numel() >= B && err.numel() >= 1, "res_gemm: row sums / err too small");
-  TORCH_CHECK(nwg >= 1 && nwg <= 65536 && (cw == 4 || cw == 8), "res_gemm: grid / consumer waves");
-  if (stamps.has_value()) {
-    need(*stamps, at::kLong, "stamps");
-    TORCH_CHECK(stamps->is_contiguous() && stamps->numel() >= nwg * 16, "res_gemm: stamps [nwg, 16] int64");
-  }
-  check(lsa_res_gemm(x.data_ptr(), w.data_ptr(), h.data_ptr<float>(), xout.data_ptr(),
-                     reinterpret_cast<long long*>(ss.data_ptr<int64_t>()), B, N, K, err.data_ptr<int>(), timeout_ticks,
-                     nwg, cw, stamps.has_value() ? reinterpret_cast<long long*>(stamps->data_ptr<int64_t>()) : nullptr,
-                     cur_stream()),
-        "res_gemm");
-}
-
 }  // namespace
 
 #ifndef LSA_BINDINGS_SELFTEST
@@ -875,14 +789,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     check(lsa_silu_parts(parts.data_ptr<float>(), S, parts.stride(0), M, F, out.data_ptr(), cur_stream()),
           "silu_parts");
   });
-  m.def("decode_block", &decode_block, py::arg("attn"), py::arg("wo"), py::arg("h"), py::arg("x"), py::arg("ss1"),
-        py::arg("ss2"), py::arg("wgu"), py::arg("act"), py::arg("wd"), py::arg("wq"), py::arg("qout"), py::arg("B"),
-        py::arg("ffn"), py::arg("nq"), py::arg("eps"), py::arg("cnt"), py::arg("err"), py::arg("timeout_ticks"),
-        py::arg("nwg"), py::arg("nbo"), py::arg("nbg"), py::arg("nbd"), py::arg("nbq"), py::arg("cw") = 4,
-        py::arg("stamps") = py::none());
-  m.def("res_gemm", &res_gemm, py::arg("x"), py::arg("w"), py::arg("h"), py::arg("xout"), py::arg("ss"), py::arg("B"),
-        py::arg("err"), py::arg("timeout_ticks"), py::arg("nwg"), py::arg("cw") = 4, py::arg("stamps") = py::none());
-  m.def("decode_block_cnt_ints", []() { return lsa_decode_block_cnt_ints(); });
   m.def("ar_alloc", &ar_alloc);
   m.def("ar_free", [](int64_t p) { check(lsa_ar_free(reinterpret_cast<void*>(p)), "ar_free"); });
   m.def("ar_handle", &ar_handle);

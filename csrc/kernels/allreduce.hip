@@ -78,6 +78,9 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
     }
     return v;
   };
+  // the group is already broken (an earlier call timed out somewhere): no push, no flag wait -- poison at once, so a
+  // captured step's remaining ~2L all-reduces each cost a launch, not a full timeout
+  if (s_timeout) goto poison;
   // 1. push this block's chunk into every peer's recv[parity][rank]
   for (long i = (long)b * AR_THREADS + tid; i < n4; i += stride) {
     const float4 v = own(i);
@@ -112,6 +115,7 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
   __syncthreads();
 
   if (s_timeout) {  // a peer never arrived: poison this block's result (NaN), never a silent partial sum
+  poison:
     const float nan = __builtin_nanf("");
     const float4 nv = make_float4(nan, nan, nan, nan);
     for (long i = (long)b * AR_THREADS + tid; i < n4; i += stride) {

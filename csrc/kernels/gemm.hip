@@ -24,10 +24,6 @@
 #define EPI_BF16 0
 #define EPI_F32 1
 #define EPI_SILU 2
-#ifndef LSA_XSAME
-#define LSA_XSAME 0  // experiment knob (LSA_HIP_EXTRA=-DLSA_XSAME=1): every k-step reads the same 2 activation
-                     // fragments (L1-resident) -> upper bound of removing activation traffic
-#endif
 
 
 template <int EPI>
@@ -123,7 +119,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
         if constexpr (XF) {
-          xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)(LSA_XSAME ? (kk & 1) : kk) * MT * 512);
+          xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * MT * 512);
         } else {
           const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff[j] + (uint32_t)kk * 64u, 0, 0);
           xr[u][j] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -261,119 +257,6 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       __syncthreads();
       if (threadIdx.x < M) atomicAdd(reinterpret_cast<unsigned long long*>(ep.ss_out) + threadIdx.x, ssw[threadIdx.x]);
     }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// decode kernel with the activation block staged in LDS (M in 17..64, f32 split-K slabs only)
-//
-// At M = 32 the fragment-shaped activation loads (16 rows x 64 B per wave-instruction) cost as much
-// memory-pipe issue as the weight stream itself (rocprofv3: +20 % VMEM instructions, +18 % issue
-// stalls vs M = 1).  Here the workgroup first copies its x[0:M, k-range] block into LDS with
-// full-line, coalesced 16 B loads (XOR-swizzled by row so the 16 rows a ds_read_b128 lane group
-// reads sit in distinct bank slots), then the waves stream only weights from HBM and read their
-// B fragments from LDS.  No x registers -> ~100 fewer VGPRs -> more resident waves.
-// ------------------------------------------------------------------------------------------------
-template <int MT, int NB, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void gemm_xlds_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
-                                                               const uint4* __restrict__ Wf, float* __restrict__ out,
-                                                               int ldo, int kb_per_split) {
-  constexpr int U = 16 / NB;
-  extern __shared__ __attribute__((aligned(16))) uint4 xs[];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int nb0 = blockIdx.x * NB;
-  const int kbA = blockIdx.y * kb_per_split;
-  const int kbB = min(KB, kbA + kb_per_split);
-  const int nk = kbB - kbA;
-  const int ppr = nk * 4;                       // 16 B pieces per staged row
-  const int swz = (ppr & 15) == 0 ? 15 : 0;     // row XOR (needs >= 16 pieces per row)
-  // 1) stage x[0:16*MT, k-range] (rows >= M zero-filled)
-  for (int idx = threadIdx.x; idx < 16 * MT * ppr; idx += 64 * WAVES) {
-    const int row = idx / ppr, pc = idx - row * ppr;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (row < M) v = *reinterpret_cast<const uint4*>(X + (size_t)row * ldx + (size_t)kbA * 32 + pc * 8);
-    xs[row * ppr + (pc ^ (row & swz))] = v;
-  }
-  __syncthreads();
-
-  const int nch = (nk + U - 1) / U;
-  const int n_it = nch > w ? (nch - w + WAVES - 1) / WAVES : 0;
-  const int last_c = w + WAVES * (n_it - 1);
-  f32x4_t acc[NB][MT];
-#pragma unroll
-  for (int i = 0; i < NB; ++i)
-#pragma unroll
-    for (int j = 0; j < MT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const uint4* wp[NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) wp[i] = Wf + (size_t)(nb0 + i) * KB * 64 + lane;
-
-  auto load = [&](uint4 (&wr)[U][NB], int c) {
-    const int kb = kbA + c * U;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = min(kb + u, kbB - 1);
-#pragma unroll
-      for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
-    }
-  };
-  auto comp = [&](uint4 (&wr)[U][NB], int c) {
-    const int rel0 = c * U;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int rel = rel0 + u;
-      const bool live = rel < nk;
-      const int pc = min(rel, nk - 1) * 4 + g;
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        uint4 wv = wr[u][i];
-        wv.x = live ? wv.x : 0u; wv.y = live ? wv.y : 0u; wv.z = live ? wv.z : 0u; wv.w = live ? wv.w : 0u;
-        wr[u][i] = wv;
-      }
-#pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int row = j * 16 + r;
-        const uint4 xv = xs[row * ppr + (pc ^ (row & swz))];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) acc[i][j] = mfma16x16x32(wr[u][i], xv, acc[i][j]);
-      }
-    }
-  };
-  if (n_it > 0) {
-    uint4 wA[U][NB], wB[U][NB];
-    load(wA, w);
-    int i = 0;
-    for (; i + 1 < n_it; i += 2) {
-      load(wB, w + WAVES * (i + 1));
-      __builtin_amdgcn_sched_barrier(0);
-      comp(wA, w + WAVES * i);
-      __builtin_amdgcn_sched_barrier(0);
-      load(wA, min(w + WAVES * (i + 2), last_c));
-      __builtin_amdgcn_sched_barrier(0);
-      comp(wB, w + WAVES * (i + 1));
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (i < n_it) comp(wA, w + WAVES * i);
-  }
-  // cross-wave reduction reuses the x staging area (all waves are past their last x read)
-  __syncthreads();
-  f32x4_t* red = reinterpret_cast<f32x4_t*>(xs);  // [WAVES][NB*MT][64]
-#pragma unroll
-  for (int i = 0; i < NB; ++i)
-#pragma unroll
-    for (int j = 0; j < MT; ++j) red[(w * NB * MT + i * MT + j) * 64 + lane] = acc[i][j];
-  __syncthreads();
-  const size_t slab = (size_t)blockIdx.y * M * ldo;
-  for (int idx = threadIdx.x; idx < NB * MT * 64; idx += 64 * WAVES) {
-    const int l = idx & 63, t = idx >> 6;
-    const int j = t % MT, i = t / MT;
-    f32x4_t sacc = red[t * 64 + l];
-#pragma unroll
-    for (int ww = 1; ww < WAVES; ++ww) sacc += red[(ww * NB * MT + t) * 64 + l];
-    const int m = j * 16 + (l & 15);
-    if (m < M) store4<EPI_F32>(out, ldo, slab, m, (nb0 + i) * 16 + 4 * (l >> 4), sacc);
   }
 }
 
@@ -544,11 +427,6 @@ static void launch_skinny_t(const uint16_t* X, int ldx, int M, int KB, const uin
   else launch_skinny_x<MT, NB, EPI, false>(X, ldx, M, KB, Wf, NBtot, out, ldo, splitk, s);
 }
 
-// LDS-staged activation kernel for 16 < M <= 64 (f32 epilogue): measured slower than the register
-// pipeline with div 4 on every decode shape (its x prologue delays the weight stream), so it is off
-// unless a tuning entry asks for it.
-static thread_local int g_xlds = 0;
-
 template <int EPI>
 static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
                             int ldo, int nb, int splitk, hipStream_t s) {
@@ -592,11 +470,11 @@ extern "C" int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf,
   if ((ep || epi == EPI_RES) && (M > 64 || (splitk > 1 && epi != EPI_F32 && epi != EPI_RES))) return -7;
   if (epi == EPI_RES && (!ep || !ep->h || !ep->xout || !ep->ss_out || ep->ldh != N || (splitk > 1 && !ep->tickets)))
     return -8;
-  if (ep && xlds == 1) xlds = 0;  // the LDS-staged variant has no epilogue extensions
   g_skinny_waves = (waves == 8 || waves == 16) ? waves : 4;
   g_skinny_div = (div == 1 || div == 2) ? div : 4;
-  // xlds: 0 = row-major X, 1 = row-major X staged through LDS, 2 = fragment-major X (ops.to_xfrag)
-  g_xlds = xlds == 1 ? 1 : 0;
+  // xlds: 0 = row-major X, 2 = fragment-major X (ops.to_xfrag); the LDS-staged variant (1) was removed in
+  // round 4 (measured slower than the register pipeline on every decode shape, ARCHITECTURE.md §4)
+  if (xlds != 0 && xlds != 2) return -6;
   g_xfrag = xlds == 2 ? 1 : 0;
   if (K % 32 != 0 || N % 16 != 0 || M <= 0) return -1;
   if (g_xfrag && M > 64) return -5;
@@ -604,30 +482,6 @@ extern "C" int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf,
   const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
   const uint4* w = reinterpret_cast<const uint4*>(Wf);
   const int ldo = (epi == EPI_SILU) ? N / 2 : N;
-  if (M > 16 && M <= 64 && epi == EPI_F32 && g_xlds) {
-    if (nb <= 0) nb = 4;
-    if (M > 32 && nb > 2) nb = 2;
-    if (NBtot % nb != 0) return -2;
-    if (splitk < 1) splitk = 1;
-    const int kbps = (KB + splitk - 1) / splitk;
-    const int mt = M <= 32 ? 2 : 4;
-    const size_t xbytes = (size_t)16 * mt * kbps * 64;
-    const size_t rbytes = (size_t)g_skinny_waves * nb * mt * 64 * 16;
-    const size_t lds = xbytes > rbytes ? xbytes : rbytes;
-    if (lds <= 64 * 1024) {
-      dim3 grid(NBtot / nb, splitk);
-      float* o = reinterpret_cast<float*>(out);
-#define LSA_XL(MTV, NBV, WV)                                                                               \
-  if (mt == MTV && nb == NBV && g_skinny_waves == WV) {                                                    \
-    hipLaunchKernelGGL((gemm_xlds_kernel<MTV, NBV, WV>), grid, dim3(64 * WV), lds, stream, x, ldx, M, KB, w, o, \
-                       N, kbps);                                                                           \
-    return (int)hipGetLastError();                                                                        \
-  }
-      LSA_XL(2, 4, 4) LSA_XL(2, 2, 4) LSA_XL(2, 1, 4) LSA_XL(4, 2, 4) LSA_XL(4, 1, 4)
-      LSA_XL(2, 4, 8) LSA_XL(2, 2, 8) LSA_XL(2, 1, 8) LSA_XL(4, 2, 8) LSA_XL(4, 1, 8)
-#undef LSA_XL
-    }
-  }
   if (M <= 64) {
     if (nb <= 0) nb = 1;
     if (epi == EPI_SILU && nb < 2) nb = 2;

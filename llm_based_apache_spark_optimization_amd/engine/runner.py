@@ -177,18 +177,13 @@ class ModelRunner:
         # inside the step: 192 output blocks per row-parallel GEMM leave CUs idle without split-K, and split-K
         # adds the last-arriver tail (3B 2k explain 1.733 vs 1.708 ms per step norm-free vs norm launches,
         # 7B b1 2.625 vs 2.69 ms) -- so the default is per hidden size
-        # (o / down as non-split residual GEMMs on the decode block's ring engine, ops.res_gemm, in the norm-free
+        # (o / down as non-split residual GEMMs on the decode block's ring engine (ops.res_gemm, removed in round 4), in the norm-free
         # step at batch 32 measured slower than the split-K GEMMs + norm launches: 7B 3.77 vs 3.49 ms per step,
         # profiles/r3/res_ring_ab_mi355x.txt -- a standalone full-K stream cannot ramp 128-352 KB per CU fast
         # enough with <= 63 KB of LDS-DMA in flight per loader wave; not wired in)
         mb = os.environ.get("LSA_FUSED_NORM_MAX_B")
         self.fused_norm_max_batch = int(mb) if mb is not None else (16 if self.d >= 4096 else 0)
         self.ssq = torch.zeros(2 * self.L + 2, S, dtype=torch.int64, device=dev)  # Q24 fixed point (ops.ss_q24)
-        # buckets above fused_norm_max_batch: the MLP half only norm-free (o projection with the residual epilogue,
-        # gate_up row-scaled by its sums of squares; the attention-side norm launch stays).  bf16 / W8A16 weights
-        # (the W8A8 gate_up input is quantised by the norm launch)
-        self.mlp_res = (os.environ.get("LSA_MLP_RES", "0") != "0" and tps == 1
-                        and all(lw.norms_folded for lw in weights.layers))
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)
         # buckets that keep the norm launches (above fused_norm_max_batch): the norms as WIDE raw residual adds
@@ -198,13 +193,6 @@ class ModelRunner:
         # quantisation needs the whole-row amax in the norm launch) or the MLP residual epilogue
         self.wide_norm = (os.environ.get("LSA_WIDE_NORM", "1") != "0" and tps == 1
                           and all(lw.norms_folded for lw in weights.layers))
-        # one persistent launch per layer for the post-attention block (ops.decode_block: o -> residual -> gate_up ->
-        # down -> residual -> next qkv) at decode batches <= 64: TP = 1, bf16 weights, folded norms (LSA_DECODE_BLOCK)
-        self.block_decode = (os.environ.get("LSA_DECODE_BLOCK", "0") != "0" and tps == 1 and self.d % 32 == 0
-                             and weights.layers[0].wqkv.kind in ("bf16", "dense")
-                             and all(lw.norms_folded for lw in weights.layers))
-        self.blk_cnt = torch.zeros(self.L, ops.DECODE_BLOCK_CNT_INTS, dtype=torch.int32, device=dev)  # per layer
-        self.blk_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graphs: dict = {}
         self._pending_bt: dict = {}  # slot -> block-table row of a prompt still being prefilled in chunks
         if self.tp is not None and self.tp.size > 1 and self.on_gpu:
@@ -276,8 +264,6 @@ class ModelRunner:
         return tuple(ops.decode_split_plan(B, self.Hkv, tier))
 
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
-        if self.block_decode and B <= 64:
-            return self._decode_step_block(B, sample, plan)
         if self.fused_norm and B <= self.fused_norm_max_batch:
             return self._decode_step_fused(B, sample, plan)
         w, d = self.w, self.d
@@ -293,17 +279,17 @@ class ModelRunner:
                 else self._splitk(B, d, nqkv, tp_reduced=False, xf=xf))
         q8 = dict(x8=self.x8, sx8=self.sx8) if a8 else {}
         q8m = dict(x8=self.x8, sx8=self.sx8) if a8m else {}
-        mres = self.mlp_res and not a8m
-        # attention side: a wide residual add + qkv row scale unless qkv runs W8A8 (its e4m3 input comes from the norm
-        # launch); MLP side: the o projection's residual epilogue (mres), else a wide add unless gate_up runs W8A8
+        # each side of the layer: a wide residual add + row scale in the next GEMM unless that GEMM runs W8A8 (its
+        # e4m3 input comes from the quantising norm launch)
         wna = self.wide_norm and not a8
-        wnm = self.wide_norm and not a8m and not mres
-        raw0 = wna or mres  # the embedding launch writes raw rows + row sums and zeroes every later accumulator
+        wnm = self.wide_norm and not a8m
+        # the embedding launch writes raw rows + row sums and zeroes every later accumulator whenever any side uses them
+        # (layer 0's qkv then row-scales, whatever its later layers do)
+        raw0 = wna or wnm
         ssq = self.ssq
         rn_a = lambda l: dict(rownorm=(ssq[2 * l], self.eps)) if (wna or (l == 0 and raw0)) else {}  # noqa: E731
+        assert not (a8 and wna), "a W8A8 qkv input comes from the quantising norm launch"
         rn_m = lambda l: dict(rownorm=(ssq[2 * l + 1], self.eps)) if wnm else {}  # noqa: E731
-        if mres:
-            sk_o = ops.pick_gemm_config(B, d, self.H * self.D, "res", xf=xf, kind=w.layers[0].wo.kind)[1]
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
@@ -329,8 +315,8 @@ class ModelRunner:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_red, rows=B, xf=xf, **q8)
             # QKV as f32 split-K slabs; the attention kernel sums them, applies RoPE and appends the new
             # token's k/v to the paged cache itself (no separate rope/append launch)
-            if a8:
-                ops.linear_a8(self.x8, self.sx8, B, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q)
+            if a8:  # (layer 0 after a raw embedding launch: its e4m3 rows are un-normalised -> row scale)
+                ops.linear_a8(self.x8, self.sx8, B, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q, **rn_a(l))
             else:
                 lin(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q, **rn_a(l))
             kc, vc = self.kv[l, 0], self.kv[l, 1]
@@ -342,20 +328,16 @@ class ModelRunner:
                             attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
                             qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
                             sin=self.sin if fr else None, kv_scales=self._kv_scales(l))
-            if mres:
-                lin(attn, lw.wo, "res", out=o_parts, splitk=sk_o, res=(h, xn, ssq[2 * l + 1], self.res_tickets))
-                lin(xn, lw.w_gate_up, "silu", out=act, rownorm=(ssq[2 * l + 1], self.eps))
+            lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
+            o_red = self._reduce_parts(o_parts)
+            if wnm:
+                ops.res_add_ss(h, o_red, xn, B, ssq[2 * l + 1], xf=xf)
             else:
-                lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
-                o_red = self._reduce_parts(o_parts)
-                if wnm:
-                    ops.res_add_ss(h, o_red, xn, B, ssq[2 * l + 1], xf=xf)
-                else:
-                    ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
-                if a8m:
-                    ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=act)
-                else:
-                    lin(xn, lw.w_gate_up, "silu", out=act, **rn_m(l))
+                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
+            if a8m:
+                ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=act)
+            else:
+                lin(xn, lw.w_gate_up, "silu", out=act, **rn_m(l))
             lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
             d_red = self._reduce_parts(d_parts)
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_red, rows=B, xf=xf)
@@ -407,37 +389,6 @@ class ModelRunner:
             lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk))
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, rows=B, xf=xf, write_h=False)
         self._decode_tail(B, sample, xn, xf)
-
-    def _decode_step_block(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
-        """Decode step with the post-attention block of every layer in ONE persistent launch (ops.decode_block):
-
-          embed (+ row sums of squares) -> qkv[0] (row-scaled, f32) -> per layer:
-            attn_decode (RoPE + KV append from the f32 qkv, fragment-major output)
-            -> decode_block (o + residual -> gate_up -> down + residual -> qkv[l + 1])
-          -> final RMSNorm -> lm_head -> token commit
-
-        2 launches per layer instead of 5-7; every activation in the fragment-major layout (any bucket <= 64)."""
-        w, L = self.w, self.L
-        ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
-        h = self.h[:B]
-        nqkv = (self.H + 2 * self.Hkv) * self.D
-        qkv = self.qkv_buf[: B * nqkv].view(1, B, nqkv)  # one f32 slab, rewritten by every block's last phase
-        plan = plan or ops.decode_split_plan(B, self.Hkv, self.max_model_len)
-        ssq, S = self.ssq, self.max_slots
-        xn, attn, act = self.xn_f, self.attn_f, self.act_f
-        self.blk_cnt.zero_()  # one memset node per step: every layer's claim / done counters
-        ops.add_rmsnorm(h, w.layers[0].attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=True,
-                        ss_out=ssq.view(-1), ss_ld=S, ss_nzero=2 * L)
-        ops.linear_xf(xn, B, w.layers[0].wqkv, "f32", out=qkv, splitk=1, rownorm=(ssq[0], self.eps))
-        for l, lw in enumerate(w.layers):
-            ops.attn_decode(self.q[:B], self.kv[l, 0], self.kv[l, 1], bt, pos, self.H, self.Hkv, self.scale, attn,
-                            workspace=self.attn_ws, plan=plan, xf=True, qkv_parts=qkv, cos=self.cos,
-                            sin=self.sin, kv_scales=self._kv_scales(l))
-            nxt = w.layers[l + 1].wqkv if l + 1 < L else None
-            ops.decode_block(attn, lw.wo, h, xn, ssq[2 * l + 1], ssq[2 * l + 2], lw.w_gate_up, act, lw.w_down, nxt,
-                             qkv, B, self.eps, self.blk_cnt[l], self.blk_err)
-        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, rows=B, xf=True, write_h=False)
-        self._decode_tail(B, sample, xn, True)
 
     def _decode_tail(self, B: int, sample: bool, xn, xf: bool) -> None:
         logits = self._lm_head(xn, B, xf)
@@ -797,14 +748,10 @@ class ModelRunner:
         car = getattr(self.tp, "car", None) if self.tp is not None else None
         if car is not None:
             parts.append(car.err)  # one-shot all-reduce timeout flag, read in the same transfer
-        if self.block_decode:
-            parts.append(self.blk_err)  # persistent decode block: a phase wait that timed out
         host = torch.cat(parts).cpu()
         if car is not None and int(host[2 * n]):
             raise TPCommError("tensor-parallel all-reduce: a peer did not arrive within the timeout; "
                               "this replica's outputs since the last sync are invalid")
-        if self.block_decode and int(host[-1]):
-            raise RuntimeError("decode block: a phase wait timed out; the outputs since the last sync are invalid")
         return host[:n], host[n:2 * n], idx
 
     def tokens_of(self, slot: int, n: int) -> list[int]:

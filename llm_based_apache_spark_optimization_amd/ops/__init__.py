@@ -415,12 +415,7 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
             x8, sx = quantize_rows_fp8(x)
             e.fp8_gemm_t256(x8, sx, w.data, w.scale, w.N, out, EPI[epi], splitk)
         else:  # weight-only fallback: dequantise the layer into a bf16 scratch, bf16 tile GEMM
-            buf = _dq_scratch.get(x.device)
-            if buf is None or buf.numel() < w.N * w.K:
-                buf = torch.empty(w.N * w.K, device=x.device, dtype=torch.bfloat16)
-                _dq_scratch[x.device] = buf
-            e.fp8_dequant(w.data, w.scale, w.N, w.K, buf)
-            e.gemm(x, buf[: w.N * w.K], w.N, out, EPI[epi], nb, splitk, waves, div)
+            e.gemm(x, _dequant_scratch(w, x.device), w.N, out, EPI[epi], nb, splitk, waves, div)
     elif w.kind == "mxfp4":
         if M <= 64:  # W4A16 decode GEMM, e2m1 -> bf16 in registers (v_cvt_scalef32_pk_bf16_fp4)
             e.fp4_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, **kw)
@@ -438,12 +433,16 @@ T256_SPLIT = os.environ.get("LSA_T256_SPLIT", "1") != "0"
 
 
 def _dequant_scratch(w: PackedWeight, device) -> torch.Tensor:
-    """One layer's weight dequantised to the bf16 fragment layout in a per-device scratch (prefill of quantised
-    models: one pass over 0.5-1 byte per weight, then the bf16 tile GEMM)."""
-    buf = _dq_scratch.get(device)
+    """One layer's weight dequantised to the bf16 fragment layout in a scratch (prefill of quantised models: one
+    pass over 0.5-1 byte per weight, then the bf16 tile GEMM).  One scratch per (device, HIP stream): co-served
+    engines prefill on their own streams (client.py), and a scratch shared across streams would let one stream's
+    dequant overwrite the weights another stream's GEMM is still reading.  A regrown scratch is freed on the same
+    stream that used it, so the caching allocator orders its reuse behind that stream's pending kernels."""
+    key = (torch.device(device), torch.cuda.current_stream(device).cuda_stream)
+    buf = _dq_scratch.get(key)
     if buf is None or buf.numel() < w.N * w.K:
         buf = torch.empty(w.N * w.K, device=device, dtype=torch.bfloat16)
-        _dq_scratch[device] = buf
+        _dq_scratch[key] = buf
     if w.kind == "mxfp4":
         ext().fp4_dequant(w.data, w.scale, w.N, w.K, buf)
     else:
@@ -508,28 +507,6 @@ def tile_splitk(M: int, N: int, K: int, kind: str = "bf16") -> int:
     return sk
 
 
-# Persistent post-attention decode block (csrc/kernels/decode_block.hip): n-blocks per work item of each phase and
-# consumer waves per workgroup, (nbo, nbg, nbd, nbq, cw); LSA_DECODE_BLOCK_CFG="nbo,nbg,nbd,nbq[,cw]" overrides
-# (tuning: scripts/bench_decode_block.py)
-DECODE_BLOCK_DEFAULT = (1, 2, 1, 1, 4)
-DECODE_BLOCK_CNT_INTS = 1152  # per-layer claim / done counter block (36 lines of 128 B; kernel's DB_CNT_INTS)
-
-
-def decode_block_cfg(B: int) -> tuple:
-    env = os.environ.get("LSA_DECODE_BLOCK_CFG")
-    if env:
-        c = tuple(int(v) for v in env.split(","))
-        return c + DECODE_BLOCK_DEFAULT[len(c):]
-    return DECODE_BLOCK_DEFAULT
-
-
-def decode_block_grid(B: int, device) -> int:
-    """Workgroups of the persistent block: LSA_DECODE_BLOCK_NWG, else one per CU (every workgroup owns items
-    i, i + grid, .. of each phase, so any grid size is correct; the ring's LDS admits one workgroup per CU)."""
-    env = int(os.environ.get("LSA_DECODE_BLOCK_NWG", "0"))
-    return env or num_cus(device)
-
-
 _NUM_CUS: dict = {}
 
 
@@ -538,66 +515,6 @@ def num_cus(device) -> int:
     if idx not in _NUM_CUS:
         _NUM_CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
     return _NUM_CUS[idx]
-
-
-def decode_block(attn_xf, wo: "PackedWeight", h, x_xf, ss1, ss2, wgu: "PackedWeight", act_xf, wd: "PackedWeight",
-                 wq: Optional["PackedWeight"], qout, B: int, eps: float, cnt, err, cfg: Optional[tuple] = None,
-                 timeout_s: float = 2.0, nwg: Optional[int] = None, stamps=None) -> None:
-    """One layer's post-attention block in ONE persistent launch (TP = 1, bf16 weights, B <= 64, fragment-major
-    activations): o projection + residual (h += o, x = bf16(h), ss1 += sum h^2) -> gate_up (row-scaled by ss1,
-    SiLU * up -> act) -> down + residual (h, x, ss2) -> [next layer's qkv, row-scaled by ss2, into ``qout``
-    f32 [B, nq] (a one-slab ``qkv_parts`` for the fused-RoPE attention)].  ``cnt`` (int32,
-    >= DECODE_BLOCK_CNT_INTS) must be zero at the launch (the runner zeroes every layer's counters with one memset
-    per step); ss1 / ss2 must be zero.  ``stamps`` (int64 [nwg, 16]): per-workgroup wall-clock stamps of the
-    phase boundaries (0 start, 1 prologue done, 2 o done, 3 o complete, 4 gate_up done, 5 complete, 6 down done,
-    7 complete, 8 qkv done; 9-12 items per phase)."""
-    nbo, nbg, nbd, nbq, cw = (tuple(cfg) + DECODE_BLOCK_DEFAULT[len(cfg):]) if cfg else decode_block_cfg(B)
-    d, ffn = wo.N, wd.K
-    if not _gpu(h):
-        a = from_xfrag(attn_xf, B, wo.K)
-        hn = h[:B].float() + ref.linear(a, wo.dense(), "f32")
-        h[:B].copy_(hn)
-        x16 = hn.to(torch.bfloat16)
-        x_xf.view(-1)[: xfrag_tiles(B) * 16 * d].copy_(to_xfrag(x16))
-        ss1[:B] += ss_q24(hn.pow(2).sum(1))
-        rs1 = torch.rsqrt(ss_float(ss1[:B]) / d + eps)[:, None]
-        gu = ref.linear(x16, wgu.dense(), "f32") * rs1
-        g, u = gu.view(B, -1, 2, 16)[:, :, 0].reshape(B, -1), gu.view(B, -1, 2, 16)[:, :, 1].reshape(B, -1)
-        act = (torch.nn.functional.silu(g) * u).to(torch.bfloat16)
-        act_xf.view(-1)[: xfrag_tiles(B) * 16 * ffn].copy_(to_xfrag(act))
-        hn = h[:B].float() + ref.linear(act, wd.dense(), "f32")
-        h[:B].copy_(hn)
-        x16 = hn.to(torch.bfloat16)
-        x_xf.view(-1)[: xfrag_tiles(B) * 16 * d].copy_(to_xfrag(x16))
-        ss2[:B] += ss_q24(hn.pow(2).sum(1))
-        if wq is not None:
-            rs2 = torch.rsqrt(ss_float(ss2[:B]) / d + eps)[:, None]
-            qout.view(-1)[: B * wq.N].view(B, wq.N).copy_(ref.linear(x16, wq.dense(), "f32") * rs2)
-        return
-    assert wo.kind == wgu.kind == wd.kind == "bf16" and (wq is None or wq.kind == "bf16"), "decode_block: bf16 weights"
-    ticks = int(timeout_s * ext().ar_wallclock_khz() * 1000)
-    ext().decode_block(attn_xf, wo.data, h, x_xf, ss1, ss2, wgu.data, act_xf, wd.data,
-                       wq.data if wq is not None else None, qout, B, ffn, wq.N if wq is not None else 0, float(eps),
-                       cnt, err, ticks, nwg or decode_block_grid(B, h.device), nbo, nbg, nbd, nbq, cw, stamps)
-
-
-def res_gemm(x_xf, w: "PackedWeight", h, xout_xf, ss, B: int, err, timeout_s: float = 2.0, nwg: Optional[int] = None,
-             cw: int = 4, stamps=None) -> None:
-    """Residual row-parallel projection on the decode block's LDS-DMA ring engine (csrc/kernels/decode_block.hip
-    lsa_res_gemm; TP = 1, bf16 weights, B <= 64): h[:B] += x @ W^T (f32), xout = bf16(h) in the fragment-major
-    layout, ss[:B] += row sums of h^2 (Q24).  Every workgroup owns whole 16-column n-blocks over the full K (no
-    split-K slabs, no arrival tickets), streamed into LDS by its own loader wave -- the norm-free decode step's o /
-    down projection without the slab round trip of the split-K residual epilogue."""
-    N, K = w.N, w.K
-    if not _gpu(h):
-        hn = h[:B].float() + ref.linear(from_xfrag(x_xf, B, K), w.dense(), "f32")
-        h[:B].copy_(hn)
-        xout_xf.view(-1)[: xfrag_tiles(B) * 16 * N].copy_(to_xfrag(hn.to(torch.bfloat16)))
-        ss[:B] += ss_q24(hn.pow(2).sum(1))
-        return
-    assert w.kind == "bf16", "res_gemm: bf16 weights"
-    ticks = int(timeout_s * ext().ar_wallclock_khz() * 1000)
-    ext().res_gemm(x_xf, w.data, h, xout_xf, ss, B, err, ticks, nwg or num_cus(h.device), cw, stamps)
 
 
 def xfrag_tiles(M: int) -> int:

@@ -74,7 +74,7 @@ def build_hip(jobs: int = 8, verbose: bool = False) -> Path:
     kdir = CSRC / "kernels"
     headers = sorted(kdir.glob("*.h"))
     kflags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast", "-Wno-unused-result"]
-    kflags += shlex.split(os.environ.get("LSA_HIP_EXTRA", ""))  # experiment knobs, e.g. -DLSA_XSAME=1
+    kflags += shlex.split(os.environ.get("LSA_HIP_EXTRA", ""))  # experiment knobs, e.g. -DLSA_ATTN_NT=0
     srcs = sorted(kdir.glob("*.hip"))
     tflags, ldflags = _torch_flags()
     bflags = ["-O2", "-std=c++17", "-fPIC", "-Wno-deprecated-declarations", "-Wno-unused-result", *tflags]

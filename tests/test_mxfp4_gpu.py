@@ -91,3 +91,27 @@ def test_mxfp4_engine_numerics(gpu, batch):
     assert res["ok"], res
     out = eng.generate(prompts[:2], SamplingParams(max_tokens=8, ignore_eos=True))
     assert all(r.eval_count == 8 for r in out)
+
+
+def test_fp4_prefill_two_streams_match_serial(gpu):
+    """Co-served MXFP4 engines prefill on their own streams (client.py): each stream has its own dequant scratch,
+    so interleaved prefill GEMMs of two different models give the same results as serial runs."""
+    torch.manual_seed(3)
+    M, K = 256, 2048
+    wa = ops.PackedWeight.from_dense(torch.randn(2048, K, device=gpu) / math.sqrt(K), "mxfp4")
+    wb = ops.PackedWeight.from_dense(torch.randn(4096, K, device=gpu) / math.sqrt(K), "mxfp4")  # regrows the scratch
+    xa = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    xb = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    ya0, yb0 = ops.linear(xa, wa, "bf16"), ops.linear(xb, wb, "bf16")
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(8):
+        with torch.cuda.stream(sa):
+            ya = ops.linear(xa, wa, "bf16")
+        with torch.cuda.stream(sb):
+            yb = ops.linear(xb, wb, "bf16")
+        outs.append((ya, yb))
+    torch.cuda.synchronize()
+    for ya, yb in outs:
+        assert torch.equal(ya, ya0) and torch.equal(yb, yb0)
