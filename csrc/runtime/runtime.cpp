@@ -41,9 +41,12 @@ PYBIND11_MODULE(_lsa_runtime, m) {
       .def_property_readonly("num_blocks", &BlockAllocator::num_blocks)
       .def_property_readonly("block_size", &BlockAllocator::block_size);
   py::class_<Scheduler>(m, "Scheduler")
-      .def(py::init<int, int, int, int, int>(), py::arg("num_blocks"), py::arg("block_size"), py::arg("max_slots"),
-           py::arg("max_prefill_tokens"), py::arg("max_blocks_per_seq"))
+      .def(py::init<int, int, int, int, int, int>(), py::arg("num_blocks"), py::arg("block_size"), py::arg("max_slots"),
+           py::arg("max_prefill_tokens"), py::arg("max_blocks_per_seq"), py::arg("reserve_tokens") = 64)
       .def("add", &Scheduler::add)
+      .def("grow", &Scheduler::grow, py::arg("id"), py::arg("tokens"))
+      .def("preempt", &Scheduler::preempt, py::arg("id"), py::arg("prompt_len"), py::arg("max_new"))
+      .def("youngest_first", &Scheduler::youngest_first)
       .def("admit", &Scheduler::admit)
       .def("finish", &Scheduler::finish)
       .def("block_table", &Scheduler::block_table)
@@ -54,5 +57,6 @@ PYBIND11_MODULE(_lsa_runtime, m) {
       .def_property_readonly("num_running", &Scheduler::num_running)
       .def_property_readonly("highest_slot", &Scheduler::highest_slot)
       .def_property_readonly("kv_usage", &Scheduler::kv_usage)
-      .def_property_readonly("free_blocks", &Scheduler::free_blocks);
+      .def_property_readonly("free_blocks", &Scheduler::free_blocks)
+      .def_property_readonly("reserve_tokens", &Scheduler::reserve_tokens);
 }

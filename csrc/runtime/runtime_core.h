@@ -90,27 +90,43 @@ class BlockAllocator {
 };
 
 // ------------------------------------------------------------------------------------- scheduler
+// KV reservation is lazy: admission reserves the prompt plus at most `reserve_tokens` generated tokens (one 64-token
+// block by default; < 0 = the whole prompt + max_new up front, the pre-round-4 behaviour), and the engine grows a
+// running request's table before each decode run (grow) as its context crosses block boundaries.  When the arena is
+// exhausted the engine preempts (preempt): the request's blocks and slot are released and it is re-queued at the
+// FRONT of the waiting queue with its generated tokens folded into its prompt (recompute on re-admission).  Without
+// this, Ollama's generate-until-EOS default (max_new = the whole remaining window) pinned a full-window KV reservation
+// per request for a ~30-token SQL answer.
 struct Req {
   long long id;
   int prompt_len;
   int max_new;
   int slot = -1;
+  long long admit_seq = -1;  // admission order (preemption picks the youngest)
   std::vector<int> blocks;
 };
 
 class Scheduler {
  public:
-  Scheduler(int num_blocks, int block_size, int max_slots, int max_prefill_tokens, int max_blocks_per_seq)
+  Scheduler(int num_blocks, int block_size, int max_slots, int max_prefill_tokens, int max_blocks_per_seq,
+            int reserve_tokens = 64)
       : alloc_(num_blocks, block_size), max_slots_(max_slots), max_prefill_tokens_(max_prefill_tokens),
-        max_blocks_per_seq_(max_blocks_per_seq), slots_(max_slots, -1) {}
+        max_blocks_per_seq_(max_blocks_per_seq), reserve_tokens_(reserve_tokens), slots_(max_slots, -1) {}
 
   void add(long long id, int prompt_len, int max_new) {
     if (reqs_.count(id)) throw std::invalid_argument("duplicate request id");
+    if (prompt_len < 1 || max_new < 1) throw std::invalid_argument("empty prompt or max_new < 1");
     const int need = alloc_.blocks_for(prompt_len + max_new);
     if (need > max_blocks_per_seq_) throw std::invalid_argument("request exceeds max model length");
     if (need > alloc_.num_blocks() - 1) throw std::invalid_argument("request larger than the whole KV cache");
     reqs_[id] = Req{id, prompt_len, max_new};
     waiting_.push_back(id);
+  }
+
+  // blocks reserved when a request is admitted
+  int admit_blocks(const Req& r) const {
+    const int gen = reserve_tokens_ < 0 ? r.max_new : std::min(r.max_new, reserve_tokens_);
+    return alloc_.blocks_for(r.prompt_len + gen);
   }
 
   // Admit waiting requests (FCFS) while a slot, the prefill budget and KV blocks allow.
@@ -121,7 +137,7 @@ class Scheduler {
     while (!waiting_.empty()) {
       Req& r = reqs_.at(waiting_.front());
       if (!out.empty() && r.prompt_len > budget) break;  // always admit at least one if it fits
-      const int need = alloc_.blocks_for(r.prompt_len + r.max_new);
+      const int need = admit_blocks(r);
       if (!alloc_.can_alloc(need)) break;
       int slot = -1;
       for (int s = 0; s < max_slots_; ++s)
@@ -129,11 +145,55 @@ class Scheduler {
       if (slot < 0) break;
       r.blocks = alloc_.alloc(need);
       r.slot = slot;
+      r.admit_seq = ++admit_counter_;
       slots_[slot] = r.id;
       budget -= r.prompt_len;
       out.push_back(r.id);
       waiting_.pop_front();
     }
+    return out;
+  }
+
+  // Make a running request own the blocks for its first `tokens` cache positions (capped at prompt + max_new).
+  // Returns the number of blocks added (0 if it already had them), or -1 when the arena cannot supply them
+  // (nothing is allocated then).
+  int grow(long long id, int tokens) {
+    Req& r = reqs_.at(id);
+    if (r.slot < 0) throw std::invalid_argument("grow: request is not running");
+    const int want = std::min(alloc_.blocks_for(std::min(tokens, r.prompt_len + r.max_new)), max_blocks_per_seq_);
+    const int add = want - (int)r.blocks.size();
+    if (add <= 0) return 0;
+    if (!alloc_.can_alloc(add)) return -1;
+    const std::vector<int> nb = alloc_.alloc(add);
+    r.blocks.insert(r.blocks.end(), nb.begin(), nb.end());
+    return add;
+  }
+
+  // Release a running request's slot and blocks and put it back at the front of the waiting queue with a new
+  // (prompt, max_new): the engine folds the tokens generated so far into the prompt and re-prefills them.
+  void preempt(long long id, int prompt_len, int max_new) {
+    Req& r = reqs_.at(id);
+    if (r.slot < 0) throw std::invalid_argument("preempt: request is not running");
+    if (prompt_len < 1 || max_new < 1 || alloc_.blocks_for(prompt_len + max_new) > max_blocks_per_seq_)
+      throw std::invalid_argument("preempt: bad resumed lengths");
+    slots_[r.slot] = -1;
+    r.slot = -1;
+    r.admit_seq = -1;
+    alloc_.release(r.blocks);
+    r.blocks.clear();
+    r.prompt_len = prompt_len;
+    r.max_new = max_new;
+    waiting_.push_front(id);
+  }
+
+  // running requests, youngest admission first (the engine's preemption order)
+  std::vector<long long> youngest_first() const {
+    std::vector<std::pair<long long, long long>> v;
+    for (long long s : slots_)
+      if (s >= 0) v.emplace_back(-reqs_.at(s).admit_seq, s);
+    std::sort(v.begin(), v.end());
+    std::vector<long long> out;
+    for (auto& p : v) out.push_back(p.second);
     return out;
   }
 
@@ -171,12 +231,13 @@ class Scheduler {
     return 1.0 - (double)alloc_.num_free() / (double)(alloc_.num_blocks() - 1);
   }
   int free_blocks() const { return alloc_.num_free(); }
+  int reserve_tokens() const { return reserve_tokens_; }
 
  private:
   BlockAllocator alloc_;
-  int max_slots_, max_prefill_tokens_, max_blocks_per_seq_;
+  int max_slots_, max_prefill_tokens_, max_blocks_per_seq_, reserve_tokens_;
+  long long admit_counter_ = 0;
   std::vector<long long> slots_;
   std::deque<long long> waiting_;
   std::unordered_map<long long, Req> reqs_;
 };
-

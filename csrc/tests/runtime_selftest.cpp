@@ -67,8 +67,26 @@ static void test_scheduler(std::mt19937& rng) {
   long long next = 1;
   std::set<long long> known;
   for (int step = 0; step < 5000; ++step) {
-    const int op = rng() % 3;
-    if (op == 0) {
+    const int op = rng() % 5;
+    if (op == 3 && s.num_running() > 0) {  // lazy growth of a random running request
+      const auto run = s.running();
+      const long long id = run[rng() % run.size()];
+      const int before = (int)s.block_table(id).size(), free0 = s.free_blocks();
+      const int got = s.grow(id, 1 + rng() % (bs * maxb + 100));
+      REQUIRE(got == -1 ? ((int)s.block_table(id).size() == before && s.free_blocks() == free0)
+                        : ((int)s.block_table(id).size() == before + got && s.free_blocks() == free0 - got));
+      REQUIRE((int)s.block_table(id).size() <= maxb);
+    } else if (op == 4 && s.num_running() > 0) {  // preempt the youngest, re-queued first
+      const long long id = s.youngest_first().front();
+      const int p = 1 + rng() % 300, m = 1 + rng() % 200;
+      if ((p + m + bs - 1) / bs > maxb) {
+        REQUIRE(throws([&] { s.preempt(id, p, m); }));
+      } else {
+        const int w0 = s.num_waiting();
+        s.preempt(id, p, m);
+        REQUIRE(s.slot(id) == -1 && s.block_table(id).empty() && s.num_waiting() == w0 + 1);
+      }
+    } else if (op == 0) {
       const int p = 1 + rng() % 300, m = 1 + rng() % 400;
       if ((p + m + bs - 1) / bs > maxb) {
         REQUIRE(throws([&] { s.add(next, p, m); }));
@@ -83,7 +101,7 @@ static void test_scheduler(std::mt19937& rng) {
         const int sl = s.slot(id);
         REQUIRE(sl >= 0 && sl < slots && s.slot_owners()[sl] == id);
       }
-    } else if (!known.empty()) {
+    } else if (op == 2 && !known.empty()) {
       auto it = known.begin();
       std::advance(it, rng() % known.size());
       s.finish(*it);

@@ -58,6 +58,9 @@ class Settings:
     # server safety cap on generated tokens per request (0 = the model context window); far above any
     # typical NL->SQL or explanation answer, it only bounds a model that never emits EOS
     max_new_cap: int = dataclasses.field(default_factory=lambda: _env("MAX_NEW_CAP", 0, int))
+    # KV reservation at admission: prompt + this many generated tokens; decode runs grow the tables block by block
+    # and an exhausted arena preempts the youngest request (-1 = reserve prompt + max_new up front)
+    kv_reserve_tokens: int = dataclasses.field(default_factory=lambda: _env("KV_RESERVE_TOKENS", 64, int))
     # chunked-prefill interleave: prompt tokens prefilled per engine iteration (0 = whole prompts); longer
     # prompts stall the running decode batch one chunk at a time.  The budget also caps prefill throughput
     # (one chunk per decode run): 512 collapsed co-serving at 16 QPS (nl2sql p50 0.56 -> 3.4 s), 2048 does not

@@ -5,8 +5,11 @@ The request lifecycle mirrors what the reference gets from the Ollama daemon beh
 160-164; Model_Evaluation_&_Comparision.py:23,114): template -> tokenize -> prefill -> decode loop ->
 detokenize, with the timing fields Ollama reports (and the reference ignored).
 
-Scheduling is native (``runtime/_lsa_runtime.Scheduler``): FCFS admission into fixed decode slots
-with KV reserved for prompt + max_new tokens.  Each engine iteration prefills newly admitted
+Scheduling is native (``runtime/_lsa_runtime.Scheduler``): FCFS admission into fixed decode slots.  KV is
+reserved lazily: admission takes the prompt plus one 64-token block, each decode run first grows the running
+tables to the context the run will reach, and when the arena is exhausted the youngest running request is
+preempted (blocks and slot released, re-queued first with its generated tokens folded into its prompt and
+re-prefilled on re-admission).  Each engine iteration prefills newly admitted
 requests (packed, one launch sequence) and then replays the captured decode graph for
 ``sync_every`` steps before reading the finished flags back — the host touches the GPU once per
 ``sync_every`` tokens, not once per token.
@@ -93,6 +96,15 @@ class Request:
     # streaming: ("tokens", ids-so-far) after every host sync that saw new tokens, then ("done", None)
     stream: Optional[queue.Queue] = None
     streamed: int = 0
+    # tokens generated before a preemption (lazy KV growth ran the arena dry): the current incarnation's prompt is
+    # prompt_ids + resumed and its params.max_tokens the remaining budget
+    resumed: list = dataclasses.field(default_factory=list)
+    preemptions: int = 0
+
+    @property
+    def ctx_ids(self) -> list:
+        """Tokens the current incarnation prefills: the prompt plus anything generated before a preemption."""
+        return self.prompt_ids + self.resumed if self.resumed else self.prompt_ids
 
 
 @dataclasses.dataclass
@@ -110,7 +122,7 @@ class GenerationResult:
 
 class LLMEngine:
     def __init__(self, runner: ModelRunner, tokenizer=None, max_prefill_tokens: int = 16384, sync_every: int = 8,
-                 name: Optional[str] = None, prefill_chunk: Optional[int] = None):
+                 name: Optional[str] = None, prefill_chunk: Optional[int] = None, kv_reserve_tokens: int = BLOCK):
         self.runner = runner
         self.spec = runner.spec
         self.name = name or self.spec.name
@@ -118,8 +130,10 @@ class LLMEngine:
         tok_eos = [e for e in getattr(self.tok, "eos_ids", ()) if 0 <= e < self.spec.vocab_size]
         if tok_eos and sorted(tok_eos) != sorted(runner.eos_list):
             runner.set_eos(sorted(set(tok_eos) | set(e for e in runner.eos_list if e >= 0)))
+        # kv_reserve_tokens: generated tokens reserved at admission (< 0: prompt + max_new up front, no growth)
         self.sched = native.Scheduler(runner.num_kv_blocks, BLOCK, runner.max_slots, max_prefill_tokens,
-                                      runner.max_blocks)
+                                      runner.max_blocks, kv_reserve_tokens)
+        self._admit_hold = False  # set by a preemption: no admissions until a running request retires
         self.sync_every = sync_every
         # decode steps per iteration when every running request ignores EOS: None = run to the first
         # length limit (offline batches); a server sets a bound so new arrivals are admitted promptly
@@ -137,7 +151,8 @@ class LLMEngine:
         self._slot_owner: dict[int, int] = {}
         self.load_time_s = 0.0
         self.stats = {"requests": 0, "prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0,
-                      "prefill_s": 0.0, "decode_s": 0.0, "decode_device_s": 0.0, "aborted": 0}
+                      "prefill_s": 0.0, "decode_s": 0.0, "decode_device_s": 0.0, "aborted": 0, "preempted": 0,
+                      "kv_grown_blocks": 0}
         # per-decode-run device timing (hipEvents around the graph replays, read after the host sync the
         # run ends with anyway): lsa_decode_step_device_seconds{model} = GPU time per token step
         self.device_timing = runner.on_gpu
@@ -187,20 +202,25 @@ class LLMEngine:
         set), run decode steps over the requests whose prompt is complete, retire finished ones."""
         r = self.runner
         with self._lock:
-            admitted = self.sched.admit()
+            # after a preemption, admit nothing while requests still run: the preempted one would otherwise be
+            # re-admitted at once and evicted again by the same growth
+            admitted = [] if (self._admit_hold and self.sched.num_running > 0) else self.sched.admit()
+            if self.sched.num_running == 0:
+                self._admit_hold = False
             t0 = time.perf_counter()
             entries = []
             for rid in admitted:
                 req = self._reqs[rid]
                 slot = self.sched.slot(rid)
-                req.slot, req.admitted = slot, t0
+                req.slot = slot
+                req.admitted = req.admitted or t0
                 self._slot_owner[slot] = rid
                 sp = req.params
                 seed = sp.seed if sp.seed is not None else (rid * 7919 + 17)
                 entries.append(dict(slot=slot, blocks=self.sched.block_table(rid), limit=sp.max_tokens,
                                     temperature=sp.temperature, top_k=sp.top_k, top_p=sp.top_p, seed=seed,
                                     eos_on=not sp.ignore_eos, repeat_penalty=sp.repeat_penalty,
-                                    repeat_last_n=sp.repeat_last_n, prompt_ids=req.prompt_ids,
+                                    repeat_last_n=sp.repeat_last_n, prompt_ids=req.ctx_ids,
                                     defer_table=self.prefill_chunk is not None))
                 self._prefilling.append(req)
             r.set_slots(entries)  # one batched host -> device transfer for every admitted request
@@ -208,17 +228,16 @@ class LLMEngine:
                 done_now = self._prefill_some()
                 t1 = time.perf_counter()
                 for q in done_now:
-                    q.first_token = t1
+                    q.first_token = q.first_token or t1
                     q.gen_host = 1
                     if q.stream is not None:  # the prefill's token goes out now (one sync, streaming only)
-                        q.streamed = 1
-                        q.stream.put(("tokens", r.tokens_of(q.slot, 1)))
+                        q.streamed = len(q.resumed) + 1
+                        q.stream.put(("tokens", q.resumed + r.tokens_of(q.slot, 1)))
                 self.stats["prefill_s"] += t1 - t0
             pending = {q.rid for q in self._prefilling}
             running = [rid for rid in self.sched.running() if rid not in pending]
             if not running:
                 return []
-            B = r.bucket(self.sched.highest_slot + 1)
             sample = any(self._reqs[rid].params.needs_sampler for rid in running)
             # steps until the earliest request can hit its length limit; with EOS possible, at most
             # sync_every steps between host checks
@@ -230,8 +249,14 @@ class LLMEngine:
                 n_steps = remaining if self.run_ahead is None else min(self.run_ahead, remaining)
             else:
                 n_steps = min(self.sync_every, remaining)
+            if n_steps:
+                reqs = self._grow_kv(reqs, n_steps)  # lazy KV: grow the tables for this run, preempting if needed
+                running = [q.rid for q in reqs]
+                if not reqs:
+                    return []
+            B = r.bucket(self.sched.highest_slot + 1)
             # host-side bound on every row's context during the run (selects the decode graph's split plan)
-            max_ctx = max(len(q.prompt_ids) + min(q.gen_host + n_steps, q.params.max_tokens) for q in reqs) + 1
+            max_ctx = max(len(q.ctx_ids) + min(q.gen_host + n_steps, q.params.max_tokens) for q in reqs) + 1
         # the decode run needs no scheduler state: new requests may be added meanwhile
         t0 = time.perf_counter()
         ev = None
@@ -263,13 +288,14 @@ class LLMEngine:
                 q = self._reqs[rid]
                 if q.stream is not None and not int(fin[i]):
                     n = min(int(gl[i]), q.params.max_tokens)
-                    if n > q.streamed:  # the rows are host-visible after read_rows' sync
-                        q.streamed = n
-                        q.stream.put(("tokens", r.tokens_of(q.slot, n)))
+                    if len(q.resumed) + n > q.streamed:  # the rows are host-visible after read_rows' sync
+                        q.streamed = len(q.resumed) + n
+                        q.stream.put(("tokens", q.resumed + r.tokens_of(q.slot, n)))
                 if int(fin[i]):
                     req = self._reqs.pop(rid)
-                    n = min(int(gl[i]), req.params.max_tokens)
-                    req.output_ids = fin_toks[req.slot]
+                    req.output_ids = req.resumed + fin_toks[req.slot]
+                    n = len(req.output_ids)
+                    self._admit_hold = False
                     req.finished_at = now
                     r.release_slot(req.slot)
                     self._slot_owner.pop(req.slot, None)
@@ -282,6 +308,51 @@ class LLMEngine:
                         req.stream.put(("done", None))
                     done.append(req)
             return done
+
+    def _grow_kv(self, reqs: list, n_steps: int) -> list:
+        """Lazy KV reservation: before a decode run of ``n_steps`` every running request must own the blocks of
+        every cache position the run writes (the context after the run, less the last generated token, which is
+        never written).  Requests grow oldest admission first; when the arena runs dry the youngest running
+        request is preempted (possibly the one growing).  Returns the requests that stay in the run; the device
+        block tables of the grown ones are updated in one batched transfer."""
+        need = {q.rid: len(q.ctx_ids) + min(q.gen_host - 1 + n_steps, q.params.max_tokens - 1) for q in reqs}
+        order = self.sched.youngest_first()
+        alive = set(need)
+        grown = {}
+        for rid in reversed(order):  # oldest first
+            if rid not in alive:
+                continue
+            while True:
+                got = self.sched.grow(rid, need[rid])
+                if got >= 0:
+                    if got > 0:
+                        grown[rid] = got
+                    break
+                victim = next(v for v in order if v in alive)
+                self._preempt(self._reqs[victim])
+                alive.discard(victim)
+                grown.pop(victim, None)
+                if victim == rid:
+                    break
+        if grown:
+            self.stats["kv_grown_blocks"] += sum(grown.values())
+            self.runner.extend_tables([(self._reqs[rid].slot, self.sched.block_table(rid)) for rid in grown])
+        return [q for q in reqs if q.rid in alive]
+
+    def _preempt(self, q: Request) -> None:
+        """Release a running request's slot and KV blocks and re-queue it first; its generated tokens become part
+        of the prompt it re-prefills (recompute), its budget shrinks by as many."""
+        n = min(q.gen_host, q.params.max_tokens)
+        toks = self.runner.tokens_of(q.slot, n) if n else []
+        q.resumed = q.resumed + toks
+        q.params = dataclasses.replace(q.params, max_tokens=q.params.max_tokens - n)
+        self.runner.release_slot(q.slot)
+        self._slot_owner.pop(q.slot, None)
+        self.sched.preempt(q.rid, len(q.ctx_ids), q.params.max_tokens)
+        q.slot, q.gen_host, q.prefilled = -1, 0, 0
+        q.preemptions += 1
+        self.stats["preempted"] += 1
+        self._admit_hold = True
 
     def _trace_done(self, req: Request, n: int) -> None:
         """Engine spans of a finished request (queue -> prefill -> decode), fed to lsa_stage_seconds and,
@@ -324,13 +395,14 @@ class LLMEngine:
         final, partial, done = [], [], []
         any_sample = False
         for q in list(self._prefilling):
-            rest = len(q.prompt_ids) - q.prefilled
+            ids = q.ctx_ids
+            rest = len(ids) - q.prefilled
             take = rest if budget is None else min(rest, budget)
             if take <= 0:
                 break
-            seg = (q.slot, q.prompt_ids[q.prefilled:q.prefilled + take], q.prefilled)
+            seg = (q.slot, ids[q.prefilled:q.prefilled + take], q.prefilled)
             q.prefilled += take
-            if q.prefilled == len(q.prompt_ids):
+            if q.prefilled == len(ids):
                 final.append(seg)
                 done.append(q)
                 any_sample |= q.params.needs_sampler

@@ -17,9 +17,12 @@ def build_engine(model: str, device: Optional[str] = None, checkpoint: Optional[
                  use_graphs: bool = True, sync_every: int = 8, num_kv_blocks: Optional[int] = None,
                  max_prefill_tokens: int = 16384, kv_memory_fraction: float = 0.85,
                  warm_graphs: bool = False, prefill_chunk: Optional[int] = None,
-                 kv_dtype: Optional[str] = None, max_new_cap: Optional[int] = None) -> LLMEngine:
+                 kv_dtype: Optional[str] = None, max_new_cap: Optional[int] = None,
+                 kv_reserve_tokens: int = 64) -> LLMEngine:
     """kv_dtype: paged KV cache dtype, "bf16" | "fp8" (None: LSA_KV_FP8, default bf16).
-    max_new_cap: generated-token cap per request (None: the context window)."""
+    max_new_cap: generated-token cap per request (None: the context window).
+    kv_reserve_tokens: generated tokens whose KV is reserved at admission (the rest grows lazily; < 0 reserves
+    prompt + max_new up front)."""
     if device is None:
         device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
     t0 = time.perf_counter()
@@ -35,7 +38,7 @@ def build_engine(model: str, device: Optional[str] = None, checkpoint: Optional[
                          num_kv_blocks=num_kv_blocks, kv_memory_fraction=kv_memory_fraction, kv_dtype=kv_dtype,
                          max_new_cap=max_new_cap)
     eng = LLMEngine(runner, tok, sync_every=sync_every, max_prefill_tokens=max_prefill_tokens, name=model,
-                    prefill_chunk=prefill_chunk or None)
+                    prefill_chunk=prefill_chunk or None, kv_reserve_tokens=kv_reserve_tokens)
     if torch.device(device).type == "cuda":
         if warm_graphs:
             runner.capture_all()

@@ -536,6 +536,24 @@ class ModelRunner:
                                 dtype=torch.long)
             self.hist.index_copy_(0, idx[hsel.to(self.device)], hv[hsel].to(self.device, non_blocking=True))
 
+    def extend_tables(self, entries: Sequence[tuple]) -> None:
+        """Lazy KV growth (engine._grow_kv): rewrite the decode-visible block-table rows of running slots,
+        ``entries`` = [(slot, blocks)], whose tables gained blocks -- one pinned transfer + one index_copy for all
+        of them, between decode runs (a captured graph reads the table from device memory at every replay)."""
+        if not entries:
+            return
+        mb = self.max_blocks
+        rows = torch.zeros(len(entries), mb, dtype=torch.int32)
+        for i, (_, blocks) in enumerate(entries):
+            assert len(blocks) <= mb, "block table longer than max_model_len"
+            rows[i, : len(blocks)] = torch.tensor(list(blocks), dtype=torch.int32)
+        if self.on_gpu:
+            rows = rows.pin_memory()
+        idx = torch.tensor([int(sl) for sl, _ in entries], dtype=torch.long)
+        for sl, _ in entries:
+            assert int(sl) not in self._pending_bt, "growing a slot whose prompt is still being prefilled"
+        self.block_tables.index_copy_(0, idx.to(self.device, non_blocking=True), rows.to(self.device, non_blocking=True))
+
     def set_eos(self, ids: Sequence[int]) -> None:
         """Replace the stop-token set (same length keeps captured graphs valid; otherwise recapture)."""
         ids = list(ids) or [-1]

@@ -30,7 +30,7 @@ import torch
 log = logging.getLogger(__name__)
 
 # ModelRunner methods that launch kernels or mutate device-resident state
-MUTATORS = frozenset({"set_slot", "set_slots", "release_slot", "prefill", "prefill_chunk", "decode", "set_eos", "capture",
+MUTATORS = frozenset({"set_slot", "set_slots", "extend_tables", "release_slot", "prefill", "prefill_chunk", "decode", "set_eos", "capture",
                       "capture_all"})
 
 

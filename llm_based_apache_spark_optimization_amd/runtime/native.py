@@ -74,23 +74,33 @@ class _PyBlockAllocator:
 
 
 class _PyScheduler:
-    def __init__(self, num_blocks, block_size, max_slots, max_prefill_tokens, max_blocks_per_seq):
+    """Pure-Python twin of csrc/runtime/runtime_core.h Scheduler (lazy KV reservation + preemption)."""
+
+    def __init__(self, num_blocks, block_size, max_slots, max_prefill_tokens, max_blocks_per_seq, reserve_tokens=64):
         self._alloc = _PyBlockAllocator(num_blocks, block_size)
         self._max_slots, self._budget, self._maxb = max_slots, max_prefill_tokens, max_blocks_per_seq
+        self._reserve = reserve_tokens
         self._slots = [-1] * max_slots
         self._waiting = collections.deque()
         self._reqs = {}
+        self._admits = 0
 
     def add(self, rid, prompt_len, max_new):
         if rid in self._reqs:
             raise ValueError("duplicate request id")
+        if prompt_len < 1 or max_new < 1:
+            raise ValueError("empty prompt or max_new < 1")
         need = self._alloc.blocks_for(prompt_len + max_new)
         if need > self._maxb:
             raise ValueError("request exceeds max model length")
         if need > self._alloc.num_blocks - 1:
             raise ValueError("request larger than the whole KV cache")
-        self._reqs[rid] = {"p": prompt_len, "n": max_new, "slot": -1, "blocks": []}
+        self._reqs[rid] = {"p": prompt_len, "n": max_new, "slot": -1, "blocks": [], "seq": -1}
         self._waiting.append(rid)
+
+    def _admit_blocks(self, r):
+        gen = r["n"] if self._reserve < 0 else min(r["n"], self._reserve)
+        return self._alloc.blocks_for(r["p"] + gen)
 
     def admit(self):
         out, budget = [], self._budget
@@ -98,7 +108,7 @@ class _PyScheduler:
             r = self._reqs[self._waiting[0]]
             if out and r["p"] > budget:
                 break
-            need = self._alloc.blocks_for(r["p"] + r["n"])
+            need = self._admit_blocks(r)
             if not self._alloc.can_alloc(need):
                 break
             try:
@@ -106,11 +116,39 @@ class _PyScheduler:
             except ValueError:
                 break
             rid = self._waiting.popleft()
-            r["blocks"], r["slot"] = self._alloc.alloc(need), slot
+            self._admits += 1
+            r["blocks"], r["slot"], r["seq"] = self._alloc.alloc(need), slot, self._admits
             self._slots[slot] = rid
             budget -= r["p"]
             out.append(rid)
         return out
+
+    def grow(self, rid, tokens):
+        r = self._reqs[rid]
+        if r["slot"] < 0:
+            raise ValueError("grow: request is not running")
+        want = min(self._alloc.blocks_for(min(tokens, r["p"] + r["n"])), self._maxb)
+        add = want - len(r["blocks"])
+        if add <= 0:
+            return 0
+        if not self._alloc.can_alloc(add):
+            return -1
+        r["blocks"] += self._alloc.alloc(add)
+        return add
+
+    def preempt(self, rid, prompt_len, max_new):
+        r = self._reqs[rid]
+        if r["slot"] < 0:
+            raise ValueError("preempt: request is not running")
+        if prompt_len < 1 or max_new < 1 or self._alloc.blocks_for(prompt_len + max_new) > self._maxb:
+            raise ValueError("preempt: bad resumed lengths")
+        self._slots[r["slot"]] = -1
+        self._alloc.release(r["blocks"])
+        r.update(slot=-1, blocks=[], seq=-1, p=prompt_len, n=max_new)
+        self._waiting.appendleft(rid)
+
+    def youngest_first(self):
+        return sorted((s for s in self._slots if s >= 0), key=lambda rid: -self._reqs[rid]["seq"])
 
     def finish(self, rid):
         r = self._reqs.pop(rid, None)
@@ -157,6 +195,10 @@ class _PyScheduler:
     @property
     def free_blocks(self):
         return self._alloc.num_free
+
+    @property
+    def reserve_tokens(self):
+        return self._reserve
 
 
 def _py_levenshtein(a: str, b: str) -> int:

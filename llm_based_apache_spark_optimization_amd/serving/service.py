@@ -29,7 +29,8 @@ def engine_factory(settings: Settings, tp_factory=None):
                             dtype=dtype, max_slots=settings.max_batch, max_model_len=settings.max_model_len,
                             kv_memory_fraction=settings.kv_memory_fraction, warm_graphs=True, tp=tp,
                             prefill_chunk=settings.prefill_chunk, kv_dtype=settings.kv_dtype,
-                            max_new_cap=settings.max_new_cap or None)
+                            max_new_cap=settings.max_new_cap or None,
+                            kv_reserve_tokens=settings.kv_reserve_tokens)
 
     return build
 

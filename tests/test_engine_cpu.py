@@ -21,7 +21,8 @@ def test_block_allocator():
 
 
 def test_scheduler_admission_and_release():
-    s = native.Scheduler(num_blocks=9, block_size=64, max_slots=2, max_prefill_tokens=1000, max_blocks_per_seq=8)
+    s = native.Scheduler(num_blocks=9, block_size=64, max_slots=2, max_prefill_tokens=1000, max_blocks_per_seq=8,
+                         reserve_tokens=-1)  # reserve prompt + max_new up front
     s.add(1, 100, 28)   # 2 blocks
     s.add(2, 300, 100)  # 7 blocks -> must wait for space
     s.add(3, 10, 10)
