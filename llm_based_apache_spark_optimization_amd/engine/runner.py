@@ -402,6 +402,13 @@ class ModelRunner:
             ops.argmax_commit(logits, *st, self.eos, self.limit[:B], self.eos_on[:B],
                               part=self.amax_part if self.on_gpu else None)
 
+    def final_hidden(self, B: int) -> torch.Tensor:
+        """[B, d] bf16: the final-norm output rows of the last decode step (what the lm_head read), in row order
+        whatever layout the step's bucket used (the numerics check of tied-embedding models reads it)."""
+        if self.use_xfrag(B):
+            return ops.from_xfrag(self.xn_f, B, self.d)
+        return self.xn[:B]
+
     def bucket(self, n: int) -> int:
         b = 1
         while b < n:

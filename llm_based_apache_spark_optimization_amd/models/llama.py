@@ -182,7 +182,7 @@ def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[st
 @torch.no_grad()
 def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant_rows: int = 0,
                       decode_a8: bool = False, decode_a8_mlp: Optional[bool] = None,
-                      kv_fp8: bool = False) -> torch.Tensor:
+                      kv_fp8: bool = False, return_hidden: bool = False):
     """fp32 causal forward of one sequence over the weights exactly as packed (``dense()`` undoes the
     fragment shuffle and the fp8 quantisation, so an fp8 model is compared against its own dequantised
     weights): logits [T, V] f32.  The numerics oracle for the engine at production shapes
@@ -196,7 +196,8 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
     output does), o / down inputs stay bf16.  ``decode_a8_mlp`` (default: = decode_a8) sets the gate_up input
     separately (the engine runs gate_up W8A8 from a smaller batch than qkv).  ``kv_fp8``: the engine's fp8 KV
     cache (ops.KV_FP8) -- every rotated key and value row is rounded per (token, kv-head) to e4m3 with its
-    amax / 448 scale (ops.reference.quant_kv_rows) before attention."""
+    amax / 448 scale (ops.reference.quant_kv_rows) before attention.  ``return_hidden``: (logits, the final
+    normalised hidden states [T, d] the lm_head reads)."""
     from ..ops import reference as ref
 
     spec, dev = w.spec, w.device
@@ -264,4 +265,5 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
         act = bf(torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(T, -1)
         h = h + q8(act) @ lw.w_down.dense().float().t()
     x = bf(norm(h, w.final_norm))
-    return x @ w.lm_head.dense().float().t()
+    logits = x @ w.lm_head.dense().float().t()
+    return (logits, x) if return_hidden else logits

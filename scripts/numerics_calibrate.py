@@ -3,6 +3,8 @@ the two injected faults (one layer's down scale x1.25, swapped cached keys) per 
 4-layer duckdb-nsql-7B shape and at full depth.  One JSON line per (model, dtype, kv, batch, case).
 
     python scripts/numerics_calibrate.py [n_layers ...]      (GPU; default 4 32)
+    python scripts/numerics_calibrate.py --tied [n_layers ...]   Llama-3.2-3B shape (tied head: probe statistics;
+                                                                  default 4 28, batch 1 and 4)
 """
 import dataclasses
 import json
@@ -24,17 +26,21 @@ def prompts(n, seed=3):
 
 def main():
     dev = torch.device("cuda:0")
-    layers = [int(v) for v in sys.argv[1:]] or [4, 32]
+    args = sys.argv[1:]
+    tied = "--tied" in args
+    args = [a for a in args if a != "--tied"]
+    layers = [int(v) for v in args] or ([4, 28] if tied else [4, 32])
+    model = "llama3.2" if tied else "duckdb-nsql"
     for nl in layers:
-        spec = dataclasses.replace(get_spec("duckdb-nsql"), n_layers=nl, name=f"duckdb-nsql-{nl}l")
+        spec = dataclasses.replace(get_spec(model), n_layers=nl, name=f"{model}-{nl}l")
         for dtype, kv in (("bf16", "bf16"), ("fp8", "bf16"), ("fp8", "fp8")):
-            for B in (4, 32):
+            for B in ((1, 4) if tied else (4, 32)):
                 w = init_random(spec, dev, seed=5, kind=dtype)
                 r = ModelRunner(w, max_slots=32, max_model_len=512, use_graphs=True, num_kv_blocks=32 * 8 + 1,
                                 kv_dtype=kv)
                 eng = LLMEngine(r, name=spec.name)
                 ps = prompts(B)
-                rows = (0, B - 1)
+                rows = (0, B - 1) if B > 1 else (0,)
                 out = {"good": nm.teacher_forced_check(eng, ps, 64, check_rows=rows)}
                 truth = init_random(spec, dev, seed=5, kind=dtype)
                 with nm.scale_fault(eng, 1, 1.25):
@@ -43,7 +49,8 @@ def main():
                     out["bad_kv"] = nm.teacher_forced_check(eng, ps, 64, check_rows=rows, weights=truth)
                 for case, res in out.items():
                     res.pop("criterion", None)
-                    print(json.dumps({"layers": nl, "dtype": dtype, "kv": kv, "B": B, "case": case, **res}), flush=True)
+                    print(json.dumps({"model": model, "layers": nl, "dtype": dtype, "kv": kv, "B": B, "case": case,
+                                      **res}), flush=True)
                 del eng, r, w, truth
                 torch.cuda.empty_cache()
 
