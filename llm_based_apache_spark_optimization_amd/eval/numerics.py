@@ -50,13 +50,19 @@ THRESHOLDS = {
 # the final normalised hidden state x (what the lm_head reads), through an UNTIED seeded random probe head
 # P [PROBE_V, d] ~ N(0, PROBE_SCALE^2 / d) -- probe logits ~ N(0, PROBE_SCALE^2), a spread distribution whose
 # KL(oracle||engine) ~ PROBE_SCALE^2 / 2 x the relative error of x squared -- plus the per-position relative L2
-# error of x itself.  (mean probe KL PER LAYER, mean relative error of x) bounds per class, calibrated on MI355X at the
+# error of x itself.  Bounds per class: (mean probe KL PER LAYER, mean relative error / sqrt(n_layers)) -- healthy
+# probe KL grows ~linearly with depth, the relative error ~ as its square root.  Calibrated on MI355X at the
 # Llama-3.2-3B shape (GQA 3:1, tied), 4 and 28 layers, batch 1 and 4 (profiles/r4/numerics_calibration_tied_mi355x.jsonl,
 # scripts/numerics_calibrate.py --tied):
+#
+#   class   healthy KL / layer, rel / sqrt(L)    scale x1.25: KL / layer, rel / sqrt(L)   swapped keys
+#   bf16    8.5e-5 .. 9.6e-5, 0.0035 .. 0.0038   2.5e-2 .. 4.2e-2, 0.064 .. 0.075         6.9e-2 .., 0.10 ..
+#   w8a16   9.9e-4 .. 2.2e-3, 0.011 .. 0.018     2.8e-2 .. 4.5e-2, 0.066 .. 0.076         7.0e-2 .., 0.10 ..
+#   w8a8    1.2e-3 .. 2.8e-3, 0.014 .. 0.020     2.8e-2 .. 5.0e-2, 0.066 .. 0.076         1.1e-1 .., 0.12 ..
 TIED_THRESHOLDS = {
-    "bf16": (1.5e-4, 0.02),
-    "w8a16": (1.2e-3, 0.06),
-    "w8a8": (2.5e-3, 0.09),
+    "bf16": (4e-4, 0.012),
+    "w8a16": (6e-3, 0.035),
+    "w8a8": (7e-3, 0.038),
 }
 PROBE_V, PROBE_SCALE, PROBE_SEED = 8192, 4.0, 1234
 
@@ -191,14 +197,15 @@ def check_recorded(eng, prompts, toks, elog, n_steps: int, check_rows: Sequence[
                             f"top-5 overlap >= {t5_min}, top-1 agreement >= {t1_min}")
         return res
     pk, rel = torch.cat(pks), torch.cat(rels)
-    pk_layer, rel_max = TIED_THRESHOLDS[cls]
+    pk_layer, rel_c = TIED_THRESHOLDS[cls]
     pk_max = round(pk_layer * nl, 6)
+    rel_max = round(rel_c * nl ** 0.5, 5)
     res.update(tied_head=True, probe_kl=round(float(pk.mean()), 6), probe_kl_max=round(float(pk.max()), 6),
                hidden_rel_err=round(float(rel.mean()), 5), hidden_rel_err_max=round(float(rel.max()), 5))
     res["ok"] = bool(res["probe_kl"] < pk_max and res["hidden_rel_err"] < rel_max and res["top1_agree"] >= t1_min)
     res["criterion"] = (f"{cls}, tied lm_head: teacher-forced over {n_steps} decode steps: mean KL(oracle||engine) of an "
                         f"untied random probe head over the final hidden state < {pk_max} ({pk_layer} x {nl} layers), "
-                        f"mean relative L2 error of the final hidden state < {rel_max}, top-1 agreement of the tied "
+                        f"mean relative L2 error of the final hidden state < {rel_max} ({rel_c} x sqrt({nl})), top-1 agreement of the tied "
                         f"head >= {t1_min} (its KL is reported, but a random-init tied head is near one-hot)")
     return res
 
