@@ -35,15 +35,6 @@
 typedef __attribute__((address_space(1))) unsigned long long g_u64;
 typedef __attribute__((address_space(1))) int g_i32;
 
-// Per-sequence split of the context (the grid is sized for the longest context a captured graph can
-// see; each sequence uses what its own length needs): <= 4 blocks run unsplit (a split costs a combine
-// pass, measured slower below ~256 keys, scripts/bench_attn.py), longer contexts use splits of
-// chunk_blocks blocks, widened when the grid has fewer splits than that needs.
-// unsplit_max: the host plan's unsplit threshold (4; lower for grids too small to fill the chip).
-__device__ __forceinline__ void eff_split(int nblk, int chunk_blocks, int nsplit, int unsplit_max, int& ech, int& nse) {
-  ech = nblk <= unsplit_max ? max(nblk, 1) : max(chunk_blocks, (nblk + nsplit - 1) / nsplit);
-  nse = (nblk + ech - 1) / ech;
-}
 
 // Fused RoPE + KV append (decode): q/k/v of the new token come straight from the QKV projection's f32
 // split-K slabs; every workgroup rotates its own G query heads, the workgroup holding the last block
@@ -125,7 +116,8 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
                                                           const int* __restrict__ pos, int Hkv, float scale_log2,
                                                           int chunk_blocks, int nsplit, int unsplit_max,
                                                           uint16_t* __restrict__ out, float* __restrict__ opart, float* __restrict__ mlpart,
-                                                          int* __restrict__ counters, int xf_mt, RopeArgs ra) {
+                                                          int* __restrict__ counters, int xf_mt, RopeArgs ra,
+                                                          int part_only) {
   constexpr int D = 128;
   constexpr int NT = 64 * WV;      // threads
   constexpr int NLG = 4 * WV;      // 16-lane groups
@@ -497,7 +489,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
       O[0] += v.x * wgt; O[1] += v.y * wgt; O[2] += v.z * wgt; O[3] += v.w * wgt;
     }
     const int h = hk * G + g;
-    if (nse == 1) {
+    if (nse == 1 && !part_only) {
       const float inv = L > 0.f ? 1.f / L : 0.f;
       uint2 pk;
       pk.x = pack2bf(O[0] * inv, O[1] * inv);
@@ -514,7 +506,9 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
                            __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (nse == 1) return;
+  // part_only: every split (a single one too) leaves its (o, m, l) partial for the consumer -- the batch-<=4 latency
+  // path's o projection combines them in its prologue (decode_lat.hip), so no split waits on another here
+  if (nse == 1 || part_only) return;
 
   // split-KV combine inside the launch: the last of this (sequence, kv-head)'s nse workgroups to arrive
   // merges all partials (guide §6 G16 counter form: sc1 stores drained -> barrier -> one relaxed agent
@@ -596,7 +590,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
                                int unsplit_max, void* out, float* opart, float* mlpart, int* counters, int xf_mt,
                                const float* qkv_parts, int nparts,
                                long part_stride, const float* cos_t, const float* sin_t, const float* ks,
-                               const float* vs, hipStream_t s) {
+                               const float* vs, int part_only, hipStream_t s) {
   if (H % Hkv) return -1;
   if (xf_mt && B > 16 * xf_mt) return -4;
   if (nsplit > 256) return -3;
@@ -613,7 +607,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
 #define LSA_ADL(GV, RP, WV, KV8, SB)                                                                              \
   hipLaunchKernelGGL((attn_decode_kernel<GV, RP, WV, KV8, SB>), grid, dim3(64 * (WV)), 0, s, qq, kk, vv, ks, vs,     \
                      block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart,  \
-                     counters, xf_mt, ra)
+                     counters, xf_mt, ra, part_only)
   // waves per workgroup: 8 for G = 1 (single-buffered at >= LSA_ATTN_SB_MIN_WG workgroups); for G = 2, 3 four on
   // grids of <= LSA_ATTN_SMALL23_WG workgroups (3B batch 1, 2k context: 11.34 -> 10.74 us -- half the cross-wave
   // merge, profiles/r3/attn_decode_wv23_ab_mi355x.jsonl) and eight above (3B batch 32: 10.54 vs 11.33 us); else 4
