@@ -43,17 +43,29 @@ __device__ __forceinline__ void st_release_sys(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Residual epilogue of a row-parallel projection under TP (RES = 1, rows of D floats, D % 256 == 0): instead of
+// writing the sum back, h[i] += sum; xn = bf16(h) (fragment-major with xmt row tiles, else row-major [rows][D]); and
+// ss[row] += sum over the row of h^2 (Q24 int64 atomics, one per wave and 256 columns): the all-reduce, the residual
+// add and the folded RMSNorm's row sums in ONE launch, so a TP decode layer issues as many launches as a TP = 1 one
+// (engine/runner.py _reduce_add; the next GEMM scales its rows by rsqrt(ss / D + eps), gammas in its weights).
+struct ArRes {
+  float* h;
+  uint16_t* xn;
+  long long* ss;
+  int D, xmt;
+};
+
 // GATHER = 0: sum into data (slab 0).  GATHER = 1: all-gather, out[p * n4 + i] = rank p's data[i].
 // nslab > 1 (sum only): data holds nslab split-K partial slabs [nslab][n] (slab stride slab4 float4s,
 // e.g. a row-parallel GEMM's f32 split-K output); each rank first sums its own slabs in slab order, so
 // the split-K reduction rides along and the GEMM keeps its split-K parallelism under TP.
-template <int W, int GATHER>
+template <int W, int GATHER, int RES>
 __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restrict__ data, const long n4,
                                                                  float4* __restrict__ out,
                                                                  uint8_t* const* __restrict__ regions, const int rank,
                                                                  const size_t maxb, const long long timeout_ticks,
                                                                  int* __restrict__ err, const int nslab,
-                                                                 const long slab4) {
+                                                                 const long slab4, const ArRes res) {
   const int b = blockIdx.x, tid = threadIdx.x;
   uint8_t* mine = regions[rank];
   uint32_t* my_epoch = reinterpret_cast<uint32_t*>(mine + AR_EPOCH_OFF);
@@ -121,6 +133,8 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
     for (long i = (long)b * AR_THREADS + tid; i < n4; i += stride) {
       if (GATHER) {
         for (int p = 0; p < W; ++p) out[(long)p * n4 + i] = nv;
+      } else if (RES) {
+        reinterpret_cast<float4*>(res.h)[i] = nv;  // the residual stream itself is poisoned: every later token NaN
       } else {
         data[i] = nv;
       }
@@ -149,7 +163,25 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
                            : reinterpret_cast<const float4*>(mine + slot_off + (size_t)p * maxb)[i];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-    data[i] = acc;
+    if constexpr (RES) {
+      float4* hp = reinterpret_cast<float4*>(res.h) + i;
+      float4 hv = *hp;
+      hv.x += acc.x; hv.y += acc.y; hv.z += acc.z; hv.w += acc.w;
+      *hp = hv;
+      const long e = i * 4;
+      const int m = (int)(e / res.D), c = (int)(e - (long)m * res.D);
+      uint2 pk;
+      pk.x = pack2bf(hv.x, hv.y);
+      pk.y = pack2bf(hv.z, hv.w);
+      *reinterpret_cast<uint2*>(res.xn + (res.xmt ? xf_off(m, c, res.xmt) : (size_t)m * res.D + c)) = pk;
+      // the 64 lanes of a wave hold 256 consecutive columns of one row (D % 256 == 0, wave-aligned strides)
+      float sq = hv.x * hv.x + hv.y * hv.y + hv.z * hv.z + hv.w * hv.w;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) sq += __shfl_xor(sq, o, 64);
+      if ((tid & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(res.ss) + m, (unsigned long long)ss_to_q24(sq));
+    } else {
+      data[i] = acc;
+    }
   }
   if (tid == 0) my_epoch[b] = ep;
 }
@@ -199,10 +231,15 @@ int lsa_ar_header_bytes() { return AR_DATA_OFF; }
 
 // data: n floats (n % 4 == 0, 16-B aligned), regions: device array of `world` region pointers;
 // out == nullptr: in-place all-reduce; otherwise all-gather into out[world * n]
+// res (nullable): the residual epilogue (ArRes above) instead of writing the sum back into data
 int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
-               int nblocks, long long timeout_ticks, int* err, int nslab, long slab_stride, hipStream_t s) {
+               int nblocks, long long timeout_ticks, int* err, int nslab, long slab_stride, const float* res_h,
+               void* res_xn, long long* res_ss, int res_d, int res_xmt, hipStream_t s) {
   if (n % 4 || (size_t)n * 4 > maxb || world < 2 || world > AR_MAX_WORLD || rank < 0 || rank >= world) return -1;
   if (nslab < 1 || (nslab > 1 && (out || slab_stride % 4 || slab_stride < n))) return -1;
+  const bool rs = res_h != nullptr;
+  if (rs && (out || !res_xn || !res_ss || res_d <= 0 || res_d % 256 || n % res_d)) return -2;
+  const ArRes res{const_cast<float*>(res_h), reinterpret_cast<uint16_t*>(res_xn), res_ss, res_d, res_xmt};
   const long n4 = n / 4;
   long want = (n4 + AR_THREADS - 1) / AR_THREADS;
   int grid = (int)(want < nblocks ? want : nblocks);
@@ -210,13 +247,17 @@ int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int ran
   if (grid > AR_MAX_BLOCKS) grid = AR_MAX_BLOCKS;
 #define AR_LAUNCH(WV)                                                                                        \
   if (out)                                                                                                     \
-    hipLaunchKernelGGL((ar_oneshot_kernel<WV, 1>), dim3(grid), dim3(AR_THREADS), 0, s,                         \
+    hipLaunchKernelGGL((ar_oneshot_kernel<WV, 1, 0>), dim3(grid), dim3(AR_THREADS), 0, s,                      \
                        reinterpret_cast<float4*>(data), n4, reinterpret_cast<float4*>(out), regions, rank, maxb, \
-                       timeout_ticks, err, 1, 0L);                                                             \
-  else                                                                                                         \
-    hipLaunchKernelGGL((ar_oneshot_kernel<WV, 0>), dim3(grid), dim3(AR_THREADS), 0, s,                         \
+                       timeout_ticks, err, 1, 0L, res);                                                        \
+  else if (rs)                                                                                                 \
+    hipLaunchKernelGGL((ar_oneshot_kernel<WV, 0, 1>), dim3(grid), dim3(AR_THREADS), 0, s,                      \
                        reinterpret_cast<float4*>(data), n4, nullptr, regions, rank, maxb, timeout_ticks, err, nslab, \
-                       slab_stride / 4)
+                       slab_stride / 4, res);                                                                  \
+  else                                                                                                         \
+    hipLaunchKernelGGL((ar_oneshot_kernel<WV, 0, 0>), dim3(grid), dim3(AR_THREADS), 0, s,                      \
+                       reinterpret_cast<float4*>(data), n4, nullptr, regions, rank, maxb, timeout_ticks, err, nslab, \
+                       slab_stride / 4, res)
   switch (world) {
     case 2: AR_LAUNCH(2); break;
     case 3: AR_LAUNCH(3); break;

@@ -191,7 +191,9 @@ class ModelRunner:
         # scaling moved into the qkv / gate_up GEMMs (rownorm; gammas folded into their weights) instead of one
         # 512-thread workgroup per row with a block reduction.  TP = 1; not with W8A8 inputs (their e4m3
         # quantisation needs the whole-row amax in the norm launch) or the MLP residual epilogue
-        self.wide_norm = (os.environ.get("LSA_WIDE_NORM", "1") != "0" and tps == 1
+        # Under TP the residual add rides in the one-shot all-reduce (TPGroup.reduce_add: the sum over ranks, h +=,
+        # bf16 / fragment-major xn and the row sums in one launch), so a TP layer issues as many launches as TP = 1.
+        self.wide_norm = (os.environ.get("LSA_WIDE_NORM", "1") != "0"
                           and all(lw.norms_folded for lw in weights.layers))
         # latency path for decode buckets of <= ops.LAT_MAX_B rows (csrc/kernels/decode_lat.hip): the residual stream as
         # Q32 integer atomics, folded norms with in-kernel row sums, attention partials merged by the o projection --
@@ -215,6 +217,15 @@ class ModelRunner:
     def _kv_scales(self, l: int):
         """(ks, vs) scale tensors of layer l's fp8 cache, None for a bf16 cache."""
         return (self.kv_scale[l, 0], self.kv_scale[l, 1]) if self.kv_fp8 else None
+
+    def _reduce_add(self, parts: torch.Tensor, h: torch.Tensor, xn: torch.Tensor, ss: torch.Tensor, B: int,
+                    xf: bool) -> None:
+        """Wide residual add of a row-parallel projection's split-K slabs (+ the TP all-reduce, fused on the IPC
+        kernel): h[:B] += sum; xn = bf16(h); ss[:B] += row sums of h^2."""
+        if self.tp is None or self.tp.size == 1:
+            ops.res_add_ss(h, parts, xn, B, ss, xf=xf)
+        else:
+            self.tp.reduce_add(parts, self.h, xn, ss, B, xf=xf)
 
     def _reduce_parts(self, parts: torch.Tensor) -> torch.Tensor:
         """TP all-reduce of a row-parallel GEMM's split-K slabs; returns what the next add_rmsnorm sums."""
@@ -325,9 +336,9 @@ class ModelRunner:
             elif l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=B, xf=xf, **q8)
             elif wna:
-                ops.res_add_ss(h, d_red, xn, B, ssq[2 * l], xf=xf)
+                self._reduce_add(d_parts, h, xn, ssq[2 * l], B, xf)
             else:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_red, rows=B, xf=xf, **q8)
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=self._reduce_parts(d_parts), rows=B, xf=xf, **q8)
             # QKV as f32 split-K slabs; the attention kernel sums them, applies RoPE and appends the new
             # token's k/v to the paged cache itself (no separate rope/append launch)
             if a8:  # (layer 0 after a raw embedding launch: its e4m3 rows are un-normalised -> row scale)
@@ -344,18 +355,16 @@ class ModelRunner:
                             qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
                             sin=self.sin if fr else None, kv_scales=self._kv_scales(l))
             lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
-            o_red = self._reduce_parts(o_parts)
             if wnm:
-                ops.res_add_ss(h, o_red, xn, B, ssq[2 * l + 1], xf=xf)
+                self._reduce_add(o_parts, h, xn, ssq[2 * l + 1], B, xf)
             else:
-                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_red, rows=B, xf=xf, **q8m)
+                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=self._reduce_parts(o_parts), rows=B, xf=xf, **q8m)
             if a8m:
                 ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=act)
             else:
                 lin(xn, lw.w_gate_up, "silu", out=act, **rn_m(l))
             lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
-            d_red = self._reduce_parts(d_parts)
-        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=d_red, rows=B, xf=xf)
+        ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=self._reduce_parts(d_parts), rows=B, xf=xf)
         self._decode_tail(B, sample, xn, xf)
 
     def _decode_step_fused(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:

@@ -148,6 +148,15 @@ class IpcAllReduce:
                          t.shape[0])
         return t[:1]
 
+    def reduce_slabs_res(self, t: torch.Tensor, h: torch.Tensor, xn: torch.Tensor, ss: torch.Tensor,
+                         xmt: int = 0) -> None:
+        """The all-reduce of ``reduce_slabs`` with the residual epilogue of a row-parallel projection fused in: h
+        [rows, D] f32 += the sum over ranks of every rank's slab sum; xn = bf16(h) (fragment-major with ``xmt`` row
+        tiles, else row-major); ss[rows] += row sums of h^2 (Q24 int64).  One launch where the unfused TP step ran
+        an all-reduce and then a residual-add launch (D % 256 == 0)."""
+        ops.ext().ar_run(t, None, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err,
+                         t.shape[0], res_h=h, res_xn=xn, res_ss=ss, res_xmt=xmt)
+
     def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
         """out[world * n] = concatenation of every rank's t[n] in rank order (same push protocol)."""
         ops.ext().ar_run(t, out, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err)

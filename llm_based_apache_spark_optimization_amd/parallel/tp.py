@@ -45,6 +45,20 @@ class TPGroup:
         self.all_reduce(red)
         return red
 
+    def reduce_add(self, parts: torch.Tensor, h: torch.Tensor, xn: torch.Tensor, ss: torch.Tensor, rows: int,
+                   xf: bool = False) -> None:
+        """Residual epilogue of a row-parallel projection: h[:rows] += all-reduced slab sum of parts [nslab, rows, D];
+        xn = bf16(h) (fragment-major when xf); ss[:rows] += row sums of h^2 (Q24).  On the one-shot IPC kernel this is
+        ONE launch (``IpcAllReduce.reduce_slabs_res``); otherwise the all-reduce, then the wide residual add."""
+        from .. import ops
+
+        D = h.shape[1]
+        if (self.car is not None and parts.is_cuda and self.car.fits_slabs(parts) and D % 256 == 0
+                and h.is_contiguous() and parts.shape[1] == rows):
+            self.car.reduce_slabs_res(parts, h[:rows], xn, ss, ops.xfrag_tiles(rows) if xf else 0)
+            return
+        ops.res_add_ss(h, self.reduce_parts(parts), xn, rows, ss, xf=xf)
+
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         if self.car is not None and self.car.fits(inp) and out.is_contiguous():
             self.car.all_gather(out, inp)

@@ -60,6 +60,32 @@ def _worker(rank, world, port, q):
             if red.shape[0] != 1 or not torch.equal(red[0].cpu(), want):
                 errs.append(f"slabs ns={ns} n={n} it={it}")
             it += 1
+        # residual epilogue fused into the all-reduce (TPGroup.reduce_add): h += sum over ranks of each rank's slab
+        # sum, xn = bf16(h) (row-major and fragment-major), ss += row sums of h^2 in Q24 -- against fp32 PyTorch
+        from llm_based_apache_spark_optimization_amd import ops
+
+        for ns, rows, D in ((2, 1, 3072), (4, 32, 4096), (1, 20, 4096)):
+            n = rows * D
+            slabs = torch.stack([_inputs(rank, it + 100 * k, n) for k in range(ns)]).view(ns, rows, D).to(dev)
+            h0 = _inputs(7, it, n).view(rows, D)
+            h = h0.to(dev).clone()
+            xmt = ops.xfrag_tiles(rows) if rows > 16 else 0
+            xn = torch.zeros((xmt * 16 if xmt else rows) * D, dtype=torch.bfloat16, device=dev)
+            ss = torch.full((rows,), 5, dtype=torch.int64, device=dev)
+            car.reduce_slabs_res(slabs, h, xn, ss, xmt)
+            tot = torch.zeros(rows, D)
+            for r in range(world):
+                tot = tot + sum(_inputs(r, it + 100 * k, n) for k in range(ns)).view(rows, D)
+            want = h0 + tot
+            if (h.cpu() - want).abs().max() > 1e-4 * want.abs().max():
+                errs.append(f"res h ns={ns} rows={rows}")
+            xr = ops.from_xfrag(xn, rows, D) if xmt else xn.view(rows, D)
+            if not torch.equal(xr.cpu(), h.cpu().to(torch.bfloat16)):
+                errs.append(f"res xn rows={rows} xmt={xmt}")
+            ssw = (ss.cpu() - 5).double() / ops.SS_SCALE
+            if not torch.allclose(ssw, h.cpu().double().pow(2).sum(1), rtol=1e-5):
+                errs.append(f"res ss rows={rows}")
+            it += 1
         for n in (4096, 32 * 16000):  # all-gather (vocab-parallel logits), rank-major output
             t = _inputs(rank, it, n).to(dev)
             out = torch.empty(world * n, device=dev)
