@@ -19,7 +19,6 @@ then add_rmsnorm(final) -> gemm lm_head [-> all_gather] -> argmax/sample + commi
 """
 from __future__ import annotations
 
-import os
 
 import math
 from typing import Optional, Sequence
@@ -51,10 +50,10 @@ class ModelRunner:
         self.kv_fp8 = kv_dtype == "fp8"
         # Megatron sequence parallelism for TP prefill (SURVEY.md §2.6 P-SP): reduce-scatter the row-parallel
         # outputs, residual + RMSNorm on T/tp rows, all-gather the bf16 normalised activations
-        self.seq_parallel = (os.environ.get("LSA_SEQ_PARALLEL", "1") != "0") if seq_parallel is None else seq_parallel
-        self.sp_min_tokens = int(os.environ.get("LSA_SP_MIN_TOKENS", 256)) if sp_min_tokens is None else sp_min_tokens
-        # decode RoPE + KV append inside the attention kernel (LSA_FUSE_ROPE=0 restores the separate launch)
-        self.fuse_rope = (os.environ.get("LSA_FUSE_ROPE", "1") != "0") if fuse_rope is None else fuse_rope
+        self.seq_parallel = True if seq_parallel is None else seq_parallel
+        self.sp_min_tokens = 256 if sp_min_tokens is None else sp_min_tokens
+        # decode RoPE + KV append inside the attention kernel (fuse_rope=False restores the separate launch)
+        self.fuse_rope = True if fuse_rope is None else fuse_rope
         self.spec = spec = weights.spec
         self.device = weights.device
         self.tp = tp
@@ -148,10 +147,10 @@ class ModelRunner:
         # (7B qkv 22.0 -> 16.1 us, gate_up 33.4 -> 23.5), at 32 rows it ties on qkv and the 7B b32 bench
         # did not move (10425 vs 10357 tok/s) while the e4m3 activations cost top-1 agreement
         # (profiles/bench_fp8a_decode_mi355x.jsonl)
-        self.a8_min_batch = int(os.environ.get("LSA_FP8_A8_MIN_B", "32"))
+        self.a8_min_batch = 32
         # ... and the gate_up projection from 17 rows: at 32 rows it is 13 % faster than W8A16 (7B 22.8 -> 19.8 us,
         # profiles/bench_fp8a_decode_mi355x.jsonl) where the qkv one ties
-        self.a8_mlp_min_batch = int(os.environ.get("LSA_FP8_A8_MLP_MIN_B", "16"))
+        self.a8_mlp_min_batch = 16
         self.x8 = torch.zeros(xr * self.d if self.a8 else 1, dtype=torch.uint8, device=dev)
         self.sx8 = torch.ones(max(S, 64), **f32)
         self.o_buf = torch.zeros(8 * S * self.d, **f32)
@@ -167,8 +166,7 @@ class ModelRunner:
         # norm-free decode (TP = 1, gammas folded into wqkv / w_gate_up): the GEMMs read the raw residual
         # stream and scale rows by its RMS; the row sums of squares are produced by the embedding kernel
         # and the o / down residual epilogues into ssq[2l], ssq[2l + 1], ssq[2l + 2]
-        self.fused_norm = (os.environ.get("LSA_FUSED_NORM", "1") != "0" and tps == 1
-                           and all(lw.norms_folded for lw in weights.layers))
+        self.fused_norm = tps == 1 and all(lw.norms_folded for lw in weights.layers)
         # ... for decode buckets up to this batch: measured on MI355X (rocprofv3 decode-step spans,
         # profiles/rocprof_fused_norm_ab.txt) the norm-free step wins at batch 1 (3B 2k explain 1788 -> 1738 us,
         # 7B 2.77 -> 2.71 ms) but loses at batch 32 for the 3B (2029 -> 2087 us: the residual epilogue's
@@ -181,8 +179,7 @@ class ModelRunner:
         # step at batch 32 measured slower than the split-K GEMMs + norm launches: 7B 3.77 vs 3.49 ms per step,
         # profiles/r3/res_ring_ab_mi355x.txt -- a standalone full-K stream cannot ramp 128-352 KB per CU fast
         # enough with <= 63 KB of LDS-DMA in flight per loader wave; not wired in)
-        mb = os.environ.get("LSA_FUSED_NORM_MAX_B")
-        self.fused_norm_max_batch = int(mb) if mb is not None else (16 if self.d >= 4096 else 0)
+        self.fused_norm_max_batch = 16 if self.d >= 4096 else 0
         self.ssq = torch.zeros(2 * self.L + 2, S, dtype=torch.int64, device=dev)  # Q24 fixed point (ops.ss_q24)
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)
@@ -193,8 +190,7 @@ class ModelRunner:
         # quantisation needs the whole-row amax in the norm launch) or the MLP residual epilogue
         # Under TP the residual add rides in the one-shot all-reduce (TPGroup.reduce_add: the sum over ranks, h +=,
         # bf16 / fragment-major xn and the row sums in one launch), so a TP layer issues as many launches as TP = 1.
-        self.wide_norm = (os.environ.get("LSA_WIDE_NORM", "1") != "0"
-                          and all(lw.norms_folded for lw in weights.layers))
+        self.wide_norm = all(lw.norms_folded for lw in weights.layers)
         # latency path for decode buckets of <= ops.LAT_MAX_B rows (csrc/kernels/decode_lat.hip): the residual stream as
         # Q32 integer atomics, folded norms with in-kernel row sums, attention partials merged by the o projection --
         # five launches per layer and no residual-add / combine round trips.  TP = 1, bf16 weights, folded norms.

@@ -24,11 +24,11 @@ from .. import ops
 from .spec import ModelSpec, spec_from_hf_config
 
 
-# RMSNorm gammas folded into the following projections at load time (LSA_FOLD_NORMS=0 keeps them apart):
+# RMSNorm gammas folded into the following projections at load time (FOLD_NORMS = False keeps them apart):
 # rmsnorm(x) * g @ W^T == rmsnorm(x) @ (W * g)^T, so wqkv / w_gate_up carry the attention / MLP norm
 # weights and the stored norm vectors are ones.  The decode path then needs no norm launch at all: the
 # GEMMs read the raw residual stream and scale their output rows by its RMS (engine/runner.py fused path).
-FOLD_NORMS = os.environ.get("LSA_FOLD_NORMS", "1") != "0"
+FOLD_NORMS = True
 
 
 @dataclasses.dataclass

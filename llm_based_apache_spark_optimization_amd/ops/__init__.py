@@ -215,7 +215,7 @@ def pick_nb_splitk(M: int, N: int, K: int, epi: str) -> tuple[int, int]:
 
 
 # ----------------------------------------------------------------------------------- tuning
-_TUNING_PATH = os.environ.get("LSA_GEMM_TUNING") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
+_TUNING_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _tuning: Optional[dict] = None
 
 
@@ -278,13 +278,12 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
         key = f"{N}x{K}:{epi}:{'s' if M <= 16 else 'm'}"
         tab = _tuning_table()
         e = None
-        if os.environ.get("LSA_GEMM_BUCKETS", "1") != "0":
-            # per-batch-bucket entries (power-of-two M) where a sweep beat the s/m entry by > 3 %
-            # (scripts/bench_gemm_buckets.py, profiles/gemm_buckets_mi355x.jsonl)
-            b = 1
-            while b < M:
-                b *= 2
-            e = tab.get(f"{N}x{K}:{epi}:b{b}" + (":fp8" if kind == "fp8" else ":xf" if xf else ""))
+        # per-batch-bucket entries (power-of-two M) where a sweep beat the s/m entry by > 3 %
+        # (scripts/bench_gemm_buckets.py, profiles/gemm_buckets_mi355x.jsonl)
+        b = 1
+        while b < M:
+            b *= 2
+        e = tab.get(f"{N}x{K}:{epi}:b{b}" + (":fp8" if kind == "fp8" else ":xf" if xf else ""))
         if e is None and kind == "fp8":
             e = tab.get(key + ":fp8")
         fp8_entry = e is not None and kind == "fp8"
@@ -427,9 +426,9 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
 
 
 FP8_W8A8 = os.environ.get("LSA_FP8_W8A8", "1") != "0"
-# prefill GEMMs of >= 1024 rows whose 256^2 tile grid under-fills the chip split K on that kernel (LSA_T256_SPLIT=0:
-# the 128^2 tile kernel with split-K, as before round 3)
-T256_SPLIT = os.environ.get("LSA_T256_SPLIT", "1") != "0"
+# prefill GEMMs of >= 1024 rows whose 256^2 tile grid under-fills the chip split K on that kernel (False: the 128^2
+# tile kernel with split-K, as before round 3)
+T256_SPLIT = True
 
 
 def _dequant_scratch(w: PackedWeight, device) -> torch.Tensor:
@@ -499,8 +498,7 @@ def tile_splitk(M: int, N: int, K: int, kind: str = "bf16") -> int:
     if t256 >= 128:
         return 1
     tiles = ((nbt + 7) // 8) * ((M + 127) // 128)
-    target = int(os.environ.get("LSA_TILE_SPLIT_TARGET", "256"))
-    max_sk = int(os.environ.get("LSA_TILE_SPLIT_MAX", "8"))
+    target, max_sk = 256, 8
     sk = 1
     while tiles * sk < target and sk < max_sk and (K // 32) // (sk * 2) >= 16:
         sk *= 2
@@ -966,7 +964,7 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
 # "16" = the 16 x 16 kernel of attention.hip (64 rows per workgroup); "auto" = 32 when the longest packed
 # sequence has >= 512 rows (measured, scripts/bench_attn_prefill.py: 7B 2k 146 -> 119 us, 3B 2k 118 -> 115 us,
 # 8k 1051 -> 1021 us), else 16 (32 x 128-token prompts: 28 vs 31 us, twice the work items)
-PREFILL_ATTN = os.environ.get("LSA_PREFILL_ATTN", "auto")
+PREFILL_ATTN = "auto"
 
 
 def _prefill_kernel(cu_q: list) -> str:
@@ -1033,8 +1031,8 @@ def prefill_plan(cu_q: list[int], ctx: Optional[list[int]] = None, heads: int = 
     return PrefillPlan(kernel, w)
 
 
-# LSA_PREFILL_PAIR: auto | 1 | 0 -- heavy/light paired query blocks in the 32-row prefill kernel
-PREFILL_PAIR = os.environ.get("LSA_PREFILL_PAIR", "auto")
+# auto | 1 | 0 -- heavy/light paired query blocks in the 32-row prefill kernel
+PREFILL_PAIR = "auto"
 
 
 def _pair_blocks(n_items: int, heads: int, longest: int, qblock: int) -> bool:
