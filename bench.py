@@ -60,6 +60,29 @@ def fp8_label(r, B):
     return f"fp8 (prefill W8A8 on fp8 MFMA; decode {' / '.join(a8)} W8A8 on fp8 MFMA, the rest W8A16)"
 
 
+def apply_overrides(eng, items) -> dict:
+    """--set NAME=VALUE experiment overrides: ModelRunner attributes, or ops.NAME module constants."""
+    import ast
+
+    from llm_based_apache_spark_optimization_amd import ops
+
+    out = {}
+    for it in items:
+        k, v = it.split("=", 1)
+        try:
+            val = ast.literal_eval(v)
+        except (ValueError, SyntaxError):
+            val = v
+        if k.startswith("ops."):
+            assert hasattr(ops, k[4:]), k
+            setattr(ops, k[4:], val)
+        else:
+            assert hasattr(eng.runner, k), k
+            setattr(eng.runner, k, val)
+        out[k] = val
+    return out
+
+
 def numerics_check(eng, prompts, n_steps, rank0: bool, tp: int, model: str, dtype: str, device):
     """Teacher-forced check of the decode path at the benchmark's batch (eval/numerics.py): every rank runs the
     recording decode (TP ranks in lockstep), global rank 0 compares rows against the fp32 oracle over the
@@ -156,6 +179,9 @@ def main() -> int:
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the untimed BASELINE config 2 (batch 1) / config 3 (3B 2k explain) rounds after the "
                          "timed region (they run on one-GPU-per-replica GPU benches by default)")
+    ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
+                    help="experiment override (A/B runs; reported as 'overrides'): a ModelRunner attribute, or "
+                         "ops.NAME for a module constant of ops, e.g. --set fused_norm_max_batch=32")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -192,6 +218,7 @@ def main() -> int:
     eng = build_engine(args.model, device=str(device), dtype=args.dtype, max_slots=args.batch,
                        max_model_len=max_len, seed=0, tp=tpg, use_graphs=not args.no_graphs,
                        max_prefill_tokens=max(16384, args.batch * args.prompt_len), kv_dtype=args.kv_dtype)
+    overrides = apply_overrides(eng, args.set)
     V = eng.spec.vocab_size
     g = torch.Generator().manual_seed(1234 + replica)
     prompts = [[eng.spec.bos_id if eng.spec.bos_id < V else 1]
@@ -278,6 +305,7 @@ def main() -> int:
             "decode_device_ms_per_step": round(decode_dev_ms, 3),
             "per_gpu_tokens_per_sec": round(value / world, 2),
             "numerics": numerics,
+            **({"overrides": overrides} if overrides else {}),
             **extras,
         }
         print(json.dumps(out), flush=True)

@@ -180,6 +180,7 @@ class ModelRunner:
         # profiles/r3/res_ring_ab_mi355x.txt -- a standalone full-K stream cannot ramp 128-352 KB per CU fast
         # enough with <= 63 KB of LDS-DMA in flight per loader wave; not wired in)
         self.fused_norm_max_batch = 16 if self.d >= 4096 else 0
+        self.res_cfg = None  # experiment hook: (nb, splitk, waves, div) of the norm-free step's o / down GEMMs
         self.ssq = torch.zeros(2 * self.L + 2, S, dtype=torch.int64, device=dev)  # Q24 fixed point (ops.ss_q24)
         # arrival counters of the split-K residual epilogues (one per 16 output columns; left zeroed)
         self.res_tickets = torch.zeros(max(64, self.d // 16), dtype=torch.int32, device=dev)
@@ -382,6 +383,11 @@ class ModelRunner:
         # f32 pick where none is tuned)
         sk_o = ops.pick_gemm_config(B, d, self.H * self.D, "res", xf=xf, kind=w.layers[0].wo.kind)[1]
         sk_d = ops.pick_gemm_config(B, d, self.ffn_l, "res", xf=xf, kind=w.layers[0].w_down.kind)[1]
+        rc = {}
+        if self.res_cfg is not None:  # experiment override (bench.py --set res_cfg=(nb,splitk,waves,div))
+            nb_, sk_o, wv_, dv_ = self.res_cfg
+            sk_d = sk_o
+            rc = dict(nb=nb_, waves=wv_, div=dv_)
         qkv_parts = self.qkv_buf[: sk_q * B * nqkv].view(sk_q, B, nqkv)
         o_parts = self.o_buf[: sk_o * B * d].view(sk_o, B, d)
         d_parts = self.down_buf[: sk_d * B * d].view(sk_d, B, d)
@@ -404,9 +410,9 @@ class ModelRunner:
             ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale,
                             attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
                             qkv_parts=qkv_parts, cos=self.cos, sin=self.sin, kv_scales=self._kv_scales(l))
-            lin(attn, lw.wo, "res", out=o_parts, splitk=sk_o, res=(h, xn, ssq[2 * l + 1], tk))
+            lin(attn, lw.wo, "res", out=o_parts, splitk=sk_o, res=(h, xn, ssq[2 * l + 1], tk), **rc)
             lin(xn, lw.w_gate_up, "silu", out=act, rownorm=(ssq[2 * l + 1], self.eps))
-            lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk))
+            lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk), **rc)
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, rows=B, xf=xf, write_h=False)
         self._decode_tail(B, sample, xn, xf)
 
