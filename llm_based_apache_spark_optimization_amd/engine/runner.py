@@ -497,6 +497,36 @@ class ModelRunner:
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graphs[key] = g
 
+    def count_step_kernels(self, B: int, sample: bool = False) -> int:
+        """Kernel launches of one captured decode step of bucket B (a throw-away capture whose graph is kept and
+        walked with hipGraphGetNodes): the launch-count check of the fused TP step (tests/test_tp_launches_gpu.py)."""
+        import ctypes
+
+        assert self.use_graphs, "needs graph capture"
+        plan = tuple(self.ctx_plan(B))
+        if self.tp is not None and self.tp.size > 1:
+            self.tp.warmup()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self._decode_step(B, sample, plan)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        lib = ctypes.CDLL("libamdhip64.so")
+        graph = ctypes.c_void_p(g.raw_cuda_graph())
+        n = ctypes.c_size_t(0)
+        assert lib.hipGraphGetNodes(graph, None, ctypes.byref(n)) == 0
+        nodes = (ctypes.c_void_p * n.value)()
+        assert lib.hipGraphGetNodes(graph, nodes, ctypes.byref(n)) == 0
+        kernels = 0
+        for nd in nodes:
+            t = ctypes.c_int(-1)
+            assert lib.hipGraphNodeGetType(ctypes.c_void_p(nd), ctypes.byref(t)) == 0
+            kernels += t.value == 0  # hipGraphNodeTypeKernel
+        g.reset()
+        return kernels
+
     def buckets(self) -> list[int]:
         out, b = [], 1
         while b < self.max_slots:
