@@ -80,6 +80,7 @@ def test_tp2_step_launches_no_more_than_tp1(gpu):
         assert got[r]["fused"], "the one-shot IPC all-reduce must be available between the test ranks"
     tp2 = got[0]["n32"]
     print({"tp1_kernels": tp1, "tp2_kernels": tp2, "layers": LAYERS})
-    # the vocab-parallel logits add the one-shot all-gather and its rank-major -> row-major copy, once per step;
-    # any extra launch per layer would add LAYERS more
-    assert tp2 <= tp1 + 2, (tp1, tp2)
+    # once per step TP adds three launches: the last down projection's all-reduce ahead of the final RMSNorm (TP = 1
+    # sums its slabs inside that launch), the vocab-parallel logits' one-shot all-gather and its rank-major ->
+    # row-major copy (measured 32 -> 35 at 4 layers); any extra launch per layer would add LAYERS = 4 more
+    assert tp2 <= tp1 + 3 < tp1 + LAYERS, (tp1, tp2)
