@@ -50,11 +50,13 @@ MODEL_NAMES = {"duckdb-nsql": "duckdb-nsql-7B", "llama3.2": "Llama-3.2-3B-Instru
 
 def fp8_label(r, B):
     """Which decode GEMMs of an fp8 model run W8A8 (fp8 activations) at batch B (engine/runner.py)."""
+    a8 = [name for name, on in zip(("qkv", "gate_up", "o", "down"), r.a8_plan(B)) if on]
     if r.w.layers[0].wqkv.kind == "mxfp4":
+        if a8:
+            return (f"mxfp4 weights (e2m1 + E8M0 per 32; decode {' / '.join(a8)} W4A8: e2m1 weights and e4m3 "
+                    "activations straight into the block-scaled fp8 MFMA; prefill on the dequantised bf16 layer)")
         return ("mxfp4 weights (e2m1 + E8M0 per 32, decode W4A16: dequantised to bf16 in registers, bf16 MFMA; "
                 "prefill on the dequantised bf16 layer), bf16 activations")
-    xf = r.a8 and r.use_xfrag(B) and not (r.fused_norm and B <= r.fused_norm_max_batch)
-    a8 = [name for name, on in (("qkv", xf and B > r.a8_min_batch), ("gate_up", xf and B > r.a8_mlp_min_batch)) if on]
     if not a8:
         return "fp8 (prefill W8A8 on fp8 MFMA, decode W8A16)"
     return f"fp8 (prefill W8A8 on fp8 MFMA; decode {' / '.join(a8)} W8A8 on fp8 MFMA, the rest W8A16)"

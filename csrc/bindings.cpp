@@ -23,9 +23,11 @@ int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, 
                     int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, void* x8, float* sx8, hipStream_t s);
 int lsa_res_add_ss(float* h, const float* parts, int nparts, long part_stride, void* xn, int rows, int D, int xf_mt,
                    long long* ss_out, hipStream_t s);
-int lsa_fp8a_gemm(const void* X8, const float* sx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
-                  int epi, int nb, int splitk, int waves, int depth, int xfo, const LsaEpi* ep, hipStream_t stream);
+int lsa_a8_gemm(const void* X8, const void* s8, const float* sx, int M, int K, const void* Wq, const float* wscale,
+                const void* Sw, int wk, int N, void* out, void* out_s8, int epi, int nb, int splitk, int waves, int depth,
+                int xfo, const LsaEpi* ep, hipStream_t stream);
 int lsa_quant_xf8(const void* x, int ldx, int M, int K, int MT, void* x8, float* sx, hipStream_t s);
+int lsa_quant_xf8_blocks(const void* x, int ldx, int M, int K, int MT, int blk, void* x8, void* s8, hipStream_t s);
 int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
                 int waves, int div, int xlds, const LsaEpi* ep, hipStream_t stream);
 int lsa_fp8_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
@@ -38,7 +40,8 @@ int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* bl
                     const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit, int unsplit_max,
                     void* out, float* opart, float* mlpart, int* counters, int xf_mt, const float* qkv_parts, int nparts,
                     long part_stride,
-                    const float* cos_t, const float* sin_t, const float* ks, const float* vs, int part_only, hipStream_t s);
+                    const float* cos_t, const float* sin_t, const float* ks, const float* vs, int part_only,
+                    void* out_s8, hipStream_t s);
 int lsa_kv8_dequant(const void* kc, const void* vc, const float* ks, const float* vs, const int* block_tables,
                     int max_blocks, const int* ctx_lens, int nseq, int Hkv, int mb, void* ko, void* vo, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
@@ -255,23 +258,61 @@ void fp8_gemm_xf(const at::Tensor& xf, int64_t M, int64_t K, const at::Tensor& w
         "fp8_gemm_xf");
 }
 
-// W8A8 decode GEMM (kernels/gemm_fp8a.hip): x8 fp8 activations in the xf8 layout + per-row scales sx
-void fp8a_gemm(const at::Tensor& x8, const at::Tensor& sx, int64_t M, int64_t K, const at::Tensor& wq,
-               const at::Tensor& wscale, int64_t N, at::Tensor& out, int64_t epi, int64_t nb, int64_t splitk,
-               int64_t waves, int64_t depth, int64_t xfo, const c10::optional<at::Tensor>& rowss, double eps) {
-  need(sx, at::kFloat, "sx");
-  need(wscale, at::kFloat, "wscale");
-  TORCH_CHECK(on_dev(wq) && wq.element_size() == 1 && wq.numel() == N * K, "wq must be N*K fp8 bytes");
-  TORCH_CHECK(M >= 1 && M <= 64 && K % 128 == 0, "fp8a_gemm: M in 1..64, K % 128 == 0");
-  TORCH_CHECK(epi == 1 || epi == 2, "fp8a_gemm: f32 slabs or silu");
+// W8A8 / W4A8 decode GEMM (kernels/gemm_fp8a.hip): x8 e4m3 activations in the xf8 layout with per-row f32 scales
+// sx and / or per-lane-block E8M0 scales s8; fp8 weights (wscale per channel) or MXFP4 weights (wsc8 = their E8M0
+// block-scale words).  xfo 2: the SiLU output as e4m3 + E8M0 blocks into (out, out_s8).
+void a8_gemm(const at::Tensor& x8, const c10::optional<at::Tensor>& s8, const c10::optional<at::Tensor>& sx, int64_t M,
+             int64_t K, const at::Tensor& wq, const c10::optional<at::Tensor>& wscale,
+             const c10::optional<at::Tensor>& wsc8, int64_t N, at::Tensor& out, const c10::optional<at::Tensor>& out_s8,
+             int64_t epi, int64_t nb, int64_t splitk, int64_t waves, int64_t depth, int64_t xfo,
+             const c10::optional<at::Tensor>& rowss, double eps) {
+  const bool fp4 = wsc8.has_value();
+  TORCH_CHECK(fp4 != wscale.has_value(), "a8_gemm: exactly one of wscale (fp8) / wsc8 (mxfp4)");
+  TORCH_CHECK(M >= 1 && M <= 64 && K % 128 == 0 && N % 16 == 0, "a8_gemm: M in 1..64, K % 128 == 0, N % 16 == 0");
+  TORCH_CHECK(epi == 1 || epi == 2, "a8_gemm: f32 slabs or silu");
+  TORCH_CHECK(on_dev(wq) && wq.element_size() == 1 && wq.numel() == (fp4 ? N * K / 2 : N * K), "a8_gemm: weight bytes");
+  if (fp4) {
+    TORCH_CHECK(on_dev(*wsc8) && wsc8->numel() * wsc8->element_size() >= (N / 16) * ((K / 128 + 3) / 4) * 256,
+                "a8_gemm: mxfp4 scales too small");
+  } else {
+    need(*wscale, at::kFloat, "wscale");
+    TORCH_CHECK(wscale->numel() >= N, "a8_gemm: wscale too small");
+  }
   const int64_t mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   TORCH_CHECK(on_dev(x8) && x8.element_size() == 1 && x8.is_contiguous() && x8.numel() >= mt * 16 * K, "x8 too small");
-  TORCH_CHECK(sx.numel() >= M, "sx too small");
-  check_out(epi, out, splitk, M, N, xfo ? mt : 0);
+  TORCH_CHECK(s8.has_value() || sx.has_value(), "a8_gemm: per-row (sx) and / or block (s8) activation scales");
+  if (s8.has_value())
+    TORCH_CHECK(on_dev(*s8) && s8->element_size() == 1 && s8->numel() >= mt * 64 * (K / 128), "s8 too small");
+  if (sx.has_value()) {
+    need(*sx, at::kFloat, "sx");
+    TORCH_CHECK(sx->numel() >= M, "sx too small");
+  }
+  if (epi == 2 && xfo == 2) {
+    TORCH_CHECK(on_dev(out) && out.element_size() == 1 && out.numel() >= mt * 16 * (N / 2), "e4m3 SiLU out too small");
+    TORCH_CHECK(out_s8.has_value() && on_dev(*out_s8) && out_s8->element_size() == 1 &&
+                    out_s8->numel() >= mt * 64 * (N / 2 / 128) && (N / 2) % 128 == 0,
+                "a8_gemm: e4m3 SiLU output needs out_s8 (and N / 2 % 128 == 0)");
+  } else {
+    check_out(epi, out, splitk, M, N, xfo ? mt : 0);
+  }
   const EpiOpts eo = epi_opts(epi, M, N, K, rowss, eps, c10::nullopt, c10::nullopt, 0, c10::nullopt, c10::nullopt, N / 16);
-  check(lsa_fp8a_gemm(x8.data_ptr(), sx.data_ptr<float>(), M, K, wq.data_ptr(), wscale.data_ptr<float>(), N,
-                      out.data_ptr(), epi, nb, splitk, waves, depth, xfo, eo.on ? &eo.e : nullptr, cur_stream()),
-        "fp8a_gemm");
+  check(lsa_a8_gemm(x8.data_ptr(), s8.has_value() ? s8->data_ptr() : nullptr,
+                    sx.has_value() ? sx->data_ptr<float>() : nullptr, M, K, wq.data_ptr(),
+                    fp4 ? nullptr : wscale->data_ptr<float>(), fp4 ? wsc8->data_ptr() : nullptr, fp4 ? 1 : 0, N,
+                    out.data_ptr(), out_s8.has_value() ? out_s8->data_ptr() : nullptr, epi, nb, splitk, waves, depth, xfo,
+                    eo.on ? &eo.e : nullptr, cur_stream()),
+        "a8_gemm");
+}
+
+void quant_xf8_blocks(const at::Tensor& x, int64_t mt, int64_t blk, at::Tensor& x8, at::Tensor& s8) {
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(on_dev(x8) && x8.element_size() == 1 && x8.numel() >= mt * 16 * K, "x8 too small");
+  TORCH_CHECK(on_dev(s8) && s8.element_size() == 1 && s8.numel() >= mt * 64 * (K / 128), "s8 too small");
+  check(lsa_quant_xf8_blocks(x.data_ptr(), x.stride(0), M, K, (int)mt, (int)blk, x8.data_ptr(), s8.data_ptr(),
+                             cur_stream()),
+        "quant_xf8_blocks");
 }
 
 void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) {
@@ -486,7 +527,8 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                  at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, at::Tensor& counters, int64_t xf_mt,
                  const c10::optional<at::Tensor>& qkv_parts, const c10::optional<at::Tensor>& cos_t,
                  const c10::optional<at::Tensor>& sin_t, int64_t unsplit_max, const c10::optional<at::Tensor>& ks,
-                 const c10::optional<at::Tensor>& vs, int64_t part_only = 0) {
+                 const c10::optional<at::Tensor>& vs, int64_t part_only = 0,
+                 const c10::optional<at::Tensor>& out_s8 = c10::nullopt) {
   need(q, at::kBFloat16, "q");
   check_cache(kc, vc, ks, vs);
   need(pos, at::kInt, "pos");
@@ -495,8 +537,15 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && block_tables.is_contiguous(),
               "block_tables [>= B, max_blocks]");
   TORCH_CHECK(H > 0 && Hkv > 0 && H % Hkv == 0 && kc.size(1) == Hkv, "heads: H % Hkv == 0, cache has Hkv heads");
-  need(out, at::kBFloat16, "out");
-  TORCH_CHECK(out.numel() >= (xf_mt ? xf_mt * 16 : B) * H * 128, "attn_decode out too small");
+  if (out_s8.has_value()) {  // e4m3 output (xf8 layout) + E8M0 per (row, head): the W8A8 / W4A8 o projection's input
+    TORCH_CHECK(xf_mt > 0 && on_dev(out) && out.element_size() == 1 && out.numel() >= xf_mt * 16 * H * 128,
+                "attn_decode: e4m3 out needs xf_mt and xf_mt * 16 * H * 128 bytes");
+    TORCH_CHECK(on_dev(*out_s8) && out_s8->element_size() == 1 && out_s8->numel() >= xf_mt * 64 * H,
+                "attn_decode: out_s8 too small");
+  } else {
+    need(out, at::kBFloat16, "out");
+    TORCH_CHECK(out.numel() >= (xf_mt ? xf_mt * 16 : B) * H * 128, "attn_decode out too small");
+  }
   need(opart, at::kFloat, "opart");
   need(mlpart, at::kFloat, "mlpart");
   need(counters, at::kInt, "counters");
@@ -521,7 +570,8 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                         (int)unsplit_max, out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), counters.data_ptr<int>(), xf_mt,
                         ptr<const float>(qkv_parts), qkv_parts.has_value() ? qkv_parts->size(0) : 0,
                         qkv_parts.has_value() ? qkv_parts->stride(0) : 0, ptr<const float>(cos_t),
-                        ptr<const float>(sin_t), ptr<const float>(ks), ptr<const float>(vs), (int)part_only, cur_stream()),
+                        ptr<const float>(sin_t), ptr<const float>(ks), ptr<const float>(vs), (int)part_only,
+                        out_s8.has_value() ? out_s8->data_ptr() : nullptr, cur_stream()),
         "attn_decode");
 }
 
@@ -889,10 +939,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ids"), py::arg("emb"), py::arg("row_idx"), py::arg("write_h"), py::arg("w"), py::arg("eps"),
         py::arg("xn"), py::arg("rows"), py::arg("xf_mt") = 0, py::arg("ss_out") = py::none(), py::arg("ss_ld") = 0,
         py::arg("ss_nzero") = 0, py::arg("x8") = py::none(), py::arg("sx8") = py::none());
-  m.def("fp8a_gemm", &fp8a_gemm, py::arg("x8"), py::arg("sx"), py::arg("M"), py::arg("K"), py::arg("wq"),
-        py::arg("wscale"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"),
-        py::arg("waves") = 4, py::arg("depth") = 1, py::arg("xfo") = 1, py::arg("rowss") = py::none(),
+  m.def("a8_gemm", &a8_gemm, py::arg("x8"), py::arg("s8"), py::arg("sx"), py::arg("M"), py::arg("K"), py::arg("wq"),
+        py::arg("wscale"), py::arg("wsc8"), py::arg("N"), py::arg("out"), py::arg("out_s8"), py::arg("epi"), py::arg("nb"),
+        py::arg("splitk"), py::arg("waves"), py::arg("depth"), py::arg("xfo"), py::arg("rowss") = py::none(),
         py::arg("eps") = 1e-5);
+  m.def("quant_xf8_blocks", &quant_xf8_blocks, py::arg("x"), py::arg("mt"), py::arg("blk"), py::arg("x8"), py::arg("s8"));
   m.def("quant_xf8", &quant_xf8, py::arg("x"), py::arg("mt"), py::arg("x8"), py::arg("sx"));
   m.def("attn_set_stamps", &attn_set_stamps, py::arg("stamps") = py::none());
   m.def("rope_append", &rope_append, py::arg("qkv"), py::arg("pos"), py::arg("tok_seq"), py::arg("block_tables"),
@@ -905,7 +956,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("counters"), py::arg("xf_mt") = 0,
         py::arg("qkv_parts") = py::none(),
         py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4,
-        py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("part_only") = 0);
+        py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("part_only") = 0,
+        py::arg("out_s8") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
         py::arg("out"), py::arg("rows32") = 0);

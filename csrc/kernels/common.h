@@ -104,13 +104,29 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return t;
 }
 
-// Byte offset of fp8 activation (m, k) in the W8A8 decode layout X8[k/128][mt][64 lanes][32 B]: lane (g, r)
-// holds row 16 mt + r at k = 128 s + 16 g .. +15 (bytes 0..15) and 128 s + 64 + 16 g .. +15 (bytes 16..31),
-// the k-set of the fp8 weight layout's fragment pair (2 s, 2 s + 1).  8 consecutive k from a multiple of 8
-// are contiguous.
+// Byte offset of fp8 activation (m, k) in the W8A8 / W4A8 decode layout X8[k/128][mt][64 lanes][32 B]: lane
+// (g, r) holds row 16 mt + r at k = 128 s + 32 g .. +31 -- the B operand of one v_mfma_scale_f32_16x16x128_f8f6f4
+// step as-is, and one MX block (32 consecutive k) per lane, so a per-lane E8M0 block scale is the MFMA's own
+// scale operand.  Consecutive k are contiguous within a 32-block.
 __device__ __forceinline__ size_t xf8_off(int m, int k, int mt) {
-  const int kc = k & 127;
-  return (((size_t)(k >> 7) * mt + (m >> 4)) * 64 + 16 * ((kc & 63) >> 4) + (m & 15)) * 32 + 16 * (kc >> 6) + (kc & 15);
+  return (((size_t)(k >> 7) * mt + (m >> 4)) * 64 + 16 * ((k & 127) >> 5) + (m & 15)) * 32 + (k & 31);
+}
+// Byte offset of the E8M0 scale of that lane block in the block-scale array S8[k/128][mt][64 lanes]
+__device__ __forceinline__ size_t xs8_off(int m, int k, int mt) {
+  return ((size_t)(k >> 7) * mt + (m >> 4)) * 64 + 16 * ((k & 127) >> 5) + (m & 15);
+}
+// E8M0 exponent of the smallest power of two s with amax / s <= 448 (the e4m3 maximum), clamped to [1, 253];
+// e8m0_inv(e) = 1 / s.  ops.e8m0_for_amax is the host twin.
+__device__ __forceinline__ int e8m0_for_amax(float amax) {
+  const uint32_t b = __float_as_uint(amax * (1.0f / 448.0f));
+  const int e = (int)(b >> 23) + ((b & 0x7fffffu) != 0u);
+  return e < 1 ? 1 : (e > 253 ? 253 : e);
+}
+__device__ __forceinline__ float e8m0_inv(int e) { return __uint_as_float((uint32_t)(254 - e) << 23); }
+// 4 floats * inv -> 4 OCP e4m3 bytes
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d, float inv) {
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a * inv, b * inv, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c * inv, d * inv, lo, true);
 }
 
 // 8 floats * inv -> 8 OCP e4m3 bytes (v_cvt_pk_fp8_f32: round to nearest even, saturating)

@@ -94,11 +94,25 @@ int main() {
     expect_ok("fp8_gemm_xf", [&] { fp8_gemm_xf(xf, 4, 128, wq, sc, 64, o, 1, 1, 1, 4, 1, none, 1e-5, none, none, 0, none, none); });
     auto wq_bad = T({64 * 127}, U8);
     expect_reject("fp8_gemm_xf wq numel", [&] { fp8_gemm_xf(xf, 4, 128, wq_bad, sc, 64, o, 1, 1, 1, 4, 1, none, 1e-5, none, none, 0, none, none); });
-    auto x8 = T({16 * 128}, U8), sx = T({4}, F32);
-    expect_ok("fp8a_gemm", [&] { fp8a_gemm(x8, sx, 4, 128, wq, sc, 64, o, 1, 1, 1, 4, 1, 1, none, 1e-5); });
-    expect_reject("fp8a_gemm K % 128", [&] { fp8a_gemm(x8, sx, 4, 64, wq, sc, 128, o, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    auto x8 = T({16 * 128}, U8), sx = T({4}, F32), s8 = T({64}, U8);
+    expect_ok("a8_gemm", [&] { a8_gemm(x8, none, sx, 4, 128, wq, sc, none, 64, o, none, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    expect_ok("a8_gemm block scales", [&] { a8_gemm(x8, s8, none, 4, 128, wq, sc, none, 64, o, none, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    expect_reject("a8_gemm K % 128", [&] { a8_gemm(x8, none, sx, 4, 64, wq, sc, none, 128, o, none, 1, 1, 1, 4, 1, 1, none, 1e-5); });
     auto sx_small = T({2}, F32);
-    expect_reject("fp8a_gemm sx too small", [&] { fp8a_gemm(x8, sx_small, 4, 128, wq, sc, 64, o, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    expect_reject("a8_gemm sx too small", [&] { a8_gemm(x8, none, sx_small, 4, 128, wq, sc, none, 64, o, none, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    expect_reject("a8_gemm no activation scales", [&] { a8_gemm(x8, none, none, 4, 128, wq, sc, none, 64, o, none, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    auto s8_small = T({32}, U8);
+    expect_reject("a8_gemm s8 too small", [&] { a8_gemm(x8, s8_small, none, 4, 128, wq, sc, none, 64, o, none, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    // MXFP4 weights: N * K / 2 bytes + E8M0 words [N/16][ceil(K/512)][64]
+    auto w4 = T({64 * 64}, U8), sw4 = T({4 * 64 * 4}, U8);
+    expect_ok("a8_gemm mxfp4", [&] { a8_gemm(x8, s8, none, 4, 128, w4, none, sw4, 64, o, none, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    expect_reject("a8_gemm both weight scales", [&] { a8_gemm(x8, s8, none, 4, 128, w4, sc, sw4, 64, o, none, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    auto sw4_small = T({64}, U8);
+    expect_reject("a8_gemm mxfp4 scales", [&] { a8_gemm(x8, s8, none, 4, 128, w4, none, sw4_small, 64, o, none, 1, 1, 1, 4, 1, 1, none, 1e-5); });
+    // e4m3 SiLU output: N / 2 % 128 == 0 bytes out + block scales
+    auto wq2 = T({256 * 128}, U8), sc2 = T({256}, F32), o8 = T({16 * 128}, U8), os8 = T({64}, U8);
+    expect_ok("a8_gemm silu e4m3", [&] { a8_gemm(x8, s8, none, 4, 128, wq2, sc2, none, 256, o8, os8, 2, 4, 1, 4, 1, 2, none, 1e-5); });
+    expect_reject("a8_gemm silu e4m3 no scales", [&] { a8_gemm(x8, s8, none, 4, 128, wq2, sc2, none, 256, o8, none, 2, 4, 1, 4, 1, 2, none, 1e-5); });
     auto x = T({300, 128}, BF), xq = T({300, 128}, U8), sxq = T({300}, F32);
     expect_ok("quant_rows_fp8", [&] { quant_rows_fp8(x, xq, sxq); });
     auto xq_small = T({200, 128}, U8);

@@ -139,20 +139,34 @@ class ModelRunner:
         self.xn_f = torch.zeros(xr * self.d, **bf)
         self.attn_f = torch.zeros(xr * self.H * self.D, **bf)
         self.act_f = torch.zeros(xr * self.ffn_l, **bf)
-        # W8A8 decode (fp8 weights, fragment-major buckets): the norm launches also write the qkv / gate_up
-        # inputs as per-row-scaled e4m3 (xf8 layout) for the fp8-MFMA GEMM (ops.linear_a8)
-        self.a8 = (ops.FP8_A8_DECODE and self.on_gpu and weights.layers[0].wqkv.kind == "fp8"
-                   and self.d % 128 == 0)
-        # ... for buckets above this batch: at 64 rows the fp8-activation GEMM is 27-30 % faster than W8A16
-        # (7B qkv 22.0 -> 16.1 us, gate_up 33.4 -> 23.5), at 32 rows it ties on qkv and the 7B b32 bench
+        # W8A8 / W4A8 decode (fp8 or MXFP4 weights, ops.linear_a8 on the block-scaled fp8 MFMA, activations in the
+        # xf8 layout): the norm launches write the qkv / gate_up inputs as per-row-scaled e4m3, the decode attention
+        # writes the o input as e4m3 with one E8M0 scale per (row, head), and the gate_up GEMM's SiLU epilogue writes
+        # the down input as e4m3 with one E8M0 scale per (row, 32 columns)
+        wkind = weights.layers[0].wqkv.kind
+        self.a8 = (ops.FP8_A8_DECODE and self.on_gpu and wkind in ("fp8", "mxfp4") and self.d % 128 == 0)
+        # the down projection W8A8 needs whole 32-column blocks per SiLU workgroup (gate_up n-blocks % 4 == 0)
+        self.a8_down_ok = self.ffn_l % 128 == 0 and (2 * self.ffn_l // 16) % 4 == 0
+        # fp8: qkv W8A8 for buckets above this batch: at 64 rows the fp8-activation GEMM is 27-30 % faster than
+        # W8A16 (7B qkv 22.0 -> 16.1 us, gate_up 33.4 -> 23.5), at 32 rows it ties on qkv and the 7B b32 bench
         # did not move (10425 vs 10357 tok/s) while the e4m3 activations cost top-1 agreement
-        # (profiles/bench_fp8a_decode_mi355x.jsonl)
-        self.a8_min_batch = 32
-        # ... and the gate_up projection from 17 rows: at 32 rows it is 13 % faster than W8A16 (7B 22.8 -> 19.8 us,
-        # profiles/bench_fp8a_decode_mi355x.jsonl) where the qkv one ties
-        self.a8_mlp_min_batch = 16
+        # (profiles/bench_fp8a_decode_mi355x.jsonl); MXFP4: every bucket (the W4A16 kernel widens each e2m1 weight
+        # on the VALU -- README: its gate_up streams ~3.1 TB/s)
+        self.a8_min_batch = 32 if wkind == "fp8" else 0
+        # ... the gate_up (and with it the down) projection from 17 rows: at 32 rows it is 13 % faster than W8A16
+        # (7B 22.8 -> 19.8 us, profiles/bench_fp8a_decode_mi355x.jsonl) where the qkv one ties
+        self.a8_mlp_min_batch = 16 if wkind == "fp8" else 0
+        # ... and the o projection from the same batch
+        self.a8_o_min_batch = 16 if wkind == "fp8" else 0
         self.x8 = torch.zeros(xr * self.d if self.a8 else 1, dtype=torch.uint8, device=dev)
         self.sx8 = torch.ones(max(S, 64), **f32)
+        mt64 = ops.xfrag_tiles(min(S, 64))
+        self.x8o = torch.zeros(xr * self.H * self.D if self.a8 else 1, dtype=torch.uint8, device=dev)
+        self.s8o = torch.full((mt64 * 64 * (self.H * self.D // 128) if self.a8 else 1,), 127, dtype=torch.uint8,
+                              device=dev)
+        a8d = self.a8 and self.a8_down_ok
+        self.x8d = torch.zeros(xr * self.ffn_l if a8d else 1, dtype=torch.uint8, device=dev)
+        self.s8d = torch.full((mt64 * 64 * (self.ffn_l // 128) if a8d else 1,), 127, dtype=torch.uint8, device=dev)
         self.o_buf = torch.zeros(8 * S * self.d, **f32)
         self.down_buf = torch.zeros(8 * S * self.d, **f32)
         self.qkv_buf = torch.zeros(8 * S * (self.H + 2 * self.Hkv) * self.D, **f32)
@@ -240,6 +254,13 @@ class ModelRunner:
             return 1  # RCCL reduces one slab; the one-shot kernel folds split-K slabs into the all-reduce
         return ops.pick_gemm_config(M, N or self.d, K, "f32", xf=xf, kind=self.w.layers[0].wo.kind)[1]
 
+    def a8_plan(self, B: int) -> tuple[bool, bool, bool, bool]:
+        """Which decode projections run W8A8 / W4A8 (e4m3 activations) at bucket B: (qkv, gate_up, o, down)."""
+        if not self.a8 or B > 64:
+            return (False, False, False, False)
+        qkv, gu, o = B > self.a8_min_batch, B > self.a8_mlp_min_batch, B > self.a8_o_min_batch
+        return (qkv, gu, o, gu and self.a8_down_ok)
+
     def use_xfrag(self, B: int) -> bool:
         """Fragment-major activations pay off once a decode batch spans >1 row tile (B > 16):
         measured 8-20 % faster GEMMs at B = 32 (scripts/bench_xf.py); bf16 and fp8 weights."""
@@ -287,18 +308,21 @@ class ModelRunner:
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         if self.lat and B <= self.lat_max_batch:
             return self._decode_step_lat(B, sample, plan)
-        if self.fused_norm and B <= self.fused_norm_max_batch:
+        a8, a8m, a8o, a8d = self.a8_plan(B)  # qkv / gate_up / o / down W8A8 (W4A8)
+        if self.fused_norm and B <= self.fused_norm_max_batch and not (a8 or a8m or a8o):
             return self._decode_step_fused(B, sample, plan)
         w, d = self.w, self.d
         ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
         h = self.h[:B]
-        xf = self.use_xfrag(B)
-        sk_o = self._splitk(B, self.H * self.D, xf=xf)
-        sk_d = self._splitk(B, self.ffn_l, xf=xf)
+        # e4m3 activations live in the xf8 layout: every GEMM input of the step is then fragment-major
+        xf = self.step_xfrag(B)
+        ak = "fp8a" if w.layers[0].wo.kind == "fp8" else "fp4a"
+        sk_o = (self._splitk(B, self.H * self.D, xf=xf) if not a8o else
+                ops.pick_gemm_config(B, d, self.H * self.D, "f32", xf=True, kind=ak)[1])
+        sk_d = (self._splitk(B, self.ffn_l, xf=xf) if not a8d else
+                ops.pick_gemm_config(B, d, self.ffn_l, "f32", xf=True, kind=ak)[1])
         nqkv = (self.H + 2 * self.Hkv) * self.D
-        a8 = self.a8 and xf and B > self.a8_min_batch  # qkv W8A8
-        a8m = self.a8 and xf and B > self.a8_mlp_min_batch  # gate_up W8A8
-        sk_q = (ops.pick_gemm_config(B, nqkv, d, "f32", xf=True, kind="fp8a")[1] if a8
+        sk_q = (ops.pick_gemm_config(B, nqkv, d, "f32", xf=True, kind=ak)[1] if a8
                 else self._splitk(B, d, nqkv, tp_reduced=False, xf=xf))
         q8 = dict(x8=self.x8, sx8=self.sx8) if a8 else {}
         q8m = dict(x8=self.x8, sx8=self.sx8) if a8m else {}
@@ -348,19 +372,27 @@ class ModelRunner:
                                 kv_scales=self._kv_scales(l))
             fr = self.fuse_rope
             ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale,
-                            attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
-                            qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
-                            sin=self.sin if fr else None, kv_scales=self._kv_scales(l))
-            lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
+                            (self.x8o if a8o else attn) if xf else attn.view(B, self.H, self.D), workspace=ws,
+                            plan=plan, xf=xf, qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
+                            sin=self.sin if fr else None, kv_scales=self._kv_scales(l),
+                            out_s8=self.s8o if a8o else None)
+            if a8o:
+                ops.linear_a8(self.x8o, None, B, lw.wo, "f32", out=o_parts, splitk=sk_o, s8=self.s8o)
+            else:
+                lin(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
             if wnm:
                 self._reduce_add(o_parts, h, xn, ssq[2 * l + 1], B, xf)
             else:
                 ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=self._reduce_parts(o_parts), rows=B, xf=xf, **q8m)
             if a8m:
-                ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=act)
+                ops.linear_a8(self.x8, self.sx8, B, lw.w_gate_up, "silu", out=self.x8d if a8d else act,
+                              out_s8=self.s8d if a8d else None)
             else:
                 lin(xn, lw.w_gate_up, "silu", out=act, **rn_m(l))
-            lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
+            if a8d:
+                ops.linear_a8(self.x8d, None, B, lw.w_down, "f32", out=d_parts, splitk=sk_d, s8=self.s8d)
+            else:
+                lin(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, parts=self._reduce_parts(d_parts), rows=B, xf=xf)
         self._decode_tail(B, sample, xn, xf)
 
@@ -468,9 +500,17 @@ class ModelRunner:
     def final_hidden(self, B: int) -> torch.Tensor:
         """[B, d] bf16: the final-norm output rows of the last decode step (what the lm_head read), in row order
         whatever layout the step's bucket used (the numerics check of tied-embedding models reads it)."""
-        if self.use_xfrag(B):
+        if self.step_xfrag(B):
             return ops.from_xfrag(self.xn_f, B, self.d)
         return self.xn[:B]
+
+    def step_xfrag(self, B: int) -> bool:
+        """Whether the decode step of bucket B hands its activations on in the fragment-major layouts (use_xfrag,
+        or -- any W8A8 / W4A8 projection -- the xf8 one, which forces it at any batch)."""
+        if self.lat and B <= self.lat_max_batch:
+            return False
+        a8, a8m, a8o, _ = self.a8_plan(B)
+        return self.use_xfrag(B) or a8 or a8m or a8o
 
     def bucket(self, n: int) -> int:
         b = 1

@@ -132,11 +132,9 @@ def compare_hidden(engine_x: torch.Tensor, oracle_x: torch.Tensor) -> dict:
 
 def numerics_class(runner, decode_batch: int) -> str:
     """Which threshold row applies to the decode path at ``decode_batch`` (see engine/runner.py)."""
+    a8 = any(runner.a8_plan(decode_batch))
     if runner.w.layers[0].wqkv.kind != "fp8":
-        return "bf16"
-    xf = runner.a8 and runner.use_xfrag(decode_batch) and not (
-        runner.fused_norm and decode_batch <= runner.fused_norm_max_batch)
-    a8 = xf and (decode_batch > runner.a8_min_batch or decode_batch > runner.a8_mlp_min_batch)
+        return "w8a8" if a8 else "bf16"  # MXFP4: the oracle multiplies its dequantised weights; W4A8 rounds activations
     return "w8a8" if a8 or runner.kv_fp8 else "w8a16"
 
 
@@ -161,9 +159,7 @@ def check_recorded(eng, prompts, toks, elog, n_steps: int, check_rows: Sequence[
     w = weights if weights is not None else r.w
     fp8 = w.layers[0].wqkv.kind == "fp8"
     rows = prefill_rows if prefill_rows is not None else sum(len(p) for p in prompts)
-    unfused_xf = bool(r.a8 and r.use_xfrag(B) and not (r.fused_norm and B <= r.fused_norm_max_batch))
-    da8 = unfused_xf and B > r.a8_min_batch
-    da8m = unfused_xf and B > r.a8_mlp_min_batch
+    plan = dict(zip(("qkv", "gate_up", "o", "down"), r.a8_plan(B)))
     ehid = None
     if isinstance(elog, tuple):
         elog, ehid = elog
@@ -171,8 +167,8 @@ def check_recorded(eng, prompts, toks, elog, n_steps: int, check_rows: Sequence[
     for i in sorted(set(check_rows)):
         p = list(prompts[i])
         aq = len(p) if (fp8 and rows > 64 and ops.FP8_W8A8) else 0
-        lg, xo = reference_forward(w, p + list(toks[i][:n_steps]), act_quant_rows=aq, decode_a8=da8,
-                                   decode_a8_mlp=da8m, kv_fp8=r.kv_fp8, return_hidden=True)
+        lg, xo = reference_forward(w, p + list(toks[i][:n_steps]), act_quant_rows=aq, decode_a8=plan,
+                                   kv_fp8=r.kv_fp8, return_hidden=True)
         c = compare(elog[i], lg[len(p):len(p) + n_steps])
         kls.append(c["kl"])
         t1s.append(c["top1"])

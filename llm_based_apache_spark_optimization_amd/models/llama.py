@@ -181,7 +181,7 @@ def load_safetensors_dir(path: str, device="cpu", kind="bf16", name: Optional[st
 
 @torch.no_grad()
 def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant_rows: int = 0,
-                      decode_a8: bool = False, decode_a8_mlp: Optional[bool] = None,
+                      decode_a8=False, decode_a8_mlp: Optional[bool] = None,
                       kv_fp8: bool = False, return_hidden: bool = False):
     """fp32 causal forward of one sequence over the weights exactly as packed (``dense()`` undoes the
     fragment shuffle and the fp8 quantisation, so an fp8 model is compared against its own dequantised
@@ -194,7 +194,11 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
     ``decode_a8`` (the W8A8 decode GEMMs of fragment-major buckets, ops.linear_a8) the qkv / gate_up inputs of
     the rows past the prompt are rounded per row to e4m3 from the f32 norm output (as add_rmsnorm's fp8
     output does), o / down inputs stay bf16.  ``decode_a8_mlp`` (default: = decode_a8) sets the gate_up input
-    separately (the engine runs gate_up W8A8 from a smaller batch than qkv).  ``kv_fp8``: the engine's fp8 KV
+    separately (the engine runs gate_up W8A8 from a smaller batch than qkv).  ``decode_a8`` may also be a dict
+    {qkv, gate_up, o, down} of the projections the engine runs W8A8 / W4A8 (ModelRunner.a8_plan): the o input is
+    then rounded to e4m3 with one E8M0 scale per (row, head) from the f32 attention output, the down input with one
+    per (row, 32 columns) from the f32 SiLU product (ops.quantize_blocks_fp8, as the kernels write them); fp8 and
+    MXFP4 weights alike.  ``kv_fp8``: the engine's fp8 KV
     cache (ops.KV_FP8) -- every rotated key and value row is rounded per (token, kv-head) to e4m3 with its
     amax / 448 scale (ops.reference.quant_kv_rows) before attention.  ``return_hidden``: (logits, the final
     normalised hidden states [T, d] the lm_head reads)."""
@@ -230,8 +234,20 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
         return torch.cat([head, x[aq:]], 0)
 
     fp8w = w.layers[0].wqkv.kind == "fp8"
-    da8 = decode_a8 and fp8w
-    da8m = (decode_a8 if decode_a8_mlp is None else decode_a8_mlp) and fp8w
+    if isinstance(decode_a8, dict):
+        qw = w.layers[0].wqkv.kind in ("fp8", "mxfp4")
+        da8, da8m = bool(decode_a8.get("qkv")) and qw, bool(decode_a8.get("gate_up")) and qw
+        da8o, da8d = bool(decode_a8.get("o")) and qw, bool(decode_a8.get("down")) and qw
+    else:
+        da8 = decode_a8 and fp8w
+        da8m = (decode_a8 if decode_a8_mlp is None else decode_a8_mlp) and fp8w
+        da8o = da8d = False
+
+    def qblk(x, raw, on, blk):  # o / down inputs of the decode rows: block-scaled e4m3 from the f32 values
+        if not on or aq >= T:
+            return x
+        from ..ops import dequant_blocks_fp8, quantize_blocks_fp8
+        return torch.cat([x[:aq], dequant_blocks_fp8(*quantize_blocks_fp8(raw[aq:], blk))], 0)
 
     def e4m3_rows(x):
         amax = x.abs().amax(1, keepdim=True)
@@ -258,11 +274,13 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
             q, k, v = bf(rope(q)), bf(rope(k)), bf(v)
         k, v = k.repeat_interleave(G, 1), v.repeat_interleave(G, 1)
         s = torch.einsum("qhd,khd->hqk", q, k) / math.sqrt(hd) + mask
-        a = bf(torch.einsum("hqk,khd->qhd", s.softmax(-1), v).reshape(T, H * hd))
+        a32 = torch.einsum("hqk,khd->qhd", s.softmax(-1), v).reshape(T, H * hd)
+        a = qblk(bf(a32), a32, da8o, 128)
         h = h + q8(a) @ lw.wo.dense().float().t()
         x = qin(norm(h, lw.mlp_norm), da8m)
         gu = (x @ lw.w_gate_up.dense().float().t()).view(T, -1, 2, 16)
-        act = bf(torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(T, -1)
+        act32 = (torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(T, -1)
+        act = qblk(bf(act32), act32, da8d, 32)
         h = h + q8(act) @ lw.w_down.dense().float().t()
     x = bf(norm(h, w.final_norm))
     logits = x @ w.lm_head.dense().float().t()

@@ -256,14 +256,20 @@ def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
             while (nbt // nb) * sk < target and sk < 8 and K // (128 * sk * 2) >= 4:
                 sk *= 2
         return nb, sk, 4, 4
-    if kind == "fp8a":  # W8A8 decode GEMM: its own sweep entries, else the fp8 (nb, splitk) at default knobs
+    if kind in ("fp8a", "fp4a"):  # W8A8 / W4A8 decode GEMM: its own sweep entries, else the 16-bit-activation
+        # kernel's (nb, splitk) at default knobs; 'silu8' = the e4m3 SiLU output (whole 32-column blocks: nb % 4 == 0)
         b = 1
         while b < M:
             b *= 2
-        e = _tuning_table().get(f"{N}x{K}:{epi}:b{b}:fp8a")
+        e = _tuning_table().get(f"{N}x{K}:{epi}:b{b}:{kind}")
         if e is not None:
             return e["nb"], e["splitk"], e["waves"], e["div"]
-        nb, sk, _, _ = pick_gemm_config(M, N, K, epi, xf=xf, kind="fp8")
+        if epi == "silu8":
+            nbt = N // 16
+            nb = 8 if (M <= 16 and nbt % 8 == 0 and nbt // 8 >= 256) else 4
+            assert nbt % nb == 0, f"e4m3 SiLU output needs N / 16 % 4 == 0 (N = {N})"
+            return nb, 1, 4, 4
+        nb, sk, _, _ = pick_gemm_config(M, N, K, epi, xf=xf, kind="fp8" if kind == "fp8a" else "mxfp4")
         return (2 if (M > 32 and nb > 2) else nb), sk, 4, 4
     if epi == "res":  # the residual epilogue runs the f32-slab main loop (split-K with a last-arriver finish):
         # its own measured entries (scripts/bench_res_epi.py --tune) first, else the f32 entries
@@ -580,20 +586,62 @@ FP8_A8_DECODE = os.environ.get("LSA_FP8_A8", "1") != "0"
 
 
 def to_xf8(x8: torch.Tensor, mt: int) -> torch.Tensor:
-    """uint8 [M, K] e4m3 bytes -> the flat xf8 layout X8[K/128][mt][64 lanes][32 B] of the W8A8 decode GEMM
-    (csrc/kernels/gemm_fp8a.hip; lane 16 g + r: row 16 t + r at k = 128 s + 16 g .. +15 and 128 s + 64 + 16 g ..
-    +15), rows >= M zero."""
+    """uint8 [M, K] e4m3 bytes -> the flat xf8 layout X8[K/128][mt][64 lanes][32 B] of the W8A8 / W4A8 decode GEMM
+    (csrc/kernels/gemm_fp8a.hip, common.h xf8_off; lane 16 g + r: row 16 t + r at k = 128 s + 32 g .. +31), rows >= M
+    zero."""
     M, K = x8.shape
     full = torch.zeros(16 * mt, K, dtype=torch.uint8, device=x8.device)
     full[:M] = x8
-    v = full.view(mt, 16, K // 128, 2, 4, 16)  # t, r, s, h, g, e
-    return v.permute(2, 0, 4, 1, 3, 5).contiguous().view(-1)  # s, t, g, r, h, e
+    v = full.view(mt, 16, K // 128, 4, 32)  # t, r, s, g, e
+    return v.permute(2, 0, 3, 1, 4).contiguous().view(-1)  # s, t, g, r, e
 
 
 def from_xf8(x8f: torch.Tensor, M: int, K: int) -> torch.Tensor:
     mt = xfrag_tiles(M)
-    v = x8f.view(-1)[: mt * 16 * K].view(K // 128, mt, 4, 16, 2, 16)  # s, t, g, r, h, e
-    return v.permute(1, 3, 0, 4, 2, 5).reshape(16 * mt, K)[:M]
+    v = x8f.view(-1)[: mt * 16 * K].view(K // 128, mt, 4, 16, 32)  # s, t, g, r, e
+    return v.permute(1, 3, 0, 2, 4).reshape(16 * mt, K)[:M]
+
+
+def to_xs8(s: torch.Tensor, mt: int) -> torch.Tensor:
+    """E8M0 bytes [M, K/32] (one per row and 32-column block) -> the block-scale layout S8[K/128][mt][64 lanes]
+    (common.h xs8_off), rows >= M = 127 (2^0)."""
+    M, nb32 = s.shape
+    full = torch.full((16 * mt, nb32), 127, dtype=torch.uint8, device=s.device)
+    full[:M] = s
+    return full.view(mt, 16, nb32 // 4, 4).permute(2, 0, 3, 1).contiguous().view(-1)  # s, t, g, r
+
+
+def from_xs8(s8: torch.Tensor, M: int, K: int) -> torch.Tensor:
+    mt = xfrag_tiles(M)
+    v = s8.view(-1)[: mt * 64 * (K // 128)].view(K // 128, mt, 4, 16)  # s, t, g, r
+    return v.permute(1, 3, 0, 2).reshape(16 * mt, K // 32)[:M]
+
+
+def e8m0_for_amax(amax: torch.Tensor) -> torch.Tensor:
+    """E8M0 exponent (int32) of the smallest power of two s with amax / s <= 448, clamped to [1, 253] -- the host
+    twin of common.h e8m0_for_amax (same f32 bit arithmetic)."""
+    b = (amax.float() * (1.0 / 448.0)).contiguous().view(torch.int32)
+    e = (b >> 23) + ((b & 0x7FFFFF) != 0).to(torch.int32)
+    return e.clamp(1, 253)
+
+
+def quantize_blocks_fp8(x: torch.Tensor, blk: int = 32):
+    """[M, K] -> (e4m3 bytes [M, K] uint8, E8M0 bytes [M, K/32] uint8): one power-of-two scale per row and block of
+    ``blk`` (32 | 128) consecutive columns (a 128-block's byte repeated for its four 32-blocks) -- what the decode
+    attention (blk 128: per head) and the W8A8 SiLU epilogue (blk 32) write for the next W8A8 / W4A8 GEMM."""
+    M, K = x.shape
+    xf = x.float().view(M, K // blk, blk)
+    e = e8m0_for_amax(xf.abs().amax(-1))
+    inv = torch.exp2(127.0 - e.float())
+    q = (xf * inv[..., None]).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8).view(M, K)
+    return q, e.to(torch.uint8).repeat_interleave(blk // 32, dim=1)
+
+
+def dequant_blocks_fp8(x8: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """(e4m3 bytes [M, K], E8M0 [M, K/32]) -> f32 [M, K]."""
+    M, K = x8.shape
+    v = x8.view(torch.float8_e4m3fn).float().view(M, K // 32, 32)
+    return (v * torch.exp2(s.float() - 127.0)[..., None]).view(M, K)
 
 
 def quantize_xf8(x: torch.Tensor, mt: Optional[int] = None, out: Optional[torch.Tensor] = None,
@@ -614,15 +662,51 @@ def quantize_xf8(x: torch.Tensor, mt: Optional[int] = None, out: Optional[torch.
     return out, sx
 
 
-def linear_a8(x8: torch.Tensor, sx: torch.Tensor, M: int, w: PackedWeight, epi: str = "f32",
+def quantize_xf8_blocks(x: torch.Tensor, blk: int = 32, mt: Optional[int] = None, out: Optional[torch.Tensor] = None,
+                        s8: Optional[torch.Tensor] = None):
+    """(x8 flat xf8 bytes, s8 flat block scales): block-scaled e4m3 activations (``quantize_blocks_fp8``) in the
+    layouts ``linear_a8(..., s8=)`` reads."""
+    M, K = x.shape
+    mt = mt or xfrag_tiles(M)
+    if out is None:
+        out = torch.zeros(mt * 16 * K, dtype=torch.uint8, device=x.device)
+    if s8 is None:
+        s8 = torch.full((mt * 64 * (K // 128),), 127, dtype=torch.uint8, device=x.device)
+    if not _gpu(x):
+        q, s = quantize_blocks_fp8(x, blk)
+        out.view(-1)[: mt * 16 * K].copy_(to_xf8(q, mt))
+        s8.view(-1)[: mt * 64 * (K // 128)].copy_(to_xs8(s, mt))
+        return out, s8
+    ext().quant_xf8_blocks(x.contiguous(), mt, blk, out, s8)
+    return out, s8
+
+
+def xf8_dequant(x8: torch.Tensor, M: int, K: int, sx: Optional[torch.Tensor] = None,
+                s8: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The f32 [M, K] activations a W8A8 / W4A8 GEMM multiplies: xf8 bytes x per-row sx x per-block E8M0."""
+    v = from_xf8(x8, M, K).view(torch.float8_e4m3fn).float()
+    if s8 is not None:
+        v = (v.view(M, K // 32, 32) * torch.exp2(from_xs8(s8, M, K).float() - 127.0)[..., None]).view(M, K)
+    if sx is not None:
+        v = v * sx[:M, None].float()
+    return v
+
+
+def linear_a8(x8: torch.Tensor, sx: Optional[torch.Tensor], M: int, w: PackedWeight, epi: str = "f32",
               out: Optional[torch.Tensor] = None, splitk: Optional[int] = None, nb: Optional[int] = None,
-              waves: Optional[int] = None, div: Optional[int] = None, rownorm=None, xfo: bool = True) -> torch.Tensor:
-    """W8A8 decode GEMM (M <= 64, fp8 weights): out = (x8 * sx) @ w^T with the activations in the xf8 layout
-    (``quantize_xf8`` / the fp8 output of ``add_rmsnorm``) on the fp8 MFMA.  epi 'f32' -> [splitk, M, N]
-    slabs; 'silu' -> bf16 [M, N/2] in the fragment-major layout (``xfo``) or row-major."""
+              waves: Optional[int] = None, div: Optional[int] = None, rownorm=None, xfo: bool = True,
+              s8: Optional[torch.Tensor] = None, out_s8: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """W8A8 / W4A8 decode GEMM (M <= 64; fp8 or MXFP4 weights): out = (x8 . scales) @ w^T with the activations in
+    the xf8 layout on the block-scaled fp8 MFMA.  Activation scales: per-row f32 ``sx`` (``quantize_xf8`` / the
+    fp8 output of ``add_rmsnorm``) and / or per-block E8M0 ``s8`` (``quantize_xf8_blocks`` / the e4m3 outputs of
+    ``attn_decode(out_s8=)`` and of this GEMM's SiLU epilogue).  epi 'f32' -> [splitk, M, N] slabs; 'silu' -> bf16
+    [M, N/2] in the fragment-major layout (``xfo``) or row-major, or -- ``out_s8`` given -- e4m3 xf8 bytes in
+    ``out`` with one E8M0 scale per (row, 32 columns) in ``out_s8`` (nb a multiple of 4)."""
     assert epi in ("f32", "silu")
+    assert sx is not None or s8 is not None
+    f8o = epi == "silu" and out_s8 is not None
     if not _gpu(x8):
-        xd = from_xf8(x8, M, w.K).view(torch.float8_e4m3fn).float() * sx[:M, None]
+        xd = xf8_dequant(x8, M, w.K, sx, s8)
         if rownorm is not None:
             xd = xd * torch.rsqrt(ss_float(rownorm[0][:M]) / w.K + rownorm[1])[:, None]
         y = xd @ w.dense().float().t()
@@ -634,14 +718,22 @@ def linear_a8(x8: torch.Tensor, sx: torch.Tensor, M: int, w: PackedWeight, epi: 
             return o
         F = w.N // 2
         y3 = y.view(M, F // 16, 2, 16)
-        act = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, F).to(torch.bfloat16)
+        act = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, F)
+        if f8o:
+            q, s = quantize_blocks_fp8(act, 32)
+            mt = xfrag_tiles(M)
+            out.view(-1)[: mt * 16 * F].copy_(to_xf8(q, mt))
+            out_s8.view(-1)[: mt * 64 * (F // 128)].copy_(to_xs8(s, mt))
+            return out
+        act = act.to(torch.bfloat16)
         act = to_xfrag(act) if xfo else act
         if out is None:
             return act
         out.view(-1)[: act.numel()].copy_(act.view(-1))
         return out
-    assert w.kind == "fp8", "linear_a8 runs fp8 weights"
-    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, w.K, epi, xf=True, kind="fp8a")
+    assert w.kind in ("fp8", "mxfp4"), "linear_a8 runs fp8 / MXFP4 weights"
+    kind = "fp8a" if w.kind == "fp8" else "fp4a"
+    nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, w.K, "silu8" if f8o else epi, xf=True, kind=kind)
     nb = nb0 if nb is None else nb
     splitk = sk0 if splitk is None else splitk
     waves = wv0 if waves is None else waves
@@ -652,8 +744,9 @@ def linear_a8(x8: torch.Tensor, sx: torch.Tensor, M: int, w: PackedWeight, epi: 
         else:
             out = torch.zeros((xfrag_tiles(M) * 16 if xfo else M) * (w.N // 2), device=x8.device, dtype=torch.bfloat16)
     kw = _epi_kw(rownorm, None, 0)
-    ext().fp8a_gemm(x8, sx, M, w.K, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, _fp8_depth(div),
-                    1 if xfo else 0, **kw)
+    fp4 = w.kind == "mxfp4"
+    ext().a8_gemm(x8, s8, sx, M, w.K, w.data, None if fp4 else w.scale, w.scale if fp4 else None, w.N, out, out_s8,
+                  EPI[epi], nb, splitk, waves, _fp8_depth(div), 2 if f8o else (1 if xfo else 0), **kw)
     return out
 
 
@@ -929,18 +1022,26 @@ def decode_workspace(B: int, H: int, Hkv: int, nsplit: int, device) -> tuple:
 
 
 def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None, xf=False,
-                qkv_parts=None, cos=None, sin=None, kv_scales=None, part_only=False):
+                qkv_parts=None, cos=None, sin=None, kv_scales=None, part_only=False, out_s8=None):
     """q [B,H,128] vs paged cache, context = pos + 1.  workspace = decode_workspace(...) for split-KV.
     xf=True: out is a flat buffer receiving the fragment-major layout of the [B, H*128] output.
     qkv_parts ([S, B, (H+2Hkv)*128] f32 split-K slabs of the QKV projection) + cos/sin: RoPE and the
     KV-cache append of the new token are fused in (``q`` is then only a [B, H, 128] scratch buffer).
     kv_scales = (ks, vs): fp8 cache (see ``KV_FP8``).
     part_only: every split leaves its (o, m, l) partial in the workspace and nothing is combined (the latency path's o
-    projection merges them, ``lat_linear(src='part')``); on the CPU the finished rows still land in ``out``."""
+    projection merges them, ``lat_linear(src='part')``); on the CPU the finished rows still land in ``out``.
+    out_s8 (xf only): ``out`` is a uint8 buffer receiving the output as e4m3 in the xf8 layout with one E8M0 scale
+    per (row, head) in ``out_s8`` -- the input of a W8A8 / W4A8 o projection (``linear_a8(s8=)``)."""
     B = pos.shape[0]
+    assert out_s8 is None or xf, "the e4m3 attention output lives in the xf8 layout"
     if not _gpu(pos):
         if qkv_parts is not None:
             ref.rope_append(qkv_parts, pos, None, block_tables, cos, sin, q, kc, vc, H, Hkv, kv_scales)
+        if out_s8 is not None:
+            tmp = torch.empty(B, H, q.shape[-1], dtype=torch.bfloat16, device=q.device)
+            ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, tmp, kv_scales)
+            quantize_xf8_blocks(tmp.view(B, -1), 128, xfrag_tiles(B), out, out_s8)
+            return out
         if not xf:
             return ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, kv_scales)
         tmp = torch.empty(B, H, q.shape[-1], dtype=torch.bfloat16, device=q.device)
@@ -956,7 +1057,8 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     opart, mlpart, counters = workspace
     ks, vs = kv_scales if kv_scales is not None else (None, None)
     ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart, counters,
-                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs, 1 if part_only else 0)
+                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs, 1 if part_only else 0,
+                      out_s8)
     return out
 
 

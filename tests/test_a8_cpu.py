@@ -1,0 +1,143 @@
+"""CPU semantics of the W8A8 / W4A8 decode activations (csrc/kernels/gemm_fp8a.hip, common.h xf8_off / xs8_off /
+e8m0_for_amax): the xf8 and block-scale layouts, the E8M0 block quantisation the decode attention and the SiLU
+epilogue write, ``linear_a8``'s host path, and the oracle's emulation of the block-scaled o / down inputs."""
+import math
+
+import pytest
+import torch
+
+from llm_based_apache_spark_optimization_amd import ops
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 20, 33])
+def test_xf8_layout_roundtrip_and_lane_blocks(M):
+    K = 384
+    x8 = torch.randint(0, 255, (M, K), dtype=torch.uint8)
+    mt = ops.xfrag_tiles(M)
+    f = ops.to_xf8(x8, mt)
+    assert f.numel() == mt * 16 * K
+    assert torch.equal(ops.from_xf8(f, M, K), x8)
+    # lane (g, r) of k-step s, tile t holds row 16 t + r, k = 128 s + 32 g .. +31 as 32 contiguous bytes
+    v = f.view(K // 128, mt, 64, 32)
+    for (m, k) in [(0, 0), (M - 1, K - 1), (M // 2, 200)]:
+        s, t, g, r = k // 128, m // 16, (k % 128) // 32, m % 16
+        assert v[s, t, 16 * g + r, k % 32] == x8[m, k]
+    s8 = torch.randint(1, 254, (M, K // 32), dtype=torch.uint8)
+    sf = ops.to_xs8(s8, mt)
+    assert torch.equal(ops.from_xs8(sf, M, K), s8)
+    sv = sf.view(K // 128, mt, 64)
+    m, k = M - 1, 300
+    assert sv[k // 128, m // 16, 16 * ((k % 128) // 32) + m % 16] == s8[m, k // 32]
+
+
+def test_e8m0_for_amax():
+    amax = torch.tensor([0.0, 448.0, 448.5, 1.0, 224.0, 1e-30, 3e38, 896.0])
+    e = ops.e8m0_for_amax(amax)
+    s = torch.exp2(e.float() - 127)
+    assert e[0] == 1 and e[1] == 127 and e[2] == 128 and e[7] == 128
+    ok = amax > 0
+    # the smallest power of two with amax / s <= 448 (inside the clamp range)
+    assert (amax[ok][:-2] / s[ok][:-2] <= 448).all() and (amax[ok][:-2] / s[ok][:-2] > 224).all()
+    assert e.max() <= 253 and e.min() >= 1
+
+
+@pytest.mark.parametrize("blk", [32, 128])
+def test_quantize_blocks_fp8(blk):
+    g = torch.Generator().manual_seed(blk)
+    M, K = 6, 512
+    mag = torch.exp2(torch.randint(-10, 8, (M, K // 32), generator=g).float()).repeat_interleave(32, 1)
+    x = torch.randn(M, K, generator=g) * mag
+    q, s = ops.quantize_blocks_fp8(x, blk)
+    assert q.dtype == torch.uint8 and s.shape == (M, K // 32)
+    if blk == 128:  # one exponent per 128 columns, repeated for its four 32-blocks
+        assert (s.view(M, K // 128, 4) == s.view(M, K // 128, 4)[..., :1]).all()
+    y = ops.dequant_blocks_fp8(q, s)
+    # e4m3 (3 mantissa bits) relative to each block's amax: at most half an ulp of the top binade
+    err = (y - x).abs().view(M, K // blk, blk).amax(-1)
+    amax = x.abs().view(M, K // blk, blk).amax(-1)
+    assert (err <= amax * 2 ** -4 + 1e-38).all()
+    # a block never saturates: its amax lands in [224, 448] x 2^(e - 127)
+    top = y.abs().view(M, K // blk, blk).amax(-1) / torch.exp2(s.view(M, K // 32)[:, :: blk // 32].float() - 127)
+    assert ((top >= 224) & (top <= 448)).all()
+
+
+@pytest.mark.parametrize("epi", ["f32", "silu", "silu8"])
+def test_linear_a8_host_path(epi):
+    """linear_a8 on the CPU = (xf8 bytes x per-row sx x per-block E8M0) @ the dequantised weights."""
+    torch.manual_seed(0)
+    M, N, K = 5, 512, 256
+    x = torch.randn(M, K).to(torch.bfloat16)
+    w = (torch.randn(N, K) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    x8, s8 = ops.quantize_xf8_blocks(x, 32)
+    sx = torch.full((M,), 2.0)
+    xd = ops.xf8_dequant(x8, M, K, sx, s8)
+    assert torch.allclose(xd, 2 * x.float(), rtol=2 ** -4, atol=1e-6)
+    yr = xd @ w.float().t()
+    if epi == "f32":
+        y = ops.linear_a8(x8, sx, M, pw, "f32", s8=s8)
+        assert torch.allclose(y[0], yr, rtol=1e-5, atol=1e-5)
+        return
+    y3 = yr.view(M, N // 32, 2, 16)
+    want = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, N // 2)
+    if epi == "silu":
+        got = ops.from_xfrag(ops.linear_a8(x8, sx, M, pw, "silu", s8=s8), M, N // 2)
+        assert torch.allclose(got.float(), want, rtol=1e-2, atol=1e-3)
+        return
+    mt = ops.xfrag_tiles(M)
+    o8 = torch.zeros(mt * 16 * N // 2, dtype=torch.uint8)
+    os8 = torch.zeros(mt * 64 * (N // 2 // 128), dtype=torch.uint8)
+    ops.linear_a8(x8, sx, M, pw, "silu", out=o8, out_s8=os8, s8=s8)
+    q, s = ops.quantize_blocks_fp8(want, 32)
+    assert torch.equal(ops.from_xf8(o8, M, N // 2), q) and torch.equal(ops.from_xs8(os8, M, N // 2), s)
+
+
+def test_attn_decode_e4m3_output_host_path():
+    """attn_decode(out_s8=) on the CPU: the bf16 attention rows, block-quantised per (row, head)."""
+    from llm_based_apache_spark_optimization_amd.ops import reference as ref
+
+    torch.manual_seed(1)
+    B, H, Hkv, D = 3, 4, 2, 128
+    kc = torch.randn(4, Hkv, 64, D).to(torch.bfloat16)
+    vc = torch.randn(4, Hkv, 64, D).to(torch.bfloat16)
+    bt = torch.tensor([[1, 2], [3, 0], [2, 1]], dtype=torch.int32)
+    pos = torch.tensor([70, 10, 100], dtype=torch.int32)
+    q = torch.randn(B, H, D).to(torch.bfloat16)
+    want = torch.empty(B, H, D, dtype=torch.bfloat16)
+    ref.attn_decode(q, kc, vc, bt, pos, H, Hkv, 0.1, want)
+    mt = ops.xfrag_tiles(B)
+    x8 = torch.zeros(mt * 16 * H * D, dtype=torch.uint8)
+    s8 = torch.zeros(mt * 64 * H, dtype=torch.uint8)
+    ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, 0.1, x8, xf=True, out_s8=s8)
+    got = ops.xf8_dequant(x8, B, H * D, None, s8)
+    assert torch.allclose(got, want.view(B, -1).float(), rtol=2 ** -4, atol=1e-6)
+
+
+def test_oracle_block_scaled_decode_inputs():
+    """reference_forward(decode_a8={...}) rounds the o / down inputs of the decode rows (only) to block-scaled e4m3;
+    with every flag off it is the bf16 forward."""
+    from llm_based_apache_spark_optimization_amd.models import get_spec
+    from llm_based_apache_spark_optimization_amd.models.llama import init_random, reference_forward
+
+    w = init_random(get_spec("tiny-llama3"), "cpu", seed=3)
+    ids = list(range(5, 17))
+    base = reference_forward(w, ids)
+    off = reference_forward(w, ids, decode_a8=dict(qkv=False, gate_up=False, o=False, down=False))
+    assert torch.equal(base, off)
+    # dense (CPU) weights: the dict flags apply to fp8 / MXFP4 weights only
+    on = reference_forward(w, ids, act_quant_rows=4, decode_a8=dict(qkv=True, gate_up=True, o=True, down=True))
+    assert torch.equal(on, base)
+    # fp8-packed weights (host quantisation): each flag moves only the decode rows (past act_quant_rows), by e4m3
+    # rounding-level amounts
+    for lw in w.layers:
+        for name in ("wqkv", "wo", "w_gate_up", "w_down"):
+            p = getattr(lw, name)
+            setattr(lw, name, ops.PackedWeight(p.N, p.K, "fp8", *ops.quantize_fp8(p.dense())))
+    f8 = reference_forward(w, ids, act_quant_rows=len(ids))  # every row a prompt row: W8A8 prefill emulation
+    prev = reference_forward(w, ids, act_quant_rows=4)
+    for flag in ("o", "down"):
+        got = reference_forward(w, ids, act_quant_rows=4, decode_a8={flag: True})
+        assert torch.equal(got[:4], prev[:4]), flag
+        d = (got[4:] - prev[4:]).abs().max()
+        assert 0 < d < 0.05 * prev[4:].abs().max(), (flag, float(d))
+    assert f8.shape == prev.shape

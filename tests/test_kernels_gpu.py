@@ -393,6 +393,21 @@ def test_attn_decode(gpu, HH, lens):
         ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, xf, plan=plan, xf=True)
         ro = out if plan is None else out3
         assert torch.equal(ops.from_xfrag(xf, B, H * D), ro.view(B, -1))
+    # e4m3 output (the W8A8 / W4A8 o projection's input): one E8M0 scale per (row, head), vs the fp32 oracle
+    for plan in (None, (bt.shape[1], 1)):
+        mt = ops.xfrag_tiles(B)
+        x8 = torch.zeros(mt * 16 * H * D, device=gpu, dtype=torch.uint8)
+        s8 = torch.full((mt * 64 * H,), 127, device=gpu, dtype=torch.uint8)
+        ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, x8, plan=plan, xf=True, out_s8=s8)
+        got = ops.xf8_dequant(x8, B, H * D, None, s8)
+        want = out2.view(B, -1).float()
+        assert _rel(got, want) < 4e-2, plan
+        # the scale is the head's own: its amax lands in the top binade of e4m3 ([224, 448])
+        se = ops.from_xs8(s8, B, H * D).view(B, H, 4).cpu().int()
+        assert (se == se[:, :, :1]).all()
+        amax = want.view(B, H, D).abs().amax(-1).cpu()
+        ratio = amax / torch.exp2(se[:, :, 0].float() - 127)
+        assert ((ratio > 200) & (ratio <= 448)).all(), ratio
 
 
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
@@ -829,6 +844,72 @@ def test_fp8a_gemm(gpu, M, epi, nb):
             y = ops.linear_a8(x8, sx, M, pw, "silu", nb=nb, xfo=xfo)
             got = ops.from_xfrag(y, M, N // 2) if xfo else y.view(M, N // 2)
             assert _rel(got, want) < 1e-2, xfo
+
+
+def _blocky(M, K, gen_dev, seed):
+    """[M, K] bf16 whose 32-column blocks span 2^-8 .. 2^6 in magnitude (exercises per-block scales)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    mag = torch.exp2(torch.randint(-8, 7, (M, K // 32), generator=g).float()).repeat_interleave(32, 1)
+    return (torch.randn(M, K, generator=g) * mag).to(torch.bfloat16).to(gen_dev)
+
+
+@pytest.mark.parametrize("M", [1, 9, 20, 32, 48, 64])
+def test_quant_xf8_blocks(gpu, M):
+    """GPU block-scaled e4m3 quantisation (E8M0 per 32 / 128 columns) vs the CPU definition."""
+    K = 1024
+    x = _blocky(M, K, gpu, M)
+    for blk in (32, 128):
+        x8, s8 = ops.quantize_xf8_blocks(x, blk)
+        c8, cs8 = ops.quantize_xf8_blocks(x.cpu(), blk)
+        assert torch.equal(ops.from_xs8(s8, M, K).cpu(), ops.from_xs8(cs8, M, K)), blk
+        a = ops.xf8_dequant(x8, M, K, None, s8).cpu()
+        b = ops.xf8_dequant(c8, M, K, None, cs8)
+        assert torch.allclose(a, b, rtol=0.13, atol=0), blk
+        assert _rel(a, x.float().cpu()) < 4e-2
+
+
+@pytest.mark.parametrize("M", [1, 9, 20, 32, 48, 64])
+@pytest.mark.parametrize("wkind", ["fp8", "mxfp4"])
+def test_a8_gemm_block_scales(gpu, M, wkind):
+    """W8A8 / W4A8 decode GEMM (ops.linear_a8) with per-block E8M0 activation scales (the MFMA's B scale operand) and,
+    for MXFP4, the weights' own E8M0 block scales (A operand, e2m1 elements straight into the MFMA) vs the fp32
+    product of the dequantised operands; f32 split-K slabs, the bf16 SiLU epilogue, and the e4m3 SiLU epilogue
+    (E8M0 per (row, 32 columns): the down projection's input) vs the CPU quantisation of the fp32 product."""
+    N, K = 2048, 1536
+    torch.manual_seed(M)
+    x = _blocky(M, K, gpu, 7 * M)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
+    x8, s8 = ops.quantize_xf8_blocks(x, 32)
+    xd = ops.xf8_dequant(x8, M, K, None, s8)
+    sx = torch.full((M,), 0.5, device=gpu)  # a per-row scale on top of the blocks multiplies in
+    for epi in ("f32", "silu"):
+        pw = ops.PackedWeight.from_dense(w if epi == "f32" else ops.interleave_gate_up(w[: N // 2], w[N // 2:]), wkind)
+        wd = (ops.dequantize_fp8(pw.data, pw.scale, N, K) if wkind == "fp8"
+              else ops.dequantize_mxfp4(pw.data, pw.scale, N, K)).float()
+        yr = xd @ wd.t()
+        if epi == "f32":
+            for sk in (1, 3):
+                y = ops.linear_a8(x8, None, M, pw, "f32", splitk=sk, s8=s8)
+                assert _rel(y.sum(0), yr) < 1e-4, sk
+            y = ops.linear_a8(x8, sx, M, pw, "f32", s8=s8)
+            assert _rel(y.sum(0), 0.5 * yr) < 1e-4
+            continue
+        y3 = yr.view(M, N // 32, 2, 16)
+        want = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, N // 2)
+        got = ops.from_xfrag(ops.linear_a8(x8, None, M, pw, "silu", s8=s8), M, N // 2)
+        assert _rel(got, want) < 1e-2
+        mt = ops.xfrag_tiles(M)
+        for nb in (4, 8):
+            if nb == 8 and M > 32:
+                continue
+            o8 = torch.zeros(mt * 16 * N // 2, device=gpu, dtype=torch.uint8)
+            os8 = torch.full((mt * 64 * (N // 2 // 128),), 0, device=gpu, dtype=torch.uint8)
+            ops.linear_a8(x8, None, M, pw, "silu", out=o8, out_s8=os8, s8=s8, nb=nb)
+            got8 = ops.xf8_dequant(o8, M, N // 2, None, os8)
+            assert _rel(got8, want) < 4e-2, nb
+            _, ws = ops.quantize_blocks_fp8(want.cpu(), 32)
+            # the block exponents agree except where f32 accumulation order moves an amax across a binade
+            assert (ops.from_xs8(os8, M, N // 2).cpu() != ws).float().mean() < 0.02, nb
 
 
 @pytest.mark.parametrize("M", [20, 32, 64])
