@@ -209,8 +209,13 @@ def check_recorded(eng, prompts, toks, elog, n_steps: int, check_rows: Sequence[
 # ---- fault injection (tests/test_numerics_gpu.py, scripts/numerics_calibrate.py): the check must catch these
 @contextlib.contextmanager
 def scale_fault(eng, layer: int = 1, factor: float = 1.25):
-    """One layer's down-projection dequantisation scale (fp8) / weights (bf16) x ``factor`` in the ENGINE."""
+    """One layer's down-projection dequantisation scale (fp8) / weights (bf16) x ``factor`` in the ENGINE; MXFP4: a
+    wrong E8M0 block scale instead (``e8m0_fault``: every 8th block of that layer's down projection one binade up)."""
     lw = eng.runner.w.layers[layer].w_down
+    if lw.kind == "mxfp4":
+        with e8m0_fault(eng, layer):
+            yield
+        return
     saved = lw.scale.clone() if lw.scale is not None else lw.data.clone()
     if lw.scale is not None:
         lw.scale.mul_(factor)
@@ -220,6 +225,21 @@ def scale_fault(eng, layer: int = 1, factor: float = 1.25):
         yield
     finally:
         (lw.scale if lw.scale is not None else lw.data).copy_(saved)
+
+
+@contextlib.contextmanager
+def e8m0_fault(eng, layer: int = 1, every: int = 8, delta: int = 1):
+    """MXFP4: every ``every``-th E8M0 block-scale byte of one layer's down projection + ``delta`` in the ENGINE (those
+    32-weight blocks scaled by 2^delta) -- the wrong-block-scale bug class of the W4A8 / W4A16 kernels."""
+    lw = eng.runner.w.layers[layer].w_down
+    assert lw.kind == "mxfp4", lw.kind
+    saved = lw.scale.clone()
+    v = lw.scale.view(-1)
+    v[::every] = (v[::every].int() + delta).clamp(0, 254).to(v.dtype)
+    try:
+        yield
+    finally:
+        lw.scale.copy_(saved)
 
 
 @contextlib.contextmanager

@@ -219,12 +219,11 @@ def test_decode_tokens_kv_fp8_prod_shapes(gpu, model, dtype, B):
     res = eng.generate(prompts, SamplingParams(max_tokens=12, ignore_eos=True))
     rows = sum(len(q) for q in prompts)
     bk = r.bucket(B)
-    xfu = r.a8 and r.use_xfrag(bk) and not (r.fused_norm and bk <= r.fused_norm_max_batch)
+    plan = dict(zip(("qkv", "gate_up", "o", "down"), r.a8_plan(bk)))
     worst = 0.0
     for p, out in zip(prompts, res[: min(B, 6)]):
         lg = reference_forward(r.w, p + out.token_ids[:-1], act_quant_rows=len(p) if rows > 64 else 0,
-                               decode_a8=xfu and bk > r.a8_min_batch, decode_a8_mlp=xfu and bk > r.a8_mlp_min_batch,
-                               kv_fp8=True)[len(p) - 1:]
+                               decode_a8=plan, kv_fp8=True)[len(p) - 1:]
         chosen = lg.gather(1, torch.tensor(out.token_ids, device=lg.device).view(-1, 1)).squeeze(1)
         worst = max(worst, ((lg.max(1).values - chosen) / lg.std(1)).max().item())
     assert worst < 0.15, (model, dtype, B, worst)

@@ -5,7 +5,9 @@ Llama-3.2-3B-shaped one (GQA 3:1, tied lm_head: checked through the final hidden
 eval/numerics.py TIED_THRESHOLDS) decode a batch for 64 steps; the teacher-forced comparison against the fp32 oracle passes at HEAD and fails when a
 fault is injected into the ENGINE only (the oracle keeps the true weights / cache semantics):
 
-* one layer's down-projection weight scale x1.25 (fp8) / weights x1.25 (bf16): a wrong dequantisation scale;
+* one layer's down-projection weight scale x1.25 (fp8) / weights x1.25 (bf16) / every 8th E8M0 block scale one
+  binade up (MXFP4, decoded W4A8: e2m1 weights + E8M0 scales straight into the block-scaled MFMA): a wrong
+  dequantisation scale;
 * a swapped token pair in the K cache layout (keys of positions 2k and 2k + 1 exchanged in the first block of
   every layer after prefill, values left in place): a KV layout bug.
 """
@@ -41,13 +43,15 @@ def _check(eng, B, weights=None):
     return nm.teacher_forced_check(eng, _prompts(B), 64, check_rows=(0, B - 1) if B > 1 else (0,), weights=weights)
 
 
-@pytest.mark.parametrize("dtype,kv", [("bf16", "bf16"), ("fp8", "bf16"), ("fp8", "fp8")])
+@pytest.mark.parametrize("dtype,kv", [("bf16", "bf16"), ("fp8", "bf16"), ("fp8", "fp8"), ("mxfp4", "bf16")])
 @pytest.mark.parametrize("model,B", [("7b", 4), ("7b", 32), ("3b", 1), ("3b", 4)])
 def test_numerics_check_passes_and_catches_faults(gpu, dtype, kv, model, B):
     spec = SPEC if model == "7b" else SPEC3B
     eng = _engine(gpu, dtype, kv, spec)
     good = _check(eng, B)
     assert good["ok"] and good["tokens_checked"] >= 64, good
+    if dtype == "mxfp4":  # every projection runs W4A8 at every decode bucket
+        assert eng.runner.a8_plan(B) == (True, True, True, True) and good["class"] == "w8a8", good
     if spec is SPEC3B:  # the tied head's own KL is degenerate (~0): the probe statistic must not be
         assert good["tied_head"] and good["probe_kl"] > 0, good
 

@@ -72,12 +72,10 @@ def test_decode_tokens_prod_shapes(gpu, model, dtype, B):
     worst = 0.0
     for p, out in zip(prompts, res[: min(B, 6)] if B > 1 else res):
         rows = sum(len(q) for q in prompts)  # one packed prefill: W8A8 for fp8 weights when > 64 rows
-        # fragment-major decode buckets of an fp8 model run qkv / gate_up W8A8 (ops.linear_a8)
+        # decode buckets of an fp8 model run some projections W8A8 (ops.linear_a8, ModelRunner.a8_plan)
         r, bk = eng.runner, eng.runner.bucket(B)
-        xfu = r.a8 and r.use_xfrag(bk) and not (r.fused_norm and bk <= r.fused_norm_max_batch)
         lg = reference_forward(r.w, p + out.token_ids[:-1], act_quant_rows=len(p) if rows > 64 else 0,
-                               decode_a8=xfu and bk > r.a8_min_batch,
-                               decode_a8_mlp=xfu and bk > r.a8_mlp_min_batch)[len(p) - 1:]
+                               decode_a8=dict(zip(("qkv", "gate_up", "o", "down"), r.a8_plan(bk))))[len(p) - 1:]
         chosen = lg.gather(1, torch.tensor(out.token_ids, device=lg.device).view(-1, 1)).squeeze(1)
         top = lg.max(1).values
         spread = lg.std(1)
