@@ -20,15 +20,14 @@ int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* 
              hipStream_t stream);
 int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
                     const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
-                    int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, void* x8, float* sx8, int x8c, hipStream_t s);
+                    int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, void* x8, float* sx8, hipStream_t s);
 int lsa_res_add_ss(float* h, const float* parts, int nparts, long part_stride, void* xn, int rows, int D, int xf_mt,
                    long long* ss_out, hipStream_t s);
 int lsa_a8_gemm(const void* X8, const void* s8, const float* sx, int M, int K, const void* Wq, const float* wscale,
                 const void* Sw, int wk, int N, void* out, void* out_s8, int epi, int nb, int splitk, int waves, int depth,
                 int xfo, const LsaEpi* ep, hipStream_t stream);
-int lsa_quant_xf8(const void* x, int ldx, int M, int K, int MT, void* x8, float* sx, int x8c, hipStream_t s);
-int lsa_quant_xf8_blocks(const void* x, int ldx, int M, int K, int MT, int blk, void* x8, void* s8, int x8c,
-                         hipStream_t s);
+int lsa_quant_xf8(const void* x, int ldx, int M, int K, int MT, void* x8, float* sx, hipStream_t s);
+int lsa_quant_xf8_blocks(const void* x, int ldx, int M, int K, int MT, int blk, void* x8, void* s8, hipStream_t s);
 int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
                 int waves, int div, int xlds, const LsaEpi* ep, hipStream_t stream);
 int lsa_fp8_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
@@ -42,7 +41,7 @@ int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* bl
                     void* out, float* opart, float* mlpart, int* counters, int xf_mt, const float* qkv_parts, int nparts,
                     long part_stride,
                     const float* cos_t, const float* sin_t, const float* ks, const float* vs, int part_only,
-                    void* out_s8, int x8c, hipStream_t s);
+                    void* out_s8, hipStream_t s);
 int lsa_kv8_dequant(const void* kc, const void* vc, const float* ks, const float* vs, const int* block_tables,
                     int max_blocks, const int* ctx_lens, int nseq, int Hkv, int mb, void* ko, void* vo, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
@@ -305,25 +304,24 @@ void a8_gemm(const at::Tensor& x8, const c10::optional<at::Tensor>& s8, const c1
         "a8_gemm");
 }
 
-void quant_xf8_blocks(const at::Tensor& x, int64_t mt, int64_t blk, at::Tensor& x8, at::Tensor& s8, int64_t x8c) {
+void quant_xf8_blocks(const at::Tensor& x, int64_t mt, int64_t blk, at::Tensor& x8, at::Tensor& s8) {
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
   const int M = x.size(0), K = x.size(1);
   TORCH_CHECK(on_dev(x8) && x8.element_size() == 1 && x8.numel() >= mt * 16 * K, "x8 too small");
   TORCH_CHECK(on_dev(s8) && s8.element_size() == 1 && s8.numel() >= mt * 64 * (K / 128), "s8 too small");
   check(lsa_quant_xf8_blocks(x.data_ptr(), x.stride(0), M, K, (int)mt, (int)blk, x8.data_ptr(), s8.data_ptr(),
-                             (int)x8c, cur_stream()),
+                             cur_stream()),
         "quant_xf8_blocks");
 }
 
-void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx, int64_t x8c) {
+void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) {
   need(x, at::kBFloat16, "x");
   need(sx, at::kFloat, "sx");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
   const int M = x.size(0), K = x.size(1);
   TORCH_CHECK(on_dev(x8) && x8.element_size() == 1 && x8.numel() >= mt * 16 * K && sx.numel() >= M, "x8 / sx too small");
-  check(lsa_quant_xf8(x.data_ptr(), x.stride(0), M, K, (int)mt, x8.data_ptr(), sx.data_ptr<float>(), (int)x8c,
-                      cur_stream()),
+  check(lsa_quant_xf8(x.data_ptr(), x.stride(0), M, K, (int)mt, x8.data_ptr(), sx.data_ptr<float>(), cur_stream()),
         "quant_xf8");
 }
 
@@ -439,7 +437,7 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
                  const c10::optional<at::Tensor>& row_idx, bool write_h, const at::Tensor& w, double eps,
                  const c10::optional<at::Tensor>& xn, int64_t rows, int64_t xf_mt, const c10::optional<at::Tensor>& ss_out,
                  int64_t ss_ld, int64_t ss_nzero, const c10::optional<at::Tensor>& x8,
-                 const c10::optional<at::Tensor>& sx8, int64_t x8c = 0) {
+                 const c10::optional<at::Tensor>& sx8) {
   need(h, at::kFloat, "h");
   need(w, at::kBFloat16, "w");
   if (xn.has_value()) need(*xn, at::kBFloat16, "xn");
@@ -457,7 +455,7 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
                         w.data_ptr(), (float)eps, xn.has_value() ? xn->data_ptr() : nullptr, rows, D, xf_mt,
                         ss_out.has_value() ? reinterpret_cast<long long*>(ss_out->data_ptr<int64_t>()) : nullptr, (int)ss_ld,
                         (int)ss_nzero, x8.has_value() ? x8->data_ptr() : nullptr,
-                        sx8.has_value() ? sx8->data_ptr<float>() : nullptr, (int)x8c, cur_stream()),
+                        sx8.has_value() ? sx8->data_ptr<float>() : nullptr, cur_stream()),
         "add_rmsnorm");
 }
 
@@ -530,7 +528,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                  const c10::optional<at::Tensor>& qkv_parts, const c10::optional<at::Tensor>& cos_t,
                  const c10::optional<at::Tensor>& sin_t, int64_t unsplit_max, const c10::optional<at::Tensor>& ks,
                  const c10::optional<at::Tensor>& vs, int64_t part_only = 0,
-                 const c10::optional<at::Tensor>& out_s8 = c10::nullopt, int64_t x8c = 0) {
+                 const c10::optional<at::Tensor>& out_s8 = c10::nullopt) {
   need(q, at::kBFloat16, "q");
   check_cache(kc, vc, ks, vs);
   need(pos, at::kInt, "pos");
@@ -573,7 +571,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                         ptr<const float>(qkv_parts), qkv_parts.has_value() ? qkv_parts->size(0) : 0,
                         qkv_parts.has_value() ? qkv_parts->stride(0) : 0, ptr<const float>(cos_t),
                         ptr<const float>(sin_t), ptr<const float>(ks), ptr<const float>(vs), (int)part_only,
-                        out_s8.has_value() ? out_s8->data_ptr() : nullptr, (int)x8c, cur_stream()),
+                        out_s8.has_value() ? out_s8->data_ptr() : nullptr, cur_stream()),
         "attn_decode");
 }
 
@@ -940,14 +938,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
         py::arg("ids"), py::arg("emb"), py::arg("row_idx"), py::arg("write_h"), py::arg("w"), py::arg("eps"),
         py::arg("xn"), py::arg("rows"), py::arg("xf_mt") = 0, py::arg("ss_out") = py::none(), py::arg("ss_ld") = 0,
-        py::arg("ss_nzero") = 0, py::arg("x8") = py::none(), py::arg("sx8") = py::none(), py::arg("x8c") = 0);
+        py::arg("ss_nzero") = 0, py::arg("x8") = py::none(), py::arg("sx8") = py::none());
   m.def("a8_gemm", &a8_gemm, py::arg("x8"), py::arg("s8"), py::arg("sx"), py::arg("M"), py::arg("K"), py::arg("wq"),
         py::arg("wscale"), py::arg("wsc8"), py::arg("N"), py::arg("out"), py::arg("out_s8"), py::arg("epi"), py::arg("nb"),
         py::arg("splitk"), py::arg("waves"), py::arg("depth"), py::arg("xfo"), py::arg("rowss") = py::none(),
         py::arg("eps") = 1e-5);
-  m.def("quant_xf8_blocks", &quant_xf8_blocks, py::arg("x"), py::arg("mt"), py::arg("blk"), py::arg("x8"), py::arg("s8"),
-        py::arg("x8c"));
-  m.def("quant_xf8", &quant_xf8, py::arg("x"), py::arg("mt"), py::arg("x8"), py::arg("sx"), py::arg("x8c"));
+  m.def("quant_xf8_blocks", &quant_xf8_blocks, py::arg("x"), py::arg("mt"), py::arg("blk"), py::arg("x8"), py::arg("s8"));
+  m.def("quant_xf8", &quant_xf8, py::arg("x"), py::arg("mt"), py::arg("x8"), py::arg("sx"));
   m.def("attn_set_stamps", &attn_set_stamps, py::arg("stamps") = py::none());
   m.def("rope_append", &rope_append, py::arg("qkv"), py::arg("pos"), py::arg("tok_seq"), py::arg("block_tables"),
         py::arg("cos"), py::arg("sin"), py::arg("q_out"), py::arg("kc"), py::arg("vc"), py::arg("H"), py::arg("Hkv"),
@@ -960,7 +957,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("qkv_parts") = py::none(),
         py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4,
         py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("part_only") = 0,
-        py::arg("out_s8") = py::none(), py::arg("x8c") = 0);
+        py::arg("out_s8") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
         py::arg("out"), py::arg("rows32") = 0);

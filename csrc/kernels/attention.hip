@@ -108,13 +108,12 @@ struct RopeArgs {
 // 22.1 -> 18.6 us, decode step 3.60 -> 3.50 ms (profiles/attn_decode_sb_ab_mi355x.jsonl).  Small grids keep the
 // two-set pipeline (7B b1: 6.8 vs 7.1 us).
 // Dims d0 .. d0 + 3 of head h of row b: bf16 (row-major [B, H, 128], or fragment-major with xf_mt row tiles), or
-// -- s8 set -- e4m3 in the xf8 layout (x8c: consecutive-k, common.h xf8_off) with one E8M0 scale per (row, head)
-// into s8 (common.h xs8_off; the byte of
+// -- s8 set -- e4m3 in the xf8 layout with one E8M0 scale per (row, head) into s8 (common.h xs8_off; the byte of
 // each of the head's four 32-dim lane blocks): the W8A8 / W4A8 o projection's input.  The 32 threads finishing a
 // head are one aligned half-wave (e = tid + k * NT, NT a multiple of 64), so the head's amax is 5 xor shuffles;
 // every thread of the workgroup's loop iteration must call this (no early exits around it).
-__device__ __forceinline__ void attn_store4(uint16_t* out, uint8_t* s8, int x8c, int xf_mt, int b, int H, int h, int d0,
-                                            float o0, float o1, float o2, float o3) {
+__device__ __forceinline__ void attn_store4(uint16_t* out, uint8_t* s8, int xf_mt, int b, int H, int h, int d0, float o0,
+                                            float o1, float o2, float o3) {
   if (s8 == nullptr) {
     uint2 pk;
     pk.x = pack2bf(o0, o1);
@@ -127,8 +126,7 @@ __device__ __forceinline__ void attn_store4(uint16_t* out, uint8_t* s8, int x8c,
   for (int off = 1; off < 32; off <<= 1) a = fmaxf(a, __shfl_xor(a, off, 64));
   const int e = e8m0_for_amax(a);
   const int k = h * 128 + d0;
-  *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out) + xf8_off(b, k, xf_mt, x8c != 0)) =
-      pack4_fp8(o0, o1, o2, o3, e8m0_inv(e));
+  *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out) + xf8_off(b, k, xf_mt)) = pack4_fp8(o0, o1, o2, o3, e8m0_inv(e));
   if ((d0 & 31) == 0) s8[xs8_off(b, k, xf_mt)] = (uint8_t)e;
 }
 
@@ -142,7 +140,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
                                                           int chunk_blocks, int nsplit, int unsplit_max,
                                                           uint16_t* __restrict__ out, float* __restrict__ opart, float* __restrict__ mlpart,
                                                           int* __restrict__ counters, int xf_mt, RopeArgs ra,
-                                                          int part_only, uint8_t* __restrict__ s8, int x8c) {
+                                                          int part_only, uint8_t* __restrict__ s8) {
   constexpr int D = 128;
   constexpr int NT = 64 * WV;      // threads
   constexpr int NLG = 4 * WV;      // 16-lane groups
@@ -516,7 +514,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
     const int h = hk * G + g;
     if (nse == 1 && !part_only) {
       const float inv = L > 0.f ? 1.f / L : 0.f;
-      attn_store4(out, s8, x8c, xf_mt, b, H, h, d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv);
+      attn_store4(out, s8, xf_mt, b, H, h, d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv);
     } else {
       // publish the partial write-through (sc1): the reducing workgroup may sit on another XCD
       const size_t pi = ((size_t)b * H + h) * nsplit + split;
@@ -594,7 +592,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
     }
     const int h = hk * G + g;
     const float inv = L > 0.f ? 1.f / L : 0.f;
-    attn_store4(out, s8, x8c, xf_mt, b, H, h, d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv);
+    attn_store4(out, s8, xf_mt, b, H, h, d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv);
   }
   LSA_STAMP(6);
 }
@@ -609,7 +607,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
                                int unsplit_max, void* out, float* opart, float* mlpart, int* counters, int xf_mt,
                                const float* qkv_parts, int nparts,
                                long part_stride, const float* cos_t, const float* sin_t, const float* ks,
-                               const float* vs, int part_only, void* out_s8, int x8c, hipStream_t s) {
+                               const float* vs, int part_only, void* out_s8, hipStream_t s) {
   if (H % Hkv) return -1;
   if (xf_mt && B > 16 * xf_mt) return -4;
   if (out_s8 && !xf_mt) return -6;  // the e4m3 output lives in the xf8 layout
@@ -627,7 +625,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
 #define LSA_ADL(GV, RP, WV, KV8, SB)                                                                              \
   hipLaunchKernelGGL((attn_decode_kernel<GV, RP, WV, KV8, SB>), grid, dim3(64 * (WV)), 0, s, qq, kk, vv, ks, vs,     \
                      block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart,  \
-                     counters, xf_mt, ra, part_only, reinterpret_cast<uint8_t*>(out_s8), x8c)
+                     counters, xf_mt, ra, part_only, reinterpret_cast<uint8_t*>(out_s8))
   // waves per workgroup: 8 for G = 1 (single-buffered at >= LSA_ATTN_SB_MIN_WG workgroups); for G = 2, 3 four on
   // grids of <= LSA_ATTN_SMALL23_WG workgroups (3B batch 1, 2k context: 11.34 -> 10.74 us -- half the cross-wave
   // merge, profiles/r3/attn_decode_wv23_ab_mi355x.jsonl) and eight above (3B batch 32: 10.54 vs 11.33 us); else 4

@@ -105,20 +105,17 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 }
 
 // Byte offset of e4m3 activation (m, k) in the W8A8 / W4A8 decode layout X8[k/128][mt][64 lanes][32 B]: lane (g, r)
-// holds row 16 mt + r, as the B operand of one v_mfma_scale_f32_16x16x128_f8f6f4 step, in the K order the matrix
-// core uses for that operand pair (measured, scripts/probe_mfma_scale.py -> profiles/r4/probe_mfma_scale_mi355x.jsonl):
-//   * e4m3 x e4m3 (fp8 weights, consec = false): bytes 0..15 = k 128 s + 16 g .. +15, bytes 16..31 = 128 s + 64 + 16 g
-//     .. +15 -- the MFMA's K index is then k itself, and the scale byte of lane group b covers k 128 s + 32 b .. +31;
-//   * e2m1 x e4m3 (MXFP4 weights, consec = true): bytes 0..31 = k 128 s + 32 g .. +31 -- one MX block per lane, the
-//     scale byte of lane group b again covers k 128 s + 32 b .. +31.
-// Either way a block scale covers 32 consecutive k, and 8 consecutive k from a multiple of 8 are contiguous.
-__device__ __forceinline__ size_t xf8_off(int m, int k, int mt, bool consec) {
-  const size_t lane_base = ((size_t)(k >> 7) * mt + (m >> 4)) * 64 + (m & 15);
+// holds row 16 mt + r at k = 128 s + 16 g .. +15 (bytes 0..15) and 128 s + 64 + 16 g .. +15 (bytes 16..31).  That is
+// the K order in which v_mfma_scale_f32_16x16x128_f8f6f4 reads an 8-bit operand, so the MFMA's K index is k itself;
+// a 4-bit operand lane (g, r) holds K 128 s + 32 g .. +31 (one MX block), and the scale byte of lane group b covers
+// K 128 s + 32 b .. +31 for either operand (measured: scripts/probe_mfma_scale.py, profiles/r4/probe_mfma_scale_mi355x.jsonl;
+// tests/test_kernels_gpu.py::test_a8_gemm_block_scales).  So activation block scales cover 32 consecutive k, for
+// e4m3 and e2m1 weights alike.  8 consecutive k from a multiple of 8 are contiguous.
+__device__ __forceinline__ size_t xf8_off(int m, int k, int mt) {
   const int kc = k & 127;
-  return consec ? (lane_base + 16 * (kc >> 5)) * 32 + (kc & 31)
-                : (lane_base + 16 * ((kc & 63) >> 4)) * 32 + 16 * (kc >> 6) + (kc & 15);
+  return (((size_t)(k >> 7) * mt + (m >> 4)) * 64 + 16 * ((kc & 63) >> 4) + (m & 15)) * 32 + 16 * (kc >> 6) + (kc & 15);
 }
-// Byte offset of the E8M0 scale of k's 32-block (both layouts) in the block-scale array S8[k/128][mt][64 lanes]
+// Byte offset of the E8M0 scale of k's 32-block in the block-scale array S8[k/128][mt][64 lanes] (lane group b = block b)
 __device__ __forceinline__ size_t xs8_off(int m, int k, int mt) {
   return ((size_t)(k >> 7) * mt + (m >> 4)) * 64 + 16 * ((k & 127) >> 5) + (m & 15);
 }

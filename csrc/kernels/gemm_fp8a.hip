@@ -10,20 +10,19 @@
 // the skinny kernels: chunks of U k128-steps dealt round-robin to the waves, split-K over blockIdx.y, a two-deep
 // register pipeline pinned with sched_barrier, cross-wave reduction through LDS.
 //
-// Activations ("xf8", common.h xf8_off): X8[kb128][MT][lane][32 B], lane (g, r) holds row 16 mt + r in the K order
-// the matrix core uses for the operand pair (measured, scripts/probe_mfma_scale.py): e4m3 x e4m3 (WK 0) = k 128 s + 16 g
-// .. +15 then 128 s + 64 + 16 g .. +15; e2m1 x e4m3 (WK 1) = k 128 s + 32 g .. +31.  Either way the block scale byte
-// of lane group b covers k 128 s + 32 b .. +31.  Two scalings:
+// Activations ("xf8", common.h xf8_off): X8[kb128][MT][lane][32 B], lane (g, r) holds row 16 mt + r at k = 128 s + 16 g
+// .. +15 and 128 s + 64 + 16 g .. +15 -- the K order the matrix core reads an 8-bit operand in (measured,
+// scripts/probe_mfma_scale.py), so the MFMA's K index is k itself.  Two scalings:
 //   * per-row f32 sx (the RMSNorm launch quantises its output rows by amax / 448; ops.quantize_xf8), and/or
-//   * ASC: per-32-k-block E8M0 bytes S8[kb128][MT][lane] (common.h xs8_off) fed to the MFMA's B scale operand --
-//     what the decode attention (o input: one scale per (row, head)) and this kernel's own SiLU epilogue (down
-//     input: one per (row, 32 columns)) produce without a whole-row reduction.
+//   * ASC: per-32-k-block E8M0 bytes S8[kb128][MT][lane] (common.h xs8_off: lane group b = k 128 s + 32 b .. +31)
+//     fed to the MFMA's B scale operand -- what the decode attention (o input: one scale per (row, head)) and this
+//     kernel's own SiLU epilogue (down input: one per (row, 32 columns)) produce without a whole-row reduction.
 // Weights: WK 0 -- the fp8 decode layout Wq[nb][kb64][lane][16 B] (lane 16 g + r = W[16 nb + r][64 kb64 + 16 g ..
-//   +15]); an MFMA step kk takes the lane's fragments of k64 blocks 2 kk and 2 kk + 1 (the e4m3 x e4m3 K order above),
-//   the per-output-channel f32 scale applies in the epilogue.
-//   WK 1 -- MXFP4 Wq[nb][kb128][lane][16 B] (lane (g, r) = W[16 nb + r][128 kb + 32 g .. +31] as e2m1 nibbles, one
-//   MX block) + S[nb][kb128 / 4][lane][4 B] E8M0 (gemm_fp4.hip's layout: the W4A16 path reads the same bytes), the
-//   lane's byte as the MFMA's A scale operand.
+//   +15]); an MFMA step kk takes the lane's fragments of k64 blocks 2 kk and 2 kk + 1 (the 8-bit K order above), the
+//   per-output-channel f32 scale applies in the epilogue.
+//   WK 1 -- MXFP4 Wq[nb][kb128][lane][16 B] (lane (g, r) = W[16 nb + r][128 kb + 32 g .. +31] as e2m1 nibbles: the
+//   4-bit K order, one MX block per lane) + S[nb][kb128 / 4][lane][4 B] E8M0 (gemm_fp4.hip's layout: the W4A16 path
+//   reads the same bytes), the lane's byte as the MFMA's A scale operand.
 //
 // Epilogues: EPI_F32 -> f32 split-K slabs [splitk][M][N];  EPI_SILU -> silu(gate) * up, gate / up rows interleaved
 // per 16, written as bf16 (row-major, XFO 0, or fragment-major, XFO 1, for a 16-bit down projection) or -- XFO 2 --
@@ -225,7 +224,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
           const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
           const f32x4_t v = red[0][(2 * p) * MT + j][l];
           const int e = e8m0_for_amax(__uint_as_float(bmax[m][(p >> 1) % NBLK]));
-          *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out) + xf8_off(m, n, MT, WK == 1)) =
+          *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out) + xf8_off(m, n, MT)) =
               pack4_fp8(v[0], v[1], v[2], v[3], e8m0_inv(e));
           if ((l >> 4) == 0 && (p & 1) == 0) out_s8[xs8_off(m, n, MT)] = (uint8_t)e;
         }
@@ -373,7 +372,7 @@ extern "C" int lsa_a8_gemm(const void* X8, const void* s8, const float* sx, int 
 // x [M, K] bf16 -> xf8 fragment layout (rows of the mt tiles past M zeroed) + per-row scale amax / 448:
 // the standalone form of the add_rmsnorm fp8 output (tests, benches, prefill-free callers)
 __global__ __launch_bounds__(256) void quant_xf8_kernel(const uint16_t* __restrict__ x, int ldx, int M, int K, int MT,
-                                                        uint8_t* __restrict__ x8, float* __restrict__ sx, int x8c) {
+                                                        uint8_t* __restrict__ x8, float* __restrict__ sx) {
   __shared__ float red[8];
   const int m = blockIdx.x;  // one workgroup per row of the MT tiles
   float amax = 0.f;
@@ -395,14 +394,14 @@ __global__ __launch_bounds__(256) void quant_xf8_kernel(const uint16_t* __restri
       unpack8(*reinterpret_cast<const uint4*>(x + (size_t)m * ldx + c), f);
       q = pack8_fp8(f, inv);
     }
-    *reinterpret_cast<uint2*>(x8 + xf8_off(m, c, MT, x8c != 0)) = q;
+    *reinterpret_cast<uint2*>(x8 + xf8_off(m, c, MT)) = q;
   }
 }
 
-extern "C" int lsa_quant_xf8(const void* x, int ldx, int M, int K, int MT, void* x8, float* sx, int x8c, hipStream_t s) {
+extern "C" int lsa_quant_xf8(const void* x, int ldx, int M, int K, int MT, void* x8, float* sx, hipStream_t s) {
   if (M <= 0 || M > 16 * MT || K % 128 != 0) return -1;
   hipLaunchKernelGGL(quant_xf8_kernel, dim3(16 * MT), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(x), ldx, M, K, MT,
-                     reinterpret_cast<uint8_t*>(x8), sx, x8c);
+                     reinterpret_cast<uint8_t*>(x8), sx);
   return (int)hipGetLastError();
 }
 
@@ -411,7 +410,7 @@ extern "C" int lsa_quant_xf8(const void* x, int ldx, int M, int K, int MT, void*
 // e4m3 outputs (tests, benches)
 __global__ __launch_bounds__(256) void quant_xf8_blocks_kernel(const uint16_t* __restrict__ x, int ldx, int M, int K,
                                                                int MT, int blk, uint8_t* __restrict__ x8,
-                                                               uint8_t* __restrict__ s8, int x8c) {
+                                                               uint8_t* __restrict__ s8) {
   // one thread per (row of the mt tiles, 32-column block)
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
   const int nb32 = K / 32;
@@ -435,17 +434,17 @@ __global__ __launch_bounds__(256) void quant_xf8_blocks_kernel(const uint16_t* _
       unpack8(*reinterpret_cast<const uint4*>(x + (size_t)m * ldx + c), f);
       q = pack8_fp8(f, inv);
     }
-    *reinterpret_cast<uint2*>(x8 + xf8_off(m, c, MT, x8c != 0)) = q;
+    *reinterpret_cast<uint2*>(x8 + xf8_off(m, c, MT)) = q;
   }
   s8[xs8_off(m, c0, MT)] = (uint8_t)e;
 }
 
-extern "C" int lsa_quant_xf8_blocks(const void* x, int ldx, int M, int K, int MT, int blk, void* x8, void* s8, int x8c,
+extern "C" int lsa_quant_xf8_blocks(const void* x, int ldx, int M, int K, int MT, int blk, void* x8, void* s8,
                                     hipStream_t s) {
   if (M <= 0 || M > 16 * MT || K % 128 != 0 || (blk != 32 && blk != 128)) return -1;
   const long n = (long)16 * MT * (K / 32);
   hipLaunchKernelGGL(quant_xf8_blocks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                      reinterpret_cast<const uint16_t*>(x), ldx, M, K, MT, blk, reinterpret_cast<uint8_t*>(x8),
-                     reinterpret_cast<uint8_t*>(s8), x8c);
+                     reinterpret_cast<uint8_t*>(s8));
   return (int)hipGetLastError();
 }

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
                                                            const uint16_t* __restrict__ w, float eps,
                                                            uint16_t* __restrict__ xn, int D, int xf_mt,
                                                            long long* __restrict__ ss_out, int ss_ld, int ss_nzero,
-                                                           uint8_t* __restrict__ x8, float* __restrict__ sx8, int x8c) {
+                                                           uint8_t* __restrict__ x8, float* __restrict__ sx8) {
   __shared__ float red[16];
   const int m = blockIdx.x;
   const int r = row_idx ? row_idx[m] : m;
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(1024) void add_rmsnorm_kernel(float* __restrict__ h
 #pragma unroll
     for (int q = 0; q < VPT; ++q) {
       const int c = (threadIdx.x + q * nt) * 8;
-      if (c < D) *reinterpret_cast<uint2*>(x8 + xf8_off(m, c, xf_mt, x8c != 0)) = pack8_fp8(v[q], isc);
+      if (c < D) *reinterpret_cast<uint2*>(x8 + xf8_off(m, c, xf_mt)) = pack8_fp8(v[q], isc);
     }
   }
 }
@@ -117,10 +117,10 @@ template <int VPT>
 static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, const float* parts, size_t ps,
                            const int* ids, const uint16_t* e, const int* row_idx, int write_h, const uint16_t* w,
                            float eps, uint16_t* o, int D, int xf_mt, long long* ss_out, int ss_ld, int ss_nzero,
-                           uint8_t* x8, float* sx8, int x8c) {
+                           uint8_t* x8, float* sx8) {
 #define LSA_RN(NP)                                                                                         \
   hipLaunchKernelGGL((add_rmsnorm_kernel<NP, VPT>), dim3(rows), dim3(nt), 0, s, h, parts, np, ps, ids, e, \
-                     row_idx, write_h, w, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero, x8, sx8, x8c)
+                     row_idx, write_h, w, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero, x8, sx8)
   switch (parts ? np : 0) {
     case 0: LSA_RN(0); break;
     case 1: LSA_RN(1); break;
@@ -135,12 +135,11 @@ static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, co
 }
 
 // x8 / sx8 (optional): also write the output rows as fp8 e4m3 in the xf8 layout of xf_mt row tiles with a
-// per-row scale (the W8A8 / W4A8 decode GEMM input; x8c: the consecutive-k layout of MXFP4 weights, else the
-// fp8-weight one, common.h xf8_off); xn may then be null (no bf16 copy)
+// per-row scale (the W8A8 decode GEMM input); xn may then be null (no bf16 copy)
 extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids,
                                const void* emb, const int* row_idx, int write_h, const void* w, float eps, void* xn,
                                int rows, int D, int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, void* x8,
-                               float* sx8, int x8c, hipStream_t s) {
+                               float* sx8, hipStream_t s) {
   if (D % 8 != 0 || rows <= 0) return -1;
   if (xf_mt && (D % 32 != 0 || rows > 16 * xf_mt)) return -3;
   if (ss_out && (row_idx || ss_ld < rows || ss_nzero < 0)) return -4;
@@ -153,10 +152,10 @@ extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long pa
   uint8_t* q8 = reinterpret_cast<uint8_t*>(x8);
   if (vec <= 1024) {
     launch_rmsnorm<1>(nparts, rows, (vec + 63) / 64 * 64, s, h, parts, (size_t)part_stride, ids, e, row_idx, write_h,
-                      ww, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero, q8, sx8, x8c);
+                      ww, eps, o, D, xf_mt, ss_out, ss_ld, ss_nzero, q8, sx8);
   } else if (vec <= 4096) {
     launch_rmsnorm<4>(nparts, rows, 1024, s, h, parts, (size_t)part_stride, ids, e, row_idx, write_h, ww, eps, o, D, xf_mt,
-                      ss_out, ss_ld, ss_nzero, q8, sx8, x8c);
+                      ss_out, ss_ld, ss_nzero, q8, sx8);
   } else {
     return -2;
   }

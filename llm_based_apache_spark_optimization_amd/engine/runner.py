@@ -324,9 +324,8 @@ class ModelRunner:
         nqkv = (self.H + 2 * self.Hkv) * self.D
         sk_q = (ops.pick_gemm_config(B, nqkv, d, "f32", xf=True, kind=ak)[1] if a8
                 else self._splitk(B, d, nqkv, tp_reduced=False, xf=xf))
-        x8c = ops.x8_consec(w.layers[0].wqkv)  # the xf8 K order of the weight format
-        q8 = dict(x8=self.x8, sx8=self.sx8, x8c=x8c) if a8 else {}
-        q8m = dict(x8=self.x8, sx8=self.sx8, x8c=x8c) if a8m else {}
+        q8 = dict(x8=self.x8, sx8=self.sx8) if a8 else {}
+        q8m = dict(x8=self.x8, sx8=self.sx8) if a8m else {}
         # each side of the layer: a wide residual add + row scale in the next GEMM unless that GEMM runs W8A8 (its
         # e4m3 input comes from the quantising norm launch)
         wna = self.wide_norm and not a8
@@ -376,7 +375,7 @@ class ModelRunner:
                             (self.x8o if a8o else attn) if xf else attn.view(B, self.H, self.D), workspace=ws,
                             plan=plan, xf=xf, qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
                             sin=self.sin if fr else None, kv_scales=self._kv_scales(l),
-                            out_s8=self.s8o if a8o else None, x8c=x8c)
+                            out_s8=self.s8o if a8o else None)
             if a8o:
                 ops.linear_a8(self.x8o, None, B, lw.wo, "f32", out=o_parts, splitk=sk_o, s8=self.s8o)
             else:

@@ -585,32 +585,19 @@ def linear_xf(xf: torch.Tensor, M: int, w: PackedWeight, epi: str = "bf16", out:
 FP8_A8_DECODE = os.environ.get("LSA_FP8_A8", "1") != "0"
 
 
-def x8_consec(w: "PackedWeight") -> bool:
-    """The xf8 K order a W8A8 / W4A8 GEMM over weights ``w`` reads: consecutive 32-k per lane for MXFP4 (e2m1 x e4m3),
-    the split order for fp8 weights (e4m3 x e4m3) -- common.h xf8_off, scripts/probe_mfma_scale.py."""
-    return w.kind == "mxfp4"
-
-
-def to_xf8(x8: torch.Tensor, mt: int, consec: bool = False) -> torch.Tensor:
+def to_xf8(x8: torch.Tensor, mt: int) -> torch.Tensor:
     """uint8 [M, K] e4m3 bytes -> the flat xf8 layout X8[K/128][mt][64 lanes][32 B] of the W8A8 / W4A8 decode GEMM
-    (csrc/kernels/gemm_fp8a.hip, common.h xf8_off), rows >= M zero.  Lane 16 g + r holds row 16 t + r at
-    k = 128 s + 16 g .. +15 and 128 s + 64 + 16 g .. +15 (fp8 weights), or -- ``consec`` (MXFP4 weights) -- at
-    k = 128 s + 32 g .. +31."""
+    (csrc/kernels/gemm_fp8a.hip, common.h xf8_off; lane 16 g + r: row 16 t + r at k = 128 s + 16 g .. +15 and
+    128 s + 64 + 16 g .. +15 -- the MFMA's own K order for an 8-bit operand), rows >= M zero."""
     M, K = x8.shape
     full = torch.zeros(16 * mt, K, dtype=torch.uint8, device=x8.device)
     full[:M] = x8
-    if consec:
-        v = full.view(mt, 16, K // 128, 4, 32)  # t, r, s, g, e
-        return v.permute(2, 0, 3, 1, 4).contiguous().view(-1)  # s, t, g, r, e
     v = full.view(mt, 16, K // 128, 2, 4, 16)  # t, r, s, h, g, e
     return v.permute(2, 0, 4, 1, 3, 5).contiguous().view(-1)  # s, t, g, r, h, e
 
 
-def from_xf8(x8f: torch.Tensor, M: int, K: int, consec: bool = False) -> torch.Tensor:
+def from_xf8(x8f: torch.Tensor, M: int, K: int) -> torch.Tensor:
     mt = xfrag_tiles(M)
-    if consec:
-        v = x8f.view(-1)[: mt * 16 * K].view(K // 128, mt, 4, 16, 32)  # s, t, g, r, e
-        return v.permute(1, 3, 0, 2, 4).reshape(16 * mt, K)[:M]
     v = x8f.view(-1)[: mt * 16 * K].view(K // 128, mt, 4, 16, 2, 16)  # s, t, g, r, h, e
     return v.permute(1, 3, 0, 4, 2, 5).reshape(16 * mt, K)[:M]
 
@@ -658,7 +645,7 @@ def dequant_blocks_fp8(x8: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
 
 
 def quantize_xf8(x: torch.Tensor, mt: Optional[int] = None, out: Optional[torch.Tensor] = None,
-                 sx: Optional[torch.Tensor] = None, consec: bool = False):
+                 sx: Optional[torch.Tensor] = None):
     """(x8 flat xf8 bytes, sx [M] f32): per-row e4m3 activations (scale amax / 448) for ``linear_a8``."""
     M, K = x.shape
     mt = mt or xfrag_tiles(M)
@@ -668,15 +655,15 @@ def quantize_xf8(x: torch.Tensor, mt: Optional[int] = None, out: Optional[torch.
         sx = torch.empty(M, dtype=torch.float32, device=x.device)
     if not _gpu(x):
         q, s = quantize_rows_fp8(x)
-        out.view(-1)[: mt * 16 * K].copy_(to_xf8(q, mt, consec))
+        out.view(-1)[: mt * 16 * K].copy_(to_xf8(q, mt))
         sx[:M].copy_(s)
         return out, sx
-    ext().quant_xf8(x, mt, out, sx, 1 if consec else 0)
+    ext().quant_xf8(x, mt, out, sx)
     return out, sx
 
 
 def quantize_xf8_blocks(x: torch.Tensor, blk: int = 32, mt: Optional[int] = None, out: Optional[torch.Tensor] = None,
-                        s8: Optional[torch.Tensor] = None, consec: bool = False):
+                        s8: Optional[torch.Tensor] = None):
     """(x8 flat xf8 bytes, s8 flat block scales): block-scaled e4m3 activations (``quantize_blocks_fp8``) in the
     layouts ``linear_a8(..., s8=)`` reads."""
     M, K = x.shape
@@ -687,17 +674,17 @@ def quantize_xf8_blocks(x: torch.Tensor, blk: int = 32, mt: Optional[int] = None
         s8 = torch.full((mt * 64 * (K // 128),), 127, dtype=torch.uint8, device=x.device)
     if not _gpu(x):
         q, s = quantize_blocks_fp8(x, blk)
-        out.view(-1)[: mt * 16 * K].copy_(to_xf8(q, mt, consec))
+        out.view(-1)[: mt * 16 * K].copy_(to_xf8(q, mt))
         s8.view(-1)[: mt * 64 * (K // 128)].copy_(to_xs8(s, mt))
         return out, s8
-    ext().quant_xf8_blocks(x.contiguous(), mt, blk, out, s8, 1 if consec else 0)
+    ext().quant_xf8_blocks(x.contiguous(), mt, blk, out, s8)
     return out, s8
 
 
 def xf8_dequant(x8: torch.Tensor, M: int, K: int, sx: Optional[torch.Tensor] = None,
-                s8: Optional[torch.Tensor] = None, consec: bool = False) -> torch.Tensor:
+                s8: Optional[torch.Tensor] = None) -> torch.Tensor:
     """The f32 [M, K] activations a W8A8 / W4A8 GEMM multiplies: xf8 bytes x per-row sx x per-block E8M0."""
-    v = from_xf8(x8, M, K, consec).view(torch.float8_e4m3fn).float()
+    v = from_xf8(x8, M, K).view(torch.float8_e4m3fn).float()
     if s8 is not None:
         v = (v.view(M, K // 32, 32) * torch.exp2(from_xs8(s8, M, K).float() - 127.0)[..., None]).view(M, K)
     if sx is not None:
@@ -718,9 +705,8 @@ def linear_a8(x8: torch.Tensor, sx: Optional[torch.Tensor], M: int, w: PackedWei
     assert epi in ("f32", "silu")
     assert sx is not None or s8 is not None
     f8o = epi == "silu" and out_s8 is not None
-    consec = x8_consec(w)
     if not _gpu(x8):
-        xd = xf8_dequant(x8, M, w.K, sx, s8, consec)
+        xd = xf8_dequant(x8, M, w.K, sx, s8)
         if rownorm is not None:
             xd = xd * torch.rsqrt(ss_float(rownorm[0][:M]) / w.K + rownorm[1])[:, None]
         y = xd @ w.dense().float().t()
@@ -736,7 +722,7 @@ def linear_a8(x8: torch.Tensor, sx: Optional[torch.Tensor], M: int, w: PackedWei
         if f8o:
             q, s = quantize_blocks_fp8(act, 32)
             mt = xfrag_tiles(M)
-            out.view(-1)[: mt * 16 * F].copy_(to_xf8(q, mt, consec))
+            out.view(-1)[: mt * 16 * F].copy_(to_xf8(q, mt))
             out_s8.view(-1)[: mt * 64 * (F // 128)].copy_(to_xs8(s, mt))
             return out
         act = act.to(torch.bfloat16)
@@ -878,20 +864,19 @@ def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
                 emb: Optional[torch.Tensor] = None, row_idx: Optional[torch.Tensor] = None,
                 write_h: bool = True, rows: Optional[int] = None, xf: bool = False,
                 ss_out: Optional[torch.Tensor] = None, ss_ld: int = 0, ss_nzero: int = 0,
-                x8: Optional[torch.Tensor] = None, sx8: Optional[torch.Tensor] = None,
-                x8c: bool = False) -> torch.Tensor:
+                x8: Optional[torch.Tensor] = None, sx8: Optional[torch.Tensor] = None) -> torch.Tensor:
     """h[r] (= emb[ids[r]]) (+= sum parts[:, r]); xn[m] = rmsnorm(h[row_idx[m]]) * w.
     xf=True: xn is a flat buffer receiving the fragment-major layout (``to_xfrag``) of ``rows`` rows.
     ss_out (raw mode, the norm folded into the next GEMMs): xn = bf16(h) un-normalised, ss_out[m] = sum h^2,
     and ss_out[k * ss_ld + m] = 0 for k = 1..ss_nzero (the accumulators of the later residual epilogues).
     x8 / sx8: the same rows also as per-row-scaled e4m3 in the xf8 layout (``linear_a8`` input; quantised from
-    the f32 values, before the bf16 rounding of xn; ``x8c``: the consecutive-k order of MXFP4 weights, ``x8_consec``)."""
+    the f32 values, before the bf16 rounding of xn)."""
     assert x8 is None or xf, "the fp8 output rides on the fragment-major (xf) decode layout"
     if x8 is not None and not _gpu(h):
         add_rmsnorm(h, w, eps, xn, parts, ids, emb, row_idx, write_h, rows, xf, ss_out, ss_ld, ss_nzero)
         n = rows if rows is not None else xn.shape[0]
         xr = from_xfrag(xn, n, w.numel()) if xf else xn[:n]
-        quantize_xf8(xr, xfrag_tiles(n), x8, sx8, consec=x8c)
+        quantize_xf8(xr, xfrag_tiles(n), x8, sx8)
         return xn
     if rows is None:
         assert not xf, "xf output needs rows"
@@ -921,8 +906,7 @@ def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
     nparts = parts.shape[0] if parts is not None else 0
     stride = parts.stride(0) if parts is not None else 0
     ext().add_rmsnorm(h, parts, nparts, stride, ids, emb, row_idx, write_h, w, eps, xn, rows,
-                      xfrag_tiles(rows) if (xf or x8 is not None) else 0, ss_out, ss_ld, ss_nzero, x8, sx8,
-                      1 if x8c else 0)
+                      xfrag_tiles(rows) if (xf or x8 is not None) else 0, ss_out, ss_ld, ss_nzero, x8, sx8)
     return xn
 
 
@@ -1038,7 +1022,7 @@ def decode_workspace(B: int, H: int, Hkv: int, nsplit: int, device) -> tuple:
 
 
 def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None, xf=False,
-                qkv_parts=None, cos=None, sin=None, kv_scales=None, part_only=False, out_s8=None, x8c=False):
+                qkv_parts=None, cos=None, sin=None, kv_scales=None, part_only=False, out_s8=None):
     """q [B,H,128] vs paged cache, context = pos + 1.  workspace = decode_workspace(...) for split-KV.
     xf=True: out is a flat buffer receiving the fragment-major layout of the [B, H*128] output.
     qkv_parts ([S, B, (H+2Hkv)*128] f32 split-K slabs of the QKV projection) + cos/sin: RoPE and the
@@ -1047,8 +1031,7 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     part_only: every split leaves its (o, m, l) partial in the workspace and nothing is combined (the latency path's o
     projection merges them, ``lat_linear(src='part')``); on the CPU the finished rows still land in ``out``.
     out_s8 (xf only): ``out`` is a uint8 buffer receiving the output as e4m3 in the xf8 layout with one E8M0 scale
-    per (row, head) in ``out_s8`` -- the input of a W8A8 / W4A8 o projection (``linear_a8(s8=)``; ``x8c``: the
-    consecutive-k order of MXFP4 weights, ``x8_consec``)."""
+    per (row, head) in ``out_s8`` -- the input of a W8A8 / W4A8 o projection (``linear_a8(s8=)``)."""
     B = pos.shape[0]
     assert out_s8 is None or xf, "the e4m3 attention output lives in the xf8 layout"
     if not _gpu(pos):
@@ -1057,7 +1040,7 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
         if out_s8 is not None:
             tmp = torch.empty(B, H, q.shape[-1], dtype=torch.bfloat16, device=q.device)
             ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, tmp, kv_scales)
-            quantize_xf8_blocks(tmp.view(B, -1), 128, xfrag_tiles(B), out, out_s8, consec=x8c)
+            quantize_xf8_blocks(tmp.view(B, -1), 128, xfrag_tiles(B), out, out_s8)
             return out
         if not xf:
             return ref.attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, kv_scales)
@@ -1075,7 +1058,7 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     ks, vs = kv_scales if kv_scales is not None else (None, None)
     ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart, counters,
                       xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs, 1 if part_only else 0,
-                      out_s8, 1 if x8c else 0)
+                      out_s8)
     return out
 
 

@@ -54,10 +54,10 @@ for name, (N, K, epi, scal) in SHAPES.items():
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
         xf = ops.to_xfrag(x)
         if scal == "row":
-            x8, sx = ops.quantize_xf8(x, consec=KIND == "mxfp4")
+            x8, sx = ops.quantize_xf8(x)
             s8 = None
         else:
-            x8, s8 = ops.quantize_xf8_blocks(x, 128 if scal == "b128" else 32, consec=KIND == "mxfp4")
+            x8, s8 = ops.quantize_xf8_blocks(x, 128 if scal == "b128" else 32)
             sx = None
         o8 = torch.zeros(mt * 16 * N // 2, device=dev, dtype=torch.uint8) if epi == "silu8" else None
         os8 = torch.zeros(mt * 64 * max(1, N // 2 // 128), device=dev, dtype=torch.uint8) if epi == "silu8" else None

@@ -394,12 +394,12 @@ def test_attn_decode(gpu, HH, lens):
         ro = out if plan is None else out3
         assert torch.equal(ops.from_xfrag(xf, B, H * D), ro.view(B, -1))
     # e4m3 output (the W8A8 / W4A8 o projection's input): one E8M0 scale per (row, head), vs the fp32 oracle
-    for plan, x8c in ((None, False), ((bt.shape[1], 1), False), (None, True)):
+    for plan in (None, (bt.shape[1], 1)):
         mt = ops.xfrag_tiles(B)
         x8 = torch.zeros(mt * 16 * H * D, device=gpu, dtype=torch.uint8)
         s8 = torch.full((mt * 64 * H,), 127, device=gpu, dtype=torch.uint8)
-        ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, x8, plan=plan, xf=True, out_s8=s8, x8c=x8c)
-        got = ops.xf8_dequant(x8, B, H * D, None, s8, consec=x8c)
+        ops.attn_decode(q, kc, vc, bt, pos, H, Hkv, scale, x8, plan=plan, xf=True, out_s8=s8)
+        got = ops.xf8_dequant(x8, B, H * D, None, s8)
         want = out2.view(B, -1).float()
         assert _rel(got, want) < 4e-2, plan
         # the scale is the head's own: its amax lands in the top binade of e4m3 ([224, 448])
@@ -858,12 +858,12 @@ def test_quant_xf8_blocks(gpu, M):
     """GPU block-scaled e4m3 quantisation (E8M0 per 32 / 128 columns) vs the CPU definition."""
     K = 1024
     x = _blocky(M, K, gpu, M)
-    for blk, consec in ((32, False), (128, False), (32, True)):
-        x8, s8 = ops.quantize_xf8_blocks(x, blk, consec=consec)
-        c8, cs8 = ops.quantize_xf8_blocks(x.cpu(), blk, consec=consec)
+    for blk in (32, 128):
+        x8, s8 = ops.quantize_xf8_blocks(x, blk)
+        c8, cs8 = ops.quantize_xf8_blocks(x.cpu(), blk)
         assert torch.equal(ops.from_xs8(s8, M, K).cpu(), ops.from_xs8(cs8, M, K)), blk
-        a = ops.xf8_dequant(x8, M, K, None, s8, consec=consec).cpu()
-        b = ops.xf8_dequant(c8, M, K, None, cs8, consec=consec)
+        a = ops.xf8_dequant(x8, M, K, None, s8).cpu()
+        b = ops.xf8_dequant(c8, M, K, None, cs8)
         assert torch.allclose(a, b, rtol=0.13, atol=0), blk
         assert _rel(a, x.float().cpu()) < 4e-2
 
@@ -879,9 +879,8 @@ def test_a8_gemm_block_scales(gpu, M, wkind):
     torch.manual_seed(M)
     x = _blocky(M, K, gpu, 7 * M)
     w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
-    consec = wkind == "mxfp4"  # the K order of the operand pair (ops.x8_consec)
-    x8, s8 = ops.quantize_xf8_blocks(x, 32, consec=consec)
-    xd = ops.xf8_dequant(x8, M, K, None, s8, consec=consec)
+    x8, s8 = ops.quantize_xf8_blocks(x, 32)
+    xd = ops.xf8_dequant(x8, M, K, None, s8)
     sx = torch.full((M,), 0.5, device=gpu)  # a per-row scale on top of the blocks multiplies in
     for epi in ("f32", "silu"):
         pw = ops.PackedWeight.from_dense(w if epi == "f32" else ops.interleave_gate_up(w[: N // 2], w[N // 2:]), wkind)
@@ -906,7 +905,7 @@ def test_a8_gemm_block_scales(gpu, M, wkind):
             o8 = torch.zeros(mt * 16 * N // 2, device=gpu, dtype=torch.uint8)
             os8 = torch.full((mt * 64 * (N // 2 // 128),), 0, device=gpu, dtype=torch.uint8)
             ops.linear_a8(x8, None, M, pw, "silu", out=o8, out_s8=os8, s8=s8, nb=nb)
-            got8 = ops.xf8_dequant(o8, M, N // 2, None, os8, consec=consec)
+            got8 = ops.xf8_dequant(o8, M, N // 2, None, os8)
             assert _rel(got8, want) < 4e-2, nb
             _, ws = ops.quantize_blocks_fp8(want.cpu(), 32)
             # the block exponents agree except where f32 accumulation order moves an amax across a binade
