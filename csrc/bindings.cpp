@@ -13,7 +13,6 @@
 #endif
 
 #include "kernels/lsa_epi.h"
-#include "kernels/lsa_lat.h"
 
 extern "C" {
 int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb, int splitk,
@@ -40,8 +39,8 @@ int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* bl
                     const int* pos, int B, int H, int Hkv, float scale, int chunk_blocks, int nsplit, int unsplit_max,
                     void* out, float* opart, float* mlpart, int* counters, int xf_mt, const float* qkv_parts, int nparts,
                     long part_stride,
-                    const float* cos_t, const float* sin_t, const float* ks, const float* vs, int part_only,
-                    void* out_s8, hipStream_t s);
+                    const float* cos_t, const float* sin_t, const float* ks, const float* vs, void* out_s8,
+                    hipStream_t s);
 int lsa_kv8_dequant(const void* kc, const void* vc, const float* ks, const float* vs, const int* block_tables,
                     int max_blocks, const int* ctx_lens, int nseq, int Hkv, int mb, void* ko, void* vo, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
@@ -89,10 +88,6 @@ int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int ran
 int lsa_fp4_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const void* S, int N, void* out, int epi,
                     int nb, int splitk, int waves, int xfrag, const LsaEpi* ep, hipStream_t stream);
 int lsa_fp4_dequant(const void* Wq, const void* S, int N, int K, void* Wf, hipStream_t s);
-int lsa_lat_embed(const int* ids, const void* emb, int M, int D, long long* hq, unsigned long long* ss, int ss_ld,
-                  int nzero, hipStream_t s);
-int lsa_lat_final_norm(const long long* hq, const void* w, float eps, void* xn, int M, int D, hipStream_t s);
-int lsa_lat_gemv(const LatArgs* args, int src, int epi, int nb, int waves, int splitk, hipStream_t s);
 }
 
 namespace {
@@ -527,8 +522,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                  at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, at::Tensor& counters, int64_t xf_mt,
                  const c10::optional<at::Tensor>& qkv_parts, const c10::optional<at::Tensor>& cos_t,
                  const c10::optional<at::Tensor>& sin_t, int64_t unsplit_max, const c10::optional<at::Tensor>& ks,
-                 const c10::optional<at::Tensor>& vs, int64_t part_only = 0,
-                 const c10::optional<at::Tensor>& out_s8 = c10::nullopt) {
+                 const c10::optional<at::Tensor>& vs, const c10::optional<at::Tensor>& out_s8 = c10::nullopt) {
   need(q, at::kBFloat16, "q");
   check_cache(kc, vc, ks, vs);
   need(pos, at::kInt, "pos");
@@ -570,7 +564,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                         (int)unsplit_max, out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), counters.data_ptr<int>(), xf_mt,
                         ptr<const float>(qkv_parts), qkv_parts.has_value() ? qkv_parts->size(0) : 0,
                         qkv_parts.has_value() ? qkv_parts->stride(0) : 0, ptr<const float>(cos_t),
-                        ptr<const float>(sin_t), ptr<const float>(ks), ptr<const float>(vs), (int)part_only,
+                        ptr<const float>(sin_t), ptr<const float>(ks), ptr<const float>(vs),
                         out_s8.has_value() ? out_s8->data_ptr() : nullptr, cur_stream()),
         "attn_decode");
 }
@@ -795,114 +789,6 @@ void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Te
 }
 
 // ---------------------------------------------------------------------------------------- latency path (B <= 4)
-// kernels/decode_lat.hip: Q32 residual stream hq [>= M, d] int64, packed row-sum words ss [>= M] int64
-void lat_embed(const at::Tensor& ids, const at::Tensor& emb, at::Tensor& hq, at::Tensor& ss, int64_t M, int64_t ss_ld,
-               int64_t nzero) {
-  need(ids, at::kInt, "ids");
-  need(emb, at::kBFloat16, "emb");
-  need(hq, at::kLong, "hq");
-  need(ss, at::kLong, "ss");
-  TORCH_CHECK(M >= 1 && M <= 4 && ids.numel() >= M, "lat_embed: 1..4 rows");
-  TORCH_CHECK(emb.dim() == 2 && emb.is_contiguous() && hq.dim() == 2 && hq.is_contiguous() && hq.size(0) >= M &&
-                  hq.size(1) == emb.size(1), "lat_embed: emb [V, d], hq [>= M, d]");
-  TORCH_CHECK(ss.is_contiguous() && ss_ld >= M && ss.numel() >= nzero * ss_ld, "lat_embed: row-sum words too small");
-  check(lsa_lat_embed(ids.data_ptr<int>(), emb.data_ptr(), M, emb.size(1), reinterpret_cast<long long*>(hq.data_ptr<int64_t>()),
-                      reinterpret_cast<unsigned long long*>(ss.data_ptr<int64_t>()), ss_ld, nzero, cur_stream()),
-        "lat_embed");
-}
-
-void lat_final_norm(const at::Tensor& hq, const at::Tensor& w, double eps, at::Tensor& xn, int64_t M) {
-  need(hq, at::kLong, "hq");
-  need(w, at::kBFloat16, "w");
-  need(xn, at::kBFloat16, "xn");
-  TORCH_CHECK(hq.dim() == 2 && hq.is_contiguous() && hq.size(0) >= M && M >= 1, "lat_final_norm: hq [>= M, d]");
-  const int64_t d = hq.size(1);
-  TORCH_CHECK(w.numel() == d && xn.is_contiguous() && xn.numel() >= M * d, "lat_final_norm: w [d], xn [>= M, d]");
-  check(lsa_lat_final_norm(reinterpret_cast<const long long*>(hq.data_ptr<int64_t>()), w.data_ptr(), (float)eps,
-                           xn.data_ptr(), M, d, cur_stream()),
-        "lat_final_norm");
-}
-
-// src 0 = bf16 activations x [>= M, K] row-major, 1 = Q32 residual hq [>= M, K] (+ ss words, folded RMSNorm), 2 =
-// attention partials (opart, mlpart, pos, plan); epi 0 = f32 slabs out [splitk, M, N], 1 = SiLU act [>= M, N / 2] bf16,
-// 2 = Q32 atomics into hq_out [>= M, N]
-void lat_gemv(const at::Tensor& w, int64_t N, int64_t K, int64_t M, int64_t src, int64_t epi, int64_t nb, int64_t waves,
-              int64_t splitk, const c10::optional<at::Tensor>& x, const c10::optional<at::Tensor>& hq,
-              const c10::optional<at::Tensor>& ss, double eps, int64_t timeout_ticks,
-              const c10::optional<at::Tensor>& opart, const c10::optional<at::Tensor>& mlpart,
-              const c10::optional<at::Tensor>& pos, int64_t nsplit, int64_t chunk_blocks, int64_t unsplit_max, int64_t H,
-              const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& act,
-              const c10::optional<at::Tensor>& hq_out, const c10::optional<at::Tensor>& stats) {
-  need(w, at::kBFloat16, "w");
-  TORCH_CHECK(M >= 1 && M <= 4, "lat_gemv: 1..4 rows");
-  TORCH_CHECK(N % 16 == 0 && K % 32 == 0 && w.numel() == N * K, "lat_gemv: w [N, K] fragment-major, N % 16, K % 32");
-  LatArgs a{};
-  a.W = w.data_ptr();
-  a.KB = (int)(K / 32);
-  a.N = (int)N;
-  a.M = (int)M;
-  a.eps = (float)eps;
-  a.inv_k = 1.0f / (float)K;
-  a.timeout = timeout_ticks;
-  if (src == 0) {
-    TORCH_CHECK(x.has_value(), "lat_gemv: src 0 needs x");
-    need(*x, at::kBFloat16, "x");
-    TORCH_CHECK(x->dim() == 2 && x->size(0) >= M && x->size(1) == K && x->stride(1) == 1, "lat_gemv: x [>= M, K]");
-    a.X = reinterpret_cast<const uint16_t*>(x->data_ptr());
-    a.ldx = (int)x->stride(0);
-  } else if (src == 1) {
-    TORCH_CHECK(hq.has_value() && ss.has_value(), "lat_gemv: src 1 needs hq and ss");
-    need(*hq, at::kLong, "hq");
-    need(*ss, at::kLong, "ss");
-    TORCH_CHECK(hq->dim() == 2 && hq->is_contiguous() && hq->size(0) >= M && hq->size(1) == K, "lat_gemv: hq [>= M, K]");
-    TORCH_CHECK(ss->is_contiguous() && ss->numel() >= M, "lat_gemv: ss words [>= M]");
-    a.hq = reinterpret_cast<const long long*>(hq->data_ptr<int64_t>());
-    a.ldh = (int)K;
-    a.ss_acc = reinterpret_cast<unsigned long long*>(ss->data_ptr<int64_t>());
-  } else if (src == 2) {
-    TORCH_CHECK(opart.has_value() && mlpart.has_value() && pos.has_value(), "lat_gemv: src 2 needs the partials");
-    need(*opart, at::kFloat, "opart");
-    need(*mlpart, at::kFloat, "mlpart");
-    need(*pos, at::kInt, "pos");
-    TORCH_CHECK(H * 128 == K && nsplit >= 1 && pos->numel() >= M, "lat_gemv: partials of H heads of 128");
-    TORCH_CHECK(opart->numel() >= M * H * nsplit * 128 && mlpart->numel() >= M * H * nsplit * 2,
-                "lat_gemv: partial workspace too small");
-    a.opart = opart->data_ptr<float>();
-    a.mlpart = reinterpret_cast<const unsigned long long*>(mlpart->data_ptr<float>());
-    a.pos = pos->data_ptr<int>();
-    a.nsplit = (int)nsplit;
-    a.chunk_blocks = (int)chunk_blocks;
-    a.unsplit_max = (int)unsplit_max;
-    a.H = (int)H;
-  } else {
-    TORCH_CHECK(false, "lat_gemv: src 0 | 1 | 2");
-  }
-  if (epi == 0) {
-    TORCH_CHECK(out.has_value(), "lat_gemv: epi 0 needs out");
-    need(*out, at::kFloat, "out");
-    TORCH_CHECK(out->is_contiguous() && out->numel() >= splitk * M * N, "lat_gemv: f32 slabs too small");
-    a.out = out->data_ptr<float>();
-  } else if (epi == 1) {
-    TORCH_CHECK(act.has_value(), "lat_gemv: epi 1 needs act");
-    need(*act, at::kBFloat16, "act");
-    TORCH_CHECK(act->is_contiguous() && act->numel() >= M * (N / 2), "lat_gemv: act too small");
-    a.act = reinterpret_cast<uint16_t*>(act->data_ptr());
-  } else if (epi == 2) {
-    TORCH_CHECK(hq_out.has_value(), "lat_gemv: epi 2 needs hq_out");
-    need(*hq_out, at::kLong, "hq_out");
-    TORCH_CHECK(hq_out->dim() == 2 && hq_out->is_contiguous() && hq_out->size(0) >= M && hq_out->size(1) == N,
-                "lat_gemv: hq_out [>= M, N]");
-    a.hq_out = reinterpret_cast<long long*>(hq_out->data_ptr<int64_t>());
-  } else {
-    TORCH_CHECK(false, "lat_gemv: epi 0 | 1 | 2");
-  }
-  if (stats.has_value()) {
-    need(*stats, at::kInt, "stats");
-    a.stats = stats->data_ptr<int>();
-  }
-  check(lsa_lat_gemv(&a, (int)src, (int)epi, (int)nb, (int)waves, (int)splitk, cur_stream()), "lat_gemv");
-}
-
 }  // namespace
 
 #ifndef LSA_BINDINGS_SELFTEST
@@ -956,8 +842,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("counters"), py::arg("xf_mt") = 0,
         py::arg("qkv_parts") = py::none(),
         py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4,
-        py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("part_only") = 0,
-        py::arg("out_s8") = py::none());
+        py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("out_s8") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
         py::arg("out"), py::arg("rows32") = 0);
@@ -975,16 +860,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     check(lsa_silu_parts(parts.data_ptr<float>(), S, parts.stride(0), M, F, out.data_ptr(), cur_stream()),
           "silu_parts");
   });
-  m.def("lat_embed", &lat_embed, py::arg("ids"), py::arg("emb"), py::arg("hq"), py::arg("ss"), py::arg("M"),
-        py::arg("ss_ld"), py::arg("nzero"));
-  m.def("lat_final_norm", &lat_final_norm, py::arg("hq"), py::arg("w"), py::arg("eps"), py::arg("xn"), py::arg("M"));
-  m.def("lat_gemv", &lat_gemv, py::arg("w"), py::arg("N"), py::arg("K"), py::arg("M"), py::arg("src"), py::arg("epi"),
-        py::arg("nb"), py::arg("waves"), py::arg("splitk"), py::arg("x") = py::none(), py::arg("hq") = py::none(),
-        py::arg("ss") = py::none(), py::arg("eps") = 1e-5, py::arg("timeout_ticks") = 3000,
-        py::arg("opart") = py::none(), py::arg("mlpart") = py::none(), py::arg("pos") = py::none(),
-        py::arg("nsplit") = 1, py::arg("chunk_blocks") = 1, py::arg("unsplit_max") = 0, py::arg("H") = 0,
-        py::arg("out") = py::none(), py::arg("act") = py::none(), py::arg("hq_out") = py::none(),
-        py::arg("stats") = py::none());
   m.def("ar_alloc", &ar_alloc);
   m.def("ar_free", [](int64_t p) { check(lsa_ar_free(reinterpret_cast<void*>(p)), "ar_free"); });
   m.def("ar_handle", &ar_handle);

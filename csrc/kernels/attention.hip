@@ -140,7 +140,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
                                                           int chunk_blocks, int nsplit, int unsplit_max,
                                                           uint16_t* __restrict__ out, float* __restrict__ opart, float* __restrict__ mlpart,
                                                           int* __restrict__ counters, int xf_mt, RopeArgs ra,
-                                                          int part_only, uint8_t* __restrict__ s8) {
+                                                          uint8_t* __restrict__ s8) {
   constexpr int D = 128;
   constexpr int NT = 64 * WV;      // threads
   constexpr int NLG = 4 * WV;      // 16-lane groups
@@ -512,7 +512,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
       O[0] += v.x * wgt; O[1] += v.y * wgt; O[2] += v.z * wgt; O[3] += v.w * wgt;
     }
     const int h = hk * G + g;
-    if (nse == 1 && !part_only) {
+    if (nse == 1) {
       const float inv = L > 0.f ? 1.f / L : 0.f;
       attn_store4(out, s8, xf_mt, b, H, h, d0, O[0] * inv, O[1] * inv, O[2] * inv, O[3] * inv);
     } else {
@@ -526,9 +526,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
                            __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  // part_only: every split (a single one too) leaves its (o, m, l) partial for the consumer -- the batch-<=4 latency
-  // path's o projection combines them in its prologue (decode_lat.hip), so no split waits on another here
-  if (nse == 1 || part_only) return;
+  if (nse == 1) return;
 
   // split-KV combine inside the launch: the last of this (sequence, kv-head)'s nse workgroups to arrive
   // merges all partials (guide §6 G16 counter form: sc1 stores drained -> barrier -> one relaxed agent
@@ -607,7 +605,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
                                int unsplit_max, void* out, float* opart, float* mlpart, int* counters, int xf_mt,
                                const float* qkv_parts, int nparts,
                                long part_stride, const float* cos_t, const float* sin_t, const float* ks,
-                               const float* vs, int part_only, void* out_s8, hipStream_t s) {
+                               const float* vs, void* out_s8, hipStream_t s) {
   if (H % Hkv) return -1;
   if (xf_mt && B > 16 * xf_mt) return -4;
   if (out_s8 && !xf_mt) return -6;  // the e4m3 output lives in the xf8 layout
@@ -625,7 +623,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
 #define LSA_ADL(GV, RP, WV, KV8, SB)                                                                              \
   hipLaunchKernelGGL((attn_decode_kernel<GV, RP, WV, KV8, SB>), grid, dim3(64 * (WV)), 0, s, qq, kk, vv, ks, vs,     \
                      block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart,  \
-                     counters, xf_mt, ra, part_only, reinterpret_cast<uint8_t*>(out_s8))
+                     counters, xf_mt, ra, reinterpret_cast<uint8_t*>(out_s8))
   // waves per workgroup: 8 for G = 1 (single-buffered at >= LSA_ATTN_SB_MIN_WG workgroups); for G = 2, 3 four on
   // grids of <= LSA_ATTN_SMALL23_WG workgroups (3B batch 1, 2k context: 11.34 -> 10.74 us -- half the cross-wave
   // merge, profiles/r3/attn_decode_wv23_ab_mi355x.jsonl) and eight above (3B batch 32: 10.54 vs 11.33 us); else 4

@@ -269,8 +269,7 @@ __device__ __forceinline__ f32x4_t res_slab_sum(__amdgpu_buffer_rsrc_t rs, size_
 // Per-sequence split of the decode-attention context (attention.hip; the grid is sized for the longest context a
 // captured graph can see; each sequence uses what its own length needs): <= unsplit_max blocks run unsplit (a split
 // costs a combine pass, measured slower below ~256 keys, scripts/bench_attn.py), longer contexts use splits of
-// chunk_blocks blocks, widened when the grid has fewer splits than that needs.  The consumer of part_only partials
-// (decode_lat.hip) recomputes the same split count from the position.
+// chunk_blocks blocks, widened when the grid has fewer splits than that needs.
 __device__ __forceinline__ void eff_split(int nblk, int chunk_blocks, int nsplit, int unsplit_max, int& ech, int& nse) {
   ech = nblk <= unsplit_max ? max(nblk, 1) : max(chunk_blocks, (nblk + nsplit - 1) / nsplit);
   nse = (nblk + ech - 1) / ech;

@@ -42,7 +42,7 @@ class ModelRunner:
                  num_kv_blocks: Optional[int] = None, kv_memory_fraction: float = 0.85,
                  max_new_cap: Optional[int] = None, tp=None, use_graphs: bool = True,
                  fuse_rope: Optional[bool] = None, seq_parallel: Optional[bool] = None, sp_min_tokens: Optional[int] = None,
-                 kv_dtype: Optional[str] = None, lat: Optional[bool] = None):
+                 kv_dtype: Optional[str] = None):
         self.w = weights
         # paged KV cache dtype: "bf16" or "fp8" (e4m3 rows with per-(token, kv-head) scales, ops.KV_FP8)
         kv_dtype = kv_dtype or ("fp8" if ops.KV_FP8 else "bf16")
@@ -206,17 +206,6 @@ class ModelRunner:
         # Under TP the residual add rides in the one-shot all-reduce (TPGroup.reduce_add: the sum over ranks, h +=,
         # bf16 / fragment-major xn and the row sums in one launch), so a TP layer issues as many launches as TP = 1.
         self.wide_norm = all(lw.norms_folded for lw in weights.layers)
-        # latency path for decode buckets of <= ops.LAT_MAX_B rows (csrc/kernels/decode_lat.hip): the residual stream as
-        # Q32 integer atomics, folded norms with in-kernel row sums, attention partials merged by the o projection --
-        # five launches per layer and no residual-add / combine round trips.  TP = 1, bf16 weights, folded norms.
-        kinds = ("bf16", "dense")
-        self.lat = ((lat if lat is not None else True) and tps == 1 and fuse_rope is not False
-                    and all(lw.norms_folded for lw in weights.layers)
-                    and all(p.kind in kinds for lw in weights.layers for p in (lw.wqkv, lw.wo, lw.w_gate_up, lw.w_down)))
-        self.lat_max_batch = min(ops.LAT_MAX_B, S)
-        self.hq = torch.zeros(ops.LAT_MAX_B, self.d, dtype=torch.int64, device=dev) if self.lat else None
-        self.lat_stats = torch.zeros(1, dtype=torch.int32, device=dev)  # row-sum polls that fell back (stay 0)
-        self.lat_ws = (ops.decode_workspace(ops.LAT_MAX_B, self.H, self.Hkv, self.max_blocks, dev) if self.lat else None)
         self.graphs: dict = {}
         self._pending_bt: dict = {}  # slot -> block-table row of a prompt still being prefilled in chunks
         if self.tp is not None and self.tp.size > 1 and self.on_gpu:
@@ -301,13 +290,9 @@ class ModelRunner:
         while tier < t:
             tier *= 2
         tier = min(tier, self.max_model_len)
-        if self.lat and B <= self.lat_max_batch:  # one 64-key block per split; every split leaves a partial
-            return (1, (tier + BLOCK - 1) // BLOCK, 0)
         return tuple(ops.decode_split_plan(B, self.Hkv, tier))
 
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
-        if self.lat and B <= self.lat_max_batch:
-            return self._decode_step_lat(B, sample, plan)
         a8, a8m, a8o, a8d = self.a8_plan(B)  # qkv / gate_up / o / down W8A8 (W4A8)
         if self.fused_norm and B <= self.fused_norm_max_batch and not (a8 or a8m or a8o):
             return self._decode_step_fused(B, sample, plan)
@@ -448,43 +433,6 @@ class ModelRunner:
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, rows=B, xf=xf, write_h=False)
         self._decode_tail(B, sample, xn, xf)
 
-    def _decode_step_lat(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
-        """Latency-path decode step (B <= ops.LAT_MAX_B, csrc/kernels/decode_lat.hip): 5 launches per layer.
-
-          embed -> Q32 residual hq (+ zeroed row-sum words)  ->  per layer:
-            qkv GEMV (hq -> bf16, row sums published in-kernel, rows RMS-scaled; f32 split-K slabs)
-            -> attn_decode (RoPE + KV append; every split leaves its partial)
-            -> o GEMV (prologue merges the partials of its head; hq += Q32 atomics)
-            -> gate_up GEMV (hq, row-scaled, SiLU * up -> bf16)  -> down GEMV (hq += Q32 atomics)
-          -> final RMSNorm of hq -> lm_head -> token commit
-        """
-        w, d, L = self.w, self.d, self.L
-        ids, pos, bt = self.input_ids[:B], self.positions[:B], self.block_tables[:B]
-        hq, ssq, S, eps = self.hq, self.ssq, self.max_slots, self.eps
-        nqkv = (self.H + 2 * self.Hkv) * self.D
-        plan = tuple(plan or self.ctx_plan(B))
-        cq = ops.lat_config("qkv", nqkv, d)
-        co = ops.lat_config("o", d, self.H * self.D, self.H)
-        cg = ops.lat_config("gate_up", 2 * self.ffn_l, d)
-        cd = ops.lat_config("down", d, self.ffn_l)
-        qkv_parts = self.qkv_buf[: cq[1] * B * nqkv].view(cq[1], B, nqkv)
-        opart, mlpart, _ = self.lat_ws
-        part = (opart, mlpart, pos, plan, self.H)
-        attn, act, st = self.attn[:B], self.act[:B], self.lat_stats
-        ops.lat_embed(ids, w.embed, hq, ssq, B, S, 2 * L)
-        for l, lw in enumerate(w.layers):
-            ops.lat_linear(lw.wqkv, B, "hq", "f32", cq[1], cq[0], cq[2], hq=hq, ss=ssq[2 * l], eps=eps,
-                           out=qkv_parts, stats=st)
-            ops.attn_decode(self.q[:B], self.kv[l, 0], self.kv[l, 1], bt, pos, self.H, self.Hkv, self.scale,
-                            attn.view(B, self.H, self.D), workspace=self.lat_ws, plan=plan, qkv_parts=qkv_parts,
-                            cos=self.cos, sin=self.sin, kv_scales=self._kv_scales(l), part_only=True)
-            ops.lat_linear(lw.wo, B, "part", "atom", co[1], co[0], co[2], part=part, attn_ref=attn, hq_out=hq)
-            ops.lat_linear(lw.w_gate_up, B, "hq", "silu", cg[1], cg[0], cg[2], hq=hq, ss=ssq[2 * l + 1], eps=eps,
-                           act=act, stats=st)
-            ops.lat_linear(lw.w_down, B, "act", "atom", cd[1], cd[0], cd[2], x=act, hq_out=hq)
-        ops.lat_final_norm(hq, w.final_norm, eps, self.xn, B)
-        self._decode_tail(B, sample, self.xn[:B], False)
-
     def _decode_tail(self, B: int, sample: bool, xn, xf: bool) -> None:
         logits = self._lm_head(xn, B, xf)
         st = (self.out_tokens[:B], self.gen_len[:B], self.input_ids[:B], self.positions[:B], self.finished[:B])
@@ -507,8 +455,6 @@ class ModelRunner:
     def step_xfrag(self, B: int) -> bool:
         """Whether the decode step of bucket B hands its activations on in the fragment-major layouts (use_xfrag,
         or -- any W8A8 / W4A8 projection -- the xf8 one, which forces it at any batch)."""
-        if self.lat and B <= self.lat_max_batch:
-            return False
         a8, a8m, a8o, _ = self.a8_plan(B)
         return self.use_xfrag(B) or a8 or a8m or a8o
 

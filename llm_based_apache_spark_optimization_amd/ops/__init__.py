@@ -750,114 +750,6 @@ def linear_a8(x8: torch.Tensor, sx: Optional[torch.Tensor], M: int, w: PackedWei
     return out
 
 
-# ----------------------------------------------------------------------------------- latency path (B <= 4)
-# csrc/kernels/decode_lat.hip: the batch-<=4 decode layer (BASELINE configs 2 and 3) with the residual stream as Q32
-# fixed point in int64 (x 2^32), row-parallel GEMVs that ADD into it with integer atomics, the next projection's
-# RMSNorm folded (gamma in the weights, row scale from in-kernel row sums of squares), and the o projection merging
-# the decode attention's split partials in its prologue.
-LAT_MAX_B = 4
-LAT_SRC = {"act": 0, "hq": 1, "part": 2}
-LAT_EPI = {"f32": 0, "silu": 1, "atom": 2}
-Q32 = float(1 << 32)
-
-
-# (nb, splitk, waves) per (projection, N, K) measured on MI355X (scripts/bench_lat.py); the heuristic below otherwise
-LAT_TUNING: dict = {}
-
-
-def lat_config(proj: str, N: int, K: int, H: int = 0) -> tuple[int, int, int]:
-    """(nb, splitk, waves) of a latency-path GEMV.  proj: 'qkv' | 'o' | 'gate_up' | 'down'.  The o projection splits K
-    by whole heads (its prologue merges each head's attention partials); gate_up cannot split K (SiLU of the sum)."""
-    e = LAT_TUNING.get(f"{proj}:{N}x{K}")
-    if e is not None:
-        return tuple(e)
-    nbt = N // 16
-    if proj == "o":
-        nb = 8 if nbt % 8 == 0 else (4 if nbt % 4 == 0 else 2)
-        return nb, H, 4
-    if proj == "gate_up":
-        return 2, 1, 4
-    nb = 2 if nbt >= 512 and nbt % 2 == 0 else 1
-    sk = 1
-    while (nbt // nb) * sk < 512 and sk < 8 and K // 32 // (sk * 2) >= 8:
-        sk *= 2
-    return nb, sk, 4
-
-
-def to_q32(v: torch.Tensor) -> torch.Tensor:
-    return (v.float() * Q32).to(torch.int64)  # truncating, like the device conversion
-
-
-def from_q32(q: torch.Tensor) -> torch.Tensor:
-    return (q.double() / Q32).float()
-
-
-def lat_embed(ids: torch.Tensor, emb: torch.Tensor, hq: torch.Tensor, ss: torch.Tensor, M: int, ss_ld: int,
-              nzero: int) -> None:
-    """hq[:M] = Q32(emb[ids[:M]]); ss words [k * ss_ld + m] (k < nzero, m < M) zeroed (the step's row-sum publishers)."""
-    if not _gpu(hq):
-        hq[:M].copy_(to_q32(emb[ids[:M].long()].float()))
-        sv = ss.view(-1)
-        for k in range(nzero):
-            sv[k * ss_ld: k * ss_ld + M] = 0
-        return
-    ext().lat_embed(ids, emb, hq, ss, M, ss_ld, nzero)
-
-
-def lat_final_norm(hq: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor, M: int) -> torch.Tensor:
-    """xn[:M] = bf16(rmsnorm(h) * w) of the Q32 stream (the lm_head input)."""
-    if not _gpu(hq):
-        h = from_q32(hq[:M])
-        xn[:M].copy_((h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + eps) * w.float()).to(xn.dtype))
-        return xn
-    ext().lat_final_norm(hq, w, eps, xn, M)
-    return xn
-
-
-def lat_linear(w: "PackedWeight", M: int, src: str, epi: str, splitk: int = 1, nb: int = 1, waves: int = 4, *,
-               x: Optional[torch.Tensor] = None, hq: Optional[torch.Tensor] = None, ss: Optional[torch.Tensor] = None,
-               eps: float = 1e-5, part=None, attn_ref: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-               act: Optional[torch.Tensor] = None, hq_out: Optional[torch.Tensor] = None,
-               stats: Optional[torch.Tensor] = None, timeout_ticks: int = 3000) -> None:
-    """One latency-path GEMV (decode_lat.hip), M <= 4 rows, bf16 weights.
-
-    src 'act': x [M, K] bf16; 'hq': the Q32 stream hq [M, K] -- its rows are RMS-scaled in the epilogue from their
-    sums of squares, published through the per-row words ``ss`` (zeroed by ``lat_embed``); 'part': the attention
-    partials part = (opart, mlpart, pos, (chunk_blocks, nsplit, unsplit_max), H) of ``attn_decode(part_only=True)``
-    (on the CPU ``attn_ref``, the finished attention rows, stands in for them).
-    epi 'f32': out [splitk, M, N] slabs (rows scaled); 'silu': act [M, N/2] bf16 = silu(gate) * up; 'atom': hq_out
-    [M, N] += Q32(y) (integer adds: order-independent)."""
-    N, K = w.N, w.K
-    if not _gpu(w.data):
-        if src == "hq":
-            xf = from_q32(hq[:M])
-            xin = xf.to(torch.bfloat16)
-        elif src == "part":
-            xin = attn_ref[:M].reshape(M, K).to(torch.bfloat16)
-        else:
-            xin = x[:M].to(torch.bfloat16)
-        y = xin.float() @ w.dense().float().t()
-        if src == "hq":
-            y = y * torch.rsqrt(xf.pow(2).sum(1, keepdim=True) / K + eps)
-        if epi == "f32":
-            o = out.view(-1)[: splitk * M * N].view(splitk, M, N)
-            o.zero_()
-            o[0].copy_(y)
-        elif epi == "silu":
-            y3 = y.view(M, N // 32, 2, 16)
-            act[:M].copy_((torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(M, N // 2).to(act.dtype))
-        else:
-            hq_out[:M] += to_q32(y)
-        return
-    assert w.kind == "bf16", "latency path: bf16 weights"
-    kw = {}
-    if part is not None:
-        opart, mlpart, pos, plan, H = part
-        kw = dict(opart=opart, mlpart=mlpart, pos=pos, chunk_blocks=plan[0], nsplit=plan[1], unsplit_max=plan[2], H=H)
-    ext().lat_gemv(w.data, N, K, M, LAT_SRC[src], LAT_EPI[epi], nb, waves, splitk, x=x, hq=hq, ss=ss, eps=eps,
-                   timeout_ticks=timeout_ticks, out=out, act=act, hq_out=hq_out, stats=stats, **kw)
-
-
 # ----------------------------------------------------------------------------------- norms / rope
 def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
                 parts: Optional[torch.Tensor] = None, ids: Optional[torch.Tensor] = None,
@@ -1022,14 +914,12 @@ def decode_workspace(B: int, H: int, Hkv: int, nsplit: int, device) -> tuple:
 
 
 def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None, xf=False,
-                qkv_parts=None, cos=None, sin=None, kv_scales=None, part_only=False, out_s8=None):
+                qkv_parts=None, cos=None, sin=None, kv_scales=None, out_s8=None):
     """q [B,H,128] vs paged cache, context = pos + 1.  workspace = decode_workspace(...) for split-KV.
     xf=True: out is a flat buffer receiving the fragment-major layout of the [B, H*128] output.
     qkv_parts ([S, B, (H+2Hkv)*128] f32 split-K slabs of the QKV projection) + cos/sin: RoPE and the
     KV-cache append of the new token are fused in (``q`` is then only a [B, H, 128] scratch buffer).
     kv_scales = (ks, vs): fp8 cache (see ``KV_FP8``).
-    part_only: every split leaves its (o, m, l) partial in the workspace and nothing is combined (the latency path's o
-    projection merges them, ``lat_linear(src='part')``); on the CPU the finished rows still land in ``out``.
     out_s8 (xf only): ``out`` is a uint8 buffer receiving the output as e4m3 in the xf8 layout with one E8M0 scale
     per (row, head) in ``out_s8`` -- the input of a W8A8 / W4A8 o projection (``linear_a8(s8=)``)."""
     B = pos.shape[0]
@@ -1057,8 +947,7 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     opart, mlpart, counters = workspace
     ks, vs = kv_scales if kv_scales is not None else (None, None)
     ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart, counters,
-                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs, 1 if part_only else 0,
-                      out_s8)
+                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs, out_s8=out_s8)
     return out
 
 
