@@ -91,8 +91,8 @@ for name, (N, K, epi, scal) in SHAPES.items():
                         continue
                     if M > 32 and nb > 2 and not (epi == "silu8" and nb == 4):
                         continue
-                    if nb >= 6 and (waves != 4 or depth != 1 or M > 32):
-                        continue
+                    if nb >= 6 and (waves != 4 or depth != 1 or M > 32 or (nb == 6 and M <= 16)):
+                        continue  # (nb 6 is instantiated for the two-row-tile kernels only)
                     for sk in ((1, 2, 4, 8) if epi == "f32" else (1,)):
                         kb = K // 128
                         kbps = (kb + sk - 1) // sk
