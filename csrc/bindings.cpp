@@ -61,8 +61,6 @@ int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, vo
                  int waves, int div, int xlds, hipStream_t stream);
 int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
-int lsa_gemm_w4(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int splitk, int ring,
-                hipStream_t stream);
 int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int splitk,
                   hipStream_t stream);
 int lsa_gemm_t256x(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int xf_tiles,
@@ -339,28 +337,6 @@ void gemm_t256(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor&
   }
   check(lsa_gemm_t256(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, (int)splitk, cur_stream()),
         "gemm_t256");
-}
-
-// large-M (prefill) linear layer on the 4-wave 256x256 tile kernel (kernels/gemm_w4.hip); ring = LDS slices (4 | 5)
-void gemm_w4(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, int64_t splitk,
-             int64_t ring) {
-  need(x, at::kBFloat16, "x");
-  need(wf, at::kBFloat16, "wf");
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
-  const int M = x.size(0), K = x.size(1);
-  TORCH_CHECK(wf.numel() == N * K, "weight numel mismatch");
-  TORCH_CHECK(splitk >= 1 && (splitk == 1 || epi == 1), "gemm_w4: only the f32 epilogue splits K");
-  TORCH_CHECK(ring == 4 || ring == 5, "gemm_w4: ring 4 | 5");
-  if (epi == 1) {
-    need(out, at::kFloat, "out");
-    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small for the slabs");
-  } else {
-    need(out, at::kBFloat16, "out");
-    TORCH_CHECK(out.numel() >= M * (epi == 2 ? N / 2 : N), "bf16 out too small");
-  }
-  check(lsa_gemm_w4(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, (int)splitk, (int)ring,
-                    cur_stream()),
-        "gemm_w4");
 }
 
 // the 256^2 tile GEMM over fragment-major X (xf: [K / 32][xf_tiles][64][8] bf16, rows >= M zero or ignored)
@@ -826,8 +802,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_t256", &gemm_t256, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"),
         py::arg("splitk") = 1);
-  m.def("gemm_w4", &gemm_w4, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"),
-        py::arg("splitk") = 1, py::arg("ring") = 5);
   m.def("fp4_gemm", &fp4_gemm, py::arg("x"), py::arg("wq"), py::arg("sw"), py::arg("N"), py::arg("out"), py::arg("epi"),
         py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("rowss") = py::none(), py::arg("eps") = 1e-5,
         py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(),

@@ -91,13 +91,6 @@ int main() {
   }
   {
     auto xf = T({16 * 128}, BF), wq = T({64 * 128}, U8), sc = T({64}, F32), o = T({1, 4, 64}, F32);
-    {
-      auto xw = T({300, 128}, BF), wfw = T({64 * 128}, BF), ow = T({300, 64}, BF), ow32 = T({2, 300, 64}, F32);
-      expect_ok("gemm_w4", [&] { gemm_w4(xw, wfw, 64, ow, 0, 1, 5); });
-      expect_ok("gemm_w4 split-K", [&] { gemm_w4(xw, wfw, 64, ow32, 1, 2, 4); });
-      expect_reject("gemm_w4 ring", [&] { gemm_w4(xw, wfw, 64, ow, 0, 1, 3); });
-      expect_reject("gemm_w4 bf16 split", [&] { gemm_w4(xw, wfw, 64, ow, 0, 2, 5); });
-    }
     expect_ok("fp8_gemm_xf", [&] { fp8_gemm_xf(xf, 4, 128, wq, sc, 64, o, 1, 1, 1, 4, 1, none, 1e-5, none, none, 0, none, none); });
     auto wq_bad = T({64 * 127}, U8);
     expect_reject("fp8_gemm_xf wq numel", [&] { fp8_gemm_xf(xf, 4, 128, wq_bad, sc, 64, o, 1, 1, 1, 4, 1, none, 1e-5, none, none, 0, none, none); });

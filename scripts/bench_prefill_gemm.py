@@ -1,5 +1,4 @@
-"""Prefill GEMM on MI355X: 128^2 tile kernel vs 256^2 tile kernels (8-wave gemm_tile256, 4-wave gemm_w4 with a 4 / 5
-slice LDS ring) vs hipBLASLt (torch.matmul) at the
+"""Prefill GEMM on MI355X: 128^2 tile kernel vs 256^2 tile kernel vs hipBLASLt (torch.matmul) at the
 prefill shapes of the BASELINE configs (7B: 32 x 128-token prompts = 4096 rows; 3B: one 2k prompt),
 plus a square 8192^3 reference.  Random operands (TF/s on zero-filled data reads high).  Checks each
 kernel against an fp32 product first."""
@@ -57,9 +56,7 @@ for name, (M, N, K, epi) in shapes.items():
     xf = xp.view(mtt, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).contiguous().view(-1)
     for kname, fn in (("tile128", lambda: e.gemm(x, pw.data, N, out, EPI[epi], 1, 1, 4, 4, 0)),
                       ("tile256", lambda: e.gemm_t256(x, pw.data, N, out, EPI[epi])),
-                      ("tile256_xf", lambda: e.gemm_t256_xf(xf, mtt, M, pw.data, N, out, EPI[epi])),
-                      ("w4_r5", lambda: e.gemm_w4(x, pw.data, N, out, EPI[epi], 1, 5)),
-                      ("w4_r4", lambda: e.gemm_w4(x, pw.data, N, out, EPI[epi], 1, 4))):
+                      ("tile256_xf", lambda: e.gemm_t256_xf(xf, mtt, M, pw.data, N, out, EPI[epi]))):
         fn()
         torch.cuda.synchronize()
         err = ((out.float() - ref).norm() / ref.norm()).item()

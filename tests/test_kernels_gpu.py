@@ -193,33 +193,6 @@ def test_gemm_tile256(gpu, M, NK, epi):
     assert _rel(out, yr) < (1e-5 if epi == "f32" else 1e-2)
 
 
-@pytest.mark.parametrize("M", [65, 300, 777, 2048])
-@pytest.mark.parametrize("NK", [(800, 4096), (1024, 1376), (4096, 512), (256, 96)])
-@pytest.mark.parametrize("epi", ["bf16", "f32", "silu"])
-def test_gemm_w4(gpu, M, NK, epi):
-    """4-wave 256^2 prefill kernel (gemm_w4.hip, 4 / 5 slice LDS rings): M / N edges (partial row / n-block tiles),
-    K of 3 k-steps (shorter than the ring) to 128, every epilogue, and split-K f32 slabs (every slab written) vs fp32."""
-    N, K = NK
-    torch.manual_seed(M + N + K + 1)
-    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
-    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
-    pw = ops.PackedWeight.from_dense(w)
-    ncol = N // 2 if epi == "silu" else N
-    yr = x.float() @ w.float().t()
-    if epi == "silu":
-        r3 = yr.view(M, N // 32, 2, 16)
-        yr = (torch.nn.functional.silu(r3[:, :, 0]) * r3[:, :, 1]).reshape(M, N // 2)
-    for ring in (4, 5):
-        out = torch.empty(M, ncol, device=gpu, dtype=torch.float32 if epi == "f32" else torch.bfloat16)
-        ops.ext().gemm_w4(x, pw.data, N, out, ops.EPI[epi], 1, ring)
-        assert _rel(out, yr) < (1e-5 if epi == "f32" else 1e-2), ring
-    if epi == "f32" and K >= 512:
-        for sk in (2, 3):
-            out = torch.full((sk, M, N), float("nan"), device=gpu)
-            ops.ext().gemm_w4(x, pw.data, N, out, 1, sk, 5)
-            assert not torch.isnan(out).any() and _rel(out.sum(0), yr) < 1e-4, sk
-
-
 def test_gemm_asymmetric_exact(gpu):
     """Small-integer operands: the result is exact, so any lane/row/col map error shows up."""
     M, N, K = 7, 48, 64
