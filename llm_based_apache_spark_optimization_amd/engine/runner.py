@@ -147,17 +147,20 @@ class ModelRunner:
         self.a8 = (ops.FP8_A8_DECODE and self.on_gpu and wkind in ("fp8", "mxfp4") and self.d % 128 == 0)
         # the down projection W8A8 needs whole 32-column blocks per SiLU workgroup (gate_up n-blocks % 4 == 0)
         self.a8_down_ok = self.ffn_l % 128 == 0 and (2 * self.ffn_l // 16) % 4 == 0
-        # fp8: qkv W8A8 for buckets above this batch: at 64 rows the fp8-activation GEMM is 27-30 % faster than
-        # W8A16 (7B qkv 22.0 -> 16.1 us, gate_up 33.4 -> 23.5), at 32 rows it ties on qkv and the 7B b32 bench
-        # did not move (10425 vs 10357 tok/s) while the e4m3 activations cost top-1 agreement
-        # (profiles/bench_fp8a_decode_mi355x.jsonl); MXFP4: every bucket (the W4A16 kernel widens each e2m1 weight
-        # on the VALU -- README: its gate_up streams ~3.1 TB/s)
-        self.a8_min_batch = 32 if wkind == "fp8" else 0
-        # ... the gate_up (and with it the down) projection from 17 rows: at 32 rows it is 13 % faster than W8A16
-        # (7B 22.8 -> 19.8 us, profiles/bench_fp8a_decode_mi355x.jsonl) where the qkv one ties
-        self.a8_mlp_min_batch = 16 if wkind == "fp8" else 0
-        # ... and the o projection from the same batch
-        self.a8_o_min_batch = 16 if wkind == "fp8" else 0
+        # Which projections take e4m3 activations, per weight format and bucket (standalone sweeps with weights
+        # streaming from HBM: profiles/r4/bench_a8_decode_{fp8,mxfp4}_mi355x.jsonl, scripts/bench_a8_decode.py):
+        #   qkv: fp8 above 32 rows -- at 32 the W8A8 GEMM ties / loses to W8A16 (7B 13.3 vs 12.4 us) and the 7B b32
+        #        bench did not move while the e4m3 activations cost top-1 agreement (profiles/bench_fp8a_decode_mi355x.jsonl);
+        #        MXFP4 at every bucket (7B 8.0 vs 10.2 us at 1 row, 9.4 vs 11.9 at 32: no VALU e2m1 widening);
+        #   gate_up: fp8 from 17 rows (7B 19.0 vs 22.7 us at 32), MXFP4 at every bucket (11.2 vs 15.7, 13.0 vs 15.5);
+        #   o and down: only where it pays -- MXFP4 up to 16 rows (7B o 6.1 vs 10.0 us, down 7.9 vs 10.0 at 1 row); at 32
+        #        rows they tie or lose (o 6.3 vs 6.1, down 9.6 vs 10.5 but the e4m3 SiLU output it needs costs gate_up
+        #        15.3 vs 13.0 us), and fp8 never gains (7B b32 step 2.80 vs 2.60 ms with them,
+        #        profiles/r4/rocprof_fp8_b32_a8all_summary.txt)
+        mx = wkind == "mxfp4"
+        self.a8_min_batch = 0 if mx else 32
+        self.a8_mlp_min_batch = 0 if mx else 16
+        self.a8_od_max_batch = 16 if mx else 0  # o / down W8A8 (W4A8) up to this bucket
         self.x8 = torch.zeros(xr * self.d if self.a8 else 1, dtype=torch.uint8, device=dev)
         self.sx8 = torch.ones(max(S, 64), **f32)
         mt64 = ops.xfrag_tiles(min(S, 64))
@@ -247,8 +250,8 @@ class ModelRunner:
         """Which decode projections run W8A8 / W4A8 (e4m3 activations) at bucket B: (qkv, gate_up, o, down)."""
         if not self.a8 or B > 64:
             return (False, False, False, False)
-        qkv, gu, o = B > self.a8_min_batch, B > self.a8_mlp_min_batch, B > self.a8_o_min_batch
-        return (qkv, gu, o, gu and self.a8_down_ok)
+        qkv, gu, od = B > self.a8_min_batch, B > self.a8_mlp_min_batch, B <= self.a8_od_max_batch
+        return (qkv, gu, od, gu and od and self.a8_down_ok)
 
     def use_xfrag(self, B: int) -> bool:
         """Fragment-major activations pay off once a decode batch spans >1 row tile (B > 16):
