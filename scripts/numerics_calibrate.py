@@ -5,6 +5,8 @@ the two injected faults (one layer's down scale x1.25, swapped cached keys) per 
     python scripts/numerics_calibrate.py [n_layers ...]      (GPU; default 4 32)
     python scripts/numerics_calibrate.py --tied [n_layers ...]   Llama-3.2-3B shape (tied head: probe statistics;
                                                                   default 4 28, batch 1 and 4)
+    --dtypes mxfp4,fp8 ...   weight formats to run (default bf16, fp8, fp8 + fp8 KV); MXFP4's scale fault is a wrong
+                             E8M0 block scale (eval/numerics.py e8m0_fault)
 """
 import dataclasses
 import json
@@ -29,11 +31,16 @@ def main():
     args = sys.argv[1:]
     tied = "--tied" in args
     args = [a for a in args if a != "--tied"]
+    combos = (("bf16", "bf16"), ("fp8", "bf16"), ("fp8", "fp8"))
+    if "--dtypes" in args:
+        i = args.index("--dtypes")
+        combos = tuple((d, "bf16") for d in args[i + 1].split(","))
+        args = args[:i] + args[i + 2:]
     layers = [int(v) for v in args] or ([4, 28] if tied else [4, 32])
     model = "llama3.2" if tied else "duckdb-nsql"
     for nl in layers:
         spec = dataclasses.replace(get_spec(model), n_layers=nl, name=f"{model}-{nl}l")
-        for dtype, kv in (("bf16", "bf16"), ("fp8", "bf16"), ("fp8", "fp8")):
+        for dtype, kv in combos:
             for B in ((1, 4) if tied else (4, 32)):
                 w = init_random(spec, dev, seed=5, kind=dtype)
                 r = ModelRunner(w, max_slots=32, max_model_len=512, use_graphs=True, num_kv_blocks=32 * 8 + 1,
