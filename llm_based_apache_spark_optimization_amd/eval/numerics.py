@@ -37,10 +37,17 @@ import torch
 # random-init network; the fp8 bounds sit 1.6-2.8x above the worst healthy row and 1.6-2.7x below the scale
 # fault (bf16: ~10x above, ~19x below).
 # Top-5 / top-1 floors are gross-failure guards (at 32 random layers healthy fp8 top-1 is only ~0.4-0.7).
+#   w4a8    1.6e-3 .. 3.3e-3         1.2e-2 .. 1.8e-2 (E8M0 fault)         1.7e-2 .. 4.9e-2
+# w4a8 = MXFP4 weights with e4m3 activations on the W4A8 projections (ModelRunner.a8_plan): the oracle multiplies
+# the dequantised e2m1 weights, so the healthy noise is the activation rounding of every W4A8 input (qkv / gate_up
+# per row, o / down per 32-block up to 16 rows); its scale fault is every 8th E8M0 block scale of one layer's down
+# projection one binade up (e8m0_fault).  Calibrated in round 4 (profiles/r4/numerics_calibration_w4a8_mi355x.jsonl):
+# the bound sits 1.8x above the worst healthy row and 2x below the weakest fault.
 THRESHOLDS = {
     "bf16": (2.5e-4, 0.85, 0.8),
     "w8a16": (2.0e-3, 0.5, 0.4),
     "w8a8": (3.5e-3, 0.4, 0.3),
+    "w4a8": (6.0e-3, 0.35, 0.25),
 }
 
 # Tied-embedding models (Llama-3.2-3B: lm_head = the embedding table).  With random-init weights the final hidden
@@ -59,10 +66,12 @@ THRESHOLDS = {
 #   bf16    8.5e-5 .. 9.6e-5, 0.0035 .. 0.0038   2.5e-2 .. 4.2e-2, 0.064 .. 0.075         6.9e-2 .., 0.10 ..
 #   w8a16   9.9e-4 .. 2.2e-3, 0.011 .. 0.018     2.8e-2 .. 4.5e-2, 0.066 .. 0.076         7.0e-2 .., 0.10 ..
 #   w8a8    1.2e-3 .. 2.8e-3, 0.014 .. 0.020     2.8e-2 .. 5.0e-2, 0.066 .. 0.076         1.1e-1 .., 0.12 ..
+#   w4a8    1.1e-2 .. 1.7e-2, 0.043 .. 0.046     6.2e-2 .. 0.11, 0.100 .. 0.133 (E8M0)    7.3e-2 .., 0.10 ..
 TIED_THRESHOLDS = {
     "bf16": (4e-4, 0.012),
     "w8a16": (6e-3, 0.035),
     "w8a8": (7e-3, 0.038),
+    "w4a8": (3e-2, 0.07),
 }
 PROBE_V, PROBE_SCALE, PROBE_SEED = 8192, 4.0, 1234
 
@@ -134,7 +143,7 @@ def numerics_class(runner, decode_batch: int) -> str:
     """Which threshold row applies to the decode path at ``decode_batch`` (see engine/runner.py)."""
     a8 = any(runner.a8_plan(decode_batch))
     if runner.w.layers[0].wqkv.kind != "fp8":
-        return "w8a8" if a8 else "bf16"  # MXFP4: the oracle multiplies its dequantised weights; W4A8 rounds activations
+        return "w4a8" if a8 else "bf16"  # MXFP4: the oracle multiplies its dequantised weights; W4A8 rounds activations
     return "w8a8" if a8 or runner.kv_fp8 else "w8a16"
 
 

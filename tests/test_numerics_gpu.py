@@ -51,7 +51,7 @@ def test_numerics_check_passes_and_catches_faults(gpu, dtype, kv, model, B):
     good = _check(eng, B)
     assert good["ok"] and good["tokens_checked"] >= 64, good
     if dtype == "mxfp4":  # qkv / gate_up run W4A8 at every bucket, o / down up to 16 rows (ModelRunner.a8_plan)
-        assert eng.runner.a8_plan(B) == (True, True, B <= 16, B <= 16) and good["class"] == "w8a8", good
+        assert eng.runner.a8_plan(B) == (True, True, B <= 16, B <= 16) and good["class"] == "w4a8", good
     if spec is SPEC3B:  # the tied head's own KL is degenerate (~0): the probe statistic must not be
         assert good["tied_head"] and good["probe_kl"] > 0, good
 
