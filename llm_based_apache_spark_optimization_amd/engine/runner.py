@@ -791,7 +791,7 @@ class ModelRunner:
     def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T):
         kc, vc = self.kv[l, 0], self.kv[l, 1]
         kvs = self._kv_scales(l)
-        sk_q = self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D)
+        sk_q = 1 if ops.uses_blas(lw.wqkv, T) else self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D)
         if sk_q > 1:  # small tile grid: f32 split-K slabs, summed by rope_append while it rotates
             parts = ops.linear(xn, lw.wqkv, "f32", splitk=sk_q)
             ops.rope_append(parts, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)

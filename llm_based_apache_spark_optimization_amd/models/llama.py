@@ -97,8 +97,11 @@ def pack_layer(spec: ModelSpec, wq, wk, wv, wo, wg, wu, wd, an, mn, rank=0, tp=1
         gu = (gu.float() * mn.float()[None, :]).to(torch.bfloat16)
         an, mn = torch.ones_like(an), torch.ones_like(mn)
     P = ops.PackedWeight.from_dense
-    return LayerWeights(P(wqkv.contiguous(), kind), P(wo_s.contiguous(), kind), P(gu.contiguous(), kind),
-                        P(wd_s.contiguous(), kind), an.contiguous(), mn.contiguous(), norms_folded=FOLD_NORMS)
+    # qkv / o / down also keep a row-major copy for the vendor prefill GEMM (ops.PREFILL_BLAS); gate_up's fused SiLU
+    # prefill stays on the 256^2 kernel
+    return LayerWeights(P(wqkv.contiguous(), kind, rowmajor=True), P(wo_s.contiguous(), kind, rowmajor=True),
+                        P(gu.contiguous(), kind), P(wd_s.contiguous(), kind, rowmajor=True), an.contiguous(),
+                        mn.contiguous(), norms_folded=FOLD_NORMS)
 
 
 def init_random(spec: ModelSpec, device="cpu", seed: int = 0, kind: str = "bf16", std: float = 0.02,

@@ -161,9 +161,12 @@ class PackedWeight:
     kind: str  # "dense" (CPU reference) | "bf16" (fragment layout) | "fp8" | "mxfp4"
     data: torch.Tensor
     scale: Optional[torch.Tensor] = None
+    rm: Optional[torch.Tensor] = None  # bf16 weights only: a row-major [N, K] copy for the vendor prefill GEMM
 
     @staticmethod
-    def from_dense(w: torch.Tensor, kind: str = "bf16") -> "PackedWeight":
+    def from_dense(w: torch.Tensor, kind: str = "bf16", rowmajor: bool = False) -> "PackedWeight":
+        """``rowmajor`` (bf16 on the GPU, with ``PREFILL_BLAS``): also keep the row-major copy the plain prefill GEMMs
+        hand to hipBLASLt (``linear``)."""
         N, K = w.shape
         if not w.is_cuda:
             return PackedWeight(N, K, "dense", w.to(torch.bfloat16).contiguous())
@@ -173,7 +176,9 @@ class PackedWeight:
         if kind == "mxfp4":
             wq, sw = pack_mxfp4(*quantize_mxfp4(w))
             return PackedWeight(N, K, "mxfp4", wq, sw)
-        return PackedWeight(N, K, "bf16", shuffle_weight(w.to(torch.bfloat16)))
+        wb = w.to(torch.bfloat16)
+        return PackedWeight(N, K, "bf16", shuffle_weight(wb),
+                            rm=wb.contiguous().clone() if (rowmajor and PREFILL_BLAS) else None)
 
     def dense(self) -> torch.Tensor:
         if self.kind == "dense":
@@ -187,7 +192,8 @@ class PackedWeight:
     @property
     def nbytes(self) -> int:
         return self.data.numel() * self.data.element_size() + (
-            self.scale.numel() * self.scale.element_size() if self.scale is not None else 0)
+            self.scale.numel() * self.scale.element_size() if self.scale is not None else 0) + (
+            self.rm.numel() * self.rm.element_size() if self.rm is not None else 0)
 
 
 def pick_nb_splitk(M: int, N: int, K: int, epi: str) -> tuple[int, int]:
@@ -372,6 +378,33 @@ def _epi_ref(y: torch.Tensor, M: int, K: int, epi: str, rownorm, res, xf: bool):
     ss_out[:M] += ss_q24(hn.pow(2).sum(1))
 
 
+# Plain prefill projections (M > 64, bf16 weights, the bf16 / f32-slab epilogues: qkv, o, down) run on the vendor
+# library -- hipBLASLt through torch.mm, from a row-major copy of the weight made at load time (+ the qkv / o / down
+# bytes of HBM: 7.2 GB for the 7B, 2.8 GB for the 3B).  Measured against the hand-written 256^2 kernel
+# (profiles/r3/prefill_gemm_vs_hipblaslt_head_mi355x.jsonl, profiles/r4/prefill_gemm_*): the library's stream-K
+# kernels win every plain shape (7B qkv 1.37 vs 1.21 PF, o 1.45 vs 1.17, down 1.53 vs 1.22, 3B down 1.06 vs 0.62,
+# M = 300 0.71 vs 0.34).  The fused SiLU gate_up, the decode GEMMs and the quantised formats stay on this package's
+# kernels.
+PREFILL_BLAS = True
+
+
+def uses_blas(w: "PackedWeight", M: int) -> bool:
+    return PREFILL_BLAS and M > 64 and w.rm is not None
+
+
+def _blas_linear(x: torch.Tensor, w: PackedWeight, epi: str, out: Optional[torch.Tensor]) -> torch.Tensor:
+    M = x.shape[0]
+    if epi == "bf16":
+        o = out.view(-1)[: M * w.N].view(M, w.N) if out is not None else torch.empty(M, w.N, device=x.device,
+                                                                                   dtype=torch.bfloat16)
+        torch.mm(x, w.rm.t(), out=o)
+        return o
+    o = out.view(-1)[: M * w.N].view(1, M, w.N) if out is not None else torch.empty(1, M, w.N, device=x.device,
+                                                                                   dtype=torch.float32)
+    torch.mm(x, w.rm.t(), out_dtype=torch.float32, out=o[0])
+    return o
+
+
 def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
            splitk: Optional[int] = None, nb: Optional[int] = None, waves: Optional[int] = None,
            div: Optional[int] = None, rownorm=None, res=None, _xf: bool = False) -> torch.Tensor:
@@ -393,6 +426,8 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
             out.view(-1)[: y.numel()].copy_(y.reshape(-1))
             return out
         return y
+    if epi in ("bf16", "f32") and uses_blas(w, M) and rownorm is None:
+        return _blas_linear(x, w, epi, out)  # one f32 slab whatever splitk asked for
     nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi, kind=w.kind)
     nb = nb0 if nb is None else nb
     if M > 64:  # prefill tile kernels: split-K (f32 slabs) only where the tile grid is small

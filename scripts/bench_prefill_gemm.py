@@ -65,6 +65,9 @@ for name, (M, N, K, epi) in shapes.items():
     wt = w.t()
     us = timeit(lambda: torch.matmul(x, wt))
     res["hipblaslt"] = {"us": round(us, 1), "TF": round(flops / us / 1e6, 1)}
+    o32 = torch.empty(M, N, device=dev, dtype=torch.float32)
+    us = timeit(lambda: torch.mm(x, wt, out_dtype=torch.float32, out=o32))
+    res["hipblaslt_f32out"] = {"us": round(us, 1), "TF": round(flops / us / 1e6, 1)}
     print(json.dumps(res), flush=True)
     del x, w, pw, out, ref
     torch.cuda.empty_cache()
