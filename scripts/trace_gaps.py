@@ -51,14 +51,27 @@ if idle:
         by[k] = (c + 1, s + g)
     for (a, b), (c, s) in sorted(by.items(), key=lambda kv: -kv[1][1])[:12]:
         print(f"  {c:4d} x {s / c:9.1f} us  after {a}  before {b}")
-# prefill segments: runs of tile-GEMM / prefill-attention kernels (M > 64 paths) between decode runs
+# prefill segments: from the first prefill kernel (tile GEMM, vendor GEMM, prefill attention, rope/append) to the
+# commit kernel that ends the prefill; kernel-busy = every kernel in that window; per-kernel totals of the median one
+PRE = ("t256", "prefill", "rope_append", "Cijk")
 seg, segs = [], []
 for r in rows:
-    if "t256" in r[2] or "prefill" in r[2] or "rope_append" in r[2]:
+    if seg or any(p in r[2] for p in PRE):
         seg.append(r)
-    elif seg and "commit_kernel" in r[2]:
-        segs.append((seg[0][0], r[1], sum(e - s for s, e, _ in seg)))
-        seg = []
+        if "commit_kernel" in r[2]:
+            segs.append(seg)
+            seg = []
 if segs:
-    print(f"prefill segments {len(segs)}: span median {statistics.median([(b - a) / 1e3 for a, b, _ in segs]):.0f} us, "
-          f"tile/attention kernel time median {statistics.median([k / 1e3 for _, _, k in segs]):.0f} us")
+    spans = sorted(((s[-1][1] - s[0][0]) / 1e3, i) for i, s in enumerate(segs))
+    med_span, mi = spans[len(spans) // 2]
+    ms = segs[mi]
+    busy = sum(e - s for s, e, _ in ms) / 1e3
+    print(f"prefill segments {len(segs)}: median span {med_span:.0f} us, its kernel time {busy:.0f} us "
+          f"({len(ms)} kernels, {med_span - busy:.0f} us idle)")
+    by = {}
+    for s, e, n in ms:
+        k = n[:60]
+        c, t = by.get(k, (0, 0.0))
+        by[k] = (c + 1, t + (e - s) / 1e3)
+    for k, (c, t) in sorted(by.items(), key=lambda kv: -kv[1][1])[:14]:
+        print(f"  {t:8.1f} us  {c:4d} x {t / c:7.1f}  {k}")
