@@ -124,7 +124,10 @@ def run(args) -> dict:
     app.router.on_startup.append(_widen_threadpool)
     port = _free_port()
     rng = random.Random(args.seed)
-    opts = {"num_predict": args.new_tokens, "ignore_eos": True, "temperature": 0.0}
+    # --option-less: the reference's call shape (no num_predict): every request may run to its context window, and
+    # the engines reserve KV lazily (prompt + one block at admission, growth per decode run, youngest preempted)
+    opts = {"temperature": 0.0} if args.option_less else {"num_predict": args.new_tokens, "ignore_eos": True,
+                                                           "temperature": 0.0}
     # random-init engines tokenize bytes (no tokenizer files offline): 1 char = 1 token there, ~4 with
     # the real Llama-3 BPE, so size the error text in tokens of the tokenizer actually serving it
     from .models import get_spec, tokenizer_for
@@ -155,7 +158,16 @@ def run(args) -> dict:
                 phases.append(_phase(cl, args, float(q), rng, make_request))
                 # progress on stderr (long multi-phase runs stay visibly alive)
                 print(f"phase qps={q}: {phases[-1].get('output_tokens_per_sec')} tok/s", file=sys.stderr, flush=True)
+    # per-engine admission / KV statistics (peak concurrently running requests, lazy-KV growth and preemptions)
+    eng_stats = {}
+    for m, lp in getattr(ctx.backend, "_loops", {}).items():
+        st = getattr(getattr(lp, "engine", None), "stats", None)
+        if st:
+            r = lp.engine.runner
+            eng_stats[m] = {k: st.get(k) for k in ("requests", "peak_running", "preempted", "kv_grown_blocks")}
+            eng_stats[m].update(kv_blocks=getattr(r, "num_kv_blocks", None), max_slots=getattr(r, "max_slots", None))
     for p in phases:
+        p.update(engines=eng_stats, option_less=bool(args.option_less))
         p.update(warmup_s=round(warm_s, 2), models={"nl2sql": f"duckdb-nsql-7B ({args.nl2sql_dtype})",
                                                     "explain_error": f"Llama-3.2-3B-Instruct ({args.explain_dtype})"},
                  new_tokens=args.new_tokens, explain_prompt_tokens_approx=args.explain_tokens,
@@ -254,6 +266,8 @@ def main(argv=None) -> None:
     ap.add_argument("--timeout", type=float, default=600.0)
     ap.add_argument("--engine", default="hip", help="hip | fake (plumbing only)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--option-less", action="store_true",
+                    help="requests carry no num_predict / ignore_eos (generate until EOS or the context window)")
     ap.add_argument("--stream", action="store_true",
                     help="send each request as a streaming /api/generate call and report time to first piece")
     print(json.dumps(run(ap.parse_args(argv))), flush=True)

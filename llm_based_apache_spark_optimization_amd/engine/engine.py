@@ -152,7 +152,7 @@ class LLMEngine:
         self.load_time_s = 0.0
         self.stats = {"requests": 0, "prompt_tokens": 0, "generated_tokens": 0, "decode_steps": 0,
                       "prefill_s": 0.0, "decode_s": 0.0, "decode_device_s": 0.0, "aborted": 0, "preempted": 0,
-                      "kv_grown_blocks": 0}
+                      "kv_grown_blocks": 0, "peak_running": 0}
         # per-decode-run device timing (hipEvents around the graph replays, read after the host sync the
         # run ends with anyway): lsa_decode_step_device_seconds{model} = GPU time per token step
         self.device_timing = runner.on_gpu
@@ -207,6 +207,7 @@ class LLMEngine:
             admitted = [] if (self._admit_hold and self.sched.num_running > 0) else self.sched.admit()
             if self.sched.num_running == 0:
                 self._admit_hold = False
+            self.stats["peak_running"] = max(self.stats["peak_running"], self.sched.num_running)
             t0 = time.perf_counter()
             entries = []
             for rid in admitted:

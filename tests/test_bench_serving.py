@@ -15,6 +15,11 @@ def test_bench_serving_streaming_fake_engine():
     assert out["nl2sql"]["ttft_p50_s"] is not None and out["nl2sql"]["ttft_p50_s"] <= out["nl2sql"]["p99_s"]
 
 
+def test_bench_serving_option_less_fake_engine():
+    out = bench_serving.run(bench_serving_args(qps=40, duration=0.5, option_less=True))
+    assert out["failed"] == 0 and out["requests"] > 5 and out["option_less"] is True
+
+
 def test_synthetic_prompts_sizes():
     import random
 
@@ -30,7 +35,7 @@ def bench_serving_args(**kw):
 
     a = argparse.Namespace(qps=8.0, duration=1.0, explain_frac=0.3, explain_tokens=256, new_tokens=16,
                            nl2sql_dtype="bf16", explain_dtype="bf16", max_batch=8, max_model_len=1024,
-                           concurrency=32, timeout=30.0, engine="fake", seed=0)
+                           concurrency=32, timeout=30.0, engine="fake", seed=0, option_less=False)
     for k, v in kw.items():
         setattr(a, k, v)
     return a
