@@ -20,6 +20,7 @@ int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* 
 int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids, const void* emb,
                     const int* row_idx, int write_h, const void* w, float eps, void* xn, int rows, int D,
                     int xf_mt, long long* ss_out, int ss_ld, int ss_nzero, void* x8, float* sx8, hipStream_t s);
+int lsa_prefetch(const void* const* ptrs, const long* bytes, int nr, int wgs, hipStream_t s);
 int lsa_res_add_ss(float* h, const float* parts, int nparts, long part_stride, void* xn, int rows, int D, int xf_mt,
                    long long* ss_out, hipStream_t s);
 int lsa_a8_gemm(const void* X8, const void* s8, const float* sx, int M, int K, const void* Wq, const float* wscale,
@@ -454,6 +455,20 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
         "add_rmsnorm");
 }
 
+// Infinity-Cache warm-up of up to four tensors (the first bytes[k] bytes of each; -1 = all of it)
+void prefetch(const std::vector<at::Tensor>& ts, const std::vector<int64_t>& bytes, int64_t wgs) {
+  TORCH_CHECK(!ts.empty() && ts.size() <= 4 && bytes.size() == ts.size(), "prefetch: 1-4 tensors, one byte count each");
+  const void* ptrs[4];
+  long nb[4];
+  for (size_t k = 0; k < ts.size(); ++k) {
+    TORCH_CHECK(ts[k].is_contiguous(), "prefetch: contiguous tensors");
+    const int64_t all = ts[k].numel() * ts[k].element_size();
+    ptrs[k] = ts[k].data_ptr();
+    nb[k] = (long)(bytes[k] < 0 || bytes[k] > all ? all : bytes[k]);
+  }
+  check(lsa_prefetch(ptrs, nb, (int)ts.size(), (int)wgs, cur_stream()), "prefetch");
+}
+
 // wide raw residual add of the folded-norm decode step: h += sum parts; xn = bf16(h); ss_out[m] += sum h^2 (Q24)
 void res_add_ss(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t nparts, int64_t part_stride,
                 at::Tensor& xn, int64_t rows, int64_t D, int64_t xf_mt, at::Tensor& ss_out) {
@@ -819,6 +834,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4,
         py::arg("depth") = 1,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
+  m.def("prefetch", &prefetch, py::arg("tensors"), py::arg("bytes"), py::arg("wgs") = 512);
   m.def("res_add_ss", &res_add_ss, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),
         py::arg("xn"), py::arg("rows"), py::arg("D"), py::arg("xf_mt"), py::arg("ss_out"));
   m.def("add_rmsnorm", &add_rmsnorm, py::arg("h"), py::arg("parts"), py::arg("nparts"), py::arg("part_stride"),

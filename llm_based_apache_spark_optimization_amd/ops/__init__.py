@@ -837,6 +837,17 @@ def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
     return xn
 
 
+def prefetch(tensors, nbytes=None, wgs: int = 512) -> None:
+    """Infinity-Cache warm-up: stream (the first ``nbytes[k]`` bytes of) up to four tensors through the memory
+    hierarchy with allocating loads and no stores, so the next kernel reading them hits the 256 MiB die-level cache.
+    Issued on a side stream of the captured decode step (``ModelRunner.prefetch_plan``).  No-op off the GPU."""
+    tensors = [t for t in tensors if t is not None]
+    if not tensors or not _gpu(tensors[0]):
+        return
+    nb = list(nbytes) if nbytes is not None else [-1] * len(tensors)
+    ext().prefetch(tensors, [int(b) for b in nb], int(wgs))
+
+
 def res_add_ss(h: torch.Tensor, parts: Optional[torch.Tensor], xn: torch.Tensor, rows: int, ss_out: torch.Tensor,
                xf: bool = False) -> torch.Tensor:
     """Residual add of the folded-norm decode step (the RMSNorm gammas live in the next GEMM's weight, which scales
