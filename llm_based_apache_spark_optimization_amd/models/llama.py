@@ -100,7 +100,7 @@ def pack_layer(spec: ModelSpec, wq, wk, wv, wo, wg, wu, wd, an, mn, rank=0, tp=1
     # qkv / o / down also keep a row-major copy for the vendor prefill GEMM (ops.PREFILL_BLAS); gate_up's fused SiLU
     # prefill stays on the 256^2 kernel
     return LayerWeights(P(wqkv.contiguous(), kind, rowmajor=True), P(wo_s.contiguous(), kind, rowmajor=True),
-                        P(gu.contiguous(), kind), P(wd_s.contiguous(), kind, rowmajor=True), an.contiguous(),
+                        P(gu.contiguous(), kind, rowmajor=ops.PREFILL_BLAS_SILU_MAX_M > 64), P(wd_s.contiguous(), kind, rowmajor=True), an.contiguous(),
                         mn.contiguous(), norms_folded=FOLD_NORMS)
 
 

@@ -388,12 +388,27 @@ def _epi_ref(y: torch.Tensor, M: int, K: int, epi: str, rownorm, res, xf: bool):
 PREFILL_BLAS = True
 
 
-def uses_blas(w: "PackedWeight", M: int) -> bool:
+# the fused-SiLU gate_up prefill goes to the vendor GEMM (f32 out) + the SiLU*up pass for 64 < M <= this many rows
+# (where the 256^2 tile grid is mostly padding); above it the gemm_t256 SiLU epilogue stays ahead.  Measured
+# (profiles/r4/prefill_gateup_blas_silu_vs_t256_mi355x.jsonl, us): 7B M=300 64.5 vs 89.8, 3B M=300 43.0 vs 67.0,
+# 7B M=1024 178.9 vs 185.9; 3B M=2048 191.4 vs 164.3, 7B M=4096 754.9 vs 607.8
+PREFILL_BLAS_SILU_MAX_M = 1024
+
+
+def uses_blas(w: "PackedWeight", M: int, epi: str = "bf16") -> bool:
+    if epi == "silu":
+        return PREFILL_BLAS and 64 < M <= PREFILL_BLAS_SILU_MAX_M and w.rm is not None
     return PREFILL_BLAS and M > 64 and w.rm is not None
 
 
 def _blas_linear(x: torch.Tensor, w: PackedWeight, epi: str, out: Optional[torch.Tensor]) -> torch.Tensor:
     M = x.shape[0]
+    if epi == "silu":  # gate/up rows interleaved per 16 (as packed): one f32 slab, then SiLU(gate) * up
+        y = torch.empty(1, M, w.N, device=x.device, dtype=torch.float32)
+        torch.mm(x, w.rm.t(), out_dtype=torch.float32, out=y[0])
+        o = out.view(-1)[: M * (w.N // 2)].view(M, w.N // 2) if out is not None else torch.empty(
+            M, w.N // 2, device=x.device, dtype=torch.bfloat16)
+        return silu_parts(y, o)
     if epi == "bf16":
         o = out.view(-1)[: M * w.N].view(M, w.N) if out is not None else torch.empty(M, w.N, device=x.device,
                                                                                    dtype=torch.bfloat16)
@@ -426,7 +441,7 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
             out.view(-1)[: y.numel()].copy_(y.reshape(-1))
             return out
         return y
-    if epi in ("bf16", "f32") and uses_blas(w, M) and rownorm is None:
+    if epi in ("bf16", "f32", "silu") and uses_blas(w, M, epi) and rownorm is None:
         return _blas_linear(x, w, epi, out)  # one f32 slab whatever splitk asked for
     nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi, kind=w.kind)
     nb = nb0 if nb is None else nb

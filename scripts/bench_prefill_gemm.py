@@ -34,6 +34,8 @@ shapes = {"7b_qkv": (4096, 12288, 4096, "bf16"), "7b_o": (4096, 4096, 4096, "f32
           "7b_gateup": (4096, 22016, 4096, "silu"), "7b_down": (4096, 4096, 11008, "f32"),
           "3b_qkv": (2048, 5120, 3072, "bf16"), "3b_gateup": (2048, 16384, 3072, "silu"),
           "3b_down": (2048, 3072, 8192, "f32"), "7b_qkv_m300": (300, 12288, 4096, "bf16"),
+          "7b_gateup_m300": (300, 22016, 4096, "silu"), "7b_gateup_m1024": (1024, 22016, 4096, "silu"),
+          "3b_gateup_m300": (300, 16384, 3072, "silu"),
           "sq8192": (8192, 8192, 8192, "bf16")}
 if len(sys.argv) > 1:
     shapes = {k: v for k, v in shapes.items() if k in sys.argv[1].split(",")}
@@ -68,6 +70,15 @@ for name, (M, N, K, epi) in shapes.items():
     o32 = torch.empty(M, N, device=dev, dtype=torch.float32)
     us = timeit(lambda: torch.mm(x, wt, out_dtype=torch.float32, out=o32))
     res["hipblaslt_f32out"] = {"us": round(us, 1), "TF": round(flops / us / 1e6, 1)}
+    if epi == "silu":  # vendor GEMM (f32 out, gate/up rows interleaved per 16 as packed) + the SiLU*up pass
+        def blas_silu():
+            torch.mm(x, wt, out_dtype=torch.float32, out=o32)
+            e.silu_parts(o32.view(1, M, N), out)
+        blas_silu()
+        torch.cuda.synchronize()
+        err = ((out.float() - ref).norm() / ref.norm()).item()
+        us = timeit(blas_silu)
+        res["hipblaslt_silu"] = {"us": round(us, 1), "TF": round(flops / us / 1e6, 1), "rel_err": float(f"{err:.2e}")}
     print(json.dumps(res), flush=True)
     del x, w, pw, out, ref
     torch.cuda.empty_cache()

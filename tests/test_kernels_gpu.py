@@ -44,14 +44,18 @@ def test_gemm_skinny_f32_splitk(gpu, M, splitk):
     assert _rel(y.sum(0), yr) < 1e-4
 
 
-@pytest.mark.parametrize("M", [1, 20, 64, 100, 257])
-def test_gemm_silu(gpu, M):
+@pytest.mark.parametrize("M", [1, 20, 64, 100, 257, 1100])
+@pytest.mark.parametrize("rowmajor", [False, True])
+def test_gemm_silu(gpu, M, rowmajor):
+    """rowmajor: 64 < M <= PREFILL_BLAS_SILU_MAX_M runs the vendor GEMM (f32 out) + the SiLU*up pass, else the
+    hand kernels (the row-major copy is ignored)."""
     F, K = 1024, 2048
     torch.manual_seed(2)
     x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
     wg = (torch.randn(F, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
     wu = (torch.randn(F, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
-    pw = ops.PackedWeight.from_dense(ops.interleave_gate_up(wg, wu))
+    pw = ops.PackedWeight.from_dense(ops.interleave_gate_up(wg, wu), rowmajor=rowmajor)
+    assert ops.uses_blas(pw, M, "silu") == (rowmajor and 64 < M <= ops.PREFILL_BLAS_SILU_MAX_M)
     y = ops.linear(x, pw, "silu")
     yr = torch.nn.functional.silu(x.float() @ wg.float().t()) * (x.float() @ wu.float().t())
     assert y.shape == (M, F)
