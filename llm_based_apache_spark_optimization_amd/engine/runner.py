@@ -761,27 +761,38 @@ class ModelRunner:
         sk_o = self._splitk(T, self.H * self.D)
         sk_d = self._splitk(T, self.ffn_l)
         d_parts = None
+        # TP = 1, vendor prefill GEMMs: o / down accumulate into the f32 residual (beta = 1), the norms read h alone
+        res_o = self.on_gpu and ops.PREFILL_BLAS_RES and (self.tp is None or self.tp.size == 1) and ops.uses_blas(w.layers[0].wo, T)
+        res_d = res_o and ops.uses_blas(w.layers[0].w_down, T)
         for l, lw in enumerate(w.layers):
             if l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
             else:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts)
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, write_h=not res_d)
             self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T)
-            o_parts = ops.linear(attn, lw.wo, "f32", splitk=sk_o)
-            if not self.on_gpu:
-                o_parts = o_parts.view(1, T, d)
-            o_parts = self._reduce_parts(o_parts)
-            ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
+            if res_o:
+                ops.blas_residual(attn, lw.wo, h)
+                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, write_h=False)
+            else:
+                o_parts = ops.linear(attn, lw.wo, "f32", splitk=sk_o)
+                if not self.on_gpu:
+                    o_parts = o_parts.view(1, T, d)
+                o_parts = self._reduce_parts(o_parts)
+                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
             sk_g = self._splitk(T, self.d, lw.w_gate_up.N)
             if sk_g > 1:  # small tile grid: f32 split-K slabs, then silu(gate) * up over the slabs
                 act = ops.silu_parts(ops.linear(xn, lw.w_gate_up, "f32", splitk=sk_g),
                                      torch.empty(T, lw.w_gate_up.N // 2, **bf))
             else:
                 act = ops.linear(xn, lw.w_gate_up, "silu")
-            d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
-            if not self.on_gpu:
-                d_parts = d_parts.view(1, T, d)
-            d_parts = self._reduce_parts(d_parts)
+            if res_d:
+                ops.blas_residual(act, lw.w_down, h)
+                d_parts = None
+            else:
+                d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
+                if not self.on_gpu:
+                    d_parts = d_parts.view(1, T, d)
+                d_parts = self._reduce_parts(d_parts)
         if not commit:
             return None
         xl = torch.empty(n, d, **bf)

@@ -393,6 +393,8 @@ PREFILL_BLAS = True
 # (profiles/r4/prefill_gateup_blas_silu_vs_t256_mi355x.jsonl, us): 7B M=300 64.5 vs 89.8, 3B M=300 43.0 vs 67.0,
 # 7B M=1024 178.9 vs 185.9; 3B M=2048 191.4 vs 164.3, 7B M=4096 754.9 vs 607.8
 PREFILL_BLAS_SILU_MAX_M = 1024
+# TP = 1 prefill: the vendor o / down GEMMs accumulate into the f32 residual (``blas_residual``)
+PREFILL_BLAS_RES = True
 
 
 def uses_blas(w: "PackedWeight", M: int, epi: str = "bf16") -> bool:
@@ -418,6 +420,16 @@ def _blas_linear(x: torch.Tensor, w: PackedWeight, epi: str, out: Optional[torch
                                                                                    dtype=torch.float32)
     torch.mm(x, w.rm.t(), out_dtype=torch.float32, out=o[0])
     return o
+
+
+def blas_residual(x: torch.Tensor, w: PackedWeight, h: torch.Tensor) -> torch.Tensor:
+    """h[:M] += x @ W^T in f32 on the vendor GEMM (beta = 1, bf16 operands, f32 C / D): the prefill's o / down
+    projections fold the residual add into the GEMM, so the norm after them reads h alone (no f32 slab written
+    by the GEMM and read back by the add).  Needs ``uses_blas(w, M)``."""
+    M = x.shape[0]
+    hv = h[:M]
+    torch.addmm(hv, x, w.rm.t(), out_dtype=torch.float32, out=hv)
+    return h
 
 
 def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
