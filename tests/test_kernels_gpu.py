@@ -977,3 +977,4 @@ def test_gemm_ragged_grid(gpu, kind, M, nb):
         else:
             got = ops.from_xfrag(y, M, N // 2) if (xf or kind == "fp8a") else y.view(M, N // 2)
             assert _rel(got, want_silu) < 1e-2, (kind, epi)
+
