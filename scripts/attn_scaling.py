@@ -50,16 +50,17 @@ def run(B, H, Hkv, ctx, nparts=2, plan_ctx=None):
             "TBps": round(mb / us, 2)}
 
 
-# graphs are planned for the engine's max_model_len; short live contexts leave most splits empty
-for pc in (None, 512, 2048, 4096, 8192):
-    print(json.dumps({"plan_ctx": pc, **run(32, 32, 32, 200, plan_ctx=pc)}), flush=True)
-for pc in (None, 4096, 8192):
-    print(json.dumps({"plan_ctx": pc, **run(1, 24, 8, 300, plan_ctx=pc)}), flush=True)
-if len(sys.argv) > 1 and sys.argv[1] == "plans":
-    sys.exit(0)
-for B in (1, 4, 8, 16, 32, 64):
-    print(json.dumps(run(B, 32, 32, 200)), flush=True)
-for ctx in (64, 128, 256, 512, 1024, 2048, 4096):
-    print(json.dumps(run(32, 32, 32, ctx)), flush=True)
-for ctx in (256, 512, 1024, 2100, 4096, 8192):
-    print(json.dumps(run(1, 24, 8, ctx)), flush=True)
+if __name__ == "__main__":
+    # graphs are planned for the engine's max_model_len; short live contexts leave most splits empty
+    for pc in (None, 512, 2048, 4096, 8192):
+        print(json.dumps({"plan_ctx": pc, **run(32, 32, 32, 200, plan_ctx=pc)}), flush=True)
+    for pc in (None, 4096, 8192):
+        print(json.dumps({"plan_ctx": pc, **run(1, 24, 8, 300, plan_ctx=pc)}), flush=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "plans":
+        sys.exit(0)
+    for B in (1, 4, 8, 16, 32, 64):
+        print(json.dumps(run(B, 32, 32, 200)), flush=True)
+    for ctx in (64, 128, 256, 512, 1024, 2048, 4096):
+        print(json.dumps(run(32, 32, 32, ctx)), flush=True)
+    for ctx in (256, 512, 1024, 2100, 4096, 8192):
+        print(json.dumps(run(1, 24, 8, ctx)), flush=True)
