@@ -67,6 +67,7 @@ int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, v
 int lsa_gemm_t256x(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int xf_tiles,
                    hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
+int lsa_silu_bf16(const void* y, int M, int F, void* out, hipStream_t s);
 void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                        const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
@@ -875,6 +876,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     const int S = parts.size(0), M = parts.size(1), F = parts.size(2) / 2;
     check(lsa_silu_parts(parts.data_ptr<float>(), S, parts.stride(0), M, F, out.data_ptr(), cur_stream()),
           "silu_parts");
+  });
+  m.def("silu_bf16", [](const at::Tensor& y, at::Tensor& out) {
+    // y: bf16 [M, 2F] (gate/up interleaved per 16 columns) -> out bf16 [M, F] = silu(gate) * up
+    need(y, at::kBFloat16, "y");
+    need(out, at::kBFloat16, "out");
+    TORCH_CHECK(y.dim() == 2 && y.is_contiguous() && y.size(1) % 32 == 0, "silu_bf16: y [M, 2F] contiguous");
+    const int M = y.size(0), F = y.size(1) / 2;
+    TORCH_CHECK(out.is_contiguous() && out.numel() >= (int64_t)M * F, "silu_bf16: out too small");
+    check(lsa_silu_bf16(y.data_ptr(), M, F, out.data_ptr(), cur_stream()), "silu_bf16");
   });
   m.def("ar_alloc", &ar_alloc);
   m.def("ar_free", [](int64_t p) { check(lsa_ar_free(reinterpret_cast<void*>(p)), "ar_free"); });

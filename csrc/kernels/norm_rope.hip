@@ -509,3 +509,34 @@ extern "C" int lsa_prefetch(const void* const* ptrs, const long* bytes, int nr, 
   hipLaunchKernelGGL(prefetch_kernel, dim3(wgs), dim3(256), 0, s, r);
   return (int)hipGetLastError();
 }
+
+// silu(gate) * up from the bf16 output of the vendor gate_up GEMM (prefill): y [M][2F] bf16 with gate / up rows
+// interleaved per 16 columns as packed -> out [M][F] bf16.  Eight outputs per thread (one 16-byte gate and one
+// 16-byte up load), so the pass streams 3 bytes per output at full width.
+__global__ __launch_bounds__(256) void silu_bf16_kernel(const uint16_t* __restrict__ y, int M, int F,
+                                                        uint16_t* __restrict__ out) {
+  const long total8 = (long)M * F / 8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
+    const long e = i * 8;
+    const int m = (int)(e / F), f = (int)(e - (long)m * F);
+    const int blk = f >> 4, off = f & 15;
+    const size_t gi = (size_t)m * 2 * F + (size_t)(2 * blk) * 16 + off;
+    const uint4 g = *reinterpret_cast<const uint4*>(y + gi);
+    const uint4 u = *reinterpret_cast<const uint4*>(y + gi + 16);
+    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, uw[4] = {u.x, u.y, u.z, u.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = pack2bf(silu(bf2f(gw[j] & 0xffffu)) * bf2f(uw[j] & 0xffffu), silu(bf2f(gw[j] >> 16)) * bf2f(uw[j] >> 16));
+    *reinterpret_cast<uint4*>(out + e) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+extern "C" int lsa_silu_bf16(const void* y, int M, int F, void* out, hipStream_t s) {
+  if (F % 16 || M <= 0) return -1;
+  const long total8 = (long)M * F / 8;
+  const long gl = (total8 + 255) / 256;
+  hipLaunchKernelGGL(silu_bf16_kernel, dim3((unsigned)(gl < 8192 ? gl : 8192)), dim3(256), 0, s,
+                     reinterpret_cast<const uint16_t*>(y), M, F, reinterpret_cast<uint16_t*>(out));
+  return (int)hipGetLastError();
+}

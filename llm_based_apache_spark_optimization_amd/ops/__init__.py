@@ -388,11 +388,13 @@ def _epi_ref(y: torch.Tensor, M: int, K: int, epi: str, rownorm, res, xf: bool):
 PREFILL_BLAS = True
 
 
-# the fused-SiLU gate_up prefill goes to the vendor GEMM (f32 out) + the SiLU*up pass for 64 < M <= this many rows
-# (where the 256^2 tile grid is mostly padding); above it the gemm_t256 SiLU epilogue stays ahead.  Measured
-# (profiles/r4/prefill_gateup_blas_silu_vs_t256_mi355x.jsonl, us): 7B M=300 64.5 vs 89.8, 3B M=300 43.0 vs 67.0,
-# 7B M=1024 178.9 vs 185.9; 3B M=2048 191.4 vs 164.3, 7B M=4096 754.9 vs 607.8
-PREFILL_BLAS_SILU_MAX_M = 1024
+# the fused-SiLU gate_up prefill goes to the vendor GEMM (bf16 gate / up, the reference model's own rounding) + the
+# bf16 SiLU*up pass for 64 < M <= this many rows; above it the gemm_t256 SiLU epilogue stays ahead.  Measured
+# (profiles/r4/prefill_gateup_blas_silu_vs_t256_mi355x.jsonl, us, f32-out variant): 7B M=300 64.5 vs 89.8, 3B M=300
+# 43.0 vs 67.0, 7B M=1024 178.9 vs 185.9; end to end (profiles/r4/prefill_ab_silu_bf16_mi355x.jsonl): 3B 2k TTFT
+# 14.09 -> 13.86 ms, 7B 300 tokens 8.80 -> 8.27 ms, but 7B 4096 rows 49.5 -> 50.7 ms (hence the cap)
+PREFILL_BLAS_SILU_MAX_M = 2048
+PREFILL_BLAS_SILU_BF16 = True
 # TP = 1 prefill: the vendor o / down GEMMs accumulate into the f32 residual (``blas_residual``)
 PREFILL_BLAS_RES = True
 
@@ -405,11 +407,15 @@ def uses_blas(w: "PackedWeight", M: int, epi: str = "bf16") -> bool:
 
 def _blas_linear(x: torch.Tensor, w: PackedWeight, epi: str, out: Optional[torch.Tensor]) -> torch.Tensor:
     M = x.shape[0]
-    if epi == "silu":  # gate/up rows interleaved per 16 (as packed): one f32 slab, then SiLU(gate) * up
-        y = torch.empty(1, M, w.N, device=x.device, dtype=torch.float32)
-        torch.mm(x, w.rm.t(), out_dtype=torch.float32, out=y[0])
+    if epi == "silu":  # gate/up rows interleaved per 16 (as packed), then SiLU(gate) * up
         o = out.view(-1)[: M * (w.N // 2)].view(M, w.N // 2) if out is not None else torch.empty(
             M, w.N // 2, device=x.device, dtype=torch.bfloat16)
+        if PREFILL_BLAS_SILU_BF16:  # bf16 gate / up (the reference model's own rounding), half the pass's bytes
+            y = torch.mm(x, w.rm.t())
+            ext().silu_bf16(y, o)
+            return o
+        y = torch.empty(1, M, w.N, device=x.device, dtype=torch.float32)
+        torch.mm(x, w.rm.t(), out_dtype=torch.float32, out=y[0])
         return silu_parts(y, o)
     if epi == "bf16":
         o = out.view(-1)[: M * w.N].view(M, w.N) if out is not None else torch.empty(M, w.N, device=x.device,

@@ -44,11 +44,14 @@ def test_gemm_skinny_f32_splitk(gpu, M, splitk):
     assert _rel(y.sum(0), yr) < 1e-4
 
 
-@pytest.mark.parametrize("M", [1, 20, 64, 100, 257, 1100])
-@pytest.mark.parametrize("rowmajor", [False, True])
-def test_gemm_silu(gpu, M, rowmajor):
+@pytest.mark.parametrize("M", [1, 20, 64, 100, 257, 1100, 2100])
+@pytest.mark.parametrize("rowmajor", [False, True, "bf16"])
+def test_gemm_silu(gpu, M, rowmajor, monkeypatch):
     """rowmajor: 64 < M <= PREFILL_BLAS_SILU_MAX_M runs the vendor GEMM (f32 out) + the SiLU*up pass, else the
-    hand kernels (the row-major copy is ignored)."""
+    hand kernels (the row-major copy is ignored).  "bf16": the vendor GEMM writes bf16 gate / up and the bf16 SiLU
+    pass (``silu_bf16``) reads them."""
+    monkeypatch.setattr(ops, "PREFILL_BLAS_SILU_BF16", rowmajor == "bf16")
+    rowmajor = bool(rowmajor)
     F, K = 1024, 2048
     torch.manual_seed(2)
     x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
