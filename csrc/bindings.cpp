@@ -41,7 +41,7 @@ int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* bl
                     void* out, float* opart, float* mlpart, int* counters, int xf_mt, const float* qkv_parts, int nparts,
                     long part_stride,
                     const float* cos_t, const float* sin_t, const float* ks, const float* vs, void* out_s8,
-                    const void* pf, long pf_bytes, int pf_wgs, hipStream_t s);
+                    hipStream_t s);
 int lsa_kv8_dequant(const void* kc, const void* vc, const float* ks, const float* vs, const int* block_tables,
                     int max_blocks, const int* ctx_lens, int nseq, int Hkv, int mb, void* ko, void* vo, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
@@ -538,9 +538,7 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                  at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, at::Tensor& counters, int64_t xf_mt,
                  const c10::optional<at::Tensor>& qkv_parts, const c10::optional<at::Tensor>& cos_t,
                  const c10::optional<at::Tensor>& sin_t, int64_t unsplit_max, const c10::optional<at::Tensor>& ks,
-                 const c10::optional<at::Tensor>& vs, const c10::optional<at::Tensor>& out_s8 = c10::nullopt,
-                 const c10::optional<at::Tensor>& prefetch = c10::nullopt, int64_t prefetch_bytes = -1,
-                 int64_t prefetch_wgs = 0) {
+                 const c10::optional<at::Tensor>& vs, const c10::optional<at::Tensor>& out_s8 = c10::nullopt) {
   need(q, at::kBFloat16, "q");
   check_cache(kc, vc, ks, vs);
   need(pos, at::kInt, "pos");
@@ -577,25 +575,13 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
     TORCH_CHECK(cos_t->size(0) >= block_tables.size(1) * 64 && sin_t->size(0) >= block_tables.size(1) * 64,
                 "rope tables have fewer rows than the block tables address (", block_tables.size(1) * 64, ")");
   }
-  // Infinity-Cache warm-up of the next projection's weights by extra workgroups (the first prefetch_bytes bytes of a
-  // contiguous device tensor; -1 = all of it)
-  const void* pf_ptr = nullptr;
-  long pf_bytes = 0;
-  if (prefetch.has_value() && prefetch_wgs > 0) {
-    TORCH_CHECK(on_dev(*prefetch) && prefetch->is_contiguous(), "attn_decode: prefetch must be a contiguous device tensor");
-    const int64_t all = prefetch->numel() * prefetch->element_size();
-    pf_ptr = prefetch->data_ptr();
-    pf_bytes = (long)(prefetch_bytes < 0 || prefetch_bytes > all ? all : prefetch_bytes);
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(pf_ptr) % 16 == 0, "attn_decode: prefetch tensor must be 16-byte aligned");
-  }
   check(lsa_attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                         block_tables.size(1), pos.data_ptr<int>(), B, H, Hkv, (float)scale, chunk_blocks, nsplit,
                         (int)unsplit_max, out.data_ptr(), opart.data_ptr<float>(), mlpart.data_ptr<float>(), counters.data_ptr<int>(), xf_mt,
                         ptr<const float>(qkv_parts), qkv_parts.has_value() ? qkv_parts->size(0) : 0,
                         qkv_parts.has_value() ? qkv_parts->stride(0) : 0, ptr<const float>(cos_t),
                         ptr<const float>(sin_t), ptr<const float>(ks), ptr<const float>(vs),
-                        out_s8.has_value() ? out_s8->data_ptr() : nullptr, pf_ptr, pf_bytes, (int)prefetch_wgs,
-                        cur_stream()),
+                        out_s8.has_value() ? out_s8->data_ptr() : nullptr, cur_stream()),
         "attn_decode");
 }
 
@@ -873,8 +859,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("counters"), py::arg("xf_mt") = 0,
         py::arg("qkv_parts") = py::none(),
         py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4,
-        py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("out_s8") = py::none(),
-        py::arg("prefetch") = py::none(), py::arg("prefetch_bytes") = -1, py::arg("prefetch_wgs") = 0);
+        py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("out_s8") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
         py::arg("out"), py::arg("rows32") = 0);

@@ -56,9 +56,6 @@ struct RopeArgs {
   uint16_t* vc;
   float* ks;           // fp8 cache: per-(token, kv-head) scales (writable aliases of ksc / vsc)
   float* vs;
-  const uint4* pf;     // Infinity-Cache warm-up of the next projection's weights (null: none), pf_n 16-byte units
-  long pf_n;
-  int pf_z;            // grid z index of the first warm-up workgroup (= nsplit)
 };
 
 // WV = waves per workgroup: 8 for G <= 3 (two keys per lane group per block -> half the K/V registers,
@@ -154,23 +151,6 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
   const int hk = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int H = Hkv * G;
   const int tid = threadIdx.x;
-  if (ra.pf && split >= ra.pf_z) {
-    // warm-up workgroups (the grid's last z planes, dispatched after every attention workgroup): while the
-    // latency-bound attention leaves HBM mostly idle, stream the o projection's weights through the memory
-    // hierarchy with allocating loads and no stores, so its GEMM reads them from the Infinity Cache
-    const long nw = (long)gridDim.x * gridDim.y * (gridDim.z - ra.pf_z);
-    const long wi = ((long)(split - ra.pf_z) * gridDim.y + b) * gridDim.x + hk;
-    const long per = (ra.pf_n + nw - 1) / nw, i0 = wi * per, i1 = min(ra.pf_n, i0 + per);
-    uint32_t acc = 0;
-    long i = i0 + tid;
-    for (; i + 3 * NT < i1; i += 4 * NT) {
-      const uint4 a = ra.pf[i], c = ra.pf[i + NT], d = ra.pf[i + 2 * NT], e = ra.pf[i + 3 * NT];
-      acc ^= a.x ^ c.x ^ d.x ^ e.x;
-    }
-    for (; i < i1; i += NT) acc ^= ra.pf[i].x;
-    asm volatile("" ::"v"(acc));
-    return;
-  }
   unsigned long long* const stp = g_attn_stamps;
   LSA_STAMP(0);
   const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(opart, 0, 0x7fffffff, 0x00020000);
@@ -226,8 +206,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
   // unsplit threshold, because the host plan has nsplit * chunk_blocks >= every context the captured graph
   // serves -- so its first K/V fetch also leaves before pos[b] is read (one dependent round trip off the
   // chain, 3B 2k explain: start->ctx 1.2 us); a mismatch (a short context) re-fetches below.
-  const int zatt = ra.pf ? ra.pf_z : (int)gridDim.z;  // the attention grid's z extent (warm-up planes excluded)
-  const int spec_blk = (split != 0 && (int)(gridDim.x * gridDim.y) * zatt <= LSA_ATTN_SPEC_MAX_WG &&
+  const int spec_blk = (split != 0 && (int)(gridDim.x * gridDim.y * gridDim.z) <= LSA_ATTN_SPEC_MAX_WG &&
                         split * chunk_blocks < max_blocks) ? split * chunk_blocks : -1;
   if (split == 0) fetch(kA, vA, ksA, vsA, 0, 63);
   else if (spec_blk >= 0) fetch(kA, vA, ksA, vsA, spec_blk, 63);
@@ -626,8 +605,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
                                int unsplit_max, void* out, float* opart, float* mlpart, int* counters, int xf_mt,
                                const float* qkv_parts, int nparts,
                                long part_stride, const float* cos_t, const float* sin_t, const float* ks,
-                               const float* vs, void* out_s8, const void* pf, long pf_bytes, int pf_wgs,
-                               hipStream_t s) {
+                               const float* vs, void* out_s8, hipStream_t s) {
   if (H % Hkv) return -1;
   if (xf_mt && B > 16 * xf_mt) return -4;
   if (out_s8 && !xf_mt) return -6;  // the e4m3 output lives in the xf8 layout
@@ -636,15 +614,12 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
   const int G = H / Hkv;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid(Hkv, B, nsplit);
-  // warm-up planes: about pf_wgs extra workgroups streaming pf_bytes of the next projection's weights
-  const int pf_planes = (pf && pf_bytes >= 16 && pf_wgs > 0) ? (pf_wgs + Hkv * B - 1) / (Hkv * B) : 0;
   const uint16_t* qq = reinterpret_cast<const uint16_t*>(q);
   const uint16_t* kk = reinterpret_cast<const uint16_t*>(kc);
   const uint16_t* vv = reinterpret_cast<const uint16_t*>(vc);
   uint16_t* oo = reinterpret_cast<uint16_t*>(out);
   const RopeArgs ra{qkv_parts, (size_t)part_stride, nparts, cos_t, sin_t, const_cast<uint16_t*>(kk),
-                    const_cast<uint16_t*>(vv), const_cast<float*>(ks), const_cast<float*>(vs),
-                    pf_planes ? reinterpret_cast<const uint4*>(pf) : nullptr, pf_bytes / 16, nsplit};
+                    const_cast<uint16_t*>(vv), const_cast<float*>(ks), const_cast<float*>(vs)};
 #define LSA_ADL(GV, RP, WV, KV8, SB)                                                                              \
   hipLaunchKernelGGL((attn_decode_kernel<GV, RP, WV, KV8, SB>), grid, dim3(64 * (WV)), 0, s, qq, kk, vv, ks, vs,     \
                      block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart,  \
@@ -654,7 +629,6 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
   // merge, profiles/r3/attn_decode_wv23_ab_mi355x.jsonl) and eight above (3B batch 32: 10.54 vs 11.33 us); else 4
   const long nwg = (long)grid.x * grid.y * grid.z;
   const bool sb = nwg >= LSA_ATTN_SB_MIN_WG, small23 = nwg <= LSA_ATTN_SMALL23_WG;
-  grid.z += pf_planes;
 #define LSA_ADK(GV, RP)                                                                                               \
   do {                                                                                                                 \
     if constexpr (GV == 1) {                                                                                           \

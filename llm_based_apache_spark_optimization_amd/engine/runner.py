@@ -161,10 +161,6 @@ class ModelRunner:
         self.a8_min_batch = 0 if mx else 32
         self.a8_mlp_min_batch = 0 if mx else 16
         self.a8_od_max_batch = 16 if mx else 0  # o / down W8A8 (W4A8) up to this bucket
-        # decode attention on small grids (B x Hkv <= attn_prefetch_max_pairs, latency-bound, HBM mostly idle) carries
-        # attn_prefetch_wgs extra workgroups that stream the o projection's weights into the Infinity Cache
-        self.attn_prefetch_wgs = 0
-        self.attn_prefetch_max_pairs = 64
         self.x8 = torch.zeros(xr * self.d if self.a8 else 1, dtype=torch.uint8, device=dev)
         self.sx8 = torch.ones(max(S, 64), **f32)
         mt64 = ops.xfrag_tiles(min(S, 64))
@@ -367,7 +363,7 @@ class ModelRunner:
                             (self.x8o if a8o else attn) if xf else attn.view(B, self.H, self.D), workspace=ws,
                             plan=plan, xf=xf, qkv_parts=qkv_parts if fr else None, cos=self.cos if fr else None,
                             sin=self.sin if fr else None, kv_scales=self._kv_scales(l),
-                            out_s8=self.s8o if a8o else None, prefetch=self._attn_prefetch(B, lw))
+                            out_s8=self.s8o if a8o else None)
             if a8o:
                 ops.linear_a8(self.x8o, None, B, lw.wo, "f32", out=o_parts, splitk=sk_o, s8=self.s8o)
             else:
@@ -433,8 +429,7 @@ class ModelRunner:
             kc, vc = self.kv[l, 0], self.kv[l, 1]
             ops.attn_decode(self.q[:B], kc, vc, bt, pos, self.H, self.Hkv, self.scale,
                             attn if xf else attn.view(B, self.H, self.D), workspace=ws, plan=plan, xf=xf,
-                            qkv_parts=qkv_parts, cos=self.cos, sin=self.sin, kv_scales=self._kv_scales(l),
-                            prefetch=self._attn_prefetch(B, lw))
+                            qkv_parts=qkv_parts, cos=self.cos, sin=self.sin, kv_scales=self._kv_scales(l))
             lin(attn, lw.wo, "res", out=o_parts, splitk=sk_o, res=(h, xn, ssq[2 * l + 1], tk), **rc)
             lin(xn, lw.w_gate_up, "silu", out=act, rownorm=(ssq[2 * l + 1], self.eps))
             lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk), **rc)
@@ -459,12 +454,6 @@ class ModelRunner:
         if self.step_xfrag(B):
             return ops.from_xfrag(self.xn_f, B, self.d)
         return self.xn[:B]
-
-    def _attn_prefetch(self, B: int, lw) -> Optional[tuple]:
-        """(tensor, bytes, workgroups) of the o projection's weights for ``ops.attn_decode(prefetch=)``, or None."""
-        if not (self.on_gpu and self.attn_prefetch_wgs > 0 and B * self.Hkv <= self.attn_prefetch_max_pairs):
-            return None
-        return (lw.wo.data, -1, self.attn_prefetch_wgs)
 
     def step_xfrag(self, B: int) -> bool:
         """Whether the decode step of bucket B hands its activations on in the fragment-major layouts (use_xfrag,

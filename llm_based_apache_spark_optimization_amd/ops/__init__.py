@@ -993,16 +993,14 @@ def decode_workspace(B: int, H: int, Hkv: int, nsplit: int, device) -> tuple:
 
 
 def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None, xf=False,
-                qkv_parts=None, cos=None, sin=None, kv_scales=None, out_s8=None, prefetch=None):
+                qkv_parts=None, cos=None, sin=None, kv_scales=None, out_s8=None):
     """q [B,H,128] vs paged cache, context = pos + 1.  workspace = decode_workspace(...) for split-KV.
     xf=True: out is a flat buffer receiving the fragment-major layout of the [B, H*128] output.
     qkv_parts ([S, B, (H+2Hkv)*128] f32 split-K slabs of the QKV projection) + cos/sin: RoPE and the
     KV-cache append of the new token are fused in (``q`` is then only a [B, H, 128] scratch buffer).
     kv_scales = (ks, vs): fp8 cache (see ``KV_FP8``).
     out_s8 (xf only): ``out`` is a uint8 buffer receiving the output as e4m3 in the xf8 layout with one E8M0 scale
-    per (row, head) in ``out_s8`` -- the input of a W8A8 / W4A8 o projection (``linear_a8(s8=)``).
-    prefetch = (tensor, nbytes, workgroups): extra workgroups of the launch stream the first nbytes of ``tensor`` (the
-    o projection's weights) into the Infinity Cache while the latency-bound attention runs (no-op off the GPU)."""
+    per (row, head) in ``out_s8`` -- the input of a W8A8 / W4A8 o projection (``linear_a8(s8=)``)."""
     B = pos.shape[0]
     assert out_s8 is None or xf, "the e4m3 attention output lives in the xf8 layout"
     if not _gpu(pos):
@@ -1027,9 +1025,8 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
         workspace = decode_workspace(B, H, Hkv, nsplit, q.device)
     opart, mlpart, counters = workspace
     ks, vs = kv_scales if kv_scales is not None else (None, None)
-    pf = dict(prefetch=prefetch[0], prefetch_bytes=int(prefetch[1]), prefetch_wgs=int(prefetch[2])) if prefetch else {}
     ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart, counters,
-                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs, out_s8=out_s8, **pf)
+                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs, out_s8=out_s8)
     return out
 
 
