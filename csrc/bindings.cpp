@@ -456,13 +456,23 @@ void add_rmsnorm(at::Tensor& h, const c10::optional<at::Tensor>& parts, int64_t 
         "add_rmsnorm");
 }
 
+// y: bf16 [M, 2F] (gate/up interleaved per 16 columns, the vendor prefill GEMM's output) -> out bf16 [M, F]
+void silu_bf16(const at::Tensor& y, at::Tensor& out) {
+  need(y, at::kBFloat16, "y");
+  need(out, at::kBFloat16, "out");
+  TORCH_CHECK(y.dim() == 2 && y.is_contiguous() && y.size(1) % 32 == 0, "silu_bf16: y [M, 2F] contiguous");
+  const int M = y.size(0), F = y.size(1) / 2;
+  TORCH_CHECK(out.is_contiguous() && out.numel() >= (int64_t)M * F, "silu_bf16: out too small");
+  check(lsa_silu_bf16(y.data_ptr(), M, F, out.data_ptr(), cur_stream()), "silu_bf16");
+}
+
 // Infinity-Cache warm-up of up to four tensors (the first bytes[k] bytes of each; -1 = all of it)
 void prefetch(const std::vector<at::Tensor>& ts, const std::vector<int64_t>& bytes, int64_t wgs) {
   TORCH_CHECK(!ts.empty() && ts.size() <= 4 && bytes.size() == ts.size(), "prefetch: 1-4 tensors, one byte count each");
   const void* ptrs[4];
   long nb[4];
   for (size_t k = 0; k < ts.size(); ++k) {
-    TORCH_CHECK(ts[k].is_contiguous(), "prefetch: contiguous tensors");
+    TORCH_CHECK(on_dev(ts[k]) && ts[k].is_contiguous(), "prefetch: contiguous GPU tensors");
     const int64_t all = ts[k].numel() * ts[k].element_size();
     ptrs[k] = ts[k].data_ptr();
     nb[k] = (long)(bytes[k] < 0 || bytes[k] > all ? all : bytes[k]);
@@ -877,15 +887,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     check(lsa_silu_parts(parts.data_ptr<float>(), S, parts.stride(0), M, F, out.data_ptr(), cur_stream()),
           "silu_parts");
   });
-  m.def("silu_bf16", [](const at::Tensor& y, at::Tensor& out) {
-    // y: bf16 [M, 2F] (gate/up interleaved per 16 columns) -> out bf16 [M, F] = silu(gate) * up
-    need(y, at::kBFloat16, "y");
-    need(out, at::kBFloat16, "out");
-    TORCH_CHECK(y.dim() == 2 && y.is_contiguous() && y.size(1) % 32 == 0, "silu_bf16: y [M, 2F] contiguous");
-    const int M = y.size(0), F = y.size(1) / 2;
-    TORCH_CHECK(out.is_contiguous() && out.numel() >= (int64_t)M * F, "silu_bf16: out too small");
-    check(lsa_silu_bf16(y.data_ptr(), M, F, out.data_ptr(), cur_stream()), "silu_bf16");
-  });
+  m.def("silu_bf16", &silu_bf16);
   m.def("ar_alloc", &ar_alloc);
   m.def("ar_free", [](int64_t p) { check(lsa_ar_free(reinterpret_cast<void*>(p)), "ar_free"); });
   m.def("ar_handle", &ar_handle);

@@ -137,6 +137,16 @@ int main() {
     expect_reject("res_add_ss parts too small", [&] { res_add_ss(hr, pr, 3, 4 * 1024, xr, 4, 1024, 0, ss1); });
     auto g = T({1000}, BF), u = T({1000}, BF), o = T({1000}, BF), us = T({999}, BF);
     expect_ok("silu_mul", [&] { silu_mul(g, u, o); });
+    {
+      auto y = T({4, 64}, BF), so = T({4, 32}, BF), small = T({4, 31}, BF), bad = T({4, 48}, BF);
+      expect_ok("silu_bf16", [&] { silu_bf16(y, so); });
+      expect_reject("silu_bf16 out too small", [&] { silu_bf16(y, small); });
+      expect_reject("silu_bf16 width not a multiple of 32", [&] { silu_bf16(bad, so); });
+      auto a = T({1024}, F32), b = T({64}, BF);
+      expect_ok("prefetch", [&] { prefetch({a, b}, {-1, 64}, 256); });
+      expect_reject("prefetch 5 tensors", [&] { prefetch({a, a, a, a, a}, {-1, -1, -1, -1, -1}, 256); });
+      expect_reject("prefetch byte counts", [&] { prefetch({a, b}, {-1}, 256); });
+    }
     expect_reject("silu_mul size mismatch", [&] { silu_mul(g, us, o); });
   }
   // ---- attention
