@@ -391,9 +391,10 @@ PREFILL_BLAS = True
 # the fused-SiLU gate_up prefill goes to the vendor GEMM (bf16 gate / up, the reference model's own rounding) + the
 # bf16 SiLU*up pass for 64 < M <= this many rows; above it the gemm_t256 SiLU epilogue stays ahead.  Measured
 # (profiles/r4/prefill_gateup_blas_silu_vs_t256_mi355x.jsonl, us, f32-out variant): 7B M=300 64.5 vs 89.8, 3B M=300
-# 43.0 vs 67.0, 7B M=1024 178.9 vs 185.9; end to end (profiles/r4/prefill_ab_silu_bf16_mi355x.jsonl): 3B 2k TTFT
-# 14.09 -> 13.86 ms, 7B 300 tokens 8.80 -> 8.27 ms, but 7B 4096 rows 49.5 -> 50.7 ms (hence the cap)
-PREFILL_BLAS_SILU_MAX_M = 2048
+# 43.0 vs 67.0, 7B M=1024 178.9 vs 185.9; end to end: 7B 300-token TTFT 8.80 -> 8.27 ms
+# (profiles/r4/prefill_ab_silu_bf16_mi355x.jsonl), while at 2048 rows the 256^2 kernel wins interleaved on one box
+# (3B 2k TTFT 13.61-13.72 vs 13.97-14.04 ms, profiles/r4/ttft_gateup_cap_ab_mi355x.jsonl)
+PREFILL_BLAS_SILU_MAX_M = 1024
 PREFILL_BLAS_SILU_BF16 = True
 # TP = 1 prefill: the vendor o / down GEMMs accumulate into the f32 residual (``blas_residual``)
 PREFILL_BLAS_RES = True
