@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restri
 // host launchers
 // ------------------------------------------------------------------------------------------------
 // Per-call tuning knobs (chosen by ops.pick_gemm_config from the measured table):
-//   waves 4|8 (16: one 16-row tile, nb <= 2) per workgroup; div 1|2|4 divides the chunk depth U (fewer VGPRs -> more resident waves;
+//   waves 4|8 per workgroup (a 16-wave variant for one 16-row tile never won a sweep: removed in round 4); div 1|2|4 divides the chunk depth U (fewer VGPRs -> more resident waves;
 //   on MI355X div 4 won most decode shapes, scripts/bench_gemm.py).
 static thread_local int g_skinny_waves = 4;
 static thread_local int g_skinny_div = 4;
@@ -396,16 +396,6 @@ static void launch_skinny_x(const uint16_t* X, int ldx, int M, int KB, const uin
     // reduction buffer is WAVES * NB * MT KiB
     if (g_skinny_div == 1) LSA_SKL(4, 1);
     else LSA_SKL(4, 2);
-  } else if (g_skinny_waves == 16) {
-    // batch <= 16 GEMV over few columns per workgroup (the residual epilogue's split-K-free grids): 16 waves keep
-    // the workgroup's whole weight slice in flight at once instead of 4 waves' 32 KiB -- a per-CU latency-bound
-    // stream on grids of N / 16 <= 256 workgroups
-    if constexpr (MT == 1 && NB <= 2 && !XF) {
-      if (g_skinny_div == 1) LSA_SKL(16, 1);
-      else LSA_SKL(16, 2);
-    } else {
-      LSA_SKL(4, 4);
-    }
   } else if (g_skinny_div == 2) {
     if (g_skinny_waves == 8) LSA_SKL(8, 2);
     else LSA_SKL(4, 2);
@@ -470,7 +460,7 @@ extern "C" int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf,
   if ((ep || epi == EPI_RES) && (M > 64 || (splitk > 1 && epi != EPI_F32 && epi != EPI_RES))) return -7;
   if (epi == EPI_RES && (!ep || !ep->h || !ep->xout || !ep->ss_out || ep->ldh != N || (splitk > 1 && !ep->tickets)))
     return -8;
-  g_skinny_waves = (waves == 8 || waves == 16) ? waves : 4;
+  g_skinny_waves = waves == 8 ? 8 : 4;
   g_skinny_div = (div == 1 || div == 2) ? div : 4;
   // xlds: 0 = row-major X, 2 = fragment-major X (ops.to_xfrag); the LDS-staged variant (1) was removed in
   // round 4 (measured slower than the register pipeline on every decode shape, ARCHITECTURE.md §4)

@@ -60,7 +60,7 @@ for name, (N, K, epi) in SHAPES.items():
         picked = ops.pick_gemm_config(M, N, K, epi, xf=xf, kind=KIND)
         res = {"shape": name, "M": M, "xf": xf, "kind": KIND, "picked": list(picked), "picked_us": round(timeit(call(picked)), 2)}
         best = None
-        for waves, dv in (((4, 1), (4, 2), (4, 4), (8, 2), (16, 1), (16, 2)) if KIND == "bf16" else ((4, 4),)):
+        for waves, dv in (((4, 1), (4, 2), (4, 4), (8, 2)) if KIND == "bf16" else ((4, 4),)):
             for nb in NBS:
                 if (N // 16) % nb or (epi == "silu" and nb % 2) or (M > 32 and nb > 2) or (nb == 6 and M <= 16):
                     continue

@@ -84,7 +84,7 @@ for name, (N, K) in ROWP.items():
                 if K // 32 // sk < 8:
                     continue
                 pb = torch.empty(sk, M, N, device=dev)
-                for waves, dv in (((4, 1), (4, 2), (4, 4), (8, 2), (16, 1), (16, 2)) if KIND == "bf16" else ((4, 4),)):
+                for waves, dv in (((4, 1), (4, 2), (4, 4), (8, 2)) if KIND == "bf16" else ((4, 4),)):
                     if nb >= 6 and (KIND != "bf16" or (waves, dv) not in ((4, 1), (4, 2))):
                         continue
                     if waves == 16 and (M > 16 or nb > 2):  # the 16-wave kernel: one row tile, nb <= 2
