@@ -225,6 +225,11 @@ _TUNING_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tu
 _tuning: Optional[dict] = None
 
 
+# experiment overrides of tuning entries (in-pipeline A/Bs: bench.py --set 'ops.TUNING_OVERRIDES={"key": {...}}'),
+# consulted before the measured table; empty in production
+TUNING_OVERRIDES: dict = {}
+
+
 def _tuning_table() -> dict:
     """Measured best decode-GEMM configs on MI355X ({"NxK:epi:s|m": {nb, splitk, waves, div}}),
     produced by scripts/bench_gemm.py (median of 3 interleaved runs per config)."""
@@ -235,7 +240,7 @@ def _tuning_table() -> dict:
                 _tuning = json.load(f)
         except (OSError, ValueError):
             _tuning = {}
-    return _tuning
+    return {**_tuning, **TUNING_OVERRIDES} if TUNING_OVERRIDES else _tuning
 
 
 def pick_gemm_config(M: int, N: int, K: int, epi: str, xf: bool = False,
