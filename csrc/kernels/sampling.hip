@@ -219,7 +219,9 @@ __global__ __launch_bounds__(1024) void sample_commit_kernel(const unsigned long
       const float x = __shfl_up(cumk, o, 64);
       if (i >= o) cumk += x;
     }
-    const float u = uniform01(seeds[b], (unsigned long long)st.gen_len[b] * 1315423911ull + b);
+    // draw g of a request depends on seed + g only (as ops/reference.py): a preempted request re-admitted with
+    // seed + len(resumed) continues the same stream, whatever slot it lands in
+    const float u = uniform01(seeds[b] + (unsigned long long)st.gen_len[b], 0ull);
     // first kept index whose cumulative mass exceeds u (fallback: last kept index)
     int first_hit = (keep && u < cumk) ? i : 64;
     int last_kept = keep ? i : -1;

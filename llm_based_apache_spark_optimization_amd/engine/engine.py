@@ -133,7 +133,11 @@ class LLMEngine:
         # kv_reserve_tokens: generated tokens reserved at admission (< 0: prompt + max_new up front, no growth)
         self.sched = native.Scheduler(runner.num_kv_blocks, BLOCK, runner.max_slots, max_prefill_tokens,
                                       runner.max_blocks, kv_reserve_tokens)
-        self._admit_hold = False  # set by a preemption: no admissions until a running request retires
+        # set by a preemption: no admissions while requests run and fewer than _admit_hold_blocks KV blocks are free
+        # (the preempted request's re-admission plus one block of growth per running request), so the preempted
+        # request is not re-admitted at once and evicted again by the same growth
+        self._admit_hold = False
+        self._admit_hold_blocks = 0
         self.sync_every = sync_every
         # decode steps per iteration when every running request ignores EOS: None = run to the first
         # length limit (offline batches); a server sets a bound so new arrivals are admitted promptly
@@ -204,9 +208,9 @@ class LLMEngine:
         with self._lock:
             # after a preemption, admit nothing while requests still run: the preempted one would otherwise be
             # re-admitted at once and evicted again by the same growth
-            admitted = [] if (self._admit_hold and self.sched.num_running > 0) else self.sched.admit()
-            if self.sched.num_running == 0:
+            if self._admit_hold and (self.sched.num_running == 0 or self.sched.free_blocks >= self._admit_hold_blocks):
                 self._admit_hold = False
+            admitted = [] if self._admit_hold else self.sched.admit()
             self.stats["peak_running"] = max(self.stats["peak_running"], self.sched.num_running)
             t0 = time.perf_counter()
             entries = []
@@ -217,7 +221,10 @@ class LLMEngine:
                 req.admitted = req.admitted or t0
                 self._slot_owner[slot] = rid
                 sp = req.params
-                seed = sp.seed if sp.seed is not None else (rid * 7919 + 17)
+                # a re-admitted (preempted) request continues its random stream where it stopped: the sampler draws
+                # token g from seed + g (ops/reference.py sample_commit, sampling.hip), and this incarnation's g
+                # restarts at 0 after len(resumed) tokens
+                seed = (sp.seed if sp.seed is not None else (rid * 7919 + 17)) + len(req.resumed)
                 entries.append(dict(slot=slot, blocks=self.sched.block_table(rid), limit=sp.max_tokens,
                                     temperature=sp.temperature, top_k=sp.top_k, top_p=sp.top_p, seed=seed,
                                     eos_on=not sp.ignore_eos, repeat_penalty=sp.repeat_penalty,
@@ -353,7 +360,10 @@ class LLMEngine:
         q.slot, q.gen_host, q.prefilled = -1, 0, 0
         q.preemptions += 1
         self.stats["preempted"] += 1
+        reserve = self.sched.reserve_tokens
+        gen = q.params.max_tokens if reserve < 0 else min(q.params.max_tokens, reserve)
         self._admit_hold = True
+        self._admit_hold_blocks = -(-(len(q.ctx_ids) + gen) // BLOCK) + self.sched.num_running
 
     def _trace_done(self, req: Request, n: int) -> None:
         """Engine spans of a finished request (queue -> prefill -> decode), fed to lsa_stage_seconds and,

@@ -242,7 +242,8 @@ def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_t
             toks[b] = int(row.argmax())
             continue
         idx, p = sample_probs(row, T, int(top_k[b]), float(top_p[b]))
-        if generator is None:
-            generator = torch.Generator().manual_seed(int(seeds[b]) + int(gen_len[b]))
-        toks[b] = int(idx[torch.multinomial(p.cpu(), 1, generator=generator)])
+        # draw g of a row comes from seed + g alone (one generator per row: a generator shared across rows made a
+        # row's draws depend on the rows sampled before it in the batch)
+        g = generator if generator is not None else torch.Generator().manual_seed(int(seeds[b]) + int(gen_len[b]))
+        toks[b] = int(idx[torch.multinomial(p.cpu(), 1, generator=g)])
     commit(toks, out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on, hist=hist)

@@ -3,8 +3,10 @@ tables as contexts cross 64-token boundaries, an exhausted arena preempts the yo
 re-admission).  CPU engine (fp32 reference ops) and the native scheduler; the Python fallback scheduler is held to
 the same semantics."""
 import pytest
+import torch
 
 from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build_engine
+from llm_based_apache_spark_optimization_amd.ops import reference as ref
 from llm_based_apache_spark_optimization_amd.runtime import native
 
 
@@ -85,3 +87,57 @@ def test_preemption_recomputes_identical_tokens():
     assert eng.stats["preempted"] >= 1 and any(q.preemptions for q in reqs)
     assert all(len(q.output_ids) == 150 for q in reqs)
     assert eng.sched.free_blocks == 8 and eng.sched.num_running == 0
+
+
+def test_preemption_keeps_seeded_sampling_stream():
+    """Sampling at temperature > 0 with a fixed seed: a request that is preempted and re-admitted continues its
+    random stream where it stopped (the resumed incarnation draws from seed + len(resumed)).  Its tokens after the
+    resume point follow the solo run's; they are compared over the first 8 only, because the re-prefill of the
+    generated tokens rounds the bf16 activations differently from the incremental decode, and a later draw that
+    lands near a CDF boundary may then flip (the unmodified stream diverges at once: every draw is shifted)."""
+    prompts = [[1] + list(range(3 + k, 40 + k)) for k in range(3)]
+    eng = build_engine("tiny-nsql", device="cpu", max_slots=3, max_model_len=512, num_kv_blocks=9)
+    sps = [SamplingParams(max_tokens=150, ignore_eos=True, temperature=0.9, top_k=40, top_p=0.95, seed=100 + k)
+           for k in range(3)]
+    solo = [eng.generate([p], sp)[0].token_ids for p, sp in zip(prompts, sps)]
+    eng.run_ahead = 16
+    reqs = [eng.add_request(p, sp) for p, sp in zip(prompts, sps)]
+    eng.run_until_done(reqs)
+    assert eng.stats["preempted"] >= 1 and any(q.preemptions for q in reqs)
+    for q, s in zip(reqs, solo):
+        if not q.preemptions:
+            assert q.output_ids == s
+        else:
+            n = len(q.resumed) + 8
+            assert q.output_ids[:n] == s[:n]
+
+
+def test_sampler_stream_depends_on_seed_plus_step():
+    """The reference sampler's draw for step g of a row comes from seed + g alone: (seed + R, g) == (seed, g + R),
+    whatever the other rows of the batch are."""
+    torch.manual_seed(0)
+    V, B = 300, 3
+    logits = torch.randn(B, V)
+    args = dict(temperature=torch.full((B,), 0.9), top_k=torch.full((B,), 50, dtype=torch.int32),
+                top_p=torch.full((B,), 0.95))
+
+    def draw(seeds, gl):
+        st = [torch.zeros(B, 32, dtype=torch.int32), torch.tensor(gl, dtype=torch.int32),
+              torch.zeros(B, dtype=torch.int32), torch.zeros(B, dtype=torch.int32), torch.zeros(B, dtype=torch.int32)]
+        ref.sample_commit(logits.clone(), None, None, args["temperature"], args["top_k"], args["top_p"],
+                          torch.tensor(seeds), st[0], st[1], st[2], st[3], st[4], torch.tensor([-1]))
+        return [int(st[0][b, gl[b]]) for b in range(B)]
+
+    toks = [draw([7 + R, 11, 13], [3, 0, 0])[0] for R in range(20)]
+    assert toks == [draw([7, 11, 13], [3 + R, 0, 0])[0] for R in range(20)]
+    assert draw([7, 11, 13], [3, 0, 0])[0] == draw([7, 99, 5], [3, 2, 1])[0]
+
+
+def test_admission_hold_clears_on_free_blocks():
+    """After a preemption the engine holds admissions only until enough KV blocks are free for the preempted
+    request plus one block of growth per running request, not until a running request retires."""
+    eng = build_engine("tiny-nsql", device="cpu", max_slots=3, max_model_len=512, num_kv_blocks=9)
+    eng._admit_hold, eng._admit_hold_blocks = True, 1
+    q = eng.add_request([1, 5, 6, 7], SamplingParams(max_tokens=4, ignore_eos=True))
+    eng.run_until_done([q])
+    assert not eng._admit_hold and len(q.output_ids) == 4
