@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #endif
 
+#include "kernels/gemm_sk.h"
 #include "kernels/lsa_epi.h"
 
 extern "C" {
@@ -62,10 +63,8 @@ int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, vo
                  int waves, int div, int xlds, hipStream_t stream);
 int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
-int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int splitk,
-                  hipStream_t stream);
-int lsa_gemm_t256x(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int xf_tiles,
-                   hipStream_t stream);
+int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
+                int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 int lsa_silu_bf16(const void* y, int M, int F, void* out, hipStream_t s);
 void lsa_fp8_gemm_knobs(int waves, int depth);
@@ -322,43 +321,36 @@ void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) 
         "quant_xf8");
 }
 
-// large-M (prefill) linear layer on the 256x256 tile kernel (kernels/gemm_tile256.hip)
-void gemm_t256(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, int64_t splitk) {
+// large-M (prefill) linear layer on the stream-K 256x256 tile kernel (kernels/gemm_tile256.hip).  epi: 0 bf16 [M][N],
+// 1 f32 [M][N], 2 SiLU(gate) * up bf16 [M][N / 2], 3 h f32 [M][N] += x @ W^T.  ws / tickets: the per-stream
+// workspace (ops._sk_workspace).  cfg: -1 = the kernel's cost model, else a tile configuration index (+ 8: whole
+// tiles only).  Returns grid * 16 + the configuration used.
+int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, at::Tensor& ws,
+                at::Tensor& tickets, int64_t ncu, int64_t min_share, int64_t cfg) {
   need(x, at::kBFloat16, "x");
   need(wf, at::kBFloat16, "wf");
+  need(ws, at::kFloat, "ws");
+  need(tickets, at::kInt, "tickets");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
   const int M = x.size(0), K = x.size(1);
-  TORCH_CHECK(wf.numel() == N * K, "weight numel mismatch");
-  TORCH_CHECK(splitk >= 1 && (splitk == 1 || epi == 1), "gemm_t256: only the f32 epilogue splits K");
-  if (epi == 1) {
+  TORCH_CHECK(M > 0 && N > 0 && wf.numel() == N * K, "weight numel mismatch");
+  TORCH_CHECK(ncu >= 8 && ncu <= 1024, "gemm_sk: ncu out of range");
+  TORCH_CHECK(ws.numel() * 4 >= lsa_gemm_sk_ws_bytes((int)ncu) && tickets.numel() >= lsa_gemm_sk_tickets((int)ncu),
+              "gemm_sk: workspace too small");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_sk: epi");
+  if (epi == 1 || epi == 3) {
     need(out, at::kFloat, "out");
-    TORCH_CHECK(out.numel() >= splitk * M * N, "f32 out too small for the slabs");
+    TORCH_CHECK(out.numel() >= (int64_t)M * N, "f32 out too small");
   } else {
     need(out, at::kBFloat16, "out");
-    TORCH_CHECK(out.numel() >= M * (epi == 2 ? N / 2 : N), "bf16 out too small");
+    TORCH_CHECK(out.numel() >= (int64_t)M * (epi == 2 ? N / 2 : N), "bf16 out too small");
   }
-  check(lsa_gemm_t256(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, (int)splitk, cur_stream()),
-        "gemm_t256");
-}
-
-// the 256^2 tile GEMM over fragment-major X (xf: [K / 32][xf_tiles][64][8] bf16, rows >= M zero or ignored)
-void gemm_t256_xf(const at::Tensor& xf, int64_t xf_tiles, int64_t M, const at::Tensor& wf, int64_t N, at::Tensor& out,
-                  int64_t epi) {
-  need(xf, at::kBFloat16, "xf");
-  need(wf, at::kBFloat16, "wf");
-  TORCH_CHECK(N > 0 && wf.numel() % N == 0, "weight numel mismatch");
-  const int64_t K = wf.numel() / N;
-  TORCH_CHECK(M > 0 && xf_tiles * 16 >= M && xf.is_contiguous() && xf.numel() >= xf_tiles * 16 * K,
-              "fragment-major x too small");
-  if (epi == 1) {
-    need(out, at::kFloat, "out");
-    TORCH_CHECK(out.numel() >= M * N, "f32 out too small");
-  } else {
-    need(out, at::kBFloat16, "out");
-    TORCH_CHECK(out.numel() >= M * (epi == 2 ? N / 2 : N), "bf16 out too small");
-  }
-  check(lsa_gemm_t256x(xf.data_ptr(), 0, M, K, wf.data_ptr(), N, out.data_ptr(), epi, xf_tiles, cur_stream()),
-        "gemm_t256_xf");
+  TORCH_CHECK(cfg >= -1 && cfg < 16, "gemm_sk: cfg");
+  int grid = 0, used = 0;
+  check(lsa_gemm_sk(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), (int)epi, ws.data_ptr<float>(),
+                    tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, &grid, &used, cur_stream()),
+        "gemm_sk");
+  return (int64_t)grid * 16 + used;
 }
 
 void fp8_gemm(const at::Tensor& x, const at::Tensor& wq, const at::Tensor& wscale, int64_t N, at::Tensor& out,
@@ -826,8 +818,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_xf", &gemm_xf, py::arg("xf"), py::arg("M"), py::arg("K"), py::arg("wf"), py::arg("N"), py::arg("out"),
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
-  m.def("gemm_t256", &gemm_t256, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"),
-        py::arg("splitk") = 1);
+  m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("ws"),
+        py::arg("tickets"), py::arg("ncu"), py::arg("min_share") = 0, py::arg("cfg") = -1);
+  m.def("gemm_sk_ws_bytes", [](int64_t ncu) { return lsa_gemm_sk_ws_bytes((int)ncu); });
+  m.def("gemm_sk_tickets", [](int64_t ncu) { return (int64_t)lsa_gemm_sk_tickets((int)ncu); });
   m.def("fp4_gemm", &fp4_gemm, py::arg("x"), py::arg("wq"), py::arg("sw"), py::arg("N"), py::arg("out"), py::arg("epi"),
         py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("rowss") = py::none(), py::arg("eps") = 1e-5,
         py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(),
@@ -837,7 +831,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(),
         py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("fp4_dequant", &fp4_dequant);
-  m.def("gemm_t256_xf", &gemm_t256_xf);
   m.def("fp8_gemm", &fp8_gemm, py::arg("x"), py::arg("wq"), py::arg("wscale"), py::arg("N"), py::arg("out"),
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("depth") = 1,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());

@@ -261,118 +261,6 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
 }
 
 // ------------------------------------------------------------------------------------------------
-// prefill / large-M kernel: 128 (N) x 128 (M) x 64 (K) tile, 4 waves (2 x 2) of 64 x 64
-// ------------------------------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-__device__ __forceinline__ void glds16(const void* g, void* l) {
-  __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)l, 16, 0, 0);
-}
-
-template <int EPI>
-__global__ __launch_bounds__(256) void gemm_tile_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KBtot,
-                                                        const uint4* __restrict__ Wf, int NBtot,
-                                                        void* __restrict__ out, int ldo, int kb_per_split) {
-  // [stage][operand 0 = W, 1 = X][frag = sub * 2 + kf][lane]
-  __shared__ __attribute__((aligned(16))) uint4 lds[2][2][16][64];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int nbase = blockIdx.x * 8;
-  const int mbase = blockIdx.y * 128;
-  // split-K (f32 slabs only): blockIdx.z owns k-blocks [kbA, kbA + KB) of the KBtot; small prefill grids
-  // (M <= 512: O / down have only N / 128 tiles) would otherwise stream all of K on a few dozen CUs
-  const int kbA = blockIdx.z * kb_per_split;
-  const int KB = min(KBtot - kbA, kb_per_split);
-
-  // staging sources: this wave stages frags f = 4w .. 4w+3 of each operand
-  const uint4* wsrc[4];
-  const uint16_t* xsrc[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int f = 4 * w + q;
-    const int sub = f >> 1, kf = f & 1;
-    const int nb = min(nbase + sub, NBtot - 1);
-    wsrc[q] = Wf + ((size_t)nb * KBtot + kbA + kf) * 64 + lane;
-    const int m = min(mbase + sub * 16 + (lane & 15), M - 1);
-    xsrc[q] = X + (size_t)m * ldx + (size_t)(kbA + kf) * 32 + 8 * (lane >> 4);
-  }
-
-  auto stage = [&](int st, int kb0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int f = 4 * w + q;
-      const int kf = f & 1;
-      const int kbo = min(kb0 + kf, KB - 1) - kf;  // clamp the odd tail fragment (masked in compute)
-      glds16(wsrc[q] + (size_t)kbo * 64, &lds[st][0][f][0]);
-      glds16(xsrc[q] + (size_t)kbo * 32, &lds[st][1][f][0]);
-    }
-  };
-
-  f32x4_t acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int T = (KB + 1) >> 1;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < T; ++t) {
-    const int st = t & 1;
-    if (t + 1 < T) stage(st ^ 1, 2 * (t + 1));
-    const int nkf = min(2, KB - 2 * t);
-#pragma unroll
-    for (int kf = 0; kf < 2; ++kf) {
-      if (kf < nkf) {
-        uint4 a[4], b[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = lds[st][0][(wn * 4 + i) * 2 + kf][lane];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = lds[st][1][(wm * 4 + j) * 2 + kf][lane];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  const int g = lane >> 4;
-  if constexpr (EPI == EPI_SILU) {
-#pragma unroll
-    for (int i = 0; i < 4; i += 2) {
-      const int nb = nbase + wn * 4 + i;  // even -> gate block, nb + 1 -> up block
-      if (nb + 1 >= NBtot) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = mbase + (wm * 4 + j) * 16 + (lane & 15);
-        if (m >= M) continue;
-        f32x4_t v;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = silu(acc[i][j][q]) * acc[i + 1][j][q];
-        store4<EPI_SILU>(out, ldo, 0, m, (nb >> 1) * 16 + 4 * g, v);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int nb = nbase + wn * 4 + i;
-      if (nb >= NBtot) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = mbase + (wm * 4 + j) * 16 + (lane & 15);
-        if (m >= M) continue;
-        store4<EPI>(out, ldo, (size_t)blockIdx.z * M * ldo, m, nb * 16 + 4 * g, acc[i][j]);
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
 // Per-call tuning knobs (chosen by ops.pick_gemm_config from the measured table):
@@ -437,8 +325,6 @@ static void launch_skinny_e(const uint16_t* X, int ldx, int M, int KB, const uin
 
 extern "C" int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
                             int splitk, int waves, int div, int xlds, hipStream_t stream);
-extern "C" int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi,
-                             int splitk, hipStream_t stream);
 
 extern "C" int lsa_gemm(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, int nb,
                         int splitk, hipStream_t stream) {
@@ -490,29 +376,7 @@ extern "C" int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf,
       default: return -4;
     }
   } else {
-    if (splitk < 1) splitk = 1;
-    if (splitk != 1 && (epi != EPI_F32 || splitk > KB)) return -3;
-    // the 256^2 8-phase kernel (gemm_tile256.hip) once its grid fills half the CUs; measured 1.2-1.34 PF
-    // vs 0.73-0.86 PF for the 128^2 tile at the 7B/3B prefill shapes (scripts/bench_prefill_gemm.py)
-    if (splitk == 1 && ((M + 255) / 256) * ((NBtot + 15) / 16) >= 128 && (epi != EPI_SILU || NBtot % 2 == 0))
-      return lsa_gemm_t256(X, ldx, M, K, Wf, N, out, epi, 1, stream);
-    // from 1024 rows a small 256^2 grid splits K instead of falling back to the 128^2 tile (ops.tile_splitk)
-    if (splitk > 1 && epi == EPI_F32 && M >= 1024) return lsa_gemm_t256(X, ldx, M, K, Wf, N, out, epi, splitk, stream);
-    const int kbps = (KB + splitk - 1) / splitk;
-    if ((KB + kbps - 1) / kbps != splitk) return -3;  // every slab must own >= 1 k-block (no unwritten slab)
-    dim3 grid((NBtot + 7) / 8, (M + 127) / 128, splitk);
-    switch (epi) {
-      case EPI_BF16:
-        hipLaunchKernelGGL(gemm_tile_kernel<EPI_BF16>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, kbps);
-        break;
-      case EPI_F32:
-        hipLaunchKernelGGL(gemm_tile_kernel<EPI_F32>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, kbps);
-        break;
-      case EPI_SILU:
-        hipLaunchKernelGGL(gemm_tile_kernel<EPI_SILU>, grid, dim3(256), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, kbps);
-        break;
-      default: return -4;
-    }
+    return -9;  // M > 64: the stream-K prefill kernel (gemm_tile256.hip lsa_gemm_sk)
   }
   return (int)hipGetLastError();
 }

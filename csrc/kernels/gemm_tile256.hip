@@ -1,21 +1,35 @@
-// Prefill / large-M linear layers on MFMA:  out[M, N] = X[M, K] @ W[N, K]^T   (bf16 in, f32 accumulate)
+// Prefill / large-M linear layers on MFMA:  out[M, N] = X[M, K] @ W[N, K]^T   (bf16 in, f32 accumulate),
+// stream-K over 256 x 256 output tiles.
 //
-// 256 x 256 output tile per workgroup, 8 waves (2 along M x 4 along N, 128 x 64 each), BK = 64, one
-// workgroup per CU (128 KiB of LDS), on the MI355X guide's recipe for breaking the ~900 TF ceiling of
-// the 128^2 two-barrier structure (cdna_hip_programming.md §5 "The 256^2 8-phase template"):
-//   * both operands staged with global_load_lds (16 B per lane, 1 KiB per wave-instruction) into ONE
-//     __shared__ array; fragment reads are inline-asm ds_read_b128 (hipcc would otherwise drain vmcnt(0)
-//     before every compiler-visible LDS read while a DMA is in flight);
-//   * four phases per K-tile, each: a quadrant's fragment reads, one half-tile of prefetch, raw
-//     s_barrier, 16 MFMAs under s_setprio(1), s_barrier; one counted `s_waitcnt vmcnt(4)` per K-tile,
-//     never vmcnt(0) inside the loop, so two half-tiles stay in flight across every barrier;
-//   * LDS images are fragment-major (W is already stored that way, ops.shuffle_weight; X fragments are
-//     gathered lane-wise by the DMA addresses), so every ds_read_b128 is lane-linear and conflict-free
-//     without a swizzle;
-//   * XCD-aware bijective tile remap: each XCD gets a contiguous run of tiles, M fastest, so the tiles
-//     that share a W column panel run on the same L2.
-// Epilogues as gemm.hip: EPI_BF16, EPI_F32 (one slab), EPI_SILU (gate/up rows interleaved per 16).
+// Tile body (unchanged from round 3): 8 waves (2 along M x 4 along N, 128 x 64 each), BK = 64, one workgroup per CU
+// (128 KiB of LDS), the MI355X guide's recipe for breaking the ~900 TF ceiling of the 128^2 two-barrier structure
+// (cdna_hip_programming.md §5 "The 256^2 8-phase template"):
+//   * both operands staged with global_load_lds (16 B per lane, 1 KiB per wave-instruction) into ONE __shared__
+//     array; fragment reads are inline-asm ds_read_b128 (hipcc would otherwise drain vmcnt(0) before every
+//     compiler-visible LDS read while a DMA is in flight);
+//   * four phases per K-tile, each: a quadrant's fragment reads, one half-tile of prefetch, raw s_barrier, 16 MFMAs
+//     under s_setprio(1), s_barrier; one counted `s_waitcnt vmcnt(4)` per K-tile, never vmcnt(0) inside the loop;
+//   * LDS images are fragment-major (W is stored that way, ops.shuffle_weight; X fragments are gathered lane-wise by
+//     the DMA addresses), so every ds_read_b128 is lane-linear and conflict-free without a swizzle.
+//
+// Decomposition (round 5): a persistent grid of one workgroup per CU walks the (tile, K-tile) iteration space.
+//   * Data-parallel part: whole tiles, one per workgroup per round.
+//   * Stream-K part: the last (tiles mod CUs) + CUs tiles (all of them when the grid has fewer tiles than CUs) are
+//     cut by K-tile ranges, every workgroup taking an equal share of their iterations, so no CU idles in a partial
+//     last round (3B 2k prefill: 96 / 160 tiles on 256 CUs; 7B gate_up at 4096 rows: 1376 tiles = 5.4 rounds).
+//     A workgroup that covers only part of a tile publishes its f32 partial write-through (sc1), takes the tile's
+//     ticket, and the last to arrive sums every contributor's partial in contributor order (so the rounding does
+//     not depend on who arrives last) and runs the epilogue -- the counter hand-off of MI355X_MICROARCH.md "Valid
+//     forms", row 1; nothing ever waits on another workgroup, so the kernel cannot deadlock whatever the residency.
+//   * Virtual CU index: consecutive indices share an XCD (blocks b and b + 8 do), so a run of consecutive tiles
+//     (one W column panel, neighbouring X row tiles) meets in one L2.
+// Epilogues: EPI_BF16, EPI_F32 (plain f32 store), EPI_SILU (gate / up rows interleaved per 16, bf16 SiLU(g) * u),
+// EPI_RES (h[M][N] f32 += acc: the o / down projections accumulate into the residual stream, the norm after them
+// reads h alone).
 #include "common.h"
+#include "gemm_sk.h"
+
+#include <type_traits>
 
 #define EPI_BF16 0
 #define EPI_F32 1
@@ -29,9 +43,9 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)l, 16, 0, 0);
 }
 
-// ds_read_b128 as inline asm: hipcc treats an LDS-DMA in flight as a pending write to every LDS
-// location and would drain vmcnt(0) before each compiler-visible ds_read, serialising the prefetch
-// with the compute.  The asm read is ordered by the explicit counted waits + raw barriers instead.
+// ds_read_b128 as inline asm: hipcc treats an LDS-DMA in flight as a pending write to every LDS location and would
+// drain vmcnt(0) before each compiler-visible ds_read, serialising the prefetch with the compute.  The asm read is
+// ordered by the explicit counted waits + raw barriers instead.
 __device__ __forceinline__ u32x4_t ds_read16(const void* p) {
   u32x4_t v;
   const uint32_t a = (uint32_t)(uintptr_t)(lds_ptr_t)p;
@@ -39,251 +53,478 @@ __device__ __forceinline__ u32x4_t ds_read16(const void* p) {
   return v;
 }
 
-template <int EPI>
-__device__ __forceinline__ void store_out(void* out, int ldo, int m, int n, const f32x4_t& v) {
-  if constexpr (EPI == EPI_F32) {
-    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
-  } else {
-    uint2 p;
-    p.x = pack2bf(v[0], v[1]);
-    p.y = pack2bf(v[2], v[3]);
-    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + (size_t)m * ldo + n) = p;
-  }
+// the same with a compile-time byte offset in the instruction's 16-bit immediate field (no address VALU)
+template <int OFF>
+__device__ __forceinline__ u32x4_t ds_read16_off(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds_read offset field");
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF) : "memory");
+  return v;
+}
+
+// N consecutive fragments (1 KiB apart) of LDS half HALF, starting at fragment 0 of the wave's base address
+template <int HALF, int... Is>
+__device__ __forceinline__ void ds_read_frags(u32x4_t* r, uint32_t base, std::integer_sequence<int, Is...>) {
+  ((r[Is] = ds_read16_off<(HALF * 16 + Is) * 1024>(base)), ...);
+}
+
+struct SkPlan {
+  int ntm;              // 256-row tiles
+  int ntiles;           // output tiles (row tile fastest)
+  int T;                // K-tiles of 64 per output tile
+  int sk_tiles;         // tiles [0, sk_tiles) are stream-K, the rest data-parallel
+  int sk_iters;         // sk_tiles * T (host-checked: sk_iters * (grid + 1) < 2^31, so 32-bit index math)
+};
+
+// first stream-K iteration of virtual CU c
+__device__ __forceinline__ int sk_start(int c, int iters, int P) { return (int)((unsigned)(c * iters) / (unsigned)P); }
+// virtual CU whose range holds iteration g: the largest c with sk_start(c) <= g
+__device__ __forceinline__ int sk_owner(int g, int iters, int P) {
+  return (int)((unsigned)((g + 1) * P + iters - 1) / (unsigned)iters) - 1;
+}
+// partial slot of virtual CU c's segment in tile t: 2c for the segment that opens c's range, 2c + 1 for the one
+// that closes it (a range meets at most two partial tiles: its first and its last)
+__device__ __forceinline__ int sk_slot(int c, int t, int iters, int P, int T) {
+  return 2 * c + (t == sk_start(c, iters, P) / T ? 0 : 1);
 }
 
 }  // namespace
 
-// LDS: [buffer][half][fragment][lane].  Halves are cut by the C-quadrant that reads them, so each one
-// falls free at a different phase and can be restaged while the rest of its tile is still in use:
-//   half 0 = XQ0: X rows {0-63, 128-191} of the tile   (read in phase 1)
-//   half 1 = XQ1: X rows {64-127, 192-255}              (read in phase 3)
-//   half 2 = WQ0: W n-blocks {0,1, 4,5, 8,9, 12,13}     (read in phases 1 and 4)
-//   half 3 = WQ1: W n-blocks {2,3, 6,7, 10,11, 14,15}   (read in phase 2)
-// fragment within an X half: (wr * 4 + i) * 2 + ks;  within a W half: (wc * 2 + j) * 2 + ks.
-//
-// Four phases per K-tile t (quadrant (qm, qn) of each wave's 128 x 64 output, 16 MFMAs each):
-//   P1 (0,0): read XQ0 + WQ0 (12 x ds_read_b128)   stage XQ1(t+1)
-//   P2 (0,1): read WQ1 (4)                           stage WQ0(t+1)
-//   P3 (1,1): read XQ1 (8)                           stage XQ0(t+2)
-//   P4 (1,0): read WQ0 (4)                           stage WQ1(t+2), then s_waitcnt vmcnt(4): tile t+1 landed
-// Every restage comes >= 2 phases after the last read of that half (WAR); every read comes a phase after
-// the wait that retired it (RAW) - cdna_hip_programming.md §5, 8-phase template rules.  Tiles past the
-// end are staged from clamped addresses (never read) so the counted wait stays exact.
-// XF: X is fragment-major too, Xf[K / 32][mtt][64 lanes][8] (ops.to_xfrag layout with mtt 16-row tiles): every
-// X staging DMA then reads one contiguous 1 KiB fragment (8 full 128-B lines) instead of 16 rows x 64 B
-template <int EPI, bool XF = false>
-__global__ __launch_bounds__(512) void gemm_t256_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
-                                                        const uint4* __restrict__ Wf, int NBtot,
-                                                        void* __restrict__ out, int ldo, int ntm, int kts) {
+// Tile geometry: BM rows (128 | 256) x WN * 64 columns (WN n-blocks of 16 per wave: 2 | 3 | 4), 8 waves as 2 (M) x 4
+// (N), each wave owning (BM / 2) x (WN * 16).  A wave's output splits into quadrants (qm, qn): qm halves its rows,
+// qn its n-blocks (NQ0 = ceil(WN / 2), NQ1 = WN / 2).  The operands are staged as four LDS halves, each falling free
+// at a different phase so it can be restaged while the rest of its K-tile is still in use:
+//   half 0 = XQ0: every wave row-group's first BM / 4 rows   (read in phase 1)
+//   half 1 = XQ1: the other BM / 4 rows                       (read in phase 3)
+//   half 2 = WQ0: every wave's first NQ0 n-blocks            (read in phases 1 and 4)
+//   half 3 = WQ1: every wave's last NQ1 n-blocks             (read in phase 2)
+// fragment (1 KiB, one 16 x 32 MFMA operand) within an X half: (wr * MI + i) * 2 + ks; within a W half
+// (wc * NQ + j) * 2 + ks.  Each wave moves (half fragments) / 8 of them per half-stage, one global_load_lds each.
+template <int BM, int WN>
+struct TileCfg {
+  static constexpr int MI = BM / 64;                      // 16-row fragments per M quadrant of a wave
+  static constexpr int NQ0 = (WN + 1) / 2, NQ1 = WN / 2;  // n-blocks per N quadrant of a wave
+  static constexpr int XF = 4 * MI;                       // fragments per X half
+  static constexpr int WF0 = 8 * NQ0, WF1 = 8 * NQ1;      // fragments per W half
+  static constexpr int GX = XF / 8, GW0 = WF0 / 8, GW1 = WF1 / 8;  // glds per wave per half-stage
+  static constexpr int WAIT = GX + GW1;  // the K-tile-(t+2) loads a wave has in flight after phase 4's stage
+  static constexpr int NBT = 4 * WN;     // n-blocks per tile
+};
+
+template <int BM, int WN, int EPI>
+__global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
+                                                      const uint4* __restrict__ Wf, int NBtot,
+                                                      void* __restrict__ out, int ldo, SkPlan pl,
+                                                      float* __restrict__ ws, int* __restrict__ tickets) {
+  using C = TileCfg<BM, WN>;
+  constexpr int MI = C::MI, NQ0 = C::NQ0, NQ1 = C::NQ1;
+  static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF <= 16 && C::WF0 <= 16, "tile geometry");
+  static_assert(EPI != EPI_SILU || WN % 2 == 0, "SiLU pairs (gate, up) n-blocks inside one wave");
   __shared__ __attribute__((aligned(16))) uint4 lds[2][4][16][64];
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;  // 0..7
+  // wave ids through readfirstlane: provably uniform, so every per-wave address term lives in SGPRs
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0..7
   const int wm = w >> 2, wn = w & 3;
-
-  // XCD-aware bijective remap (consecutive ids go round-robin over the 8 XCDs)
-  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  // split-K (EPI_F32 only, kts > 0): workgroup = (output tile, K split); split s covers K-tiles [s*kts, (s+1)*kts)
-  // and writes f32 slab s (the consumer sums the slabs)
-  const int ntiles = ntm * ((NBtot + 15) >> 4);
-  const int split = kts > 0 ? wgid0 / ntiles : 0;
-  const int wgid = kts > 0 ? wgid0 - split * ntiles : wgid0;
-  const int tm = wgid % ntm, tn = wgid / ntm;
-  const int mbase = tm * 256, nbase = tn * 16;  // first row / first n-block
-
-  const int T = (KB + 1) >> 1;  // K-tiles of the whole product
-  const int kt0 = kts > 0 ? split * kts : 0;
-  const int Tl = kts > 0 ? min(T, kt0 + kts) - kt0 : T;  // this workgroup's K-tiles (>= 1: host-checked)
+  const int P = gridDim.x, b = blockIdx.x, xcd = b & 7;
+  const int q8 = P >> 3, r8 = P & 7;
+  const int vc = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int T = pl.T;
   const bool odd_tail = KB & 1;  // the last K-tile has one k-step (its second fragments re-read the first)
   const int r16 = lane & 15, c16 = 8 * (lane >> 4);
-  // stage half h of K-tile t (clamped to the last tile) into buffer t & 1: this wave moves fragments
-  // 2w and 2w + 1 of the half, one global_load_lds (1 KiB) each
-  auto stage = [&](int h, int t) {
-    const int tc = kt0 + min(t, Tl - 1);  // global K-tile (clamped to this split's last)
-    const int buf = t & 1;
+
+  // operand staging by buffer_load ... lds: the per-lane byte offset of each staged fragment is fixed for a segment
+  // (one VGPR each), the K-tile's offset rides in the SGPR soffset -- no VALU per load in the K loop
+  // (byte-exact ranges: an odd K's missing last k-step is staged from past the end, which the buffer unit reads as
+  // zeros, so the MFMAs of that k-step add nothing and the K loop has no odd-tail branch)
+  const int xbytes = ((M - 1) * ldx + KB * 32) * 2, wbytes = NBtot * KB * 1024;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, wbytes, 0x00020000);
+  int vx[2][C::GX], vw0[C::GW0], vw1[C::GW1];
+  int kt0 = 0, Tl = 1;  // the segment's K-tiles [kt0, kt0 + Tl)
+  int mbase = 0, nbase = 0;
+
+  // fragment f of a half: X (wr * MI + i) * 2 + ks, W (wc * NQ + j) * 2 + ks; this wave stages f = per * w + e
+  auto setup = [&](int tile) {
+    const int tm = tile % pl.ntm, tn = tile / pl.ntm;
+    mbase = tm * BM;
+    nbase = tn * C::NBT;
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int f = 2 * w + e;  // fragment index in the half
-      const int ks = (odd_tail && tc == T - 1) ? 0 : (f & 1);
-      const int kstep = 2 * tc + ks;
-      const char* g;
-      if (h < 2) {  // X half h (qm = h): fragment (wr * 4 + i) * 2 + ks
-        const int wi = f >> 1, wr = wi >> 2, i = wi & 3;
-        if constexpr (XF) {  // ldx = row tiles of the fragment-major X
-          const int rt = min((mbase + wr * 128 + h * 64 + i * 16) >> 4, ldx - 1);
-          g = reinterpret_cast<const char*>(X + (((size_t)kstep * ldx + rt) * 64 + lane) * 8);
-        } else {
-          const int row = min(mbase + wr * 128 + h * 64 + i * 16 + r16, M - 1);
-          g = reinterpret_cast<const char*>(X + (size_t)row * ldx + kstep * 32 + c16);
-        }
-      } else {      // W half h - 2 (qn): fragment (wc * 2 + j) * 2 + ks -> n-block wc * 4 + qn * 2 + j
-        const int wj = f >> 1, wc = wj >> 1, j = wj & 1;
-        const int nb = min(nbase + wc * 4 + (h - 2) * 2 + j, NBtot - 1);
-        g = reinterpret_cast<const char*>(Wf + ((size_t)nb * KB + kstep) * 64) + lane * 16;
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < C::GX; ++e) {
+        const int f = C::GX * w + e, wi = f >> 1, ks = f & 1, wr_ = wi / MI, i = wi % MI;
+        const int row = min(mbase + wr_ * (BM / 2) + h * (BM / 4) + i * 16 + r16, M - 1);
+        vx[h][e] = (row * ldx + c16) * 2 + ks * 64;
       }
-      glds16(g, &lds[buf][h][f][0]);
+#pragma unroll
+    for (int e = 0; e < C::GW0; ++e) {
+      const int f = C::GW0 * w + e, wj = f >> 1, ks = f & 1, wc = wj / NQ0, j = wj % NQ0;
+      const int nb = min(nbase + wc * WN + j, NBtot - 1);
+      vw0[e] = (nb * KB + ks) * 1024 + lane * 16;
+    }
+#pragma unroll
+    for (int e = 0; e < C::GW1; ++e) {
+      const int f = C::GW1 * w + e, wj = f >> 1, ks = f & 1, wc = wj / NQ1, j = wj % NQ1;
+      const int nb = min(nbase + wc * WN + NQ0 + j, NBtot - 1);
+      vw1[e] = (nb * KB + ks) * 1024 + lane * 16;
+    }
+  };
+  // stage half H of segment K-tile t (clamped to the segment's last) into buffer B
+  auto stage = [&](auto Hc, auto Bc, int t) {
+    constexpr int H = decltype(Hc)::value, B = decltype(Bc)::value;
+    const int tc = kt0 + min(t, Tl - 1);
+    const bool last_odd = odd_tail && tc == T - 1;  // its second k-step does not exist: stage zeros
+    constexpr int per = H < 2 ? C::GX : (H == 2 ? C::GW0 : C::GW1);
+#pragma unroll
+    for (int e = 0; e < per; ++e) {
+      const int f = per * w + e;
+      const bool oob = last_odd && (f & 1);
+      void* dst = &lds[B][H][f][0];
+      if constexpr (H < 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, vx[H][e], oob ? xbytes : tc * 128, 0, 0);
+      else if constexpr (H == 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)dst, 16, vw0[e], oob ? wbytes : tc * 2048, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)dst, 16, vw1[e], oob ? wbytes : tc * 2048, 0, 0);
     }
   };
 
-  f32x4_t acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  u32x4_t xr[4][2], wr[2][2];  // X fragments of one M quadrant, W fragments of one N quadrant
-  auto read_x = [&](int buf, int qm) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) xr[i][ks] = ds_read16(&lds[buf][qm][(wm * 4 + i) * 2 + ks][lane]);
+  f32x4_t acc[2 * MI][WN];
+  // X fragments of one M quadrant, W fragments of one N quadrant: [i or j][ks] flattened as i * 2 + ks
+  u32x4_t xr[MI * 2], wr[NQ0 * 2];
+  // fragment reads: one base VGPR per (operand, buffer), the half / fragment offset as the ds_read immediate
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)&lds[0][0][0][0] + lane * 16;
+  const uint32_t xb[2] = {lds0 + wm * MI * 2 * 1024, lds0 + wm * MI * 2 * 1024 + 65536};
+  const uint32_t wb0[2] = {lds0 + wn * NQ0 * 2 * 1024, lds0 + wn * NQ0 * 2 * 1024 + 65536};
+  const uint32_t wb1[2] = {lds0 + wn * NQ1 * 2 * 1024, lds0 + wn * NQ1 * 2 * 1024 + 65536};
+  auto read_x = [&](auto Bc, auto QMc) {
+    constexpr int B = decltype(Bc)::value, QM = decltype(QMc)::value;
+    ds_read_frags<QM>(xr, xb[B], std::make_integer_sequence<int, MI * 2>{});
   };
-  auto read_w = [&](int buf, int qn) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) wr[j][ks] = ds_read16(&lds[buf][2 + qn][((wn * 2 + j) * 2) + ks][lane]);
+  auto read_w = [&](auto Bc, auto QNc) {
+    constexpr int B = decltype(Bc)::value, QN = decltype(QNc)::value;
+    if constexpr (QN == 0)
+      ds_read_frags<2>(wr, wb0[B], std::make_integer_sequence<int, NQ0 * 2>{});
+    else
+      ds_read_frags<3>(wr, wb1[B], std::make_integer_sequence<int, NQ1 * 2>{});
   };
-  auto mma = [&](int qm, int qn, int nks) {
+  auto mma = [&](auto QMc, auto QNc) {
+    constexpr int QM = decltype(QMc)::value, QN = decltype(QNc)::value;
+    constexpr int nq = QN ? NQ1 : NQ0;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      if (ks < nks) {
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[qm * 4 + i][qn * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8_t, wr[j][ks]), __builtin_bit_cast(bf16x8_t, xr[i][ks]),
-                acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
-      }
-    }
+        for (int j = 0; j < nq; ++j)
+          acc[QM * MI + i][QN * NQ0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8_t, wr[j * 2 + ks]), __builtin_bit_cast(bf16x8_t, xr[i * 2 + ks]),
+              acc[QM * MI + i][QN * NQ0 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-  // one phase: fragment reads, one half-tile of prefetch, [counted wait], barrier, MFMAs, barrier
-#define LSA_PHASE(READS, STAGE_H, STAGE_T, WAIT, QM, QN)        \
+
+  // one tile segment: acc = X[tile rows] @ W[tile cols]^T over K-tiles [k0, k1).  Four phases per K-tile t
+  // (buffer t & 1, the loop unrolled by two so every LDS address is an immediate):
+  //   P1 (0,0): read XQ0 + WQ0   stage XQ1(t+1)
+  //   P2 (0,1): read WQ1         stage WQ0(t+1)
+  //   P3 (1,1): read XQ1         stage XQ0(t+2)
+  //   P4 (1,0): read WQ0         stage WQ1(t+2), then s_waitcnt vmcnt(GX + GW1): tile t+1 landed
+  // Every restage comes >= 2 phases after the last read of that half (WAR); every read comes a phase after the wait
+  // that retired it (RAW) - cdna_hip_programming.md §5, 8-phase template rules.  K-tiles past the segment's end are
+  // staged from clamped addresses (never read) so the counted wait stays exact.
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  auto segment = [&](int tile, int k0, int k1) {
+    setup(tile);
+    kt0 = k0;
+    Tl = k1 - k0;
+#pragma unroll
+    for (int i = 0; i < 2 * MI; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();  // the previous segment's LDS reads (and flag word) are done before the DMA overwrites them
+#define LSA_WAITV(N) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory")
+#define LSA_PHASE(READS, STAGE, WAIT, QM, QN)                   \
   do {                                                          \
     READS;                                                      \
-    stage(STAGE_H, STAGE_T);                                    \
+    STAGE;                                                      \
     WAIT;                                                       \
     __builtin_amdgcn_s_barrier();                               \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
     __builtin_amdgcn_sched_barrier(0);                          \
-    mma(QM, QN, nks);                                           \
+    mma(QM{}, QN{});                                            \
     __builtin_amdgcn_sched_barrier(0);                          \
     __builtin_amdgcn_s_barrier();                               \
   } while (0)
-
-  // prologue: all of tile 0, and XQ0 / WQ1 of tile 1
-  stage(0, 0);
-  stage(3, 0);
-  stage(1, 0);
-  stage(2, 0);
-  stage(0, 1);
-  stage(3, 1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  // ping-pong: the second M wave group runs one barrier behind, so one group's MFMA section overlaps the
-  // other's fragment reads + prefetch issue (the >= 2-phase WAR/RAW slack above covers the offset)
-  if (wm == 1) __builtin_amdgcn_s_barrier();
-  for (int t = 0; t < Tl; ++t) {
-    const int b = t & 1;
-    const int nks = (odd_tail && kt0 + t == T - 1) ? 1 : 2;
-    LSA_PHASE((read_x(b, 0), read_w(b, 0)), 1, t + 1, (void)0, 0, 0);
-    LSA_PHASE(read_w(b, 1), 2, t + 1, (void)0, 0, 1);
-    LSA_PHASE(read_x(b, 1), 0, t + 2, (void)0, 1, 1);
-    LSA_PHASE(read_w(b, 0), 3, t + 2, asm volatile("s_waitcnt vmcnt(4)" ::: "memory"), 1, 0);
-  }
+#define LSA_KTILE(B, NB, t)                                                                        \
+  do {                                                                                             \
+    LSA_PHASE((read_x(B{}, I0{}), read_w(B{}, I0{})), stage(I1{}, NB{}, (t) + 1), (void)0, I0, I0); \
+    LSA_PHASE(read_w(B{}, I1{}), stage(I2{}, NB{}, (t) + 1), (void)0, I0, I1);                     \
+    LSA_PHASE(read_x(B{}, I1{}), stage(I0{}, B{}, (t) + 2), (void)0, I1, I1);                      \
+    LSA_PHASE(read_w(B{}, I0{}), stage(I3{}, B{}, (t) + 2), LSA_WAITV(C::WAIT), I1, I0);           \
+  } while (0)
+    stage(I0{}, I0{}, 0);
+    stage(I3{}, I0{}, 0);
+    stage(I1{}, I0{}, 0);
+    stage(I2{}, I0{}, 0);
+    stage(I0{}, I1{}, 1);
+    stage(I3{}, I1{}, 1);
+    LSA_WAITV(C::WAIT);
+    __builtin_amdgcn_s_barrier();
+    // ping-pong: the second M wave group runs one barrier behind, so one group's MFMA section overlaps the other's
+    // fragment reads + prefetch issue (the >= 2-phase WAR/RAW slack above covers the offset)
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    int t = 0;
+    for (; t + 1 < Tl; t += 2) {
+      LSA_KTILE(I0, I1, t);
+      LSA_KTILE(I1, I0, t + 1);
+    }
+    if (t < Tl) LSA_KTILE(I0, I1, t);
+#undef LSA_KTILE
 #undef LSA_PHASE
-  if (wm == 0) __builtin_amdgcn_s_barrier();  // rebalance the barrier count
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+#undef LSA_WAITV
+    if (wm == 0) __builtin_amdgcn_s_barrier();  // rebalance the barrier count
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the segment
+  };
 
-  // epilogue: acc[i][j] = D[n = nb_j * 16 + 4 g + q][m = mb_i * 16 + (lane & 15)]
+  // epilogue of a finished tile: acc[i][j] = D[n = nb_j * 16 + 4 g + q][m = mb_i * 16 + (lane & 15)]
   const int g = lane >> 4;
+  auto store_tile = [&]() {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = mbase + (wm * 8 + i) * 16 + (lane & 15);
-    if (m >= M) continue;
-    if constexpr (EPI == EPI_SILU) {
+    for (int i = 0; i < 2 * MI; ++i) {
+      const int m = mbase + wm * (BM / 2) + i * 16 + (lane & 15);
+      if (m >= M) continue;
+      if constexpr (EPI == EPI_SILU) {
 #pragma unroll
-      for (int j = 0; j < 4; j += 2) {
-        const int nb = nbase + wn * 4 + j;  // even: gate block, nb + 1: up block
-        if (nb + 1 >= NBtot) continue;
-        f32x4_t v;
+        for (int j = 0; j < WN; j += 2) {
+          const int nb = nbase + wn * WN + j;  // even: gate block, nb + 1: up block
+          if (nb + 1 >= NBtot) continue;
+          uint2 p;
+          p.x = pack2bf(silu(acc[i][j][0]) * acc[i][j + 1][0], silu(acc[i][j][1]) * acc[i][j + 1][1]);
+          p.y = pack2bf(silu(acc[i][j][2]) * acc[i][j + 1][2], silu(acc[i][j][3]) * acc[i][j + 1][3]);
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + (size_t)m * ldo + (nb >> 1) * 16 + 4 * g) = p;
+        }
+      } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = silu(acc[i][j][q]) * acc[i][j + 1][q];
-        store_out<EPI_SILU>(out, ldo, m, (nb >> 1) * 16 + 4 * g, v);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int nb = nbase + wn * 4 + j;
-        if (nb >= NBtot) continue;
-        store_out<EPI>(EPI == EPI_F32 ? reinterpret_cast<void*>(reinterpret_cast<float*>(out) + (size_t)split * M * ldo)
-                                      : out,
-                       ldo, m, nb * 16 + 4 * g, acc[i][j]);
+        for (int j = 0; j < WN; ++j) {
+          const int nb = nbase + wn * WN + j;
+          if (nb >= NBtot) continue;
+          const size_t o = (size_t)m * ldo + nb * 16 + 4 * g;
+          if constexpr (EPI == EPI_BF16) {
+            uint2 p;
+            p.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+            p.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+            *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + o) = p;
+          } else if constexpr (EPI == EPI_RES) {
+            float4* hp = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o);
+            float4 hv = *hp;
+            hv.x += acc[i][j][0]; hv.y += acc[i][j][1]; hv.z += acc[i][j][2]; hv.w += acc[i][j][3];
+            *hp = hv;
+          } else {
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) =
+                make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+          }
+        }
       }
     }
+  };
+
+  // stream-K part: this virtual CU's iterations [s0, s1) of the first sk_tiles tiles
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
+  int* flag = reinterpret_cast<int*>(&lds[0][0][0][0]);
+  const int iters = pl.sk_iters;
+  const int s1 = iters > 0 ? sk_start(vc + 1, iters, P) : 0;
+  constexpr int WSTRIDE = 2 * MI * WN * 64 * 4;  // floats of one wave's accumulators in a partial slot
+  for (int gi = iters > 0 ? sk_start(vc, iters, P) : 0; gi < s1;) {
+    const int tile = gi / T;
+    const int k0 = gi - tile * T;
+    const int k1 = min(T, k0 + (s1 - gi));
+    segment(tile, k0, k1);
+    gi += k1 - k0;
+    if (k0 == 0 && k1 == T) {
+      store_tile();
+      continue;
+    }
+    // partial tile: publish (sc1 stores, 1 KiB per wave-instruction), ticket, the last arriver finishes
+    const int cf = sk_owner(tile * T, iters, P), cl = sk_owner(tile * T + T - 1, iters, P);
+    {
+      // this lane's byte offset in its slot (one VGPR); the fragment's 1 KiB step rides in the SGPR offset
+      const int voff = (sk_slot(vc, tile, iters, P, T) * LSA_SK_SLOT_FLOATS + w * WSTRIDE + lane * 4) * 4;
+#pragma unroll
+      for (int i = 0; i < 2 * MI; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          const u32x4_t u = {__float_as_uint(acc[i][j][0]), __float_as_uint(acc[i][j][1]),
+                             __float_as_uint(acc[i][j][2]), __float_as_uint(acc[i][j][3])};
+          __builtin_amdgcn_raw_buffer_store_b128(u, rs, voff, (i * WN + j) * 1024, LSA_SC1_AUX);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 partial stores
+    __syncthreads();
+    if (threadIdx.x == 0)
+      *flag = __hip_atomic_fetch_add((lsa_g_i32*)tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              cl - cf;
+    __syncthreads();
+    if (!*flag) continue;
+    if (threadIdx.x == 0)
+      __hip_atomic_store((lsa_g_i32*)tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // sum the contributors' partials in contributor order (cf .. cl), two fragment rows at a time
+#pragma unroll
+    for (int hh = 0; hh < MI; ++hh) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) acc[2 * hh + i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int c = cf; c <= cl; ++c) {
+        const int voff = (sk_slot(c, tile, iters, P, T) * LSA_SK_SLOT_FLOATS + w * WSTRIDE + lane * 4) * 4;
+        u32x4_t v[2][WN];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            v[i][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, ((2 * hh + i) * WN + j) * 1024, LSA_SC1_AUX);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[2 * hh + i][j][q] += __uint_as_float(v[i][j][q]);
+      }
+    }
+    store_tile();
+  }
+
+  // data-parallel part: whole tiles sk_tiles + vc, + P, ...
+  for (int tile = pl.sk_tiles + vc; tile < pl.ntiles; tile += P) {
+    segment(tile, 0, T);
+    store_tile();
   }
 }
 
-// M > 64 linear layer on the 256^2 tile (K % 32 == 0, N % 16 == 0; EPI_SILU needs N % 32 == 0)
-// xf_tiles > 0: X is fragment-major with that many 16-row tiles (>= ceil(M / 16))
-extern "C" int lsa_gemm_t256x(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi,
-                              int xf_tiles, hipStream_t stream) {
-  if (K % 32 != 0 || N % 16 != 0 || M <= 0 || (xf_tiles > 0 && xf_tiles * 16 < M)) return -1;
-  const int KB = K / 32, NBtot = N / 16;
-  const int ntm = (M + 255) / 256, ntn = (NBtot + 15) / 16;
-  const int ldo = epi == EPI_SILU ? N / 2 : N;
-  const dim3 grid(ntm * ntn);
-  const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
-  const uint4* w = reinterpret_cast<const uint4*>(Wf);
-  if (xf_tiles <= 0) return -5;
+// Plan for a grid of (at most) ncu workgroups over BM x (NBT * 16) tiles: the data-parallel rounds keep whole tiles;
+// the remainder round plus one full round (or every tile, when there are fewer tiles than CUs) is split by K-tile
+// ranges.  min_share: the fewest K-tiles a workgroup's stream-K range may hold (a shorter range gives up parallelism
+// for fewer partial tiles: the grid shrinks instead).  sk = false: whole tiles only (ceil(tiles / ncu) rounds).
+static SkPlan sk_plan(int M, int KB, int NBtot, int BM, int NBT, int ncu, int min_share, bool sk, int* grid) {
+  SkPlan pl;
+  pl.ntm = (M + BM - 1) / BM;
+  pl.ntiles = pl.ntm * ((NBtot + NBT - 1) / NBT);
+  pl.T = (KB + 1) / 2;
+  const int P = ncu;
+  if (!sk) {
+    pl.sk_tiles = 0;
+    *grid = pl.ntiles < P ? pl.ntiles : P;
+  } else if (pl.ntiles >= P) {
+    const int rem = pl.ntiles % P;
+    pl.sk_tiles = rem ? rem + P : 0;
+    if (pl.sk_tiles > pl.ntiles) pl.sk_tiles = pl.ntiles;
+    *grid = P;
+  } else {
+    pl.sk_tiles = pl.ntiles;
+    const long long it = (long long)pl.ntiles * pl.T;
+    long long g = it / (min_share > 0 ? min_share : 1);
+    if (g > P) g = P;
+    if (g < pl.ntiles) g = pl.ntiles;
+    *grid = (int)g;
+  }
+  pl.sk_iters = pl.sk_tiles * pl.T;
+  return pl;
+}
+
+// Tile configurations (BM, WN) and their cost per output element per K-tile relative to the 256 x 256 tile (the
+// narrower tiles stage more operand bytes per MFMA and run shorter phases); a partial-tile seam (a 64-256 KiB f32
+// partial written and read back by one CU) is priced in 256 x 256 K-tiles.  Measured: scripts/bench_prefill_gemm.py.
+struct SkCfg {
+  int bm, wn;
+  float cost;
+};
+static const SkCfg kSkCfgs[] = {{256, 4, 1.00f}, {256, 3, 1.06f}, {256, 2, 1.18f},
+                                {128, 4, 1.18f}, {128, 3, 1.28f}, {128, 2, 1.45f}};
+#define LSA_SK_SEAM_KTILES 8.0f
+
+// predicted time (256 x 256 K-tiles) of config c on the shape; *use_sk: whether the stream-K remainder beats whole
+// rounds
+static float sk_cfg_time(const SkCfg& c, int M, int KB, int NBtot, int ncu, bool* use_sk) {
+  const int nbt = 4 * c.wn;
+  const long long tiles = (long long)((M + c.bm - 1) / c.bm) * ((NBtot + nbt - 1) / nbt);
+  const float T = (float)((KB + 1) / 2);
+  const float per_tile = T * c.cost * (float)(c.bm * nbt) / 4096.0f;
+  const float dp = (float)((tiles + ncu - 1) / ncu) * per_tile;
+  const float skt = (float)tiles / ncu * per_tile + LSA_SK_SEAM_KTILES * (c.bm * nbt) / 4096.0f;
+  *use_sk = tiles % ncu != 0 && skt < dp;
+  return *use_sk ? skt : dp;
+}
+
+template <int BM, int WN>
+static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
+                     float* ws, int* tickets, int ncu, int min_share, bool sk, int* grid_out, hipStream_t stream) {
+  int grid = 0;
+  const SkPlan pl = sk_plan(M, KB, NBtot, BM, 4 * WN, ncu, min_share, sk, &grid);
+  if (pl.sk_tiles > 2 * ncu || grid > ncu || (long long)pl.sk_tiles * pl.T * (grid + 1) >= (1LL << 31)) return -3;
+  if (grid_out) *grid_out = grid;
   switch (epi) {
-    case EPI_BF16:
-      hipLaunchKernelGGL((gemm_t256_kernel<EPI_BF16, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm, 0);
-      break;
-    case EPI_F32:
-      hipLaunchKernelGGL((gemm_t256_kernel<EPI_F32, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm, 0);
-      break;
+#define LSA_SKL(E) \
+  hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, \
+                     pl, ws, tickets)
+    case EPI_BF16: LSA_SKL(EPI_BF16); break;
+    case EPI_F32: LSA_SKL(EPI_F32); break;
+    case EPI_RES: LSA_SKL(EPI_RES); break;
     case EPI_SILU:
-      hipLaunchKernelGGL((gemm_t256_kernel<EPI_SILU, true>), grid, dim3(512), 0, stream, x, xf_tiles, M, KB, w, NBtot, out, ldo, ntm, 0);
-      break;
-    default:
-      return -4;
+      if constexpr (WN % 2 == 0) {
+        LSA_SKL(EPI_SILU);
+        break;
+      } else {
+        return -2;
+      }
+#undef LSA_SKL
+    default: return -4;
   }
   return (int)hipGetLastError();
 }
 
-// splitk > 1 (EPI_F32 only): the K range is cut into splitk pieces of ceil(K-tiles / splitk) 64-deep tiles, one
-// workgroup per (output tile, piece), f32 slab per piece in out[splitk][M][N] -- fills the chip when the 256^2 tile
-// grid alone would not (3B 2k prefill o / down: 96 tiles -> x3)
-extern "C" int lsa_gemm_t256(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi,
-                             int splitk, hipStream_t stream) {
-  if (K % 32 != 0 || N % 16 != 0 || M <= 0) return -1;
+// M > 64 linear layer (K % 32 == 0, N % 16 == 0; EPI_SILU needs N % 32 == 0).  ws: lsa_gemm_sk_ws_bytes(ncu)
+// bytes; tickets: lsa_gemm_sk_tickets(ncu) int32, zero before the first call (every call leaves them zero).
+// out: bf16 [M][N] (EPI_BF16), f32 [M][N] (EPI_F32), bf16 [M][N / 2] (EPI_SILU), f32 h [M][N] accumulated (EPI_RES).
+// cfg: -1 = the cost model's pick, else an index into kSkCfgs (+ 8: whole tiles only, no stream-K remainder);
+// *cfg_out = the configuration used (same encoding).
+extern "C" int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
+                           int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out,
+                           hipStream_t stream) {
+  if (K % 32 != 0 || N % 16 != 0 || M <= 0 || ncu < 8 || ncu > 1024 || !ws || !tickets) return -1;
+  if (epi == EPI_SILU && N % 32 != 0) return -2;
   const int KB = K / 32, NBtot = N / 16;
-  const int ntm = (M + 255) / 256, ntn = (NBtot + 15) / 16;
-  const int ldo = epi == EPI_SILU ? N / 2 : N;
-  if (splitk < 1) splitk = 1;
-  if (splitk > 1 && epi != EPI_F32) return -3;
-  const int T = (KB + 1) / 2, kts = splitk > 1 ? (T + splitk - 1) / splitk : 0;
-  if (splitk > 1 && (T + kts - 1) / kts != splitk) return -3;  // every piece owns >= 1 K-tile
-  const dim3 grid(ntm * ntn * splitk);
+  const int ncfg = (int)(sizeof(kSkCfgs) / sizeof(kSkCfgs[0]));
+  bool sk = true;
+  if (cfg < 0) {
+    float best = 3.0e38f;
+    for (int i = 0; i < ncfg; ++i) {
+      if (epi == EPI_SILU && kSkCfgs[i].wn % 2) continue;
+      bool u = false;
+      const float t = sk_cfg_time(kSkCfgs[i], M, KB, NBtot, ncu, &u);
+      if (t < best) best = t, cfg = i, sk = u;
+    }
+  } else {
+    sk = cfg < 8;
+    cfg &= 7;
+    if (cfg >= ncfg) return -5;
+  }
+  if (cfg_out) *cfg_out = cfg + (sk ? 0 : 8);
   const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
   const uint4* w = reinterpret_cast<const uint4*>(Wf);
-  switch (epi) {
-    case EPI_BF16:
-      hipLaunchKernelGGL(gemm_t256_kernel<EPI_BF16>, grid, dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, ntm, 0);
-      break;
-    case EPI_F32:
-      hipLaunchKernelGGL(gemm_t256_kernel<EPI_F32>, grid, dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, ntm, kts);
-      break;
-    case EPI_SILU:
-      hipLaunchKernelGGL(gemm_t256_kernel<EPI_SILU>, grid, dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, ntm, 0);
-      break;
-    default:
-      return -4;
+  const int ldo = epi == EPI_SILU ? N / 2 : N;
+  switch (cfg) {
+#define LSA_SKC(I, BMV, WNV) \
+  case I: return sk_launch<BMV, WNV>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, grid_out, stream);
+    LSA_SKC(0, 256, 4)
+    LSA_SKC(1, 256, 3)
+    LSA_SKC(2, 256, 2)
+    LSA_SKC(3, 128, 4)
+    LSA_SKC(4, 128, 3)
+    LSA_SKC(5, 128, 2)
+#undef LSA_SKC
+    default: return -5;
   }
-  return (int)hipGetLastError();
 }

@@ -761,9 +761,11 @@ class ModelRunner:
         sk_o = self._splitk(T, self.H * self.D)
         sk_d = self._splitk(T, self.ffn_l)
         d_parts = None
-        # TP = 1, vendor prefill GEMMs: o / down accumulate into the f32 residual (beta = 1), the norms read h alone
-        res_o = self.on_gpu and ops.PREFILL_BLAS_RES and (self.tp is None or self.tp.size == 1) and ops.uses_blas(w.layers[0].wo, T)
-        res_d = res_o and ops.uses_blas(w.layers[0].w_down, T)
+        # TP = 1: o / down accumulate into the f32 residual in the stream-K GEMM's epilogue (ops.linear_res), so the
+        # norms after them read h alone (no f32 slab written by the GEMM and read back by the add)
+        tp1 = self.tp is None or self.tp.size == 1
+        res_o = tp1 and ops.res_supported(w.layers[0].wo)
+        res_d = tp1 and ops.res_supported(w.layers[0].w_down)
         for l, lw in enumerate(w.layers):
             if l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
@@ -771,7 +773,7 @@ class ModelRunner:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, write_h=not res_d)
             self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T)
             if res_o:
-                ops.blas_residual(attn, lw.wo, h)
+                ops.linear_res(attn, lw.wo, h)
                 ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, write_h=False)
             else:
                 o_parts = ops.linear(attn, lw.wo, "f32", splitk=sk_o)
@@ -786,7 +788,7 @@ class ModelRunner:
             else:
                 act = ops.linear(xn, lw.w_gate_up, "silu")
             if res_d:
-                ops.blas_residual(act, lw.w_down, h)
+                ops.linear_res(act, lw.w_down, h)
                 d_parts = None
             else:
                 d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
@@ -802,7 +804,7 @@ class ModelRunner:
     def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T):
         kc, vc = self.kv[l, 0], self.kv[l, 1]
         kvs = self._kv_scales(l)
-        sk_q = 1 if ops.uses_blas(lw.wqkv, T) else self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D)
+        sk_q = self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D)
         if sk_q > 1:  # small tile grid: f32 split-K slabs, summed by rope_append while it rotates
             parts = ops.linear(xn, lw.wqkv, "f32", splitk=sk_q)
             ops.rope_append(parts, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)

@@ -97,12 +97,8 @@ def pack_layer(spec: ModelSpec, wq, wk, wv, wo, wg, wu, wd, an, mn, rank=0, tp=1
         gu = (gu.float() * mn.float()[None, :]).to(torch.bfloat16)
         an, mn = torch.ones_like(an), torch.ones_like(mn)
     P = ops.PackedWeight.from_dense
-    # qkv / o / down also keep a row-major copy for the vendor prefill GEMM (ops.PREFILL_BLAS); gate_up too when its
-    # short-prompt prefill goes to the vendor GEMM + SiLU pass (ops.PREFILL_BLAS_SILU_MAX_M), longer ones stay on the
-    # 256^2 kernel's fused SiLU epilogue
-    return LayerWeights(P(wqkv.contiguous(), kind, rowmajor=True), P(wo_s.contiguous(), kind, rowmajor=True),
-                        P(gu.contiguous(), kind, rowmajor=ops.PREFILL_BLAS_SILU_MAX_M > 64),
-                        P(wd_s.contiguous(), kind, rowmajor=True), an.contiguous(),
+    return LayerWeights(P(wqkv.contiguous(), kind), P(wo_s.contiguous(), kind), P(gu.contiguous(), kind),
+                        P(wd_s.contiguous(), kind), an.contiguous(),
                         mn.contiguous(), norms_folded=FOLD_NORMS)
 
 

@@ -161,12 +161,9 @@ class PackedWeight:
     kind: str  # "dense" (CPU reference) | "bf16" (fragment layout) | "fp8" | "mxfp4"
     data: torch.Tensor
     scale: Optional[torch.Tensor] = None
-    rm: Optional[torch.Tensor] = None  # bf16 weights only: a row-major [N, K] copy for the vendor prefill GEMM
 
     @staticmethod
-    def from_dense(w: torch.Tensor, kind: str = "bf16", rowmajor: bool = False) -> "PackedWeight":
-        """``rowmajor`` (bf16 on the GPU, with ``PREFILL_BLAS``): also keep the row-major copy the plain prefill GEMMs
-        hand to hipBLASLt (``linear``)."""
+    def from_dense(w: torch.Tensor, kind: str = "bf16") -> "PackedWeight":
         N, K = w.shape
         if not w.is_cuda:
             return PackedWeight(N, K, "dense", w.to(torch.bfloat16).contiguous())
@@ -177,8 +174,7 @@ class PackedWeight:
             wq, sw = pack_mxfp4(*quantize_mxfp4(w))
             return PackedWeight(N, K, "mxfp4", wq, sw)
         wb = w.to(torch.bfloat16)
-        return PackedWeight(N, K, "bf16", shuffle_weight(wb),
-                            rm=wb.contiguous().clone() if (rowmajor and PREFILL_BLAS) else None)
+        return PackedWeight(N, K, "bf16", shuffle_weight(wb))
 
     def dense(self) -> torch.Tensor:
         if self.kind == "dense":
@@ -192,8 +188,7 @@ class PackedWeight:
     @property
     def nbytes(self) -> int:
         return self.data.numel() * self.data.element_size() + (
-            self.scale.numel() * self.scale.element_size() if self.scale is not None else 0) + (
-            self.rm.numel() * self.rm.element_size() if self.rm is not None else 0)
+            self.scale.numel() * self.scale.element_size() if self.scale is not None else 0)
 
 
 def pick_nb_splitk(M: int, N: int, K: int, epi: str) -> tuple[int, int]:
@@ -383,65 +378,60 @@ def _epi_ref(y: torch.Tensor, M: int, K: int, epi: str, rownorm, res, xf: bool):
     ss_out[:M] += ss_q24(hn.pow(2).sum(1))
 
 
-# Plain prefill projections (M > 64, bf16 weights, the bf16 / f32-slab epilogues: qkv, o, down) run on the vendor
-# library -- hipBLASLt through torch.mm, from a row-major copy of the weight made at load time (+ the qkv / o / down
-# bytes of HBM: 7.2 GB for the 7B, 2.8 GB for the 3B).  Measured against the hand-written 256^2 kernel
-# (profiles/r3/prefill_gemm_vs_hipblaslt_head_mi355x.jsonl, profiles/r4/prefill_gemm_*): the library's stream-K
-# kernels win every plain shape (7B qkv 1.37 vs 1.21 PF, o 1.45 vs 1.17, down 1.53 vs 1.22, 3B down 1.06 vs 0.62,
-# M = 300 0.71 vs 0.34).  The fused SiLU gate_up, the decode GEMMs and the quantised formats stay on this package's
-# kernels.
-PREFILL_BLAS = True
+# ----------------------------------------------------------------------------------- prefill GEMM (M > 64)
+# Every prefill projection runs on the stream-K 256^2 MFMA kernel (csrc/kernels/gemm_tile256.hip): a persistent grid
+# of one workgroup per CU, whole tiles for the full rounds and K-range shares of the rest, partial tiles summed by the
+# last workgroup to arrive.  Its workspace (partial slots + tickets) is per (device, HIP stream): co-served engines
+# prefill on their own streams and must not share tickets.
+_sk_ws: dict = {}
+# fewest K-tiles (64 deep) a workgroup's stream-K share may hold: below it the grid shrinks instead (fewer partial
+# tiles, each summed from fewer contributors)
+SK_MIN_SHARE = int(os.environ.get("LSA_SK_MIN_SHARE", "8"))
+_SK_EPI = {"bf16": 0, "f32": 1, "silu": 2, "res": 3}
 
 
-# the fused-SiLU gate_up prefill goes to the vendor GEMM (bf16 gate / up, the reference model's own rounding) + the
-# bf16 SiLU*up pass for 64 < M <= this many rows; above it the gemm_t256 SiLU epilogue stays ahead.  Measured
-# (profiles/r4/prefill_gateup_blas_silu_vs_t256_mi355x.jsonl, us, f32-out variant): 7B M=300 64.5 vs 89.8, 3B M=300
-# 43.0 vs 67.0, 7B M=1024 178.9 vs 185.9; end to end: 7B 300-token TTFT 8.80 -> 8.27 ms
-# (profiles/r4/prefill_ab_silu_bf16_mi355x.jsonl), while at 2048 rows the 256^2 kernel wins interleaved on one box
-# (3B 2k TTFT 13.61-13.72 vs 13.97-14.04 ms, profiles/r4/ttft_gateup_cap_ab_mi355x.jsonl)
-PREFILL_BLAS_SILU_MAX_M = 1024
-PREFILL_BLAS_SILU_BF16 = True
-# TP = 1 prefill: the vendor o / down GEMMs accumulate into the f32 residual (``blas_residual``)
-PREFILL_BLAS_RES = True
+def _sk_workspace(device) -> tuple:
+    dev = torch.device(device)
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    got = _sk_ws.get(key)
+    if got is None:
+        ncu = num_cus(dev)
+        e = ext()
+        ws = torch.empty(e.gemm_sk_ws_bytes(ncu) // 4, device=dev, dtype=torch.float32)
+        tk = torch.zeros(e.gemm_sk_tickets(ncu), device=dev, dtype=torch.int32)
+        got = _sk_ws[key] = (ws, tk, ncu)
+    return got
 
 
-def uses_blas(w: "PackedWeight", M: int, epi: str = "bf16") -> bool:
-    if epi == "silu":
-        return PREFILL_BLAS and 64 < M <= PREFILL_BLAS_SILU_MAX_M and w.rm is not None
-    return PREFILL_BLAS and M > 64 and w.rm is not None
+# tile configurations of the stream-K kernel (index = the kernel's kSkCfgs; + 8 = whole tiles only): (BM, BN)
+SK_CFGS = ((256, 256), (256, 192), (256, 128), (128, 256), (128, 192), (128, 128))
 
 
-def _blas_linear(x: torch.Tensor, w: PackedWeight, epi: str, out: Optional[torch.Tensor]) -> torch.Tensor:
+def gemm_sk(x: torch.Tensor, wf: torch.Tensor, N: int, out: torch.Tensor, epi: str,
+            min_share: Optional[int] = None, cfg: int = -1) -> torch.Tensor:
+    """out (epi 'bf16' / 'f32' / 'silu') or h (epi 'res': h[:M] += x @ W^T) from the stream-K prefill GEMM over the
+    fragment-layout bf16 weight ``wf``.  cfg: -1 = the kernel's tile-shape cost model, else an SK_CFGS index."""
+    ws, tk, ncu = _sk_workspace(x.device)
+    ext().gemm_sk(x, wf, N, out, _SK_EPI[epi], ws, tk, ncu, SK_MIN_SHARE if min_share is None else min_share, cfg)
+    return out
+
+
+def linear_res(x: torch.Tensor, w: PackedWeight, h: torch.Tensor) -> torch.Tensor:
+    """h[:M] += x @ W^T in f32 (prefill o / down, M > 64, TP = 1): the residual add rides in the GEMM epilogue, so the
+    norm after it reads h alone.  bf16 weights, or quantised ones through their bf16 dequantisation scratch; W8A8
+    fp8 prefill keeps its slab path (``res_supported``)."""
     M = x.shape[0]
-    if epi == "silu":  # gate/up rows interleaved per 16 (as packed), then SiLU(gate) * up
-        o = out.view(-1)[: M * (w.N // 2)].view(M, w.N // 2) if out is not None else torch.empty(
-            M, w.N // 2, device=x.device, dtype=torch.bfloat16)
-        if PREFILL_BLAS_SILU_BF16:  # bf16 gate / up (the reference model's own rounding), half the pass's bytes
-            y = torch.mm(x, w.rm.t())
-            ext().silu_bf16(y, o)
-            return o
-        y = torch.empty(1, M, w.N, device=x.device, dtype=torch.float32)
-        torch.mm(x, w.rm.t(), out_dtype=torch.float32, out=y[0])
-        return silu_parts(y, o)
-    if epi == "bf16":
-        o = out.view(-1)[: M * w.N].view(M, w.N) if out is not None else torch.empty(M, w.N, device=x.device,
-                                                                                   dtype=torch.bfloat16)
-        torch.mm(x, w.rm.t(), out=o)
-        return o
-    o = out.view(-1)[: M * w.N].view(1, M, w.N) if out is not None else torch.empty(1, M, w.N, device=x.device,
-                                                                                   dtype=torch.float32)
-    torch.mm(x, w.rm.t(), out_dtype=torch.float32, out=o[0])
-    return o
+    if not _gpu(x):
+        h[:M] += ref.linear(x, w.dense(), "f32")
+        return h
+    wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
+    return gemm_sk(x, wf, w.N, h, "res")
 
 
-def blas_residual(x: torch.Tensor, w: PackedWeight, h: torch.Tensor) -> torch.Tensor:
-    """h[:M] += x @ W^T in f32 on the vendor GEMM (beta = 1, bf16 operands, f32 C / D): the prefill's o / down
-    projections fold the residual add into the GEMM, so the norm after them reads h alone (no f32 slab written
-    by the GEMM and read back by the add).  Needs ``uses_blas(w, M)``."""
-    M = x.shape[0]
-    hv = h[:M]
-    torch.addmm(hv, x, w.rm.t(), out_dtype=torch.float32, out=hv)
-    return h
+def res_supported(w: PackedWeight) -> bool:
+    """Whether ``linear_res`` takes this weight (everything but W8A8 fp8 prefill, whose fp8 tile kernel writes
+    split-K slabs)."""
+    return not (w.kind == "fp8" and FP8_W8A8 and w.K % 128 == 0)
 
 
 def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
@@ -465,8 +455,14 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
             out.view(-1)[: y.numel()].copy_(y.reshape(-1))
             return out
         return y
-    if epi in ("bf16", "f32", "silu") and uses_blas(w, M, epi) and rownorm is None:
-        return _blas_linear(x, w, epi, out)  # one f32 slab whatever splitk asked for
+    if M > 64 and epi in ("bf16", "f32", "silu") and not (w.kind == "fp8" and FP8_W8A8 and K % 128 == 0):
+        # prefill: the stream-K tile kernel (epi 'f32' returns one [1, M, N] slab whatever splitk asked for)
+        assert rownorm is None and res is None, "epilogue extensions are decode-only (M <= 64)"
+        if out is None:
+            out = torch.empty(*((1, M, w.N) if epi == "f32" else (M, w.N // 2 if epi == "silu" else w.N)),
+                              device=x.device, dtype=torch.float32 if epi == "f32" else torch.bfloat16)
+        wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
+        return gemm_sk(x, wf, w.N, out, epi)
     nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi, kind=w.kind)
     nb = nb0 if nb is None else nb
     if M > 64:  # prefill tile kernels: split-K (f32 slabs) only where the tile grid is small
@@ -489,26 +485,17 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
     elif w.kind == "fp8":
         if M <= 64:  # fp8 knobs: waves, and the tuning entry's "div" field is the chunk depth (1 | 2)
             e.fp8_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, _fp8_depth(div), **kw)
-        elif K % 128 == 0 and FP8_W8A8:
-            # W8A8 on the block-scaled fp8 MFMA: per-token activation scales, no weight dequantisation
+        else:  # W8A8 on the block-scaled fp8 MFMA: per-token activation scales, no weight dequantisation
             x8, sx = quantize_rows_fp8(x)
             e.fp8_gemm_t256(x8, sx, w.data, w.scale, w.N, out, EPI[epi], splitk)
-        else:  # weight-only fallback: dequantise the layer into a bf16 scratch, bf16 tile GEMM
-            e.gemm(x, _dequant_scratch(w, x.device), w.N, out, EPI[epi], nb, splitk, waves, div)
-    elif w.kind == "mxfp4":
-        if M <= 64:  # W4A16 decode GEMM, e2m1 -> bf16 in registers (v_cvt_scalef32_pk_bf16_fp4)
-            e.fp4_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, **kw)
-        else:  # prefill: dequantise the layer into a bf16 fragment-layout scratch, bf16 tile GEMM
-            e.gemm(x, _dequant_scratch(w, x.device), w.N, out, EPI[epi], nb, splitk, waves, div)
+    elif w.kind == "mxfp4":  # W4A16 decode GEMM, e2m1 -> bf16 in registers (v_cvt_scalef32_pk_bf16_fp4)
+        e.fp4_gemm(x, w.data, w.scale, w.N, out, EPI[epi], nb, splitk, waves, **kw)
     else:
         raise ValueError(f"weight kind {w.kind} on GPU")
     return out
 
 
 FP8_W8A8 = os.environ.get("LSA_FP8_W8A8", "1") != "0"
-# prefill GEMMs of >= 1024 rows whose 256^2 tile grid under-fills the chip split K on that kernel (False: the 128^2
-# tile kernel with split-K, as before round 3)
-T256_SPLIT = True
 
 
 def _dequant_scratch(w: PackedWeight, device) -> torch.Tensor:
@@ -557,32 +544,11 @@ def fp8_tile_splitk(M: int, N: int, K: int) -> int:
 
 
 def tile_splitk(M: int, N: int, K: int, kind: str = "bf16") -> int:
-    """Split-K of a prefill GEMM (M > 64, f32 slab epilogue) on the 128x128 tile kernel: 1 where the
-    256x256 kernel takes the shape (its grid fills >= half the CUs), else doubled until the grid has
-    >= 256 workgroups, at most 8 slabs and >= 16 k-blocks (512 of K) per slab.  Without it a 128-token
-    7B prompt runs the O / down projections on 32 workgroups (N / 128 tiles) streaming all of K.
-    fp8 weights (W8A8 256^2 fp8 kernel): ``fp8_tile_splitk``."""
+    """Split-K (f32 slabs) of a prefill GEMM (M > 64): only the W8A8 fp8 tile kernel splits K (``fp8_tile_splitk``);
+    every other prefill projection runs on the stream-K kernel, which balances the K ranges itself."""
     if kind == "fp8" and FP8_W8A8 and K % 128 == 0:
         return fp8_tile_splitk(M, N, K)
-    nbt = N // 16
-    t256 = ((M + 255) // 256) * ((nbt + 15) // 16)
-    if M >= 1024 and t256 < 256 and T256_SPLIT:
-        # the 256^2 kernel with K split over sk pieces (f32 slabs): the sk in 2..4 whose grid rounds over 256 CUs,
-        # ceil(t256 * sk / 256) / sk, are shortest, each piece >= 4 K-tiles of 64 (3B 2k prefill o / down: 96 tiles,
-        # sk 2; qkv 160 tiles, sk 3)
-        best = (1.0, 1)
-        for sk in (2, 3, 4):
-            if (K // 64) // sk >= 4:
-                best = min(best, (-(-t256 * sk // 256) / sk, sk))
-        return best[1]
-    if t256 >= 128:
-        return 1
-    tiles = ((nbt + 7) // 8) * ((M + 127) // 128)
-    target, max_sk = 256, 8
-    sk = 1
-    while tiles * sk < target and sk < max_sk and (K // 32) // (sk * 2) >= 16:
-        sk *= 2
-    return sk
+    return 1
 
 
 _NUM_CUS: dict = {}

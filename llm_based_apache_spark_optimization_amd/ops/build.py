@@ -81,7 +81,7 @@ def build_hip(jobs: int = 8, verbose: bool = False) -> Path:
     odir = BUILD / ARCH
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         futs = [ex.submit(_compile, s, odir, HIPCC, kflags, headers) for s in srcs]
-        futs.append(ex.submit(_compile, CSRC / "bindings.cpp", odir, HIPCC, bflags, [kdir / "lsa_epi.h"]))
+        futs.append(ex.submit(_compile, CSRC / "bindings.cpp", odir, HIPCC, bflags, headers))
         objs = [f.result() for f in futs]
     key = hashlib.sha1("".join(sorted(o.name for o in objs)).encode()).hexdigest()[:16]
     stamp = HIP_EXT.with_suffix(".stamp")

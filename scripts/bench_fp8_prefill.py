@@ -62,8 +62,8 @@ for name, (M, N, K, epi) in shapes.items():
             ("fp8_w8a8_with_quant", lambda: (ops.quantize_rows_fp8(x),
                                              e.fp8_gemm_t256(x8, sx, pw8.data, pw8.scale, N, out, EPI[epi], 1))),
             ("fp8_weight_only_dequant", lambda: (e.fp8_dequant(pw8.data, pw8.scale, N, K, dq),
-                                                 e.gemm_t256(x, dq, N, out, EPI[epi]))),
-            ("bf16_tile256", lambda: e.gemm_t256(x, pwb.data, N, out, EPI[epi])))
+                                                 ops.gemm_sk(x, dq, N, out, epi))),
+            ("bf16_stream_k", lambda: ops.gemm_sk(x, pwb.data, N, out, epi)))
     for kname, fn in arms:
         fn()
         torch.cuda.synchronize()

@@ -18,7 +18,7 @@ starts, last_commit = [], True
 for i, r in enumerate(rows):
     if "commit_kernel" in r[2]:
         last_commit = True
-    elif ("gemm_t256" in r[2] or "gemm_tile_kernel" in r[2]) and last_commit:
+    elif ("gemm_sk" in r[2] or "gemm_t256" in r[2]) and last_commit:
         starts.append(i)
         last_commit = False
 for k, s0 in enumerate(starts):

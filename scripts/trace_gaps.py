@@ -53,7 +53,7 @@ if idle:
         print(f"  {c:4d} x {s / c:9.1f} us  after {a}  before {b}")
 # prefill segments: from the first prefill kernel (tile GEMM, vendor GEMM, prefill attention, rope/append) to the
 # commit kernel that ends the prefill; kernel-busy = every kernel in that window; per-kernel totals of the median one
-PRE = ("t256", "prefill", "rope_append", "Cijk")
+PRE = ("gemm_sk", "t256", "prefill", "rope_append", "Cijk")
 seg, segs = [], []
 for r in rows:
     if seg or any(p in r[2] for p in PRE):

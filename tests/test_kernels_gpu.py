@@ -45,20 +45,14 @@ def test_gemm_skinny_f32_splitk(gpu, M, splitk):
 
 
 @pytest.mark.parametrize("M", [1, 20, 64, 100, 257, 1100, 2100])
-@pytest.mark.parametrize("rowmajor", [False, True, "bf16"])
-def test_gemm_silu(gpu, M, rowmajor, monkeypatch):
-    """rowmajor: 64 < M <= PREFILL_BLAS_SILU_MAX_M runs the vendor GEMM (f32 out) + the SiLU*up pass, else the
-    hand kernels (the row-major copy is ignored).  "bf16": the vendor GEMM writes bf16 gate / up and the bf16 SiLU
-    pass (``silu_bf16``) reads them."""
-    monkeypatch.setattr(ops, "PREFILL_BLAS_SILU_BF16", rowmajor == "bf16")
-    rowmajor = bool(rowmajor)
+def test_gemm_silu(gpu, M):
+    """Fused SiLU(gate) * up through ops.linear: the skinny decode kernel (M <= 64) and the stream-K prefill kernel."""
     F, K = 1024, 2048
     torch.manual_seed(2)
     x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
     wg = (torch.randn(F, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
     wu = (torch.randn(F, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
-    pw = ops.PackedWeight.from_dense(ops.interleave_gate_up(wg, wu), rowmajor=rowmajor)
-    assert ops.uses_blas(pw, M, "silu") == (rowmajor and 64 < M <= ops.PREFILL_BLAS_SILU_MAX_M)
+    pw = ops.PackedWeight.from_dense(ops.interleave_gate_up(wg, wu))
     y = ops.linear(x, pw, "silu")
     yr = torch.nn.functional.silu(x.float() @ wg.float().t()) * (x.float() @ wu.float().t())
     assert y.shape == (M, F)
@@ -137,67 +131,80 @@ def test_silu_parts(gpu, M):
     assert _rel(act, yr) < 1e-2
 
 
-@pytest.mark.parametrize("M", [65, 128, 200, 1000])
-@pytest.mark.parametrize("NK", [(800, 4096), (1024, 1376), (4096, 512)])
-@pytest.mark.parametrize("epi", ["bf16", "f32"])
-def test_gemm_tile(gpu, M, NK, epi):
-    N, K = NK
-    torch.manual_seed(M + N)
-    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
-    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(torch.bfloat16)
-    pw = ops.PackedWeight.from_dense(w)
-    y = ops.linear(x, pw, epi)
-    yr = x.float() @ w.float().t()
-    if epi == "f32":
-        assert y.shape[0] == ops.tile_splitk(M, N, K)  # small tile grids split K into f32 slabs
-        assert _rel(y.sum(0), yr) < 1e-4
-        # explicit splits, uneven (K / 32 = 43 k-blocks -> 15 + 15 + 13) and one slab
-        for sk in (1, 3, 8):
-            if (K // 32) >= sk:
-                ys = ops.linear(x, pw, "f32", splitk=sk)
-                assert ys.shape[0] == sk and _rel(ys.sum(0), yr) < 1e-4
-    else:
-        assert _rel(y, yr) < 1e-2
-
-
-@pytest.mark.parametrize("M", [1024, 2048, 1100])
-@pytest.mark.parametrize("NK", [(3072, 3072), (5120, 3072), (3072, 8192), (1024, 1376)])
-@pytest.mark.parametrize("sk", [2, 3, 4])
-def test_gemm_tile256_splitk(gpu, M, NK, sk):
-    """The 256^2 kernel with K split into sk pieces (f32 slabs summing to the product; odd K/32 in the last piece), and
-    the prefill dispatch (ops.linear, ops.tile_splitk) that picks it for >= 1024 rows on small tile grids."""
-    N, K = NK
-    torch.manual_seed(M + N + K + sk)
-    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
-    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
-    pw = ops.PackedWeight.from_dense(w)
-    yr = x.float() @ w.float().t()
-    out = torch.full((sk, M, N), float("nan"), device=gpu)
-    ops.ext().gemm_t256(x, pw.data, N, out, 1, sk)
-    assert not torch.isnan(out).any()  # every slab element written
-    assert _rel(out.sum(0), yr) < 1e-4
-    y = ops.linear(x, pw, "f32")  # dispatch: the tile_splitk pick
-    assert y.shape[0] == ops.tile_splitk(M, N, K) and _rel(y.sum(0), yr) < 1e-4
-
-
-@pytest.mark.parametrize("M", [65, 256, 300, 777])
-@pytest.mark.parametrize("NK", [(800, 4096), (1024, 1376), (4096, 512), (256, 96)])
-@pytest.mark.parametrize("epi", ["bf16", "f32", "silu"])
-def test_gemm_tile256(gpu, M, NK, epi):
-    """256^2 8-phase prefill kernel: M / N edges, odd K/32 (1376 -> 43 k-steps), every epilogue."""
-    N, K = NK
-    torch.manual_seed(M + N + K)
-    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
-    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
-    pw = ops.PackedWeight.from_dense(w)
-    ncol = N // 2 if epi == "silu" else N
-    out = torch.empty(M, ncol, device=gpu, dtype=torch.float32 if epi == "f32" else torch.bfloat16)
-    ops.ext().gemm_t256(x, pw.data, N, out, ops.EPI[epi])
+def _sk_ref(x, w, epi, h0=None):
     yr = x.float() @ w.float().t()
     if epi == "silu":
+        M, N = yr.shape
         r3 = yr.view(M, N // 32, 2, 16)
-        yr = (torch.nn.functional.silu(r3[:, :, 0]) * r3[:, :, 1]).reshape(M, N // 2)
-    assert _rel(out, yr) < (1e-5 if epi == "f32" else 1e-2)
+        return (torch.nn.functional.silu(r3[:, :, 0]) * r3[:, :, 1]).reshape(M, N // 2)
+    return yr + h0 if epi == "res" else yr
+
+
+def _sk_case(gpu, M, N, K, epi, share, ncu=None, seed=0, cfg=-1):
+    torch.manual_seed(seed + M + N + K)
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    h0 = torch.randn(M, N, device=gpu) if epi == "res" else None
+    ncol = N // 2 if epi == "silu" else N
+    dt = torch.float32 if epi in ("f32", "res") else torch.bfloat16
+    out = h0.clone() if epi == "res" else torch.full((M, ncol), float("nan"), device=gpu, dtype=dt)
+    ws, tk, ncu0 = ops._sk_workspace(gpu)
+    grid = ops.ext().gemm_sk(x, pw.data, N, out, ops._SK_EPI[epi], ws, tk, ncu or ncu0, share, cfg)
+    torch.cuda.synchronize()
+    assert int(tk.abs().sum()) == 0  # every call leaves the tickets zero
+    yr = _sk_ref(x, w, epi, h0)
+    assert not torch.isnan(out).any()  # every output element written
+    assert _rel(out, yr) < (1e-5 if dt == torch.float32 else 1e-2), (M, N, K, epi, share, grid)
+    return x, pw, out, h0, grid
+
+
+@pytest.mark.parametrize("M", [65, 300, 777, 2048])
+@pytest.mark.parametrize("NK", [(800, 4096), (1024, 1376), (4096, 512), (3072, 3072), (256, 96)])
+@pytest.mark.parametrize("epi", ["bf16", "f32", "silu", "res"])
+def test_gemm_stream_k(gpu, M, NK, epi):
+    """Stream-K prefill kernel (the cost model's tile pick) vs the fp32 product: M / N tile edges (N = 800: a
+    partial column tile), odd K / 32 (1376 -> 43 k-steps), every epilogue (the residual one accumulates into h),
+    grids from 4 tiles to a full chip of K-range shares."""
+    N, K = NK
+    _sk_case(gpu, M, N, K, epi, ops.SK_MIN_SHARE)
+
+
+@pytest.mark.parametrize("cfg", list(range(6)) + [8, 11, 13])
+@pytest.mark.parametrize("MNK", [(300, 3072, 1376), (2048, 5120, 1024), (1100, 800, 512)])
+@pytest.mark.parametrize("epi", ["bf16", "silu", "res"])
+def test_gemm_stream_k_tile_shapes(gpu, cfg, MNK, epi):
+    """Every tile configuration (BM 128 / 256 x BN 128 / 192 / 256; + 8: whole tiles only) on shapes whose edges cut
+    every tile kind."""
+    M, N, K = MNK
+    if epi == "silu" and ops.SK_CFGS[cfg & 7][1] % 128:
+        pytest.skip("SiLU needs an even n-block count per wave")
+    _sk_case(gpu, M, N, K, epi, 4, cfg=cfg)
+
+
+@pytest.mark.parametrize("share", [1, 2, 5])
+@pytest.mark.parametrize("MNK", [(300, 3072, 3072), (2048, 3072, 8192), (128, 4096, 4096)])
+def test_gemm_stream_k_many_partials(gpu, share, MNK):
+    """Small stream-K shares: tiles cut among many workgroups (up to 64-way at share 1), every partial summed by the
+    last to arrive in contributor order, so a repeated call is bitwise identical."""
+    M, N, K = MNK
+    x, pw, out, h0, _ = _sk_case(gpu, M, N, K, "f32", share)
+    first = out.clone()
+    ws, tk, ncu = ops._sk_workspace(gpu)
+    for _ in range(3):
+        ops.ext().gemm_sk(x, pw.data, N, out, 1, ws, tk, ncu, share, -1)
+        torch.cuda.synchronize()
+        assert torch.equal(out, first)
+
+
+@pytest.mark.parametrize("ncu", [8, 24, 40])
+@pytest.mark.parametrize("MN", [(777, 1280), (2048, 10240), (1024, 4096)])
+def test_gemm_stream_k_dp_rounds(gpu, ncu, MN):
+    """A plan on a grid smaller than the chip (ncu workgroups): several data-parallel rounds of whole tiles plus the
+    stream-K remainder (tiles mod ncu + ncu), and grids whose size is not a multiple of the 8 XCDs."""
+    M, N = MN
+    for epi in ("bf16", "res"):
+        _sk_case(gpu, M, N, 1024, epi, 4, ncu=ncu)
 
 
 def test_gemm_asymmetric_exact(gpu):
