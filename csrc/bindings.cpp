@@ -85,7 +85,7 @@ int lsa_ar_wallclock_khz(int* out);
 int lsa_ar_header_bytes();
 int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int rank, int world, size_t maxb,
                int nblocks, long long timeout_ticks, int* err, int nslab, long slab_stride, const float* res_h,
-               void* res_xn, long long* res_ss, int res_d, int res_xmt, hipStream_t s);
+               void* res_xn, long long* res_ss, int res_d, int res_xmt, int mode, hipStream_t s);
 int lsa_fp4_gemm_ex(const void* X, int ldx, int M, int K, const void* Wq, const void* S, int N, void* out, int epi,
                     int nb, int splitk, int waves, int xfrag, const LsaEpi* ep, hipStream_t stream);
 int lsa_fp4_dequant(const void* Wq, const void* S, int N, int K, void* Wf, hipStream_t s);
@@ -767,8 +767,9 @@ int64_t ar_open(const std::string& h) {
 void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Tensor& regions, int64_t rank,
             int64_t maxb, int64_t nblocks, int64_t timeout_ticks, at::Tensor& err, int64_t nslab = 1,
             const c10::optional<at::Tensor>& res_h = c10::nullopt, const c10::optional<at::Tensor>& res_xn = c10::nullopt,
-            const c10::optional<at::Tensor>& res_ss = c10::nullopt, int64_t res_xmt = 0) {
-  // nslab > 1: data is [nslab, n] split-K slabs; the sum lands in slab 0
+            const c10::optional<at::Tensor>& res_ss = c10::nullopt, int64_t res_xmt = 0, int64_t mode = 0) {
+  // nslab > 1: data is [nslab, n] split-K slabs; the sum lands in slab 0.  mode: bit 0 bf16 payload, bit 1 two-shot
+  // (sums only; the caller sized the regions for the two-shot result area)
   need(data, at::kFloat, "data");
   need(regions, at::kLong, "regions");
   need(err, at::kInt, "err");
@@ -784,6 +785,7 @@ void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Te
     need(*out, at::kFloat, "out");
     TORCH_CHECK(out->is_contiguous() && out->numel() == n * regions.numel(), "all-gather out size");
   }
+  TORCH_CHECK(mode >= 0 && mode <= 3 && (mode == 0 || !out.has_value()), "all-reduce mode: 0..3, sums only");
   int64_t D = 0;
   if (res_h.has_value()) {  // residual epilogue: h [rows, D] f32 += the sum; xn = bf16(h); ss[rows] += sum h^2 (Q24)
     TORCH_CHECK(!out.has_value() && res_xn.has_value() && res_ss.has_value(), "all-reduce residual: h, xn, ss");
@@ -802,7 +804,7 @@ void ar_run(at::Tensor& data, const c10::optional<at::Tensor>& out, const at::Te
                    rank, regions.numel(), maxb, nblocks, timeout_ticks, err.data_ptr<int>(), nslab, n,
                    res_h.has_value() ? res_h->data_ptr<float>() : nullptr, res_xn.has_value() ? res_xn->data_ptr() : nullptr,
                    res_ss.has_value() ? reinterpret_cast<long long*>(res_ss->data_ptr<int64_t>()) : nullptr, (int)D,
-                   (int)res_xmt, cur_stream()),
+                   (int)res_xmt, (int)mode, cur_stream()),
         "ar_run");
 }
 
@@ -889,7 +891,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ar_run", &ar_run, py::arg("data"), py::arg("out"), py::arg("regions"), py::arg("rank"), py::arg("maxb"),
         py::arg("nblocks"), py::arg("timeout_ticks"), py::arg("err"), py::arg("nslab") = 1,
         py::arg("res_h") = py::none(), py::arg("res_xn") = py::none(), py::arg("res_ss") = py::none(),
-        py::arg("res_xmt") = 0);
+        py::arg("res_xmt") = 0, py::arg("mode") = 0);
   m.def("ar_wallclock_khz", []() {
     int k = 0;
     check(lsa_ar_wallclock_khz(&k), "ar_wallclock_khz");

@@ -218,6 +218,10 @@ int main() {
     expect_reject("ar_run gather out", [&] { ar_run(data, gout, regions, 0, 1 << 20, 64, 1000, err, 1); });
     auto slabs = T({3, 4096}, F32);
     expect_ok("ar_run slabs", [&] { ar_run(slabs, none, regions, 1, 1 << 20, 64, 1000, err, 3); });
+    expect_ok("ar_run bf16 two-shot", [&] { ar_run(slabs, none, regions, 1, 1 << 20, 64, 1000, err, 3, none, none, none, 0, 3); });
+    auto gout2 = T({8192}, F32);
+    expect_reject("ar_run gather mode", [&] { ar_run(data, gout2, regions, 0, 1 << 20, 64, 1000, err, 1, none, none, none, 0, 1); });
+    expect_reject("ar_run mode range", [&] { ar_run(data, none, regions, 0, 1 << 20, 64, 1000, err, 1, none, none, none, 0, 4); });
   }
   if (failures) {
     std::printf("bindings selftest: %d failure(s)\n", failures);

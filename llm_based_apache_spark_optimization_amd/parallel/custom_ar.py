@@ -28,6 +28,12 @@ log = logging.getLogger(__name__)
 
 DEFAULT_MAX_BYTES = 8 << 20  # B=64 x d=4096 f32 all-reduces; B=32 x 64128 vocab-parallel logit gathers (3B, TP2)
 DEFAULT_TIMEOUT_S = 60.0
+# sums push bf16 partials (each rank rounds its contribution, its own copy too, and sums in f32 in rank order: every
+# rank still gets bitwise the same result) -- half the xGMI bytes of the f32 payload; LSA_CUSTOM_AR_BF16=0 keeps f32
+AR_BF16 = os.environ.get("LSA_CUSTOM_AR_BF16", "1") != "0"
+# two-shot (reduce-scatter + all-gather) above this many payload bytes when the group has more than 2 ranks: each rank
+# then sends (W - 1) / W of the tensor instead of the whole tensor to each of W - 1 peers (TP = 2 gains nothing from it)
+AR_TWO_SHOT_MIN_BYTES = int(os.environ.get("LSA_CUSTOM_AR_TWO_SHOT_BYTES", str(128 << 10)))
 
 
 class IpcUnavailable(RuntimeError):
@@ -107,19 +113,25 @@ def open_regions(group, rank: int, world: int, ext, nbytes: int,
 
 
 class IpcAllReduce:
-    """In-place f32 sum over the ``world`` ranks of ``group`` for tensors up to ``max_bytes``."""
+    """In-place f32 sum over the ``world`` ranks of ``group`` for tensors up to ``max_bytes``: one-shot (every rank
+    pushes its tensor to every peer) for TP = 2 and small messages, two-shot (reduce-scatter + all-gather) above
+    ``two_shot_min_bytes`` with more than 2 ranks; bf16 payloads by default (``AR_BF16``)."""
 
     def __init__(self, group, rank: int, world: int, device: torch.device, max_bytes: int = DEFAULT_MAX_BYTES,
-                 nblocks: int = 128, timeout_s: float = DEFAULT_TIMEOUT_S):
+                 nblocks: int = 128, timeout_s: float = DEFAULT_TIMEOUT_S, bf16: Optional[bool] = None,
+                 two_shot_min_bytes: Optional[int] = None):
         ext = ops.ext()
         if not 2 <= world <= ext.ar_max_world:
             raise ValueError(f"IpcAllReduce supports 2..{ext.ar_max_world} ranks, got {world}")
         self.rank, self.world, self.device = rank, world, device
         self.max_bytes = int(max_bytes)
         self.nblocks = int(nblocks)
+        self.bf16 = AR_BF16 if bf16 is None else bool(bf16)
+        self.two_shot_min_bytes = AR_TWO_SHOT_MIN_BYTES if two_shot_min_bytes is None else int(two_shot_min_bytes)
         with torch.cuda.device(device):
+            # recv[2][world][max_bytes] + the two-shot result area res[2][max_bytes]
             self._base, ptrs, self._opened = open_regions(group, rank, world, ext,
-                                                          ext.ar_header_bytes + 2 * world * self.max_bytes,
+                                                          ext.ar_header_bytes + (2 * world + 2) * self.max_bytes,
                                                           device_index=device.index)
             self.regions = torch.tensor(ptrs, dtype=torch.int64, device=device)
             self.err = torch.zeros(1, dtype=torch.int32, device=device)
@@ -127,12 +139,18 @@ class IpcAllReduce:
         # every rank has mapped every peer before anyone pushes
         dist.barrier(group=group)
 
+    def mode(self, payload_bytes: int) -> int:
+        """Kernel mode of a sum over ``payload_bytes`` of f32: bit 0 bf16 payload, bit 1 two-shot."""
+        two = self.world > 2 and payload_bytes > self.two_shot_min_bytes
+        return (1 if self.bf16 else 0) | (2 if two else 0)
+
     def fits(self, t: torch.Tensor) -> bool:
         return (t.dtype == torch.float32 and t.is_cuda and t.is_contiguous() and t.numel() % 4 == 0
                 and t.numel() * 4 <= self.max_bytes and t.data_ptr() % 16 == 0)
 
     def __call__(self, t: torch.Tensor) -> torch.Tensor:
-        ops.ext().ar_run(t, None, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err)
+        ops.ext().ar_run(t, None, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err,
+                         mode=self.mode(t.numel() * 4))
         return t
 
     def fits_slabs(self, t: torch.Tensor) -> bool:
@@ -145,7 +163,7 @@ class IpcAllReduce:
         """Sum over ranks of each rank's slab-sum of t [nslab, ...]; the result lands in t[0] (returned
         as a [1, ...] view) — split-K partials and the TP all-reduce in one kernel."""
         ops.ext().ar_run(t, None, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err,
-                         t.shape[0])
+                         t.shape[0], mode=self.mode(t.numel() // t.shape[0] * 4))
         return t[:1]
 
     def reduce_slabs_res(self, t: torch.Tensor, h: torch.Tensor, xn: torch.Tensor, ss: torch.Tensor,
@@ -155,7 +173,8 @@ class IpcAllReduce:
         tiles, else row-major); ss[rows] += row sums of h^2 (Q24 int64).  One launch where the unfused TP step ran
         an all-reduce and then a residual-add launch (D % 256 == 0)."""
         ops.ext().ar_run(t, None, self.regions, self.rank, self.max_bytes, self.nblocks, self.timeout_ticks, self.err,
-                         t.shape[0], res_h=h, res_xn=xn, res_ss=ss, res_xmt=xmt)
+                         t.shape[0], res_h=h, res_xn=xn, res_ss=ss, res_xmt=xmt,
+                         mode=self.mode(t.numel() // t.shape[0] * 4))
 
     def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
         """out[world * n] = concatenation of every rank's t[n] in rank order (same push protocol)."""

@@ -1,6 +1,7 @@
-"""One-shot IPC all-reduce kernel (csrc/kernels/allreduce.hip) vs the fp32 rank-ordered
-sum.  The test box has one GPU, so the ranks are processes sharing it (IPC handles of the same device);
-on the 8-GPU node the same code maps peer GPUs over xGMI.  gloo exchanges the handles."""
+"""IPC all-reduce kernels (csrc/kernels/allreduce.hip): one-shot and two-shot (reduce-scatter +
+all-gather), f32 and bf16 payloads, vs the fp32 rank-ordered sum of the same (rounded) contributions.  Rank r runs on
+cuda:r when the box has at least `world` GPUs (peer regions mapped across devices over xGMI), else every rank shares
+cuda:0 (IPC handles of the same device).  gloo exchanges the handles."""
 import queue
 import socket
 import time
@@ -18,14 +19,31 @@ def _inputs(rank: int, it: int, n: int) -> torch.Tensor:
     return torch.randn(n, generator=g)
 
 
-def _expected(world: int, it: int, n: int) -> torch.Tensor:
+def _bf(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.bfloat16).float()
+
+
+# kernel variants: (bf16 payload, two-shot) -- the reference rounds each rank's contribution as the kernel does
+VARIANT = (False, False)
+
+
+def _expected(world: int, it: int, n: int, variant=None) -> torch.Tensor:
+    bf16, two = VARIANT if variant is None else variant
     acc = torch.zeros(n)
     for r in range(world):  # the kernel's summation order
-        acc = acc + _inputs(r, it, n)
-    return acc
+        x = _inputs(r, it, n)
+        acc = acc + (_bf(x) if bf16 else x)
+    return _bf(acc) if (bf16 and two) else acc  # the two-shot owner pushes the bf16 sum
 
 
-def _worker(rank, world, port, q):
+def _device(rank: int, world: int) -> torch.device:
+    """cuda:rank when every rank has a GPU of its own (the cross-device IPC path), else the shared cuda:0."""
+    return torch.device("cuda", rank if torch.cuda.device_count() >= world else 0)
+
+
+def _worker(rank, world, port, q, variant=(False, False)):
+    global VARIANT
+    VARIANT = variant
     import os
 
     import torch.distributed as dist
@@ -34,11 +52,17 @@ def _worker(rank, world, port, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = torch.device("cuda", 0)
+    dev = _device(rank, world)
     torch.cuda.set_device(dev)
     errs = []
+    bf16, two = variant
     try:
-        car = IpcAllReduce(dist.group.WORLD, rank, world, dev, max_bytes=4 << 20, timeout_s=30)
+        car = IpcAllReduce(dist.group.WORLD, rank, world, dev, max_bytes=4 << 20, timeout_s=30, bf16=bf16,
+                           two_shot_min_bytes=0 if two else 1 << 40)
+        assert car.mode(4096) == (1 if bf16 else 0) | (2 if (two and world > 2) else 0) or (two and world == 2)
+        if two and world == 2:
+            car.two_shot_min_bytes = -1
+            car.mode = lambda nbytes: (1 if bf16 else 0) | 2  # exercise the two-shot kernel at TP = 2 too
         it = 0
         for n in SIZES:  # eager, several epochs per size (both slot parities, block counts change)
             for _ in range(3):
@@ -46,6 +70,13 @@ def _worker(rank, world, port, q):
                 car(t)
                 if not torch.equal(t.cpu(), _expected(world, it, n)):
                     errs.append(f"eager n={n} it={it}: max err {(t.cpu() - _expected(world, it, n)).abs().max()}")
+                # stated bound vs the exact fp32 sum: each bf16 rounding (RNE) moves a value by <= 2^-9 of it
+                xs = [_inputs(r, it, n) for r in range(world)]
+                exact = torch.stack(xs).double().sum(0)
+                bound = torch.stack(xs).abs().double().sum(0) * 2.0 ** -9 * bf16 + exact.abs() * 2.0 ** -9 * (
+                    bf16 and two) + exact.abs() * 1e-6 + 1e-30
+                if ((t.cpu().double() - exact).abs() > bound).any():
+                    errs.append(f"bound n={n} it={it}")
                 it += 1
         for ns, n in ((2, 4096), (4, 32 * 4096), (3, 4100)):  # split-K slabs folded into the all-reduce
             slabs = [_inputs(rank, it + 100 * k, n) for k in range(ns)]
@@ -56,7 +87,9 @@ def _worker(rank, world, port, q):
                 own = _inputs(r, it, n)
                 for k in range(1, ns):
                     own = own + _inputs(r, it + 100 * k, n)
-                want = want + own
+                want = want + (_bf(own) if bf16 else own)
+            if bf16 and two:
+                want = _bf(want)
             if red.shape[0] != 1 or not torch.equal(red[0].cpu(), want):
                 errs.append(f"slabs ns={ns} n={n} it={it}")
             it += 1
@@ -75,7 +108,10 @@ def _worker(rank, world, port, q):
             car.reduce_slabs_res(slabs, h, xn, ss, xmt)
             tot = torch.zeros(rows, D)
             for r in range(world):
-                tot = tot + sum(_inputs(r, it + 100 * k, n) for k in range(ns)).view(rows, D)
+                own = sum(_inputs(r, it + 100 * k, n) for k in range(ns)).view(rows, D)
+                tot = tot + (_bf(own) if bf16 else own)
+            if bf16 and two:
+                tot = _bf(tot)
             want = h0 + tot
             if (h.cpu() - want).abs().max() > 1e-4 * want.abs().max():
                 errs.append(f"res h ns={ns} rows={rows}")
@@ -122,7 +158,13 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_ipc_allreduce_matches_rank_ordered_sum(gpu, world):
+@pytest.mark.parametrize("variant", [(False, False), (True, False), (False, True), (True, True)],
+                         ids=["f32_oneshot", "bf16_oneshot", "f32_twoshot", "bf16_twoshot"])
+def test_ipc_allreduce_matches_rank_ordered_sum(gpu, world, variant):
+    """Every kernel variant equals the rank-ordered f32 sum of the contributions as pushed (bf16: each rounded to
+    bf16; two-shot bf16: the sum rounded too), bitwise on every rank; and the bf16 variants stay within the bf16
+    rounding bound of the exact fp32 sum: |result - sum| <= 2^-9 (sum of |x_r|, + |sum| for the two-shot bf16
+    sum) + 1e-6 |sum|."""
     import torch.multiprocessing as tmp
 
     with socket.socket() as so:
@@ -130,7 +172,7 @@ def test_ipc_allreduce_matches_rank_ordered_sum(gpu, world):
         port = so.getsockname()[1]
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, variant)) for r in range(world)]
     [p.start() for p in ps]
     got, t0 = {}, time.time()
     try:
@@ -162,7 +204,7 @@ def _engine_worker(rank, world, port, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LSA_CUSTOM_AR_TIMEOUT_S="0.3")
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
-    dev = torch.device("cuda", 0)
+    dev = _device(rank, world)
     torch.cuda.set_device(dev)
     out = []
     try:
@@ -251,7 +293,7 @@ def _follower_timeout_worker(rank, world, port, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = torch.device("cuda", 0)
+    dev = _device(rank, world)
     torch.cuda.set_device(dev)
     out = {}
     try:
@@ -299,7 +341,7 @@ def _fallback_worker(rank, world, port, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = torch.device("cuda", 0)
+    dev = _device(rank, world)
     torch.cuda.set_device(dev)
     out = {}
     try:

@@ -179,7 +179,7 @@ def _tp_gpu_worker(rank, world, port, q, graphs=False):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", rank if torch.cuda.device_count() >= world else 0)  # own GPU when there are enough
     tp = TPGroup(dist.group.WORLD, rank, world, dev)
     e = build_engine("tiny-nsql", device=str(dev), max_slots=4, max_model_len=256, tp=tp, use_graphs=graphs)
     prompts = [[1] + list(range(5, 40)), [1, 7, 7]]

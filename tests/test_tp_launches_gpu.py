@@ -37,7 +37,7 @@ def _worker(rank, world, port, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", rank if torch.cuda.device_count() >= world else 0)  # own GPU when there are enough
     torch.cuda.set_device(dev)
     out = {}
     try:
