@@ -63,6 +63,7 @@ int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, vo
                  int waves, int div, int xlds, hipStream_t stream);
 int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
+void lsa_gemm_sk_epilogue(int mode);
 int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
                 int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
@@ -822,6 +823,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("ws"),
         py::arg("tickets"), py::arg("ncu"), py::arg("min_share") = 0, py::arg("cfg") = -1);
+  m.def("gemm_sk_epilogue", [](int64_t mode) { lsa_gemm_sk_epilogue((int)mode); });
   m.def("gemm_sk_ws_bytes", [](int64_t ncu) { return lsa_gemm_sk_ws_bytes((int)ncu); });
   m.def("gemm_sk_tickets", [](int64_t ncu) { return (int64_t)lsa_gemm_sk_tickets((int)ncu); });
   m.def("fp4_gemm", &fp4_gemm, py::arg("x"), py::arg("wq"), py::arg("sw"), py::arg("N"), py::arg("out"), py::arg("epi"),

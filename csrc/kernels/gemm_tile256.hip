@@ -74,6 +74,7 @@ struct SkPlan {
   int T;                // K-tiles of 64 per output tile
   int sk_tiles;         // tiles [0, sk_tiles) are stream-K, the rest data-parallel
   int sk_iters;         // sk_tiles * T (host-checked: sk_iters * (grid + 1) < 2^31, so 32-bit index math)
+  int epl;              // epilogue: 0 = straight from the accumulators, 1 = through an LDS image (full-row stores)
 };
 
 // first stream-K iteration of virtual CU c
@@ -332,6 +333,68 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict
     }
   };
 
+  // The same epilogue through LDS: the accumulators hold 4 consecutive columns of one row per lane, so a direct
+  // store instruction covers 16 rows x 64 B (f32) / 32 B (bf16).  Here each half of the tile's rows (one M wave
+  // group) is written to an f32 LDS image [BM / 2][OC] (16-B chunk ch of row r at ch ^ (r & 15): conflict-free
+  // writes of 16 rows and reads of one row) and read back one full row per wave-instruction, so the global stores
+  // (and the residual's h reads) are whole 128-B lines.
+  auto store_tile_lds = [&]() {
+    constexpr int OC = EPI == EPI_SILU ? C::NBT * 8 : C::NBT * 16;  // output columns of the tile
+    constexpr int CH = OC / 4;                                      // 16-B f32 chunks per image row
+    static_assert(CH % 16 == 0, "swizzle stays inside the row");
+    float* img = reinterpret_cast<float*>(&lds[0][0][0][0]);
+    const int ncol_out = EPI == EPI_SILU ? NBtot * 8 : NBtot * 16;
+    const int col0 = EPI == EPI_SILU ? nbase * 8 : nbase * 16;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      __syncthreads();  // the previous readers (main loop or the other pass) are done with the image
+      if (wm == pass) {
+#pragma unroll
+        for (int i = 0; i < 2 * MI; ++i) {
+          const int r = i * 16 + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < WN; ++j) {
+            f32x4_t v = acc[i][j];
+            int ch;
+            if constexpr (EPI == EPI_SILU) {
+              if (j & 1) continue;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = silu(acc[i][j][q]) * acc[i][j + 1][q];
+              ch = ((wn * WN + j) >> 1) * 4 + (lane >> 4);
+            } else {
+              ch = (wn * WN + j) * 4 + (lane >> 4);
+            }
+            *reinterpret_cast<f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2)) = v;
+          }
+        }
+      }
+      __syncthreads();
+      for (int r = w; r < BM / 2; r += 8) {
+        const int m = mbase + pass * (BM / 2) + r;
+        const int ch = lane;
+        if (ch < CH && m < M && col0 + ch * 4 < ncol_out) {
+          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2));
+          const size_t o = (size_t)m * ldo + col0 + ch * 4;
+          if constexpr (EPI == EPI_BF16 || EPI == EPI_SILU) {
+            *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + o) =
+                make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+          } else if constexpr (EPI == EPI_RES) {
+            float4* hp = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o);
+            float4 hv = *hp;
+            hv.x += v[0]; hv.y += v[1]; hv.z += v[2]; hv.w += v[3];
+            *hp = hv;
+          } else {
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+        }
+      }
+    }
+  };
+  auto finish_tile = [&]() {
+    if (pl.epl) store_tile_lds();
+    else store_tile();
+  };
+
   // stream-K part: this virtual CU's iterations [s0, s1) of the first sk_tiles tiles
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
   int* flag = reinterpret_cast<int*>(&lds[0][0][0][0]);
@@ -345,7 +408,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict
     segment(tile, k0, k1);
     gi += k1 - k0;
     if (k0 == 0 && k1 == T) {
-      store_tile();
+      finish_tile();
       continue;
     }
     // partial tile: publish (sc1 stores, 1 KiB per wave-instruction), ticket, the last arriver finishes
@@ -394,13 +457,13 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict
             for (int q = 0; q < 4; ++q) acc[2 * hh + i][j][q] += __uint_as_float(v[i][j][q]);
       }
     }
-    store_tile();
+    finish_tile();
   }
 
   // data-parallel part: whole tiles sk_tiles + vc, + P, ...
   for (int tile = pl.sk_tiles + vc; tile < pl.ntiles; tile += P) {
     segment(tile, 0, T);
-    store_tile();
+    finish_tile();
   }
 }
 
@@ -410,6 +473,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict
 // for fewer partial tiles: the grid shrinks instead).  sk = false: whole tiles only (ceil(tiles / ncu) rounds).
 static SkPlan sk_plan(int M, int KB, int NBtot, int BM, int NBT, int ncu, int min_share, bool sk, int* grid) {
   SkPlan pl;
+  pl.epl = 0;
   pl.ntm = (M + BM - 1) / BM;
   pl.ntiles = pl.ntm * ((NBtot + NBT - 1) / NBT);
   pl.T = (KB + 1) / 2;
@@ -458,11 +522,16 @@ static float sk_cfg_time(const SkCfg& c, int M, int KB, int NBtot, int ncu, bool
   return *use_sk ? skt : dp;
 }
 
+// epilogue mode of the next launches (lsa_gemm_sk_epilogue): 0 direct, 1 through LDS
+static int g_sk_epl = 1;
+extern "C" void lsa_gemm_sk_epilogue(int mode) { g_sk_epl = mode ? 1 : 0; }
+
 template <int BM, int WN>
 static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
                      float* ws, int* tickets, int ncu, int min_share, bool sk, int* grid_out, hipStream_t stream) {
   int grid = 0;
-  const SkPlan pl = sk_plan(M, KB, NBtot, BM, 4 * WN, ncu, min_share, sk, &grid);
+  SkPlan pl = sk_plan(M, KB, NBtot, BM, 4 * WN, ncu, min_share, sk, &grid);
+  pl.epl = g_sk_epl;
   if (pl.sk_tiles > 2 * ncu || grid > ncu || (long long)pl.sk_tiles * pl.T * (grid + 1) >= (1LL << 31)) return -3;
   if (grid_out) *grid_out = grid;
   switch (epi) {

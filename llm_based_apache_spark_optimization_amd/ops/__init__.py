@@ -15,6 +15,7 @@ import dataclasses
 import importlib
 import importlib.util
 import json
+import math
 import os
 from typing import NamedTuple, Optional
 
@@ -407,10 +408,34 @@ def _sk_workspace(device) -> tuple:
 SK_CFGS = ((256, 256), (256, 192), (256, 128), (128, 256), (128, 192), (128, 128))
 
 
+_SK_TUNING_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_sk_tuning.json")
+_sk_tuning: Optional[dict] = None
+_SK_BUCKETS = (128, 256, 512, 1024, 2048, 4096)
+
+
+def sk_config(M: int, N: int, K: int, epi: str) -> int:
+    """Tile configuration for a prefill GEMM: the measured table (scripts/bench_prefill_gemm.py --grid ->
+    scripts/make_sk_tuning.py -> gemm_sk_tuning.json; the nearest measured M in log scale), else -1 (the kernel's
+    tile-shape cost model)."""
+    global _sk_tuning
+    if _sk_tuning is None:
+        try:
+            with open(_SK_TUNING_PATH) as f:
+                _sk_tuning = json.load(f)
+        except (OSError, ValueError):
+            _sk_tuning = {}
+    b = min(_SK_BUCKETS, key=lambda c: abs(math.log2(c) - math.log2(max(M, 1))))
+    e = _sk_tuning.get(f"{N}x{K}:{'res' if epi in ('res', 'f32') else epi}:m{b}")
+    return int(e["cfg"]) if e is not None else -1
+
+
 def gemm_sk(x: torch.Tensor, wf: torch.Tensor, N: int, out: torch.Tensor, epi: str,
-            min_share: Optional[int] = None, cfg: int = -1) -> torch.Tensor:
+            min_share: Optional[int] = None, cfg: Optional[int] = None) -> torch.Tensor:
     """out (epi 'bf16' / 'f32' / 'silu') or h (epi 'res': h[:M] += x @ W^T) from the stream-K prefill GEMM over the
-    fragment-layout bf16 weight ``wf``.  cfg: -1 = the kernel's tile-shape cost model, else an SK_CFGS index."""
+    fragment-layout bf16 weight ``wf``.  cfg: None = the measured table (``sk_config``), -1 = the kernel's
+    tile-shape cost model, else an SK_CFGS index (+ 8: whole tiles only)."""
+    if cfg is None:
+        cfg = sk_config(x.shape[0], N, x.shape[1], epi)
     ws, tk, ncu = _sk_workspace(x.device)
     ext().gemm_sk(x, wf, N, out, _SK_EPI[epi], ws, tk, ncu, SK_MIN_SHARE if min_share is None else min_share, cfg)
     return out

@@ -50,8 +50,10 @@ for m in (128, 256, 512, 1024, 2048, 4096):
 ap = argparse.ArgumentParser()
 ap.add_argument("shapes", nargs="?", default="")
 ap.add_argument("--shares", default=str(ops.SK_MIN_SHARE))
-ap.add_argument("--cfgs", default="-1", help="tile configurations (ops.SK_CFGS index, +8 whole tiles only; -1 auto)")
+ap.add_argument("--cfgs", default="-2", help="tile configurations (ops.SK_CFGS index, +8 whole tiles only; -1 the "
+                "kernel's cost model, -2 the measured table the engine uses)")
 ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--epls", default="1", help="epilogue modes to compare (0 direct, 1 through LDS)")
 ap.add_argument("--grid", action="store_true")
 ap.add_argument("--no-vendor", action="store_true")
 args = ap.parse_args()
@@ -59,6 +61,7 @@ src = GRID if args.grid else SHAPES
 shapes = {k: v for k, v in src.items() if not args.shapes or k in args.shapes.split(",")}
 shares = [int(s) for s in args.shares.split(",")]
 cfgs = [int(c) for c in args.cfgs.split(",")]
+epls = [int(c) for c in args.epls.split(",")]
 e = ops.ext()
 for name, (M, N, K, epi) in shapes.items():
     torch.manual_seed(0)
@@ -83,8 +86,15 @@ for name, (M, N, K, epi) in shapes.items():
         if epi == "silu" and cf >= 0 and ops.SK_CFGS[cf & 7][1] % 128:
             continue  # SiLU pairs need an even n-block count per wave
         for sh in shares:
-            tag = "auto" if cf < 0 else ("%dx%d" % ops.SK_CFGS[cf & 7]) + ("dp" if cf >= 8 else "")
-            arms[f"sk_{tag}_s{sh}"] = (lambda sh=sh, cf=cf: ops.gemm_sk(x, pw.data, N, out, epi, min_share=sh, cfg=cf))
+            for ep in epls:
+                tag = ("table" if cf == -2 else "auto") if cf < 0 else ("%dx%d" % ops.SK_CFGS[cf & 7]) + (
+                    "dp" if cf >= 8 else "")
+                name = f"sk_{tag}_s{sh}" + ("" if len(epls) == 1 else f"_e{ep}")
+
+                def arm(sh=sh, cf=cf, ep=ep):
+                    e.gemm_sk_epilogue(ep)
+                    ops.gemm_sk(x, pw.data, N, out, epi, min_share=sh, cfg=None if cf == -2 else cf)
+                arms[name] = arm
     if epi == "silu":
         def blas():
             torch.mm(x, wt, out=y16)
