@@ -68,14 +68,6 @@ __device__ __forceinline__ void ds_read_frags(u32x4_t* r, uint32_t base, std::in
   ((r[Is] = ds_read16_off<(HALF * 16 + Is) * 1024>(base)), ...);
 }
 
-struct SkPlan {
-  int ntm;              // 256-row tiles
-  int ntiles;           // output tiles (row tile fastest)
-  int T;                // K-tiles of 64 per output tile
-  int sk_tiles;         // tiles [0, sk_tiles) are stream-K, the rest data-parallel
-  int sk_iters;         // sk_tiles * T (host-checked: sk_iters * (grid + 1) < 2^31, so 32-bit index math)
-  int epl;              // epilogue: 0 = straight from the accumulators, 1 = through an LDS image (full-row stores)
-};
 
 // first stream-K iteration of virtual CU c
 __device__ __forceinline__ int sk_start(int c, int iters, int P) { return (int)((unsigned)(c * iters) / (unsigned)P); }
@@ -90,6 +82,17 @@ __device__ __forceinline__ int sk_slot(int c, int t, int iters, int P, int T) {
 }
 
 }  // namespace
+
+// stream-K plan of a launch (external linkage: the kernel templates take it by value)
+struct SkPlan {
+  int ntm;              // 256-row tiles
+  int ntiles;           // output tiles (row tile fastest)
+  int T;                // K-tiles of 64 per output tile
+  int sk_tiles;         // tiles [0, sk_tiles) are stream-K, the rest data-parallel
+  int sk_iters;         // sk_tiles * T (host-checked: sk_iters * (grid + 1) < 2^31, so 32-bit index math)
+  int epl;              // epilogue: 0 = straight from the accumulators, 1 = through an LDS image (full-row stores)
+};
+
 
 // Tile geometry: BM rows (128 | 256) x WN * 64 columns (WN n-blocks of 16 per wave: 2 | 3 | 4), 8 waves as 2 (M) x 4
 // (N), each wave owning (BM / 2) x (WN * 16).  A wave's output splits into quadrants (qm, qn): qm halves its rows,
@@ -112,11 +115,12 @@ struct TileCfg {
   static constexpr int NBT = 4 * WN;     // n-blocks per tile
 };
 
+// The kernel body is a __device__ function template behind a thin __global__ wrapper: hipcc's host pass does not
+// emit the launch stub of a kernel template whose own body holds generic (integral_constant) lambdas.
 template <int BM, int WN, int EPI>
-__global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
-                                                      const uint4* __restrict__ Wf, int NBtot,
-                                                      void* __restrict__ out, int ldo, SkPlan pl,
-                                                      float* __restrict__ ws, int* __restrict__ tickets) {
+__device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int ldx, int M, int KB,
+                                             const uint4* __restrict__ Wf, int NBtot, void* __restrict__ out, int ldo,
+                                             const SkPlan& pl, float* __restrict__ ws, int* __restrict__ tickets) {
   using C = TileCfg<BM, WN>;
   constexpr int MI = C::MI, NQ0 = C::NQ0, NQ1 = C::NQ1;
   static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF <= 16 && C::WF0 <= 16, "tile geometry");
@@ -465,6 +469,14 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict
     segment(tile, 0, T);
     finish_tile();
   }
+}
+
+template <int BM, int WN, int EPI>
+__global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
+                                                      const uint4* __restrict__ Wf, int NBtot,
+                                                      void* __restrict__ out, int ldo, SkPlan pl,
+                                                      float* __restrict__ ws, int* __restrict__ tickets) {
+  gemm_sk_body<BM, WN, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets);
 }
 
 // Plan for a grid of (at most) ncu workgroups over BM x (NBT * 16) tiles: the data-parallel rounds keep whole tiles;

@@ -48,7 +48,45 @@ def ext():
             "gfx950 extension _lsa_hip is not built/loadable; run "
             "`python -m llm_based_apache_spark_optimization_amd.ops.build`"
         ) from _ext_err
+    if not BUILD_INFO:
+        _check_provenance()
     return _ext
+
+
+# build provenance of the loaded extension (ops/build.py writes _lsa_hip.provenance.json next to the .so): the
+# sources hash it was built from, its own hash, and whether both still match the tree -- a stale .so (kernels
+# edited, not rebuilt) fails loudly on load instead of silently running old kernels (LSA_ALLOW_STALE_EXT=1 to
+# override, e.g. for A/B builds)
+BUILD_INFO: dict = {}
+
+
+def _check_provenance() -> None:
+    import hashlib
+
+    from . import build as _b
+
+    so = getattr(_ext, "__file__", "") or ""
+    info = {"so": os.path.basename(so)}
+    try:
+        rec = json.loads(_b.PROVENANCE.read_text())
+    except (OSError, ValueError):
+        rec = None
+    info["provenance"] = rec
+    if rec is not None and so and os.path.abspath(so) == str(_b.HIP_EXT):
+        try:
+            with open(so, "rb") as f:
+                info["so_match"] = hashlib.sha256(f.read()).hexdigest()[:16] == rec.get("so_sha256")
+        except OSError:
+            info["so_match"] = False
+        try:
+            info["sources_match"] = _b.sources_sha() == rec.get("sources_sha")
+        except OSError:  # sources not shipped with this tree
+            info["sources_match"] = None
+    BUILD_INFO.update(info)
+    if (info.get("so_match") is False or info.get("sources_match") is False) and \
+            os.environ.get("LSA_ALLOW_STALE_EXT") != "1":
+        raise RuntimeError(f"_lsa_hip.so does not match its sources / provenance record ({info}); rebuild with "
+                           "`python -m llm_based_apache_spark_optimization_amd.ops.build`")
 
 
 def hip_available() -> bool:

@@ -70,6 +70,38 @@ def _torch_flags() -> tuple[list[str], list[str]]:
     return cflags, ldflags
 
 
+def hip_sources() -> list[Path]:
+    """Every source the gfx950 extension is compiled from (kernels, headers, bindings)."""
+    kdir = CSRC / "kernels"
+    return sorted(kdir.glob("*.hip")) + sorted(kdir.glob("*.h")) + [CSRC / "bindings.cpp"]
+
+
+def sources_sha() -> str:
+    """Content hash of the extension's sources (relative path + bytes, in path order): what a build provenance
+    record pins and what ``ops.ext()`` re-checks on load."""
+    h = hashlib.sha256()
+    for p in hip_sources():
+        h.update(str(p.relative_to(REPO)).encode() + b"\0" + p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+PROVENANCE = HIP_EXT.with_suffix(".provenance.json")
+
+
+def _write_provenance(kflags: list[str]) -> None:
+    import json
+    import time
+
+    try:
+        ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.splitlines()
+    except OSError:
+        ver = []
+    rec = {"sources_sha": sources_sha(), "so_sha256": hashlib.sha256(HIP_EXT.read_bytes()).hexdigest()[:16],
+           "arch": ARCH, "kernel_flags": kflags, "hipcc": next((v for v in ver if "version" in v.lower()), ""),
+           "built_unix": int(time.time())}
+    PROVENANCE.write_text(json.dumps(rec, indent=1))
+
+
 def build_hip(jobs: int = 8, verbose: bool = False) -> Path:
     kdir = CSRC / "kernels"
     headers = sorted(kdir.glob("*.h"))
@@ -86,9 +118,12 @@ def build_hip(jobs: int = 8, verbose: bool = False) -> Path:
     key = hashlib.sha1("".join(sorted(o.name for o in objs)).encode()).hexdigest()[:16]
     stamp = HIP_EXT.with_suffix(".stamp")
     if HIP_EXT.exists() and stamp.exists() and stamp.read_text() == key:
+        if not PROVENANCE.exists():
+            _write_provenance(kflags)
         return HIP_EXT
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(HIP_EXT), *ldflags])
     stamp.write_text(key)
+    _write_provenance(kflags)
     if verbose:
         print(f"built {HIP_EXT}")
     return HIP_EXT
