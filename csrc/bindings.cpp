@@ -64,6 +64,10 @@ int lsa_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wf, int N, vo
 int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const float* wscale, int N, void* out,
                      int epi, int nb, int splitk, int xfrag, hipStream_t stream);
 void lsa_gemm_sk_epilogue(int mode);
+int lsa_gemm_sk_rope(const void* X, int ldx, int M, int K, const void* Wf, int N, float* ws, int* tickets, int ncu,
+                     int min_share, int cfg, const int* pos, const int* tok_seq, const int* block_tables,
+                     int max_blocks, const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int H,
+                     int Hkv, int* grid_out, int* cfg_out, hipStream_t stream);
 int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
                 int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
@@ -351,6 +355,48 @@ int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor
   check(lsa_gemm_sk(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), (int)epi, ws.data_ptr<float>(),
                     tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, &grid, &used, cur_stream()),
         "gemm_sk");
+  return (int64_t)grid * 16 + used;
+}
+
+// the prefill qkv projection with RoPE and the paged bf16 KV-cache append in its epilogue (gemm_tile256.hip
+// EPI_ROPE): q_out [T, H, 128], kc / vc [blocks, Hkv, 64, 128] bf16, pos / tok_seq [T] int32, block_tables
+// [seqs, max_blocks] int32, cos / sin [max_pos, 64] f32.  Returns grid * 16 + the configuration used.
+int64_t gemm_sk_rope(const at::Tensor& x, const at::Tensor& wf, at::Tensor& ws, at::Tensor& tickets, int64_t ncu,
+                     int64_t min_share, int64_t cfg, const at::Tensor& pos, const c10::optional<at::Tensor>& tok_seq,
+                     const at::Tensor& block_tables, const at::Tensor& cos_t, const at::Tensor& sin_t,
+                     at::Tensor& q_out, at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv) {
+  need(x, at::kBFloat16, "x");
+  need(wf, at::kBFloat16, "wf");
+  need(ws, at::kFloat, "ws");
+  need(tickets, at::kInt, "tickets");
+  need(pos, at::kInt, "pos");
+  need(block_tables, at::kInt, "block_tables");
+  need(cos_t, at::kFloat, "cos_t");
+  need(sin_t, at::kFloat, "sin_t");
+  need(q_out, at::kBFloat16, "q_out");
+  need(kc, at::kBFloat16, "kc");
+  need(vc, at::kBFloat16, "vc");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
+  const int64_t M = x.size(0), K = x.size(1), N = (H + 2 * Hkv) * 128;
+  TORCH_CHECK(H > 0 && Hkv > 0 && wf.numel() == N * K, "gemm_sk_rope: weight numel != (H + 2 Hkv) * 128 * K");
+  TORCH_CHECK(pos.numel() >= M && q_out.is_contiguous() && q_out.numel() >= M * H * 128, "gemm_sk_rope: q_out / pos");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(2) == 64 && kc.size(3) == 128 && kc.sizes() == vc.sizes() &&
+                  kc.is_contiguous() && vc.is_contiguous(), "gemm_sk_rope: cache [blocks, Hkv, 64, 128]");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.is_contiguous(), "gemm_sk_rope: block_tables [seqs, max_blocks]");
+  TORCH_CHECK(cos_t.dim() == 2 && cos_t.size(1) == 64 && cos_t.sizes() == sin_t.sizes(), "gemm_sk_rope: cos / sin");
+  if (tok_seq.has_value()) {
+    need(*tok_seq, at::kInt, "tok_seq");
+    TORCH_CHECK(tok_seq->numel() >= M, "gemm_sk_rope: tok_seq");
+  }
+  TORCH_CHECK(ncu >= 8 && ncu <= 1024 && ws.numel() * 4 >= lsa_gemm_sk_ws_bytes((int)ncu) &&
+                  tickets.numel() >= lsa_gemm_sk_tickets((int)ncu), "gemm_sk_rope: workspace too small");
+  int grid = 0, used = 0;
+  check(lsa_gemm_sk_rope(x.data_ptr(), x.stride(0), (int)M, (int)K, wf.data_ptr(), (int)N, ws.data_ptr<float>(),
+                         tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, pos.data_ptr<int>(),
+                         ptr<int>(tok_seq), block_tables.data_ptr<int>(), (int)block_tables.size(1),
+                         cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), q_out.data_ptr(), kc.data_ptr(),
+                         vc.data_ptr(), (int)H, (int)Hkv, &grid, &used, cur_stream()),
+        "gemm_sk_rope");
   return (int64_t)grid * 16 + used;
 }
 
@@ -823,6 +869,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("ws"),
         py::arg("tickets"), py::arg("ncu"), py::arg("min_share") = 0, py::arg("cfg") = -1);
+  m.def("gemm_sk_rope", &gemm_sk_rope);
   m.def("gemm_sk_epilogue", [](int64_t mode) { lsa_gemm_sk_epilogue((int)mode); });
   m.def("gemm_sk_ws_bytes", [](int64_t ncu) { return lsa_gemm_sk_ws_bytes((int)ncu); });
   m.def("gemm_sk_tickets", [](int64_t ncu) { return (int64_t)lsa_gemm_sk_tickets((int)ncu); });

@@ -93,6 +93,24 @@ struct SkPlan {
   int epl;              // epilogue: 0 = straight from the accumulators, 1 = through an LDS image (full-row stores)
 };
 
+// EPI_ROPE (prefill qkv projection, bf16 KV cache): the GEMM's output row t is token t's q | k | v; the epilogue
+// rotates q and k (RoPE, rotate-half, from the f32 accumulators), writes q to q_out [T][H][128] and appends k / v
+// to the paged cache at (block_tables[tok_seq[t]][pos[t] / 64], kv-head, pos[t] % 64) -- the qkv activation never
+// makes a round trip through HBM and the rope_append launch is gone.  Tiles of 128 / 256 columns hold whole heads.
+#define EPI_ROPE 4
+struct RopeEpi {
+  const int* pos;
+  const int* tok_seq;
+  const int* bt;
+  int max_blocks;
+  const float* cos_t;  // [max_pos][64]
+  const float* sin_t;
+  uint16_t* q_out;
+  uint16_t* kc;
+  uint16_t* vc;
+  int H, Hkv;
+};
+
 
 // Tile geometry: BM rows (128 | 256) x WN * 64 columns (WN n-blocks of 16 per wave: 2 | 3 | 4), 8 waves as 2 (M) x 4
 // (N), each wave owning (BM / 2) x (WN * 16).  A wave's output splits into quadrants (qm, qn): qm halves its rows,
@@ -120,11 +138,13 @@ struct TileCfg {
 template <int BM, int WN, int EPI>
 __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                              const uint4* __restrict__ Wf, int NBtot, void* __restrict__ out, int ldo,
-                                             const SkPlan& pl, float* __restrict__ ws, int* __restrict__ tickets) {
+                                             const SkPlan& pl, float* __restrict__ ws, int* __restrict__ tickets,
+                                             const RopeEpi& re) {
   using C = TileCfg<BM, WN>;
   constexpr int MI = C::MI, NQ0 = C::NQ0, NQ1 = C::NQ1;
   static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF <= 16 && C::WF0 <= 16, "tile geometry");
   static_assert(EPI != EPI_SILU || WN % 2 == 0, "SiLU pairs (gate, up) n-blocks inside one wave");
+  static_assert(EPI != EPI_ROPE || WN % 2 == 0, "RoPE tiles hold whole 128-column heads");
   __shared__ __attribute__((aligned(16))) uint4 lds[2][4][16][64];
   const int lane = threadIdx.x & 63;
   // wave ids through readfirstlane: provably uniform, so every per-wave address term lives in SGPRs
@@ -298,6 +318,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   // epilogue of a finished tile: acc[i][j] = D[n = nb_j * 16 + 4 g + q][m = mb_i * 16 + (lane & 15)]
   const int g = lane >> 4;
   auto store_tile = [&]() {
+    if constexpr (EPI == EPI_ROPE) return;  // the RoPE epilogue always runs through the LDS image
 #pragma unroll
     for (int i = 0; i < 2 * MI; ++i) {
       const int m = mbase + wm * (BM / 2) + i * 16 + (lane & 15);
@@ -373,6 +394,41 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
         }
       }
       __syncthreads();
+      if constexpr (EPI == EPI_ROPE) {
+        // one row per wave-instruction: the token's position, sequence and cache block are wave-uniform
+        for (int r = w; r < BM / 2; r += 8) {
+          const int m = mbase + pass * (BM / 2) + r;
+          const int ch = lane;
+          if (m >= M || ch >= CH || col0 + ch * 4 >= ncol_out) continue;
+          const int c = col0 + ch * 4, head = c >> 7, d = c & 127;
+          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2));
+          f32x4_t y = v;
+          const int p = re.pos[m];
+          if (head < re.H + re.Hkv) {  // rotate-half with the partner 64 dims away (same tile: whole heads)
+            const int pch = d < 64 ? ch + 16 : ch - 16;
+            const f32x4_t pv = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((pch ^ (r & 15)) << 2));
+            const int d0 = d & 63;
+            const float4 cs = *reinterpret_cast<const float4*>(re.cos_t + (size_t)p * 64 + d0);
+            const float4 sn = *reinterpret_cast<const float4*>(re.sin_t + (size_t)p * 64 + d0);
+            const float sg = d < 64 ? -1.f : 1.f;
+            y[0] = v[0] * cs.x + sg * pv[0] * sn.x;
+            y[1] = v[1] * cs.y + sg * pv[1] * sn.y;
+            y[2] = v[2] * cs.z + sg * pv[2] * sn.z;
+            y[3] = v[3] * cs.w + sg * pv[3] * sn.w;
+          }
+          const uint2 pk = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+          if (head < re.H) {
+            *reinterpret_cast<uint2*>(re.q_out + ((size_t)m * re.H + head) * 128 + d) = pk;
+          } else {
+            const int seq = re.tok_seq ? re.tok_seq[m] : m;
+            const int blk = re.bt[(size_t)seq * re.max_blocks + (p >> 6)];
+            const int hk = head < re.H + re.Hkv ? head - re.H : head - re.H - re.Hkv;
+            uint16_t* cache = head < re.H + re.Hkv ? re.kc : re.vc;
+            *reinterpret_cast<uint2*>(cache + (((size_t)blk * re.Hkv + hk) * 64 + (p & 63)) * 128 + d) = pk;
+          }
+        }
+        continue;
+      }
       for (int r = w; r < BM / 2; r += 8) {
         const int m = mbase + pass * (BM / 2) + r;
         const int ch = lane;
@@ -395,8 +451,8 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     }
   };
   auto finish_tile = [&]() {
-    if (pl.epl) store_tile_lds();
-    else store_tile();
+    if (EPI == EPI_ROPE || pl.epl) store_tile_lds();
+    else if constexpr (EPI != EPI_ROPE) store_tile();
   };
 
   // stream-K part: this virtual CU's iterations [s0, s1) of the first sk_tiles tiles
@@ -475,8 +531,9 @@ template <int BM, int WN, int EPI>
 __global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                                       const uint4* __restrict__ Wf, int NBtot,
                                                       void* __restrict__ out, int ldo, SkPlan pl,
-                                                      float* __restrict__ ws, int* __restrict__ tickets) {
-  gemm_sk_body<BM, WN, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets);
+                                                      float* __restrict__ ws, int* __restrict__ tickets,
+                                                      RopeEpi re) {
+  gemm_sk_body<BM, WN, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets, re);
 }
 
 // Plan for a grid of (at most) ncu workgroups over BM x (NBT * 16) tiles: the data-parallel rounds keep whole tiles;
@@ -540,7 +597,8 @@ extern "C" void lsa_gemm_sk_epilogue(int mode) { g_sk_epl = mode ? 1 : 0; }
 
 template <int BM, int WN>
 static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
-                     float* ws, int* tickets, int ncu, int min_share, bool sk, int* grid_out, hipStream_t stream) {
+                     float* ws, int* tickets, int ncu, int min_share, bool sk, int* grid_out, const RopeEpi& re,
+                     hipStream_t stream) {
   int grid = 0;
   SkPlan pl = sk_plan(M, KB, NBtot, BM, 4 * WN, ncu, min_share, sk, &grid);
   pl.epl = g_sk_epl;
@@ -549,13 +607,20 @@ static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const u
   switch (epi) {
 #define LSA_SKL(E) \
   hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, \
-                     pl, ws, tickets)
+                     pl, ws, tickets, re)
     case EPI_BF16: LSA_SKL(EPI_BF16); break;
     case EPI_F32: LSA_SKL(EPI_F32); break;
     case EPI_RES: LSA_SKL(EPI_RES); break;
     case EPI_SILU:
       if constexpr (WN % 2 == 0) {
         LSA_SKL(EPI_SILU);
+        break;
+      } else {
+        return -2;
+      }
+    case EPI_ROPE:
+      if constexpr (WN % 2 == 0) {
+        LSA_SKL(EPI_ROPE);
         break;
       } else {
         return -2;
@@ -571,18 +636,19 @@ static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const u
 // out: bf16 [M][N] (EPI_BF16), f32 [M][N] (EPI_F32), bf16 [M][N / 2] (EPI_SILU), f32 h [M][N] accumulated (EPI_RES).
 // cfg: -1 = the cost model's pick, else an index into kSkCfgs (+ 8: whole tiles only, no stream-K remainder);
 // *cfg_out = the configuration used (same encoding).
-extern "C" int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
-                           int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out,
-                           hipStream_t stream) {
+static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
+                        int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, const RopeEpi& re,
+                        hipStream_t stream) {
   if (K % 32 != 0 || N % 16 != 0 || M <= 0 || ncu < 8 || ncu > 1024 || !ws || !tickets) return -1;
   if (epi == EPI_SILU && N % 32 != 0) return -2;
+  const bool even_wn = epi == EPI_SILU || epi == EPI_ROPE;  // tile configurations with an even n-block count/wave
   const int KB = K / 32, NBtot = N / 16;
   const int ncfg = (int)(sizeof(kSkCfgs) / sizeof(kSkCfgs[0]));
   bool sk = true;
   if (cfg < 0) {
     float best = 3.0e38f;
     for (int i = 0; i < ncfg; ++i) {
-      if (epi == EPI_SILU && kSkCfgs[i].wn % 2) continue;
+      if (even_wn && kSkCfgs[i].wn % 2) continue;
       bool u = false;
       const float t = sk_cfg_time(kSkCfgs[i], M, KB, NBtot, ncu, &u);
       if (t < best) best = t, cfg = i, sk = u;
@@ -591,6 +657,7 @@ extern "C" int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf,
     sk = cfg < 8;
     cfg &= 7;
     if (cfg >= ncfg) return -5;
+    if (even_wn && kSkCfgs[cfg].wn % 2) cfg = kSkCfgs[cfg].bm == 256 ? 0 : 3;  // BN 192 -> the 256-column tile
   }
   if (cfg_out) *cfg_out = cfg + (sk ? 0 : 8);
   const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
@@ -598,7 +665,7 @@ extern "C" int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf,
   const int ldo = epi == EPI_SILU ? N / 2 : N;
   switch (cfg) {
 #define LSA_SKC(I, BMV, WNV) \
-  case I: return sk_launch<BMV, WNV>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, grid_out, stream);
+  case I: return sk_launch<BMV, WNV>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, grid_out, re, stream);
     LSA_SKC(0, 256, 4)
     LSA_SKC(1, 256, 3)
     LSA_SKC(2, 256, 2)
@@ -608,4 +675,28 @@ extern "C" int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf,
 #undef LSA_SKC
     default: return -5;
   }
+}
+
+extern "C" int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
+                           int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out,
+                           hipStream_t stream) {
+  if (epi < 0 || epi > 3) return -4;
+  return gemm_sk_impl(X, ldx, M, K, Wf, N, out, epi, ws, tickets, ncu, min_share, cfg, grid_out, cfg_out, RopeEpi{},
+                      stream);
+}
+
+// the prefill qkv projection with RoPE + the paged bf16 KV-cache append fused into its epilogue (EPI_ROPE above);
+// N = (H + 2 Hkv) * 128
+extern "C" int lsa_gemm_sk_rope(const void* X, int ldx, int M, int K, const void* Wf, int N, float* ws, int* tickets,
+                                int ncu, int min_share, int cfg, const int* pos, const int* tok_seq,
+                                const int* block_tables, int max_blocks, const float* cos_t, const float* sin_t,
+                                void* q_out, void* kc, void* vc, int H, int Hkv, int* grid_out, int* cfg_out,
+                                hipStream_t stream) {
+  if (H <= 0 || Hkv <= 0 || N != (H + 2 * Hkv) * 128 || !pos || !block_tables || !cos_t || !sin_t || !q_out || !kc ||
+      !vc)
+    return -6;
+  const RopeEpi re{pos, tok_seq, block_tables, max_blocks, cos_t, sin_t, reinterpret_cast<uint16_t*>(q_out),
+                   reinterpret_cast<uint16_t*>(kc), reinterpret_cast<uint16_t*>(vc), H, Hkv};
+  return gemm_sk_impl(X, ldx, M, K, Wf, N, nullptr, EPI_ROPE, ws, tickets, ncu, min_share, cfg, grid_out, cfg_out, re,
+                      stream);
 }

@@ -491,6 +491,30 @@ def linear_res(x: torch.Tensor, w: PackedWeight, h: torch.Tensor) -> torch.Tenso
     return gemm_sk(x, wf, w.N, h, "res")
 
 
+def linear_rope(x: torch.Tensor, w: PackedWeight, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc,
+                H: int, Hkv: int) -> None:
+    """The prefill qkv projection with RoPE and the paged bf16 KV-cache append fused into the GEMM epilogue (M > 64,
+    bf16 cache): q_out [T, H, 128] = rotated q, the cache gets rotated k and v at each token's slot.  CPU: the
+    unfused reference (bf16 qkv, then ``rope_append``)."""
+    if not _gpu(x):
+        qkv = ref.linear(x, w.dense(), "bf16")
+        return ref.rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
+    wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
+    ws, tk, ncu = _sk_workspace(x.device)
+    ext().gemm_sk_rope(x, wf, ws, tk, ncu, SK_MIN_SHARE, sk_config(x.shape[0], w.N, x.shape[1], "bf16"), pos, tok_seq,
+                       block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
+
+
+def rope_fusable(w: PackedWeight, kv_fp8: bool) -> bool:
+    """Whether the prefill qkv projection can take the fused RoPE / cache-append epilogue (``linear_rope``): bf16
+    cache, and weights the stream-K kernel reads (bf16, or quantised ones through their bf16 dequantisation; the
+    W8A8 fp8 prefill keeps its split-K path)."""
+    return not kv_fp8 and res_supported(w) and ROPE_FUSED
+
+
+ROPE_FUSED = os.environ.get("LSA_ROPE_FUSED", "1") != "0"
+
+
 def res_supported(w: PackedWeight) -> bool:
     """Whether ``linear_res`` takes this weight (everything but W8A8 fp8 prefill, whose fp8 tile kernel writes
     split-K slabs)."""

@@ -988,3 +988,40 @@ def test_gemm_ragged_grid(gpu, kind, M, nb):
             got = ops.from_xfrag(y, M, N // 2) if (xf or kind == "fp8a") else y.view(M, N // 2)
             assert _rel(got, want_silu) < 1e-2, (kind, epi)
 
+
+
+@pytest.mark.parametrize("H,Hkv", [(24, 8), (32, 32), (4, 2)])
+@pytest.mark.parametrize("T", [65, 300, 1100])
+@pytest.mark.parametrize("cfg", [-1, 0, 3, 5, 8])
+def test_gemm_rope_epilogue(gpu, H, Hkv, T, cfg):
+    """Prefill qkv GEMM with RoPE + the paged KV-cache append in its epilogue (ops.linear_rope / EPI_ROPE) vs the
+    fp32 product rotated by the reference: q_out, and every appended cache row at its (block, kv-head, slot) --
+    two sequences packed, the second starting mid-block (chunked-prefill continuation), scattered block tables."""
+    K, D = 512, 128
+    N = (H + 2 * Hkv) * D
+    torch.manual_seed(T + H + cfg)
+    x = (torch.rand(T, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    t0 = T // 3
+    pos = torch.cat([torch.arange(t0), torch.arange(37, 37 + T - t0)]).to(torch.int32)
+    tok_seq = torch.cat([torch.zeros(t0), torch.ones(T - t0)]).to(torch.int32)
+    nblk = 64
+    perm = torch.randperm(nblk - 1) + 1
+    bt = torch.stack([perm[:24], perm[24:48]]).to(torch.int32)
+    cos, sin = ref.rope_tables(128, 4096, 10000.0, None)
+    kc = torch.zeros(nblk, Hkv, 64, D, device=gpu, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    q = torch.zeros(T, H, D, device=gpu, dtype=torch.bfloat16)
+    ws, tk, ncu = ops._sk_workspace(gpu)
+    ops.ext().gemm_sk_rope(x, pw.data, ws, tk, ncu, 4, cfg, pos.to(gpu), tok_seq.to(gpu), bt.to(gpu), cos.to(gpu),
+                           sin.to(gpu), q, kc, vc, H, Hkv)
+    torch.cuda.synchronize()
+    assert int(tk.abs().sum()) == 0
+    qkv = x.float().cpu() @ w.float().cpu().t()
+    q_r = torch.zeros(T, H, D, dtype=torch.bfloat16)
+    kc_r, vc_r = torch.zeros(nblk, Hkv, 64, D, dtype=torch.bfloat16), torch.zeros(nblk, Hkv, 64, D, dtype=torch.bfloat16)
+    ref.rope_append(qkv, pos, tok_seq, bt, cos, sin, q_r, kc_r, vc_r, H, Hkv)
+    assert _rel(q.cpu(), q_r) < 4e-3
+    assert _rel(kc.cpu(), kc_r) < 4e-3 and _rel(vc.cpu(), vc_r) < 4e-3
+    assert int((kc.cpu() != 0).any(-1).sum()) == T * Hkv  # exactly one appended row per token and kv-head
