@@ -168,3 +168,28 @@ def test_hf_tokenizer_checkpoint_llama3_specials(tmp_path):
     assert ids["<|eot_id|>"] in eng.runner.eos_list
     r = eng.generate(["SELECT"], SamplingParams(max_tokens=3, ignore_eos=True), system=EXPLAIN_SYSTEM)[0]
     assert r.eval_count == 3 and isinstance(r.text, str)
+
+
+def test_full_width_duckdb_nsql_layers_match_transformers():
+    """BASELINE config 1 at the served model's full width: duckdb-nsql-7B's exact shapes (d 4096, 32 MHA heads,
+    ffn 11008, vocab 32000, untied head) with 2 of its 32 layers, random-init in transformers, through the engine on
+    CPU: prefill logits and greedy decoding vs HF (the tiny configs above check the same path at test sizes)."""
+    import dataclasses
+
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    spec = dataclasses.replace(get_spec("duckdb-nsql"), n_layers=2)
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(LlamaConfig(**spec.to_hf_config(), initializer_range=0.02))
+    inv = m.model.rotary_emb.inv_freq.clone()
+    m = m.to(torch.bfloat16).float().eval()
+    m.model.rotary_emb.inv_freq.copy_(inv)
+    assert (m.config.hidden_size, m.config.intermediate_size, m.config.vocab_size) == (4096, 11008, 32000)
+    eng = LLMEngine(ModelRunner(from_hf_state_dict(spec, m.state_dict(), "cpu"), max_slots=2, max_model_len=256))
+    p = [1] + list(range(300, 340))
+    r = eng.generate([p], SamplingParams(max_tokens=6, ignore_eos=True))[0]
+    with torch.no_grad():
+        lg = m(torch.tensor([p + r.token_ids])).logits[0, len(p) - 1:-1]
+    chosen = lg.gather(1, torch.tensor(r.token_ids).view(-1, 1)).squeeze(1)
+    gap = lg.max(1).values - chosen
+    assert (gap <= 0.05 * lg.max(1).values.abs() + 0.05).all(), gap
