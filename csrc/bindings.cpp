@@ -75,7 +75,7 @@ int lsa_silu_bf16(const void* y, int M, int F, void* out, hipStream_t s);
 void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                        const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
-                       void* out, int ng, hipStream_t s);
+                       void* out, int ng, int pipe, hipStream_t s);
 int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
 int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
                       void* out, int epi, int splitk, hipStream_t stream);
@@ -329,7 +329,7 @@ void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) 
 // large-M (prefill) linear layer on the stream-K 256x256 tile kernel (kernels/gemm_tile256.hip).  epi: 0 bf16 [M][N],
 // 1 f32 [M][N], 2 SiLU(gate) * up bf16 [M][N / 2], 3 h f32 [M][N] += x @ W^T.  ws / tickets: the per-stream
 // workspace (ops._sk_workspace).  cfg: -1 = the kernel's cost model, else a tile configuration index (+ 8: whole
-// tiles only).  Returns grid * 16 + the configuration used.
+// tiles only; + 16 + 32 * mode: that epilogue mode for this call).  Returns grid * 16 + the configuration used.
 int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, at::Tensor& ws,
                 at::Tensor& tickets, int64_t ncu, int64_t min_share, int64_t cfg) {
   need(x, at::kBFloat16, "x");
@@ -350,7 +350,7 @@ int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor
     need(out, at::kBFloat16, "out");
     TORCH_CHECK(out.numel() >= (int64_t)M * (epi == 2 ? N / 2 : N), "bf16 out too small");
   }
-  TORCH_CHECK(cfg >= -1 && cfg < 16, "gemm_sk: cfg");
+  TORCH_CHECK(cfg >= -1 && cfg < 64, "gemm_sk: cfg");
   int grid = 0, used = 0;
   check(lsa_gemm_sk(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), (int)epi, ws.data_ptr<float>(),
                     tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, &grid, &used, cur_stream()),
@@ -665,13 +665,14 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& v
   TORCH_CHECK(q.dim() == 3 && q.size(1) == H && q.size(2) == 128 && out.sizes() == q.sizes(), "q / out [T, H, 128]");
   TORCH_CHECK(cu_q.numel() == ctx_lens.numel() + 1 && block_tables.size(0) >= ctx_lens.numel(),
               "cu_q [nseq + 1], ctx_lens [nseq], block_tables [>= nseq, max_blocks]");
-  if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip)
+  if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip); 2 = pipelined loop
     // work [n_workgroups, 4 * NG]: NG (seq, q_start, t0, t1) items per workgroup (ops.prefill_plan)
     TORCH_CHECK(work.dim() == 2 && (work.size(1) == 4 || work.size(1) == 8) && work.is_contiguous(),
                 "attn_prefill32 work must be [n, 4] or [n, 8] int32");
     check(lsa_attn_prefill32(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                              block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
-                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 4), cur_stream()),
+                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 4),
+                             rows32 == 2 ? 1 : 0, cur_stream()),
           "attn_prefill32");
     return;
   }

@@ -398,6 +398,16 @@ int lsa_ar_run(float* data, long n, float* out, uint8_t* const* regions, int ran
   } else {                                                                                                     \
     if (mode & 1) AR_SUM(WV, 0, 1); else AR_SUM(WV, 0, 0);                                                      \
   }
+  switch (world) {
+    case 2: AR_LAUNCH(2); break;
+    case 3: AR_LAUNCH(3); break;
+    case 4: AR_LAUNCH(4); break;
+    case 5: AR_LAUNCH(5); break;
+    case 6: AR_LAUNCH(6); break;
+    case 7: AR_LAUNCH(7); break;
+    case 8: AR_LAUNCH(8); break;
+    default: return -1;
+  }
 #undef AR_LAUNCH
 #undef AR_SUM
   return (int)hipGetLastError();

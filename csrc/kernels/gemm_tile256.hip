@@ -597,11 +597,11 @@ extern "C" void lsa_gemm_sk_epilogue(int mode) { g_sk_epl = mode ? 1 : 0; }
 
 template <int BM, int WN>
 static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
-                     float* ws, int* tickets, int ncu, int min_share, bool sk, int* grid_out, const RopeEpi& re,
-                     hipStream_t stream) {
+                     float* ws, int* tickets, int ncu, int min_share, bool sk, int epl, int* grid_out,
+                     const RopeEpi& re, hipStream_t stream) {
   int grid = 0;
   SkPlan pl = sk_plan(M, KB, NBtot, BM, 4 * WN, ncu, min_share, sk, &grid);
-  pl.epl = g_sk_epl;
+  pl.epl = epl;
   if (pl.sk_tiles > 2 * ncu || grid > ncu || (long long)pl.sk_tiles * pl.T * (grid + 1) >= (1LL << 31)) return -3;
   if (grid_out) *grid_out = grid;
   switch (epi) {
@@ -634,8 +634,9 @@ static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const u
 // M > 64 linear layer (K % 32 == 0, N % 16 == 0; EPI_SILU needs N % 32 == 0).  ws: lsa_gemm_sk_ws_bytes(ncu)
 // bytes; tickets: lsa_gemm_sk_tickets(ncu) int32, zero before the first call (every call leaves them zero).
 // out: bf16 [M][N] (EPI_BF16), f32 [M][N] (EPI_F32), bf16 [M][N / 2] (EPI_SILU), f32 h [M][N] accumulated (EPI_RES).
-// cfg: -1 = the cost model's pick, else an index into kSkCfgs (+ 8: whole tiles only, no stream-K remainder);
-// *cfg_out = the configuration used (same encoding).
+// cfg: -1 = the cost model's pick, else an index into kSkCfgs (+ 8: whole tiles only, no stream-K remainder), + 16:
+// the epilogue mode given in bit 5 (+ 32 = through LDS) instead of lsa_gemm_sk_epilogue's; *cfg_out = the
+// configuration used (bits 0-3).
 static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
                         int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, const RopeEpi& re,
                         hipStream_t stream) {
@@ -645,6 +646,11 @@ static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, in
   const int KB = K / 32, NBtot = N / 16;
   const int ncfg = (int)(sizeof(kSkCfgs) / sizeof(kSkCfgs[0]));
   bool sk = true;
+  int epl = g_sk_epl;
+  if (cfg >= 0 && (cfg & 16)) {
+    epl = (cfg >> 5) & 1;
+    cfg &= 15;
+  }
   if (cfg < 0) {
     float best = 3.0e38f;
     for (int i = 0; i < ncfg; ++i) {
@@ -654,6 +660,7 @@ static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, in
       if (t < best) best = t, cfg = i, sk = u;
     }
   } else {
+    if (cfg > 15) return -5;
     sk = cfg < 8;
     cfg &= 7;
     if (cfg >= ncfg) return -5;
@@ -665,7 +672,7 @@ static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, in
   const int ldo = epi == EPI_SILU ? N / 2 : N;
   switch (cfg) {
 #define LSA_SKC(I, BMV, WNV) \
-  case I: return sk_launch<BMV, WNV>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, grid_out, re, stream);
+  case I: return sk_launch<BMV, WNV>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, stream);
     LSA_SKC(0, 256, 4)
     LSA_SKC(1, 256, 3)
     LSA_SKC(2, 256, 2)

@@ -1094,6 +1094,9 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
 # sequence has >= 512 rows (measured, scripts/bench_attn_prefill.py: 7B 2k 146 -> 119 us, 3B 2k 118 -> 115 us,
 # 8k 1051 -> 1021 us), else 16 (32 x 128-token prompts: 28 vs 31 us, twice the work items)
 PREFILL_ATTN = "auto"
+# 32-row kernel loop: 1 = pipelined (K fragments of tile t + 1 read into registers under tile t's P V, 2 K + 3 V
+# LDS buffers; attention_prefill32.hip attn_prefill32p_kernel), 0 = the one-barrier double-buffered loop
+PREFILL_PIPE = int(os.environ.get("LSA_PREFILL_PIPE", "0"))
 
 
 def _prefill_kernel(cu_q: list) -> str:
@@ -1193,7 +1196,7 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, wo
         plan = (prefill_plan(cu, ctx=ctx_lens.tolist(), heads=H, device=q.device) if work is None
                 else PrefillPlan(_prefill_kernel(cu), work))
     ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out,
-                       1 if plan.kernel == "32" else 0)
+                       (2 if PREFILL_PIPE else 1) if plan.kernel == "32" else 0)
     return out
 
 

@@ -89,12 +89,12 @@ for name, (M, N, K, epi) in shapes.items():
             for ep in epls:
                 tag = ("table" if cf == -2 else "auto") if cf < 0 else ("%dx%d" % ops.SK_CFGS[cf & 7]) + (
                     "dp" if cf >= 8 else "")
-                name = f"sk_{tag}_s{sh}" + ("" if len(epls) == 1 else f"_e{ep}")
+                arm_name = f"sk_{tag}_s{sh}" + ("" if len(epls) == 1 else f"_e{ep}")
 
                 def arm(sh=sh, cf=cf, ep=ep):
                     e.gemm_sk_epilogue(ep)
                     ops.gemm_sk(x, pw.data, N, out, epi, min_share=sh, cfg=None if cf == -2 else cf)
-                arms[name] = arm
+                arms[arm_name] = arm
     if epi == "silu":
         def blas():
             torch.mm(x, wt, out=y16)

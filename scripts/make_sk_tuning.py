@@ -1,5 +1,6 @@
 """Build ops/gemm_sk_tuning.json from a bench_prefill_gemm.py --grid sweep (jsonl): for every (N, K, epilogue, M)
-the fastest tile configuration of the stream-K prefill kernel (ops.SK_CFGS index, + 8 = whole tiles only).
+the fastest tile configuration of the stream-K prefill kernel (ops.SK_CFGS index, + 8 = whole tiles only) and, when the
+sweep compared epilogue modes (arm suffix _e0 / _e1), the faster mode (stored as cfg + 16 + 32 * mode).
 Usage: make_sk_tuning.py gpurun_out/bench_prefill_gemm.jsonl [more.jsonl ...]"""
 import json
 import os
@@ -21,9 +22,12 @@ for path in sys.argv[1:]:
         for k, v in r.items():
             if not (k.startswith("sk_") and isinstance(v, dict)) or "auto" in k or "table" in k:
                 continue
-            tag = k.split("_")[1]
+            parts = k.split("_")
+            tag = parts[1]
             dp = tag.endswith("dp")
             cfg = CFG[tag[:-2] if dp else tag] + (8 if dp else 0)
+            if parts[-1] in ("e0", "e1"):
+                cfg += 16 + 32 * int(parts[-1][1])
             if v["us"] < best_us:
                 best, best_us = cfg, v["us"]
         if best is not None:

@@ -477,23 +477,33 @@ def test_attn_decode_g1_single_buffer_grids(gpu, B):
     assert torch.equal(vc, v1)
 
 
-@pytest.mark.parametrize("kernel", ["16", "32", "32pair"])
-@pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
-@pytest.mark.parametrize("case", ["fresh", "chunked", "long"])
-def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
-    """Both prefill attention kernels (16 x 16 MFMA, 64 rows per workgroup; 32 x 32 MFMA, 128 rows, single
-    or heavy/light paired query blocks per workgroup) vs the fp32 reference: packed variable-length
-    sequences, chunked continuation, multi-block causal tiles."""
+P_KERNELS = ["16", "32", "32pair", "32p", "32ppair"]
+
+
+def _set_prefill_kernel(monkeypatch, kernel):
     monkeypatch.setattr(ops, "PREFILL_ATTN", kernel[:2])
-    monkeypatch.setattr(ops, "PREFILL_PAIR", "1" if kernel == "32pair" else "0")
+    monkeypatch.setattr(ops, "PREFILL_PAIR", "1" if kernel.endswith("pair") else "0")
+    monkeypatch.setattr(ops, "PREFILL_PIPE", 1 if kernel.startswith("32p") else 0)
+
+
+@pytest.mark.parametrize("kernel", P_KERNELS)
+@pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
+@pytest.mark.parametrize("case", ["fresh", "chunked", "long", "longer"])
+def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
+    """The prefill attention kernels (16 x 16 MFMA, 64 rows per workgroup; 32 x 32 MFMA, 128 rows, single
+    or heavy/light paired query blocks per workgroup, one-barrier or pipelined loop) vs the fp32 reference:
+    packed variable-length sequences, chunked continuation, multi-block causal tiles."""
+    _set_prefill_kernel(monkeypatch, kernel)
     H, Hkv = HH
     D = 128
     if case == "fresh":
         qlens, ctx = [1, 70, 130, 64], [1, 70, 130, 64]
     elif case == "chunked":  # chunked prefill: context already holds earlier chunks
         qlens, ctx = [10, 64, 100], [200, 64, 400]
-    else:  # several 128-row query blocks and 64-key tiles per sequence, ragged ends
+    elif case == "long":  # several 128-row query blocks and 64-key tiles per sequence, ragged ends
         qlens, ctx = [300, 257], [300, 400]
+    else:  # one long prompt (many tiles through the 3-deep V ring) next to a short one
+        qlens, ctx = [1100, 40], [1100, 700]
     kc, vc, bt = _paged(ctx, Hkv, D, gpu, seed=H)
     T = sum(qlens)
     q = torch.randn(T, H, D, device=gpu).to(torch.bfloat16)
@@ -507,11 +517,10 @@ def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
     assert _rel(out, out2) < 1e-2
 
 
-@pytest.mark.parametrize("kernel", ["16", "32", "32pair"])
+@pytest.mark.parametrize("kernel", P_KERNELS)
 def test_attn_prefill_spike(gpu, kernel, monkeypatch):
     """Force the online-softmax rescale branch: one very large score late in the sequence."""
-    monkeypatch.setattr(ops, "PREFILL_ATTN", kernel[:2])
-    monkeypatch.setattr(ops, "PREFILL_PAIR", "1" if kernel == "32pair" else "0")
+    _set_prefill_kernel(monkeypatch, kernel)
     H, Hkv, D = 8, 8, 128
     n = 300
     kc, vc, bt = _paged([n], Hkv, D, gpu, seed=9)
