@@ -24,7 +24,8 @@
 // from two calls ago).  The epoch lives on the device, so the launch has fixed arguments and replays
 // inside a captured hipGraph.  Protocol invariants (per block b):
 //   * a peer can be at most one epoch ahead (it needs our flag to finish), so flags are compared
-//     with (int)(flag - ep) >= 0 and payload slots alternate by epoch parity;
+//     with (int)(flag - target) >= 0 and payload slots alternate by epoch parity; the flag targets of epoch ep are
+//     2 ep (one-shot) and 2 ep - 1, 2 ep (two-shot's two phases): one monotonic sequence whatever the mix of calls;
 //   * pushing into parity p at epoch ep is safe: reaching ep means the peer raised ep-1, which it
 //     does only after finishing ep-2 (the previous user of parity p).
 // Every wait is bounded by a wall-clock timeout that sets *err and drains the grid, so a missing
@@ -151,12 +152,14 @@ __global__ __launch_bounds__(AR_THREADS) void ar_oneshot_kernel(float4* __restri
   __syncthreads();
 
   // 2. raise our flag for block b at every peer, then wait for theirs
+  // flag value 2 ep: the same sequence the two-shot kernel's final phase raises, so one-shot and two-shot calls can
+  // alternate on one region (a flag left at 2 ep' by a two-shot call must not satisfy a later one-shot wait early)
   if (tid < W && tid != rank) {
     uint32_t* f = reinterpret_cast<uint32_t*>(regions[tid] + AR_FLAGS_OFF) + b * AR_MAX_WORLD + rank;
-    st_release_sys(f, ep);
+    st_release_sys(f, 2u * ep);
     const uint32_t* mf = reinterpret_cast<const uint32_t*>(mine + AR_FLAGS_OFF) + b * AR_MAX_WORLD + tid;
     const long long t0 = wall_clock64();
-    while ((int)(ld_relaxed_sys(mf) - ep) < 0) {  // relaxed spin, one acquire fence after it
+    while ((int)(ld_relaxed_sys(mf) - 2u * ep) < 0) {  // relaxed spin, one acquire fence after it
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > timeout_ticks) {
         atomicExch(err, 1);

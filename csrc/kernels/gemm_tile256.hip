@@ -62,10 +62,10 @@ __device__ __forceinline__ u32x4_t ds_read16_off(uint32_t a) {
   return v;
 }
 
-// N consecutive fragments (1 KiB apart) of LDS half HALF, starting at fragment 0 of the wave's base address
-template <int HALF, int... Is>
+// N consecutive fragments (1 KiB apart) starting at fragment OFF of the wave's base address
+template <int OFF, int... Is>
 __device__ __forceinline__ void ds_read_frags(u32x4_t* r, uint32_t base, std::integer_sequence<int, Is...>) {
-  ((r[Is] = ds_read16_off<(HALF * 16 + Is) * 1024>(base)), ...);
+  ((r[Is] = ds_read16_off<(OFF + Is) * 1024>(base)), ...);
 }
 
 
@@ -85,7 +85,8 @@ __device__ __forceinline__ int sk_slot(int c, int t, int iters, int P, int T) {
 
 // stream-K plan of a launch (external linkage: the kernel templates take it by value)
 struct SkPlan {
-  int ntm;              // 256-row tiles
+  int ntm;              // row tiles
+  int gm;               // row tiles per raster group (grouped tile order, below)
   int ntiles;           // output tiles (row tile fastest)
   int T;                // K-tiles of 64 per output tile
   int sk_tiles;         // tiles [0, sk_tiles) are stream-K, the rest data-parallel
@@ -131,21 +132,28 @@ struct TileCfg {
   static constexpr int GX = XF / 8, GW0 = WF0 / 8, GW1 = WF1 / 8;  // glds per wave per half-stage
   static constexpr int WAIT = GX + GW1;  // the K-tile-(t+2) loads a wave has in flight after phase 4's stage
   static constexpr int NBT = 4 * WN;     // n-blocks per tile
+  // LDS: one K-tile buffer = the four halves back to back (fragment offsets HOFF), NBUF buffers
+  static constexpr int BUFF = 2 * XF + WF0 + WF1;            // fragments (KiB) per K-tile buffer
+  static constexpr int HOFF[4] = {0, XF, 2 * XF, 2 * XF + WF0};
+  static constexpr bool CAN3 = 3 * BUFF <= 160;              // three buffers fit the 160 KiB LDS
+  static constexpr int WAIT3 = 2 * GX + GW0 + GW1;           // a whole K-tile's loads per wave (3-buffer wait)
 };
 
 // The kernel body is a __device__ function template behind a thin __global__ wrapper: hipcc's host pass does not
 // emit the launch stub of a kernel template whose own body holds generic (integral_constant) lambdas.
-template <int BM, int WN, int EPI>
+template <int BM, int WN, int EPI, int NBUF>
 __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                              const uint4* __restrict__ Wf, int NBtot, void* __restrict__ out, int ldo,
                                              const SkPlan& pl, float* __restrict__ ws, int* __restrict__ tickets,
                                              const RopeEpi& re) {
   using C = TileCfg<BM, WN>;
   constexpr int MI = C::MI, NQ0 = C::NQ0, NQ1 = C::NQ1;
+  constexpr bool BIG = BM * WN >= 1024;  // the 256 x 256 tile: 128 accumulator VGPRs, smaller epilogue load batches
   static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF <= 16 && C::WF0 <= 16, "tile geometry");
   static_assert(EPI != EPI_SILU || WN % 2 == 0, "SiLU pairs (gate, up) n-blocks inside one wave");
   static_assert(EPI != EPI_ROPE || WN % 2 == 0, "RoPE tiles hold whole 128-column heads");
-  __shared__ __attribute__((aligned(16))) uint4 lds[2][4][16][64];
+  static_assert(NBUF == 2 || (NBUF == 3 && C::CAN3), "K-tile buffers");
+  __shared__ __attribute__((aligned(16))) uint4 lds[NBUF * C::BUFF * 64];
   const int lane = threadIdx.x & 63;
   // wave ids through readfirstlane: provably uniform, so every per-wave address term lives in SGPRs
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0..7
@@ -170,7 +178,13 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
 
   // fragment f of a half: X (wr * MI + i) * 2 + ks, W (wc * NQ + j) * 2 + ks; this wave stages f = per * w + e
   auto setup = [&](int tile) {
-    const int tm = tile % pl.ntm, tn = tile / pl.ntm;
+    // grouped raster order: consecutive tile ids walk gm row tiles, then the next column, so the P / 8 consecutive
+    // tiles of one XCD's CUs form a gm x (P / 8 / gm) block and its L2 holds gm X panels + that many W panels
+    // (the plain column-major order gave each XCD every X panel: 3B down at 2048 rows 345 MB of L2 misses vs 281 MB
+    // for hipBLASLt, rocprofv3 TCC_MISS_sum)
+    const int ntn = pl.ntiles / pl.ntm, gsz = pl.gm * ntn, grp = tile / gsz, fm = grp * pl.gm;
+    const int gmr = min(pl.gm, pl.ntm - fm), loc = tile - grp * gsz;
+    const int tm = fm + loc % gmr, tn = loc / gmr;
     mbase = tm * BM;
     nbase = tn * C::NBT;
 #pragma unroll
@@ -204,7 +218,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     for (int e = 0; e < per; ++e) {
       const int f = per * w + e;
       const bool oob = last_odd && (f & 1);
-      void* dst = &lds[B][H][f][0];
+      void* dst = &lds[(B * C::BUFF + C::HOFF[H] + f) * 64];
       if constexpr (H < 2)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, vx[H][e], oob ? xbytes : tc * 128, 0, 0);
       else if constexpr (H == 2)
@@ -218,20 +232,20 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   // X fragments of one M quadrant, W fragments of one N quadrant: [i or j][ks] flattened as i * 2 + ks
   u32x4_t xr[MI * 2], wr[NQ0 * 2];
   // fragment reads: one base VGPR per (operand, buffer), the half / fragment offset as the ds_read immediate
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)&lds[0][0][0][0] + lane * 16;
-  const uint32_t xb[2] = {lds0 + wm * MI * 2 * 1024, lds0 + wm * MI * 2 * 1024 + 65536};
-  const uint32_t wb0[2] = {lds0 + wn * NQ0 * 2 * 1024, lds0 + wn * NQ0 * 2 * 1024 + 65536};
-  const uint32_t wb1[2] = {lds0 + wn * NQ1 * 2 * 1024, lds0 + wn * NQ1 * 2 * 1024 + 65536};
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)&lds[0] + lane * 16;
+  auto xb = [&](int B) { return lds0 + (B * C::BUFF + wm * MI * 2) * 1024; };
+  auto wb0 = [&](int B) { return lds0 + (B * C::BUFF + wn * NQ0 * 2) * 1024; };
+  auto wb1 = [&](int B) { return lds0 + (B * C::BUFF + wn * NQ1 * 2) * 1024; };
   auto read_x = [&](auto Bc, auto QMc) {
     constexpr int B = decltype(Bc)::value, QM = decltype(QMc)::value;
-    ds_read_frags<QM>(xr, xb[B], std::make_integer_sequence<int, MI * 2>{});
+    ds_read_frags<C::HOFF[QM]>(xr, xb(B), std::make_integer_sequence<int, MI * 2>{});
   };
   auto read_w = [&](auto Bc, auto QNc) {
     constexpr int B = decltype(Bc)::value, QN = decltype(QNc)::value;
     if constexpr (QN == 0)
-      ds_read_frags<2>(wr, wb0[B], std::make_integer_sequence<int, NQ0 * 2>{});
+      ds_read_frags<C::HOFF[2]>(wr, wb0(B), std::make_integer_sequence<int, NQ0 * 2>{});
     else
-      ds_read_frags<3>(wr, wb1[B], std::make_integer_sequence<int, NQ1 * 2>{});
+      ds_read_frags<C::HOFF[3]>(wr, wb1(B), std::make_integer_sequence<int, NQ1 * 2>{});
   };
   auto mma = [&](auto QMc, auto QNc) {
     constexpr int QM = decltype(QMc)::value, QN = decltype(QNc)::value;
@@ -291,23 +305,63 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     LSA_PHASE(read_x(B{}, I1{}), stage(I0{}, B{}, (t) + 2), (void)0, I1, I1);                      \
     LSA_PHASE(read_w(B{}, I0{}), stage(I3{}, B{}, (t) + 2), LSA_WAITV(C::WAIT), I1, I0);           \
   } while (0)
-    stage(I0{}, I0{}, 0);
-    stage(I3{}, I0{}, 0);
-    stage(I1{}, I0{}, 0);
-    stage(I2{}, I0{}, 0);
-    stage(I0{}, I1{}, 1);
-    stage(I3{}, I1{}, 1);
-    LSA_WAITV(C::WAIT);
+  // Three buffers (NBUF 3, the tiles whose three K-tile buffers fit the LDS): K-tile t in buffer t % 3, and during
+  // it every half of K-tile t + 2 goes into buffer (t + 2) % 3 (= t - 1's, each half restaged >= 2 phases after its
+  // last read there, as above):
+  //   P1 (0,0): read XQ0 + WQ0   stage XQ0, XQ1 (t+2)
+  //   P2 (0,1): read WQ1         stage WQ0, WQ1 (t+2)
+  //   P3 (1,1): read XQ1
+  //   P4 (1,0): read WQ0         s_waitcnt vmcnt(one K-tile's loads): tile t+1 landed
+  // so every half is issued 7-10 phases ahead of its first read (the two-buffer order gives WQ0 three): the
+  // weight stream's HBM latency hides behind ~2 K-tiles instead of ~0.75 (in-engine, cold-cache prefill GEMMs).
+#define LSA_KTILE3(B, B2, t)                                                                                  \
+  do {                                                                                                        \
+    LSA_PHASE((read_x(B{}, I0{}), read_w(B{}, I0{})), (stage(I0{}, B2{}, (t) + 2), stage(I1{}, B2{}, (t) + 2)), \
+              (void)0, I0, I0);                                                                               \
+    LSA_PHASE(read_w(B{}, I1{}), (stage(I2{}, B2{}, (t) + 2), stage(I3{}, B2{}, (t) + 2)), (void)0, I0, I1);  \
+    LSA_PHASE(read_x(B{}, I1{}), (void)0, (void)0, I1, I1);                                                  \
+    LSA_PHASE(read_w(B{}, I0{}), (void)0, LSA_WAITV(C::WAIT3), I1, I0);                                      \
+  } while (0)
+    if constexpr (NBUF == 3) {
+      stage(I0{}, I0{}, 0);
+      stage(I1{}, I0{}, 0);
+      stage(I2{}, I0{}, 0);
+      stage(I3{}, I0{}, 0);
+      stage(I0{}, I1{}, 1);
+      stage(I1{}, I1{}, 1);
+      stage(I2{}, I1{}, 1);
+      stage(I3{}, I1{}, 1);
+      LSA_WAITV(C::WAIT3);
+    } else {
+      stage(I0{}, I0{}, 0);
+      stage(I3{}, I0{}, 0);
+      stage(I1{}, I0{}, 0);
+      stage(I2{}, I0{}, 0);
+      stage(I0{}, I1{}, 1);
+      stage(I3{}, I1{}, 1);
+      LSA_WAITV(C::WAIT);
+    }
     __builtin_amdgcn_s_barrier();
     // ping-pong: the second M wave group runs one barrier behind, so one group's MFMA section overlaps the other's
     // fragment reads + prefetch issue (the >= 2-phase WAR/RAW slack above covers the offset)
     if (wm == 1) __builtin_amdgcn_s_barrier();
     int t = 0;
-    for (; t + 1 < Tl; t += 2) {
-      LSA_KTILE(I0, I1, t);
-      LSA_KTILE(I1, I0, t + 1);
+    if constexpr (NBUF == 3) {
+      for (; t + 2 < Tl; t += 3) {
+        LSA_KTILE3(I0, I2, t);
+        LSA_KTILE3(I1, I0, t + 1);
+        LSA_KTILE3(I2, I1, t + 2);
+      }
+      if (t < Tl) LSA_KTILE3(I0, I2, t);
+      if (t + 1 < Tl) LSA_KTILE3(I1, I0, t + 1);
+    } else {
+      for (; t + 1 < Tl; t += 2) {
+        LSA_KTILE(I0, I1, t);
+        LSA_KTILE(I1, I0, t + 1);
+      }
+      if (t < Tl) LSA_KTILE(I0, I1, t);
     }
-    if (t < Tl) LSA_KTILE(I0, I1, t);
+#undef LSA_KTILE3
 #undef LSA_KTILE
 #undef LSA_PHASE
 #undef LSA_WAITV
@@ -319,6 +373,37 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   const int g = lane >> 4;
   auto store_tile = [&]() {
     if constexpr (EPI == EPI_ROPE) return;  // the RoPE epilogue always runs through the LDS image
+    if constexpr (EPI == EPI_RES) {
+      // h += acc: the h loads of IB fragment rows x WN leave together before their first store (a load after a store
+      // through the same pointer is not hoisted, which made this a chain of 2 MI WN dependent round trips)
+      constexpr int IB = BIG ? 1 : 2;  // fragment rows per batch of h loads (IB x WN float4 in flight per lane)
+#pragma unroll
+      for (int hf = 0; hf < 2 * MI / IB; ++hf) {
+        float4 hv[IB][WN];
+#pragma unroll
+        for (int ii = 0; ii < IB; ++ii)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) {
+            const int m = mbase + wm * (BM / 2) + (hf * IB + ii) * 16 + (lane & 15);
+            const int nb = nbase + wn * WN + j;
+            if (m < M && nb < NBtot)
+              hv[ii][j] = *reinterpret_cast<const float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + nb * 16 + 4 * g);
+          }
+#pragma unroll
+        for (int ii = 0; ii < IB; ++ii)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) {
+            const int i = hf * IB + ii;
+            const int m = mbase + wm * (BM / 2) + i * 16 + (lane & 15);
+            const int nb = nbase + wn * WN + j;
+            if (m >= M || nb >= NBtot) continue;
+            float4 h = hv[ii][j];
+            h.x += acc[i][j][0]; h.y += acc[i][j][1]; h.z += acc[i][j][2]; h.w += acc[i][j][3];
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + nb * 16 + 4 * g) = h;
+          }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 2 * MI; ++i) {
       const int m = mbase + wm * (BM / 2) + i * 16 + (lane & 15);
@@ -344,11 +429,6 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
             p.x = pack2bf(acc[i][j][0], acc[i][j][1]);
             p.y = pack2bf(acc[i][j][2], acc[i][j][3]);
             *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + o) = p;
-          } else if constexpr (EPI == EPI_RES) {
-            float4* hp = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o);
-            float4 hv = *hp;
-            hv.x += acc[i][j][0]; hv.y += acc[i][j][1]; hv.z += acc[i][j][2]; hv.w += acc[i][j][3];
-            *hp = hv;
           } else {
             *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) =
                 make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
@@ -367,7 +447,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     constexpr int OC = EPI == EPI_SILU ? C::NBT * 8 : C::NBT * 16;  // output columns of the tile
     constexpr int CH = OC / 4;                                      // 16-B f32 chunks per image row
     static_assert(CH % 16 == 0, "swizzle stays inside the row");
-    float* img = reinterpret_cast<float*>(&lds[0][0][0][0]);
+    float* img = reinterpret_cast<float*>(&lds[0]);
     const int ncol_out = EPI == EPI_SILU ? NBtot * 8 : NBtot * 16;
     const int col0 = EPI == EPI_SILU ? nbase * 8 : nbase * 16;
 #pragma unroll
@@ -394,55 +474,101 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
         }
       }
       __syncthreads();
+      // this wave's rows of the pass: r = w + 8 k, k < RPW (one row per wave-instruction, lanes = 16-B column chunks).
+      // Every global load of those rows is issued before the first store: a load after a store through the same
+      // output pointer cannot be hoisted by the compiler, so a row-by-row loop paid one full load latency per row
+      // (16 rows per wave and pass at BM = 256)
+      constexpr int RPW = BM / 16;
+      const bool live_ch = lane < CH && col0 + lane * 4 < ncol_out;
       if constexpr (EPI == EPI_ROPE) {
-        // one row per wave-instruction: the token's position, sequence and cache block are wave-uniform
-        for (int r = w; r < BM / 2; r += 8) {
-          const int m = mbase + pass * (BM / 2) + r;
-          const int ch = lane;
-          if (m >= M || ch >= CH || col0 + ch * 4 >= ncol_out) continue;
-          const int c = col0 + ch * 4, head = c >> 7, d = c & 127;
-          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2));
-          f32x4_t y = v;
-          const int p = re.pos[m];
-          if (head < re.H + re.Hkv) {  // rotate-half with the partner 64 dims away (same tile: whole heads)
-            const int pch = d < 64 ? ch + 16 : ch - 16;
-            const f32x4_t pv = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((pch ^ (r & 15)) << 2));
-            const int d0 = d & 63;
-            const float4 cs = *reinterpret_cast<const float4*>(re.cos_t + (size_t)p * 64 + d0);
-            const float4 sn = *reinterpret_cast<const float4*>(re.sin_t + (size_t)p * 64 + d0);
-            const float sg = d < 64 ? -1.f : 1.f;
-            y[0] = v[0] * cs.x + sg * pv[0] * sn.x;
-            y[1] = v[1] * cs.y + sg * pv[1] * sn.y;
-            y[2] = v[2] * cs.z + sg * pv[2] * sn.z;
-            y[3] = v[3] * cs.w + sg * pv[3] * sn.w;
-          }
-          const uint2 pk = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
-          if (head < re.H) {
-            *reinterpret_cast<uint2*>(re.q_out + ((size_t)m * re.H + head) * 128 + d) = pk;
-          } else {
+        // per-row metadata once per pass, lane k for row k: the token's position and its paged-cache block
+        int my_pos = 0, my_blk = 0;
+        if (lane < RPW) {
+          const int m = mbase + pass * (BM / 2) + w + 8 * lane;
+          if (m < M) {
+            my_pos = re.pos[m];
             const int seq = re.tok_seq ? re.tok_seq[m] : m;
-            const int blk = re.bt[(size_t)seq * re.max_blocks + (p >> 6)];
-            const int hk = head < re.H + re.Hkv ? head - re.H : head - re.H - re.Hkv;
-            uint16_t* cache = head < re.H + re.Hkv ? re.kc : re.vc;
-            *reinterpret_cast<uint2*>(cache + (((size_t)blk * re.Hkv + hk) * 64 + (p & 63)) * 128 + d) = pk;
+            my_blk = re.bt[(size_t)seq * re.max_blocks + (my_pos >> 6)];
+          }
+        }
+        const int ch = lane;
+        const int c = col0 + ch * 4, head = c >> 7, d = c & 127, d0 = d & 63;
+        const bool rot = head < re.H + re.Hkv;  // q and k heads rotate (rotate-half, partner 64 dims away)
+        const int pch = d < 64 ? ch + 16 : ch - 16;
+        const float sg = d < 64 ? -1.f : 1.f;
+        const int hk = head < re.H + re.Hkv ? head - re.H : head - re.H - re.Hkv;
+        uint16_t* cache = head < re.H + re.Hkv ? re.kc : re.vc;
+        constexpr int RG = BIG ? 2 : 4;  // rows whose cos / sin loads leave together
+#pragma unroll 1
+        for (int k0 = 0; k0 < RPW; k0 += RG) {
+          float4 cs[RG], sn[RG];
+          int pk_[RG];
+#pragma unroll
+          for (int u = 0; u < RG; ++u) {
+            pk_[u] = __builtin_amdgcn_readlane(my_pos, k0 + u);
+            cs[u] = *reinterpret_cast<const float4*>(re.cos_t + (size_t)pk_[u] * 64 + d0);
+            sn[u] = *reinterpret_cast<const float4*>(re.sin_t + (size_t)pk_[u] * 64 + d0);
+          }
+#pragma unroll
+          for (int u = 0; u < RG; ++u) {
+            const int r = w + 8 * (k0 + u);
+            const int m = mbase + pass * (BM / 2) + r;
+            if (m >= M || !live_ch) continue;
+            const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2));
+            f32x4_t y = v;
+            if (rot) {
+              const f32x4_t pv = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((pch ^ (r & 15)) << 2));
+              y[0] = v[0] * cs[u].x + sg * pv[0] * sn[u].x;
+              y[1] = v[1] * cs[u].y + sg * pv[1] * sn[u].y;
+              y[2] = v[2] * cs[u].z + sg * pv[2] * sn[u].z;
+              y[3] = v[3] * cs[u].w + sg * pv[3] * sn[u].w;
+            }
+            const uint2 pk = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+            if (head < re.H) {
+              *reinterpret_cast<uint2*>(re.q_out + ((size_t)m * re.H + head) * 128 + d) = pk;
+            } else {
+              const int p = pk_[u], blk = __builtin_amdgcn_readlane(my_blk, k0 + u);
+              *reinterpret_cast<uint2*>(cache + (((size_t)blk * re.Hkv + hk) * 64 + (p & 63)) * 128 + d) = pk;
+            }
           }
         }
         continue;
       }
-      for (int r = w; r < BM / 2; r += 8) {
+      if constexpr (EPI == EPI_RES) {
+        constexpr int RB = BIG ? 2 : 8;  // rows whose h loads leave together
+#pragma unroll 1
+        for (int k0 = 0; k0 < RPW; k0 += RB) {
+        float4 hv[RB];
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+          const int m = mbase + pass * (BM / 2) + w + 8 * (k0 + u);
+          if (m < M && live_ch) hv[u] = *reinterpret_cast<const float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + col0 + lane * 4);
+        }
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+          const int k = k0 + u;
+          const int r = w + 8 * k;
+          const int m = mbase + pass * (BM / 2) + r;
+          if (m >= M || !live_ch) continue;
+          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((lane ^ (r & 15)) << 2));
+          float4 h = hv[u];
+          h.x += v[0]; h.y += v[1]; h.z += v[2]; h.w += v[3];
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + col0 + lane * 4) = h;
+        }
+        }
+        continue;
+      }
+#pragma unroll 4
+      for (int k = 0; k < RPW; ++k) {
+        const int r = w + 8 * k;
         const int m = mbase + pass * (BM / 2) + r;
         const int ch = lane;
-        if (ch < CH && m < M && col0 + ch * 4 < ncol_out) {
+        if (live_ch && m < M) {
           const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2));
           const size_t o = (size_t)m * ldo + col0 + ch * 4;
           if constexpr (EPI == EPI_BF16 || EPI == EPI_SILU) {
             *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + o) =
                 make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
-          } else if constexpr (EPI == EPI_RES) {
-            float4* hp = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o);
-            float4 hv = *hp;
-            hv.x += v[0]; hv.y += v[1]; hv.z += v[2]; hv.w += v[3];
-            *hp = hv;
           } else {
             *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) = make_float4(v[0], v[1], v[2], v[3]);
           }
@@ -457,7 +583,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
 
   // stream-K part: this virtual CU's iterations [s0, s1) of the first sk_tiles tiles
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
-  int* flag = reinterpret_cast<int*>(&lds[0][0][0][0]);
+  int* flag = reinterpret_cast<int*>(&lds[0]);
   const int iters = pl.sk_iters;
   const int s1 = iters > 0 ? sk_start(vc + 1, iters, P) : 0;
   constexpr int WSTRIDE = 2 * MI * WN * 64 * 4;  // floats of one wave's accumulators in a partial slot
@@ -527,13 +653,13 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   }
 }
 
-template <int BM, int WN, int EPI>
+template <int BM, int WN, int EPI, int NBUF>
 __global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                                       const uint4* __restrict__ Wf, int NBtot,
                                                       void* __restrict__ out, int ldo, SkPlan pl,
                                                       float* __restrict__ ws, int* __restrict__ tickets,
                                                       RopeEpi re) {
-  gemm_sk_body<BM, WN, EPI>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets, re);
+  gemm_sk_body<BM, WN, EPI, NBUF>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets, re);
 }
 
 // Plan for a grid of (at most) ncu workgroups over BM x (NBT * 16) tiles: the data-parallel rounds keep whole tiles;
@@ -545,6 +671,18 @@ static SkPlan sk_plan(int M, int KB, int NBtot, int BM, int NBT, int ncu, int mi
   pl.epl = 0;
   pl.ntm = (M + BM - 1) / BM;
   pl.ntiles = pl.ntm * ((NBtot + NBT - 1) / NBT);
+  // raster group: the power-of-two row count a of an XCD's block of tiles (ncu / 8 of them) that minimises the L2
+  // footprint a * BM + (ncu / 8 / a) * BN (an X panel is BM x K, a W panel BN x K)
+  {
+    const int per_xcd = ncu / 8 > 0 ? ncu / 8 : 1, bn = NBT * 16;
+    int best = 1;
+    long long bcost = 1LL << 62;
+    for (int a = 1; a <= per_xcd && a <= pl.ntm; a *= 2) {
+      const long long c = (long long)a * BM + (long long)((per_xcd + a - 1) / a) * bn;
+      if (c < bcost) bcost = c, best = a;
+    }
+    pl.gm = best;
+  }
   pl.T = (KB + 1) / 2;
   const int P = ncu;
   if (!sk) {
@@ -594,6 +732,9 @@ static float sk_cfg_time(const SkCfg& c, int M, int KB, int NBtot, int ncu, bool
 // epilogue mode of the next launches (lsa_gemm_sk_epilogue): 0 direct, 1 through LDS
 static int g_sk_epl = 1;
 extern "C" void lsa_gemm_sk_epilogue(int mode) { g_sk_epl = mode ? 1 : 0; }
+// K-tile buffers (lsa_gemm_sk_nbuf): 3 wherever three fit the LDS (default), 2 = the two-buffer schedule everywhere
+static int g_sk_nbuf = 3;
+extern "C" void lsa_gemm_sk_nbuf(int n) { g_sk_nbuf = n == 2 ? 2 : 3; }
 
 template <int BM, int WN>
 static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
@@ -605,9 +746,18 @@ static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const u
   if (pl.sk_tiles > 2 * ncu || grid > ncu || (long long)pl.sk_tiles * pl.T * (grid + 1) >= (1LL << 31)) return -3;
   if (grid_out) *grid_out = grid;
   switch (epi) {
-#define LSA_SKL(E) \
-  hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, out, ldo, \
-                     pl, ws, tickets, re)
+#define LSA_SKL(E)                                                                                                \
+  do {                                                                                                            \
+    if constexpr (TileCfg<BM, WN>::CAN3) {                                                                        \
+      if (g_sk_nbuf == 3) {                                                                                       \
+        hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 3>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w,   \
+                           NBtot, out, ldo, pl, ws, tickets, re);                                                 \
+        break;                                                                                                    \
+      }                                                                                                           \
+    }                                                                                                             \
+    hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 2>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, \
+                       out, ldo, pl, ws, tickets, re);                                                            \
+  } while (0)
     case EPI_BF16: LSA_SKL(EPI_BF16); break;
     case EPI_F32: LSA_SKL(EPI_F32); break;
     case EPI_RES: LSA_SKL(EPI_RES); break;

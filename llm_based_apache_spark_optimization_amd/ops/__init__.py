@@ -512,13 +512,20 @@ def rope_fusable(w: PackedWeight, kv_fp8: bool) -> bool:
     return not kv_fp8 and res_supported(w) and ROPE_FUSED
 
 
-ROPE_FUSED = os.environ.get("LSA_ROPE_FUSED", "1") != "0"
+# Off by default: measured slower in the engine (scripts/ttft_ab.py, profiles/r5/ttft_ab_mi355x.jsonl: 3B 2k TTFT 14.41
+# vs 14.30 ms, 7B 300-token 11.29 vs 10.96 ms) -- the epilogue needs a whole-head (256-column) tile, which loses to
+# the 192-column tile plus the separate rope_append launch
+ROPE_FUSED = os.environ.get("LSA_ROPE_FUSED", "0") != "0"
 
 
 def res_supported(w: PackedWeight) -> bool:
     """Whether ``linear_res`` takes this weight (everything but W8A8 fp8 prefill, whose fp8 tile kernel writes
     split-K slabs)."""
-    return not (w.kind == "fp8" and FP8_W8A8 and w.K % 128 == 0)
+    return RES_FUSED and not (w.kind == "fp8" and FP8_W8A8 and w.K % 128 == 0)
+
+
+# prefill o / down: residual add in the GEMM epilogue (1) or an f32 GEMM output summed by the next add_rmsnorm (0)
+RES_FUSED = os.environ.get("LSA_RES_FUSED", "1") != "0"
 
 
 def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,

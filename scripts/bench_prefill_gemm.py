@@ -7,7 +7,7 @@ Each shape runs the epilogue the engine uses: qkv bf16, gate_up SiLU(gate) * up 
 pass), o / down accumulated into the f32 residual (vendor: addmm beta = 1 into f32).  Random operands (zero-filled
 data reads high), every arm checked against an fp32 product first, arms interleaved over rounds in one process
 (cdna_hip_programming.md §5.4 rule 24), median of the rounds.  Usage: bench_prefill_gemm.py [shape,shape,...]
-[--shares 4,8,16]."""
+[--shares 4,8,16] [--cold]."""
 import argparse
 import json
 import sys
@@ -20,7 +20,21 @@ from llm_based_apache_spark_optimization_amd import ops  # noqa: E402
 dev = torch.device("cuda:0")
 
 
+_flush = None
+
+
 def timeit(fn, it=20):
+    if args.cold:  # every call from cold caches: a 512 MiB write (> the 256 MiB Infinity Cache) before each, timed alone
+        ts = []
+        for _ in range(it // 2):
+            _flush.fill_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1000)
+        return sorted(ts)[len(ts) // 2]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(it):
@@ -54,14 +68,20 @@ ap.add_argument("--cfgs", default="-2", help="tile configurations (ops.SK_CFGS i
                 "kernel's cost model, -2 the measured table the engine uses)")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--epls", default="1", help="epilogue modes to compare (0 direct, 1 through LDS)")
+ap.add_argument("--nbufs", default="3", help="K-tile buffer counts to compare (3: three where they fit, 2: two)")
 ap.add_argument("--grid", action="store_true")
 ap.add_argument("--no-vendor", action="store_true")
+ap.add_argument("--cold", action="store_true", help="time each call alone after a 512 MiB cache-flushing write (the "
+                "engine's case: a layer's weights come from HBM, not from the Infinity Cache of the previous call)")
 args = ap.parse_args()
+if args.cold:
+    _flush = torch.empty(128 << 20, device=dev)
 src = GRID if args.grid else SHAPES
 shapes = {k: v for k, v in src.items() if not args.shapes or k in args.shapes.split(",")}
 shares = [int(s) for s in args.shares.split(",")]
 cfgs = [int(c) for c in args.cfgs.split(",")]
 epls = [int(c) for c in args.epls.split(",")]
+nbufs = [int(c) for c in args.nbufs.split(",")]
 e = ops.ext()
 for name, (M, N, K, epi) in shapes.items():
     torch.manual_seed(0)
@@ -87,14 +107,17 @@ for name, (M, N, K, epi) in shapes.items():
             continue  # SiLU pairs need an even n-block count per wave
         for sh in shares:
             for ep in epls:
-                tag = ("table" if cf == -2 else "auto") if cf < 0 else ("%dx%d" % ops.SK_CFGS[cf & 7]) + (
-                    "dp" if cf >= 8 else "")
-                arm_name = f"sk_{tag}_s{sh}" + ("" if len(epls) == 1 else f"_e{ep}")
+                for nbf in nbufs:
+                    tag = ("table" if cf == -2 else "auto") if cf < 0 else ("%dx%d" % ops.SK_CFGS[cf & 7]) + (
+                        "dp" if cf >= 8 else "")
+                    arm_name = (f"sk_{tag}_s{sh}" + ("" if len(nbufs) == 1 else f"_b{nbf}") +
+                                ("" if len(epls) == 1 else f"_e{ep}"))
 
-                def arm(sh=sh, cf=cf, ep=ep):
-                    e.gemm_sk_epilogue(ep)
-                    ops.gemm_sk(x, pw.data, N, out, epi, min_share=sh, cfg=None if cf == -2 else cf)
-                arms[arm_name] = arm
+                    def arm(sh=sh, cf=cf, ep=ep, nbf=nbf):
+                        e.gemm_sk_epilogue(ep)
+                        e.gemm_sk_nbuf(nbf)
+                        ops.gemm_sk(x, pw.data, N, out, epi, min_share=sh, cfg=None if cf == -2 else cf)
+                    arms[arm_name] = arm
     if epi == "silu":
         def blas():
             torch.mm(x, wt, out=y16)

@@ -51,9 +51,11 @@ if idle:
         by[k] = (c + 1, s + g)
     for (a, b), (c, s) in sorted(by.items(), key=lambda kv: -kv[1][1])[:12]:
         print(f"  {c:4d} x {s / c:9.1f} us  after {a}  before {b}")
-# prefill segments: from the first prefill kernel (tile GEMM, vendor GEMM, prefill attention, rope/append) to the
-# commit kernel that ends the prefill; kernel-busy = every kernel in that window; per-kernel totals of the median one
-PRE = ("gemm_sk", "t256", "prefill", "rope_append", "Cijk")
+# prefill segments: from the first engine prefill kernel (stream-K GEMM, prefill attention, rope/append) to the commit
+# kernel that ends the prefill; kernel-busy = every kernel in that window; per-kernel totals of the median one.  Vendor
+# GEMMs (Cijk_*) inside a segment are counted and reported; outside them (the bench's fp32 numerics oracle) they are not
+# engine work.  ("gemm_sk_kernel", not "gemm_sk": the decode GEMV is gemm_skinny_kernel.)
+PRE = ("gemm_sk_kernel", "attn_prefill", "rope_append")
 seg, segs = [], []
 for r in rows:
     if seg or any(p in r[2] for p in PRE):
@@ -75,3 +77,5 @@ if segs:
         by[k] = (c + 1, t + (e - s) / 1e3)
     for k, (c, t) in sorted(by.items(), key=lambda kv: -kv[1][1])[:14]:
         print(f"  {t:8.1f} us  {c:4d} x {t / c:7.1f}  {k}")
+    vendor = sum(1 for sg in segs for r in sg if "Cijk" in r[2])
+    print(f"vendor (Cijk_*) kernels inside the {len(segs)} prefill segments: {vendor}")

@@ -170,16 +170,22 @@ def test_gemm_stream_k(gpu, M, NK, epi):
     _sk_case(gpu, M, N, K, epi, ops.SK_MIN_SHARE)
 
 
+@pytest.mark.parametrize("nbuf", [3, 2])
 @pytest.mark.parametrize("cfg", list(range(6)) + [8, 11, 13])
-@pytest.mark.parametrize("MNK", [(300, 3072, 1376), (2048, 5120, 1024), (1100, 800, 512)])
+@pytest.mark.parametrize("MNK", [(300, 3072, 1376), (2048, 5120, 1024), (1100, 800, 512), (640, 1536, 2048)])
 @pytest.mark.parametrize("epi", ["bf16", "silu", "res"])
-def test_gemm_stream_k_tile_shapes(gpu, cfg, MNK, epi):
+def test_gemm_stream_k_tile_shapes(gpu, cfg, MNK, epi, nbuf):
     """Every tile configuration (BM 128 / 256 x BN 128 / 192 / 256; + 8: whole tiles only) on shapes whose edges cut
-    every tile kind."""
+    every tile kind, with the three-buffer K-tile pipeline (where it fits) and the two-buffer one; K-tile counts 22,
+    16, 8 and 32 exercise every tail of the three-way unrolled loop."""
     M, N, K = MNK
     if epi == "silu" and ops.SK_CFGS[cfg & 7][1] % 128:
         pytest.skip("SiLU needs an even n-block count per wave")
-    _sk_case(gpu, M, N, K, epi, 4, cfg=cfg)
+    ops.ext().gemm_sk_nbuf(nbuf)
+    try:
+        _sk_case(gpu, M, N, K, epi, 4, cfg=cfg)
+    finally:
+        ops.ext().gemm_sk_nbuf(3)
 
 
 @pytest.mark.parametrize("share", [1, 2, 5])
