@@ -804,7 +804,7 @@ class ModelRunner:
     def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T):
         kc, vc = self.kv[l, 0], self.kv[l, 1]
         kvs = self._kv_scales(l)
-        if self.on_gpu and ops.rope_fusable(lw.wqkv, self.kv_fp8) and bt.shape[1] > 0:
+        if self.on_gpu and ops.rope_fusable(lw.wqkv, self.kv_fp8, T) and bt.shape[1] > 0:
             # RoPE + the KV-cache append in the qkv GEMM's epilogue: no qkv round trip, no rope_append launch
             ops.linear_rope(xn, lw.wqkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
             ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),

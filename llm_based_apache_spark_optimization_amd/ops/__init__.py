@@ -505,17 +505,19 @@ def linear_rope(x: torch.Tensor, w: PackedWeight, pos, tok_seq, block_tables, co
                        block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
 
 
-def rope_fusable(w: PackedWeight, kv_fp8: bool) -> bool:
-    """Whether the prefill qkv projection can take the fused RoPE / cache-append epilogue (``linear_rope``): bf16
-    cache, and weights the stream-K kernel reads (bf16, or quantised ones through their bf16 dequantisation; the
-    W8A8 fp8 prefill keeps its split-K path)."""
-    return not kv_fp8 and res_supported(w) and ROPE_FUSED
+def rope_fusable(w: PackedWeight, kv_fp8: bool, M: int = 1 << 30) -> bool:
+    """Whether the prefill qkv projection of M rows takes the fused RoPE / cache-append epilogue (``linear_rope``):
+    bf16 cache, weights the stream-K kernel reads (bf16, or quantised ones through their bf16 dequantisation; the
+    W8A8 fp8 prefill keeps its split-K path), and at least ROPE_FUSED_MIN_M rows."""
+    return not kv_fp8 and res_supported(w) and ROPE_FUSED and M >= ROPE_FUSED_MIN_M
 
 
-# Off by default: measured slower in the engine (scripts/ttft_ab.py, profiles/r5/ttft_ab_mi355x.jsonl: 3B 2k TTFT 14.41
-# vs 14.30 ms, 7B 300-token 11.29 vs 10.96 ms) -- the epilogue needs a whole-head (256-column) tile, which loses to
-# the 192-column tile plus the separate rope_append launch
-ROPE_FUSED = os.environ.get("LSA_ROPE_FUSED", "0") != "0"
+# The fused epilogue needs a whole-head (256-column) tile.  In the engine (rocprofv3 / scripts/ttft_ab.py,
+# profiles/r5/ttft_ab_mi355x.jsonl, profiles/r5/rocprof_b32_gaps.txt) it wins where the qkv round trip it removes is
+# large -- the 7B b32 bench prefill, 4096 rows: 361 us fused vs 320 + 65 (rope_append) -- and loses below, where the
+# 192-column tile plus the separate launch is faster (3B 2k TTFT 14.41 vs 14.30 ms, 7B 300-token 11.29 vs 10.96 ms)
+ROPE_FUSED = os.environ.get("LSA_ROPE_FUSED", "1") != "0"
+ROPE_FUSED_MIN_M = int(os.environ.get("LSA_ROPE_FUSED_MIN_M", "4096"))
 
 
 def res_supported(w: PackedWeight) -> bool:

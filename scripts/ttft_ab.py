@@ -23,7 +23,7 @@ arms = {"rope1_res1": (True, True), "rope0_res1": (False, True), "rope1_res0": (
 times = {a: [] for a in arms}
 for rnd in range(6):
     for a, (rope, res) in arms.items():
-        ops.ROPE_FUSED, ops.RES_FUSED = rope, res
+        ops.ROPE_FUSED, ops.RES_FUSED, ops.ROPE_FUSED_MIN_M = rope, res, 0
         t = time.perf_counter()
         eng.generate([prompt], sp)
         dt = time.perf_counter() - t
