@@ -121,14 +121,15 @@ struct RopeEpi {
 //   half 1 = XQ1: the other BM / 4 rows                       (read in phase 3)
 //   half 2 = WQ0: every wave's first NQ0 n-blocks            (read in phases 1 and 4)
 //   half 3 = WQ1: every wave's last NQ1 n-blocks             (read in phase 2)
-// fragment (1 KiB, one 16 x 32 MFMA operand) within an X half: (wr * MI + i) * 2 + ks; within a W half
-// (wc * NQ + j) * 2 + ks.  Each wave moves (half fragments) / 8 of them per half-stage, one global_load_lds each.
-template <int BM, int WN>
+// fragment (1 KiB, one 16 x 32 MFMA operand) within an X half: (wr * MI + i) * KS + ks; within a W half
+// (wc * NQ + j) * KS + ks.  Each wave moves (half fragments) / 8 of them per half-stage, one global_load_lds each.
+// KS = k-steps of 32 per K-tile (2: BK = 64; the kernel body also takes 4, BK = 128 -- measured no faster, see kSkCfgs).
+template <int BM, int WN, int KS = 2>
 struct TileCfg {
   static constexpr int MI = BM / 64;                      // 16-row fragments per M quadrant of a wave
   static constexpr int NQ0 = (WN + 1) / 2, NQ1 = WN / 2;  // n-blocks per N quadrant of a wave
-  static constexpr int XF = 4 * MI;                       // fragments per X half
-  static constexpr int WF0 = 8 * NQ0, WF1 = 8 * NQ1;      // fragments per W half
+  static constexpr int XF = 2 * MI * KS;                  // fragments per X half
+  static constexpr int WF0 = 4 * NQ0 * KS, WF1 = 4 * NQ1 * KS;  // fragments per W half
   static constexpr int GX = XF / 8, GW0 = WF0 / 8, GW1 = WF1 / 8;  // glds per wave per half-stage
   static constexpr int WAIT = GX + GW1;  // the K-tile-(t+2) loads a wave has in flight after phase 4's stage
   static constexpr int NBT = 4 * WN;     // n-blocks per tile
@@ -141,15 +142,15 @@ struct TileCfg {
 
 // The kernel body is a __device__ function template behind a thin __global__ wrapper: hipcc's host pass does not
 // emit the launch stub of a kernel template whose own body holds generic (integral_constant) lambdas.
-template <int BM, int WN, int EPI, int NBUF>
+template <int BM, int WN, int EPI, int NBUF, int KS>
 __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                              const uint4* __restrict__ Wf, int NBtot, void* __restrict__ out, int ldo,
                                              const SkPlan& pl, float* __restrict__ ws, int* __restrict__ tickets,
                                              const RopeEpi& re) {
-  using C = TileCfg<BM, WN>;
+  using C = TileCfg<BM, WN, KS>;
   constexpr int MI = C::MI, NQ0 = C::NQ0, NQ1 = C::NQ1;
   constexpr bool BIG = BM * WN >= 1024;  // the 256 x 256 tile: 128 accumulator VGPRs, smaller epilogue load batches
-  static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF <= 16 && C::WF0 <= 16, "tile geometry");
+  static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF <= 32 && C::WF0 <= 32 && NBUF * C::BUFF <= 160, "tile geometry");
   static_assert(EPI != EPI_SILU || WN % 2 == 0, "SiLU pairs (gate, up) n-blocks inside one wave");
   static_assert(EPI != EPI_ROPE || WN % 2 == 0, "RoPE tiles hold whole 128-column heads");
   static_assert(NBUF == 2 || (NBUF == 3 && C::CAN3), "K-tile buffers");
@@ -162,7 +163,6 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   const int q8 = P >> 3, r8 = P & 7;
   const int vc = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int T = pl.T;
-  const bool odd_tail = KB & 1;  // the last K-tile has one k-step (its second fragments re-read the first)
   const int r16 = lane & 15, c16 = 8 * (lane >> 4);
 
   // operand staging by buffer_load ... lds: the per-lane byte offset of each staged fragment is fixed for a segment
@@ -176,7 +176,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   int kt0 = 0, Tl = 1;  // the segment's K-tiles [kt0, kt0 + Tl)
   int mbase = 0, nbase = 0;
 
-  // fragment f of a half: X (wr * MI + i) * 2 + ks, W (wc * NQ + j) * 2 + ks; this wave stages f = per * w + e
+  // fragment f of a half: X (wr * MI + i) * KS + ks, W (wc * NQ + j) * KS + ks; this wave stages f = per * w + e
   auto setup = [&](int tile) {
     // grouped raster order: consecutive tile ids walk gm row tiles, then the next column, so the P / 8 consecutive
     // tiles of one XCD's CUs form a gm x (P / 8 / gm) block and its L2 holds gm X panels + that many W panels
@@ -191,19 +191,19 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int e = 0; e < C::GX; ++e) {
-        const int f = C::GX * w + e, wi = f >> 1, ks = f & 1, wr_ = wi / MI, i = wi % MI;
+        const int f = C::GX * w + e, wi = f / KS, ks = f % KS, wr_ = wi / MI, i = wi % MI;
         const int row = min(mbase + wr_ * (BM / 2) + h * (BM / 4) + i * 16 + r16, M - 1);
         vx[h][e] = (row * ldx + c16) * 2 + ks * 64;
       }
 #pragma unroll
     for (int e = 0; e < C::GW0; ++e) {
-      const int f = C::GW0 * w + e, wj = f >> 1, ks = f & 1, wc = wj / NQ0, j = wj % NQ0;
+      const int f = C::GW0 * w + e, wj = f / KS, ks = f % KS, wc = wj / NQ0, j = wj % NQ0;
       const int nb = min(nbase + wc * WN + j, NBtot - 1);
       vw0[e] = (nb * KB + ks) * 1024 + lane * 16;
     }
 #pragma unroll
     for (int e = 0; e < C::GW1; ++e) {
-      const int f = C::GW1 * w + e, wj = f >> 1, ks = f & 1, wc = wj / NQ1, j = wj % NQ1;
+      const int f = C::GW1 * w + e, wj = f / KS, ks = f % KS, wc = wj / NQ1, j = wj % NQ1;
       const int nb = min(nbase + wc * WN + NQ0 + j, NBtot - 1);
       vw1[e] = (nb * KB + ks) * 1024 + lane * 16;
     }
@@ -212,53 +212,60 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   auto stage = [&](auto Hc, auto Bc, int t) {
     constexpr int H = decltype(Hc)::value, B = decltype(Bc)::value;
     const int tc = kt0 + min(t, Tl - 1);
-    const bool last_odd = odd_tail && tc == T - 1;  // its second k-step does not exist: stage zeros
     constexpr int per = H < 2 ? C::GX : (H == 2 ? C::GW0 : C::GW1);
 #pragma unroll
     for (int e = 0; e < per; ++e) {
       const int f = per * w + e;
-      const bool oob = last_odd && (f & 1);
+      const bool oob = tc * KS + f % KS >= KB;  // a k-step past K (the last K-tile's tail): staged as zeros
       void* dst = &lds[(B * C::BUFF + C::HOFF[H] + f) * 64];
       if constexpr (H < 2)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, vx[H][e], oob ? xbytes : tc * 128, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, vx[H][e], oob ? xbytes : tc * (KS * 64), 0, 0);
       else if constexpr (H == 2)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)dst, 16, vw0[e], oob ? wbytes : tc * 2048, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)dst, 16, vw0[e], oob ? wbytes : tc * (KS * 1024), 0, 0);
       else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)dst, 16, vw1[e], oob ? wbytes : tc * 2048, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)dst, 16, vw1[e], oob ? wbytes : tc * (KS * 1024), 0, 0);
     }
   };
 
   f32x4_t acc[2 * MI][WN];
-  // X fragments of one M quadrant, W fragments of one N quadrant: [i or j][ks] flattened as i * 2 + ks
-  u32x4_t xr[MI * 2], wr[NQ0 * 2];
+  // X fragments of one M quadrant, W fragments of one N quadrant: [i or j][ks] flattened as i * KS + ks
+  u32x4_t xr[MI * KS], wr[NQ0 * KS];
   // fragment reads: one base VGPR per (operand, buffer), the half / fragment offset as the ds_read immediate
   const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)&lds[0] + lane * 16;
-  auto xb = [&](int B) { return lds0 + (B * C::BUFF + wm * MI * 2) * 1024; };
-  auto wb0 = [&](int B) { return lds0 + (B * C::BUFF + wn * NQ0 * 2) * 1024; };
-  auto wb1 = [&](int B) { return lds0 + (B * C::BUFF + wn * NQ1 * 2) * 1024; };
+  auto xb = [&](int B) { return lds0 + (B * C::BUFF + wm * MI * KS) * 1024; };
+  auto wb0 = [&](int B) { return lds0 + (B * C::BUFF + wn * NQ0 * KS) * 1024; };
+  auto wb1 = [&](int B) { return lds0 + (B * C::BUFF + wn * NQ1 * KS) * 1024; };
+  // the half's offset rides in the ds_read immediate while it fits the 16-bit field, else in the base VGPR
+  auto rd = [&](auto Hc, u32x4_t* r, uint32_t base, auto Nc) {
+    constexpr int H = decltype(Hc)::value, N = decltype(Nc)::value;
+    if constexpr ((C::HOFF[H] + N) * 1024 <= 65536)
+      ds_read_frags<C::HOFF[H]>(r, base, std::make_integer_sequence<int, N>{});
+    else
+      ds_read_frags<0>(r, base + C::HOFF[H] * 1024, std::make_integer_sequence<int, N>{});
+  };
   auto read_x = [&](auto Bc, auto QMc) {
     constexpr int B = decltype(Bc)::value, QM = decltype(QMc)::value;
-    ds_read_frags<C::HOFF[QM]>(xr, xb(B), std::make_integer_sequence<int, MI * 2>{});
+    rd(std::integral_constant<int, QM>{}, xr, xb(B), std::integral_constant<int, MI * KS>{});
   };
   auto read_w = [&](auto Bc, auto QNc) {
     constexpr int B = decltype(Bc)::value, QN = decltype(QNc)::value;
     if constexpr (QN == 0)
-      ds_read_frags<C::HOFF[2]>(wr, wb0(B), std::make_integer_sequence<int, NQ0 * 2>{});
+      rd(std::integral_constant<int, 2>{}, wr, wb0(B), std::integral_constant<int, NQ0 * KS>{});
     else
-      ds_read_frags<C::HOFF[3]>(wr, wb1(B), std::make_integer_sequence<int, NQ1 * 2>{});
+      rd(std::integral_constant<int, 3>{}, wr, wb1(B), std::integral_constant<int, NQ1 * KS>{});
   };
   auto mma = [&](auto QMc, auto QNc) {
     constexpr int QM = decltype(QMc)::value, QN = decltype(QNc)::value;
     constexpr int nq = QN ? NQ1 : NQ0;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < nq; ++j)
           acc[QM * MI + i][QN * NQ0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8_t, wr[j * 2 + ks]), __builtin_bit_cast(bf16x8_t, xr[i * 2 + ks]),
+              __builtin_bit_cast(bf16x8_t, wr[j * KS + ks]), __builtin_bit_cast(bf16x8_t, xr[i * KS + ks]),
               acc[QM * MI + i][QN * NQ0 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
@@ -653,20 +660,20 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   }
 }
 
-template <int BM, int WN, int EPI, int NBUF>
+template <int BM, int WN, int EPI, int NBUF, int KS>
 __global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                                       const uint4* __restrict__ Wf, int NBtot,
                                                       void* __restrict__ out, int ldo, SkPlan pl,
                                                       float* __restrict__ ws, int* __restrict__ tickets,
                                                       RopeEpi re) {
-  gemm_sk_body<BM, WN, EPI, NBUF>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets, re);
+  gemm_sk_body<BM, WN, EPI, NBUF, KS>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets, re);
 }
 
 // Plan for a grid of (at most) ncu workgroups over BM x (NBT * 16) tiles: the data-parallel rounds keep whole tiles;
 // the remainder round plus one full round (or every tile, when there are fewer tiles than CUs) is split by K-tile
 // ranges.  min_share: the fewest K-tiles a workgroup's stream-K range may hold (a shorter range gives up parallelism
 // for fewer partial tiles: the grid shrinks instead).  sk = false: whole tiles only (ceil(tiles / ncu) rounds).
-static SkPlan sk_plan(int M, int KB, int NBtot, int BM, int NBT, int ncu, int min_share, bool sk, int* grid) {
+static SkPlan sk_plan(int M, int KB, int NBtot, int BM, int NBT, int KS, int ncu, int min_share, bool sk, int* grid) {
   SkPlan pl;
   pl.epl = 0;
   pl.ntm = (M + BM - 1) / BM;
@@ -683,7 +690,7 @@ static SkPlan sk_plan(int M, int KB, int NBtot, int BM, int NBT, int ncu, int mi
     }
     pl.gm = best;
   }
-  pl.T = (KB + 1) / 2;
+  pl.T = (KB + KS - 1) / KS;
   const int P = ncu;
   if (!sk) {
     pl.sk_tiles = 0;
@@ -708,12 +715,14 @@ static SkPlan sk_plan(int M, int KB, int NBtot, int BM, int NBT, int ncu, int mi
 // Tile configurations (BM, WN) and their cost per output element per K-tile relative to the 256 x 256 tile (the
 // narrower tiles stage more operand bytes per MFMA and run shorter phases); a partial-tile seam (a 64-256 KiB f32
 // partial written and read back by one CU) is priced in 256 x 256 K-tiles.  Measured: scripts/bench_prefill_gemm.py.
+// ks: k-steps of 32 per K-tile.  BK = 128 (ks 4) for the 128-row tiles was built and measured no faster (cold caches,
+// profiles/r5/prefill_gemm_bk128_ab_cold_mi355x.jsonl: ties or loses by 1-3 %), so every configuration runs BK = 64.
 struct SkCfg {
-  int bm, wn;
+  int bm, wn, ks;
   float cost;
 };
-static const SkCfg kSkCfgs[] = {{256, 4, 1.00f}, {256, 3, 1.06f}, {256, 2, 1.18f},
-                                {128, 4, 1.18f}, {128, 3, 1.28f}, {128, 2, 1.45f}};
+static const SkCfg kSkCfgs[] = {{256, 4, 2, 1.00f}, {256, 3, 2, 1.06f}, {256, 2, 2, 1.18f},
+                                {128, 4, 2, 1.18f}, {128, 3, 2, 1.28f}, {128, 2, 2, 1.45f}};
 #define LSA_SK_SEAM_KTILES 8.0f
 
 // predicted time (256 x 256 K-tiles) of config c on the shape; *use_sk: whether the stream-K remainder beats whole
@@ -721,7 +730,7 @@ static const SkCfg kSkCfgs[] = {{256, 4, 1.00f}, {256, 3, 1.06f}, {256, 2, 1.18f
 static float sk_cfg_time(const SkCfg& c, int M, int KB, int NBtot, int ncu, bool* use_sk) {
   const int nbt = 4 * c.wn;
   const long long tiles = (long long)((M + c.bm - 1) / c.bm) * ((NBtot + nbt - 1) / nbt);
-  const float T = (float)((KB + 1) / 2);
+  const float T = (float)((KB + c.ks - 1) / c.ks) * (float)c.ks / 2.0f;  // in 64-deep K-tiles
   const float per_tile = T * c.cost * (float)(c.bm * nbt) / 4096.0f;
   const float dp = (float)((tiles + ncu - 1) / ncu) * per_tile;
   const float skt = (float)tiles / ncu * per_tile + LSA_SK_SEAM_KTILES * (c.bm * nbt) / 4096.0f;
@@ -736,27 +745,27 @@ extern "C" void lsa_gemm_sk_epilogue(int mode) { g_sk_epl = mode ? 1 : 0; }
 static int g_sk_nbuf = 3;
 extern "C" void lsa_gemm_sk_nbuf(int n) { g_sk_nbuf = n == 2 ? 2 : 3; }
 
-template <int BM, int WN>
+template <int BM, int WN, int KS = 2>
 static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
                      float* ws, int* tickets, int ncu, int min_share, bool sk, int epl, int* grid_out,
                      const RopeEpi& re, hipStream_t stream) {
   int grid = 0;
-  SkPlan pl = sk_plan(M, KB, NBtot, BM, 4 * WN, ncu, min_share, sk, &grid);
+  SkPlan pl = sk_plan(M, KB, NBtot, BM, 4 * WN, KS, ncu, min_share, sk, &grid);
   pl.epl = epl;
   if (pl.sk_tiles > 2 * ncu || grid > ncu || (long long)pl.sk_tiles * pl.T * (grid + 1) >= (1LL << 31)) return -3;
   if (grid_out) *grid_out = grid;
   switch (epi) {
 #define LSA_SKL(E)                                                                                                \
   do {                                                                                                            \
-    if constexpr (TileCfg<BM, WN>::CAN3) {                                                                        \
+    if constexpr (TileCfg<BM, WN, KS>::CAN3) {                                                                    \
       if (g_sk_nbuf == 3) {                                                                                       \
-        hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 3>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w,   \
+        hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 3, KS>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w, \
                            NBtot, out, ldo, pl, ws, tickets, re);                                                 \
         break;                                                                                                    \
       }                                                                                                           \
     }                                                                                                             \
-    hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 2>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w, NBtot, \
-                       out, ldo, pl, ws, tickets, re);                                                            \
+    hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 2, KS>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w,    \
+                       NBtot, out, ldo, pl, ws, tickets, re);                                                     \
   } while (0)
     case EPI_BF16: LSA_SKL(EPI_BF16); break;
     case EPI_F32: LSA_SKL(EPI_F32); break;

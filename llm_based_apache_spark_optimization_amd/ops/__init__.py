@@ -442,8 +442,14 @@ def _sk_workspace(device) -> tuple:
     return got
 
 
-# tile configurations of the stream-K kernel (index = the kernel's kSkCfgs; + 8 = whole tiles only): (BM, BN)
-SK_CFGS = ((256, 256), (256, 192), (256, 128), (128, 256), (128, 192), (128, 128))
+# (BM, BN, BK) of the stream-K tile configurations (gemm_tile256.hip kSkCfgs, same order)
+SK_CFGS = ((256, 256, 64), (256, 192, 64), (256, 128, 64), (128, 256, 64), (128, 192, 64), (128, 128, 64))
+
+
+def sk_cfg_tag(cfg: int) -> str:
+    """Name of a stream-K configuration code (bench arms, the tuning table): e.g. 128x192, 128x192k128dp."""
+    bm, bn, bk = SK_CFGS[cfg & 7]
+    return f"{bm}x{bn}" + ("k128" if bk == 128 else "") + ("dp" if cfg & 8 else "")
 
 
 _SK_TUNING_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_sk_tuning.json")

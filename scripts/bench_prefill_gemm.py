@@ -108,8 +108,7 @@ for name, (M, N, K, epi) in shapes.items():
         for sh in shares:
             for ep in epls:
                 for nbf in nbufs:
-                    tag = ("table" if cf == -2 else "auto") if cf < 0 else ("%dx%d" % ops.SK_CFGS[cf & 7]) + (
-                        "dp" if cf >= 8 else "")
+                    tag = ("table" if cf == -2 else "auto") if cf < 0 else ops.sk_cfg_tag(cf)
                     arm_name = (f"sk_{tag}_s{sh}" + ("" if len(nbufs) == 1 else f"_b{nbf}") +
                                 ("" if len(epls) == 1 else f"_e{ep}"))
 
