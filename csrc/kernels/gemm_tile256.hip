@@ -124,33 +124,39 @@ struct RopeEpi {
 // fragment (1 KiB, one 16 x 32 MFMA operand) within an X half: (wr * MI + i) * KS + ks; within a W half
 // (wc * NQ + j) * KS + ks.  Each wave moves (half fragments) / 8 of them per half-stage, one global_load_lds each.
 // KS = k-steps of 32 per K-tile (2: BK = 64; the kernel body also takes 4, BK = 128 -- measured no faster, see kSkCfgs).
-template <int BM, int WN, int KS = 2>
+// NW = waves per workgroup: 8 (2 M x 4 N, one workgroup per CU) or 4 (2 M x 2 N with twice the columns per wave, two
+// workgroups per CU: 30 % fewer LDS fragment bytes per MFMA for the 128-row tiles, whose 64 x 48 per-wave tiles are
+// bound by the LDS reads, profiles/r5/prefill_gemm_bk128_ab_cold_mi355x.jsonl).
+template <int BM, int WN, int KS = 2, int NW = 8>
 struct TileCfg {
+  static constexpr int WGN = NW / 2;                      // wave columns
   static constexpr int MI = BM / 64;                      // 16-row fragments per M quadrant of a wave
   static constexpr int NQ0 = (WN + 1) / 2, NQ1 = WN / 2;  // n-blocks per N quadrant of a wave
   static constexpr int XF = 2 * MI * KS;                  // fragments per X half
-  static constexpr int WF0 = 4 * NQ0 * KS, WF1 = 4 * NQ1 * KS;  // fragments per W half
-  static constexpr int GX = XF / 8, GW0 = WF0 / 8, GW1 = WF1 / 8;  // glds per wave per half-stage
+  static constexpr int WF0 = WGN * NQ0 * KS, WF1 = WGN * NQ1 * KS;  // fragments per W half
+  static constexpr int GX = XF / NW, GW0 = WF0 / NW, GW1 = WF1 / NW;  // glds per wave per half-stage
   static constexpr int WAIT = GX + GW1;  // the K-tile-(t+2) loads a wave has in flight after phase 4's stage
-  static constexpr int NBT = 4 * WN;     // n-blocks per tile
+  static constexpr int NBT = WGN * WN;   // n-blocks per tile
   // LDS: one K-tile buffer = the four halves back to back (fragment offsets HOFF), NBUF buffers
   static constexpr int BUFF = 2 * XF + WF0 + WF1;            // fragments (KiB) per K-tile buffer
   static constexpr int HOFF[4] = {0, XF, 2 * XF, 2 * XF + WF0};
-  static constexpr bool CAN3 = 3 * BUFF <= 160;              // three buffers fit the 160 KiB LDS
+  static constexpr bool CAN3 = 3 * BUFF * (NW == 4 ? 2 : 1) <= 160;  // three buffers fit (per CU: 1 or 2 workgroups)
   static constexpr int WAIT3 = 2 * GX + GW0 + GW1;           // a whole K-tile's loads per wave (3-buffer wait)
 };
 
 // The kernel body is a __device__ function template behind a thin __global__ wrapper: hipcc's host pass does not
 // emit the launch stub of a kernel template whose own body holds generic (integral_constant) lambdas.
-template <int BM, int WN, int EPI, int NBUF, int KS>
+template <int BM, int WN, int EPI, int NBUF, int KS, int NW>
 __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                              const uint4* __restrict__ Wf, int NBtot, void* __restrict__ out, int ldo,
                                              const SkPlan& pl, float* __restrict__ ws, int* __restrict__ tickets,
                                              const RopeEpi& re) {
-  using C = TileCfg<BM, WN, KS>;
+  using C = TileCfg<BM, WN, KS, NW>;
+  constexpr int SLOT = BM * C::NBT * 16;  // floats of one partial-tile slot
   constexpr int MI = C::MI, NQ0 = C::NQ0, NQ1 = C::NQ1;
-  constexpr bool BIG = BM * WN >= 1024;  // the 256 x 256 tile: 128 accumulator VGPRs, smaller epilogue load batches
-  static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF <= 32 && C::WF0 <= 32 && NBUF * C::BUFF <= 160, "tile geometry");
+  constexpr bool BIG = 2 * MI * WN >= 24;  // >= 96 accumulator VGPRs (256 x 256, 4-wave 128 x 192): smaller epilogue load batches
+  static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF % NW == 0 && C::WF0 % NW == 0 && C::WF1 % NW == 0 &&
+                    C::XF <= 32 && C::WF0 <= 32 && NBUF * C::BUFF * (NW == 4 ? 2 : 1) <= 160, "tile geometry");
   static_assert(EPI != EPI_SILU || WN % 2 == 0, "SiLU pairs (gate, up) n-blocks inside one wave");
   static_assert(EPI != EPI_ROPE || WN % 2 == 0, "RoPE tiles hold whole 128-column heads");
   static_assert(NBUF == 2 || (NBUF == 3 && C::CAN3), "K-tile buffers");
@@ -158,7 +164,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   const int lane = threadIdx.x & 63;
   // wave ids through readfirstlane: provably uniform, so every per-wave address term lives in SGPRs
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0..7
-  const int wm = w >> 2, wn = w & 3;
+  const int wm = w / C::WGN, wn = w % C::WGN;
   const int P = gridDim.x, b = blockIdx.x, xcd = b & 7;
   const int q8 = P >> 3, r8 = P & 7;
   const int vc = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
@@ -451,9 +457,10 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   // writes of 16 rows and reads of one row) and read back one full row per wave-instruction, so the global stores
   // (and the residual's h reads) are whole 128-B lines.
   auto store_tile_lds = [&]() {
-    constexpr int OC = EPI == EPI_SILU ? C::NBT * 8 : C::NBT * 16;  // output columns of the tile
-    constexpr int CH = OC / 4;                                      // 16-B f32 chunks per image row
-    static_assert(CH % 16 == 0, "swizzle stays inside the row");
+    constexpr int OC0 = EPI == EPI_SILU ? C::NBT * 8 : C::NBT * 16;  // output columns of the tile
+    constexpr int CH = OC0 / 4;                                      // 16-B f32 chunks per image row
+    constexpr int OC = (CH + 15) / 16 * 64;  // image row stride: whole 16-chunk swizzle groups (SiLU of 192: 96 -> 128)
+    static_assert(OC * (BM / 2) * 4 <= NBUF * C::BUFF * 1024, "the image fits the K-tile buffers");
     float* img = reinterpret_cast<float*>(&lds[0]);
     const int ncol_out = EPI == EPI_SILU ? NBtot * 8 : NBtot * 16;
     const int col0 = EPI == EPI_SILU ? nbase * 8 : nbase * 16;
@@ -481,17 +488,17 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
         }
       }
       __syncthreads();
-      // this wave's rows of the pass: r = w + 8 k, k < RPW (one row per wave-instruction, lanes = 16-B column chunks).
+      // this wave's rows of the pass: r = w + NW k, k < RPW (one row per wave-instruction, lanes = 16-B column chunks).
       // Every global load of those rows is issued before the first store: a load after a store through the same
       // output pointer cannot be hoisted by the compiler, so a row-by-row loop paid one full load latency per row
       // (16 rows per wave and pass at BM = 256)
-      constexpr int RPW = BM / 16;
+      constexpr int RPW = BM / 2 / NW;
       const bool live_ch = lane < CH && col0 + lane * 4 < ncol_out;
       if constexpr (EPI == EPI_ROPE) {
         // per-row metadata once per pass, lane k for row k: the token's position and its paged-cache block
         int my_pos = 0, my_blk = 0;
         if (lane < RPW) {
-          const int m = mbase + pass * (BM / 2) + w + 8 * lane;
+          const int m = mbase + pass * (BM / 2) + w + NW * lane;
           if (m < M) {
             my_pos = re.pos[m];
             const int seq = re.tok_seq ? re.tok_seq[m] : m;
@@ -518,7 +525,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
           }
 #pragma unroll
           for (int u = 0; u < RG; ++u) {
-            const int r = w + 8 * (k0 + u);
+            const int r = w + NW * (k0 + u);
             const int m = mbase + pass * (BM / 2) + r;
             if (m >= M || !live_ch) continue;
             const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2));
@@ -548,13 +555,13 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
         float4 hv[RB];
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
-          const int m = mbase + pass * (BM / 2) + w + 8 * (k0 + u);
+          const int m = mbase + pass * (BM / 2) + w + NW * (k0 + u);
           if (m < M && live_ch) hv[u] = *reinterpret_cast<const float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + col0 + lane * 4);
         }
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
           const int k = k0 + u;
-          const int r = w + 8 * k;
+          const int r = w + NW * k;
           const int m = mbase + pass * (BM / 2) + r;
           if (m >= M || !live_ch) continue;
           const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((lane ^ (r & 15)) << 2));
@@ -567,7 +574,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
       }
 #pragma unroll 4
       for (int k = 0; k < RPW; ++k) {
-        const int r = w + 8 * k;
+        const int r = w + NW * k;
         const int m = mbase + pass * (BM / 2) + r;
         const int ch = lane;
         if (live_ch && m < M) {
@@ -608,7 +615,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     const int cf = sk_owner(tile * T, iters, P), cl = sk_owner(tile * T + T - 1, iters, P);
     {
       // this lane's byte offset in its slot (one VGPR); the fragment's 1 KiB step rides in the SGPR offset
-      const int voff = (sk_slot(vc, tile, iters, P, T) * LSA_SK_SLOT_FLOATS + w * WSTRIDE + lane * 4) * 4;
+      const int voff = (sk_slot(vc, tile, iters, P, T) * SLOT + w * WSTRIDE + lane * 4) * 4;
 #pragma unroll
       for (int i = 0; i < 2 * MI; ++i)
 #pragma unroll
@@ -635,7 +642,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
 #pragma unroll
         for (int j = 0; j < WN; ++j) acc[2 * hh + i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       for (int c = cf; c <= cl; ++c) {
-        const int voff = (sk_slot(c, tile, iters, P, T) * LSA_SK_SLOT_FLOATS + w * WSTRIDE + lane * 4) * 4;
+        const int voff = (sk_slot(c, tile, iters, P, T) * SLOT + w * WSTRIDE + lane * 4) * 4;
         u32x4_t v[2][WN];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -660,13 +667,13 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   }
 }
 
-template <int BM, int WN, int EPI, int NBUF, int KS>
-__global__ __launch_bounds__(512) void gemm_sk_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
+template <int BM, int WN, int EPI, int NBUF, int KS, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_sk_kernel(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                                       const uint4* __restrict__ Wf, int NBtot,
                                                       void* __restrict__ out, int ldo, SkPlan pl,
                                                       float* __restrict__ ws, int* __restrict__ tickets,
                                                       RopeEpi re) {
-  gemm_sk_body<BM, WN, EPI, NBUF, KS>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets, re);
+  gemm_sk_body<BM, WN, EPI, NBUF, KS, NW>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets, re);
 }
 
 // Plan for a grid of (at most) ncu workgroups over BM x (NBT * 16) tiles: the data-parallel rounds keep whole tiles;
@@ -717,21 +724,24 @@ static SkPlan sk_plan(int M, int KB, int NBtot, int BM, int NBT, int KS, int ncu
 // partial written and read back by one CU) is priced in 256 x 256 K-tiles.  Measured: scripts/bench_prefill_gemm.py.
 // ks: k-steps of 32 per K-tile.  BK = 128 (ks 4) for the 128-row tiles was built and measured no faster (cold caches,
 // profiles/r5/prefill_gemm_bk128_ab_cold_mi355x.jsonl: ties or loses by 1-3 %), so every configuration runs BK = 64.
+// nw: waves per workgroup (4: two workgroups per CU, twice the columns per wave; TileCfg).
 struct SkCfg {
-  int bm, wn, ks;
+  int bm, wn, ks, nw;
   float cost;
 };
-static const SkCfg kSkCfgs[] = {{256, 4, 2, 1.00f}, {256, 3, 2, 1.06f}, {256, 2, 2, 1.18f},
-                                {128, 4, 2, 1.18f}, {128, 3, 2, 1.28f}, {128, 2, 2, 1.45f}};
+static const SkCfg kSkCfgs[] = {{256, 4, 2, 8, 1.00f}, {256, 3, 2, 8, 1.06f}, {256, 2, 2, 8, 1.18f},
+                                {128, 4, 2, 8, 1.18f}, {128, 3, 2, 8, 1.28f}, {128, 2, 2, 8, 1.45f},
+                                {128, 6, 2, 4, 1.20f}, {128, 4, 2, 4, 1.36f}};
 #define LSA_SK_SEAM_KTILES 8.0f
 
 // predicted time (256 x 256 K-tiles) of config c on the shape; *use_sk: whether the stream-K remainder beats whole
 // rounds
 static float sk_cfg_time(const SkCfg& c, int M, int KB, int NBtot, int ncu, bool* use_sk) {
-  const int nbt = 4 * c.wn;
+  const int nbt = (c.nw / 2) * c.wn;
+  ncu *= c.nw == 4 ? 2 : 1;  // workgroup slots; a slot of a shared CU runs at about half the rate (cost below)
   const long long tiles = (long long)((M + c.bm - 1) / c.bm) * ((NBtot + nbt - 1) / nbt);
   const float T = (float)((KB + c.ks - 1) / c.ks) * (float)c.ks / 2.0f;  // in 64-deep K-tiles
-  const float per_tile = T * c.cost * (float)(c.bm * nbt) / 4096.0f;
+  const float per_tile = T * c.cost * (float)(c.bm * nbt) / 4096.0f * (c.nw == 4 ? 2.0f : 1.0f);
   const float dp = (float)((tiles + ncu - 1) / ncu) * per_tile;
   const float skt = (float)tiles / ncu * per_tile + LSA_SK_SEAM_KTILES * (c.bm * nbt) / 4096.0f;
   *use_sk = tiles % ncu != 0 && skt < dp;
@@ -745,27 +755,29 @@ extern "C" void lsa_gemm_sk_epilogue(int mode) { g_sk_epl = mode ? 1 : 0; }
 static int g_sk_nbuf = 3;
 extern "C" void lsa_gemm_sk_nbuf(int n) { g_sk_nbuf = n == 2 ? 2 : 3; }
 
-template <int BM, int WN, int KS = 2>
+template <int BM, int WN, int KS = 2, int NW = 8>
 static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
                      float* ws, int* tickets, int ncu, int min_share, bool sk, int epl, int* grid_out,
                      const RopeEpi& re, hipStream_t stream) {
+  using C = TileCfg<BM, WN, KS, NW>;
+  const int P = ncu * (NW == 4 ? 2 : 1);  // persistent workgroups: one per CU, or two of the 4-wave kind
   int grid = 0;
-  SkPlan pl = sk_plan(M, KB, NBtot, BM, 4 * WN, KS, ncu, min_share, sk, &grid);
+  SkPlan pl = sk_plan(M, KB, NBtot, BM, C::NBT, KS, P, min_share, sk, &grid);
   pl.epl = epl;
-  if (pl.sk_tiles > 2 * ncu || grid > ncu || (long long)pl.sk_tiles * pl.T * (grid + 1) >= (1LL << 31)) return -3;
+  if (pl.sk_tiles > 2 * P || grid > P || (long long)pl.sk_tiles * pl.T * (grid + 1) >= (1LL << 31)) return -3;
   if (grid_out) *grid_out = grid;
   switch (epi) {
 #define LSA_SKL(E)                                                                                                \
   do {                                                                                                            \
-    if constexpr (TileCfg<BM, WN, KS>::CAN3) {                                                                    \
+    if constexpr (C::CAN3) {                                                                                      \
       if (g_sk_nbuf == 3) {                                                                                       \
-        hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 3, KS>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w, \
-                           NBtot, out, ldo, pl, ws, tickets, re);                                                 \
+        hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 3, KS, NW>), dim3(grid), dim3(64 * NW), 0, stream, x, ldx, \
+                           M, KB, w, NBtot, out, ldo, pl, ws, tickets, re);                                       \
         break;                                                                                                    \
       }                                                                                                           \
     }                                                                                                             \
-    hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 2, KS>), dim3(grid), dim3(512), 0, stream, x, ldx, M, KB, w,    \
-                       NBtot, out, ldo, pl, ws, tickets, re);                                                     \
+    hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 2, KS, NW>), dim3(grid), dim3(64 * NW), 0, stream, x, ldx, M, \
+                       KB, w, NBtot, out, ldo, pl, ws, tickets, re);                                              \
   } while (0)
     case EPI_BF16: LSA_SKL(EPI_BF16); break;
     case EPI_F32: LSA_SKL(EPI_F32); break;
@@ -823,7 +835,9 @@ static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, in
     sk = cfg < 8;
     cfg &= 7;
     if (cfg >= ncfg) return -5;
-    if (even_wn && kSkCfgs[cfg].wn % 2) cfg = kSkCfgs[cfg].bm == 256 ? 0 : 3;  // BN 192 -> the 256-column tile
+    // BN 192 -> the 256-column tile (RoPE needs whole 128-column heads; the 4-wave 192-column tile pairs fine for SiLU)
+    if (even_wn && (kSkCfgs[cfg].wn % 2 || (epi == EPI_ROPE && ((kSkCfgs[cfg].nw / 2) * kSkCfgs[cfg].wn) % 8)))
+      cfg = kSkCfgs[cfg].bm == 256 ? 0 : 3;
   }
   if (cfg_out) *cfg_out = cfg + (sk ? 0 : 8);
   const uint16_t* x = reinterpret_cast<const uint16_t*>(X);
@@ -838,6 +852,8 @@ static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, in
     LSA_SKC(3, 128, 4)
     LSA_SKC(4, 128, 3)
     LSA_SKC(5, 128, 2)
+    case 6: return sk_launch<128, 6, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, stream);
+    case 7: return sk_launch<128, 4, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, stream);
 #undef LSA_SKC
     default: return -5;
   }

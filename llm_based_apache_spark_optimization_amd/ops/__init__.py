@@ -442,14 +442,22 @@ def _sk_workspace(device) -> tuple:
     return got
 
 
-# (BM, BN, BK) of the stream-K tile configurations (gemm_tile256.hip kSkCfgs, same order)
-SK_CFGS = ((256, 256, 64), (256, 192, 64), (256, 128, 64), (128, 256, 64), (128, 192, 64), (128, 128, 64))
+# stream-K tile configurations (gemm_tile256.hip kSkCfgs, same order; + 8 = whole tiles only):
+# (BM, BN, BK, waves per workgroup; 4 = two workgroups per CU)
+SK_CFGS = ((256, 256, 64, 8), (256, 192, 64, 8), (256, 128, 64, 8), (128, 256, 64, 8), (128, 192, 64, 8),
+           (128, 128, 64, 8), (128, 192, 64, 4), (128, 128, 64, 4))
+
+
+def sk_cfg_pairs(cfg: int) -> bool:
+    """Whether a configuration's waves hold an even n-block count (the SiLU epilogue pairs gate / up n-blocks)."""
+    _, bn, _, nw = SK_CFGS[cfg & 7]
+    return (bn // 16 // (nw // 2)) % 2 == 0
 
 
 def sk_cfg_tag(cfg: int) -> str:
-    """Name of a stream-K configuration code (bench arms, the tuning table): e.g. 128x192, 128x192k128dp."""
-    bm, bn, bk = SK_CFGS[cfg & 7]
-    return f"{bm}x{bn}" + ("k128" if bk == 128 else "") + ("dp" if cfg & 8 else "")
+    """Name of a stream-K configuration code (bench arms, the tuning table): e.g. 128x192, 128x192w4dp."""
+    bm, bn, bk, nw = SK_CFGS[cfg & 7]
+    return f"{bm}x{bn}" + ("k128" if bk == 128 else "") + ("w4" if nw == 4 else "") + ("dp" if cfg & 8 else "")
 
 
 _SK_TUNING_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_sk_tuning.json")

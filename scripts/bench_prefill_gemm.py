@@ -103,7 +103,7 @@ for name, (M, N, K, epi) in shapes.items():
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     arms = {}
     for cf in cfgs:
-        if epi == "silu" and cf >= 0 and ops.SK_CFGS[cf & 7][1] % 128:
+        if epi == "silu" and cf >= 0 and not ops.sk_cfg_pairs(cf):
             continue  # SiLU pairs need an even n-block count per wave
         for sh in shares:
             for ep in epls:

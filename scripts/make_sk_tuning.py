@@ -6,8 +6,8 @@ import json
 import os
 import sys
 
-CFG = {"256x256": 0, "256x192": 1, "256x128": 2, "128x256": 3, "128x192": 4, "128x128": 5, "128x192k128": 6,
-       "128x128k128": 7}
+CFG = {"256x256": 0, "256x192": 1, "256x128": 2, "128x256": 3, "128x192": 4, "128x128": 5, "128x192w4": 6,
+       "128x128w4": 7}
 out_path = os.path.join(os.path.dirname(__file__), "..", "llm_based_apache_spark_optimization_amd", "ops",
                         "gemm_sk_tuning.json")
 tab = {}

@@ -171,7 +171,7 @@ def test_gemm_stream_k(gpu, M, NK, epi):
 
 
 @pytest.mark.parametrize("nbuf", [3, 2])
-@pytest.mark.parametrize("cfg", list(range(6)) + [8, 11, 13])
+@pytest.mark.parametrize("cfg", list(range(8)) + [8, 11, 13, 14, 15])
 @pytest.mark.parametrize("MNK", [(300, 3072, 1376), (2048, 5120, 1024), (1100, 800, 512), (640, 1536, 2048)])
 @pytest.mark.parametrize("epi", ["bf16", "silu", "res"])
 def test_gemm_stream_k_tile_shapes(gpu, cfg, MNK, epi, nbuf):
@@ -179,7 +179,7 @@ def test_gemm_stream_k_tile_shapes(gpu, cfg, MNK, epi, nbuf):
     every tile kind, with the three-buffer K-tile pipeline (where it fits) and the two-buffer one; K-tile counts 22,
     16, 8 and 32 exercise every tail of the three-way unrolled loop."""
     M, N, K = MNK
-    if epi == "silu" and ops.SK_CFGS[cfg & 7][1] % 128:
+    if epi == "silu" and not ops.sk_cfg_pairs(cfg):
         pytest.skip("SiLU needs an even n-block count per wave")
     ops.ext().gemm_sk_nbuf(nbuf)
     try:
