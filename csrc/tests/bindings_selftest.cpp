@@ -119,7 +119,7 @@ int main() {
     expect_reject("quant_rows_fp8 x8 too small", [&] { quant_rows_fp8(x, xq_small, sxq); });
     auto o2 = T({300, 64}, F32), sw = T({64}, F32);
     // stream-K prefill GEMM: workspace of lsa_gemm_sk_ws_bytes(ncu) / tickets(ncu)
-    auto wsk = T({2 * 8 * 65536}, F32), tks = T({16}, I32), ob = T({300, 64}, BF), wsb = T({64 * 128}, BF);
+    auto wsk = T({2 * 8 * 65536}, F32), tks = T({32}, I32), ob = T({300, 64}, BF), wsb = T({64 * 128}, BF);
     expect_ok("gemm_sk", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1); });
     auto wsk_small = T({65536}, F32);
     expect_reject("gemm_sk workspace", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk_small, tks, 8, 0, -1); });
