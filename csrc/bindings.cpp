@@ -76,7 +76,7 @@ int lsa_silu_bf16(const void* y, int M, int F, void* out, hipStream_t s);
 void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                        const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
-                       void* out, int ng, int pipe, hipStream_t s);
+                       void* out, int ng, int split, float* opart, float* mlpart, int* tickets, hipStream_t s);
 int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
 int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
                       void* out, int epi, int splitk, hipStream_t stream);
@@ -656,7 +656,8 @@ void kv8_dequant(const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& k
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                   const at::Tensor& cu_q, const at::Tensor& ctx_lens, const at::Tensor& work, int64_t H, int64_t Hkv,
-                  double scale, at::Tensor& out, int64_t rows32) {
+                  double scale, at::Tensor& out, int64_t rows32, const c10::optional<at::Tensor>& opart,
+                  const c10::optional<at::Tensor>& mlpart, const c10::optional<at::Tensor>& tickets) {
   need(q, at::kBFloat16, "q");
   need(work, at::kInt, "work");
   need(cu_q, at::kInt, "cu_q");
@@ -666,14 +667,41 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& v
   TORCH_CHECK(q.dim() == 3 && q.size(1) == H && q.size(2) == 128 && out.sizes() == q.sizes(), "q / out [T, H, 128]");
   TORCH_CHECK(cu_q.numel() == ctx_lens.numel() + 1 && block_tables.size(0) >= ctx_lens.numel(),
               "cu_q [nseq + 1], ctx_lens [nseq], block_tables [>= nseq, max_blocks]");
-  if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip); 2 = pipelined loop
-    // work [n_workgroups, 4 * NG]: NG (seq, q_start, t0, t1) items per workgroup (ops.prefill_plan)
-    TORCH_CHECK(work.dim() == 2 && (work.size(1) == 4 || work.size(1) == 8) && work.is_contiguous(),
-                "attn_prefill32 work must be [n, 4] or [n, 8] int32");
+  if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip)
+    // rows32 1: work [n_workgroups, 4 * NG] of (seq, q_start, t0, t1); 3: split pieces, [n, 8 * NG] of (seq, q_start,
+    // t0, t1, block slot, piece, -, -) with partial buffers for (max block slot + 1) * H slots (ops.prefill_plan)
+    const bool split = rows32 == 3;
+    TORCH_CHECK(rows32 == 1 || split, "attn_prefill: rows32 must be 0, 1 or 3");
+    const int wi = split ? 8 : 4;
+    TORCH_CHECK(work.dim() == 2 && (work.size(1) == wi || work.size(1) == 2 * wi) && work.is_contiguous(),
+                "attn_prefill32 work must be [n, 4 or 8 per group] int32");
+    float *op = nullptr, *mp = nullptr;
+    int* tk = nullptr;
+    if (split) {
+      TORCH_CHECK(opart && mlpart && tickets, "attn_prefill split: partial buffers required");
+      need(*opart, at::kFloat, "opart");
+      need(*mlpart, at::kFloat, "mlpart");
+      need(*tickets, at::kInt, "tickets");
+      // every slot field must address the buffers: checked on the host copy of the plan
+      const at::Tensor wc = work.to(at::kCPU);
+      const int* w = wc.data_ptr<int>();
+      int64_t max_slot = -1;
+      for (int64_t i = 0; i < work.numel() / 8; ++i)
+        if (w[8 * i] >= 0 && w[8 * i + 4] >= 0) {
+          TORCH_CHECK(w[8 * i + 5] == 0 || w[8 * i + 5] == 1, "attn_prefill split: piece must be 0 or 1");
+          max_slot = std::max<int64_t>(max_slot, w[8 * i + 4]);
+        }
+      const int64_t slots = (max_slot + 1) * H;
+      TORCH_CHECK(opart->numel() >= slots * 2 * 4 * 4096 && mlpart->numel() >= slots * 2 * 4 * 64 * 2 &&
+                      tickets->numel() >= slots, "attn_prefill split: partial buffers too small for the plan");
+      op = opart->data_ptr<float>();
+      mp = mlpart->data_ptr<float>();
+      tk = tickets->data_ptr<int>();
+    }
     check(lsa_attn_prefill32(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                              block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
-                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 4),
-                             rows32 == 2 ? 1 : 0, cur_stream()),
+                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / wi), split ? 1 : 0,
+                             op, mp, tk, cur_stream()),
           "attn_prefill32");
     return;
   }
@@ -919,7 +947,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("out_s8") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
-        py::arg("out"), py::arg("rows32") = 0);
+        py::arg("out"), py::arg("rows32") = 0, py::arg("opart") = py::none(), py::arg("mlpart") = py::none(),
+        py::arg("tickets") = py::none());
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);
   m.def("fp8_dequant", &fp8_dequant);

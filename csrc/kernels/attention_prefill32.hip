@@ -18,6 +18,9 @@
 #include "common.h"
 
 #define LSA_NEG_P (-1.0e30f)
+#define LSA_P32_SC1 16  // buffer cache-policy aux bit: sc1 (write-through store / L1-bypassing load)
+typedef __attribute__((address_space(1))) int lsa_p32_g_i32;
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 #ifndef LSA_P32_NBUF1
 #define LSA_P32_NBUF1 2  // K / V tile buffers of the single-group (NG = 1) kernel: the DMA runs NBUF - 1 tiles
                          // ahead.  4 (128 KiB, 3 tiles ahead) measured slower: one workgroup per CU instead of two
@@ -100,13 +103,28 @@ __device__ __forceinline__ int vp_off(int r, int col) { return r * 128 + ((((col
 // from the S^T accumulator): the accumulator's column is then the query row = the lane, so the online-
 // softmax rescale and the final 1 / l are lane-local multiplies (no cross-lane shuffles), and each lane
 // stores 4 contiguous dims of its own row per register group.
-template <int NG>
+//
+// SPLIT (work items of 8 ints: seq, q_start, t0, t1, slot, piece, -, -): a heavy causal query block is cut into two
+// key-tile ranges run by two groups (usually of different workgroups) so the longest serial tile chain halves.  Each
+// piece of a split block publishes its unnormalised O^T, row max and row sum write-through (sc1) into its half of
+// `slot`, drains, and takes the slot's ticket (one relaxed agent-scope add per group); the second to arrive merges
+// the other's partial (log-sum-exp in the exp2 domain) and writes the output -- nothing waits on another group, so
+// residency never matters (MI355X_MICROARCH.md hand-off row 1).
+struct P32Split {
+  float* opart;   // [slot][piece][wave 4][db 4][q 4][lane 64][4]
+  float* mlpart;  // [slot][piece][wave 4][lane 64][2]
+  int* tickets;   // [slot], zero between calls (the merging group resets its slot's)
+};
+
+template <int NG, bool SPLIT = false>
 __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                                      const uint16_t* __restrict__ vc,
                                                                      const int* __restrict__ block_tables, int max_blocks,
                                                                      const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
                                                                      const int* __restrict__ work, int H, int Hkv,
-                                                                     float scale_log2, uint16_t* __restrict__ out) {
+                                                                     float scale_log2, uint16_t* __restrict__ out,
+                                                                     P32Split sp) {
+  constexpr int WI = SPLIT ? 8 : 4;  // ints per work item
   constexpr int D = 128;
   // K / V tiles, NB buffers per group, filled by LDS-DMA (global_load_lds: no staging registers, and the DMAs of
   // the next NB - 1 tiles run under tile t's MFMAs)
@@ -122,14 +140,23 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   const int hk = h / (H / Hkv);
 
   // tiles of every group (the loop runs to the largest; the barriers are workgroup-wide)
-  int nt_max = 0, ntiles = 0, seq = 0, qs = 0, t0 = 0, t1 = 0;
+  int nt_max = 0, ntiles = 0, seq = 0, qs = 0, t0 = 0, t1 = 0, slot = -1, piece = 0;
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    const int* wk = work + 4 * (NG * wi + g);
+    const int* wk = work + WI * (NG * wi + g);
     const int sq = wk[0];
     const int nt = sq >= 0 ? wk[3] - wk[2] : 0;
     nt_max = max(nt_max, nt);
-    if (g == gi) { ntiles = nt; seq = sq; qs = wk[1]; t0 = wk[2]; t1 = wk[3]; }
+    if (g == gi) {
+      ntiles = nt; seq = sq; qs = wk[1]; t0 = wk[2]; t1 = wk[3];
+      if constexpr (SPLIT) {
+        slot = sq >= 0 ? wk[4] : -1;
+        piece = wk[5];
+      }
+    }
+  }
+  if constexpr (SPLIT) {  // a (head, block) pair of pieces owns slot + H * block-slot: distinct heads, distinct slots
+    if (slot >= 0) slot = slot * H + h;
   }
   const bool active = seq >= 0;
   const int sqc = active ? seq : 0;
@@ -293,220 +320,54 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
   const int qr = qs + w * 32 + r32;
-  if (active && qr < qlen) {
-    const float inv = lrow > 0.f ? 1.f / lrow : 0.f;
-    uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D + 4 * hh;
+  if constexpr (SPLIT) {
+    // piece of a split block: publish, ticket, the second to arrive merges (every thread of the workgroup passes the
+    // two barriers below; groups without a slot skip the rest)
+    __shared__ int s_last[NG];
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(sp.opart, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(sp.mlpart, 0, 0x7fffffff, 0x00020000);
+    auto obase = [&](int pc) { return (uint32_t)(((slot * 2 + pc) * 4 + w) * 4096 + lane * 4) * 4u; };
+    auto mbase = [&](int pc) { return (uint32_t)(((slot * 2 + pc) * 4 + w) * 64 + lane) * 8u; };
+    if (slot >= 0) {
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+      for (int db = 0; db < 4; ++db)
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        uint2 pk;
-        pk.x = pack2bf(o[db][4 * gq + 0] * inv, o[db][4 * gq + 1] * inv);
-        pk.y = pack2bf(o[db][4 * gq + 2] * inv, o[db][4 * gq + 3] * inv);
-        *reinterpret_cast<uint2*>(orow + 32 * db + 8 * gq) = pk;
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Pipelined variant (PIPE): the same work items, tiles and MFMA shapes, with the K fragments of tile t + 1 read
-// from LDS into registers while tile t's P V runs, so the S^T MFMAs of every tile start on operands already in
-// VGPRs (the loop above waits on an LDS read in front of each of its 16 S^T MFMAs: ~1.3 k cycles of s_waitcnt
-// per wave and tile, profiles/attn_prefill_pmc_3b2k_mi355x.txt).  One barrier per tile, between softmax(t) and
-// P V(t); buffer lifetimes:
-//   K(t) is consumed into registers before the barrier of tile t  -> 2 K buffers, K(t + 2) DMA'd after barrier t;
-//   V(t) is read by P V(t) after the barrier of tile t            -> 3 V buffers, V(t + 2) DMA'd after barrier t.
-// LDS per group 2 x 16 + 3 x 16 KiB = 80 KiB (NG = 2: the whole 160 KiB; NG = 1: two workgroups per CU).
-// Iteration t:  S^T(t) from registers, mask, softmax -> P | wait DMA(t + 1), barrier | DMA K, V (t + 2) |
-//               K(t + 1) LDS reads -> registers | P V(t) (V(t) transposed reads + MFMAs).
-// ------------------------------------------------------------------------------------------------
-template <int NG>
-__global__ __launch_bounds__(256 * NG, NG == 1 ? 2 : 1) void attn_prefill32p_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-                                                                      const uint16_t* __restrict__ vc,
-                                                                      const int* __restrict__ block_tables, int max_blocks,
-                                                                      const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
-                                                                      const int* __restrict__ work, int H, int Hkv,
-                                                                      float scale_log2, uint16_t* __restrict__ out) {
-  constexpr int D = 128;
-  constexpr int KT = 64 * D;  // elements of one 64-key tile image
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[NG][2][KT];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[NG][3][KT];
-  const int wi = blockIdx.x, h = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane((tid >> 6) & 3);
-  const int gi = NG == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 8);
-  const int r32 = lane & 31, hh = lane >> 5;
-  const int hk = h / (H / Hkv);
-
-  int nt_max = 0, ntiles = 0, seq = 0, qs = 0, t0 = 0, t1 = 0;
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    const int* wk = work + 4 * (NG * wi + g);
-    const int sq = wk[0];
-    const int nt = sq >= 0 ? wk[3] - wk[2] : 0;
-    nt_max = max(nt_max, nt);
-    if (g == gi) { ntiles = nt; seq = sq; qs = wk[1]; t0 = wk[2]; t1 = wk[3]; }
-  }
-  const bool active = seq >= 0;
-  const int sqc = active ? seq : 0;
-  const int q0 = cu_q[sqc], qlen = cu_q[sqc + 1] - q0;
-  const int ctx = ctx_lens[sqc];
-  const int pos0 = ctx - qlen;
-
-  const int qrow = qs + w * 32 + r32;
-  const int qpos = pos0 + qrow;
-  uint4 qf[8];
-  {
-    const uint16_t* qp = q + ((size_t)(q0 + max(0, min(qrow, qlen - 1))) * H + h) * D + 8 * hh;
-#pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2) qf[s2] = *reinterpret_cast<const uint4*>(qp + 16 * s2);
-  }
-  const int wave_last = min(qs + w * 32 + 31, qlen - 1);
-  const int wave_tiles = (active && qs + w * 32 < qlen) ? min(t1, (min(ctx, pos0 + wave_last + 1) + 63) >> 6) : 0;
-
-  f32x16_t o[4];
-#pragma unroll
-  for (int db = 0; db < 4; ++db) o[db] = f32x16_t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float mrow = LSA_NEG_P, lrow = 0.f;
-
-  const int* bt = block_tables + (size_t)sqc * max_blocks;
-  const int drow = lane >> 4, dslot = lane & 15;
-  unsigned koff[4], voff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 4 * (w + 4 * i) + drow;
-    koff[i] = (unsigned)(r * D + ((dslot ^ (r & 15)) << 3)) * 2u;
-    voff[i] = (unsigned)(r * D + ((dslot ^ ((r & 3) << 2)) << 3)) * 2u;
-  }
-  const unsigned kl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Ks[gi][0][4 * w * D]));
-  const unsigned vl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Vs[gi][0][4 * w * D]));
-  // one tile = 8 DMA wave-instructions per wave (4 K + 4 V row groups), into K buffer kb and V buffer vb
-  auto dma_tile = [&](int blk, int kb, int vb) {
-    const size_t base = ((size_t)blk * Hkv + hk) * 64 * D;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const unsigned lo = (unsigned)(16 * i * D) * 2u;
-      dma16s(kc + base, koff[i], kl0 + (unsigned)(kb * KT) * 2u + lo);
-      dma16s(vc + base, voff[i], vl0 + (unsigned)(vb * KT) * 2u + lo);
-    }
-  };
-  // K fragments of one tile for S^T: [kh][s2] = 32 keys (kh) x 16 dims (s2) of the row-swizzled image
-  uint4 kf[2][8];
-  auto read_k = [&](const uint16_t* Kg) {
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2) kf[kh][s2] = *reinterpret_cast<const uint4*>(&Kg[kp_off(32 * kh + r32, 2 * s2 + hh)]);
-  };
-
-  // prologue: tile 0 landed and published with its K fragments in registers, tile 1 in flight.  The full vmcnt(0)
-  // after tile 0 also retires the Q loads in hipcc's own wait tracking (it does not see the inline-asm DMAs: a
-  // counted vmcnt here left it assuming Q pending and waiting on vmcnt in front of every S^T MFMA of the loop)
-  if (0 < ntiles) dma_tile(__builtin_amdgcn_readfirstlane(bt[t0]), 0, 0);
-  __builtin_amdgcn_s_waitcnt(0x0070);
-  if (1 < ntiles) dma_tile(__builtin_amdgcn_readfirstlane(bt[t0 + 1]), 1, 1);
-  int bnext = (2 < ntiles) ? __builtin_amdgcn_readfirstlane(bt[t0 + 2]) : 0;
-  __syncthreads();
-  if (t0 < wave_tiles) read_k(Ks[gi][0]);
-
-  const int G16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-  int vcur = 0;  // V buffer of tile tt (tt % 3)
-  for (int tt = 0; tt < nt_max; ++tt) {
-    const int t = t0 + tt;
-    const bool live = t < wave_tiles;
-    uint4 pa[2][2];
-    if (live) {
-      f32x16_t st[2];
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        st[kh] = f32x16_t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2) st[kh] = mfma32x32x16(kf[kh][s2], qf[s2], st[kh]);
-      }
-      if (t * 64 + 63 > min(pos0 + qs + w * 32, ctx - 1)) {
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = t * 64 + 32 * kh + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            const bool ok = (key <= qpos) & (key < ctx);
-            st[kh][i] = ok ? st[kh][i] : -__builtin_inff();
-          }
-      }
-      float tmax = -__builtin_inff();
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[kh][i]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;
-      if (__any(tmax > mrow)) {
-        const float mnew = fmaxf(mrow, tmax);
-        const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
-        mrow = mnew;
-        lrow *= alpha;
-#pragma unroll
-        for (int db = 0; db < 4; ++db) o[db] *= alpha;
-      }
-      float psum = 0.f;
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        float p[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          p[i] = __builtin_amdgcn_exp2f(fmaf(st[kh][i], scale_log2, -mrow));
-          psum += p[i];
+        for (int gq = 0; gq < 4; ++gq) {
+          const u32x4_t u = {__float_as_uint(o[db][4 * gq]), __float_as_uint(o[db][4 * gq + 1]),
+                             __float_as_uint(o[db][4 * gq + 2]), __float_as_uint(o[db][4 * gq + 3])};
+          __builtin_amdgcn_raw_buffer_store_b128(u, ro, obase(piece), (db * 4 + gq) * 1024, LSA_P32_SC1);
         }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          pa[kh][s2].x = pack2bf(p[8 * s2 + 0], p[8 * s2 + 1]);
-          pa[kh][s2].y = pack2bf(p[8 * s2 + 2], p[8 * s2 + 3]);
-          pa[kh][s2].z = pack2bf(p[8 * s2 + 4], p[8 * s2 + 5]);
-          pa[kh][s2].w = pack2bf(p[8 * s2 + 6], p[8 * s2 + 7]);
-        }
-      }
-      psum += __shfl_xor(psum, 32, 64);
-      lrow += psum;
+      const u32x2_t ml = {__float_as_uint(mrow), __float_as_uint(lrow)};
+      __builtin_amdgcn_raw_buffer_store_b64(ml, rm, mbase(piece), 0, LSA_P32_SC1);
     }
-    // tile tt + 1 landed (its DMA, issued one iteration ago, is this wave's only one in flight) and published;
-    // every wave is past S^T(tt) and P V(tt - 1), so K buffer tt & 1 and V buffer (tt + 2) % 3 are free
-    __builtin_amdgcn_s_waitcnt(0x0070);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through partial
     __syncthreads();
-    const int vnext2 = vcur == 0 ? 2 : vcur - 1;  // (tt + 2) % 3
-    if (tt + 2 < ntiles) {
-      dma_tile(bnext, tt & 1, vnext2);
-      if (tt + 3 < ntiles) bnext = __builtin_amdgcn_readfirstlane(bt[t + 3]);
-    }
-    if (t + 1 < wave_tiles && tt + 1 < ntiles) read_k(Ks[gi][(tt + 1) & 1]);
-    if (live) {
-      // P V(t): four k-steps (kh, s2) of 4 MFMAs; the 8 transposed V reads of k-step j + 1 are issued before
-      // k-step j's MFMAs (two named register sets), so each MFMA group waits only for reads issued a group ago
-      const uint16_t* Vg = Vs[gi][vcur];
-      auto read_v = [&](uint4 (&va)[4], int j) {
-        const int r0 = 16 * j + 4 * (G16 >> 1) + qq;  // j = 2 kh + s2
+    if (slot >= 0 && (tid & 255) == 0)
+      s_last[gi] = __hip_atomic_fetch_add((lsa_p32_g_i32*)sp.tickets + slot, 1, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) == 1;
+    __syncthreads();
+    if (slot < 0) {
+      // unsplit item: normal epilogue below
+    } else if (!s_last[gi]) {
+      return;
+    } else {
+      if ((tid & 255) == 0) __hip_atomic_store((lsa_p32_g_i32*)sp.tickets + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int other = piece ^ 1;
+      const u32x2_t mo = __builtin_amdgcn_raw_buffer_load_b64(rm, mbase(other), 0, LSA_P32_SC1);
+      const float m2 = __uint_as_float(mo[0]), l2 = __uint_as_float(mo[1]);
+      const float mm = fmaxf(mrow, m2);
+      const float a1 = __builtin_amdgcn_exp2f(mrow - mm), a2 = __builtin_amdgcn_exp2f(m2 - mm);
 #pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const int col = 32 * db + 16 * (G16 & 1) + 4 * pp;
-          const uint2 v1 = ds_read_tr16p(&Vg[vp_off(r0, col)]);
-          const uint2 v2 = ds_read_tr16p(&Vg[vp_off(r0 + 8, col)]);
-          va[db] = make_uint4(v1.x, v1.y, v2.x, v2.y);
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const u32x4_t u = __builtin_amdgcn_raw_buffer_load_b128(ro, obase(other), (db * 4 + gq) * 1024, LSA_P32_SC1);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) o[db][4 * gq + c] = o[db][4 * gq + c] * a1 + __uint_as_float(u[c]) * a2;
         }
-      };
-      auto pv = [&](const uint4 (&va)[4], const uint4& p) {
-#pragma unroll
-        for (int db = 0; db < 4; ++db) o[db] = mfma32x32x16(va[db], p, o[db]);
-      };
-      uint4 vA[4], vB[4];
-      read_v(vA, 0);
-      read_v(vB, 1);
-      pv(vA, pa[0][0]);
-      read_v(vA, 2);
-      pv(vB, pa[0][1]);
-      read_v(vB, 3);
-      pv(vA, pa[1][0]);
-      pv(vB, pa[1][1]);
+      lrow = lrow * a1 + l2 * a2;
     }
-    vcur = vcur == 2 ? 0 : vcur + 1;
   }
-  const int qr = qs + w * 32 + r32;
   if (active && qr < qlen) {
     const float inv = lrow > 0.f ? 1.f / lrow : 0.f;
     uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D + 4 * hh;
@@ -522,26 +383,30 @@ __global__ __launch_bounds__(256 * NG, NG == 1 ? 2 : 1) void attn_prefill32p_ker
   }
 }
 
-// work: NG (seq, q_start, t0, t1) items per workgroup (seq < 0: that group idles), nwork workgroups;
-// pipe: 1 = the pipelined loop (attn_prefill32p_kernel)
+// work: NG (seq, q_start, t0, t1) items per workgroup (seq < 0: that group idles), nwork workgroups; split: 8-int items
+// (+ slot, piece) with the partial buffers of P32Split
 extern "C" int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                   const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv,
-                                  float scale, void* out, int ng, int pipe, hipStream_t s) {
+                                  float scale, void* out, int ng, int split, float* opart, float* mlpart, int* tickets,
+                                  hipStream_t s) {
   if (nwork <= 0) return 0;
   if (H % Hkv) return -1;
+  if (split && (!opart || !mlpart || !tickets)) return -3;
   dim3 grid(nwork, H);
   const float sl2 = scale * 1.4426950408889634f;
-#define LSA_P32_LAUNCH(KERN, NGV)                                                                                \
-  hipLaunchKernelGGL(KERN<NGV>, grid, dim3(256 * NGV), 0, s, reinterpret_cast<const uint16_t*>(q),               \
-                     reinterpret_cast<const uint16_t*>(kc), reinterpret_cast<const uint16_t*>(vc), block_tables,  \
-                     max_blocks, cu_q, ctx_lens, work, H, Hkv, sl2, reinterpret_cast<uint16_t*>(out))
+  const P32Split sp{opart, mlpart, tickets};
+#define LSA_P32_LAUNCH(NGV, SPV)                                                                                 \
+  hipLaunchKernelGGL((attn_prefill32_kernel<NGV, SPV>), grid, dim3(256 * NGV), 0, s,                             \
+                     reinterpret_cast<const uint16_t*>(q), reinterpret_cast<const uint16_t*>(kc),                 \
+                     reinterpret_cast<const uint16_t*>(vc), block_tables, max_blocks, cu_q, ctx_lens, work, H, Hkv, \
+                     sl2, reinterpret_cast<uint16_t*>(out), sp)
   if (ng != 1 && ng != 2) return -2;
-  if (pipe) {
-    if (ng == 2) LSA_P32_LAUNCH(attn_prefill32p_kernel, 2);
-    else LSA_P32_LAUNCH(attn_prefill32p_kernel, 1);
+  if (split) {
+    if (ng == 2) LSA_P32_LAUNCH(2, true);
+    else LSA_P32_LAUNCH(1, true);
   } else {
-    if (ng == 2) LSA_P32_LAUNCH(attn_prefill32_kernel, 2);
-    else LSA_P32_LAUNCH(attn_prefill32_kernel, 1);
+    if (ng == 2) LSA_P32_LAUNCH(2, false);
+    else LSA_P32_LAUNCH(1, false);
   }
 #undef LSA_P32_LAUNCH
   return (int)hipGetLastError();

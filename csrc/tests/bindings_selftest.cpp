@@ -178,11 +178,21 @@ int main() {
     expect_reject("kv8_dequant mb", [&] { kv8_dequant(k8, v8, ks, ks, bt, ctx, mb + 1, ko, ko); });
     // prefill: 2 sequences of 70 and 30 tokens
     auto qp = T({100, H, 128}, BF), outp = T({100, H, 128}, BF), cu = T({B + 1}, I32), work = T({2, 4}, I32);
-    expect_ok("attn_prefill32", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 1); });
+    expect_ok("attn_prefill32", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 1, none, none, none); });
     auto work_bad = T({2, 5}, I32);
-    expect_reject("attn_prefill32 work", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work_bad, H, Hkv, 0.08, outp, 1); });
+    expect_reject("attn_prefill32 work", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work_bad, H, Hkv, 0.08, outp, 1, none, none, none); });
     auto cu_bad = T({B}, I32);
-    expect_reject("attn_prefill offsets", [&] { attn_prefill(qp, kc, vc, bt, cu_bad, ctx, work, H, Hkv, 0.08, outp, 1); });
+    expect_reject("attn_prefill offsets", [&] { attn_prefill(qp, kc, vc, bt, cu_bad, ctx, work, H, Hkv, 0.08, outp, 1, none, none, none); });
+    // split pieces: 8-int items (slot 0, piece 0), partial buffers for H slots
+    auto work8 = T({2, 8}, I32), opp = T({H * 2 * 4 * 4096}, F32), mlp = T({H * 2 * 4 * 64 * 2}, F32), tkp = T({H}, I32);
+    expect_ok("attn_prefill32 split", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 3, opp, mlp, tkp); });
+    expect_reject("attn_prefill32 split without buffers", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 3, none, none, none); });
+    auto tkp_small = T({H - 1}, I32);
+    expect_reject("attn_prefill32 split tickets", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 3, opp, mlp, tkp_small); });
+    auto work8b = T({2, 8}, I32);
+    work8b.index_put_({0, 5}, 2);
+    expect_reject("attn_prefill32 split piece", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8b, H, Hkv, 0.08, outp, 3, opp, mlp, tkp); });
+    expect_reject("attn_prefill rows32 mode", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 2, none, none, none); });
     auto qkv = T({100, (H + 2 * Hkv) * 128}, BF), tpos = T({100}, I32), tseq = T({100}, I32), qo = T({100, H, 128}, BF);
     expect_ok("rope_append", [&] { rope_append(qkv, tpos, tseq, bt, cs, cs, qo, kc, vc, H, Hkv, none, none); });
     auto qo_small = T({99, H, 128}, BF);

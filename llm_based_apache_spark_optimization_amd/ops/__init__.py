@@ -1117,9 +1117,12 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
 # sequence has >= 512 rows (measured, scripts/bench_attn_prefill.py: 7B 2k 146 -> 119 us, 3B 2k 118 -> 115 us,
 # 8k 1051 -> 1021 us), else 16 (32 x 128-token prompts: 28 vs 31 us, twice the work items)
 PREFILL_ATTN = "auto"
-# 32-row kernel loop: 1 = pipelined (K fragments of tile t + 1 read into registers under tile t's P V, 2 K + 3 V
-# LDS buffers; attention_prefill32.hip attn_prefill32p_kernel), 0 = the one-barrier double-buffered loop
-PREFILL_PIPE = int(os.environ.get("LSA_PREFILL_PIPE", "0"))
+# KV split of heavy causal query blocks in the 32-row kernel (attention_prefill32.hip SPLIT): "0" = never (default),
+# N = every block of more than N tiles.  Off by default:
+# measured slower (profiles/r5/attn_prefill_kv_split_inlaunch_ab_mi355x.jsonl: 3B 2k 65.4 -> 74.5 us at the auto
+# threshold, 76.6-95.9 at 26 / 22 / 20 / 16; 3B 4 x 1k 74.0 -> 84.7) -- a CU is throughput-bound on one busy group
+# (two busy groups each take ~2x the tile time), so halving the longest chain only moves work between groups
+PREFILL_SPLIT = os.environ.get("LSA_PREFILL_SPLIT", "0")
 
 
 def _prefill_kernel(cu_q: list) -> str:
@@ -1134,17 +1137,30 @@ def prefill_qblock(cu_q: Optional[list] = None) -> int:
     return 128 if k == "32" else ext().prefill_qblock
 
 
+def _split_threshold(nts: list, heads: int, cus: int) -> int:
+    """Tile count above which a query block is split into two key-tile ranges (0: none) -- ``PREFILL_SPLIT``.  (An
+    automatic choice from a makespan model of the paired launch was built and dropped: the model, with pieces of
+    two busy groups at twice the tile time, still predicted the 3B 2k split at 24 tiles faster; measured slower.)"""
+    return int(PREFILL_SPLIT) if PREFILL_SPLIT not in ("", "0") else 0
+
+
+class PrefillWork(list):
+    """prefill_work's rows; ``split``: the rows are 8-int (KV-split) items."""
+    split = False
+
+
 def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[list[int]] = None,
-                 kernel: Optional[str] = None, heads: int = 32) -> list[tuple]:
+                 kernel: Optional[str] = None, heads: int = 32, cus: int = 256) -> PrefillWork:
     """Work items of the prefill attention kernel for packed sequences (cu_q offsets; ``ctx`` = per-sequence
     context length after this prefill, default = the chunk length, i.e. no cached prefix).
 
     16-row kernel: (seq, q_start) per workgroup, heaviest (latest) query blocks first.
-    32-row kernel ('32'): NG items (seq, q_start, t0, t1) per workgroup -- the key tiles [t0, t1) = the whole
-    causal range of a 128-row query block; NG = 2 pairs a heavy block with a light one (``_pair_blocks``).
-    (Cutting heavy blocks into KV splits merged by a second launch, or into two halves merged in LDS, were
-    both built and measured slower -- profiles/attn_prefill_kv_split_mi355x.jsonl,
-    profiles/attn_prefill_halves_mi355x.jsonl -- and removed.)"""
+    32-row kernel ('32'): NG items (seq, q_start, t0, t1) per workgroup -- the key tiles [t0, t1) = the whole causal
+    range of a 128-row query block; NG = 2 pairs a heavy block with a light one (``_pair_blocks``).  With KV split
+    (``_split_threshold``) a heavy block becomes two pieces [0, mid) and [mid, nt) sharing a merge slot: every item is
+    then (seq, q_start, t0, t1, slot, piece, 0, 0), slot -1 for unsplit blocks.  (A split merged by a second launch
+    and two halves merged in LDS were built in earlier rounds and measured slower -- profiles/attn_prefill_kv_split_
+    mi355x.jsonl, profiles/attn_prefill_halves_mi355x.jsonl; this one merges in the same launch.)"""
     kernel = kernel or _prefill_kernel(cu_q)
     if qblock is None:
         qblock = 128 if kernel == "32" else ext().prefill_qblock
@@ -1156,16 +1172,32 @@ def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[li
             items.append(((pos0 + min(qs + qblock, ql) + 63) // 64, s, qs))
     items.sort(key=lambda t: -t[0])
     if kernel != "32":
-        return [(s, qs) for _, s, qs in items]
-    units = [(s, qs, 0, nt) for nt, s, qs in items]
+        return PrefillWork((s, qs) for _, s, qs in items)
+    S = _split_threshold([nt for nt, _, _ in items], heads, cus)
+    if S:
+        units, slot = [], 0
+        for nt, s, qs in items:
+            if nt > S:
+                mid = nt // 2
+                units += [(s, qs, 0, mid, slot, 0, 0, 0), (s, qs, mid, nt, slot, 1, 0, 0)]
+                slot += 1
+            else:
+                units.append((s, qs, 0, nt, -1, 0, 0, 0))
+        units.sort(key=lambda u: -(u[3] - u[2]))
+        empty = (-1, 0, 0, 0, -1, 0, 0, 0)
+    else:
+        units = [(s, qs, 0, nt) for nt, s, qs in items]
+        empty = (-1, 0, 0, 0)
     n = len(units)
     longest = max(cu_q[i + 1] - cu_q[i] for i in range(len(cu_q) - 1))
+    out = PrefillWork()
+    out.split = bool(S)
     if not _pair_blocks(n, heads, longest, qblock):
-        return units
-    out = []
+        out.extend(units)
+        return out
     for i in range((n + 1) // 2):
         j = n - 1 - i
-        b = units[j] if j > i else (-1, 0, 0, 0)
+        b = units[j] if j > i else empty
         out.append(units[i] + b)
     return out
 
@@ -1173,17 +1205,41 @@ def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[li
 class PrefillPlan(NamedTuple):
     """Device-side plan of one prefill attention call (``prefill_plan``)."""
     kernel: str
-    work: torch.Tensor  # int32 [n_workgroups, 2 | 4 * NG]
+    work: torch.Tensor  # int32 [n_workgroups, 2 | 4 * NG | 8 * NG]
+    split_slots: int = 0  # merge slots per head (KV-split blocks); 0 = no split
 
 
 def prefill_plan(cu_q: list[int], ctx: Optional[list[int]] = None, heads: int = 32, device=None,
                  kernel: Optional[str] = None) -> PrefillPlan:
     """Work items of the prefill attention kernel for packed sequences, on ``device``."""
     kernel = kernel or _prefill_kernel(cu_q)
-    w = torch.tensor(prefill_work(cu_q, ctx=ctx, kernel=kernel, heads=heads), dtype=torch.int32)
+    rows = prefill_work(cu_q, ctx=ctx, kernel=kernel, heads=heads)
+    w = torch.tensor(rows, dtype=torch.int32)
+    slots = 0
+    if kernel == "32" and rows.split:
+        wv = w.view(-1, 8)
+        live = wv[:, 0] >= 0
+        slots = int(wv[live, 4].max().item()) + 1 if bool(live.any()) else 0
     if device is not None:
         w = w.to(device, non_blocking=True)
-    return PrefillPlan(kernel, w)
+    return PrefillPlan(kernel, w, slots)
+
+
+_p32_split_ws: dict = {}
+
+
+def _prefill_split_workspace(device, slots: int):
+    """(opart, mlpart, tickets) for ``slots`` merge slots (x heads, by the caller), per (device, stream): the tickets
+    are zero between calls (each merge resets its own), so one launch at a time per stream may use them."""
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    got = _p32_split_ws.get(key)
+    if got is None or got[2].numel() < slots:
+        n = max(slots, 256)
+        got = (torch.empty(n * 2 * 4 * 4096, dtype=torch.float32, device=device),
+               torch.empty(n * 2 * 4 * 64 * 2, dtype=torch.float32, device=device),
+               torch.zeros(n, dtype=torch.int32, device=device))
+        _p32_split_ws[key] = got
+    return got
 
 
 # auto | 1 | 0 -- heavy/light paired query blocks in the 32-row prefill kernel
@@ -1218,8 +1274,12 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, wo
     if plan is None:
         plan = (prefill_plan(cu, ctx=ctx_lens.tolist(), heads=H, device=q.device) if work is None
                 else PrefillPlan(_prefill_kernel(cu), work))
-    ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out,
-                       (2 if PREFILL_PIPE else 1) if plan.kernel == "32" else 0)
+    if plan.kernel == "32" and plan.split_slots:
+        op, mp, tk = _prefill_split_workspace(q.device, plan.split_slots * H)
+        ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out, 3, op, mp, tk)
+    else:
+        ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out,
+                           1 if plan.kernel == "32" else 0)
     return out
 
 

@@ -1,6 +1,6 @@
 """Prefill (causal flash) attention on MI355X: us and TFLOP/s per call for the BASELINE prefill shapes
-(packed variable-length sequences over the paged cache).  Arms (interleaved per case): the 32-row kernel's
-one-barrier loop (pipe0) and its pipelined loop (pipe1, ops.PREFILL_PIPE); LSA_ATTN_PIPES=0,1 selects."""
+(packed variable-length sequences over the paged cache).  Arms (interleaved per case): KV split thresholds
+(ops.PREFILL_SPLIT; LSA_ATTN_SPLITS=0,24 by default)."""
 import json
 import math
 import os
@@ -44,28 +44,30 @@ def case(name, nseq, qlen, H, Hkv):
     out = torch.empty_like(q)
     cud = torch.tensor(cu, dtype=torch.int32, device=dev)
     ctx = torch.full((nseq,), qlen, dtype=torch.int32, device=dev)
-    work = ops.prefill_plan(cu, heads=H, device=dev)
     flops = nseq * 4 * H * 128 * qlen * (qlen + 1) / 2  # causal QK^T + PV
     s0 = q[:qlen].float().transpose(0, 1)
     kk = kc[bt[0].long()].transpose(0, 1).reshape(Hkv, -1, 128)[:, :qlen].float().repeat_interleave(H // Hkv, 0)
     vv = vc[bt[0].long()].transpose(0, 1).reshape(Hkv, -1, 128)[:, :qlen].float().repeat_interleave(H // Hkv, 0)
     ref = torch.nn.functional.scaled_dot_product_attention(s0, kk, vv, is_causal=True).transpose(0, 1)
-    pipes = [int(p) for p in os.environ.get("LSA_ATTN_PIPES", "0,1").split(",")]
-    res = {"case": name, "kernel": work.kernel, "work": list(work.work.shape)}
-    times = {p: [] for p in pipes}
+    splits = os.environ.get("LSA_ATTN_SPLITS", "0,24").split(",")
+    plans = {}
+    for sp in splits:
+        ops.PREFILL_SPLIT = sp
+        plans[sp] = ops.prefill_plan(cu, heads=H, device=dev)
+    res = {"case": name, "kernel": plans[splits[0]].kernel}
+    times = {sp: [] for sp in splits}
     for _ in range(3):  # interleaved rounds
-        for p in pipes:
-            ops.PREFILL_PIPE = p
-            times[p].append(timeit(lambda: ops.attn_prefill(q, kc, vc, bt, cud, ctx, H, Hkv, 1 / math.sqrt(128), out,
-                                                             work=work)))
-    for p in pipes:
-        ops.PREFILL_PIPE = p
+        for sp in splits:
+            times[sp].append(timeit(lambda: ops.attn_prefill(q, kc, vc, bt, cud, ctx, H, Hkv, 1 / math.sqrt(128), out,
+                                                              work=plans[sp])))
+    for sp in splits:
         out.zero_()
-        ops.attn_prefill(q, kc, vc, bt, cud, ctx, H, Hkv, 1 / math.sqrt(128), out, work=work)
+        ops.attn_prefill(q, kc, vc, bt, cud, ctx, H, Hkv, 1 / math.sqrt(128), out, work=plans[sp])
         torch.cuda.synchronize()
         err = (out[:qlen].float() - ref).abs().max().item()  # spot check vs SDPA on the first sequence
-        us = sorted(times[p])[1]
-        res[f"pipe{p}"] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1), "max_err": round(err, 4)}
+        us = sorted(times[sp])[1]
+        res[f"split_{sp}"] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1), "max_err": round(err, 4),
+                              "work": list(plans[sp].work.shape), "slots": plans[sp].split_slots}
     print(json.dumps(res), flush=True)
 
 case("3b_explain_2k", 1, 2048, 24, 8)

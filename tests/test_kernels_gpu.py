@@ -483,22 +483,23 @@ def test_attn_decode_g1_single_buffer_grids(gpu, B):
     assert torch.equal(vc, v1)
 
 
-P_KERNELS = ["16", "32", "32pair", "32p", "32ppair"]
+P_KERNELS = ["16", "32", "32pair", "32split", "32splitpair"]
 
 
 def _set_prefill_kernel(monkeypatch, kernel):
     monkeypatch.setattr(ops, "PREFILL_ATTN", kernel[:2])
     monkeypatch.setattr(ops, "PREFILL_PAIR", "1" if kernel.endswith("pair") else "0")
-    monkeypatch.setattr(ops, "PREFILL_PIPE", 1 if kernel.startswith("32p") else 0)
+    # split variants: every block of more than 2 key tiles cut in two pieces merged in the launch
+    monkeypatch.setattr(ops, "PREFILL_SPLIT", "2" if "split" in kernel else "0")
 
 
 @pytest.mark.parametrize("kernel", P_KERNELS)
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
 @pytest.mark.parametrize("case", ["fresh", "chunked", "long", "longer"])
 def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
-    """The prefill attention kernels (16 x 16 MFMA, 64 rows per workgroup; 32 x 32 MFMA, 128 rows, single
-    or heavy/light paired query blocks per workgroup, one-barrier or pipelined loop) vs the fp32 reference:
-    packed variable-length sequences, chunked continuation, multi-block causal tiles."""
+    """The prefill attention kernels (16 x 16 MFMA, 64 rows per workgroup; 32 x 32 MFMA, 128 rows, single or
+    heavy/light paired query blocks per workgroup, whole causal ranges or KV-split pieces merged in the launch) vs
+    the fp32 reference: packed variable-length sequences, chunked continuation, multi-block causal tiles."""
     _set_prefill_kernel(monkeypatch, kernel)
     H, Hkv = HH
     D = 128
