@@ -462,7 +462,7 @@ def sk_cfg_tag(cfg: int) -> str:
 
 _SK_TUNING_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_sk_tuning.json")
 _sk_tuning: Optional[dict] = None
-_SK_BUCKETS = (128, 256, 512, 1024, 2048, 4096)
+_SK_BUCKETS = (128, 256, 300, 512, 1024, 2048, 4096)
 
 
 def sk_config(M: int, N: int, K: int, epi: str) -> int:

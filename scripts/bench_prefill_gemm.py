@@ -54,7 +54,7 @@ SHAPES.update({"3b_qkv_m2048": (2048, 5120, 3072, "bf16"), "3b_o_m2048": (2048, 
                "3b_gateup_m2048": (2048, 16384, 3072, "silu"), "3b_down_m2048": (2048, 3072, 8192, "res")})
 # --grid: every model projection at M = 128 .. 4096 (the tuning sweep behind ops/gemm_sk_tuning.json)
 GRID = {}
-for m in (128, 256, 512, 1024, 2048, 4096):
+for m in (128, 256, 300, 512, 1024, 2048, 4096):  # 300: the NL->SQL prompt length (3 row tiles of 128, one ragged)
     for mod, d, nq, f in (("7b", 4096, 12288, 11008), ("3b", 3072, 5120, 8192)):
         GRID[f"{mod}_qkv_m{m}"] = (m, nq, d, "bf16")
         GRID[f"{mod}_o_m{m}"] = (m, d, d, "res")
