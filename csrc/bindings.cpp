@@ -583,6 +583,14 @@ void attn_set_stamps(const c10::optional<at::Tensor>& st) {
   check(lsa_attn_set_stamps(st.has_value() ? st->data_ptr() : nullptr), "attn_set_stamps");
 }
 
+// diagnostic cycle stamps of the 32-row prefill attention (kernels/attention_prefill32.hip g_p32_stamps): the caller
+// sizes the buffer for the plan it launches, [nwork * H * NG * 4][8] int64
+extern "C" int lsa_p32_set_stamps(void* p);
+void attn_prefill_set_stamps(const c10::optional<at::Tensor>& st) {
+  if (st.has_value()) TORCH_CHECK(on_dev(*st) && st->element_size() == 8 && st->is_contiguous(), "stamps: int64 GPU tensor");
+  check(lsa_p32_set_stamps(st.has_value() ? st->data_ptr() : nullptr), "attn_prefill_set_stamps");
+}
+
 void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                  const at::Tensor& pos, int64_t H, int64_t Hkv, double scale, int64_t chunk_blocks, int64_t nsplit,
                  at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, at::Tensor& counters, int64_t xf_mt,
@@ -934,6 +942,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_xf8_blocks", &quant_xf8_blocks, py::arg("x"), py::arg("mt"), py::arg("blk"), py::arg("x8"), py::arg("s8"));
   m.def("quant_xf8", &quant_xf8, py::arg("x"), py::arg("mt"), py::arg("x8"), py::arg("sx"));
   m.def("attn_set_stamps", &attn_set_stamps, py::arg("stamps") = py::none());
+  m.def("attn_prefill_set_stamps", &attn_prefill_set_stamps, py::arg("stamps") = py::none());
   m.def("rope_append", &rope_append, py::arg("qkv"), py::arg("pos"), py::arg("tok_seq"), py::arg("block_tables"),
         py::arg("cos"), py::arg("sin"), py::arg("q_out"), py::arg("kc"), py::arg("vc"), py::arg("H"), py::arg("Hkv"),
         py::arg("ks") = py::none(), py::arg("vs") = py::none());

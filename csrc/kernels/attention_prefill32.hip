@@ -116,7 +116,12 @@ struct P32Split {
   int* tickets;   // [slot], zero between calls (the merging group resets its slot's)
 };
 
-template <int NG, bool SPLIT = false>
+// Diagnostic cycle stamps (STAMP instantiations only, scripts/p32_stamps.py): per wave, the s_memtime cycles of each
+// tile-loop segment summed over its tiles -> stamps[((wi * H + h) * NG + gi) * 4 + w][8]:
+//   0 DMA issue, 1 QK^T + mask + row max, 2 softmax, 3 PV issue, 4 DMA wait, 5 barrier, 6 tiles | nt_max << 32, 7 whole kernel
+__device__ unsigned long long* g_p32_stamps = nullptr;
+
+template <int NG, bool SPLIT = false, bool STAMP = false>
 __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                                      const uint16_t* __restrict__ vc,
                                                                      const int* __restrict__ block_tables, int max_blocks,
@@ -126,6 +131,21 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
                                                                      P32Split sp) {
   constexpr int WI = SPLIT ? 8 : 4;  // ints per work item
   constexpr int D = 128;
+  unsigned long long sg[6] = {0, 0, 0, 0, 0, 0}, st_t0 = 0, st_prev = 0;
+  unsigned st_tiles = 0;
+  auto stamp = [&](int k) {  // close segment k (STAMP builds only)
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long v = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      if (k >= 0) sg[k] += v - st_prev;
+      st_prev = v;
+    }
+  };
+  if constexpr (STAMP) {
+    st_t0 = __builtin_amdgcn_s_memtime();
+    st_prev = st_t0;
+  }
   // K / V tiles, NB buffers per group, filled by LDS-DMA (global_load_lds: no staging registers, and the DMAs of
   // the next NB - 1 tiles run under tile t's MFMAs)
   constexpr int NB = NG == 1 ? LSA_P32_NBUF1 : 2;  // tile buffers per group (NG = 2: 2 x 2 x 32 KiB fills the LDS)
@@ -206,117 +226,151 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
       dma16s(vc + base, voff[i], vl0 + lo);
     }
   };
-  // the DMA runs NB - 1 tiles ahead: the prologue issues tiles 0 .. NB - 2, iteration tt issues tile tt + NB - 1
-  // into the buffer tile tt - 1 left (its readers passed the previous barrier)
-  int bnext = 0;  // block of the next tile to issue (loaded one iteration ahead: no dependent load on the DMA path)
-#pragma unroll
-  for (int p = 0; p < NB - 1; ++p)
-    if (p < ntiles) dma_tile(__builtin_amdgcn_readfirstlane(bt[t0 + p]), p);
-  if (NB - 1 < ntiles) bnext = __builtin_amdgcn_readfirstlane(bt[t0 + NB - 1]);
-  // everything issued so far has landed (the Q fragments too, so hipcc's own wait tracking starts the loop with
-  // no outstanding loads and inserts no vmcnt waits of its own in front of the K reads)
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
   const int G16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-  for (int tt = 0; tt < nt_max; ++tt) {
-    const int t = t0 + tt;  // absolute key tile
-    int bnn = 0;
-    if (tt + NB - 1 < ntiles) {
-      dma_tile(bnext, (tt + NB - 1) % NB);  // its buffer's last readers (tile t - 1) passed the previous barrier
-      if (tt + NB < ntiles) bnn = __builtin_amdgcn_readfirstlane(bt[t + NB]);
+  // ---- one tile's pieces (shared by the two loop forms below)
+  // S^T for the two 32-key halves of the tile in LDS image Kg
+  auto qk = [&](const uint16_t* Kg, f32x16_t (&st)[2]) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      st[kh] = f32x16_t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2) {
+        const uint4 a = *reinterpret_cast<const uint4*>(&Kg[kp_off(32 * kh + r32, 2 * s2 + hh)]);
+        st[kh] = mfma32x32x16(a, qf[s2], st[kh]);
+      }
     }
-    const uint16_t* Kg = Ks[gi][tt % NB];
-    const uint16_t* Vg = Vs[gi][tt % NB];
-    if (t < wave_tiles) {  // causal: tiles past the wave's last row are skipped (barriers stay uniform)
-      // S^T for the two 32-key halves
-      f32x16_t st[2];
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        st[kh] = f32x16_t{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2) {
-          const uint4 a = *reinterpret_cast<const uint4*>(&Kg[kp_off(32 * kh + r32, 2 * s2 + hh)]);
-          st[kh] = mfma32x32x16(a, qf[s2], st[kh]);
-        }
-      }
-      // mask + online softmax; register i of half kh holds key t*64 + 32 kh + (i & 3) + 8 (i >> 2) + 4 hh.
-      // Raw scores: the scale is folded into one packed FMA per key pair in the exponent (v_pk_fma_f32), the
-      // row max is taken over raw scores and scaled once, masked keys are -inf (exp2 -> 0 whatever the row
-      // max; mrow starts finite, so a row with no visible key yet keeps p = 0, l = 0)
-      // causal / context mask, only on the tiles that cross this wave's diagonal or the context end (one
-      // wave-uniform branch per tile; inside it branch-free selects -- a short-circuit per element made
-      // hipcc emit 64 exec-mask branches per tile)
-      if (t * 64 + 63 > min(pos0 + qs + w * 32, ctx - 1)) {
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = t * 64 + 32 * kh + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            const bool ok = (key <= qpos) & (key < ctx);
-            st[kh][i] = ok ? st[kh][i] : -__builtin_inff();
-          }
-      }
-      float tmax = -__builtin_inff();
+  };
+  // mask + row max of absolute key tile t; register i of half kh holds key t*64 + 32 kh + (i & 3) + 8 (i >> 2) + 4 hh.
+  // Raw scores: the scale is folded into one packed FMA per key pair in the exponent (v_pk_fma_f32), the row max is
+  // taken over raw scores and scaled once, masked keys are -inf (exp2 -> 0 whatever the row max; mrow starts finite,
+  // so a row with no visible key yet keeps p = 0, l = 0).  The causal / context mask only runs on the tiles that
+  // cross this wave's diagonal or the context end (one wave-uniform branch per tile; inside it branch-free selects --
+  // a short-circuit per element made hipcc emit 64 exec-mask branches per tile)
+  auto mask_max = [&](f32x16_t (&st)[2], int t) -> float {
+    if (t * 64 + 63 > min(pos0 + qs + w * 32, ctx - 1)) {
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[kh][i]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;
-      // online softmax; the O / l rescale runs only when some row's max grew (exact: alpha = 1 otherwise),
-      // which under the causal mask is the first few tiles of a row
-      if (__any(tmax > mrow)) {
-        const float mnew = fmaxf(mrow, tmax);
-        const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
-        mrow = mnew;
-        lrow *= alpha;
-  #pragma unroll
-        for (int db = 0; db < 4; ++db) o[db] *= alpha;  // lane-local: the accumulator column is this lane's row
-      }
-      const f32x2p_t sc2 = {scale_log2, scale_log2}, mn2 = {-mrow, -mrow};
-      f32x2p_t ps2 = {0.f, 0.f};
-      uint4 pa[2][2];  // [kh][k-step s']: registers 8 s' .. 8 s' + 7 of half kh as bf16
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        float p[16];
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const f32x2p_t x = __builtin_elementwise_fma(f32x2p_t{st[kh][i], st[kh][i + 1]}, sc2, mn2);
-          p[i] = __builtin_amdgcn_exp2f(x.x);
-          p[i + 1] = __builtin_amdgcn_exp2f(x.y);
-          ps2 += f32x2p_t{p[i], p[i + 1]};
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          pa[kh][s2].x = pack2bf(p[8 * s2 + 0], p[8 * s2 + 1]);
-          pa[kh][s2].y = pack2bf(p[8 * s2 + 2], p[8 * s2 + 3]);
-          pa[kh][s2].z = pack2bf(p[8 * s2 + 4], p[8 * s2 + 5]);
-          pa[kh][s2].w = pack2bf(p[8 * s2 + 6], p[8 * s2 + 7]);
-        }
-      }
-      float psum = ps2.x + ps2.y;
-      psum += __shfl_xor(psum, 32, 64);
-      lrow += psum;
-      // O^T += V^T P^T: k-step (kh, s') covers keys 32 kh + 16 s' + 8 (j >> 2) + 4 hh + (j & 3) in element j
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int r0 = 32 * kh + 16 * s2 + 4 * (G16 >> 1) + qq;  // this lane's supplied key row (j < 4)
-#pragma unroll
-          for (int db = 0; db < 4; ++db) {
-            const int col = 32 * db + 16 * (G16 & 1) + 4 * pp;
-            const uint2 v1 = ds_read_tr16p(&Vg[vp_off(r0, col)]);
-            const uint2 v2 = ds_read_tr16p(&Vg[vp_off(r0 + 8, col)]);
-            uint4 va;
-            va.x = v1.x; va.y = v1.y; va.z = v2.x; va.w = v2.y;
-            o[db] = mfma32x32x16(va, pa[kh][s2], o[db]);
-          }
+        for (int i = 0; i < 16; ++i) {
+          const int key = t * 64 + 32 * kh + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          const bool ok = (key <= qpos) & (key < ctx);
+          st[kh][i] = ok ? st[kh][i] : -__builtin_inff();
         }
     }
-    bnext = bnn;
-    // tile t + 1's DMA has landed before the barrier publishes it; the tiles issued after it may stay in flight
-    wait_dma_tiles(min(ntiles - 1, tt + NB - 1) - (tt + 1));
+    float tmax = -__builtin_inff();
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[kh][i]);
+    return fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;
+  };
+  // online softmax; the O / l rescale runs only when some row's max grew (exact: alpha = 1 otherwise), which under
+  // the causal mask is the first few tiles of a row
+  auto rescale = [&](float tmax) {
+    if (__any(tmax > mrow)) {
+      const float mnew = fmaxf(mrow, tmax);
+      const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
+      mrow = mnew;
+      lrow *= alpha;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] *= alpha;  // lane-local: the accumulator column is this lane's row
+    }
+  };
+  // P = exp2(S * scale - m) as bf16 MFMA operands pa[kh][k-step s'] (registers 8 s' .. 8 s' + 7 of half kh); returns
+  // the row sum
+  auto softmax = [&](const f32x16_t (&st)[2], uint4 (&pa)[2][2]) -> float {
+    const f32x2p_t sc2 = {scale_log2, scale_log2}, mn2 = {-mrow, -mrow};
+    f32x2p_t ps2 = {0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      float p[16];
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const f32x2p_t x = __builtin_elementwise_fma(f32x2p_t{st[kh][i], st[kh][i + 1]}, sc2, mn2);
+        p[i] = __builtin_amdgcn_exp2f(x.x);
+        p[i + 1] = __builtin_amdgcn_exp2f(x.y);
+        ps2 += f32x2p_t{p[i], p[i + 1]};
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        pa[kh][s2].x = pack2bf(p[8 * s2 + 0], p[8 * s2 + 1]);
+        pa[kh][s2].y = pack2bf(p[8 * s2 + 2], p[8 * s2 + 3]);
+        pa[kh][s2].z = pack2bf(p[8 * s2 + 4], p[8 * s2 + 5]);
+        pa[kh][s2].w = pack2bf(p[8 * s2 + 6], p[8 * s2 + 7]);
+      }
+    }
+    float psum = ps2.x + ps2.y;
+    return psum + __shfl_xor(psum, 32, 64);
+  };
+  // O^T += V^T P^T: k-step (kh, s') covers keys 32 kh + 16 s' + 8 (j >> 2) + 4 hh + (j & 3) in element j
+  auto pv = [&](const uint16_t* Vg, const uint4 (&pa)[2][2]) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int r0 = 32 * kh + 16 * s2 + 4 * (G16 >> 1) + qq;  // this lane's supplied key row (j < 4)
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int col = 32 * db + 16 * (G16 & 1) + 4 * pp;
+          const uint2 v1 = ds_read_tr16p(&Vg[vp_off(r0, col)]);
+          const uint2 v2 = ds_read_tr16p(&Vg[vp_off(r0 + 8, col)]);
+          uint4 va;
+          va.x = v1.x; va.y = v1.y; va.z = v2.x; va.w = v2.y;
+          o[db] = mfma32x32x16(va, pa[kh][s2], o[db]);
+        }
+      }
+  };
+
+  {
+    // the DMA runs NB - 1 tiles ahead: the prologue issues tiles 0 .. NB - 2, iteration tt issues tile tt + NB - 1
+    // into the buffer tile tt - 1 left (its readers passed the previous barrier)
+    int bnext = 0;  // block of the next tile to issue (loaded one iteration ahead: no dependent load on the DMA path)
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p)
+      if (p < ntiles) dma_tile(__builtin_amdgcn_readfirstlane(bt[t0 + p]), p);
+    if (NB - 1 < ntiles) bnext = __builtin_amdgcn_readfirstlane(bt[t0 + NB - 1]);
+    // everything issued so far has landed (the Q fragments too, so hipcc's own wait tracking starts the loop with
+    // no outstanding loads and inserts no vmcnt waits of its own in front of the K reads)
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+    for (int tt = 0; tt < nt_max; ++tt) {
+      const int t = t0 + tt;  // absolute key tile
+      int bnn = 0;
+      stamp(-1);
+      if (tt + NB - 1 < ntiles) {
+        dma_tile(bnext, (tt + NB - 1) % NB);  // its buffer's last readers (tile t - 1) passed the previous barrier
+        if (tt + NB < ntiles) bnn = __builtin_amdgcn_readfirstlane(bt[t + NB]);
+      }
+      stamp(0);
+      if (t < wave_tiles) {  // causal: tiles past the wave's last row are skipped (barriers stay uniform)
+        if constexpr (STAMP) ++st_tiles;
+        f32x16_t st[2];
+        qk(Ks[gi][tt % NB], st);
+        const float tmax = mask_max(st, t);
+        stamp(1);
+        rescale(tmax);
+        uint4 pa[2][2];
+        lrow += softmax(st, pa);
+        stamp(2);
+        pv(Vs[gi][tt % NB], pa);
+        stamp(3);
+      }
+      bnext = bnn;
+      // tile t + 1's DMA has landed before the barrier publishes it; the tiles issued after it may stay in flight
+      wait_dma_tiles(min(ntiles - 1, tt + NB - 1) - (tt + 1));
+      stamp(4);
+      __syncthreads();
+      stamp(5);
+    }
+  }
+  if constexpr (STAMP) {
+    if (g_p32_stamps && lane == 0) {
+      unsigned long long* o8 = g_p32_stamps + ((((size_t)wi * H + h) * NG + gi) * 4 + w) * 8;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) o8[k] = sg[k];
+      o8[6] = (unsigned long long)st_tiles | ((unsigned long long)nt_max << 32);
+      o8[7] = __builtin_amdgcn_s_memtime() - st_t0;
+    }
   }
   // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
   const int qr = qs + w * 32 + r32;
@@ -383,6 +437,15 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
 }
 
+static bool g_p32_stamps_on = false;
+
+// stamps: [nwork * H * NG * 4][8] u64 device buffer, or null to switch the diagnostic kernel off
+extern "C" int lsa_p32_set_stamps(void* p) {
+  unsigned long long* v = reinterpret_cast<unsigned long long*>(p);
+  g_p32_stamps_on = v != nullptr;
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_p32_stamps), &v, sizeof(v));
+}
+
 // work: NG (seq, q_start, t0, t1) items per workgroup (seq < 0: that group idles), nwork workgroups; split: 8-int items
 // (+ slot, piece) with the partial buffers of P32Split
 extern "C" int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
@@ -392,22 +455,24 @@ extern "C" int lsa_attn_prefill32(const void* q, const void* kc, const void* vc,
   if (nwork <= 0) return 0;
   if (H % Hkv) return -1;
   if (split && (!opart || !mlpart || !tickets)) return -3;
+  if (ng != 1 && ng != 2) return -2;
   dim3 grid(nwork, H);
   const float sl2 = scale * 1.4426950408889634f;
   const P32Split sp{opart, mlpart, tickets};
-#define LSA_P32_LAUNCH(NGV, SPV)                                                                                 \
-  hipLaunchKernelGGL((attn_prefill32_kernel<NGV, SPV>), grid, dim3(256 * NGV), 0, s,                             \
+#define LSA_P32_LAUNCH(NGV, SPV, STV)                                                                           \
+  hipLaunchKernelGGL((attn_prefill32_kernel<NGV, SPV, STV>), grid, dim3(256 * NGV), 0, s,                        \
                      reinterpret_cast<const uint16_t*>(q), reinterpret_cast<const uint16_t*>(kc),                 \
                      reinterpret_cast<const uint16_t*>(vc), block_tables, max_blocks, cu_q, ctx_lens, work, H, Hkv, \
                      sl2, reinterpret_cast<uint16_t*>(out), sp)
-  if (ng != 1 && ng != 2) return -2;
-  if (split) {
-    if (ng == 2) LSA_P32_LAUNCH(2, true);
-    else LSA_P32_LAUNCH(1, true);
-  } else {
-    if (ng == 2) LSA_P32_LAUNCH(2, false);
-    else LSA_P32_LAUNCH(1, false);
-  }
+#define LSA_P32_NG(SPV, STV)               \
+  do {                                     \
+    if (ng == 2) LSA_P32_LAUNCH(2, SPV, STV); \
+    else LSA_P32_LAUNCH(1, SPV, STV);         \
+  } while (0)
+  if (split) LSA_P32_NG(true, false);
+  else if (g_p32_stamps_on) LSA_P32_NG(false, true);  // diagnostic build of the unsplit kernel (lsa_p32_set_stamps)
+  else LSA_P32_NG(false, false);
+#undef LSA_P32_NG
 #undef LSA_P32_LAUNCH
   return (int)hipGetLastError();
 }
