@@ -122,8 +122,7 @@ __device__ __forceinline__ void attn_store4(uint16_t* out, uint8_t* s8, int xf_m
     return;
   }
   float a = fmaxf(fmaxf(fabsf(o0), fabsf(o1)), fmaxf(fabsf(o2), fabsf(o3)));
-#pragma unroll
-  for (int off = 1; off < 32; off <<= 1) a = fmaxf(a, __shfl_xor(a, off, 64));
+  a = lsa_max_x16(lsa_row16_max(a));  // the head's 32 threads: two whole rows of one half-wave
   const int e = e8m0_for_amax(a);
   const int k = h * 128 + d0;
   *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out) + xf8_off(b, k, xf_mt)) = pack4_fp8(o0, o1, o2, o3, e8m0_inv(e));
@@ -274,7 +273,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
         const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
         const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = x[j] * cc[j] + sg * __shfl_xor(x[j], 8, 64) * sn[j];
+        for (int j = 0; j < 8; ++j) y[j] = x[j] * cc[j] + sg * lsa_xor8(x[j]) * sn[j];
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] = x[j];
@@ -285,10 +284,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
           float a = 0.f;
 #pragma unroll
           for (int j = 0; j < 8; ++j) a = fmaxf(a, fabsf(y[j]));
-          a = fmaxf(a, __shfl_xor(a, 8, 64));
-          a = fmaxf(a, __shfl_xor(a, 4, 64));
-          a = fmaxf(a, __shfl_xor(a, 2, 64));
-          a = fmaxf(a, __shfl_xor(a, 1, 64));
+          a = lsa_row16_max(a);
           new8_s[lg - G][li] = pack8_fp8(y, kv8_inv(a));
           if (li == 0) newsc_s[lg - G] = a * LSA_KV8_RMAX;
         }
@@ -370,10 +366,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
 #pragma unroll
           for (int j = 0; j < 8; ++j) d = fmaf(qf[g][j], kf[j], d);
         }
-        d += __shfl_xor(d, 8, 64);
-        d += __shfl_xor(d, 4, 64);
-        d += __shfl_xor(d, 2, 64);
-        d += __shfl_xor(d, 1, 64);
+        d = lsa_row16_sum(d);
         s[u][g] = valid ? (KV8 ? d * ksu : (DOT2 ? d * scale_log2 : d)) : LSA_NEG;
       }
     }
@@ -465,17 +458,14 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
   // (7B B=32 ctx ~190: 23.6 -> 22.1 us; 7B B=1: 7.3 -> 6.4 us, rocprofv3)
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    float mo = fmaxf(m[g], __shfl_xor(m[g], 16, 64));
-    mo = fmaxf(mo, __shfl_xor(mo, 32, 64));
+    const float mo = lsa_max_x32(lsa_max_x16(m[g]));
     const float a = __builtin_amdgcn_exp2f(m[g] - mo);
     l[g] *= a;
-    l[g] += __shfl_xor(l[g], 16, 64);
-    l[g] += __shfl_xor(l[g], 32, 64);
+    l[g] = lsa_sum_x32(lsa_sum_x16(l[g]));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       o[g][j] *= a;
-      o[g][j] += __shfl_xor(o[g][j], 16, 64);
-      o[g][j] += __shfl_xor(o[g][j], 32, 64);
+      o[g][j] = lsa_sum_x32(lsa_sum_x16(o[g][j]));
     }
     m[g] = mo;
   }
@@ -792,8 +782,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
           st[gi][kt][i] = v;
           tmax = fmaxf(tmax, v);
         }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = lsa_max_x32(lsa_max_x16(tmax));
       const float mnew = fmaxf(mrow[gi], tmax);
       const float alpha = __builtin_amdgcn_exp2f(mrow[gi] - mnew);
       mrow[gi] = mnew;
@@ -843,8 +832,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
 #undef LSA_PF_FETCH
 #pragma unroll
   for (int gi = 0; gi < QG; ++gi) {
-    float lt = lrow[gi] + __shfl_xor(lrow[gi], 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    const float lt = lsa_sum_x32(lsa_sum_x16(lrow[gi]));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float li = __shfl(lt, 4 * g + i, 64);

@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[kh][i]);
-    return fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;
+    return lsa_max_x32(tmax) * scale_log2;
   };
   // online softmax; the O / l rescale runs only when some row's max grew (exact: alpha = 1 otherwise), which under
   // the causal mask is the first few tiles of a row
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
       }
     }
     float psum = ps2.x + ps2.y;
-    return psum + __shfl_xor(psum, 32, 64);
+    return lsa_sum_x32(psum);
   };
   // O^T += V^T P^T: k-step (kh, s') covers keys 32 kh + 16 s' + 8 (j >> 2) + 4 hh + (j & 3) in element j
   auto pv = [&](const uint16_t* Vg, const uint4 (&pa)[2][2]) {

@@ -68,17 +68,60 @@ __device__ __forceinline__ f32x4_t mfma16x16x32(const uint4 a, const uint4 b, f3
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Cross-lane reductions on the VALU.  hipcc lowers every __shfl_xor to ds_bpermute_b32, an LDS-crossbar round trip
+// (address VALU + LDS pipe + lgkmcnt wait) per butterfly step of a dependent chain; within a 16-lane row DPP does the
+// step as a modifier of the add / max itself, and across rows / halves v_permlane16_swap / v_permlane32_swap exchange
+// whole rows in one VALU op.  Every pairing below is symmetric (lane a reads b iff b reads a) and each op is
+// commutative, so all lanes of a reduction end bitwise identical, as with the xor butterfly.  Callers run with whole
+// 16-lane rows active (whole waves for the x16 / x32 / wave forms): DPP from a disabled lane reads 0.
+template <int CTRL>
+__device__ __forceinline__ float lsa_dpp(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+// DPP controls: row_mirror (lane i <- 15 - i), row_half_mirror (i <- 7 - i in each 8), quad_perm [1,0,3,2] / [2,3,0,1]
+// (xor 1 / xor 2), row_ror:8 (xor 8 within the row)
+#define LSA_DPP_ROW_MIRROR 0x140
+#define LSA_DPP_HALF_MIRROR 0x141
+#define LSA_DPP_XOR1 0xB1
+#define LSA_DPP_XOR2 0x4E
+#define LSA_DPP_ROR8 0x128
+// sum / max over the 16 lanes of each row, in every lane of the row
+__device__ __forceinline__ float lsa_row16_sum(float d) {
+  d += lsa_dpp<LSA_DPP_ROW_MIRROR>(d);
+  d += lsa_dpp<LSA_DPP_HALF_MIRROR>(d);
+  d += lsa_dpp<LSA_DPP_XOR1>(d);
+  return d + lsa_dpp<LSA_DPP_XOR2>(d);
+}
+__device__ __forceinline__ float lsa_row16_max(float d) {
+  d = fmaxf(d, lsa_dpp<LSA_DPP_ROW_MIRROR>(d));
+  d = fmaxf(d, lsa_dpp<LSA_DPP_HALF_MIRROR>(d));
+  d = fmaxf(d, lsa_dpp<LSA_DPP_XOR1>(d));
+  return fmaxf(d, lsa_dpp<LSA_DPP_XOR2>(d));
+}
+// the value of lane i ^ 8 (same row)
+__device__ __forceinline__ float lsa_xor8(float x) { return lsa_dpp<LSA_DPP_ROR8>(x); }
+// lanes i and i ^ 16 / i ^ 32 combined: the swap of x with itself returns {rows [0 0 2 2], rows [1 1 3 3]} (x16) or
+// {halves [lo lo], [hi hi]} (x32), so op(r0, r1) pairs each lane with its partner in the same order in both
+__device__ __forceinline__ float lsa_sum_x16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float lsa_max_x16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float lsa_sum_x32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float lsa_max_x32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
+__device__ __forceinline__ float wave_sum(float v) { return lsa_sum_x32(lsa_sum_x16(lsa_row16_sum(v))); }
+
+__device__ __forceinline__ float wave_max(float v) { return lsa_max_x32(lsa_max_x16(lsa_row16_max(v))); }
 
 // block-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats
 __device__ __forceinline__ float block_sum(float v, float* red) {

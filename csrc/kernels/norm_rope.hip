@@ -212,8 +212,7 @@ __global__ __launch_bounds__(64) void res_add_ss_kernel(float* __restrict__ h, c
     for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
     *reinterpret_cast<uint4*>(xn + (xf_mt ? xf_off(m, c, xf_mt) : (size_t)m * D + c)) = pack8(v);
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  ss = wave_sum(ss);
   if (threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ss_out) + m, (unsigned long long)ss_to_q24(ss));
 }
 
@@ -311,10 +310,7 @@ __global__ __launch_bounds__(1024) void rope_append_kernel(const uint16_t* __res
       float a = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) a = fmaxf(a, fmaxf(fabsf(y0[j]), fabsf(y1[j])));
-      a = fmaxf(a, __shfl_xor(a, 8, 64));
-      a = fmaxf(a, __shfl_xor(a, 4, 64));
-      a = fmaxf(a, __shfl_xor(a, 2, 64));
-      a = fmaxf(a, __shfl_xor(a, 1, 64));
+      a = lsa_row16_max(a);
       const float inv = kv8_inv(a);
       const size_t r8 = ((size_t)blk * Hkv + (hd - H)) * 64 + off;
       uint8_t* tile = reinterpret_cast<uint8_t*>(kc) + (r8 - off) * D;  // token-pair order (common.h kv8_off)
@@ -353,10 +349,7 @@ __global__ __launch_bounds__(1024) void rope_append_kernel(const uint16_t* __res
       float a = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) a = fmaxf(a, fabsf(f[j]));
-      a = fmaxf(a, __shfl_xor(a, 8, 64));
-      a = fmaxf(a, __shfl_xor(a, 4, 64));
-      a = fmaxf(a, __shfl_xor(a, 2, 64));
-      a = fmaxf(a, __shfl_xor(a, 1, 64));
+      a = lsa_row16_max(a);
       const size_t r8 = ((size_t)blk * Hkv + hv) * 64 + off;
       *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(vc) + (r8 - off) * D + kv8_off(off, c)) = pack8_fp8(f, kv8_inv(a));
       if (c == 0) vs[r8] = a * LSA_KV8_RMAX;
