@@ -119,6 +119,30 @@ __device__ __forceinline__ float lsa_max_x32(float x) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// 64-lane max of a packed 64-bit key (argmax: orderable value << 32 | ~index): each half moved by the same DPP /
+// permlane pattern, compared whole
+template <int CTRL>
+__device__ __forceinline__ unsigned long long lsa_dpp64(unsigned long long x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long lsa_umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+  v = lsa_umax64(v, lsa_dpp64<LSA_DPP_ROW_MIRROR>(v));
+  v = lsa_umax64(v, lsa_dpp64<LSA_DPP_HALF_MIRROR>(v));
+  v = lsa_umax64(v, lsa_dpp64<LSA_DPP_XOR1>(v));
+  v = lsa_umax64(v, lsa_dpp64<LSA_DPP_XOR2>(v));
+  {
+    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(v >> 32), (uint32_t)(v >> 32), false, false);
+    v = lsa_umax64(((unsigned long long)hi[0] << 32) | lo[0], ((unsigned long long)hi[1] << 32) | lo[1]);
+  }
+  const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(v >> 32), (uint32_t)(v >> 32), false, false);
+  return lsa_umax64(((unsigned long long)hi[0] << 32) | lo[0], ((unsigned long long)hi[1] << 32) | lo[1]);
+}
+
 __device__ __forceinline__ float wave_sum(float v) { return lsa_sum_x32(lsa_sum_x16(lsa_row16_sum(v))); }
 
 __device__ __forceinline__ float wave_max(float v) { return lsa_max_x32(lsa_max_x16(lsa_row16_max(v))); }

@@ -28,11 +28,7 @@ __global__ __launch_bounds__(256) void argmax_partial_kernel(const float* __rest
     const unsigned long long k = pack_key(row[i], i);
     best = k > best ? k : best;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long x = __shfl_xor(best, o, 64);
-    best = x > best ? x : best;
-  }
+  best = wave_max_u64(best);
   __shared__ unsigned long long red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
   __syncthreads();
@@ -83,11 +79,7 @@ __global__ __launch_bounds__(64) void argmax_commit_kernel(const unsigned long l
     const unsigned long long k = part[(size_t)b * nch + i];
     best = k > best ? k : best;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long x = __shfl_xor(best, o, 64);
-    best = x > best ? x : best;
-  }
+  best = wave_max_u64(best);
   if (threadIdx.x == 0) commit_token(st, b, (int)(0xffffffffu - (uint32_t)(best & 0xffffffffull)));
 }
 
@@ -178,11 +170,7 @@ __global__ __launch_bounds__(1024) void sample_commit_kernel(const unsigned long
         const unsigned long long k = amax_part[(size_t)b * nch_amax + i];
         best = k > best ? k : best;
       }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long x = __shfl_xor(best, o, 64);
-        best = x > best ? x : best;
-      }
+      best = wave_max_u64(best);
       if (threadIdx.x == 0) commit_token(st, b, (int)(0xffffffffu - (uint32_t)(best & 0xffffffffull)));
     }
     return;
