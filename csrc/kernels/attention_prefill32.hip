@@ -161,6 +161,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
 
   // tiles of every group (the loop runs to the largest; the barriers are workgroup-wide)
   int nt_max = 0, ntiles = 0, seq = 0, qs = 0, t0 = 0, t1 = 0, slot = -1, piece = 0;
+  int o_nt = 0, o_seq = 0, o_t0 = 0;  // the partner group's item (HELP)
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int* wk = work + WI * (NG * wi + g);
@@ -173,6 +174,8 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
         slot = sq >= 0 ? wk[4] : -1;
         piece = wk[5];
       }
+    } else {
+      o_nt = nt; o_seq = sq >= 0 ? sq : 0; o_t0 = wk[2];
     }
   }
   if constexpr (SPLIT) {  // a (head, block) pair of pieces owns slot + H * block-slot: distinct heads, distinct slots
@@ -217,6 +220,23 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   const unsigned kl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Ks[gi][0][4 * w * D]));
   const unsigned vl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Vs[gi][0][4 * w * D]));
+  // HELP (paired groups, unsplit): once a group has computed its last tile it issues its partner's K / V DMAs, so
+  // the heavy causal block's waves -- the launch's critical path -- stop paying ~420 cycles of LDS-DMA issue per tile
+  // (scripts/p32_stamps.py).  Same kv-head, the partner's own block table and LDS images; every wave still drains
+  // its DMAs (vmcnt(0), two buffers) before the barrier that publishes the tile.
+  constexpr bool HELP = NG == 2 && !SPLIT;
+  const int* bt_o = block_tables + (size_t)o_seq * max_blocks;
+  const unsigned kl0_o = __builtin_amdgcn_readfirstlane(lds_addr(&Ks[NG - 1 - gi][0][4 * w * D]));
+  const unsigned vl0_o = __builtin_amdgcn_readfirstlane(lds_addr(&Vs[NG - 1 - gi][0][4 * w * D]));
+  auto dma_tile_o = [&](int blk, int b) {
+    const size_t base = ((size_t)blk * Hkv + hk) * 64 * D;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned lo = (unsigned)(b * 64 * D + 16 * i * D) * 2u;
+      dma16s(kc + base, koff[i], kl0_o + lo);
+      dma16s(vc + base, voff[i], vl0_o + lo);
+    }
+  };
   auto dma_tile = [&](int blk, int b) {
     const size_t base = ((size_t)blk * Hkv + hk) * 64 * D;
 #pragma unroll
@@ -338,9 +358,12 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
       int bnn = 0;
       stamp(-1);
       if (tt + NB - 1 < ntiles) {
-        dma_tile(bnext, (tt + NB - 1) % NB);  // its buffer's last readers (tile t - 1) passed the previous barrier
+        // its buffer's last readers (tile t - 1) passed the previous barrier; an idle partner issues it instead
+        if (!HELP || tt < o_nt) dma_tile(bnext, (tt + NB - 1) % NB);
         if (tt + NB < ntiles) bnn = __builtin_amdgcn_readfirstlane(bt[t + NB]);
       }
+      if (HELP && tt >= ntiles && tt + NB - 1 < o_nt)
+        dma_tile_o(__builtin_amdgcn_readfirstlane(bt_o[o_t0 + tt + NB - 1]), (tt + NB - 1) % NB);
       stamp(0);
       if (t < wave_tiles) {  // causal: tiles past the wave's last row are skipped (barriers stay uniform)
         if constexpr (STAMP) ++st_tiles;
@@ -357,7 +380,8 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
       }
       bnext = bnn;
       // tile t + 1's DMA has landed before the barrier publishes it; the tiles issued after it may stay in flight
-      wait_dma_tiles(min(ntiles - 1, tt + NB - 1) - (tt + 1));
+      if constexpr (HELP) __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): own or helped DMAs (NB = 2)
+      else wait_dma_tiles(min(ntiles - 1, tt + NB - 1) - (tt + 1));
       stamp(4);
       __syncthreads();
       stamp(5);
