@@ -68,9 +68,10 @@ void lsa_gemm_sk_nbuf(int n);
 int lsa_gemm_sk_rope(const void* X, int ldx, int M, int K, const void* Wf, int N, float* ws, int* tickets, int ncu,
                      int min_share, int cfg, const int* pos, const int* tok_seq, const int* block_tables,
                      int max_blocks, const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int H,
-                     int Hkv, int* grid_out, int* cfg_out, hipStream_t stream);
+                     int Hkv, int* grid_out, int* cfg_out, const LsaEpi* ne, hipStream_t stream);
 int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
-                int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, hipStream_t stream);
+                int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, const LsaEpi* ne,
+                hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 int lsa_silu_bf16(const void* y, int M, int F, void* out, hipStream_t s);
 void lsa_fp8_gemm_knobs(int waves, int depth);
@@ -331,8 +332,35 @@ void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) 
 // 1 f32 [M][N], 2 SiLU(gate) * up bf16 [M][N / 2], 3 h f32 [M][N] += x @ W^T.  ws / tickets: the per-stream
 // workspace (ops._sk_workspace).  cfg: -1 = the kernel's cost model, else a tile configuration index (+ 8: whole
 // tiles only; + 16 + 32 * mode: that epilogue mode for this call).  Returns grid * 16 + the configuration used.
+// norm-free prefill extensions of the stream-K GEMM (kernels/lsa_epi.h): rowss [M] int64 Q24 -> the output rows (bf16 /
+// RoPE epilogues) scaled by rsqrt(rowss / K + eps); with epi 3, xout bf16 [M][N] + ss_out [M] int64 Q24 (accumulated)
+// receive bf16(h) and the row sums of h^2
+LsaEpi sk_norm_epi(int64_t epi, int64_t M, int64_t N, int64_t K, const c10::optional<at::Tensor>& rowss, double eps,
+                   const c10::optional<at::Tensor>& xout, const c10::optional<at::Tensor>& ss_out) {
+  LsaEpi e{};
+  if (rowss.has_value()) {
+    need(*rowss, at::kLong, "rowss");
+    TORCH_CHECK(epi == 0 || epi == 4, "rowss: bf16 / RoPE epilogues only");
+    TORCH_CHECK(rowss->numel() >= M, "rowss too small");
+    e.rowss = reinterpret_cast<const long long*>(rowss->data_ptr<int64_t>());
+    e.inv_k = 1.0f / (float)K;
+    e.eps = (float)eps;
+  }
+  TORCH_CHECK(xout.has_value() == ss_out.has_value(), "xout and ss_out go together");
+  if (xout.has_value()) {
+    TORCH_CHECK(epi == 3, "xout / ss_out: residual epilogue only");
+    need(*xout, at::kBFloat16, "xout");
+    need(*ss_out, at::kLong, "ss_out");
+    TORCH_CHECK(xout->is_contiguous() && xout->numel() >= M * N && ss_out->numel() >= M, "xout / ss_out too small");
+    e.xout = reinterpret_cast<uint16_t*>(xout->data_ptr());
+    e.ss_out = reinterpret_cast<long long*>(ss_out->data_ptr<int64_t>());
+  }
+  return e;
+}
+
 int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, at::Tensor& ws,
-                at::Tensor& tickets, int64_t ncu, int64_t min_share, int64_t cfg) {
+                at::Tensor& tickets, int64_t ncu, int64_t min_share, int64_t cfg, const c10::optional<at::Tensor>& rowss,
+                double eps, const c10::optional<at::Tensor>& xout, const c10::optional<at::Tensor>& ss_out) {
   need(x, at::kBFloat16, "x");
   need(wf, at::kBFloat16, "wf");
   need(ws, at::kFloat, "ws");
@@ -352,9 +380,10 @@ int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor
     TORCH_CHECK(out.numel() >= (int64_t)M * (epi == 2 ? N / 2 : N), "bf16 out too small");
   }
   TORCH_CHECK(cfg >= -1 && cfg < 64, "gemm_sk: cfg");
+  const LsaEpi ne = sk_norm_epi(epi, M, N, K, rowss, eps, xout, ss_out);
   int grid = 0, used = 0;
   check(lsa_gemm_sk(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), (int)epi, ws.data_ptr<float>(),
-                    tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, &grid, &used, cur_stream()),
+                    tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, &grid, &used, &ne, cur_stream()),
         "gemm_sk");
   return (int64_t)grid * 16 + used;
 }
@@ -365,7 +394,8 @@ int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor
 int64_t gemm_sk_rope(const at::Tensor& x, const at::Tensor& wf, at::Tensor& ws, at::Tensor& tickets, int64_t ncu,
                      int64_t min_share, int64_t cfg, const at::Tensor& pos, const c10::optional<at::Tensor>& tok_seq,
                      const at::Tensor& block_tables, const at::Tensor& cos_t, const at::Tensor& sin_t,
-                     at::Tensor& q_out, at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv) {
+                     at::Tensor& q_out, at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv,
+                     const c10::optional<at::Tensor>& rowss, double eps) {
   need(x, at::kBFloat16, "x");
   need(wf, at::kBFloat16, "wf");
   need(ws, at::kFloat, "ws");
@@ -391,12 +421,13 @@ int64_t gemm_sk_rope(const at::Tensor& x, const at::Tensor& wf, at::Tensor& ws, 
   }
   TORCH_CHECK(ncu >= 8 && ncu <= 1024 && ws.numel() * 4 >= lsa_gemm_sk_ws_bytes((int)ncu) &&
                   tickets.numel() >= lsa_gemm_sk_tickets((int)ncu), "gemm_sk_rope: workspace too small");
+  const LsaEpi ne = sk_norm_epi(4, M, N, K, rowss, eps, c10::nullopt, c10::nullopt);
   int grid = 0, used = 0;
   check(lsa_gemm_sk_rope(x.data_ptr(), x.stride(0), (int)M, (int)K, wf.data_ptr(), (int)N, ws.data_ptr<float>(),
                          tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, pos.data_ptr<int>(),
                          ptr<int>(tok_seq), block_tables.data_ptr<int>(), (int)block_tables.size(1),
                          cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), q_out.data_ptr(), kc.data_ptr(),
-                         vc.data_ptr(), (int)H, (int)Hkv, &grid, &used, cur_stream()),
+                         vc.data_ptr(), (int)H, (int)Hkv, &grid, &used, &ne, cur_stream()),
         "gemm_sk_rope");
   return (int64_t)grid * 16 + used;
 }
@@ -906,7 +937,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("ws"),
-        py::arg("tickets"), py::arg("ncu"), py::arg("min_share") = 0, py::arg("cfg") = -1);
+        py::arg("tickets"), py::arg("ncu"), py::arg("min_share") = 0, py::arg("cfg") = -1, py::arg("rowss") = py::none(),
+        py::arg("eps") = 0.0, py::arg("xout") = py::none(), py::arg("ss_out") = py::none());
   m.def("gemm_sk_rope", &gemm_sk_rope);
   m.def("gemm_sk_epilogue", [](int64_t mode) { lsa_gemm_sk_epilogue((int)mode); });
   m.def("gemm_sk_nbuf", [](int64_t n) { lsa_gemm_sk_nbuf((int)n); });

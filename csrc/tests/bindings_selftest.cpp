@@ -120,10 +120,20 @@ int main() {
     auto o2 = T({300, 64}, F32), sw = T({64}, F32);
     // stream-K prefill GEMM: workspace of lsa_gemm_sk_ws_bytes(ncu) / tickets(ncu)
     auto wsk = T({2 * 8 * 65536}, F32), tks = T({32}, I32), ob = T({300, 64}, BF), wsb = T({64 * 128}, BF);
-    expect_ok("gemm_sk", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1); });
+    expect_ok("gemm_sk", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, none, 1e-5, none, none); });
     auto wsk_small = T({65536}, F32);
-    expect_reject("gemm_sk workspace", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk_small, tks, 8, 0, -1); });
-    expect_reject("gemm_sk residual dtype", [&] { gemm_sk(x, wsb, 64, ob, 3, wsk, tks, 8, 0, -1); });
+    expect_reject("gemm_sk workspace", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk_small, tks, 8, 0, -1, none, 1e-5, none, none); });
+    expect_reject("gemm_sk residual dtype", [&] { gemm_sk(x, wsb, 64, ob, 3, wsk, tks, 8, 0, -1, none, 1e-5, none, none); });
+    // norm-free prefill: rowss on bf16 / RoPE outputs; xout + ss_out with the residual epilogue
+    auto rss = T({300}, I64), rss_small = T({299}, I64), hs = T({300, 64}, F32), xs = T({300, 64}, BF);
+    expect_ok("gemm_sk rownorm", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, rss, 1e-5, none, none); });
+    expect_reject("gemm_sk rownorm too small", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, rss_small, 1e-5, none, none); });
+    expect_reject("gemm_sk rownorm on f32", [&] { gemm_sk(x, wsb, 64, hs, 1, wsk, tks, 8, 0, -1, rss, 1e-5, none, none); });
+    expect_reject("gemm_sk rownorm on SiLU", [&] { gemm_sk(x, wsb, 64, ob, 2, wsk, tks, 8, 0, -1, rss, 1e-5, none, none); });
+    expect_ok("gemm_sk residual xout", [&] { gemm_sk(x, wsb, 64, hs, 3, wsk, tks, 8, 0, -1, none, 1e-5, xs, rss); });
+    expect_reject("gemm_sk xout without ss_out", [&] { gemm_sk(x, wsb, 64, hs, 3, wsk, tks, 8, 0, -1, none, 1e-5, xs, none); });
+    expect_reject("gemm_sk xout on bf16", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, none, 1e-5, xs, rss); });
+    expect_reject("gemm_sk ss_out too small", [&] { gemm_sk(x, wsb, 64, hs, 3, wsk, tks, 8, 0, -1, none, 1e-5, xs, rss_small); });
     expect_ok("fp8_gemm_t256", [&] { fp8_gemm_t256(xq, sxq, wq, sw, 64, o2, 1, 1); });
     auto sw_small = T({32}, F32);
     expect_reject("fp8_gemm_t256 weight scales", [&] { fp8_gemm_t256(xq, sxq, wq, sw_small, 64, o2, 1, 1); });

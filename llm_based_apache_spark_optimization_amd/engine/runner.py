@@ -21,6 +21,7 @@ from __future__ import annotations
 
 
 import math
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -31,6 +32,9 @@ from ..ops import reference as ref
 
 BLOCK = 64
 REPEAT_WINDOW = 64  # repetition-penalty ring (Ollama repeat_last_n default; larger values are clamped)
+# norm-free attention input in prefill (Runner._prefill_layers), off by default: measured even with the norm launch
+# it removes (3B 2k TTFT 14.38 vs 14.34 ms, profiles/r5/prefill_norm_free_ab.txt)
+PREFILL_NORM_FREE = os.environ.get("LSA_PREFILL_NF", "0") == "1"
 
 
 class TPCommError(RuntimeError):
@@ -766,12 +770,23 @@ class ModelRunner:
         tp1 = self.tp is None or self.tp.size == 1
         res_o = tp1 and ops.res_supported(w.layers[0].wo)
         res_d = tp1 and ops.res_supported(w.layers[0].w_down)
+        # norm-free attention input (gammas folded into wqkv, the down residual epilogue on, no split-K slabs on the
+        # qkv GEMM): the down epilogue also writes bf16(h) and the Q24 row sums of h^2 and the qkv GEMM scales its
+        # output rows by the RMS -- the attention-side add_rmsnorm launch goes away.  The MLP side keeps its norm: a
+        # row scale in the gate_up SiLU epilogue cost that (spilling) kernel more than the launch it saves, and the
+        # down epilogue's extra store + row sums cost about as much as the norm (profiles/r5/prefill_norm_free_ab.txt)
+        nf = (res_d and PREFILL_NORM_FREE and all(lw.norms_folded for lw in w.layers)
+              and self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D) == 1)
+        ss = torch.zeros(len(w.layers), T, dtype=torch.int64, device=dev) if nf else None
         for l, lw in enumerate(w.layers):
+            rn_a = None
             if l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
+            elif nf:
+                rn_a = (ss[l - 1], self.eps)
             else:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, write_h=not res_d)
-            self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T)
+            self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T, rownorm=rn_a)
             if res_o:
                 ops.linear_res(attn, lw.wo, h)
                 ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, write_h=False)
@@ -788,7 +803,7 @@ class ModelRunner:
             else:
                 act = ops.linear(xn, lw.w_gate_up, "silu")
             if res_d:
-                ops.linear_res(act, lw.w_down, h)
+                ops.linear_res(act, lw.w_down, h, xn=(xn, ss[l]) if nf and l + 1 < len(w.layers) else None)
                 d_parts = None
             else:
                 d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
@@ -801,21 +816,23 @@ class ModelRunner:
         ops.add_rmsnorm(h, w.final_norm, self.eps, xl, parts=d_parts, row_idx=last, write_h=False)
         return xl
 
-    def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T):
+    def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T, rownorm=None):
         kc, vc = self.kv[l, 0], self.kv[l, 1]
         kvs = self._kv_scales(l)
         if self.on_gpu and ops.rope_fusable(lw.wqkv, self.kv_fp8, T) and bt.shape[1] > 0:
             # RoPE + the KV-cache append in the qkv GEMM's epilogue: no qkv round trip, no rope_append launch
-            ops.linear_rope(xn, lw.wqkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
+            ops.linear_rope(xn, lw.wqkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv,
+                            rownorm=rownorm)
             ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
                              work=work, cu_list=self._cu_host, kv_scales=kvs, kv8_scratch_=self._kv8_scratch)
             return
         sk_q = self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D)
         if sk_q > 1:  # small tile grid: f32 split-K slabs, summed by rope_append while it rotates
+            assert rownorm is None
             parts = ops.linear(xn, lw.wqkv, "f32", splitk=sk_q)
             ops.rope_append(parts, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)
         else:
-            ops.linear(xn, lw.wqkv, "bf16", out=qkv)
+            ops.linear(xn, lw.wqkv, "bf16", out=qkv, rownorm=rownorm)
             ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)
         ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
                          work=work, cu_list=self._cu_host, kv_scales=kvs, kv8_scratch_=self._kv8_scratch)

@@ -482,41 +482,56 @@ def sk_config(M: int, N: int, K: int, epi: str) -> int:
 
 
 def gemm_sk(x: torch.Tensor, wf: torch.Tensor, N: int, out: torch.Tensor, epi: str,
-            min_share: Optional[int] = None, cfg: Optional[int] = None) -> torch.Tensor:
+            min_share: Optional[int] = None, cfg: Optional[int] = None, rownorm=None, xn=None) -> torch.Tensor:
     """out (epi 'bf16' / 'f32' / 'silu') or h (epi 'res': h[:M] += x @ W^T) from the stream-K prefill GEMM over the
     fragment-layout bf16 weight ``wf``.  cfg: None = the measured table (``sk_config``), -1 = the kernel's
-    tile-shape cost model, else an SK_CFGS index (+ 8: whole tiles only)."""
+    tile-shape cost model, else an SK_CFGS index (+ 8: whole tiles only).  Norm-free prefill (RMSNorm gamma folded
+    into the weight): rownorm = (ss, eps) scales output row m by rsqrt(ss[m] / K + eps) ('bf16');
+    xn = (xout, ss_out) with 'res' also writes bf16(h) row-major to xout and adds the Q24 row sums of h^2 to ss_out
+    (the next GEMM's rownorm)."""
     if cfg is None:
         cfg = sk_config(x.shape[0], N, x.shape[1], epi)
     ws, tk, ncu = _sk_workspace(x.device)
-    ext().gemm_sk(x, wf, N, out, _SK_EPI[epi], ws, tk, ncu, SK_MIN_SHARE if min_share is None else min_share, cfg)
+    kw = {}
+    if rownorm is not None:
+        kw["rowss"], kw["eps"] = rownorm[0], float(rownorm[1])
+    if xn is not None:
+        kw["xout"], kw["ss_out"] = xn
+    ext().gemm_sk(x, wf, N, out, _SK_EPI[epi], ws, tk, ncu, SK_MIN_SHARE if min_share is None else min_share, cfg,
+                  **kw)
     return out
 
 
-def linear_res(x: torch.Tensor, w: PackedWeight, h: torch.Tensor) -> torch.Tensor:
+def linear_res(x: torch.Tensor, w: PackedWeight, h: torch.Tensor, xn=None) -> torch.Tensor:
     """h[:M] += x @ W^T in f32 (prefill o / down, M > 64, TP = 1): the residual add rides in the GEMM epilogue, so the
     norm after it reads h alone.  bf16 weights, or quantised ones through their bf16 dequantisation scratch; W8A8
-    fp8 prefill keeps its slab path (``res_supported``)."""
+    fp8 prefill keeps its slab path (``res_supported``).  xn = (xout, ss_out): the epilogue also writes bf16(h) and
+    the row sums of h^2 (Q24), so the next projection runs norm-free (``linear(..., rownorm=(ss_out, eps))``)."""
     M = x.shape[0]
     if not _gpu(x):
         h[:M] += ref.linear(x, w.dense(), "f32")
+        if xn is not None:
+            xn[0].view(-1)[: M * w.N].copy_(h[:M].to(torch.bfloat16).reshape(-1))
+            xn[1][:M] += ss_q24(h[:M].float().pow(2).sum(1))
         return h
     wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
-    return gemm_sk(x, wf, w.N, h, "res")
+    return gemm_sk(x, wf, w.N, h, "res", xn=xn)
 
 
 def linear_rope(x: torch.Tensor, w: PackedWeight, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc,
-                H: int, Hkv: int) -> None:
+                H: int, Hkv: int, rownorm=None) -> None:
     """The prefill qkv projection with RoPE and the paged bf16 KV-cache append fused into the GEMM epilogue (M > 64,
-    bf16 cache): q_out [T, H, 128] = rotated q, the cache gets rotated k and v at each token's slot.  CPU: the
-    unfused reference (bf16 qkv, then ``rope_append``)."""
+    bf16 cache): q_out [T, H, 128] = rotated q, the cache gets rotated k and v at each token's slot.  rownorm =
+    (ss, eps): norm-free input rows, as in ``gemm_sk``.  CPU: the unfused reference (bf16 qkv, then
+    ``rope_append``)."""
     if not _gpu(x):
-        qkv = ref.linear(x, w.dense(), "bf16")
+        qkv = linear(x, w, "bf16", rownorm=rownorm)
         return ref.rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
     wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
     ws, tk, ncu = _sk_workspace(x.device)
+    rowss, eps = (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
     ext().gemm_sk_rope(x, wf, ws, tk, ncu, SK_MIN_SHARE, sk_config(x.shape[0], w.N, x.shape[1], "bf16"), pos, tok_seq,
-                       block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
+                       block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, rowss, eps)
 
 
 def rope_fusable(w: PackedWeight, kv_fp8: bool, M: int = 1 << 30) -> bool:
@@ -566,13 +581,14 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
             return out
         return y
     if M > 64 and epi in ("bf16", "f32", "silu") and not (w.kind == "fp8" and FP8_W8A8 and K % 128 == 0):
-        # prefill: the stream-K tile kernel (epi 'f32' returns one [1, M, N] slab whatever splitk asked for)
-        assert rownorm is None and res is None, "epilogue extensions are decode-only (M <= 64)"
+        # prefill: the stream-K tile kernel (epi 'f32' returns one [1, M, N] slab whatever splitk asked for;
+        # rownorm with 'bf16': the norm-free prefill's qkv, see ``gemm_sk``)
+        assert res is None and (rownorm is None or epi == "bf16"), "prefill: rownorm on bf16 outputs only"
         if out is None:
             out = torch.empty(*((1, M, w.N) if epi == "f32" else (M, w.N // 2 if epi == "silu" else w.N)),
                               device=x.device, dtype=torch.float32 if epi == "f32" else torch.bfloat16)
         wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
-        return gemm_sk(x, wf, w.N, out, epi)
+        return gemm_sk(x, wf, w.N, out, epi, rownorm=rownorm)
     nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi, kind=w.kind)
     nb = nb0 if nb is None else nb
     if M > 64:  # prefill tile kernels: split-K (f32 slabs) only where the tile grid is small

@@ -203,6 +203,48 @@ def test_gemm_stream_k_many_partials(gpu, share, MNK):
         assert torch.equal(out, first)
 
 
+@pytest.mark.parametrize("cfg", [-1, 0, 2, 4, 5, 6, 12])
+@pytest.mark.parametrize("MNK", [(300, 3072, 1376), (2048, 6144, 1024), (1100, 800, 512)])
+@pytest.mark.parametrize("epi", ["bf16", "res"])
+def test_gemm_stream_k_norm_free(gpu, cfg, MNK, epi):
+    """Norm-free prefill epilogues (gemm_tile256.hip + lsa_epi.h): 'bf16' outputs scaled per row by
+    rsqrt(rowss / K + eps); 'res' also writes bf16(h) row-major and adds the Q24 row sums of h^2 into ss_out -- vs
+    the fp32 reference, over the direct (LDS-free) and LDS-image epilogues of several tile configurations."""
+    M, N, K = MNK
+    torch.manual_seed(M + N + K + cfg)
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    ws, tk, ncu = ops._sk_workspace(gpu)
+    yr = x.float() @ w.float().t()
+    if epi == "res":
+        h0 = torch.randn(M, N, device=gpu)
+        h = h0.clone()
+        xo = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        ss0 = torch.randint(0, 1 << 20, (M,), device=gpu, dtype=torch.int64)
+        ss = ss0.clone()
+        ops.ext().gemm_sk(x, pw.data, N, h, 3, ws, tk, ncu, 4, cfg, None, 0.0, xo, ss)
+        torch.cuda.synchronize()
+        assert int(tk.abs().sum()) == 0
+        hr = h0 + yr
+        assert _rel(h, hr) < 1e-5
+        assert torch.equal(xo, h.to(torch.bfloat16))  # bf16 of the stored h, every element written
+        ssr = ss0.double() + hr.double().pow(2).sum(1) * ops.SS_SCALE
+        assert ((ss.double() - ssr).abs() / ssr).max().item() < 1e-4
+        return
+    rss = (torch.rand(M, device=gpu) * 4 + 0.05) * K  # sum of squares of a raw row: mean square 0.05 .. 4.05
+    rq = ops.ss_q24(rss)
+    eps = 1e-5
+    r = torch.rsqrt(ops.ss_float(rq) / K + eps)[:, None]
+    out = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+    ops.ext().gemm_sk(x, pw.data, N, out, ops._SK_EPI[epi], ws, tk, ncu, 4, cfg, rq, eps, None, None)
+    torch.cuda.synchronize()
+    assert int(tk.abs().sum()) == 0
+    assert not torch.isnan(out.float()).any()
+    want = _sk_ref((x.float() * r), w, epi)
+    assert _rel(out, want) < 1e-2, (M, N, K, epi, cfg)
+
+
 @pytest.mark.parametrize("ncu", [8, 24, 40])
 @pytest.mark.parametrize("MN", [(777, 1280), (2048, 10240), (1024, 4096)])
 def test_gemm_stream_k_dp_rounds(gpu, ncu, MN):
@@ -1009,10 +1051,12 @@ def test_gemm_ragged_grid(gpu, kind, M, nb):
 @pytest.mark.parametrize("H,Hkv", [(24, 8), (32, 32), (4, 2)])
 @pytest.mark.parametrize("T", [65, 300, 1100])
 @pytest.mark.parametrize("cfg", [-1, 0, 3, 5, 8])
-def test_gemm_rope_epilogue(gpu, H, Hkv, T, cfg):
+@pytest.mark.parametrize("rownorm", [False, True])
+def test_gemm_rope_epilogue(gpu, H, Hkv, T, cfg, rownorm):
     """Prefill qkv GEMM with RoPE + the paged KV-cache append in its epilogue (ops.linear_rope / EPI_ROPE) vs the
     fp32 product rotated by the reference: q_out, and every appended cache row at its (block, kv-head, slot) --
-    two sequences packed, the second starting mid-block (chunked-prefill continuation), scattered block tables."""
+    two sequences packed, the second starting mid-block (chunked-prefill continuation), scattered block tables.
+    rownorm: the norm-free prefill's per-row RMS scale applied before the rotation."""
     K, D = 512, 128
     N = (H + 2 * Hkv) * D
     torch.manual_seed(T + H + cfg)
@@ -1030,11 +1074,14 @@ def test_gemm_rope_epilogue(gpu, H, Hkv, T, cfg):
     vc = torch.zeros_like(kc)
     q = torch.zeros(T, H, D, device=gpu, dtype=torch.bfloat16)
     ws, tk, ncu = ops._sk_workspace(gpu)
+    rq = ops.ss_q24((torch.rand(T, device=gpu) * 4 + 0.05) * K) if rownorm else None
     ops.ext().gemm_sk_rope(x, pw.data, ws, tk, ncu, 4, cfg, pos.to(gpu), tok_seq.to(gpu), bt.to(gpu), cos.to(gpu),
-                           sin.to(gpu), q, kc, vc, H, Hkv)
+                           sin.to(gpu), q, kc, vc, H, Hkv, rq, 1e-5)
     torch.cuda.synchronize()
     assert int(tk.abs().sum()) == 0
     qkv = x.float().cpu() @ w.float().cpu().t()
+    if rownorm:
+        qkv *= torch.rsqrt(ops.ss_float(rq).cpu() / K + 1e-5)[:, None]
     q_r = torch.zeros(T, H, D, dtype=torch.bfloat16)
     kc_r, vc_r = torch.zeros(nblk, Hkv, 64, D, dtype=torch.bfloat16), torch.zeros(nblk, Hkv, 64, D, dtype=torch.bfloat16)
     ref.rope_append(qkv, pos, tok_seq, bt, cos, sin, q_r, kc_r, vc_r, H, Hkv)
