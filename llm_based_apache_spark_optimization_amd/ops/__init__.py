@@ -530,8 +530,18 @@ def linear_rope(x: torch.Tensor, w: PackedWeight, pos, tok_seq, block_tables, co
     wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
     ws, tk, ncu = _sk_workspace(x.device)
     rowss, eps = (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
-    ext().gemm_sk_rope(x, wf, ws, tk, ncu, SK_MIN_SHARE, sk_config(x.shape[0], w.N, x.shape[1], "bf16"), pos, tok_seq,
+    ext().gemm_sk_rope(x, wf, ws, tk, ncu, SK_MIN_SHARE, rope_config(x.shape[0], w.N, x.shape[1]), pos, tok_seq,
                        block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, rowss, eps)
+
+
+def rope_config(M: int, N: int, K: int) -> int:
+    """Tile configuration of the RoPE-epilogue qkv GEMM: the table's measured "rope" entry (scripts/rope_cfg_sweep.py,
+    profiles/r5/rope_cfg_sweep_mi355x.jsonl: the bf16 entry's 192-column tile widened to 256 columns ran the 3B qkv at
+    4096 rows in 185 us vs 147.5 us on 128 x 256), else the bf16 entry."""
+    sk_config(M, N, K, "bf16")  # loads the table
+    b = min(_SK_BUCKETS, key=lambda c: abs(math.log2(c) - math.log2(max(M, 1))))
+    e = (_sk_tuning or {}).get(f"{N}x{K}:rope:m{b}")
+    return int(e["cfg"]) if e is not None else sk_config(M, N, K, "bf16")
 
 
 def rope_fusable(w: PackedWeight, kv_fp8: bool, M: int = 1 << 30) -> bool:
