@@ -160,6 +160,32 @@ def explain_round(device, prompt_len: int = 2048, new_tokens: int = 128) -> dict
     return out
 
 
+def comm_record(tpg, world: int, tp: int, device) -> dict:
+    """Self-verifying record of how the ranks communicated (collective over the world): every rank's device, and
+    per TP group the backend, ranks per group, whether the one-shot IPC all-reduce ran (else why not) and the
+    issued collectives per path -- so a scaling run shows N ranks on N distinct GPUs and which TP path it timed."""
+    mine = {"rank": dist.get_rank(), "device": str(device),
+            "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES"),
+            "tp": tpg.describe() if tpg is not None else None}
+    recs: list = [None] * world
+    dist.all_gather_object(recs, mine)
+    devs = [r["device"] for r in recs]
+    out = {"world": world, "tp": tp, "backend": dist.get_backend(), "device_per_rank": devs,
+           "distinct_devices": len(set(devs))}
+    if tp > 1:
+        groups = [r["tp"] for r in recs]
+        calls: dict = {}
+        for g in groups:
+            for k, v in g["calls"].items():
+                calls[k] = calls.get(k, 0) + v
+        out.update({"tp_backend": groups[0]["backend"], "group_ranks": sorted({g["group_ranks"] for g in groups}),
+                    "ipc_allreduce": all(g["ipc_allreduce"] for g in groups),
+                    "ipc_bf16_payload": groups[0]["ipc_bf16_payload"],
+                    "ipc_fallback": sorted({g["ipc_fallback"] for g in groups if g["ipc_fallback"]}) or None,
+                    "calls_all_ranks": dict(sorted(calls.items()))})
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -261,6 +287,7 @@ def main() -> int:
     ms_step = 1000.0 * elapsed / args.steps
     # GPU time per decode step from hipEvents around each decode run (excludes the prefill's kernels, which the
     # host-side decode_s also waits for: its first sync lands after the asynchronously launched prefill)
+    tp_comm = comm_record(tpg, world, tp, device) if world > 1 else None
     decode_ms_tok = 1000.0 * eng.stats["decode_s"] / max(1, eng.stats["decode_steps"])
     decode_dev_ms = 1000.0 * eng.stats["decode_device_s"] / max(1, eng.stats["decode_steps"])
     extras = {}
@@ -307,6 +334,7 @@ def main() -> int:
             "decode_device_ms_per_step": round(decode_dev_ms, 3),
             "per_gpu_tokens_per_sec": round(value / world, 2),
             "numerics": numerics,
+            **({"tp_comm": tp_comm} if tp_comm is not None else {}),
             **({"overrides": overrides} if overrides else {}),
             **extras,
         }

@@ -42,7 +42,9 @@ int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* bl
                     void* out, float* opart, float* mlpart, int* counters, int xf_mt, const float* qkv_parts, int nparts,
                     long part_stride,
                     const float* cos_t, const float* sin_t, const float* ks, const float* vs, void* out_s8,
-                    hipStream_t s);
+                    const long long* rowss, float inv_k, float eps, hipStream_t s);
+int lsa_gemm_rr(int K, const void* Wf, int N, void* out, int epi, int nb, int splitk, int waves, int div,
+                const LsaRr* rr, hipStream_t stream);
 int lsa_kv8_dequant(const void* kc, const void* vc, const float* ks, const float* vs, const int* block_tables,
                     int max_blocks, const int* ctx_lens, int nseq, int Hkv, int mb, void* ko, void* vo, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
@@ -220,6 +222,44 @@ void gemm(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out,
   check(lsa_gemm_cfg(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), epi, nb, splitk, waves, div,
                      xlds, cur_stream()),
         "gemm");
+}
+
+// Batch-1 decode GEMM with the residual-reduce prologue (kernels/gemm.hip, lsa_epi.h LsaRr): X = h + sum_s parts[s]
+// (h f32 [K]; parts f32 [np, 1, K] split-K slabs), h_out = X.  epi 1: f32 slabs [splitk, 1, N], the column-0
+// workgroups add each K slice's sum of X^2 (Q24) into ss_out[0] (the slab consumer applies the row scale);
+// epi 2: SiLU(gate) * up bf16 [1, N / 2] with the RMS row scale from the workgroup's own full-row sum (splitk 1).
+void gemm_rr(const at::Tensor& h, const at::Tensor& parts, at::Tensor& h_out, const at::Tensor& wf, int64_t N,
+             at::Tensor& out, int64_t epi, int64_t nb, int64_t splitk, int64_t waves, int64_t div,
+             const c10::optional<at::Tensor>& ss_out, double eps) {
+  need(h, at::kFloat, "h");
+  need(h_out, at::kFloat, "h_out");
+  need(parts, at::kFloat, "parts");
+  need(wf, at::kBFloat16, "wf");
+  const int64_t K = h.numel();
+  TORCH_CHECK(h.is_contiguous() && h_out.is_contiguous() && h_out.numel() >= K, "gemm_rr: h / h_out contiguous [K]");
+  TORCH_CHECK(h.data_ptr() != h_out.data_ptr(), "gemm_rr: h_out must not alias h (other workgroups still read h)");
+  TORCH_CHECK(parts.dim() == 3 && parts.size(1) == 1 && parts.size(2) == K && parts.stride(2) == 1 &&
+                  parts.stride(1) == K, "gemm_rr: parts must be [np, 1, K] slabs");
+  TORCH_CHECK(wf.numel() == N * K, "gemm_rr: weight numel mismatch");
+  TORCH_CHECK(epi == 1 || epi == 2, "gemm_rr: f32 slabs or silu");
+  check_out(epi, out, splitk, 1, N, 0);
+  LsaRr rr{};
+  rr.h = h.data_ptr<float>();
+  rr.parts = parts.data_ptr<float>();
+  rr.pstride = parts.stride(0);
+  rr.np = (int)parts.size(0);
+  rr.h_out = h_out.data_ptr<float>();
+  rr.local = epi == 2 ? 1 : 0;
+  rr.inv_k = 1.0f / (float)K;
+  rr.eps = (float)eps;
+  if (epi == 1) {
+    TORCH_CHECK(ss_out.has_value(), "gemm_rr: f32 slabs need ss_out");
+    need(*ss_out, at::kLong, "ss_out");
+    rr.ss_out = reinterpret_cast<long long*>(ss_out->data_ptr<int64_t>());
+  }
+  check(lsa_gemm_rr((int)K, wf.data_ptr(), (int)N, out.data_ptr(), (int)epi, (int)nb, (int)splitk, (int)waves, (int)div,
+                    &rr, cur_stream()),
+        "gemm_rr");
 }
 
 // same, with X in the fragment-major activation layout (ops.to_xfrag): xf holds ceil(M/16) row tiles
@@ -627,8 +667,14 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                  at::Tensor& out, at::Tensor& opart, at::Tensor& mlpart, at::Tensor& counters, int64_t xf_mt,
                  const c10::optional<at::Tensor>& qkv_parts, const c10::optional<at::Tensor>& cos_t,
                  const c10::optional<at::Tensor>& sin_t, int64_t unsplit_max, const c10::optional<at::Tensor>& ks,
-                 const c10::optional<at::Tensor>& vs, const c10::optional<at::Tensor>& out_s8 = c10::nullopt) {
+                 const c10::optional<at::Tensor>& vs, const c10::optional<at::Tensor>& out_s8 = c10::nullopt,
+                 const c10::optional<at::Tensor>& rowss = c10::nullopt, double eps = 1e-5, int64_t hidden = 0) {
   need(q, at::kBFloat16, "q");
+  if (rowss.has_value()) {  // residual-reduce decode step: the slabs are the projection of un-normalised rows
+    TORCH_CHECK(qkv_parts.has_value() && hidden > 0, "attn_decode rowss: needs qkv_parts and the hidden size");
+    need(*rowss, at::kLong, "rowss");
+    TORCH_CHECK(rowss->numel() >= pos.size(0), "attn_decode: rowss too small");
+  }
   check_cache(kc, vc, ks, vs);
   need(pos, at::kInt, "pos");
   need(block_tables, at::kInt, "block_tables");
@@ -670,7 +716,9 @@ void attn_decode(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc
                         ptr<const float>(qkv_parts), qkv_parts.has_value() ? qkv_parts->size(0) : 0,
                         qkv_parts.has_value() ? qkv_parts->stride(0) : 0, ptr<const float>(cos_t),
                         ptr<const float>(sin_t), ptr<const float>(ks), ptr<const float>(vs),
-                        out_s8.has_value() ? out_s8->data_ptr() : nullptr, cur_stream()),
+                        out_s8.has_value() ? out_s8->data_ptr() : nullptr,
+                        rowss.has_value() ? reinterpret_cast<const long long*>(rowss->data_ptr<int64_t>()) : nullptr,
+                        rowss.has_value() ? 1.0f / (float)hidden : 0.f, (float)eps, cur_stream()),
         "attn_decode");
 }
 
@@ -985,7 +1033,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("opart"), py::arg("mlpart"), py::arg("counters"), py::arg("xf_mt") = 0,
         py::arg("qkv_parts") = py::none(),
         py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4,
-        py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("out_s8") = py::none());
+        py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("out_s8") = py::none(),
+        py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("hidden") = 0);
+  m.def("gemm_rr", &gemm_rr, py::arg("h"), py::arg("parts"), py::arg("h_out"), py::arg("wf"), py::arg("N"),
+        py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves"), py::arg("div"),
+        py::arg("ss_out") = py::none(), py::arg("eps") = 1e-5);
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
         py::arg("out"), py::arg("rows32") = 0, py::arg("opart") = py::none(), py::arg("mlpart") = py::none(),

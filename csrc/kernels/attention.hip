@@ -56,6 +56,10 @@ struct RopeArgs {
   uint16_t* vc;
   float* ks;           // fp8 cache: per-(token, kv-head) scales (writable aliases of ksc / vsc)
   float* vs;
+  const long long* rowss;  // or null: the slabs are the QKV projection of UN-normalised rows (the residual-reduce
+                           // decode step, gemm.hip RR); row b's q / k / v are scaled by rsqrt(rowss[b] inv_k + eps)
+  float inv_k;
+  float eps;
 };
 
 // WV = waves per workgroup: 8 for G <= 3 (two keys per lane group per block -> half the K/V registers,
@@ -220,6 +224,7 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
       const float4 a1 = *reinterpret_cast<const float4*>(row + off + 4);
       xq[0] = a0.x; xq[1] = a0.y; xq[2] = a0.z; xq[3] = a0.w; xq[4] = a1.x; xq[5] = a1.y; xq[6] = a1.z; xq[7] = a1.w;
       const int np = ROPE > 0 ? ROPE : ra.nparts;
+      const long long ssq = ra.rowss ? ra.rowss[b] : 0;
 #pragma unroll
       for (int sp = 1; sp < np; ++sp) {
         const float* r2 = row + sp * ra.part_stride + off;
@@ -227,6 +232,11 @@ __attribute__((amdgpu_waves_per_eu(G == 1 && WV == 8 ? (SB ? 8 : (KV8 ? LSA_ATTN
         const float4 b1 = *reinterpret_cast<const float4*>(r2 + 4);
         xq[0] += b0.x; xq[1] += b0.y; xq[2] += b0.z; xq[3] += b0.w;
         xq[4] += b1.x; xq[5] += b1.y; xq[6] += b1.z; xq[7] += b1.w;
+      }
+      if (ra.rowss) {  // the RMS row scale of the residual-reduce step (linear: before RoPE, like the GEMM's)
+        const float rs = rsqrtf((float)ssq * (1.0f / LSA_Q24) * ra.inv_k + ra.eps);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xq[j] *= rs;
       }
     }
   }
@@ -595,7 +605,9 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
                                int unsplit_max, void* out, float* opart, float* mlpart, int* counters, int xf_mt,
                                const float* qkv_parts, int nparts,
                                long part_stride, const float* cos_t, const float* sin_t, const float* ks,
-                               const float* vs, void* out_s8, hipStream_t s) {
+                               const float* vs, void* out_s8, const long long* rowss, float inv_k, float eps,
+                               hipStream_t s) {
+  if (rowss && !qkv_parts) return -7;  // the row scale applies to the fused-RoPE slabs
   if (H % Hkv) return -1;
   if (xf_mt && B > 16 * xf_mt) return -4;
   if (out_s8 && !xf_mt) return -6;  // the e4m3 output lives in the xf8 layout
@@ -609,7 +621,7 @@ extern "C" int lsa_attn_decode(const void* q, const void* kc, const void* vc, co
   const uint16_t* vv = reinterpret_cast<const uint16_t*>(vc);
   uint16_t* oo = reinterpret_cast<uint16_t*>(out);
   const RopeArgs ra{qkv_parts, (size_t)part_stride, nparts, cos_t, sin_t, const_cast<uint16_t*>(kk),
-                    const_cast<uint16_t*>(vv), const_cast<float*>(ks), const_cast<float*>(vs)};
+                    const_cast<uint16_t*>(vv), const_cast<float*>(ks), const_cast<float*>(vs), rowss, inv_k, eps};
 #define LSA_ADL(GV, RP, WV, KV8, SB)                                                                              \
   hipLaunchKernelGGL((attn_decode_kernel<GV, RP, WV, KV8, SB>), grid, dim3(64 * (WV)), 0, s, qq, kk, vv, ks, vs,     \
                      block_tables, max_blocks, pos, Hkv, sl2, chunk_blocks, nsplit, unsplit_max, oo, opart, mlpart,  \

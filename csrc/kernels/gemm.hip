@@ -60,11 +60,19 @@ struct SkinnyCfg {
 // XF: X is in the fragment-major activation layout Xf[k/32][MT][64 lanes][8 bf16] (ops.to_xfrag,
 // written directly by the producing kernels in the decode path), so an activation fragment is one
 // lane-linear 1 KiB load (8 full lines) instead of 16 half-used row segments.
-template <int MT, int NB, int EPI, int WAVES, int DIV = 1, bool XF = false>
+//
+// RR > 0 (batch 1, MT = 1): the residual-reduce prologue of lsa_epi.h LsaRr, RR = the most split-K slabs it sums
+// (the loads are clamped to slab np - 1 and masked, so every slab load of a lane leaves before the first add).
+// The workgroup's X slice (<= RR_KMAX values) is formed once into LDS as bf16 and the k-step fragments are read
+// back from there (16 lanes of a row group read one address: broadcast, conflict-free).  Replaces the residual-add
+// launch between the row-parallel projection and this GEMM (one kernel boundary less per layer side).
+#define RR_KMAX 8192
+template <int MT, int NB, int EPI, int WAVES, int DIV = 1, bool XF = false, int RR = 0>
 __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t* __restrict__ X, int ldx, int M,
                                                                  int KB, const uint4* __restrict__ Wf,
                                                                  void* __restrict__ out, int ldo,
-                                                                 int kb_per_split, LsaEpi ep) {
+                                                                 int kb_per_split, LsaEpi ep, LsaRr rr) {
+  static_assert(RR == 0 || (MT == 1 && !XF && EPI != EPI_RES), "residual-reduce prologue: batch 1, row-major");
   constexpr int U = SkinnyCfg<MT, NB, DIV>::U;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -111,6 +119,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       for (int i = 0; i < NB; ++i) wr[u][i] = ldg_nt(wp[i] + (size_t)kk * 64);
     }
   };
+  // RR: the workgroup's X slice as bf16 (k - kbA * 32), filled by the prologue below
+  __shared__ __attribute__((aligned(16))) uint4 xs[RR ? RR_KMAX / 8 : 1];
   auto xload = [&](uint4 (&xr)[U][MT], int c) {
     const int kb = kbA + c * U;
 #pragma unroll
@@ -118,7 +128,9 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       const int kk = min(kb + u, kbB - 1);
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
-        if constexpr (XF) {
+        if constexpr (RR > 0) {
+          xr[u][j] = xs[(kk - kbA) * 4 + g];
+        } else if constexpr (XF) {
           xr[u][j] = *reinterpret_cast<const uint4*>(xp[j] + (size_t)kk * MT * 512);
         } else {
           const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff[j] + (uint32_t)kk * 64u, 0, 0);
@@ -147,9 +159,56 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
     }
   };
 
+  // RR prologue: X = h + sum_s parts[s] over this split's K slice -> LDS (bf16) and, from the f32 values, the
+  // slice's sum of squares.  The first weight chunk is requested before it (it does not depend on X), so the
+  // prologue's L2 round trip overlaps the weight stream's HBM latency.
+  float rr_scale = 1.f;
+  uint4 wA[U][NB], xA[U][MT], wB[U][NB], xB[U][MT];
+  if constexpr (RR > 0) {
+    if (n_it > 0) wload(wA, w);
+    __shared__ float rr_red[WAVES];
+    const int k0 = kbA * 32, n8 = nk * 4;  // 8-value groups of the slice
+    const bool wr_h = blockIdx.x == 0;
+    float ssl = 0.f;
+    for (int i = threadIdx.x; i < n8; i += 64 * WAVES) {
+      const size_t e = (size_t)k0 + 8 * i;
+      float4 a[RR + 1][2];
+      a[0][0] = *reinterpret_cast<const float4*>(rr.h + e);
+      a[0][1] = *reinterpret_cast<const float4*>(rr.h + e + 4);
+#pragma unroll
+      for (int s = 0; s < RR; ++s) {
+        const float* p = rr.parts + (size_t)min(s, rr.np - 1) * rr.pstride + e;
+        a[s + 1][0] = *reinterpret_cast<const float4*>(p);
+        a[s + 1][1] = *reinterpret_cast<const float4*>(p + 4);
+      }
+      float v[8] = {a[0][0].x, a[0][0].y, a[0][0].z, a[0][0].w, a[0][1].x, a[0][1].y, a[0][1].z, a[0][1].w};
+#pragma unroll
+      for (int s = 0; s < RR; ++s) {
+        const float on = s < rr.np ? 1.f : 0.f;
+        v[0] += on * a[s + 1][0].x; v[1] += on * a[s + 1][0].y; v[2] += on * a[s + 1][0].z; v[3] += on * a[s + 1][0].w;
+        v[4] += on * a[s + 1][1].x; v[5] += on * a[s + 1][1].y; v[6] += on * a[s + 1][1].z; v[7] += on * a[s + 1][1].w;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ssl += v[j] * v[j];
+      if (wr_h) {
+        *reinterpret_cast<float4*>(rr.h_out + e) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(rr.h_out + e + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+      xs[i] = pack8(v);
+    }
+    ssl = wave_sum(ssl);
+    if (lane == 0) rr_red[w] = ssl;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) tot += rr_red[ww];
+    if (rr.local) rr_scale = rsqrtf(tot * rr.inv_k + rr.eps);
+    else if (wr_h && threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(rr.ss_out), (unsigned long long)ss_to_q24(tot));
+    if (n_it > 0) xload(xA, w);
+  } else {
+    if (n_it > 0) load(wA, xA, w);
+  }
   if (n_it > 0) {
-    uint4 wA[U][NB], xA[U][MT], wB[U][NB], xB[U][MT];
-    load(wA, xA, w);
     int i = 0;
     // sched_barrier(0) pins the issue order: the next chunk's loads all leave before this chunk's
     // MFMAs (hipcc otherwise interleaves them and keeps only ~8 loads in flight)
@@ -192,7 +251,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       const int m = j * 16 + (l & 15);
       if (m < M && 2 * p < cnt) {
         const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
-        const float sc = epi_row_scale(ep, m);
+        const float sc = epi_row_scale(ep, m) * rr_scale;
         f32x4_t v;
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = silu(gs[q] * sc) * (us[q] * sc);
@@ -247,7 +306,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_skinny_kernel(const uint16_t*
       for (int ww = 1; ww < WAVES; ++ww) s += red[ww][t][l];
       const int m = j * 16 + (l & 15);
       if (m < M && i < cnt) {
-        s *= epi_row_scale(ep, m);
+        s *= epi_row_scale(ep, m) * rr_scale;
         const int n = (nb0 + i) * 16 + 4 * (l >> 4);
         if constexpr (EPI == EPI_RES) atomicAdd(&ssw[m], (unsigned long long)ss_to_q24(epi_residual4(ep, m, n, s)));
         else store4<EPI>(out, ldo, slab, m, n, s);
@@ -270,15 +329,16 @@ static thread_local int g_skinny_waves = 4;
 static thread_local int g_skinny_div = 4;
 
 static thread_local LsaEpi g_epi = {};
+static thread_local LsaRr g_rr = {};
 
-template <int MT, int NB, int EPI, bool XF>
+template <int MT, int NB, int EPI, bool XF, int RR = 0>
 static void launch_skinny_x(const uint16_t* X, int ldx, int M, int KB, const uint4* Wf, int NBtot, void* out,
                             int ldo, int splitk, hipStream_t s) {
   const int kbps = (KB + splitk - 1) / splitk;
   dim3 grid((NBtot + NB - 1) / NB, splitk);  // ragged when NB does not divide NBtot (kernel deals the blocks)
 #define LSA_SKL(WV, DV) \
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF>), grid, dim3(64 * WV), 0, s, X, \
-                     ldx, M, KB, Wf, out, ldo, kbps, g_epi)
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NB, EPI, WV, DV, XF, RR>), grid, dim3(64 * WV), 0, s, X, \
+                     ldx, M, KB, Wf, out, ldo, kbps, g_epi, g_rr)
   if constexpr (NB >= 6) {
     // wide n-groups (one activation fragment feeds NB weight fragments): 4 waves only, the cross-wave
     // reduction buffer is WAVES * NB * MT KiB
@@ -378,5 +438,56 @@ extern "C" int lsa_gemm_ex(const void* X, int ldx, int M, int K, const void* Wf,
   } else {
     return -9;  // M > 64: the stream-K prefill kernel (gemm_tile256.hip lsa_gemm_sk)
   }
+  return (int)hipGetLastError();
+}
+
+// Batch-1 decode GEMM with the residual-reduce prologue (lsa_epi.h LsaRr; kernel template RR): X = rr.h + sum of
+// rr.np f32 slabs, formed per split K slice in LDS.  epi: EPI_F32 (split-K slabs, rr.local = 0: the row scale is
+// left to the slab consumer, which reads rr.ss_out) or EPI_SILU (splitk 1, rr.local = 1: the workgroup's full-row
+// sum of squares scales the gate / up rows before SiLU).
+template <int NB, int EPI, int RR>
+static void launch_rr_nb(int KB, const uint4* Wf, int NBtot, void* out, int ldo, int splitk, hipStream_t s) {
+  launch_skinny_x<1, NB, EPI, false, RR>(nullptr, 0, 1, KB, Wf, NBtot, out, ldo, splitk, s);
+}
+
+template <int EPI, int RR>
+static int launch_rr_e(int KB, const uint4* Wf, int NBtot, void* out, int ldo, int nb, int splitk, hipStream_t s) {
+  if constexpr (EPI != EPI_SILU) {
+    if (nb == 1) {
+      launch_rr_nb<1, EPI, RR>(KB, Wf, NBtot, out, ldo, splitk, s);
+      return 0;
+    }
+  }
+  if (nb == 2) launch_rr_nb<2, EPI, RR>(KB, Wf, NBtot, out, ldo, splitk, s);
+  else if (nb == 4) launch_rr_nb<4, EPI, RR>(KB, Wf, NBtot, out, ldo, splitk, s);
+  else return -2;
+  return 0;
+}
+
+extern "C" int lsa_gemm_rr(int K, const void* Wf, int N, void* out, int epi, int nb, int splitk, int waves, int div,
+                           const LsaRr* rr, hipStream_t stream) {
+  if (!rr || !rr->h || !rr->h_out || rr->h == rr->h_out || rr->np < 1 || rr->np > 4 || !rr->parts)
+    return -1;
+  if (K % 32 != 0 || N % 16 != 0) return -1;
+  if (splitk < 1) splitk = 1;
+  const int KB = K / 32, NBtot = N / 16;
+  if ((KB + splitk - 1) / splitk * 32 > RR_KMAX) return -3;  // the K slice must fit the LDS image
+  if (epi == EPI_SILU ? (splitk != 1 || !rr->local || nb < 2) : (epi != EPI_F32 || rr->local || !rr->ss_out)) return -4;
+  if (NBtot % nb) return -2;
+  g_epi = LsaEpi{};
+  g_rr = *rr;
+  g_skinny_waves = waves == 8 ? 8 : 4;
+  g_skinny_div = (div == 1 || div == 2) ? div : 4;
+  const uint4* w = reinterpret_cast<const uint4*>(Wf);
+  const int ldo = epi == EPI_SILU ? N / 2 : N;
+  int rc;
+  if (epi == EPI_SILU)
+    rc = rr->np <= 2 ? launch_rr_e<EPI_SILU, 2>(KB, w, NBtot, out, ldo, nb, 1, stream)
+                     : launch_rr_e<EPI_SILU, 4>(KB, w, NBtot, out, ldo, nb, 1, stream);
+  else
+    rc = rr->np <= 2 ? launch_rr_e<EPI_F32, 2>(KB, w, NBtot, out, ldo, nb, splitk, stream)
+                     : launch_rr_e<EPI_F32, 4>(KB, w, NBtot, out, ldo, nb, splitk, stream);
+  g_rr = LsaRr{};
+  if (rc) return rc;
   return (int)hipGetLastError();
 }

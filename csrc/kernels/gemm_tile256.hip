@@ -158,7 +158,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF % NW == 0 && C::WF0 % NW == 0 && C::WF1 % NW == 0 &&
                     C::XF <= 32 && C::WF0 <= 32 && NBUF * C::BUFF * (NW == 4 ? 2 : 1) <= 160, "tile geometry");
   static_assert(EPI != EPI_SILU || WN % 2 == 0, "SiLU pairs (gate, up) n-blocks inside one wave");
-  static_assert(EPI != EPI_ROPE || WN % 2 == 0, "RoPE tiles hold whole 128-column heads");
+  static_assert(EPI != EPI_ROPE || C::NBT % 8 == 0, "RoPE tiles hold whole 128-column heads");
   static_assert(NBUF == 2 || (NBUF == 3 && C::CAN3), "K-tile buffers");
   __shared__ __attribute__((aligned(16))) uint4 lds[NBUF * C::BUFF * 64];
   const int lane = threadIdx.x & 63;
@@ -840,7 +840,7 @@ static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const u
         return -2;
       }
     case EPI_ROPE:
-      if constexpr (WN % 2 == 0) {
+      if constexpr (C::NBT % 8 == 0) {
         LSA_SKL(EPI_ROPE);
         break;
       } else {
@@ -881,6 +881,9 @@ static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, in
     float best = 3.0e38f;
     for (int i = 0; i < ncfg; ++i) {
       if (even_wn && kSkCfgs[i].wn % 2) continue;
+      // RoPE: a tile must hold whole 128-column heads (8 n-blocks), or the rotate-half partner of a column lies
+      // outside the tile's LDS image (the 4-wave 128 x 192 tile has 12 n-blocks)
+      if (epi == EPI_ROPE && ((kSkCfgs[i].nw / 2) * kSkCfgs[i].wn) % 8) continue;
       bool u = false;
       const float t = sk_cfg_time(kSkCfgs[i], M, KB, NBtot, ncu, &u);
       if (t < best) best = t, cfg = i, sk = u;

@@ -145,6 +145,14 @@ __global__ __launch_bounds__(256) void topk_partial_kernel(const float* __restri
   for (int i = threadIdx.x; i < LSA_TOPK; i += 256) cand[((size_t)b * nch + c) * LSA_TOPK + i] = a[i];
 }
 
+// splitmix64 finalizer of a stream key
+__device__ __forceinline__ unsigned long long lsa_key_mix(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
 __device__ __forceinline__ float uniform01(unsigned long long seed, unsigned long long ctr) {
   unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (ctr + 1);
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -207,9 +215,12 @@ __global__ __launch_bounds__(1024) void sample_commit_kernel(const unsigned long
       const float x = __shfl_up(cumk, o, 64);
       if (i >= o) cumk += x;
     }
-    // draw g of a request depends on seed + g only (as ops/reference.py): a preempted request re-admitted with
-    // seed + len(resumed) continues the same stream, whatever slot it lands in
-    const float u = uniform01(seeds[b] + (unsigned long long)st.gen_len[b], 0ull);
+    // draw g of a request: the request's seed is the stream KEY (scrambled, so seeds 0, 1, 2, ... give unrelated
+    // streams) and the draw index the counter; seeds[b] packs the key (low 40 bits) with a counter offset (high 24
+    // bits: the tokens a preempted request already generated, so its re-admission continues the same stream
+    // whatever slot it lands in).  ops/reference.py draw_seed is the host twin.
+    const unsigned long long sv = seeds[b];
+    const float u = uniform01(lsa_key_mix(sv & 0xFFFFFFFFFFull), (sv >> 40) + (unsigned long long)st.gen_len[b]);
     // first kept index whose cumulative mass exceeds u (fallback: last kept index)
     int first_hit = (keep && u < cumk) ? i : 64;
     int last_kept = keep ? i : -1;

@@ -27,6 +27,7 @@ import torch
 
 from ..models.templates import STOP_STRINGS, apply_stops, render
 from ..models.tokenizer import tokenizer_for
+from ..ops.reference import pack_seed
 from ..runtime import native
 from ..utils import tracing
 from ..utils.metrics import REGISTRY, TOKEN_BUCKETS
@@ -222,9 +223,9 @@ class LLMEngine:
                 self._slot_owner[slot] = rid
                 sp = req.params
                 # a re-admitted (preempted) request continues its random stream where it stopped: the sampler draws
-                # token g from seed + g (ops/reference.py sample_commit, sampling.hip), and this incarnation's g
-                # restarts at 0 after len(resumed) tokens
-                seed = (sp.seed if sp.seed is not None else (rid * 7919 + 17)) + len(req.resumed)
+                # token g from the stream keyed by the seed at counter g + offset (ops/reference.py draw_seed,
+                # sampling.hip), and this incarnation's g restarts at 0 after len(resumed) tokens
+                seed = pack_seed(sp.seed if sp.seed is not None else (rid * 7919 + 17), len(req.resumed))
                 entries.append(dict(slot=slot, blocks=self.sched.block_table(rid), limit=sp.max_tokens,
                                     temperature=sp.temperature, top_k=sp.top_k, top_p=sp.top_p, seed=seed,
                                     eos_on=not sp.ignore_eos, repeat_penalty=sp.repeat_penalty,

@@ -35,6 +35,8 @@ REPEAT_WINDOW = 64  # repetition-penalty ring (Ollama repeat_last_n default; lar
 # norm-free attention input in prefill (Runner._prefill_layers), off by default: measured even with the norm launch
 # it removes (3B 2k TTFT 14.38 vs 14.34 ms, profiles/r5/prefill_norm_free_ab.txt)
 PREFILL_NORM_FREE = os.environ.get("LSA_PREFILL_NF", "0") == "1"
+# batch-1 decode with the residual add folded into the next GEMM's prologue (ModelRunner._decode_step_rr)
+RR_DECODE = os.environ.get("LSA_RR", "1") != "0"
 
 
 class TPCommError(RuntimeError):
@@ -55,6 +57,10 @@ class ModelRunner:
         # Megatron sequence parallelism for TP prefill (SURVEY.md §2.6 P-SP): reduce-scatter the row-parallel
         # outputs, residual + RMSNorm on T/tp rows, all-gather the bf16 normalised activations
         self.seq_parallel = True if seq_parallel is None else seq_parallel
+        # SP prefill collective payload: the row-parallel GEMMs write bf16 and the reduce-scatter moves bf16 (half the
+        # xGMI bytes of f32; the TP partial sums are rounded once to bf16 before the sum, as the decode all-reduce's
+        # bf16 payload does); False keeps f32 slabs
+        self.sp_bf16 = os.environ.get("LSA_SP_BF16", "1") != "0"
         self.sp_min_tokens = 256 if sp_min_tokens is None else sp_min_tokens
         # decode RoPE + KV append inside the attention kernel (fuse_rope=False restores the separate launch)
         self.fuse_rope = True if fuse_rope is None else fuse_rope
@@ -213,6 +219,12 @@ class ModelRunner:
         # Under TP the residual add rides in the one-shot all-reduce (TPGroup.reduce_add: the sum over ranks, h +=,
         # bf16 / fragment-major xn and the row sums in one launch), so a TP layer issues as many launches as TP = 1.
         self.wide_norm = all(lw.norms_folded for lw in weights.layers)
+        # batch-1 residual-reduce step (_decode_step_rr): the qkv and gate_up GEMMs fold the residual add of the
+        # previous row-parallel projection's slabs into their prologue (ops.linear_rr), so a layer issues 5 launches
+        # (qkv, attention, o, gate_up, down) and no residual-add launch; TP = 1, bf16 weights, gammas folded
+        lw0 = weights.layers[0]
+        self.rr_decode = (RR_DECODE and tps == 1 and self.wide_norm and ops.rr_supported(lw0.wqkv, self.d) and ops.rr_supported(lw0.w_gate_up, self.d))
+        self.h_alt = torch.zeros(1, self.d, **f32)  # the residual stream's second buffer (h_out never aliases h)
         self.graphs: dict = {}
         self._pending_bt: dict = {}  # slot -> block-table row of a prompt still being prefilled in chunks
         if self.tp is not None and self.tp.size > 1 and self.on_gpu:
@@ -301,6 +313,8 @@ class ModelRunner:
 
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         a8, a8m, a8o, a8d = self.a8_plan(B)  # qkv / gate_up / o / down W8A8 (W4A8)
+        if B == 1 and self.rr_decode and not (a8 or a8m or a8o):
+            return self._decode_step_rr(sample, plan)
         if self.fused_norm and B <= self.fused_norm_max_batch and not (a8 or a8m or a8o):
             return self._decode_step_fused(B, sample, plan)
         w, d = self.w, self.d
@@ -439,6 +453,57 @@ class ModelRunner:
             lin(act, lw.w_down, "res", out=d_parts, splitk=sk_d, res=(h, xn, ssq[2 * l + 2], tk), **rc)
         ops.add_rmsnorm(h, w.final_norm, self.eps, xn, rows=B, xf=xf, write_h=False)
         self._decode_tail(B, sample, xn, xf)
+
+    def _decode_step_rr(self, sample: bool, plan: Optional[tuple] = None) -> None:
+        """Batch-1 decode step with the residual adds folded into the GEMM prologues (TP = 1, bf16, gammas folded):
+        5 launches per layer.
+
+          embed (raw h, bf16(h), sum h^2)  ->  per layer:
+            gemm qkv  (layer 0: bf16 x, row-scaled slabs; later layers ops.linear_rr: x = h + sum(down slabs) formed
+                       in the prologue, h_out = x, sum x^2 -> ssq[l], unscaled f32 slabs)
+            -> attn_decode (slab sum, RMS row scale from ssq[l], RoPE, KV append, split-KV attention)
+            -> gemm o (f32 split-K slabs)
+            -> gemm gate_up (ops.linear_rr: x = h + sum(o slabs), its own full-row RMS scale, SiLU * up)
+            -> gemm down (f32 split-K slabs)
+          -> final RMSNorm (h + down slabs) -> lm_head -> token commit
+        The residual stream alternates between self.h and self.h_alt (a prologue's other workgroups still read the
+        buffer the column-0 workgroups replace)."""
+        w, d, B = self.w, self.d, 1
+        ids, pos, bt = self.input_ids[:1], self.positions[:1], self.block_tables[:1]
+        nqkv = (self.H + 2 * self.Hkv) * self.D
+        sk_q = self._splitk(1, d, nqkv, tp_reduced=False)
+        sk_o = self._splitk(1, self.H * self.D)
+        sk_d = self._splitk(1, self.ffn_l)
+        assert sk_o <= 4 and sk_d <= 4, "the residual-reduce prologue sums at most 4 slabs"
+        qkv_parts = self.qkv_buf[: sk_q * nqkv].view(sk_q, 1, nqkv)
+        o_parts = self.o_buf[: sk_o * d].view(sk_o, 1, d)
+        d_parts = self.down_buf[: sk_d * d].view(sk_d, 1, d)
+        plan = plan or ops.decode_split_plan(1, self.Hkv, self.max_model_len)
+        ssq = self.ssq
+        hs = (self.h[:1], self.h_alt)
+        cur = 0
+        xn, attn, act = self.xn[:1], self.attn[:1], self.act[:1]
+        ops.add_rmsnorm(hs[0], w.layers[0].attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=1,
+                        ss_out=ssq.view(-1), ss_ld=self.max_slots, ss_nzero=self.L)
+        for l, lw in enumerate(w.layers):
+            if l == 0:
+                ops.linear(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q, rownorm=(ssq[0], self.eps))
+                rn = None
+            else:
+                ops.linear_rr(hs[cur], d_parts, hs[1 - cur], lw.wqkv, "f32", out=qkv_parts, ss_out=ssq[l],
+                              eps=self.eps, splitk=sk_q)
+                cur = 1 - cur
+                rn = (ssq[l], self.eps, d)
+            kc, vc = self.kv[l, 0], self.kv[l, 1]
+            ops.attn_decode(self.q[:1], kc, vc, bt, pos, self.H, self.Hkv, self.scale, attn.view(1, self.H, self.D),
+                            workspace=self.attn_ws, plan=plan, qkv_parts=qkv_parts, cos=self.cos, sin=self.sin,
+                            kv_scales=self._kv_scales(l), rownorm=rn)
+            ops.linear(attn, lw.wo, "f32", out=o_parts, splitk=sk_o)
+            ops.linear_rr(hs[cur], o_parts, hs[1 - cur], lw.w_gate_up, "silu", out=act, eps=self.eps)
+            cur = 1 - cur
+            ops.linear(act, lw.w_down, "f32", out=d_parts, splitk=sk_d)
+        ops.add_rmsnorm(hs[cur], w.final_norm, self.eps, xn, parts=d_parts, rows=1, write_h=False)
+        self._decode_tail(B, sample, xn, False)
 
     def _decode_tail(self, B: int, sample: bool, xn, xf: bool) -> None:
         logits = self._lm_head(xn, B, xf)
@@ -839,11 +904,11 @@ class ModelRunner:
 
     def _prefill_layers_sp(self, T, ids, posd, tsd, bt, cud, ctxd, last, work, n, commit):
         """Sequence-parallel prefill under TP: rank r owns rows [r*Tl, (r+1)*Tl) of the residual stream.
-        Row-parallel outputs (O, down; f32 [Tp, d]) are reduce-scattered instead of all-reduced, the
-        residual add + RMSNorm runs on the local Tl rows only, and the bf16 normalised rows are
-        all-gathered for the next column-parallel GEMM: half the all-reduce's second-phase bytes (bf16
-        instead of f32) and 1/tp of the norm work.  Rows past T (padding to a multiple of tp) are
-        row-independent garbage that is never read back."""
+        Row-parallel outputs (O, down; [Tp, d], bf16 when ``sp_bf16`` else f32) are reduce-scattered instead of
+        all-reduced, the residual add + RMSNorm runs on the local Tl rows only (in f32), and the bf16 normalised
+        rows are all-gathered for the next column-parallel GEMM: with bf16 payloads both collectives move half the
+        bytes of an f32 all-reduce's phases, and 1/tp of the norm work.  Rows past T (padding to a multiple of tp)
+        are row-independent garbage that is never read back."""
         dev, w, d, tp = self.device, self.w, self.d, self.tp
         f32 = dict(dtype=torch.float32, device=dev)
         bf = dict(dtype=torch.bfloat16, device=dev)
@@ -856,8 +921,17 @@ class ModelRunner:
         xn_l = torch.empty(Tl, d, **bf)
         xn_full = torch.empty(Tp, d, **bf)
         xn = xn_full[:T]
-        full = torch.zeros(Tp, d, **f32)  # row-parallel GEMM output (padding rows stay zero)
+        pay = dict(dtype=torch.bfloat16 if self.sp_bf16 else torch.float32, device=dev)
+        epi = "bf16" if self.sp_bf16 else "f32"
+        full = torch.zeros(Tp, d, **pay)  # row-parallel GEMM output (padding rows stay zero)
         loc = torch.empty(Tl, d, **f32)
+        loc_p = torch.empty(Tl, d, **pay) if self.sp_bf16 else loc
+
+        def rs():  # reduce-scatter of the row-parallel output into this rank's f32 residual slab
+            tp.reduce_scatter(loc_p, full)
+            if loc_p is not loc:
+                loc.copy_(loc_p)
+
         qkv = torch.empty(T, (self.H + 2 * self.Hkv) * self.D, **bf)
         q = torch.empty(T, self.H, self.D, **bf)
         attn = torch.empty(T, self.H * self.D, **bf)
@@ -869,13 +943,13 @@ class ModelRunner:
                 ops.add_rmsnorm(h_l, lw.attn_norm, self.eps, xn_l, parts=parts)
             tp.all_gather(xn_full.view(-1), xn_l.view(-1))
             self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T)
-            ops.linear(attn, lw.wo, "f32", out=full, splitk=1)
-            tp.reduce_scatter(loc, full)
+            ops.linear(attn, lw.wo, epi, out=full, splitk=1)
+            rs()
             ops.add_rmsnorm(h_l, lw.mlp_norm, self.eps, xn_l, parts=parts)
             tp.all_gather(xn_full.view(-1), xn_l.view(-1))
             act = ops.linear(xn, lw.w_gate_up, "silu")
-            ops.linear(act, lw.w_down, "f32", out=full, splitk=1)
-            tp.reduce_scatter(loc, full)
+            ops.linear(act, lw.w_down, epi, out=full, splitk=1)
+            rs()
         if not commit:
             return None
         ops.add_rmsnorm(h_l, w.final_norm, self.eps, xn_l, parts=parts)

@@ -989,6 +989,60 @@ def prefetch(tensors, nbytes=None, wgs: int = 512) -> None:
     ext().prefetch(tensors, [int(b) for b in nb], int(wgs))
 
 
+def rr_supported(w: PackedWeight, K: int, splitk: int = 1) -> bool:
+    """Whether a batch-1 decode GEMM can take the residual-reduce prologue (``linear_rr``): bf16 weights and a K slice
+    per split that fits the kernel's LDS image (gemm.hip RR_KMAX)."""
+    return w.kind in ("bf16", "dense") and K % 32 == 0 and (K // 32 + splitk - 1) // splitk * 32 <= 8192
+
+
+def linear_rr(h: torch.Tensor, parts: torch.Tensor, h_out: torch.Tensor, w: PackedWeight, epi: str,
+              out: Optional[torch.Tensor] = None, ss_out: Optional[torch.Tensor] = None, eps: float = 1e-5,
+              splitk: Optional[int] = None, nb: Optional[int] = None, waves: Optional[int] = None,
+              div: Optional[int] = None) -> torch.Tensor:
+    """Batch-1 decode projection with the residual add folded into its prologue (gemm.hip RR; lsa_epi.h LsaRr).
+
+    x = h + sum_s parts[s] (h: f32 [1, K] residual stream, parts: f32 [S, 1, K] split-K slabs of the previous
+    row-parallel projection); h_out <- x (the next residual stream, a different buffer than h).  The RMSNorm gamma is
+    folded into W (``norms_folded``); the RMS row scale r = rsqrt(mean(x^2) + eps) is applied
+      * epi='silu': in the epilogue (splitk 1; each workgroup reduces the whole row itself) -> bf16 [1, N/2];
+      * epi='f32': NOT here -- the output is [splitk, 1, N] f32 slabs of W @ bf16(x), and sum x^2 is added to
+        ss_out[0] (Q24 int64, must be zero on entry) for the slab consumer (``attn_decode(rownorm=...)``).
+    Replaces the ``res_add_ss`` launch between the two projections (one kernel boundary less per layer side)."""
+    K = w.K
+    assert epi in ("f32", "silu") and h.numel() >= K and parts.dim() == 3 and parts.shape[1] == 1
+    nb0, sk0, wv0, dv0 = pick_gemm_config(1, w.N, K, epi, kind=w.kind)
+    splitk = 1 if epi == "silu" else (sk0 if splitk is None else splitk)
+    nb = nb0 if nb is None else nb
+    if not _gpu(h):
+        x = h.view(-1)[:K].float() + parts.float().sum(0).view(-1)
+        h_out.view(-1)[:K].copy_(x)
+        xb = x.to(torch.bfloat16).view(1, K)
+        if epi == "silu":
+            r = torch.rsqrt(x.pow(2).sum() / K + eps)
+            y = ref.linear(xb, w.dense(), "f32") * r
+            g, u = y.view(-1, 2, 16)[:, 0].reshape(1, -1), y.view(-1, 2, 16)[:, 1].reshape(1, -1)
+            res = (torch.nn.functional.silu(g) * u).to(torch.bfloat16)
+            if out is None:
+                return res
+            out.view(-1)[: res.numel()].copy_(res.view(-1))
+            return out
+        assert ss_out is not None
+        ss_out.view(-1)[:1] += ss_q24(x.pow(2).sum().view(1))
+        y = ref.linear(xb, w.dense(), "f32").unsqueeze(0)
+        if out is None:
+            return y
+        out.view(-1)[: y.numel()].copy_(y.reshape(-1))
+        return out
+    waves = wv0 if waves is None else waves
+    div = dv0 if div is None else div
+    if out is None:
+        out = (torch.empty(splitk, 1, w.N, device=h.device, dtype=torch.float32) if epi == "f32" else
+               torch.empty(1, w.N // 2, device=h.device, dtype=torch.bfloat16))
+    ext().gemm_rr(h.view(-1)[:K], parts, h_out.view(-1), w.data, w.N, out, EPI[epi], nb, splitk, waves, div,
+                  ss_out=ss_out, eps=float(eps))
+    return out
+
+
 def res_add_ss(h: torch.Tensor, parts: Optional[torch.Tensor], xn: torch.Tensor, rows: int, ss_out: torch.Tensor,
                xf: bool = False) -> torch.Tensor:
     """Residual add of the folded-norm decode step (the RMSNorm gammas live in the next GEMM's weight, which scales
@@ -1101,17 +1155,23 @@ def decode_workspace(B: int, H: int, Hkv: int, nsplit: int, device) -> tuple:
 
 
 def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None, plan=None, xf=False,
-                qkv_parts=None, cos=None, sin=None, kv_scales=None, out_s8=None):
+                qkv_parts=None, cos=None, sin=None, kv_scales=None, out_s8=None, rownorm=None):
     """q [B,H,128] vs paged cache, context = pos + 1.  workspace = decode_workspace(...) for split-KV.
     xf=True: out is a flat buffer receiving the fragment-major layout of the [B, H*128] output.
     qkv_parts ([S, B, (H+2Hkv)*128] f32 split-K slabs of the QKV projection) + cos/sin: RoPE and the
     KV-cache append of the new token are fused in (``q`` is then only a [B, H, 128] scratch buffer).
     kv_scales = (ks, vs): fp8 cache (see ``KV_FP8``).
     out_s8 (xf only): ``out`` is a uint8 buffer receiving the output as e4m3 in the xf8 layout with one E8M0 scale
-    per (row, head) in ``out_s8`` -- the input of a W8A8 / W4A8 o projection (``linear_a8(s8=)``)."""
+    per (row, head) in ``out_s8`` -- the input of a W8A8 / W4A8 o projection (``linear_a8(s8=)``).
+    rownorm = (ss, eps, hidden): the slabs are the projection of UN-normalised rows (``linear_rr``); row b's q / k / v
+    are scaled by rsqrt(ss[b] / hidden + eps) (ss Q24 int64) before RoPE."""
     B = pos.shape[0]
     assert out_s8 is None or xf, "the e4m3 attention output lives in the xf8 layout"
+    assert rownorm is None or qkv_parts is not None, "rownorm scales the fused-RoPE slabs"
     if not _gpu(pos):
+        if rownorm is not None:
+            r = torch.rsqrt(ss_float(rownorm[0][:B]) / rownorm[2] + rownorm[1])
+            qkv_parts = qkv_parts[:, :B].sum(0, keepdim=True) * r.view(1, B, 1)
         if qkv_parts is not None:
             ref.rope_append(qkv_parts, pos, None, block_tables, cos, sin, q, kc, vc, H, Hkv, kv_scales)
         if out_s8 is not None:
@@ -1134,7 +1194,9 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
     opart, mlpart, counters = workspace
     ks, vs = kv_scales if kv_scales is not None else (None, None)
     ext().attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, chunk, nsplit, out, opart, mlpart, counters,
-                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs, out_s8=out_s8)
+                      xfrag_tiles(B) if xf else 0, qkv_parts, cos, sin, unsplit_max, ks, vs, out_s8=out_s8,
+                      **({} if rownorm is None else dict(rowss=rownorm[0], eps=float(rownorm[1]),
+                                                          hidden=int(rownorm[2]))))
     return out
 
 

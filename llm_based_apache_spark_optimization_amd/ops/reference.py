@@ -227,6 +227,31 @@ def repeat_penalty(row, hist_row, pen, pos, last_n):
     return row
 
 
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def pack_seed(key: int, offset: int = 0) -> int:
+    """Device seed word of a request: the stream key (low 40 bits) and the draw-counter offset (high 24 bits, the
+    tokens a preempted request already generated), as sampling.hip unpacks it."""
+    assert 0 <= offset < (1 << 23), offset
+    return (offset << 40) | (int(key) & ((1 << 40) - 1))
+
+
+def draw_seed(packed: int, gen_len: int) -> int:
+    """Generator seed of draw gen_len of a request (the host twin of sampling.hip's keyed counter): the scrambled
+    key plus the counter, so nearby keys give unrelated streams and the offset continues a resumed stream."""
+    packed &= _M64
+    key, off = packed & ((1 << 40) - 1), packed >> 40
+    return _mix64((_mix64(key) + 0x9E3779B97F4A7C15 * (off + gen_len + 1)) & _M64) & ((1 << 63) - 1)
+
+
 def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_tokens, gen_len, input_ids,
                   positions, finished, eos, limit=None, eos_on=None, generator: torch.Generator | None = None,
                   last_n=None):
@@ -242,8 +267,8 @@ def sample_commit(logits, hist, penalty, temperature, top_k, top_p, seeds, out_t
             toks[b] = int(row.argmax())
             continue
         idx, p = sample_probs(row, T, int(top_k[b]), float(top_p[b]))
-        # draw g of a row comes from seed + g alone (one generator per row: a generator shared across rows made a
-        # row's draws depend on the rows sampled before it in the batch)
-        g = generator if generator is not None else torch.Generator().manual_seed(int(seeds[b]) + int(gen_len[b]))
+        # draw g of a row comes from (seed key, g + offset) alone (one generator per row: a generator shared across
+        # rows made a row's draws depend on the rows sampled before it in the batch)
+        g = generator if generator is not None else torch.Generator().manual_seed(draw_seed(int(seeds[b]), int(gen_len[b])))
         toks[b] = int(idx[torch.multinomial(p.cpu(), 1, generator=g)])
     commit(toks, out_tokens, gen_len, input_ids, positions, finished, eos, limit, eos_on, hist=hist)

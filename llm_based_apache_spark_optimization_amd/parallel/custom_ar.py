@@ -203,9 +203,12 @@ def maybe_ipc_allreduce(group, rank: int, world: int, device: torch.device) -> O
 
     Unavailable includes a failure on any rank to map its peers' regions (``IpcUnavailable``): the group
     then degrades to RCCL for every collective instead of the replica dying in ``TPGroup.warmup``."""
+    maybe_ipc_allreduce.last_reason = ""
     if device.type != "cuda" or world < 2 or os.environ.get("LSA_CUSTOM_AR", "1") == "0":
+        maybe_ipc_allreduce.last_reason = "disabled" if device.type == "cuda" and world >= 2 else "not a GPU group"
         return None
     if world > ops.ext().ar_max_world:
+        maybe_ipc_allreduce.last_reason = f"group of {world} ranks exceeds the kernel's {ops.ext().ar_max_world}"
         return None
     try:
         return IpcAllReduce(group, rank, world, device,
@@ -213,4 +216,8 @@ def maybe_ipc_allreduce(group, rank: int, world: int, device: torch.device) -> O
                             timeout_s=float(os.environ.get("LSA_CUSTOM_AR_TIMEOUT_S", DEFAULT_TIMEOUT_S)))
     except IpcUnavailable as e:
         log.warning("one-shot IPC all-reduce unavailable, TP group falls back to RCCL: %s", e)
+        maybe_ipc_allreduce.last_reason = str(e)
         return None
+
+
+maybe_ipc_allreduce.last_reason = ""

@@ -9,6 +9,7 @@ the one-shot IPC kernel (``custom_ar.IpcAllReduce``); RCCL keeps 
 """
 from __future__ import annotations
 
+import collections
 import os
 from typing import Optional
 
@@ -21,11 +22,40 @@ class TPGroup:
         self.group, self.rank, self.size, self.device = group, rank, size, device
         self._warm = False
         self.car = None  # IpcAllReduce once warmed up on a GPU group
+        self.ipc_fallback = ""  # why a GPU group runs without the IPC kernel (custom_ar.maybe_ipc_allreduce)
+        # collectives ISSUED per path (eager launches and graph captures; a replayed graph re-runs its captured
+        # ones without coming back here): ipc_oneshot / ipc_twoshot / ipc_all_gather, <backend>_<collective>
+        self.calls: collections.Counter = collections.Counter()
+
+    def _backend(self) -> str:
+        try:
+            return str(dist.get_backend(self.group))
+        except Exception:  # noqa: BLE001 - not initialised (unit tests of the helpers)
+            return "none"
+
+    def _ipc(self, payload_bytes: int) -> None:
+        self.calls["ipc_twoshot" if self.car.mode(payload_bytes) & 2 else "ipc_oneshot"] += 1
+
+    def describe(self) -> dict:
+        """Which communication paths this rank's TP group runs (bench.py's ``tp_comm`` record): backend, ranks per
+        group, the device it sits on, whether the one-shot IPC all-reduce is live (else why not), and the
+        issued-collective counts per path."""
+        try:
+            nranks = dist.get_world_size(self.group)
+        except Exception:  # noqa: BLE001
+            nranks = self.size
+        return {"backend": self._backend(), "group_ranks": int(nranks), "tp_rank": self.rank,
+                "device": str(self.device), "device_index": self.device.index,
+                "ipc_allreduce": self.car is not None,
+                "ipc_bf16_payload": bool(self.car.bf16) if self.car is not None else None,
+                "ipc_fallback": self.ipc_fallback or None, "calls": dict(sorted(self.calls.items()))}
 
     def all_reduce(self, t: torch.Tensor) -> None:
         if self.car is not None and self.car.fits(t):
+            self._ipc(t.numel() * 4)
             self.car(t)
         else:
+            self.calls[f"{self._backend()}_all_reduce"] += 1
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     def can_fold_splitk(self, slab_numel: int) -> bool:
@@ -39,6 +69,7 @@ class TPGroup:
             self.all_reduce(parts)
             return parts
         if self.car is not None and self.car.fits_slabs(parts):
+            self._ipc(parts.numel() // parts.shape[0] * 4)
             return self.car.reduce_slabs(parts)
         red = parts[:1]
         red.add_(parts[1:].sum(0, keepdim=True))
@@ -55,18 +86,22 @@ class TPGroup:
         D = h.shape[1]
         if (self.car is not None and parts.is_cuda and self.car.fits_slabs(parts) and D % 256 == 0
                 and h.is_contiguous() and parts.shape[1] == rows):
+            self._ipc(parts.numel() // parts.shape[0] * 4)
             self.car.reduce_slabs_res(parts, h[:rows], xn, ss, ops.xfrag_tiles(rows) if xf else 0)
             return
         ops.res_add_ss(h, self.reduce_parts(parts), xn, rows, ss, xf=xf)
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         if self.car is not None and self.car.fits(inp) and out.is_contiguous():
+            self.calls["ipc_all_gather"] += 1
             self.car.all_gather(out, inp)
         else:
+            self.calls[f"{self._backend()}_all_gather_{str(inp.dtype).replace('torch.', '')}"] += 1
             dist.all_gather_into_tensor(out, inp, group=self.group)
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         """out = rank's 1/size row block of the sum over ranks of inp (sequence-parallel prefill)."""
+        self.calls[f"{self._backend()}_reduce_scatter_{str(inp.dtype).replace('torch.', '')}"] += 1
         if inp.is_cuda and dist.get_backend(self.group) == "gloo":  # gloo: CPU tensors only (test boxes)
             tmp = inp.clone()
             dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=self.group)
@@ -95,6 +130,7 @@ class TPGroup:
                 from .custom_ar import maybe_ipc_allreduce
 
                 self.car = maybe_ipc_allreduce(self.group, self.rank, self.size, self.device)
+                self.ipc_fallback = "" if self.car is not None else (maybe_ipc_allreduce.last_reason or "unavailable")
                 if self.car is not None:
                     self.car(t)
                 torch.cuda.synchronize(self.device)

@@ -50,3 +50,14 @@ def test_bench_contract_cpu(nproc, extra, par, batch):
     assert "CPU rehearsal" in d["data"]
     # the teacher-forced decode check runs under TP too (rank 0's tokens vs the oracle on the unsharded weights)
     assert d["numerics"]["ok"] and d["numerics"]["tokens_checked"] >= 3, d["numerics"]
+    if nproc > 1:  # the self-verifying communication record (which paths ran, on which devices)
+        c = d["tp_comm"]
+        assert c["world"] == nproc and len(c["device_per_rank"]) == nproc and c["backend"] == "gloo"
+        if "--tp" in extra:
+            assert c["tp"] == 2 and c["group_ranks"] == [2] and c["tp_backend"] == "gloo"
+            assert c["ipc_allreduce"] is False and c["ipc_fallback"] is None  # CPU groups never try the IPC kernel
+            calls = c["calls_all_ranks"]
+            assert calls.get("gloo_all_reduce", 0) > 0, calls  # decode all-reduces of the row-parallel projections
+            assert calls.get("gloo_all_gather_float32", 0) > 0, calls  # vocab-parallel logits
+    else:
+        assert "tp_comm" not in d

@@ -85,7 +85,12 @@ def _tp_worker(rank, world, port, q):
     toks = e.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
     # sequence-parallel prefill (forced for these short prompts; T = 39 is not a multiple of tp: padded)
     e.runner.sp_min_tokens = 1
+    assert e.runner.sp_bf16  # default: bf16 reduce-scatter payloads
     sp_toks = e.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+    e.runner.sp_bf16 = False  # the f32-payload SP path: same tokens (the bf16 rounding of the TP partials is
+    sp32_toks = e.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))  # below the argmax margins)
+    assert [t.token_ids for t in sp32_toks] == [t.token_ids for t in sp_toks]
+    e.runner.sp_bf16 = True
     e.runner.sp_min_tokens = 1 << 30
     # logit-level pin of the sharded math: teacher-forced decode logits of the TP engine vs the fp32 oracle run on
     # the unsharded weights (the token checks below only see argmaxes)
@@ -247,3 +252,19 @@ def test_set_slots_batched_equals_per_slot():
     assert set(a._pending_bt) == set(b._pending_bt) == {3}
     assert torch.equal(a._pending_bt[3], b._pending_bt[3])
     assert b.block_tables[3].abs().sum() == 0 and b._pending_bt[3][:3].tolist() == [6, 7, 8]
+
+
+def test_rr_step_matches_norm_launch_step():
+    """Batch 1 takes the residual-reduce step (ops.linear_rr folds the residual add into the qkv / gate_up prologues,
+    attn_decode applies the qkv row scale) and decodes the same greedy tokens as the norm-launch step."""
+    e = build_engine("tiny-nsql", device="cpu", max_slots=2, max_model_len=256)
+    r = e.runner
+    assert r.rr_decode
+    sp = SamplingParams(max_tokens=12, ignore_eos=True)
+    a = e.generate(["count rows"], sp)[0].token_ids
+    xa = r.final_hidden(1).float().clone()
+    r.rr_decode = False
+    b = e.generate(["count rows"], sp)[0].token_ids
+    xb = r.final_hidden(1).float().clone()
+    assert a == b
+    assert ((xa - xb).norm() / xb.norm()).item() < 2e-2

@@ -1048,9 +1048,9 @@ def test_gemm_ragged_grid(gpu, kind, M, nb):
 
 
 
-@pytest.mark.parametrize("H,Hkv", [(24, 8), (32, 32), (4, 2)])
+@pytest.mark.parametrize("H,Hkv", [(24, 8), (32, 32), (4, 2), (16, 4)])
 @pytest.mark.parametrize("T", [65, 300, 1100])
-@pytest.mark.parametrize("cfg", [-1, 0, 3, 5, 8, 11])
+@pytest.mark.parametrize("cfg", [-1, 0, 3, 5, 6, 7, 8, 11])
 @pytest.mark.parametrize("rownorm", [False, True])
 def test_gemm_rope_epilogue(gpu, H, Hkv, T, cfg, rownorm):
     """Prefill qkv GEMM with RoPE + the paged KV-cache append in its epilogue (ops.linear_rope / EPI_ROPE) vs the

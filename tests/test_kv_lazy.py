@@ -91,12 +91,15 @@ def test_preemption_recomputes_identical_tokens():
 
 def test_preemption_keeps_seeded_sampling_stream():
     """Sampling at temperature > 0 with a fixed seed: a request that is preempted and re-admitted continues its
-    random stream where it stopped (the resumed incarnation draws from seed + len(resumed)).  Its tokens after the
+    random stream where it stopped (the resumed incarnation draws from counter offset len(resumed)).  Its tokens after the
     resume point follow the solo run's; they are compared over the first 8 only, because the re-prefill of the
     generated tokens rounds the bf16 activations differently from the incremental decode, and a later draw that
     lands near a CDF boundary may then flip (the unmodified stream diverges at once: every draw is shifted)."""
     prompts = [[1] + list(range(3 + k, 40 + k)) for k in range(3)]
     eng = build_engine("tiny-nsql", device="cpu", max_slots=3, max_model_len=512, num_kv_blocks=9)
+    # the solo runs must decode on the batched runs' step: the batch-1 residual-reduce step rounds differently
+    # (its row scale applies to the GEMM output, the norm-launch step's CPU path scales the bf16 input)
+    eng.runner.rr_decode = False
     sps = [SamplingParams(max_tokens=150, ignore_eos=True, temperature=0.9, top_k=40, top_p=0.95, seed=100 + k)
            for k in range(3)]
     solo = [eng.generate([p], sp)[0].token_ids for p, sp in zip(prompts, sps)]
@@ -112,9 +115,10 @@ def test_preemption_keeps_seeded_sampling_stream():
             assert q.output_ids[:n] == s[:n]
 
 
-def test_sampler_stream_depends_on_seed_plus_step():
-    """The reference sampler's draw for step g of a row comes from seed + g alone: (seed + R, g) == (seed, g + R),
-    whatever the other rows of the batch are."""
+def test_sampler_stream_keyed_by_seed_with_counter_offset():
+    """The reference sampler's draw for step g of a row comes from (seed key, g + offset) alone: a resumed request
+    (offset R) continues its stream, (key, R, g) == (key, 0, g + R), whatever the other rows of the batch are; and
+    neighbouring keys are NOT shifted copies of one stream (seed s + 1 at step g used to equal seed s at g + 1)."""
     torch.manual_seed(0)
     V, B = 300, 3
     logits = torch.randn(B, V)
@@ -128,9 +132,12 @@ def test_sampler_stream_depends_on_seed_plus_step():
                           torch.tensor(seeds), st[0], st[1], st[2], st[3], st[4], torch.tensor([-1]))
         return [int(st[0][b, gl[b]]) for b in range(B)]
 
-    toks = [draw([7 + R, 11, 13], [3, 0, 0])[0] for R in range(20)]
+    toks = [draw([ref.pack_seed(7, R), 11, 13], [3, 0, 0])[0] for R in range(20)]
     assert toks == [draw([7, 11, 13], [3 + R, 0, 0])[0] for R in range(20)]
     assert draw([7, 11, 13], [3, 0, 0])[0] == draw([7, 99, 5], [3, 2, 1])[0]
+    assert all(ref.draw_seed(s + 1, g) != ref.draw_seed(s, g + 1) for s in range(50) for g in range(20))
+    shifted = [draw([8, 11, 13], [g, 0, 0])[0] == draw([7, 11, 13], [g + 1, 0, 0])[0] for g in range(20)]
+    assert sum(shifted) < 15
 
 
 def test_admission_hold_clears_on_free_blocks():

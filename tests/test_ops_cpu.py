@@ -128,3 +128,31 @@ def test_extension_loads_and_matches_its_sources():
         pytest.skip("extension not built in this tree")
     ops.ext()
     assert ops.BUILD_INFO.get("so_match") is True and ops.BUILD_INFO.get("sources_match") is True, ops.BUILD_INFO
+
+
+def test_linear_rr_cpu_semantics():
+    """ops.linear_rr == res_add_ss (h += sum parts, bf16(h), sum h^2) followed by the row-scaled projection."""
+    import math
+
+    from llm_based_apache_spark_optimization_amd import ops
+
+    torch.manual_seed(0)
+    K, N = 256, 128
+    h = torch.randn(1, K)
+    parts = torch.randn(3, 1, K)
+    w = ops.PackedWeight.from_dense((torch.randn(2 * N, K) / math.sqrt(K)).to(torch.bfloat16))
+    # composite reference: the norm-launch step's residual add, then the rownorm GEMM
+    h1 = h.clone()
+    xn = torch.empty(1, K, dtype=torch.bfloat16)
+    ss1 = torch.zeros(1, dtype=torch.int64)
+    ops.res_add_ss(h1, parts, xn, 1, ss1)
+    want_silu = ops.linear(xn, w, "silu", rownorm=(ss1, 1e-5))
+    want_f32 = ops.linear(xn, w, "f32", splitk=1)
+    h_out = torch.zeros(1, K)
+    got = ops.linear_rr(h, parts, h_out, w, "silu", eps=1e-5)
+    assert torch.allclose(h_out, h1)
+    assert torch.allclose(got.float(), want_silu.float(), rtol=2e-2, atol=2e-3)
+    ss2 = torch.zeros(2, dtype=torch.int64)
+    y = ops.linear_rr(h, parts, h_out, w, "f32", ss_out=ss2)
+    assert torch.allclose(y.sum(0), want_f32.sum(0), rtol=1e-4, atol=1e-4)
+    assert abs(ss2[0].item() - ss1[0].item()) <= 16 and ss2[1] == 0
