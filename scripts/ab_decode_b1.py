@@ -18,6 +18,7 @@ from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build
 model = sys.argv[1] if len(sys.argv) > 1 else "llama3.2"
 plen = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+only = sys.argv[4] if len(sys.argv) > 4 else None  # one arm (profiling runs)
 new = 128
 eng = build_engine(model, device="cuda:0", dtype="bf16", max_slots=2 if plen > 1024 else 32,
                    max_model_len=plen + new + 64, seed=0)
@@ -25,7 +26,7 @@ r = eng.runner
 g = torch.Generator().manual_seed(4321)
 prompt = [eng.spec.bos_id] + torch.randint(3, eng.spec.vocab_size, (plen - 1,), generator=g).tolist()
 sp = SamplingParams(max_tokens=new, temperature=0.0, ignore_eos=True)
-arms = {"rr": True, "norm_launch": False}
+arms = {k: v for k, v in {"rr": True, "norm_launch": False}.items() if only in (None, k)}
 res = {k: [] for k in arms}
 for k, on in arms.items():
     r.rr_decode = on
