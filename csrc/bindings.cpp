@@ -654,6 +654,16 @@ void attn_set_stamps(const c10::optional<at::Tensor>& st) {
   check(lsa_attn_set_stamps(st.has_value() ? st->data_ptr() : nullptr), "attn_set_stamps");
 }
 
+// diagnostic stamps of the stream-K prefill GEMM (kernels/gemm_tile256.hip g_sk_stamps): [grid][8] int64, sized by the
+// caller for the largest grid it launches (<= 2 x CUs)
+extern "C" int lsa_sk_set_stamps(unsigned long long* p);
+void sk_set_stamps(const c10::optional<at::Tensor>& st) {
+  if (st.has_value()) TORCH_CHECK(on_dev(*st) && st->element_size() == 8 && st->numel() >= 2048 * 8,
+                                  "stamps: int64 GPU tensor of >= 2048 x 8");
+  check(lsa_sk_set_stamps(st.has_value() ? reinterpret_cast<unsigned long long*>(st->data_ptr()) : nullptr),
+        "sk_set_stamps");
+}
+
 // diagnostic cycle stamps of the 32-row prefill attention (kernels/attention_prefill32.hip g_p32_stamps): the caller
 // sizes the buffer for the plan it launches, [nwork * H * NG * 4][8] int64
 extern "C" int lsa_p32_set_stamps(void* p);
@@ -1022,6 +1032,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_xf8_blocks", &quant_xf8_blocks, py::arg("x"), py::arg("mt"), py::arg("blk"), py::arg("x8"), py::arg("s8"));
   m.def("quant_xf8", &quant_xf8, py::arg("x"), py::arg("mt"), py::arg("x8"), py::arg("sx"));
   m.def("attn_set_stamps", &attn_set_stamps, py::arg("stamps") = py::none());
+  m.def("sk_set_stamps", &sk_set_stamps, py::arg("stamps") = py::none());
   m.def("attn_prefill_set_stamps", &attn_prefill_set_stamps, py::arg("stamps") = py::none());
   m.def("rope_append", &rope_append, py::arg("qkv"), py::arg("pos"), py::arg("tok_seq"), py::arg("block_tables"),
         py::arg("cos"), py::arg("sin"), py::arg("q_out"), py::arg("kc"), py::arg("vc"), py::arg("H"), py::arg("Hkv"),

@@ -144,6 +144,21 @@ struct TileCfg {
   static constexpr int WAIT3 = 2 * GX + GW0 + GW1;           // a whole K-tile's loads per wave (3-buffer wait)
 };
 
+// timing probe (scripts/sk_stamps.py): when set, thread 0 of every workgroup records s_memrealtime (100 MHz) at
+// entry [0], after its first segment's pipeline fill [1], after its last segment's K loop [2] and at exit [3], its
+// K-tile [4] and segment [5] counts, and s_memtime (shader clock) at [1] / [2] as [6] / [7]; null in production
+__device__ unsigned long long* g_sk_stamps = nullptr;
+extern "C" int lsa_sk_set_stamps(unsigned long long* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_sk_stamps), &p, sizeof(p));
+}
+// (compiled in only with -DLSA_SK_STAMPS: its live scalars cost the 256 x 256 kernels SGPR / VGPR spills)
+#ifdef LSA_SK_STAMPS
+#define LSA_SK_STAMP(K, V) \
+  if (stp && threadIdx.x == 0) stp[(size_t)blockIdx.x * 8 + (K)] = (V)
+#else
+#define LSA_SK_STAMP(K, V) (void)0
+#endif
+
 // The kernel body is a __device__ function template behind a thin __global__ wrapper: hipcc's host pass does not
 // emit the launch stub of a kernel template whose own body holds generic (integral_constant) lambdas.
 template <int BM, int WN, int EPI, int NBUF, int KS, int NW>
@@ -153,6 +168,11 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
                                              const RopeEpi& re, const LsaEpi& ne) {
   using C = TileCfg<BM, WN, KS, NW>;
   constexpr int SLOT = BM * C::NBT * 16;  // floats of one partial-tile slot
+#ifdef LSA_SK_STAMPS
+  unsigned long long* const stp = g_sk_stamps;
+  int st_seg = 0, st_kt = 0;
+#endif
+  LSA_SK_STAMP(0, __builtin_amdgcn_s_memrealtime());
   constexpr int MI = C::MI, NQ0 = C::NQ0, NQ1 = C::NQ1;
   constexpr bool BIG = 2 * MI * WN >= 24;  // >= 96 accumulator VGPRs (256 x 256, 4-wave 128 x 192): smaller epilogue load batches
   static_assert(C::GX >= 1 && C::GW1 >= 1 && C::XF % NW == 0 && C::WF0 % NW == 0 && C::WF1 % NW == 0 &&
@@ -355,6 +375,14 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
       LSA_WAITV(C::WAIT);
     }
     __builtin_amdgcn_s_barrier();
+#ifdef LSA_SK_STAMPS
+    if (st_seg == 0) {
+      LSA_SK_STAMP(1, __builtin_amdgcn_s_memrealtime());
+      LSA_SK_STAMP(6, __builtin_amdgcn_s_memtime());
+    }
+    ++st_seg;
+    st_kt += Tl;
+#endif
     // ping-pong: the second M wave group runs one barrier behind, so one group's MFMA section overlaps the other's
     // fragment reads + prefetch issue (the >= 2-phase WAR/RAW slack above covers the offset)
     if (wm == 1) __builtin_amdgcn_s_barrier();
@@ -380,6 +408,8 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
 #undef LSA_WAITV
     if (wm == 0) __builtin_amdgcn_s_barrier();  // rebalance the barrier count
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the segment
+    LSA_SK_STAMP(2, __builtin_amdgcn_s_memrealtime());
+    LSA_SK_STAMP(7, __builtin_amdgcn_s_memtime());
   };
 
   // epilogue of a finished tile: acc[i][j] = D[n = nb_j * 16 + 4 g + q][m = mb_i * 16 + (lane & 15)]
@@ -715,6 +745,9 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     segment(tile, 0, T);
     finish_tile();
   }
+  LSA_SK_STAMP(3, __builtin_amdgcn_s_memrealtime());
+  LSA_SK_STAMP(4, (unsigned long long)st_kt);
+  LSA_SK_STAMP(5, (unsigned long long)st_seg);
 }
 
 template <int BM, int WN, int EPI, int NBUF, int KS, int NW>

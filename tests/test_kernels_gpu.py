@@ -1088,3 +1088,4 @@ def test_gemm_rope_epilogue(gpu, H, Hkv, T, cfg, rownorm):
     assert _rel(q.cpu(), q_r) < 4e-3
     assert _rel(kc.cpu(), kc_r) < 4e-3 and _rel(vc.cpu(), vc_r) < 4e-3
     assert int((kc.cpu() != 0).any(-1).sum()) == T * Hkv  # exactly one appended row per token and kv-head
+
