@@ -141,6 +141,7 @@ struct TileCfg {
   static constexpr int BUFF = 2 * XF + WF0 + WF1;            // fragments (KiB) per K-tile buffer
   static constexpr int HOFF[4] = {0, XF, 2 * XF, 2 * XF + WF0};
   static constexpr bool CAN3 = 3 * BUFF * (NW == 4 ? 2 : 1) <= 160;  // three buffers fit (per CU: 1 or 2 workgroups)
+  static constexpr bool CAN4 = 4 * BUFF <= 160 && NW == 8;            // the one-phase schedule's four (128-row tiles)
   static constexpr int WAIT3 = 2 * GX + GW0 + GW1;           // a whole K-tile's loads per wave (3-buffer wait)
 };
 
@@ -179,7 +180,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
                     C::XF <= 32 && C::WF0 <= 32 && NBUF * C::BUFF * (NW == 4 ? 2 : 1) <= 160, "tile geometry");
   static_assert(EPI != EPI_SILU || WN % 2 == 0, "SiLU pairs (gate, up) n-blocks inside one wave");
   static_assert(EPI != EPI_ROPE || C::NBT % 8 == 0, "RoPE tiles hold whole 128-column heads");
-  static_assert(NBUF == 2 || (NBUF == 3 && C::CAN3), "K-tile buffers");
+  static_assert(NBUF == 2 || (NBUF == 3 && C::CAN3) || (NBUF == 4 && C::CAN4), "K-tile buffers");
   __shared__ __attribute__((aligned(16))) uint4 lds[NBUF * C::BUFF * 64];
   const int lane = threadIdx.x & 63;
   // wave ids through readfirstlane: provably uniform, so every per-wave address term lives in SGPRs
@@ -280,6 +281,30 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     else
       rd(std::integral_constant<int, 3>{}, wr, wb1(B), std::integral_constant<int, NQ1 * KS>{});
   };
+  // one-phase schedule (NBUF 4): the whole K-tile's fragments at once
+  u32x4_t xa[2][MI * KS], wa0[NQ0 * KS], wa1[(NQ1 > 0 ? NQ1 : 1) * KS];
+  auto read_all = [&](auto Bc) {
+    constexpr int B = decltype(Bc)::value;
+    rd(std::integral_constant<int, 0>{}, xa[0], xb(B), std::integral_constant<int, MI * KS>{});
+    rd(std::integral_constant<int, 1>{}, xa[1], xb(B), std::integral_constant<int, MI * KS>{});
+    rd(std::integral_constant<int, 2>{}, wa0, wb0(B), std::integral_constant<int, NQ0 * KS>{});
+    if constexpr (NQ1 > 0) rd(std::integral_constant<int, 3>{}, wa1, wb1(B), std::integral_constant<int, NQ1 * KS>{});
+  };
+  auto mma_all = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[qm * MI + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8_t, j < NQ0 ? wa0[j * KS + ks] : wa1[(j - NQ0) * KS + ks]),
+                __builtin_bit_cast(bf16x8_t, xa[qm][i * KS + ks]), acc[qm * MI + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
   auto mma = [&](auto QMc, auto QNc) {
     constexpr int QM = decltype(QMc)::value, QN = decltype(QNc)::value;
     constexpr int nq = QN ? NQ1 : NQ0;
@@ -355,7 +380,42 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     LSA_PHASE(read_x(B{}, I1{}), (void)0, (void)0, I1, I1);                                                  \
     LSA_PHASE(read_w(B{}, I0{}), (void)0, LSA_WAITV(C::WAIT3), I1, I0);                                      \
   } while (0)
-    if constexpr (NBUF == 3) {
+  // One phase per K-tile (NBUF 4, the 128-row tiles, whose four-phase split left 4-8 MFMAs between barriers): K-tile t
+  // in buffer t % 4; read all its fragments, stage all of K-tile t + 3 into buffer (t + 3) % 4 (= t - 1's), wait for
+  // the own DMAs of t + 1 and the own reads of t, barrier, then the K-tile's MFMAs in one cluster, barrier.  With the
+  // ping-pong offset one group's MFMA cluster runs under the other group's reads.  RAW: t + 1's DMAs (issued two
+  // K-tiles ahead) are waited by every wave before the barrier that precedes their reads; WAR: every wave's reads of
+  // t - 1 completed (lgkmcnt) before a barrier that precedes the restage of its buffer.
+#define LSA_KTILE4(B, BS, t)                                                      \
+  do {                                                                            \
+    read_all(B{});                                                                \
+    stage(I0{}, BS{}, (t) + 3);                                                   \
+    stage(I1{}, BS{}, (t) + 3);                                                   \
+    stage(I2{}, BS{}, (t) + 3);                                                   \
+    stage(I3{}, BS{}, (t) + 3);                                                   \
+    LSA_WAITV(2 * C::WAIT3);                                                      \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                            \
+    __builtin_amdgcn_s_barrier();                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    mma_all();                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    __builtin_amdgcn_s_barrier();                                                 \
+  } while (0)
+    if constexpr (NBUF == 4) {
+      stage(I0{}, I0{}, 0);
+      stage(I1{}, I0{}, 0);
+      stage(I2{}, I0{}, 0);
+      stage(I3{}, I0{}, 0);
+      stage(I0{}, I1{}, 1);
+      stage(I1{}, I1{}, 1);
+      stage(I2{}, I1{}, 1);
+      stage(I3{}, I1{}, 1);
+      stage(I0{}, I2{}, 2);
+      stage(I1{}, I2{}, 2);
+      stage(I2{}, I2{}, 2);
+      stage(I3{}, I2{}, 2);
+      LSA_WAITV(2 * C::WAIT3);
+    } else if constexpr (NBUF == 3) {
       stage(I0{}, I0{}, 0);
       stage(I1{}, I0{}, 0);
       stage(I2{}, I0{}, 0);
@@ -387,7 +447,17 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     // fragment reads + prefetch issue (the >= 2-phase WAR/RAW slack above covers the offset)
     if (wm == 1) __builtin_amdgcn_s_barrier();
     int t = 0;
-    if constexpr (NBUF == 3) {
+    if constexpr (NBUF == 4) {
+      for (; t + 3 < Tl; t += 4) {
+        LSA_KTILE4(I0, I3, t);
+        LSA_KTILE4(I1, I0, t + 1);
+        LSA_KTILE4(I2, I1, t + 2);
+        LSA_KTILE4(I3, I2, t + 3);
+      }
+      if (t < Tl) LSA_KTILE4(I0, I3, t);
+      if (t + 1 < Tl) LSA_KTILE4(I1, I0, t + 1);
+      if (t + 2 < Tl) LSA_KTILE4(I2, I1, t + 2);
+    } else if constexpr (NBUF == 3) {
       for (; t + 2 < Tl; t += 3) {
         LSA_KTILE3(I0, I2, t);
         LSA_KTILE3(I1, I0, t + 1);
@@ -402,6 +472,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
       }
       if (t < Tl) LSA_KTILE(I0, I1, t);
     }
+#undef LSA_KTILE4
 #undef LSA_KTILE3
 #undef LSA_KTILE
 #undef LSA_PHASE
@@ -837,6 +908,13 @@ extern "C" void lsa_gemm_sk_epilogue(int mode) { g_sk_epl = mode ? 1 : 0; }
 // K-tile buffers (lsa_gemm_sk_nbuf): 3 wherever three fit the LDS (default), 2 = the two-buffer schedule everywhere
 static int g_sk_nbuf = 3;
 extern "C" void lsa_gemm_sk_nbuf(int n) { g_sk_nbuf = n == 2 ? 2 : 3; }
+// one-phase schedule (four K-tile buffers, one MFMA cluster per K-tile) for the tiles whose four buffers fit (the
+// 128-row tiles but 128 x 256); lsa_gemm_sk_one_phase(0) restores the four-phase one.  Default on: interleaved A/B at
+// the engine's table configurations (scripts/ab_sk_sched.py, profiles/r6/prefill_gemm_one_phase_ab_mi355x.jsonl):
+// 3B o 2048 rows 50.9 -> 48.7 us warm / 65.0 -> 62.6 cold, 3B down 134.2 -> 130.6 cold, 7B qkv 300 rows 74.7 -> 70.8
+// cold; the 128 x 128 configurations tie
+static int g_sk_one = 1;
+extern "C" void lsa_gemm_sk_one_phase(int on) { g_sk_one = on ? 1 : 0; }
 
 template <int BM, int WN, int KS = 2, int NW = 8>
 static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
@@ -852,6 +930,13 @@ static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const u
   switch (epi) {
 #define LSA_SKL(E)                                                                                                \
   do {                                                                                                            \
+    if constexpr (C::CAN4) {                                                                                      \
+      if (g_sk_one) {                                                                                             \
+        hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 4, KS, NW>), dim3(grid), dim3(64 * NW), 0, stream, x, ldx, \
+                           M, KB, w, NBtot, out, ldo, pl, ws, tickets, re, ne);                                   \
+        break;                                                                                                    \
+      }                                                                                                           \
+    }                                                                                                             \
     if constexpr (C::CAN3) {                                                                                      \
       if (g_sk_nbuf == 3) {                                                                                       \
         hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 3, KS, NW>), dim3(grid), dim3(64 * NW), 0, stream, x, ldx, \

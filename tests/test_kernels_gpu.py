@@ -1089,3 +1089,36 @@ def test_gemm_rope_epilogue(gpu, H, Hkv, T, cfg, rownorm):
     assert _rel(kc.cpu(), kc_r) < 4e-3 and _rel(vc.cpu(), vc_r) < 4e-3
     assert int((kc.cpu() != 0).any(-1).sum()) == T * Hkv  # exactly one appended row per token and kv-head
 
+
+
+@pytest.mark.parametrize("cfg", [4, 5, 12, 13, -2])
+@pytest.mark.parametrize("MK", [(300, 64), (2048, 96), (128, 320), (1100, 1024), (2048, 3072)])
+@pytest.mark.parametrize("epi", ["bf16", "f32", "res", "silu"])
+def test_gemm_stream_k_one_phase(gpu, cfg, MK, epi):
+    """The one-phase four-buffer schedule of the 128-row tiles (ext.gemm_sk_one_phase) vs the fp32 product: short K
+    (fewer K-tiles than buffers), an odd k-step count, stream-K partial tiles and whole tiles (cfg + 8), every
+    epilogue; and bit-identical to the four-phase schedule (same MFMA order per accumulator)."""
+    M, K = MK
+    N = 1536
+    torch.manual_seed(M + K + max(cfg, 0))
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    shape = (M, N // 2 if epi == "silu" else N)
+    dt = torch.float32 if epi in ("f32", "res") else torch.bfloat16
+    h0 = torch.randn(*shape, device=gpu) if epi == "res" else None
+    outs = []
+    for one in (1, 0):
+        ops.ext().gemm_sk_one_phase(one)
+        out = h0.clone() if epi == "res" else torch.empty(*shape, device=gpu, dtype=dt)
+        ops.gemm_sk(x, pw.data, N, out, epi, cfg=None if cfg == -2 else cfg)
+        outs.append(out)
+    ops.ext().gemm_sk_one_phase(1)  # the default
+    torch.cuda.synchronize()
+    y = x.float() @ w.float().t()
+    got = outs[0] - h0 if epi == "res" else outs[0]
+    if epi == "silu":
+        g, u = y.view(M, -1, 2, 16)[:, :, 0].reshape(M, -1), y.view(M, -1, 2, 16)[:, :, 1].reshape(M, -1)
+        y = torch.nn.functional.silu(g) * u
+    assert _rel(got, y) < 1e-2
+    assert torch.equal(outs[0], outs[1])
