@@ -1,0 +1,46 @@
+"""Time to first token under a kernel knob, arms interleaved in one process (cdna_hip_programming.md §5.4 rule 24): a
+one-token request (prefill + first-token commit + host read-back) for each case, median (and min) of the rounds.
+Knob 'one_phase': the stream-K GEMM's one-phase K-loop schedule for the 128-row tiles (ext.gemm_sk_one_phase);
+'none': one arm, the loaded build (cross-build A/Bs: run it under LSA_HIP_SO=variants/<name>.so in turns).
+Usage: ttft_knob_ab.py [knob] [rounds]"""
+import json
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from llm_based_apache_spark_optimization_amd import ops  # noqa: E402
+from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build_engine  # noqa: E402
+
+knob = sys.argv[1] if len(sys.argv) > 1 else "one_phase"
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+KNOBS = {"one_phase": lambda v: ops.ext().gemm_sk_one_phase(v), "none": lambda v: None}
+setk = KNOBS[knob]
+# (model, prompt tokens, requests in the batch): config 3 (3B explain, 2k prompt), config 2 (7B NL->SQL prompt),
+# the headline bench's batch-32 prefill (32 x 128 tokens)
+CASES = [("llama3.2", 2048, 1), ("duckdb-nsql", 300, 1), ("duckdb-nsql", 128, 32)]
+sp = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
+for model, plen, nreq in CASES:
+    eng = build_engine(model, device="cuda:0", dtype="bf16", max_slots=max(2, nreq), max_model_len=plen + 128, seed=0,
+                       max_prefill_tokens=max(16384, plen * nreq))
+    g = torch.Generator().manual_seed(4321)
+    prompts = [[eng.spec.bos_id] + torch.randint(3, eng.spec.vocab_size, (plen - 1,), generator=g).tolist()
+               for _ in range(nreq)]
+    times = {0: [], 1: []}
+    for rnd in range(rounds + 1):
+        for v in (0, 1):
+            setk(v)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            eng.generate(prompts, sp)
+            dt = time.perf_counter() - t
+            if rnd > 0:
+                times[v].append(dt)
+    setk(1)
+    print(json.dumps({"knob": knob, "model": model, "prompt_len": plen, "requests": nreq,
+                      **{f"ttft_ms_{v}": round(1000 * statistics.median(times[v]), 2) for v in (0, 1)},
+                      **{f"min_ms_{v}": round(1000 * min(times[v]), 2) for v in (0, 1)}}), flush=True)
+    del eng
+    torch.cuda.empty_cache()
