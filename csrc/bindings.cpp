@@ -45,6 +45,8 @@ int lsa_attn_decode(const void* q, const void* kc, const void* vc, const int* bl
                     const long long* rowss, float inv_k, float eps, hipStream_t s);
 int lsa_gemm_rr(int K, const void* Wf, int N, void* out, int epi, int nb, int splitk, int waves, int div,
                 const LsaRr* rr, hipStream_t stream);
+int lsa_a8_gemm_rr(int K, const void* Wq, const float* wscale, const void* Sw, int wk, int N, void* out, void* out_s8,
+                   int epi, int nb, int splitk, int waves, int depth, const LsaRr* rr, hipStream_t stream);
 int lsa_kv8_dequant(const void* kc, const void* vc, const float* ks, const float* vs, const int* block_tables,
                     int max_blocks, const int* ctx_lens, int nseq, int Hkv, int mb, void* ko, void* vo, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
@@ -71,16 +73,15 @@ void lsa_gemm_sk_one_phase(int on);
 int lsa_gemm_sk_rope(const void* X, int ldx, int M, int K, const void* Wf, int N, float* ws, int* tickets, int ncu,
                      int min_share, int cfg, const int* pos, const int* tok_seq, const int* block_tables,
                      int max_blocks, const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int H,
-                     int Hkv, int* grid_out, int* cfg_out, const LsaEpi* ne, hipStream_t stream);
+                     int Hkv, int* grid_out, int* cfg_out, hipStream_t stream);
 int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
-                int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, const LsaEpi* ne,
-                hipStream_t stream);
+                int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 int lsa_silu_bf16(const void* y, int M, int F, void* out, hipStream_t s);
 void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                        const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
-                       void* out, int ng, int split, float* opart, float* mlpart, int* tickets, hipStream_t s);
+                       void* out, int ng, hipStream_t s);
 int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
 int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
                       void* out, int epi, int splitk, hipStream_t stream);
@@ -348,6 +349,62 @@ void a8_gemm(const at::Tensor& x8, const c10::optional<at::Tensor>& s8, const c1
         "a8_gemm");
 }
 
+// W8A8 / W4A8 batch-1 decode GEMM with the residual-reduce prologue (kernels/gemm_fp8a.hip RR): X = h + sum_s parts[s]
+// quantised in the prologue (e4m3, one E8M0 scale per 32 k); h_out = X.  epi 1: f32 slabs [splitk, 1, N] (ss_out[0] +=
+// sum X^2, the slab consumer scales the row); epi 2: the e4m3 SiLU output in the xf8 layout + E8M0 blocks in out_s8
+// (splitk 1, the row scale from the workgroup's own full-row sum).
+void a8_gemm_rr(const at::Tensor& h, const at::Tensor& parts, at::Tensor& h_out, const at::Tensor& wq,
+                const c10::optional<at::Tensor>& wscale, const c10::optional<at::Tensor>& wsc8, int64_t N, at::Tensor& out,
+                const c10::optional<at::Tensor>& out_s8, int64_t epi, int64_t nb, int64_t splitk, int64_t waves,
+                int64_t depth, const c10::optional<at::Tensor>& ss_out, double eps) {
+  const bool fp4 = wsc8.has_value();
+  TORCH_CHECK(fp4 != wscale.has_value(), "a8_gemm_rr: exactly one of wscale (fp8) / wsc8 (mxfp4)");
+  need(h, at::kFloat, "h");
+  need(h_out, at::kFloat, "h_out");
+  need(parts, at::kFloat, "parts");
+  const int64_t K = h.numel();
+  TORCH_CHECK(K % 128 == 0 && N % 16 == 0, "a8_gemm_rr: K % 128 == 0, N % 16 == 0");
+  TORCH_CHECK(h.is_contiguous() && h_out.is_contiguous() && h_out.numel() >= K, "a8_gemm_rr: h / h_out contiguous [K]");
+  TORCH_CHECK(h.data_ptr() != h_out.data_ptr(), "a8_gemm_rr: h_out must not alias h");
+  TORCH_CHECK(parts.dim() == 3 && parts.size(1) == 1 && parts.size(2) == K && parts.stride(2) == 1 &&
+                  parts.stride(1) == K, "a8_gemm_rr: parts must be [np, 1, K] slabs");
+  TORCH_CHECK(on_dev(wq) && wq.element_size() == 1 && wq.numel() == (fp4 ? N * K / 2 : N * K), "a8_gemm_rr: weight bytes");
+  if (fp4) {
+    TORCH_CHECK(on_dev(*wsc8) && wsc8->numel() * wsc8->element_size() >= (N / 16) * ((K / 128 + 3) / 4) * 256,
+                "a8_gemm_rr: mxfp4 scales too small");
+  } else {
+    need(*wscale, at::kFloat, "wscale");
+    TORCH_CHECK(wscale->numel() >= N, "a8_gemm_rr: wscale too small");
+  }
+  TORCH_CHECK(epi == 1 || epi == 2, "a8_gemm_rr: f32 slabs or the e4m3 SiLU output");
+  if (epi == 2) {
+    TORCH_CHECK(on_dev(out) && out.element_size() == 1 && out.numel() >= 16 * (N / 2), "a8_gemm_rr: e4m3 SiLU out too small");
+    TORCH_CHECK(out_s8.has_value() && on_dev(*out_s8) && out_s8->element_size() == 1 && out_s8->numel() >= 64 * (N / 2 / 128) &&
+                    (N / 2) % 128 == 0, "a8_gemm_rr: the e4m3 SiLU output needs out_s8 (and N / 2 % 128 == 0)");
+  } else {
+    check_out(epi, out, splitk, 1, N, 0);
+  }
+  LsaRr rr{};
+  rr.h = h.data_ptr<float>();
+  rr.parts = parts.data_ptr<float>();
+  rr.pstride = parts.stride(0);
+  rr.np = (int)parts.size(0);
+  rr.h_out = h_out.data_ptr<float>();
+  rr.local = epi == 2 ? 1 : 0;
+  rr.inv_k = 1.0f / (float)K;
+  rr.eps = (float)eps;
+  if (epi == 1) {
+    TORCH_CHECK(ss_out.has_value(), "a8_gemm_rr: f32 slabs need ss_out");
+    need(*ss_out, at::kLong, "ss_out");
+    rr.ss_out = reinterpret_cast<long long*>(ss_out->data_ptr<int64_t>());
+  }
+  check(lsa_a8_gemm_rr((int)K, wq.data_ptr(), fp4 ? nullptr : wscale->data_ptr<float>(),
+                       fp4 ? wsc8->data_ptr() : nullptr, fp4 ? 1 : 0, (int)N, out.data_ptr(),
+                       out_s8.has_value() ? out_s8->data_ptr() : nullptr, (int)epi, (int)nb, (int)splitk, (int)waves,
+                       (int)depth, &rr, cur_stream()),
+        "a8_gemm_rr");
+}
+
 void quant_xf8_blocks(const at::Tensor& x, int64_t mt, int64_t blk, at::Tensor& x8, at::Tensor& s8) {
   need(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
@@ -373,35 +430,8 @@ void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) 
 // 1 f32 [M][N], 2 SiLU(gate) * up bf16 [M][N / 2], 3 h f32 [M][N] += x @ W^T.  ws / tickets: the per-stream
 // workspace (ops._sk_workspace).  cfg: -1 = the kernel's cost model, else a tile configuration index (+ 8: whole
 // tiles only; + 16 + 32 * mode: that epilogue mode for this call).  Returns grid * 16 + the configuration used.
-// norm-free prefill extensions of the stream-K GEMM (kernels/lsa_epi.h): rowss [M] int64 Q24 -> the output rows (bf16 /
-// RoPE epilogues) scaled by rsqrt(rowss / K + eps); with epi 3, xout bf16 [M][N] + ss_out [M] int64 Q24 (accumulated)
-// receive bf16(h) and the row sums of h^2
-LsaEpi sk_norm_epi(int64_t epi, int64_t M, int64_t N, int64_t K, const c10::optional<at::Tensor>& rowss, double eps,
-                   const c10::optional<at::Tensor>& xout, const c10::optional<at::Tensor>& ss_out) {
-  LsaEpi e{};
-  if (rowss.has_value()) {
-    need(*rowss, at::kLong, "rowss");
-    TORCH_CHECK(epi == 0 || epi == 4, "rowss: bf16 / RoPE epilogues only");
-    TORCH_CHECK(rowss->numel() >= M, "rowss too small");
-    e.rowss = reinterpret_cast<const long long*>(rowss->data_ptr<int64_t>());
-    e.inv_k = 1.0f / (float)K;
-    e.eps = (float)eps;
-  }
-  TORCH_CHECK(xout.has_value() == ss_out.has_value(), "xout and ss_out go together");
-  if (xout.has_value()) {
-    TORCH_CHECK(epi == 3, "xout / ss_out: residual epilogue only");
-    need(*xout, at::kBFloat16, "xout");
-    need(*ss_out, at::kLong, "ss_out");
-    TORCH_CHECK(xout->is_contiguous() && xout->numel() >= M * N && ss_out->numel() >= M, "xout / ss_out too small");
-    e.xout = reinterpret_cast<uint16_t*>(xout->data_ptr());
-    e.ss_out = reinterpret_cast<long long*>(ss_out->data_ptr<int64_t>());
-  }
-  return e;
-}
-
 int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, at::Tensor& ws,
-                at::Tensor& tickets, int64_t ncu, int64_t min_share, int64_t cfg, const c10::optional<at::Tensor>& rowss,
-                double eps, const c10::optional<at::Tensor>& xout, const c10::optional<at::Tensor>& ss_out) {
+                at::Tensor& tickets, int64_t ncu, int64_t min_share, int64_t cfg) {
   need(x, at::kBFloat16, "x");
   need(wf, at::kBFloat16, "wf");
   need(ws, at::kFloat, "ws");
@@ -421,10 +451,9 @@ int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor
     TORCH_CHECK(out.numel() >= (int64_t)M * (epi == 2 ? N / 2 : N), "bf16 out too small");
   }
   TORCH_CHECK(cfg >= -1 && cfg < 64, "gemm_sk: cfg");
-  const LsaEpi ne = sk_norm_epi(epi, M, N, K, rowss, eps, xout, ss_out);
   int grid = 0, used = 0;
   check(lsa_gemm_sk(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), (int)epi, ws.data_ptr<float>(),
-                    tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, &grid, &used, &ne, cur_stream()),
+                    tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, &grid, &used, cur_stream()),
         "gemm_sk");
   return (int64_t)grid * 16 + used;
 }
@@ -435,8 +464,7 @@ int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor
 int64_t gemm_sk_rope(const at::Tensor& x, const at::Tensor& wf, at::Tensor& ws, at::Tensor& tickets, int64_t ncu,
                      int64_t min_share, int64_t cfg, const at::Tensor& pos, const c10::optional<at::Tensor>& tok_seq,
                      const at::Tensor& block_tables, const at::Tensor& cos_t, const at::Tensor& sin_t,
-                     at::Tensor& q_out, at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv,
-                     const c10::optional<at::Tensor>& rowss, double eps) {
+                     at::Tensor& q_out, at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv) {
   need(x, at::kBFloat16, "x");
   need(wf, at::kBFloat16, "wf");
   need(ws, at::kFloat, "ws");
@@ -462,13 +490,12 @@ int64_t gemm_sk_rope(const at::Tensor& x, const at::Tensor& wf, at::Tensor& ws, 
   }
   TORCH_CHECK(ncu >= 8 && ncu <= 1024 && ws.numel() * 4 >= lsa_gemm_sk_ws_bytes((int)ncu) &&
                   tickets.numel() >= lsa_gemm_sk_tickets((int)ncu), "gemm_sk_rope: workspace too small");
-  const LsaEpi ne = sk_norm_epi(4, M, N, K, rowss, eps, c10::nullopt, c10::nullopt);
   int grid = 0, used = 0;
   check(lsa_gemm_sk_rope(x.data_ptr(), x.stride(0), (int)M, (int)K, wf.data_ptr(), (int)N, ws.data_ptr<float>(),
                          tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, pos.data_ptr<int>(),
                          ptr<int>(tok_seq), block_tables.data_ptr<int>(), (int)block_tables.size(1),
                          cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), q_out.data_ptr(), kc.data_ptr(),
-                         vc.data_ptr(), (int)H, (int)Hkv, &grid, &used, &ne, cur_stream()),
+                         vc.data_ptr(), (int)H, (int)Hkv, &grid, &used, cur_stream()),
         "gemm_sk_rope");
   return (int64_t)grid * 16 + used;
 }
@@ -754,8 +781,7 @@ void kv8_dequant(const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& k
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                   const at::Tensor& cu_q, const at::Tensor& ctx_lens, const at::Tensor& work, int64_t H, int64_t Hkv,
-                  double scale, at::Tensor& out, int64_t rows32, const c10::optional<at::Tensor>& opart,
-                  const c10::optional<at::Tensor>& mlpart, const c10::optional<at::Tensor>& tickets) {
+                  double scale, at::Tensor& out, int64_t rows32) {
   need(q, at::kBFloat16, "q");
   need(work, at::kInt, "work");
   need(cu_q, at::kInt, "cu_q");
@@ -766,40 +792,13 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& v
   TORCH_CHECK(cu_q.numel() == ctx_lens.numel() + 1 && block_tables.size(0) >= ctx_lens.numel(),
               "cu_q [nseq + 1], ctx_lens [nseq], block_tables [>= nseq, max_blocks]");
   if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip)
-    // rows32 1: work [n_workgroups, 4 * NG] of (seq, q_start, t0, t1); 3: split pieces, [n, 8 * NG] of (seq, q_start,
-    // t0, t1, block slot, piece, -, -) with partial buffers for (max block slot + 1) * H slots (ops.prefill_plan)
-    const bool split = rows32 == 3;
-    TORCH_CHECK(rows32 == 1 || split, "attn_prefill: rows32 must be 0, 1 or 3");
-    const int wi = split ? 8 : 4;
-    TORCH_CHECK(work.dim() == 2 && (work.size(1) == wi || work.size(1) == 2 * wi) && work.is_contiguous(),
-                "attn_prefill32 work must be [n, 4 or 8 per group] int32");
-    float *op = nullptr, *mp = nullptr;
-    int* tk = nullptr;
-    if (split) {
-      TORCH_CHECK(opart && mlpart && tickets, "attn_prefill split: partial buffers required");
-      need(*opart, at::kFloat, "opart");
-      need(*mlpart, at::kFloat, "mlpart");
-      need(*tickets, at::kInt, "tickets");
-      // every slot field must address the buffers: checked on the host copy of the plan
-      const at::Tensor wc = work.to(at::kCPU);
-      const int* w = wc.data_ptr<int>();
-      int64_t max_slot = -1;
-      for (int64_t i = 0; i < work.numel() / 8; ++i)
-        if (w[8 * i] >= 0 && w[8 * i + 4] >= 0) {
-          TORCH_CHECK(w[8 * i + 5] == 0 || w[8 * i + 5] == 1, "attn_prefill split: piece must be 0 or 1");
-          max_slot = std::max<int64_t>(max_slot, w[8 * i + 4]);
-        }
-      const int64_t slots = (max_slot + 1) * H;
-      TORCH_CHECK(opart->numel() >= slots * 2 * 4 * 4096 && mlpart->numel() >= slots * 2 * 4 * 64 * 2 &&
-                      tickets->numel() >= slots, "attn_prefill split: partial buffers too small for the plan");
-      op = opart->data_ptr<float>();
-      mp = mlpart->data_ptr<float>();
-      tk = tickets->data_ptr<int>();
-    }
+    // work [n_workgroups, 4 * NG] of (seq, q_start, t0, t1) (ops.prefill_plan)
+    TORCH_CHECK(rows32 == 1, "attn_prefill: rows32 must be 0 or 1");
+    TORCH_CHECK(work.dim() == 2 && (work.size(1) == 4 || work.size(1) == 8) && work.is_contiguous(),
+                "attn_prefill32 work must be [n, 4 per group] int32");
     check(lsa_attn_prefill32(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                              block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
-                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / wi), split ? 1 : 0,
-                             op, mp, tk, cur_stream()),
+                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 4), cur_stream()),
           "attn_prefill32");
     return;
   }
@@ -996,8 +995,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("ws"),
-        py::arg("tickets"), py::arg("ncu"), py::arg("min_share") = 0, py::arg("cfg") = -1, py::arg("rowss") = py::none(),
-        py::arg("eps") = 0.0, py::arg("xout") = py::none(), py::arg("ss_out") = py::none());
+        py::arg("tickets"), py::arg("ncu"), py::arg("min_share") = 0, py::arg("cfg") = -1);
   m.def("gemm_sk_rope", &gemm_sk_rope);
   m.def("gemm_sk_epilogue", [](int64_t mode) { lsa_gemm_sk_epilogue((int)mode); });
   m.def("gemm_sk_nbuf", [](int64_t n) { lsa_gemm_sk_nbuf((int)n); });
@@ -1048,13 +1046,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("unsplit_max") = 4,
         py::arg("ks") = py::none(), py::arg("vs") = py::none(), py::arg("out_s8") = py::none(),
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("hidden") = 0);
+  m.def("a8_gemm_rr", &a8_gemm_rr, py::arg("h"), py::arg("parts"), py::arg("h_out"), py::arg("wq"), py::arg("wscale"),
+        py::arg("wsc8"), py::arg("N"), py::arg("out"), py::arg("out_s8"), py::arg("epi"), py::arg("nb"), py::arg("splitk"),
+        py::arg("waves"), py::arg("depth"), py::arg("ss_out") = py::none(), py::arg("eps") = 1e-5);
   m.def("gemm_rr", &gemm_rr, py::arg("h"), py::arg("parts"), py::arg("h_out"), py::arg("wf"), py::arg("N"),
         py::arg("out"), py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves"), py::arg("div"),
         py::arg("ss_out") = py::none(), py::arg("eps") = 1e-5);
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
-        py::arg("out"), py::arg("rows32") = 0, py::arg("opart") = py::none(), py::arg("mlpart") = py::none(),
-        py::arg("tickets") = py::none());
+        py::arg("out"), py::arg("rows32") = 0);
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);
   m.def("fp8_dequant", &fp8_dequant);

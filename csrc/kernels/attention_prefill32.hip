@@ -18,9 +18,6 @@
 #include "common.h"
 
 #define LSA_NEG_P (-1.0e30f)
-#define LSA_P32_SC1 16  // buffer cache-policy aux bit: sc1 (write-through store / L1-bypassing load)
-typedef __attribute__((address_space(1))) int lsa_p32_g_i32;
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 #ifndef LSA_P32_NBUF1
 #define LSA_P32_NBUF1 2  // K / V tile buffers of the single-group (NG = 1) kernel: the DMA runs NBUF - 1 tiles
                          // ahead.  4 (128 KiB, 3 tiles ahead) measured slower: one workgroup per CU instead of two
@@ -97,39 +94,28 @@ __device__ __forceinline__ int vp_off(int r, int col) { return r * 128 + ((((col
 // Work item of a group: (seq, q_start, t0, t1) -- the key tiles [t0, t1) of one 128-row query block (the
 // whole causal range: t0 = 0; cutting heavy blocks into KV splits with a merge launch, or into two halves
 // merged in LDS, were both measured slower and removed: profiles/attn_prefill_kv_split_mi355x.jsonl,
-// profiles/attn_prefill_halves_mi355x.jsonl).
+// profiles/attn_prefill_halves_mi355x.jsonl; round 5's split merged inside the same launch through write-through
+// partials and a ticket measured slower too, profiles/r5/attn_prefill_kv_split_inlaunch_ab_mi355x.jsonl, and was
+// removed in round 6).
 //
 // O is accumulated TRANSPOSED, O^T += V^T P^T (A = V^T from the transposed LDS reads, B = P^T straight
 // from the S^T accumulator): the accumulator's column is then the query row = the lane, so the online-
 // softmax rescale and the final 1 / l are lane-local multiplies (no cross-lane shuffles), and each lane
 // stores 4 contiguous dims of its own row per register group.
 //
-// SPLIT (work items of 8 ints: seq, q_start, t0, t1, slot, piece, -, -): a heavy causal query block is cut into two
-// key-tile ranges run by two groups (usually of different workgroups) so the longest serial tile chain halves.  Each
-// piece of a split block publishes its unnormalised O^T, row max and row sum write-through (sc1) into its half of
-// `slot`, drains, and takes the slot's ticket (one relaxed agent-scope add per group); the second to arrive merges
-// the other's partial (log-sum-exp in the exp2 domain) and writes the output -- nothing waits on another group, so
-// residency never matters (MI355X_MICROARCH.md hand-off row 1).
-struct P32Split {
-  float* opart;   // [slot][piece][wave 4][db 4][q 4][lane 64][4]
-  float* mlpart;  // [slot][piece][wave 4][lane 64][2]
-  int* tickets;   // [slot], zero between calls (the merging group resets its slot's)
-};
-
 // Diagnostic cycle stamps (STAMP instantiations only, scripts/p32_stamps.py): per wave, the s_memtime cycles of each
 // tile-loop segment summed over its tiles -> stamps[((wi * H + h) * NG + gi) * 4 + w][8]:
 //   0 DMA issue, 1 QK^T + mask + row max, 2 softmax, 3 PV issue, 4 DMA wait, 5 barrier, 6 tiles | nt_max << 32, 7 whole kernel
 __device__ unsigned long long* g_p32_stamps = nullptr;
 
-template <int NG, bool SPLIT = false, bool STAMP = false>
+template <int NG, bool STAMP = false>
 __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                                      const uint16_t* __restrict__ vc,
                                                                      const int* __restrict__ block_tables, int max_blocks,
                                                                      const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
                                                                      const int* __restrict__ work, int H, int Hkv,
-                                                                     float scale_log2, uint16_t* __restrict__ out,
-                                                                     P32Split sp) {
-  constexpr int WI = SPLIT ? 8 : 4;  // ints per work item
+                                                                     float scale_log2, uint16_t* __restrict__ out) {
+  constexpr int WI = 4;  // ints per work item
   constexpr int D = 128;
   unsigned long long sg[6] = {0, 0, 0, 0, 0, 0}, st_t0 = 0, st_prev = 0;
   unsigned st_tiles = 0;
@@ -160,7 +146,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   const int hk = h / (H / Hkv);
 
   // tiles of every group (the loop runs to the largest; the barriers are workgroup-wide)
-  int nt_max = 0, ntiles = 0, seq = 0, qs = 0, t0 = 0, t1 = 0, slot = -1, piece = 0;
+  int nt_max = 0, ntiles = 0, seq = 0, qs = 0, t0 = 0, t1 = 0;
   int o_nt = 0, o_seq = 0, o_t0 = 0;  // the partner group's item (HELP)
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
@@ -170,16 +156,9 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
     nt_max = max(nt_max, nt);
     if (g == gi) {
       ntiles = nt; seq = sq; qs = wk[1]; t0 = wk[2]; t1 = wk[3];
-      if constexpr (SPLIT) {
-        slot = sq >= 0 ? wk[4] : -1;
-        piece = wk[5];
-      }
     } else {
       o_nt = nt; o_seq = sq >= 0 ? sq : 0; o_t0 = wk[2];
     }
-  }
-  if constexpr (SPLIT) {  // a (head, block) pair of pieces owns slot + H * block-slot: distinct heads, distinct slots
-    if (slot >= 0) slot = slot * H + h;
   }
   const bool active = seq >= 0;
   const int sqc = active ? seq : 0;
@@ -220,11 +199,11 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   const unsigned kl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Ks[gi][0][4 * w * D]));
   const unsigned vl0 = __builtin_amdgcn_readfirstlane(lds_addr(&Vs[gi][0][4 * w * D]));
-  // HELP (paired groups, unsplit): once a group has computed its last tile it issues its partner's K / V DMAs, so
+  // HELP (paired groups): once a group has computed its last tile it issues its partner's K / V DMAs, so
   // the heavy causal block's waves -- the launch's critical path -- stop paying ~420 cycles of LDS-DMA issue per tile
   // (scripts/p32_stamps.py).  Same kv-head, the partner's own block table and LDS images; every wave still drains
   // its DMAs (vmcnt(0), two buffers) before the barrier that publishes the tile.
-  constexpr bool HELP = NG == 2 && !SPLIT;
+  constexpr bool HELP = NG == 2;
   const int* bt_o = block_tables + (size_t)o_seq * max_blocks;
   const unsigned kl0_o = __builtin_amdgcn_readfirstlane(lds_addr(&Ks[NG - 1 - gi][0][4 * w * D]));
   const unsigned vl0_o = __builtin_amdgcn_readfirstlane(lds_addr(&Vs[NG - 1 - gi][0][4 * w * D]));
@@ -398,54 +377,6 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   }
   // normalise and store: lane = query row r32; register group gq of o[db] = dims 32 db + 8 gq + 4 hh + 0..3
   const int qr = qs + w * 32 + r32;
-  if constexpr (SPLIT) {
-    // piece of a split block: publish, ticket, the second to arrive merges (every thread of the workgroup passes the
-    // two barriers below; groups without a slot skip the rest)
-    __shared__ int s_last[NG];
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(sp.opart, 0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(sp.mlpart, 0, 0x7fffffff, 0x00020000);
-    auto obase = [&](int pc) { return (uint32_t)(((slot * 2 + pc) * 4 + w) * 4096 + lane * 4) * 4u; };
-    auto mbase = [&](int pc) { return (uint32_t)(((slot * 2 + pc) * 4 + w) * 64 + lane) * 8u; };
-    if (slot >= 0) {
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const u32x4_t u = {__float_as_uint(o[db][4 * gq]), __float_as_uint(o[db][4 * gq + 1]),
-                             __float_as_uint(o[db][4 * gq + 2]), __float_as_uint(o[db][4 * gq + 3])};
-          __builtin_amdgcn_raw_buffer_store_b128(u, ro, obase(piece), (db * 4 + gq) * 1024, LSA_P32_SC1);
-        }
-      const u32x2_t ml = {__float_as_uint(mrow), __float_as_uint(lrow)};
-      __builtin_amdgcn_raw_buffer_store_b64(ml, rm, mbase(piece), 0, LSA_P32_SC1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through partial
-    __syncthreads();
-    if (slot >= 0 && (tid & 255) == 0)
-      s_last[gi] = __hip_atomic_fetch_add((lsa_p32_g_i32*)sp.tickets + slot, 1, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT) == 1;
-    __syncthreads();
-    if (slot < 0) {
-      // unsplit item: normal epilogue below
-    } else if (!s_last[gi]) {
-      return;
-    } else {
-      if ((tid & 255) == 0) __hip_atomic_store((lsa_p32_g_i32*)sp.tickets + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int other = piece ^ 1;
-      const u32x2_t mo = __builtin_amdgcn_raw_buffer_load_b64(rm, mbase(other), 0, LSA_P32_SC1);
-      const float m2 = __uint_as_float(mo[0]), l2 = __uint_as_float(mo[1]);
-      const float mm = fmaxf(mrow, m2);
-      const float a1 = __builtin_amdgcn_exp2f(mrow - mm), a2 = __builtin_amdgcn_exp2f(m2 - mm);
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const u32x4_t u = __builtin_amdgcn_raw_buffer_load_b128(ro, obase(other), (db * 4 + gq) * 1024, LSA_P32_SC1);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) o[db][4 * gq + c] = o[db][4 * gq + c] * a1 + __uint_as_float(u[c]) * a2;
-        }
-      lrow = lrow * a1 + l2 * a2;
-    }
-  }
   if (active && qr < qlen) {
     const float inv = lrow > 0.f ? 1.f / lrow : 0.f;
     uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D + 4 * hh;
@@ -470,32 +401,27 @@ extern "C" int lsa_p32_set_stamps(void* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_p32_stamps), &v, sizeof(v));
 }
 
-// work: NG (seq, q_start, t0, t1) items per workgroup (seq < 0: that group idles), nwork workgroups; split: 8-int items
-// (+ slot, piece) with the partial buffers of P32Split
+// work: NG (seq, q_start, t0, t1) items per workgroup (seq < 0: that group idles), nwork workgroups
 extern "C" int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                   const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv,
-                                  float scale, void* out, int ng, int split, float* opart, float* mlpart, int* tickets,
-                                  hipStream_t s) {
+                                  float scale, void* out, int ng, hipStream_t s) {
   if (nwork <= 0) return 0;
   if (H % Hkv) return -1;
-  if (split && (!opart || !mlpart || !tickets)) return -3;
   if (ng != 1 && ng != 2) return -2;
   dim3 grid(nwork, H);
   const float sl2 = scale * 1.4426950408889634f;
-  const P32Split sp{opart, mlpart, tickets};
-#define LSA_P32_LAUNCH(NGV, SPV, STV)                                                                           \
-  hipLaunchKernelGGL((attn_prefill32_kernel<NGV, SPV, STV>), grid, dim3(256 * NGV), 0, s,                        \
+#define LSA_P32_LAUNCH(NGV, STV)                                                                                \
+  hipLaunchKernelGGL((attn_prefill32_kernel<NGV, STV>), grid, dim3(256 * NGV), 0, s,                             \
                      reinterpret_cast<const uint16_t*>(q), reinterpret_cast<const uint16_t*>(kc),                 \
                      reinterpret_cast<const uint16_t*>(vc), block_tables, max_blocks, cu_q, ctx_lens, work, H, Hkv, \
-                     sl2, reinterpret_cast<uint16_t*>(out), sp)
-#define LSA_P32_NG(SPV, STV)               \
-  do {                                     \
-    if (ng == 2) LSA_P32_LAUNCH(2, SPV, STV); \
-    else LSA_P32_LAUNCH(1, SPV, STV);         \
+                     sl2, reinterpret_cast<uint16_t*>(out))
+#define LSA_P32_NG(STV)                  \
+  do {                                   \
+    if (ng == 2) LSA_P32_LAUNCH(2, STV); \
+    else LSA_P32_LAUNCH(1, STV);         \
   } while (0)
-  if (split) LSA_P32_NG(true, false);
-  else if (g_p32_stamps_on) LSA_P32_NG(false, true);  // diagnostic build of the unsplit kernel (lsa_p32_set_stamps)
-  else LSA_P32_NG(false, false);
+  if (g_p32_stamps_on) LSA_P32_NG(true);  // diagnostic build of the kernel (lsa_p32_set_stamps)
+  else LSA_P32_NG(false);
 #undef LSA_P32_NG
 #undef LSA_P32_LAUNCH
   return (int)hipGetLastError();

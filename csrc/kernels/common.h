@@ -145,31 +145,6 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 
 __device__ __forceinline__ float wave_sum(float v) { return lsa_sum_x32(lsa_sum_x16(lsa_row16_sum(v))); }
 
-// Eight wave sums at once (reduce-scatter): lane L ends with the 64-lane sum of v[((L >> 5) & 1) * 4 + ((L >> 4) & 1)
-// * 2 + ((L >> 3) & 1)], in all 8 lanes of its group.  Each exchange halves the values a lane carries: the swaps with
-// two different operands hand lanes < 32 (rows 0 / 2) the first operand's pair sums and the others the second's, the
-// xor-8 step selects by lane bit 3, and the last three DPP steps sum the 8-lane group -- 10 cross-lane ops for 8 rows
-// instead of 8 x 6.  Whole wave active.
-__device__ __forceinline__ float lsa_sum8_scatter(const float (&v)[8]) {
-  const int lane = threadIdx.x & 63;
-  float s[4], u[2];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[q]), __float_as_uint(v[q + 4]), false, false);
-    s[q] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s[p]), __float_as_uint(s[p + 2]), false, false);
-    u[p] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-  const bool b3 = lane & 8;
-  float d = (b3 ? u[1] : u[0]) + lsa_xor8(b3 ? u[0] : u[1]);
-  d += lsa_dpp<LSA_DPP_HALF_MIRROR>(d);
-  d += lsa_dpp<LSA_DPP_XOR2>(d);
-  return d + lsa_dpp<LSA_DPP_XOR1>(d);
-}
-
 __device__ __forceinline__ float wave_max(float v) { return lsa_max_x32(lsa_max_x16(lsa_row16_max(v))); }
 
 // block-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats

@@ -55,13 +55,22 @@ __device__ __forceinline__ f32x4_t mfma_blk(const uint4 a0, const uint4 a1, int 
 
 }  // namespace
 
-template <int MT, int NB, int EPI, int WAVES, int U, int XFO, int WK, bool ASC>
+// RR > 0 (batch 1): the residual-reduce prologue of lsa_epi.h LsaRr (gemm.hip has the 16-bit form): X = h + sum of the
+// previous projection's f32 split-K slabs over this split's K slice, quantised in the prologue to e4m3 with one E8M0
+// scale per 32 k (the MFMA's B scale operand) into an LDS image of row 0's xf8 bytes (128 B + 4 scale bytes per k128
+// step; the 16 lanes of a row group read one address), so no quantising norm launch precedes the GEMM.  RR = the most
+// slabs summed (loads clamped to slab np - 1 and masked).  The row's RMS scale: rr.local (splitk 1) from the
+// workgroup's own full-row sum in the epilogue, else the column-0 workgroups add the slice's sum of squares to
+// rr.ss_out for the slab consumer.
+#define A8_RR_KMAX 8192
+template <int MT, int NB, int EPI, int WAVES, int U, int XFO, int WK, bool ASC, int RR = 0>
 __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4* __restrict__ X8, const uint8_t* __restrict__ S8,
                                                                     const float* __restrict__ sx, int M, int KB128,
                                                                     const uint4* __restrict__ Wq, const float* __restrict__ wscale,
                                                                     const uint32_t* __restrict__ Sw, void* __restrict__ out,
                                                                     uint8_t* __restrict__ out_s8, int ldo, int kb_per_split,
-                                                                    LsaEpi ep) {
+                                                                    LsaEpi ep, LsaRr rr) {
+  static_assert(RR == 0 || (MT == 1 && ASC), "residual-reduce prologue: batch 1, block-scaled activations");
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -97,8 +106,11 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
     }
   }
   const uint4* xp = X8 + 2 * lane;
+  // RR: row 0's xf8 bytes of the slice (lane group g of k128-step s at [s][g][32 B]) and its E8M0 bytes [s][g]
+  __shared__ __attribute__((aligned(16))) uint4 x8s[RR ? A8_RR_KMAX / 16 : 1];
+  __shared__ uint8_t s8s[RR ? A8_RR_KMAX / 32 : 1];
 
-  auto load = [&](uint4 (&wr)[U][NB][2], int (&sa)[U][NB], uint4 (&xr)[U][MT][2], int (&sb)[U][MT], int c) {
+  auto wload = [&](uint4 (&wr)[U][NB][2], int (&sa)[U][NB], int c) {
     const int kb = kbA + c * U;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -116,17 +128,30 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
         }
       }
     }
+  };
+  auto xload = [&](uint4 (&xr)[U][MT][2], int (&sb)[U][MT], int c) {
+    const int kb = kbA + c * U;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kk = min(kb + u, kbB - 1);
 #pragma unroll
       for (int j = 0; j < MT; ++j) {
-        const uint4* px = xp + (size_t)(kk * MT + j) * 128;
-        xr[u][j][0] = px[0];
-        xr[u][j][1] = px[1];
-        sb[u][j] = ASC ? (int)S8[(size_t)(kk * MT + j) * 64 + lane] : 0x7f;
+        if constexpr (RR > 0) {
+          xr[u][j][0] = x8s[(kk - kbA) * 8 + 2 * g];
+          xr[u][j][1] = x8s[(kk - kbA) * 8 + 2 * g + 1];
+          sb[u][j] = (int)s8s[(kk - kbA) * 4 + g];
+        } else {
+          const uint4* px = xp + (size_t)(kk * MT + j) * 128;
+          xr[u][j][0] = px[0];
+          xr[u][j][1] = px[1];
+          sb[u][j] = ASC ? (int)S8[(size_t)(kk * MT + j) * 64 + lane] : 0x7f;
+        }
       }
     }
+  };
+  auto load = [&](uint4 (&wr)[U][NB][2], int (&sa)[U][NB], uint4 (&xr)[U][MT][2], int (&sb)[U][MT], int c) {
+    wload(wr, sa, c);
+    xload(xr, sb, c);
   };
   auto comp = [&](const uint4 (&wr)[U][NB][2], const int (&sa)[U][NB], const uint4 (&xr)[U][MT][2], const int (&sb)[U][MT],
                   int c) {
@@ -148,10 +173,65 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
       }
     }
   };
+  uint4 wA[U][NB][2], xA[U][MT][2], wB[U][NB][2], xB[U][MT][2];
+  int saA[U][NB], sbA[U][MT], saB[U][NB], sbB[U][MT];
+  float rr_scale = 1.f;
+  if constexpr (RR > 0) {
+    if (n_it > 0) wload(wA, saA, w);  // the first weight chunk does not depend on X: in flight during the prologue
+    __shared__ float rr_red[WAVES];
+    const int k0 = kbA * 128, n8 = nk * 16;  // 8-value groups of the slice; 4 consecutive groups = one 32-k block
+    const bool wr_h = blockIdx.x == 0;
+    float ssl = 0.f;
+    for (int i = threadIdx.x; i < n8; i += 64 * WAVES) {
+      const size_t e = (size_t)k0 + 8 * i;
+      float4 a[RR + 1][2];
+      a[0][0] = *reinterpret_cast<const float4*>(rr.h + e);
+      a[0][1] = *reinterpret_cast<const float4*>(rr.h + e + 4);
+#pragma unroll
+      for (int s2 = 0; s2 < RR; ++s2) {
+        const float* p = rr.parts + (size_t)min(s2, rr.np - 1) * rr.pstride + e;
+        a[s2 + 1][0] = *reinterpret_cast<const float4*>(p);
+        a[s2 + 1][1] = *reinterpret_cast<const float4*>(p + 4);
+      }
+      float v[8] = {a[0][0].x, a[0][0].y, a[0][0].z, a[0][0].w, a[0][1].x, a[0][1].y, a[0][1].z, a[0][1].w};
+#pragma unroll
+      for (int s2 = 0; s2 < RR; ++s2) {
+        const float on = s2 < rr.np ? 1.f : 0.f;
+        v[0] += on * a[s2 + 1][0].x; v[1] += on * a[s2 + 1][0].y; v[2] += on * a[s2 + 1][0].z; v[3] += on * a[s2 + 1][0].w;
+        v[4] += on * a[s2 + 1][1].x; v[5] += on * a[s2 + 1][1].y; v[6] += on * a[s2 + 1][1].z; v[7] += on * a[s2 + 1][1].w;
+      }
+      float am = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ssl += v[j] * v[j];
+        am = fmaxf(am, fabsf(v[j]));
+      }
+      if (wr_h) {
+        *reinterpret_cast<float4*>(rr.h_out + e) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(rr.h_out + e + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+      // the 32-k block's amax over its 4 threads (a quad of lanes, whole quads active: n8 % 16 == 0)
+      am = fmaxf(am, lsa_dpp<LSA_DPP_XOR1>(am));
+      am = fmaxf(am, lsa_dpp<LSA_DPP_XOR2>(am));
+      const int eb = e8m0_for_amax(am);
+      const int kl = 8 * i, st = kl >> 7, kc = kl & 127;  // k128-step of the slice, k within it
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(x8s) + st * 128 + ((kc & 63) >> 4) * 32 + 16 * (kc >> 6) +
+                                (kc & 15)) = pack8_fp8(v, e8m0_inv(eb));
+      if ((i & 3) == 0) s8s[st * 4 + (kc >> 5)] = (uint8_t)eb;
+    }
+    ssl = wave_sum(ssl);
+    if (lane == 0) rr_red[w] = ssl;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) tot += rr_red[ww];
+    if (rr.local) rr_scale = rsqrtf(tot * rr.inv_k + rr.eps);
+    else if (wr_h && threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(rr.ss_out), (unsigned long long)ss_to_q24(tot));
+    if (n_it > 0) xload(xA, sbA, w);
+  } else {
+    if (n_it > 0) load(wA, saA, xA, sbA, w);
+  }
   if (n_it > 0) {
-    uint4 wA[U][NB][2], xA[U][MT][2], wB[U][NB][2], xB[U][MT][2];
-    int saA[U][NB], sbA[U][MT], saB[U][NB], sbB[U][MT];
-    load(wA, saA, xA, sbA, w);
     int i = 0;
     for (; i + 1 < n_it; i += 2) {
       load(wB, saB, xB, sbB, w + WAVES * (i + 1));
@@ -193,7 +273,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
         const int nrow_g = (nb0 + 2 * p) * 16 + 4 * (l >> 4);
         const int nrow_u = nrow_g + 16;
         const int n = ((nb0 + 2 * p) >> 1) * 16 + 4 * (l >> 4);
-        const float sc = (sx ? sx[m] : 1.f) * epi_row_scale(ep, m);
+        const float sc = (sx ? sx[m] : 1.f) * epi_row_scale(ep, m) * rr_scale;
         f32x4_t v;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -242,7 +322,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_a8_skinny_kernel(const uint4*
       if (m >= M || i >= cnt) continue;
       const int n = (nb0 + i) * 16 + 4 * (l >> 4);
       const float4 sc = WK == 0 ? *reinterpret_cast<const float4*>(wscale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
-      const float rs = (sx ? sx[m] : 1.f) * epi_row_scale(ep, m);
+      const float rs = (sx ? sx[m] : 1.f) * epi_row_scale(ep, m) * rr_scale;
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + slab + (size_t)m * ldo + n) =
           make_float4(s[0] * sc.x * rs, s[1] * sc.y * rs, s[2] * sc.z * rs, s[3] * sc.w * rs);
     }
@@ -264,18 +344,30 @@ struct A8Call {
   int ldo, splitk, NBtot;
   int waves, depth, xfo, wk;
   LsaEpi ep;
+  LsaRr rr;  // rr.h set: the residual-reduce prologue (M = 1; f32 slabs or the e4m3 SiLU output)
 };
 
 template <int MT, int NB, int EPI, int WV, int U, int XFO, int WK>
 void launch_a8_x(const A8Call& c, hipStream_t s) {
   const int kbps = (c.KB128 + c.splitk - 1) / c.splitk;
   const dim3 grid((c.NBtot + NB - 1) / NB, c.splitk);
+  if constexpr (MT == 1 && ((EPI == EPI_F32 && XFO == 0) || (EPI == EPI_SILU && XFO == 2))) {
+    if (c.rr.h) {
+      if (c.rr.np == 1)
+        hipLaunchKernelGGL((gemm_a8_skinny_kernel<MT, NB, EPI, WV, U, XFO, WK, true, 1>), grid, dim3(64 * WV), 0, s,
+                           c.X8, c.S8, c.sx, c.M, c.KB128, c.Wq, c.wscale, c.Sw, c.out, c.out_s8, c.ldo, kbps, c.ep, c.rr);
+      else
+        hipLaunchKernelGGL((gemm_a8_skinny_kernel<MT, NB, EPI, WV, U, XFO, WK, true, 4>), grid, dim3(64 * WV), 0, s,
+                           c.X8, c.S8, c.sx, c.M, c.KB128, c.Wq, c.wscale, c.Sw, c.out, c.out_s8, c.ldo, kbps, c.ep, c.rr);
+      return;
+    }
+  }
   if (c.S8)
     hipLaunchKernelGGL((gemm_a8_skinny_kernel<MT, NB, EPI, WV, U, XFO, WK, true>), grid, dim3(64 * WV), 0, s, c.X8, c.S8,
-                       c.sx, c.M, c.KB128, c.Wq, c.wscale, c.Sw, c.out, c.out_s8, c.ldo, kbps, c.ep);
+                       c.sx, c.M, c.KB128, c.Wq, c.wscale, c.Sw, c.out, c.out_s8, c.ldo, kbps, c.ep, LsaRr{});
   else
     hipLaunchKernelGGL((gemm_a8_skinny_kernel<MT, NB, EPI, WV, U, XFO, WK, false>), grid, dim3(64 * WV), 0, s, c.X8, c.S8,
-                       c.sx, c.M, c.KB128, c.Wq, c.wscale, c.Sw, c.out, c.out_s8, c.ldo, kbps, c.ep);
+                       c.sx, c.M, c.KB128, c.Wq, c.wscale, c.Sw, c.out, c.out_s8, c.ldo, kbps, c.ep, LsaRr{});
 }
 
 template <int MT, int NB, int EPI, int WV, int U>
@@ -363,7 +455,31 @@ extern "C" int lsa_a8_gemm(const void* X8, const void* s8, const float* sx, int 
   A8Call c{reinterpret_cast<const uint4*>(X8), reinterpret_cast<const uint8_t*>(s8), sx, M, KB128,
            reinterpret_cast<const uint4*>(Wq), wscale, reinterpret_cast<const uint32_t*>(Sw), out,
            reinterpret_cast<uint8_t*>(out_s8), epi == EPI_SILU ? N / 2 : N, splitk, NBtot,
-           waves == 8 ? 8 : 4, depth == 2 ? 2 : 1, xfo, wk, ep ? *ep : LsaEpi{}};
+           waves == 8 ? 8 : 4, depth == 2 ? 2 : 1, xfo, wk, ep ? *ep : LsaEpi{}, LsaRr{}};
+  const int rc = epi == EPI_F32 ? launch_a8_e<EPI_F32>(c, nb, stream) : launch_a8_e<EPI_SILU>(c, nb, stream);
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+// The same GEMM at batch 1 with the residual-reduce prologue (kernel template RR, lsa_epi.h LsaRr): no X8 / scales
+// in memory -- the prologue forms X from rr.h + rr.parts and quantises it itself.  epi EPI_F32 (f32 slabs, rr.local 0,
+// rr.ss_out accumulates sum X^2) or EPI_SILU with the e4m3 output (xfo 2, out_s8; splitk 1, rr.local 1).
+extern "C" int lsa_a8_gemm_rr(int K, const void* Wq, const float* wscale, const void* Sw, int wk, int N, void* out,
+                              void* out_s8, int epi, int nb, int splitk, int waves, int depth, const LsaRr* rr,
+                              hipStream_t stream) {
+  if (!rr || !rr->h || !rr->h_out || rr->h == rr->h_out || rr->np < 1 || rr->np > 4 || !rr->parts) return -1;
+  if (K % 128 != 0 || N % 16 != 0) return -1;
+  if ((wk == 0 && !wscale) || (wk == 1 && !Sw) || (wk != 0 && wk != 1)) return -8;
+  if (splitk < 1) splitk = 1;
+  const int KB128 = K / 128, NBtot = N / 16;
+  if ((KB128 + splitk - 1) / splitk * 128 > A8_RR_KMAX) return -3;
+  if ((KB128 + ((KB128 + splitk - 1) / splitk) - 1) / ((KB128 + splitk - 1) / splitk) != splitk) return -3;
+  if (epi == EPI_SILU ? (splitk != 1 || !rr->local || nb % 4 || NBtot % nb || !out_s8) : (epi != EPI_F32 || rr->local || !rr->ss_out))
+    return -4;
+  if (epi == EPI_F32 && NBtot % nb) return -2;
+  A8Call c{nullptr, nullptr, nullptr, 1, KB128, reinterpret_cast<const uint4*>(Wq), wscale,
+           reinterpret_cast<const uint32_t*>(Sw), out, reinterpret_cast<uint8_t*>(out_s8), epi == EPI_SILU ? N / 2 : N,
+           splitk, NBtot, waves == 8 ? 8 : 4, depth == 2 ? 2 : 1, epi == EPI_SILU ? 2 : 0, wk, LsaEpi{}, *rr};
   const int rc = epi == EPI_F32 ? launch_a8_e<EPI_F32>(c, nb, stream) : launch_a8_e<EPI_SILU>(c, nb, stream);
   if (rc) return rc;
   return (int)hipGetLastError();

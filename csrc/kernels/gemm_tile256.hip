@@ -166,7 +166,7 @@ template <int BM, int WN, int EPI, int NBUF, int KS, int NW>
 __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int ldx, int M, int KB,
                                              const uint4* __restrict__ Wf, int NBtot, void* __restrict__ out, int ldo,
                                              const SkPlan& pl, float* __restrict__ ws, int* __restrict__ tickets,
-                                             const RopeEpi& re, const LsaEpi& ne) {
+                                             const RopeEpi& re) {
   using C = TileCfg<BM, WN, KS, NW>;
   constexpr int SLOT = BM * C::NBT * 16;  // floats of one partial-tile slot
 #ifdef LSA_SK_STAMPS
@@ -507,7 +507,6 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
         for (int ii = 0; ii < IB; ++ii) {
           const int i = hf * IB + ii;
           const int m = mbase + wm * (BM / 2) + i * 16 + (lane & 15);
-          float ssp = 0.f;  // norm-free prefill: this lane's part of row m's sum of squares over the tile
 #pragma unroll
           for (int j = 0; j < WN; ++j) {
             const int nb = nbase + wn * WN + j;
@@ -515,15 +514,6 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
             float4 h = hv[ii][j];
             h.x += acc[i][j][0]; h.y += acc[i][j][1]; h.z += acc[i][j][2]; h.w += acc[i][j][3];
             *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + nb * 16 + 4 * g) = h;
-            if (ne.xout) {
-              *reinterpret_cast<uint2*>(ne.xout + (size_t)m * ldo + nb * 16 + 4 * g) =
-                  make_uint2(pack2bf(h.x, h.y), pack2bf(h.z, h.w));
-              ssp += h.x * h.x + h.y * h.y + h.z * h.z + h.w * h.w;
-            }
-          }
-          if (ne.ss_out) {  // the 4 lane groups hold row m's column quads: combine, one atomic per row and wave
-            ssp = lsa_sum_x32(lsa_sum_x16(ssp));
-            if (g == 0 && m < M) atomicAdd(reinterpret_cast<unsigned long long*>(ne.ss_out) + m, (unsigned long long)ss_to_q24(ssp));
           }
         }
       }
@@ -533,11 +523,6 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     for (int i = 0; i < 2 * MI; ++i) {
       const int m = mbase + wm * (BM / 2) + i * 16 + (lane & 15);
       if (m >= M) continue;
-      if (EPI == EPI_BF16 && ne.rowss) {  // norm-free prefill: the un-normalised input row's RMS scale
-        const float rs = epi_row_scale(ne, m);
-#pragma unroll
-        for (int j = 0; j < WN; ++j) acc[i][j] *= rs;
-      }
       if constexpr (EPI == EPI_SILU) {
 #pragma unroll
         for (int j = 0; j < WN; j += 2) {
@@ -611,13 +596,6 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
       // (16 rows per wave and pass at BM = 256)
       constexpr int RPW = BM / 2 / NW;
       const bool live_ch = lane < CH && col0 + lane * 4 < ncol_out;
-      // norm-free prefill: row k's RMS scale in lane k, loaded before the pass's first store (a load per row after the
-      // stores would pay its latency row by row, as above); 1 without rowss
-      float my_rs = 1.f;
-      if ((EPI == EPI_BF16 || EPI == EPI_ROPE) && lane < RPW) {
-        const int m = mbase + pass * (BM / 2) + w + NW * lane;
-        if (m < M) my_rs = epi_row_scale(ne, m);
-      }
       if constexpr (EPI == EPI_ROPE) {
         // per-row metadata once per pass, lane k for row k: the token's position and its paged-cache block
         int my_pos = 0, my_blk = 0;
@@ -652,11 +630,10 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
             const int r = w + NW * (k0 + u);
             const int m = mbase + pass * (BM / 2) + r;
             if (m >= M || !live_ch) continue;
-            const float rs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_rs), k0 + u));  // rotation is linear
-            const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2)) * rs;
+            const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2));
             f32x4_t y = v;
             if (rot) {
-              const f32x4_t pv = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((pch ^ (r & 15)) << 2)) * rs;
+              const f32x4_t pv = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((pch ^ (r & 15)) << 2));
               y[0] = v[0] * cs[u].x + sg * pv[0] * sn[u].x;
               y[1] = v[1] * cs[u].y + sg * pv[1] * sn[u].y;
               y[2] = v[2] * cs[u].z + sg * pv[2] * sn[u].z;
@@ -683,40 +660,15 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
           const int m = mbase + pass * (BM / 2) + w + NW * (k0 + u);
           if (m < M && live_ch) hv[u] = *reinterpret_cast<const float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + col0 + lane * 4);
         }
-        float ssp[RB];  // norm-free prefill: this lane's part of each row's sum of h^2 over the tile
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
-          const int k = k0 + u;
-          const int r = w + NW * k;
+          const int r = w + NW * (k0 + u);
           const int m = mbase + pass * (BM / 2) + r;
-          ssp[u] = 0.f;
           if (m < M && live_ch) {
             const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((lane ^ (r & 15)) << 2));
             float4 h = hv[u];
             h.x += v[0]; h.y += v[1]; h.z += v[2]; h.w += v[3];
             *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + col0 + lane * 4) = h;
-            if (ne.xout) {
-              *reinterpret_cast<uint2*>(ne.xout + (size_t)m * ldo + col0 + lane * 4) =
-                  make_uint2(pack2bf(h.x, h.y), pack2bf(h.z, h.w));
-              ssp[u] = h.x * h.x + h.y * h.y + h.z * h.z + h.w * h.w;
-            }
-          }
-        }
-        if (ne.ss_out) {  // the group's rows over the tile's columns: whole-wave reductions, one atomic per row
-          if constexpr (RB == 8) {
-            const float t = lsa_sum8_scatter(ssp);
-            const int m = mbase + pass * (BM / 2) + w + NW * (k0 + ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 +
-                                                              ((lane >> 3) & 1));
-            if ((lane & 7) == 0 && m < M)
-              atomicAdd(reinterpret_cast<unsigned long long*>(ne.ss_out) + m, (unsigned long long)ss_to_q24(t));
-          } else {
-#pragma unroll
-            for (int u = 0; u < RB; ++u) {
-              const float t = wave_sum(ssp[u]);
-              const int m = mbase + pass * (BM / 2) + w + NW * (k0 + u);
-              if (lane == 0 && m < M)
-                atomicAdd(reinterpret_cast<unsigned long long*>(ne.ss_out) + m, (unsigned long long)ss_to_q24(t));
-            }
           }
         }
         }
@@ -728,8 +680,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
         const int m = mbase + pass * (BM / 2) + r;
         const int ch = lane;
         if (live_ch && m < M) {
-          f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2));
-          if constexpr (EPI == EPI_BF16) v *= __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_rs), k));
+          const f32x4_t v = *reinterpret_cast<const f32x4_t*>(img + r * OC + ((ch ^ (r & 15)) << 2));
           const size_t o = (size_t)m * ldo + col0 + ch * 4;
           if constexpr (EPI == EPI_BF16 || EPI == EPI_SILU) {
             *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + o) =
@@ -826,8 +777,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_sk_kernel(const
                                                       const uint4* __restrict__ Wf, int NBtot,
                                                       void* __restrict__ out, int ldo, SkPlan pl,
                                                       float* __restrict__ ws, int* __restrict__ tickets,
-                                                      RopeEpi re, LsaEpi ne) {
-  gemm_sk_body<BM, WN, EPI, NBUF, KS, NW>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets, re, ne);
+                                                      RopeEpi re) {
+  gemm_sk_body<BM, WN, EPI, NBUF, KS, NW>(X, ldx, M, KB, Wf, NBtot, out, ldo, pl, ws, tickets, re);
 }
 
 // Plan for a grid of (at most) ncu workgroups over BM x (NBT * 16) tiles: the data-parallel rounds keep whole tiles;
@@ -919,7 +870,7 @@ extern "C" void lsa_gemm_sk_one_phase(int on) { g_sk_one = on ? 1 : 0; }
 template <int BM, int WN, int KS = 2, int NW = 8>
 static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
                      float* ws, int* tickets, int ncu, int min_share, bool sk, int epl, int* grid_out,
-                     const RopeEpi& re, const LsaEpi& ne, hipStream_t stream) {
+                     const RopeEpi& re, hipStream_t stream) {
   using C = TileCfg<BM, WN, KS, NW>;
   const int P = ncu * (NW == 4 ? 2 : 1);  // persistent workgroups: one per CU, or two of the 4-wave kind
   int grid = 0;
@@ -933,19 +884,19 @@ static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const u
     if constexpr (C::CAN4) {                                                                                      \
       if (g_sk_one) {                                                                                             \
         hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 4, KS, NW>), dim3(grid), dim3(64 * NW), 0, stream, x, ldx, \
-                           M, KB, w, NBtot, out, ldo, pl, ws, tickets, re, ne);                                   \
+                           M, KB, w, NBtot, out, ldo, pl, ws, tickets, re);                                   \
         break;                                                                                                    \
       }                                                                                                           \
     }                                                                                                             \
     if constexpr (C::CAN3) {                                                                                      \
       if (g_sk_nbuf == 3) {                                                                                       \
         hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 3, KS, NW>), dim3(grid), dim3(64 * NW), 0, stream, x, ldx, \
-                           M, KB, w, NBtot, out, ldo, pl, ws, tickets, re, ne);                                   \
+                           M, KB, w, NBtot, out, ldo, pl, ws, tickets, re);                                   \
         break;                                                                                                    \
       }                                                                                                           \
     }                                                                                                             \
     hipLaunchKernelGGL((gemm_sk_kernel<BM, WN, E, 2, KS, NW>), dim3(grid), dim3(64 * NW), 0, stream, x, ldx, M, \
-                       KB, w, NBtot, out, ldo, pl, ws, tickets, re, ne);                                          \
+                       KB, w, NBtot, out, ldo, pl, ws, tickets, re);                                          \
   } while (0)
     case EPI_BF16: LSA_SKL(EPI_BF16); break;
     case EPI_F32: LSA_SKL(EPI_F32); break;
@@ -978,12 +929,7 @@ static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const u
 // configuration used (bits 0-3).
 static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
                         int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, const RopeEpi& re,
-                        const LsaEpi* nep, hipStream_t stream) {
-  const LsaEpi ne = nep ? *nep : LsaEpi{};
-  // norm-free prefill: a row scale on the bf16 / RoPE outputs, xout + sums of squares from the residual add
-  if ((ne.rowss && epi != EPI_BF16 && epi != EPI_ROPE) || ((ne.xout != nullptr) != (ne.ss_out != nullptr)) ||
-      (ne.xout && epi != EPI_RES))
-    return -7;
+                        hipStream_t stream) {
   if (K % 32 != 0 || N % 16 != 0 || M <= 0 || ncu < 8 || ncu > 1024 || !ws || !tickets) return -1;
   if (epi == EPI_SILU && N % 32 != 0) return -2;
   const bool even_wn = epi == EPI_SILU || epi == EPI_ROPE;  // tile configurations with an even n-block count/wave
@@ -1021,29 +967,26 @@ static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, in
   const int ldo = epi == EPI_SILU ? N / 2 : N;
   switch (cfg) {
 #define LSA_SKC(I, BMV, WNV) \
-  case I: return sk_launch<BMV, WNV>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, ne, stream);
+  case I: return sk_launch<BMV, WNV>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, stream);
     LSA_SKC(0, 256, 4)
     LSA_SKC(1, 256, 3)
     LSA_SKC(2, 256, 2)
     LSA_SKC(3, 128, 4)
     LSA_SKC(4, 128, 3)
     LSA_SKC(5, 128, 2)
-    case 6: return sk_launch<128, 6, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, ne, stream);
-    case 7: return sk_launch<128, 4, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, ne, stream);
+    case 6: return sk_launch<128, 6, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, stream);
+    case 7: return sk_launch<128, 4, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, stream);
 #undef LSA_SKC
     default: return -5;
   }
 }
 
-// ne (nullable): norm-free prefill extensions (lsa_epi.h): rowss / inv_k / eps scale the rows of a bf16 / RoPE output
-// by the un-normalised input row's RMS; with EPI_RES, xout (bf16 [M][N]) and ss_out (Q24 int64 [M], accumulated)
-// receive bf16(h) and the row sums of h^2 for the next projection
 extern "C" int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
                            int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out,
-                           const LsaEpi* ne, hipStream_t stream) {
+                           hipStream_t stream) {
   if (epi < 0 || epi > 3) return -4;
   return gemm_sk_impl(X, ldx, M, K, Wf, N, out, epi, ws, tickets, ncu, min_share, cfg, grid_out, cfg_out, RopeEpi{},
-                      ne, stream);
+                      stream);
 }
 
 // the prefill qkv projection with RoPE + the paged bf16 KV-cache append fused into its epilogue (EPI_ROPE above);
@@ -1052,12 +995,12 @@ extern "C" int lsa_gemm_sk_rope(const void* X, int ldx, int M, int K, const void
                                 int ncu, int min_share, int cfg, const int* pos, const int* tok_seq,
                                 const int* block_tables, int max_blocks, const float* cos_t, const float* sin_t,
                                 void* q_out, void* kc, void* vc, int H, int Hkv, int* grid_out, int* cfg_out,
-                                const LsaEpi* ne, hipStream_t stream) {
+                                hipStream_t stream) {
   if (H <= 0 || Hkv <= 0 || N != (H + 2 * Hkv) * 128 || !pos || !block_tables || !cos_t || !sin_t || !q_out || !kc ||
       !vc)
     return -6;
   const RopeEpi re{pos, tok_seq, block_tables, max_blocks, cos_t, sin_t, reinterpret_cast<uint16_t*>(q_out),
                    reinterpret_cast<uint16_t*>(kc), reinterpret_cast<uint16_t*>(vc), H, Hkv};
   return gemm_sk_impl(X, ldx, M, K, Wf, N, nullptr, EPI_ROPE, ws, tickets, ncu, min_share, cfg, grid_out, cfg_out, re,
-                      ne, stream);
+                      stream);
 }

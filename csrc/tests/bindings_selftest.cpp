@@ -120,20 +120,13 @@ int main() {
     auto o2 = T({300, 64}, F32), sw = T({64}, F32);
     // stream-K prefill GEMM: workspace of lsa_gemm_sk_ws_bytes(ncu) / tickets(ncu)
     auto wsk = T({2 * 8 * 65536}, F32), tks = T({32}, I32), ob = T({300, 64}, BF), wsb = T({64 * 128}, BF);
-    expect_ok("gemm_sk", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, none, 1e-5, none, none); });
+    expect_ok("gemm_sk", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1); });
     auto wsk_small = T({65536}, F32);
-    expect_reject("gemm_sk workspace", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk_small, tks, 8, 0, -1, none, 1e-5, none, none); });
-    expect_reject("gemm_sk residual dtype", [&] { gemm_sk(x, wsb, 64, ob, 3, wsk, tks, 8, 0, -1, none, 1e-5, none, none); });
-    // norm-free prefill: rowss on bf16 / RoPE outputs; xout + ss_out with the residual epilogue
-    auto rss = T({300}, I64), rss_small = T({299}, I64), hs = T({300, 64}, F32), xs = T({300, 64}, BF);
-    expect_ok("gemm_sk rownorm", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, rss, 1e-5, none, none); });
-    expect_reject("gemm_sk rownorm too small", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, rss_small, 1e-5, none, none); });
-    expect_reject("gemm_sk rownorm on f32", [&] { gemm_sk(x, wsb, 64, hs, 1, wsk, tks, 8, 0, -1, rss, 1e-5, none, none); });
-    expect_reject("gemm_sk rownorm on SiLU", [&] { gemm_sk(x, wsb, 64, ob, 2, wsk, tks, 8, 0, -1, rss, 1e-5, none, none); });
-    expect_ok("gemm_sk residual xout", [&] { gemm_sk(x, wsb, 64, hs, 3, wsk, tks, 8, 0, -1, none, 1e-5, xs, rss); });
-    expect_reject("gemm_sk xout without ss_out", [&] { gemm_sk(x, wsb, 64, hs, 3, wsk, tks, 8, 0, -1, none, 1e-5, xs, none); });
-    expect_reject("gemm_sk xout on bf16", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, none, 1e-5, xs, rss); });
-    expect_reject("gemm_sk ss_out too small", [&] { gemm_sk(x, wsb, 64, hs, 3, wsk, tks, 8, 0, -1, none, 1e-5, xs, rss_small); });
+    expect_reject("gemm_sk workspace", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk_small, tks, 8, 0, -1); });
+    expect_reject("gemm_sk residual dtype", [&] { gemm_sk(x, wsb, 64, ob, 3, wsk, tks, 8, 0, -1); });
+    auto hs = T({300, 64}, F32), hs_small = T({299, 64}, F32);
+    expect_ok("gemm_sk residual", [&] { gemm_sk(x, wsb, 64, hs, 3, wsk, tks, 8, 0, -1); });
+    expect_reject("gemm_sk residual too small", [&] { gemm_sk(x, wsb, 64, hs_small, 3, wsk, tks, 8, 0, -1); });
     expect_ok("fp8_gemm_t256", [&] { fp8_gemm_t256(xq, sxq, wq, sw, 64, o2, 1, 1); });
     auto sw_small = T({32}, F32);
     expect_reject("fp8_gemm_t256 weight scales", [&] { fp8_gemm_t256(xq, sxq, wq, sw_small, 64, o2, 1, 1); });
@@ -188,21 +181,14 @@ int main() {
     expect_reject("kv8_dequant mb", [&] { kv8_dequant(k8, v8, ks, ks, bt, ctx, mb + 1, ko, ko); });
     // prefill: 2 sequences of 70 and 30 tokens
     auto qp = T({100, H, 128}, BF), outp = T({100, H, 128}, BF), cu = T({B + 1}, I32), work = T({2, 4}, I32);
-    expect_ok("attn_prefill32", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 1, none, none, none); });
-    auto work_bad = T({2, 5}, I32);
-    expect_reject("attn_prefill32 work", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work_bad, H, Hkv, 0.08, outp, 1, none, none, none); });
+    expect_ok("attn_prefill32", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 1); });
+    auto work_bad = T({2, 5}, I32), work8 = T({2, 8}, I32);
+    expect_ok("attn_prefill32 paired", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 1); });
+    expect_reject("attn_prefill removed split mode", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 3); });
+    expect_reject("attn_prefill32 work", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work_bad, H, Hkv, 0.08, outp, 1); });
     auto cu_bad = T({B}, I32);
-    expect_reject("attn_prefill offsets", [&] { attn_prefill(qp, kc, vc, bt, cu_bad, ctx, work, H, Hkv, 0.08, outp, 1, none, none, none); });
-    // split pieces: 8-int items (slot 0, piece 0), partial buffers for H slots
-    auto work8 = T({2, 8}, I32), opp = T({H * 2 * 4 * 4096}, F32), mlp = T({H * 2 * 4 * 64 * 2}, F32), tkp = T({H}, I32);
-    expect_ok("attn_prefill32 split", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 3, opp, mlp, tkp); });
-    expect_reject("attn_prefill32 split without buffers", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 3, none, none, none); });
-    auto tkp_small = T({H - 1}, I32);
-    expect_reject("attn_prefill32 split tickets", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 3, opp, mlp, tkp_small); });
-    auto work8b = T({2, 8}, I32);
-    work8b.index_put_({0, 5}, 2);
-    expect_reject("attn_prefill32 split piece", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8b, H, Hkv, 0.08, outp, 3, opp, mlp, tkp); });
-    expect_reject("attn_prefill rows32 mode", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 2, none, none, none); });
+    expect_reject("attn_prefill offsets", [&] { attn_prefill(qp, kc, vc, bt, cu_bad, ctx, work, H, Hkv, 0.08, outp, 1); });
+    expect_reject("attn_prefill rows32 mode", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 2); });
     auto qkv = T({100, (H + 2 * Hkv) * 128}, BF), tpos = T({100}, I32), tseq = T({100}, I32), qo = T({100, H, 128}, BF);
     expect_ok("rope_append", [&] { rope_append(qkv, tpos, tseq, bt, cs, cs, qo, kc, vc, H, Hkv, none, none); });
     auto qo_small = T({99, H, 128}, BF);

@@ -34,7 +34,6 @@ BLOCK = 64
 REPEAT_WINDOW = 64  # repetition-penalty ring (Ollama repeat_last_n default; larger values are clamped)
 # norm-free attention input in prefill (Runner._prefill_layers), off by default: measured even with the norm launch
 # it removes (3B 2k TTFT 14.38 vs 14.34 ms, profiles/r5/prefill_norm_free_ab.txt)
-PREFILL_NORM_FREE = os.environ.get("LSA_PREFILL_NF", "0") == "1"
 # batch-1 decode with the residual add folded into the next GEMM's prologue (ModelRunner._decode_step_rr)
 RR_DECODE = os.environ.get("LSA_RR", "1") != "0"
 
@@ -223,7 +222,13 @@ class ModelRunner:
         # previous row-parallel projection's slabs into their prologue (ops.linear_rr), so a layer issues 5 launches
         # (qkv, attention, o, gate_up, down) and no residual-add launch; TP = 1, bf16 weights, gammas folded
         lw0 = weights.layers[0]
-        self.rr_decode = (RR_DECODE and tps == 1 and self.wide_norm and ops.rr_supported(lw0.wqkv, self.d) and ops.rr_supported(lw0.w_gate_up, self.d))
+        # quantised weights whose batch-1 step runs all four projections W8A8 / W4A8 (MXFP4): the qkv / gate_up GEMMs
+        # quantise their own residual-reduced input (ops.linear_a8_rr), so the two quantising norm launches go too
+        self.rr_a8 = all(self.a8_plan(1)) and ops.rr_a8_supported(lw0.wqkv, self.d) and ops.rr_a8_supported(
+            lw0.w_gate_up, self.d) and self._a8_splitk_b1() <= 4  # the prologue sums at most 4 slabs
+        self.rr_decode = (RR_DECODE and tps == 1 and self.wide_norm and (self.rr_a8 or (
+            ops.rr_supported(lw0.wqkv, self.d) and ops.rr_supported(lw0.w_gate_up, self.d))))
+        self.zero_slab = torch.zeros(1, 1, self.d, **f32)  # layer 0's "previous projection" in the W8A8 RR step
         self.h_alt = torch.zeros(1, self.d, **f32)  # the residual stream's second buffer (h_out never aliases h)
         self.graphs: dict = {}
         self._pending_bt: dict = {}  # slot -> block-table row of a prompt still being prefilled in chunks
@@ -269,6 +274,23 @@ class ModelRunner:
         qkv, gu, od = B > self.a8_min_batch, B > self.a8_mlp_min_batch, B <= self.a8_od_max_batch
         return (qkv, gu, od, gu and od and self.a8_down_ok)
 
+    def _a8_splitk_b1(self) -> int:
+        """The larger split-K of the batch-1 W8A8 / W4A8 o and down GEMMs (the slabs a residual-reduce prologue sums;
+        e.g. MXFP4 Llama-3.2-3B picks 8 and keeps the norm-launch step)."""
+        kind = self.w.layers[0].wqkv.kind
+        if kind not in ("fp8", "mxfp4"):
+            return 1
+        ak = "fp8a" if kind == "fp8" else "fp4a"
+        return max(ops.pick_gemm_config(1, self.d, K, "f32", xf=True, kind=ak)[1] for K in (self.H * self.D, self.ffn_l))
+
+    def oracle_plan(self, B: int) -> dict:
+        """a8_plan(B) as the numerics oracle's ``decode_a8`` dict (models/llama.py reference_forward), plus ``rr``:
+        the batch-1 residual-reduce step of fp8 / MXFP4 weights quantises the qkv / gate_up inputs per 32-block
+        (E8M0) from the raw residual and applies the RMS row scale after the GEMM (_decode_step_rr)."""
+        plan = dict(zip(("qkv", "gate_up", "o", "down"), self.a8_plan(B)))
+        plan["rr"] = B == 1 and self.rr_decode and self.rr_a8
+        return plan
+
     def use_xfrag(self, B: int) -> bool:
         """Fragment-major activations pay off once a decode batch spans >1 row tile (B > 16):
         measured 8-20 % faster GEMMs at B = 32 (scripts/bench_xf.py); bf16 and fp8 weights."""
@@ -313,7 +335,7 @@ class ModelRunner:
 
     def _decode_step(self, B: int, sample: bool, plan: Optional[tuple] = None) -> None:
         a8, a8m, a8o, a8d = self.a8_plan(B)  # qkv / gate_up / o / down W8A8 (W4A8)
-        if B == 1 and self.rr_decode and not (a8 or a8m or a8o):
+        if B == 1 and self.rr_decode and (self.rr_a8 or not (a8 or a8m or a8o)):
             return self._decode_step_rr(sample, plan)
         if self.fused_norm and B <= self.fused_norm_max_batch and not (a8 or a8m or a8o):
             return self._decode_step_fused(B, sample, plan)
@@ -467,13 +489,23 @@ class ModelRunner:
             -> gemm down (f32 split-K slabs)
           -> final RMSNorm (h + down slabs) -> lm_head -> token commit
         The residual stream alternates between self.h and self.h_alt (a prologue's other workgroups still read the
-        buffer the column-0 workgroups replace)."""
+        buffer the column-0 workgroups replace).
+        With fp8 / MXFP4 weights (``rr_a8``) every projection runs W8A8 / W4A8: qkv and gate_up quantise their
+        residual-reduced input themselves (ops.linear_a8_rr; layer 0's qkv reduces the embedding row with a zero
+        slab), attention writes the o input as e4m3 + E8M0 per head, gate_up the down input as e4m3 + E8M0 per 32."""
         w, d, B = self.w, self.d, 1
         ids, pos, bt = self.input_ids[:1], self.positions[:1], self.block_tables[:1]
         nqkv = (self.H + 2 * self.Hkv) * self.D
-        sk_q = self._splitk(1, d, nqkv, tp_reduced=False)
-        sk_o = self._splitk(1, self.H * self.D)
-        sk_d = self._splitk(1, self.ffn_l)
+        a8 = self.rr_a8
+        if a8:
+            ak = "fp8a" if w.layers[0].wqkv.kind == "fp8" else "fp4a"
+            sk_q = ops.pick_gemm_config(1, nqkv, d, "f32", xf=True, kind=ak)[1]
+            sk_o = ops.pick_gemm_config(1, d, self.H * self.D, "f32", xf=True, kind=ak)[1]
+            sk_d = ops.pick_gemm_config(1, d, self.ffn_l, "f32", xf=True, kind=ak)[1]
+        else:
+            sk_q = self._splitk(1, d, nqkv, tp_reduced=False)
+            sk_o = self._splitk(1, self.H * self.D)
+            sk_d = self._splitk(1, self.ffn_l)
         assert sk_o <= 4 and sk_d <= 4, "the residual-reduce prologue sums at most 4 slabs"
         qkv_parts = self.qkv_buf[: sk_q * nqkv].view(sk_q, 1, nqkv)
         o_parts = self.o_buf[: sk_o * d].view(sk_o, 1, d)
@@ -486,15 +518,30 @@ class ModelRunner:
         ops.add_rmsnorm(hs[0], w.layers[0].attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=1,
                         ss_out=ssq.view(-1), ss_ld=self.max_slots, ss_nzero=self.L)
         for l, lw in enumerate(w.layers):
-            if l == 0:
+            if a8:  # the qkv input (embedding row | h + down slabs) quantised in the GEMM's prologue
+                ops.linear_a8_rr(hs[cur], self.zero_slab if l == 0 else d_parts, hs[1 - cur], lw.wqkv, "f32",
+                                 out=qkv_parts, ss_out=ssq[l + 1], eps=self.eps, splitk=sk_q)
+                cur = 1 - cur
+                rn = (ssq[l + 1], self.eps, d)
+            elif l == 0:
                 ops.linear(xn, lw.wqkv, "f32", out=qkv_parts, splitk=sk_q, rownorm=(ssq[0], self.eps))
                 rn = None
             else:
-                ops.linear_rr(hs[cur], d_parts, hs[1 - cur], lw.wqkv, "f32", out=qkv_parts, ss_out=ssq[l],
+                ops.linear_rr(hs[cur], d_parts, hs[1 - cur], lw.wqkv, "f32", out=qkv_parts, ss_out=ssq[l + 1],
                               eps=self.eps, splitk=sk_q)
                 cur = 1 - cur
-                rn = (ssq[l], self.eps, d)
+                rn = (ssq[l + 1], self.eps, d)
             kc, vc = self.kv[l, 0], self.kv[l, 1]
+            if a8:
+                ops.attn_decode(self.q[:1], kc, vc, bt, pos, self.H, self.Hkv, self.scale, self.x8o, workspace=self.attn_ws,
+                                plan=plan, xf=True, qkv_parts=qkv_parts, cos=self.cos, sin=self.sin,
+                                kv_scales=self._kv_scales(l), out_s8=self.s8o, rownorm=rn)
+                ops.linear_a8(self.x8o, None, 1, lw.wo, "f32", out=o_parts, splitk=sk_o, s8=self.s8o)
+                ops.linear_a8_rr(hs[cur], o_parts, hs[1 - cur], lw.w_gate_up, "silu", out=self.x8d, out_s8=self.s8d,
+                                 eps=self.eps)
+                cur = 1 - cur
+                ops.linear_a8(self.x8d, None, 1, lw.w_down, "f32", out=d_parts, splitk=sk_d, s8=self.s8d)
+                continue
             ops.attn_decode(self.q[:1], kc, vc, bt, pos, self.H, self.Hkv, self.scale, attn.view(1, self.H, self.D),
                             workspace=self.attn_ws, plan=plan, qkv_parts=qkv_parts, cos=self.cos, sin=self.sin,
                             kv_scales=self._kv_scales(l), rownorm=rn)
@@ -832,26 +879,18 @@ class ModelRunner:
         d_parts = None
         # TP = 1: o / down accumulate into the f32 residual in the stream-K GEMM's epilogue (ops.linear_res), so the
         # norms after them read h alone (no f32 slab written by the GEMM and read back by the add)
+        # (stream-K tile kernels: T > 64 rows; shorter chunks take the skinny split-K GEMMs, whose f32 slabs the next
+        # add_rmsnorm sums).  The round-5 norm-free variant (the down epilogue also writing bf16(h) + row sums, the qkv
+        # GEMM scaling its rows) measured a tie and was removed in round 6 (ARCHITECTURE.md section 4)
         tp1 = self.tp is None or self.tp.size == 1
-        res_o = tp1 and ops.res_supported(w.layers[0].wo)
-        res_d = tp1 and ops.res_supported(w.layers[0].w_down)
-        # norm-free attention input (gammas folded into wqkv, the down residual epilogue on, no split-K slabs on the
-        # qkv GEMM): the down epilogue also writes bf16(h) and the Q24 row sums of h^2 and the qkv GEMM scales its
-        # output rows by the RMS -- the attention-side add_rmsnorm launch goes away.  The MLP side keeps its norm: a
-        # row scale in the gate_up SiLU epilogue cost that (spilling) kernel more than the launch it saves, and the
-        # down epilogue's extra store + row sums cost about as much as the norm (profiles/r5/prefill_norm_free_ab.txt)
-        nf = (res_d and PREFILL_NORM_FREE and all(lw.norms_folded for lw in w.layers)
-              and self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D) == 1)
-        ss = torch.zeros(len(w.layers), T, dtype=torch.int64, device=dev) if nf else None
+        res_o = tp1 and T > 64 and ops.res_supported(w.layers[0].wo)
+        res_d = tp1 and T > 64 and ops.res_supported(w.layers[0].w_down)
         for l, lw in enumerate(w.layers):
-            rn_a = None
             if l == 0:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
-            elif nf:
-                rn_a = (ss[l - 1], self.eps)
             else:
                 ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, write_h=not res_d)
-            self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T, rownorm=rn_a)
+            self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T)
             if res_o:
                 ops.linear_res(attn, lw.wo, h)
                 ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, write_h=False)
@@ -868,7 +907,7 @@ class ModelRunner:
             else:
                 act = ops.linear(xn, lw.w_gate_up, "silu")
             if res_d:
-                ops.linear_res(act, lw.w_down, h, xn=(xn, ss[l]) if nf and l + 1 < len(w.layers) else None)
+                ops.linear_res(act, lw.w_down, h)
                 d_parts = None
             else:
                 d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
@@ -881,23 +920,21 @@ class ModelRunner:
         ops.add_rmsnorm(h, w.final_norm, self.eps, xl, parts=d_parts, row_idx=last, write_h=False)
         return xl
 
-    def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T, rownorm=None):
+    def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T):
         kc, vc = self.kv[l, 0], self.kv[l, 1]
         kvs = self._kv_scales(l)
         if self.on_gpu and ops.rope_fusable(lw.wqkv, self.kv_fp8, T) and bt.shape[1] > 0:
             # RoPE + the KV-cache append in the qkv GEMM's epilogue: no qkv round trip, no rope_append launch
-            ops.linear_rope(xn, lw.wqkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv,
-                            rownorm=rownorm)
+            ops.linear_rope(xn, lw.wqkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
             ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
                              work=work, cu_list=self._cu_host, kv_scales=kvs, kv8_scratch_=self._kv8_scratch)
             return
         sk_q = self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D)
         if sk_q > 1:  # small tile grid: f32 split-K slabs, summed by rope_append while it rotates
-            assert rownorm is None
             parts = ops.linear(xn, lw.wqkv, "f32", splitk=sk_q)
             ops.rope_append(parts, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)
         else:
-            ops.linear(xn, lw.wqkv, "bf16", out=qkv, rownorm=rownorm)
+            ops.linear(xn, lw.wqkv, "bf16", out=qkv)
             ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)
         ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
                          work=work, cu_list=self._cu_host, kv_scales=kvs, kv8_scratch_=self._kv8_scratch)

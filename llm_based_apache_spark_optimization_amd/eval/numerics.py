@@ -42,12 +42,15 @@ import torch
 # the dequantised e2m1 weights, so the healthy noise is the activation rounding of every W4A8 input (qkv / gate_up
 # per row, o / down per 32-block up to 16 rows); its scale fault is every 8th E8M0 block scale of one layer's down
 # projection one binade up (e8m0_fault).  Calibrated in round 4 (profiles/r4/numerics_calibration_w4a8_mi355x.jsonl):
-# the bound sits 1.8x above the worst healthy row and 2x below the weakest fault.
+# the bound sits 1.8x above the worst healthy row and 2x below the weakest fault.  w4a8 gates on the mean KL and
+# the top-5 overlap only (top-1 is reported): its healthy top-1 sits at 0.3-0.4 on a 32-layer random-init network
+# and moves by +-0.05 with the summation order of an equally exact kernel (round 6: the batch-1 residual-reduce
+# step's 0.344 vs 0.391, at KL 0.126 vs 0.105 under a 0.192 bound), while the E8M0 fault's KL alone is 2x the bound.
 THRESHOLDS = {
     "bf16": (2.5e-4, 0.85, 0.8),
     "w8a16": (2.0e-3, 0.5, 0.4),
     "w8a8": (3.5e-3, 0.4, 0.3),
-    "w4a8": (6.0e-3, 0.35, 0.25),
+    "w4a8": (6.0e-3, 0.35, None),
 }
 
 # Tied-embedding models (Llama-3.2-3B: lm_head = the embedding table).  With random-init weights the final hidden
@@ -168,7 +171,7 @@ def check_recorded(eng, prompts, toks, elog, n_steps: int, check_rows: Sequence[
     w = weights if weights is not None else r.w
     fp8 = w.layers[0].wqkv.kind == "fp8"
     rows = prefill_rows if prefill_rows is not None else sum(len(p) for p in prompts)
-    plan = dict(zip(("qkv", "gate_up", "o", "down"), r.a8_plan(B)))
+    plan = r.oracle_plan(B)
     ehid = None
     if isinstance(elog, tuple):
         elog, ehid = elog
@@ -196,10 +199,11 @@ def check_recorded(eng, prompts, toks, elog, n_steps: int, check_rows: Sequence[
            "mean_kl": round(float(kl.mean()), 6), "max_kl": round(float(kl.max()), 6),
            "top1_agree": round(float(t1.mean()), 4), "top5_overlap": round(float(t5.mean()), 4)}
     if ehid is None:
-        res["ok"] = bool(res["mean_kl"] < kl_max and res["top5_overlap"] >= t5_min and res["top1_agree"] >= t1_min)
+        res["ok"] = bool(res["mean_kl"] < kl_max and res["top5_overlap"] >= t5_min
+                         and (t1_min is None or res["top1_agree"] >= t1_min))
         res["criterion"] = (f"{cls}: teacher-forced over {n_steps} decode steps: mean KL(oracle||engine) < {kl_max} "
-                            f"({kl_layer} x {nl} layers), "
-                            f"top-5 overlap >= {t5_min}, top-1 agreement >= {t1_min}")
+                            f"({kl_layer} x {nl} layers), top-5 overlap >= {t5_min}"
+                            + (f", top-1 agreement >= {t1_min}" if t1_min is not None else " (top-1 reported only)"))
         return res
     pk, rel = torch.cat(pks), torch.cat(rels)
     pk_layer, rel_c = TIED_THRESHOLDS[cls]
@@ -207,11 +211,12 @@ def check_recorded(eng, prompts, toks, elog, n_steps: int, check_rows: Sequence[
     rel_max = round(rel_c * nl ** 0.5, 5)
     res.update(tied_head=True, probe_kl=round(float(pk.mean()), 6), probe_kl_max=round(float(pk.max()), 6),
                hidden_rel_err=round(float(rel.mean()), 5), hidden_rel_err_max=round(float(rel.max()), 5))
-    res["ok"] = bool(res["probe_kl"] < pk_max and res["hidden_rel_err"] < rel_max and res["top1_agree"] >= t1_min)
+    res["ok"] = bool(res["probe_kl"] < pk_max and res["hidden_rel_err"] < rel_max
+                     and (t1_min is None or res["top1_agree"] >= t1_min))
     res["criterion"] = (f"{cls}, tied lm_head: teacher-forced over {n_steps} decode steps: mean KL(oracle||engine) of an "
                         f"untied random probe head over the final hidden state < {pk_max} ({pk_layer} x {nl} layers), "
                         f"mean relative L2 error of the final hidden state < {rel_max} ({rel_c} x sqrt({nl})), top-1 agreement of the tied "
-                        f"head >= {t1_min} (its KL is reported, but a random-init tied head is near one-hot)")
+                        f"head >= {t1_min or 0} (its KL is reported, but a random-init tied head is near one-hot)")
     return res
 
 

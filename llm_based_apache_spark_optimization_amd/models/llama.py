@@ -199,7 +199,9 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
     {qkv, gate_up, o, down} of the projections the engine runs W8A8 / W4A8 (ModelRunner.a8_plan): the o input is
     then rounded to e4m3 with one E8M0 scale per (row, head) from the f32 attention output, the down input with one
     per (row, 32 columns) from the f32 SiLU product (ops.quantize_blocks_fp8, as the kernels write them); fp8 and
-    MXFP4 weights alike.  ``kv_fp8``: the engine's fp8 KV
+    MXFP4 weights alike; its ``rr`` key (ModelRunner.oracle_plan: the batch-1 residual-reduce step) rounds the qkv /
+    gate_up inputs per (row, 32 columns) with E8M0 scales from the raw residual instead, the RMS row scale applied
+    after the GEMM (ops.linear_a8_rr).  ``kv_fp8``: the engine's fp8 KV
     cache (ops.KV_FP8) -- every rotated key and value row is rounded per (token, kv-head) to e4m3 with its
     amax / 448 scale (ops.reference.quant_kv_rows) before attention.  ``return_hidden``: (logits, the final
     normalised hidden states [T, d] the lm_head reads)."""
@@ -255,16 +257,23 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
         s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
         return (x / s).to(torch.float8_e4m3fn).float() * s
 
-    def qin(xn, on):  # qkv / gate_up input from the f32 norm output
+    rr = isinstance(decode_a8, dict) and bool(decode_a8.get("rr"))
+
+    def qin(xn, on, hraw, g):  # qkv / gate_up input from the f32 norm output
         x = q8(bf(xn))
         if on and aq < T:
+            if rr:  # residual-reduce step: e4m3 per 32-block of the raw residual, RMS row scale after the GEMM
+                from ..ops import dequant_blocks_fp8, quantize_blocks_fp8
+                hr = hraw[aq:]
+                rs = torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + spec.rms_eps)
+                return torch.cat([x[:aq], dequant_blocks_fp8(*quantize_blocks_fp8(hr, 32)) * rs * g.float()], 0)
             x = torch.cat([x[:aq], e4m3_rows(xn[aq:])], 0)
         return x
 
     h = w.embed[ids].float()
     mask = torch.full((T, T), float("-inf"), device=dev).triu(1)
     for lw in w.layers:
-        x = qin(norm(h, lw.attn_norm), da8)
+        x = qin(norm(h, lw.attn_norm), da8, h, lw.attn_norm)
         qkv = x @ lw.wqkv.dense().float().t()
         q = qkv[:, : H * hd].view(T, H, hd)
         k = qkv[:, H * hd:(H + Hkv) * hd].view(T, Hkv, hd)
@@ -278,7 +287,7 @@ def reference_forward(w: LlamaWeights, ids, layer_dtype=torch.float32, act_quant
         a32 = torch.einsum("hqk,khd->qhd", s.softmax(-1), v).reshape(T, H * hd)
         a = qblk(bf(a32), a32, da8o, 128)
         h = h + q8(a) @ lw.wo.dense().float().t()
-        x = qin(norm(h, lw.mlp_norm), da8m)
+        x = qin(norm(h, lw.mlp_norm), da8m, h, lw.mlp_norm)
         gu = (x @ lw.w_gate_up.dense().float().t()).view(T, -1, 2, 16)
         act32 = (torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(T, -1)
         act = qblk(bf(act32), act32, da8d, 32)

@@ -482,56 +482,41 @@ def sk_config(M: int, N: int, K: int, epi: str) -> int:
 
 
 def gemm_sk(x: torch.Tensor, wf: torch.Tensor, N: int, out: torch.Tensor, epi: str,
-            min_share: Optional[int] = None, cfg: Optional[int] = None, rownorm=None, xn=None) -> torch.Tensor:
+            min_share: Optional[int] = None, cfg: Optional[int] = None) -> torch.Tensor:
     """out (epi 'bf16' / 'f32' / 'silu') or h (epi 'res': h[:M] += x @ W^T) from the stream-K prefill GEMM over the
     fragment-layout bf16 weight ``wf``.  cfg: None = the measured table (``sk_config``), -1 = the kernel's
-    tile-shape cost model, else an SK_CFGS index (+ 8: whole tiles only).  Norm-free prefill (RMSNorm gamma folded
-    into the weight): rownorm = (ss, eps) scales output row m by rsqrt(ss[m] / K + eps) ('bf16');
-    xn = (xout, ss_out) with 'res' also writes bf16(h) row-major to xout and adds the Q24 row sums of h^2 to ss_out
-    (the next GEMM's rownorm)."""
+    tile-shape cost model, else an SK_CFGS index (+ 8: whole tiles only)."""
     if cfg is None:
         cfg = sk_config(x.shape[0], N, x.shape[1], epi)
     ws, tk, ncu = _sk_workspace(x.device)
-    kw = {}
-    if rownorm is not None:
-        kw["rowss"], kw["eps"] = rownorm[0], float(rownorm[1])
-    if xn is not None:
-        kw["xout"], kw["ss_out"] = xn
-    ext().gemm_sk(x, wf, N, out, _SK_EPI[epi], ws, tk, ncu, SK_MIN_SHARE if min_share is None else min_share, cfg,
-                  **kw)
+    ext().gemm_sk(x, wf, N, out, _SK_EPI[epi], ws, tk, ncu, SK_MIN_SHARE if min_share is None else min_share, cfg)
     return out
 
 
-def linear_res(x: torch.Tensor, w: PackedWeight, h: torch.Tensor, xn=None) -> torch.Tensor:
+def linear_res(x: torch.Tensor, w: PackedWeight, h: torch.Tensor) -> torch.Tensor:
     """h[:M] += x @ W^T in f32 (prefill o / down, M > 64, TP = 1): the residual add rides in the GEMM epilogue, so the
     norm after it reads h alone.  bf16 weights, or quantised ones through their bf16 dequantisation scratch; W8A8
-    fp8 prefill keeps its slab path (``res_supported``).  xn = (xout, ss_out): the epilogue also writes bf16(h) and
-    the row sums of h^2 (Q24), so the next projection runs norm-free (``linear(..., rownorm=(ss_out, eps))``)."""
+    fp8 prefill keeps its slab path (``res_supported``)."""
     M = x.shape[0]
     if not _gpu(x):
         h[:M] += ref.linear(x, w.dense(), "f32")
-        if xn is not None:
-            xn[0].view(-1)[: M * w.N].copy_(h[:M].to(torch.bfloat16).reshape(-1))
-            xn[1][:M] += ss_q24(h[:M].float().pow(2).sum(1))
         return h
     wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
-    return gemm_sk(x, wf, w.N, h, "res", xn=xn)
+    return gemm_sk(x, wf, w.N, h, "res")
 
 
 def linear_rope(x: torch.Tensor, w: PackedWeight, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc,
-                H: int, Hkv: int, rownorm=None) -> None:
+                H: int, Hkv: int) -> None:
     """The prefill qkv projection with RoPE and the paged bf16 KV-cache append fused into the GEMM epilogue (M > 64,
-    bf16 cache): q_out [T, H, 128] = rotated q, the cache gets rotated k and v at each token's slot.  rownorm =
-    (ss, eps): norm-free input rows, as in ``gemm_sk``.  CPU: the unfused reference (bf16 qkv, then
-    ``rope_append``)."""
+    bf16 cache): q_out [T, H, 128] = rotated q, the cache gets rotated k and v at each token's slot.  CPU: the
+    unfused reference (bf16 qkv, then ``rope_append``)."""
     if not _gpu(x):
-        qkv = linear(x, w, "bf16", rownorm=rownorm)
+        qkv = linear(x, w, "bf16")
         return ref.rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
     wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
     ws, tk, ncu = _sk_workspace(x.device)
-    rowss, eps = (None, 0.0) if rownorm is None else (rownorm[0], float(rownorm[1]))
     ext().gemm_sk_rope(x, wf, ws, tk, ncu, SK_MIN_SHARE, rope_config(x.shape[0], w.N, x.shape[1]), pos, tok_seq,
-                       block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, rowss, eps)
+                       block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
 
 
 def rope_config(M: int, N: int, K: int) -> int:
@@ -591,14 +576,13 @@ def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[to
             return out
         return y
     if M > 64 and epi in ("bf16", "f32", "silu") and not (w.kind == "fp8" and FP8_W8A8 and K % 128 == 0):
-        # prefill: the stream-K tile kernel (epi 'f32' returns one [1, M, N] slab whatever splitk asked for;
-        # rownorm with 'bf16': the norm-free prefill's qkv, see ``gemm_sk``)
-        assert res is None and (rownorm is None or epi == "bf16"), "prefill: rownorm on bf16 outputs only"
+        # prefill: the stream-K tile kernel (epi 'f32' returns one [1, M, N] slab whatever splitk asked for)
+        assert rownorm is None and res is None, "epilogue extensions are decode-only (M <= 64)"
         if out is None:
             out = torch.empty(*((1, M, w.N) if epi == "f32" else (M, w.N // 2 if epi == "silu" else w.N)),
                               device=x.device, dtype=torch.float32 if epi == "f32" else torch.bfloat16)
         wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
-        return gemm_sk(x, wf, w.N, out, epi, rownorm=rownorm)
+        return gemm_sk(x, wf, w.N, out, epi)
     nb0, sk0, wv0, dv0 = pick_gemm_config(M, w.N, K, epi, kind=w.kind)
     nb = nb0 if nb is None else nb
     if M > 64:  # prefill tile kernels: split-K (f32 slabs) only where the tile grid is small
@@ -926,6 +910,57 @@ def linear_a8(x8: torch.Tensor, sx: Optional[torch.Tensor], M: int, w: PackedWei
     return out
 
 
+def linear_a8_rr(h: torch.Tensor, parts: torch.Tensor, h_out: torch.Tensor, w: PackedWeight, epi: str,
+                 out: Optional[torch.Tensor] = None, out_s8: Optional[torch.Tensor] = None,
+                 ss_out: Optional[torch.Tensor] = None, eps: float = 1e-5, splitk: Optional[int] = None) -> torch.Tensor:
+    """Batch-1 W8A8 / W4A8 decode projection (fp8 or MXFP4 weights) with the residual add AND the activation
+    quantisation in its prologue (gemm_fp8a.hip RR): x = h + sum_s parts[s] (h_out <- x), quantised to e4m3 with one
+    E8M0 scale per 32 k -- no quantising norm launch before it.  The RMSNorm gamma is folded into W; the row scale
+    r = rsqrt(mean(x^2) + eps) is applied
+      * epi='silu' (gate_up): in the epilogue from the workgroup's own full-row sum; the output is the down
+        projection's e4m3 input in the xf8 layout (``out``) with one E8M0 per 32 columns (``out_s8``);
+      * epi='f32' (qkv): not here -- [splitk, 1, N] f32 slabs of W @ q(x), and sum x^2 goes to ss_out[0] (Q24) for
+        the slab consumer (``attn_decode(rownorm=...)``)."""
+    K = w.K
+    assert epi in ("f32", "silu") and parts.dim() == 3 and parts.shape[1] == 1
+    kind = "fp8a" if w.kind == "fp8" else "fp4a"
+    nb, sk0, waves, div = pick_gemm_config(1, w.N, K, "silu8" if epi == "silu" else epi, xf=True, kind=kind)
+    splitk = 1 if epi == "silu" else (sk0 if splitk is None else splitk)
+    if not _gpu(h):
+        x = h.view(-1)[:K].float() + parts.float().sum(0).view(-1)
+        h_out.view(-1)[:K].copy_(x)
+        q, s = quantize_blocks_fp8(x.view(1, K), 32)
+        y = dequant_blocks_fp8(q, s) @ w.dense().float().t()
+        if epi == "f32":
+            ss_out.view(-1)[:1] += ss_q24(x.pow(2).sum().view(1))
+            o = out if out is not None else torch.empty(splitk, 1, w.N)
+            o.view(-1)[: splitk * w.N].zero_()
+            o.view(splitk, 1, w.N)[0].copy_(y)
+            return o
+        y = y * torch.rsqrt(x.pow(2).sum() / K + eps)
+        F = w.N // 2
+        y3 = y.view(1, F // 16, 2, 16)
+        act = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(1, F)
+        qa, sa = quantize_blocks_fp8(act, 32)
+        out.view(-1)[: 16 * F].copy_(to_xf8(qa, 1))
+        out_s8.view(-1)[: 64 * (F // 128)].copy_(to_xs8(sa, 1))
+        return out
+    assert w.kind in ("fp8", "mxfp4"), "linear_a8_rr runs fp8 / MXFP4 weights"
+    if out is None:
+        assert epi == "f32"
+        out = torch.empty(splitk, 1, w.N, device=h.device, dtype=torch.float32)
+    fp4 = w.kind == "mxfp4"
+    ext().a8_gemm_rr(h.view(-1)[:K], parts, h_out.view(-1), w.data, None if fp4 else w.scale, w.scale if fp4 else None,
+                     w.N, out, out_s8, EPI[epi], nb, splitk, waves, _fp8_depth(div), ss_out=ss_out, eps=float(eps))
+    return out
+
+
+def rr_a8_supported(w: PackedWeight, K: int, splitk: int = 1) -> bool:
+    """Whether a batch-1 W8A8 / W4A8 GEMM can take the residual-reduce prologue (``linear_a8_rr``): K slices that
+    fit the kernel's LDS image (gemm_fp8a.hip A8_RR_KMAX)."""
+    return w.kind in ("fp8", "mxfp4") and K % 128 == 0 and (K // 128 + splitk - 1) // splitk * 128 <= 8192
+
+
 # ----------------------------------------------------------------------------------- norms / rope
 def add_rmsnorm(h: torch.Tensor, w: torch.Tensor, eps: float, xn: torch.Tensor,
                 parts: Optional[torch.Tensor] = None, ids: Optional[torch.Tensor] = None,
@@ -1205,12 +1240,6 @@ def attn_decode(q, kc, vc, block_tables, pos, H, Hkv, scale, out, workspace=None
 # sequence has >= 512 rows (measured, scripts/bench_attn_prefill.py: 7B 2k 146 -> 119 us, 3B 2k 118 -> 115 us,
 # 8k 1051 -> 1021 us), else 16 (32 x 128-token prompts: 28 vs 31 us, twice the work items)
 PREFILL_ATTN = "auto"
-# KV split of heavy causal query blocks in the 32-row kernel (attention_prefill32.hip SPLIT): "0" = never (default),
-# N = every block of more than N tiles.  Off by default:
-# measured slower (profiles/r5/attn_prefill_kv_split_inlaunch_ab_mi355x.jsonl: 3B 2k 65.4 -> 74.5 us at the auto
-# threshold, 76.6-95.9 at 26 / 22 / 20 / 16; 3B 4 x 1k 74.0 -> 84.7) -- a CU is throughput-bound on one busy group
-# (two busy groups each take ~2x the tile time), so halving the longest chain only moves work between groups
-PREFILL_SPLIT = os.environ.get("LSA_PREFILL_SPLIT", "0")
 
 
 def _prefill_kernel(cu_q: list) -> str:
@@ -1225,30 +1254,18 @@ def prefill_qblock(cu_q: Optional[list] = None) -> int:
     return 128 if k == "32" else ext().prefill_qblock
 
 
-def _split_threshold(nts: list, heads: int, cus: int) -> int:
-    """Tile count above which a query block is split into two key-tile ranges (0: none) -- ``PREFILL_SPLIT``.  (An
-    automatic choice from a makespan model of the paired launch was built and dropped: the model, with pieces of
-    two busy groups at twice the tile time, still predicted the 3B 2k split at 24 tiles faster; measured slower.)"""
-    return int(PREFILL_SPLIT) if PREFILL_SPLIT not in ("", "0") else 0
-
-
-class PrefillWork(list):
-    """prefill_work's rows; ``split``: the rows are 8-int (KV-split) items."""
-    split = False
-
-
 def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[list[int]] = None,
-                 kernel: Optional[str] = None, heads: int = 32, cus: int = 256) -> PrefillWork:
+                 kernel: Optional[str] = None, heads: int = 32) -> list:
     """Work items of the prefill attention kernel for packed sequences (cu_q offsets; ``ctx`` = per-sequence
     context length after this prefill, default = the chunk length, i.e. no cached prefix).
 
     16-row kernel: (seq, q_start) per workgroup, heaviest (latest) query blocks first.
     32-row kernel ('32'): NG items (seq, q_start, t0, t1) per workgroup -- the key tiles [t0, t1) = the whole causal
-    range of a 128-row query block; NG = 2 pairs a heavy block with a light one (``_pair_blocks``).  With KV split
-    (``_split_threshold``) a heavy block becomes two pieces [0, mid) and [mid, nt) sharing a merge slot: every item is
-    then (seq, q_start, t0, t1, slot, piece, 0, 0), slot -1 for unsplit blocks.  (A split merged by a second launch
-    and two halves merged in LDS were built in earlier rounds and measured slower -- profiles/attn_prefill_kv_split_
-    mi355x.jsonl, profiles/attn_prefill_halves_mi355x.jsonl; this one merges in the same launch.)"""
+    range of a 128-row query block; NG = 2 pairs a heavy block with a light one (``_pair_blocks``).  (Cutting heavy
+    blocks into KV-split pieces -- merged by a second launch, in LDS, or in the same launch through write-through
+    partials -- was built three times and measured slower each time: profiles/attn_prefill_kv_split_mi355x.jsonl,
+    profiles/attn_prefill_halves_mi355x.jsonl, profiles/r5/attn_prefill_kv_split_inlaunch_ab_mi355x.jsonl: a CU is
+    throughput-bound on one busy group, so halving the longest chain only moves work between groups.)"""
     kernel = kernel or _prefill_kernel(cu_q)
     if qblock is None:
         qblock = 128 if kernel == "32" else ext().prefill_qblock
@@ -1260,29 +1277,14 @@ def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[li
             items.append(((pos0 + min(qs + qblock, ql) + 63) // 64, s, qs))
     items.sort(key=lambda t: -t[0])
     if kernel != "32":
-        return PrefillWork((s, qs) for _, s, qs in items)
-    S = _split_threshold([nt for nt, _, _ in items], heads, cus)
-    if S:
-        units, slot = [], 0
-        for nt, s, qs in items:
-            if nt > S:
-                mid = nt // 2
-                units += [(s, qs, 0, mid, slot, 0, 0, 0), (s, qs, mid, nt, slot, 1, 0, 0)]
-                slot += 1
-            else:
-                units.append((s, qs, 0, nt, -1, 0, 0, 0))
-        units.sort(key=lambda u: -(u[3] - u[2]))
-        empty = (-1, 0, 0, 0, -1, 0, 0, 0)
-    else:
-        units = [(s, qs, 0, nt) for nt, s, qs in items]
-        empty = (-1, 0, 0, 0)
+        return [(s, qs) for _, s, qs in items]
+    units = [(s, qs, 0, nt) for nt, s, qs in items]
+    empty = (-1, 0, 0, 0)
     n = len(units)
     longest = max(cu_q[i + 1] - cu_q[i] for i in range(len(cu_q) - 1))
-    out = PrefillWork()
-    out.split = bool(S)
     if not _pair_blocks(n, heads, longest, qblock):
-        out.extend(units)
-        return out
+        return units
+    out = []
     for i in range((n + 1) // 2):
         j = n - 1 - i
         b = units[j] if j > i else empty
@@ -1293,8 +1295,7 @@ def prefill_work(cu_q: list[int], qblock: Optional[int] = None, ctx: Optional[li
 class PrefillPlan(NamedTuple):
     """Device-side plan of one prefill attention call (``prefill_plan``)."""
     kernel: str
-    work: torch.Tensor  # int32 [n_workgroups, 2 | 4 * NG | 8 * NG]
-    split_slots: int = 0  # merge slots per head (KV-split blocks); 0 = no split
+    work: torch.Tensor  # int32 [n_workgroups, 2 | 4 * NG]
 
 
 def prefill_plan(cu_q: list[int], ctx: Optional[list[int]] = None, heads: int = 32, device=None,
@@ -1303,31 +1304,9 @@ def prefill_plan(cu_q: list[int], ctx: Optional[list[int]] = None, heads: int = 
     kernel = kernel or _prefill_kernel(cu_q)
     rows = prefill_work(cu_q, ctx=ctx, kernel=kernel, heads=heads)
     w = torch.tensor(rows, dtype=torch.int32)
-    slots = 0
-    if kernel == "32" and rows.split:
-        wv = w.view(-1, 8)
-        live = wv[:, 0] >= 0
-        slots = int(wv[live, 4].max().item()) + 1 if bool(live.any()) else 0
     if device is not None:
         w = w.to(device, non_blocking=True)
-    return PrefillPlan(kernel, w, slots)
-
-
-_p32_split_ws: dict = {}
-
-
-def _prefill_split_workspace(device, slots: int):
-    """(opart, mlpart, tickets) for ``slots`` merge slots (x heads, by the caller), per (device, stream): the tickets
-    are zero between calls (each merge resets its own), so one launch at a time per stream may use them."""
-    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
-    got = _p32_split_ws.get(key)
-    if got is None or got[2].numel() < slots:
-        n = max(slots, 256)
-        got = (torch.empty(n * 2 * 4 * 4096, dtype=torch.float32, device=device),
-               torch.empty(n * 2 * 4 * 64 * 2, dtype=torch.float32, device=device),
-               torch.zeros(n, dtype=torch.int32, device=device))
-        _p32_split_ws[key] = got
-    return got
+    return PrefillPlan(kernel, w)
 
 
 # auto | 1 | 0 -- heavy/light paired query blocks in the 32-row prefill kernel
@@ -1362,12 +1341,8 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, wo
     if plan is None:
         plan = (prefill_plan(cu, ctx=ctx_lens.tolist(), heads=H, device=q.device) if work is None
                 else PrefillPlan(_prefill_kernel(cu), work))
-    if plan.kernel == "32" and plan.split_slots:
-        op, mp, tk = _prefill_split_workspace(q.device, plan.split_slots * H)
-        ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out, 3, op, mp, tk)
-    else:
-        ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out,
-                           1 if plan.kernel == "32" else 0)
+    ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out,
+                       1 if plan.kernel == "32" else 0)
     return out
 
 

@@ -3,6 +3,7 @@ process, arms interleaved (cdna_hip_programming.md §5.4 rule 24).  One JSON lin
 
     python scripts/ab_decode_b1.py llama3.2 2048     # BASELINE config 3 (3B /explain_error, 2k prompt)
     python scripts/ab_decode_b1.py duckdb-nsql 128   # BASELINE config 2 (7B NL->SQL, batch 1)
+    python scripts/ab_decode_b1.py duckdb-nsql 128 3 "" mxfp4   # the same with MXFP4 weights (W4A8 RR step)
 """
 import json
 import os
@@ -18,9 +19,10 @@ from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build
 model = sys.argv[1] if len(sys.argv) > 1 else "llama3.2"
 plen = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-only = sys.argv[4] if len(sys.argv) > 4 else None  # one arm (profiling runs)
+only = (sys.argv[4] or None) if len(sys.argv) > 4 else None  # one arm (profiling runs)
+dtype = sys.argv[5] if len(sys.argv) > 5 else "bf16"  # bf16 | fp8 | mxfp4 weights
 new = 128
-eng = build_engine(model, device="cuda:0", dtype="bf16", max_slots=2 if plen > 1024 else 32,
+eng = build_engine(model, device="cuda:0", dtype=dtype, max_slots=2 if plen > 1024 else 32,
                    max_model_len=plen + new + 64, seed=0)
 r = eng.runner
 g = torch.Generator().manual_seed(4321)
@@ -31,7 +33,7 @@ res = {k: [] for k in arms}
 for k, on in arms.items():
     r.rr_decode = on
     r.graphs.clear()
-    num = numerics_check(eng, [prompt], 64, True, 1, model, "bf16", None)
+    num = numerics_check(eng, [prompt], 64, True, 1, model, dtype, None)
     print(json.dumps({"arm": k, "numerics": num, "launches_b1": r.count_step_kernels(1)}), flush=True)
 for i in range(rounds):
     for k, on in arms.items():
@@ -41,4 +43,4 @@ for i in range(rounds):
         res[k].append(dev)
         print(json.dumps({"arm": k, "round": i, "decode_device_ms_per_step": round(dev, 4), "p50_s": round(p50, 4)}),
               flush=True)
-print(json.dumps({"model": model, "prompt_len": plen, **{k: round(statistics.median(v), 4) for k, v in res.items()}}))
+print(json.dumps({"model": model, "dtype": dtype, "prompt_len": plen, **{k: round(statistics.median(v), 4) for k, v in res.items()}}))

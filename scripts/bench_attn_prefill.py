@@ -1,6 +1,6 @@
 """Prefill (causal flash) attention on MI355X: us and TFLOP/s per call for the BASELINE prefill shapes
-(packed variable-length sequences over the paged cache).  Arms (interleaved per case): KV split thresholds
-(ops.PREFILL_SPLIT; LSA_ATTN_SPLITS=0,24 by default)."""
+(packed variable-length sequences over the paged cache).  Arms (interleaved per case): heavy / light query-block
+pairing of the 32-row kernel (ops.PREFILL_PAIR; LSA_ATTN_PAIR=auto,0 by default)."""
 import json
 import math
 import os
@@ -49,10 +49,10 @@ def case(name, nseq, qlen, H, Hkv):
     kk = kc[bt[0].long()].transpose(0, 1).reshape(Hkv, -1, 128)[:, :qlen].float().repeat_interleave(H // Hkv, 0)
     vv = vc[bt[0].long()].transpose(0, 1).reshape(Hkv, -1, 128)[:, :qlen].float().repeat_interleave(H // Hkv, 0)
     ref = torch.nn.functional.scaled_dot_product_attention(s0, kk, vv, is_causal=True).transpose(0, 1)
-    splits = os.environ.get("LSA_ATTN_SPLITS", "0,24").split(",")
+    splits = os.environ.get("LSA_ATTN_PAIR", "auto,0").split(",")  # heavy / light pairing arms (ops.PREFILL_PAIR)
     plans = {}
     for sp in splits:
-        ops.PREFILL_SPLIT = sp
+        ops.PREFILL_PAIR = sp
         plans[sp] = ops.prefill_plan(cu, heads=H, device=dev)
     res = {"case": name, "kernel": plans[splits[0]].kernel}
     times = {sp: [] for sp in splits}
@@ -66,8 +66,8 @@ def case(name, nseq, qlen, H, Hkv):
         torch.cuda.synchronize()
         err = (out[:qlen].float() - ref).abs().max().item()  # spot check vs SDPA on the first sequence
         us = sorted(times[sp])[1]
-        res[f"split_{sp}"] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1), "max_err": round(err, 4),
-                              "work": list(plans[sp].work.shape), "slots": plans[sp].split_slots}
+        res[f"pair_{sp}"] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1), "max_err": round(err, 4),
+                             "work": list(plans[sp].work.shape)}
     print(json.dumps(res), flush=True)
 
 case("3b_explain_2k", 1, 2048, 24, 8)

@@ -44,7 +44,6 @@ def case(name, nseq, qlen, H, Hkv):
     out = torch.empty_like(q)
     cud = torch.tensor(cu, dtype=torch.int32, device=dev)
     ctx = torch.full((nseq,), qlen, dtype=torch.int32, device=dev)
-    ops.PREFILL_SPLIT = "0"
     # arms: heavy / light pairing of the query blocks (ops.PREFILL_PAIR)
     ARMS = {"paired": "auto", "single": "0"}
     plans = {}

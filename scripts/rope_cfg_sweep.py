@@ -41,7 +41,7 @@ def case(name, T, d, H, Hkv):
     arms = {"unfused": unfused}
     for cfg in (-1, 0, 3, 8, 11, 16 + 0, 16 + 3, 16 + 8, 16 + 11):  # + 16: direct epilogue instead of the LDS image
         arms[f"rope_cfg{cfg}"] = (lambda c: lambda: ops.ext().gemm_sk_rope(
-            x, pw.data, ws, tk, ncu, ops.SK_MIN_SHARE, c, pos, tsq, bt, cos, sin, q, kc, vc, H, Hkv, None, 0.0))(cfg)
+            x, pw.data, ws, tk, ncu, ops.SK_MIN_SHARE, c, pos, tsq, bt, cos, sin, q, kc, vc, H, Hkv))(cfg)
     for _ in range(2):
         for a, fn in arms.items():
             try:

@@ -2,7 +2,7 @@
 one-token request (prefill + first-token commit + host read-back) for each case, median (and min) of the rounds.
 Knob 'one_phase': the stream-K GEMM's one-phase K-loop schedule for the 128-row tiles (ext.gemm_sk_one_phase);
 'none': one arm, the loaded build (cross-build A/Bs: run it under LSA_HIP_SO=variants/<name>.so in turns).
-Usage: ttft_knob_ab.py [knob] [rounds]"""
+Usage: ttft_knob_ab.py [knob] [rounds] [case,...]"""
 import json
 import statistics
 import sys
@@ -21,6 +21,8 @@ setk = KNOBS[knob]
 # (model, prompt tokens, requests in the batch): config 3 (3B explain, 2k prompt), config 2 (7B NL->SQL prompt),
 # the headline bench's batch-32 prefill (32 x 128 tokens)
 CASES = [("llama3.2", 2048, 1), ("duckdb-nsql", 300, 1), ("duckdb-nsql", 128, 32)]
+if len(sys.argv) > 3:  # a subset, e.g. "0,1" (a cross-build A/B whose older build lacks a binding the last case uses)
+    CASES = [CASES[int(i)] for i in sys.argv[3].split(",")]
 sp = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
 for model, plen, nreq in CASES:
     eng = build_engine(model, device="cuda:0", dtype="bf16", max_slots=max(2, nreq), max_model_len=plen + 128, seed=0,

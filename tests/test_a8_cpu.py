@@ -141,3 +141,13 @@ def test_oracle_block_scaled_decode_inputs():
         d = (got[4:] - prev[4:]).abs().max()
         assert 0 < d < 0.05 * prev[4:].abs().max(), (flag, float(d))
     assert f8.shape == prev.shape
+    # the batch-1 residual-reduce step's qkv / gate_up inputs (rr): per-32-block E8M0 rounding of the raw residual
+    # with the row scale after the GEMM -- moves only the decode rows, by e4m3 rounding-level amounts, and
+    # differently from the per-row rounding of the batched steps
+    rows = reference_forward(w, ids, act_quant_rows=4, decode_a8=dict(qkv=True, gate_up=True))
+    blk = reference_forward(w, ids, act_quant_rows=4, decode_a8=dict(qkv=True, gate_up=True, rr=True))
+    assert torch.equal(blk[:4], prev[:4])
+    for got in (rows, blk):
+        d = (got[4:] - prev[4:]).abs().max()
+        assert 0 < d < 0.05 * prev[4:].abs().max(), float(d)
+    assert not torch.equal(rows[4:], blk[4:])

@@ -219,7 +219,7 @@ def test_decode_tokens_kv_fp8_prod_shapes(gpu, model, dtype, B):
     res = eng.generate(prompts, SamplingParams(max_tokens=12, ignore_eos=True))
     rows = sum(len(q) for q in prompts)
     bk = r.bucket(B)
-    plan = dict(zip(("qkv", "gate_up", "o", "down"), r.a8_plan(bk)))
+    plan = r.oracle_plan(bk)
     worst = 0.0
     for p, out in zip(prompts, res[: min(B, 6)]):
         lg = reference_forward(r.w, p + out.token_ids[:-1], act_quant_rows=len(p) if rows > 64 else 0,

@@ -60,28 +60,15 @@ def test_norm_and_attention_xf_cpu():
     assert torch.equal(ops.from_xfrag(of, 2, H * Dh), o.view(2, -1))
 
 
-def _check_plan(cu, ctx, heads, pair, monkeypatch, split="0"):
+def _check_plan(cu, ctx, heads, pair, monkeypatch):
     monkeypatch.setattr(ops, "PREFILL_PAIR", pair)
-    monkeypatch.setattr(ops, "PREFILL_SPLIT", split)
     work = ops.prefill_work(cu, ctx=ctx, kernel="32", heads=heads)
-    wi = 8 if work.split else 4
-    assert all(len(w) in (wi, 2 * wi) for w in work)
-    units = [tuple(w[i:i + wi]) for w in work for i in range(0, len(w), wi) if w[i] >= 0]
-    cover, slots = {}, {}
-    for u in units:
-        s, qs, t0, t1 = u[:4]
-        if wi == 8 and u[4] >= 0:  # a split piece: the two pieces of one slot tile the block's range
-            assert u[5] in (0, 1) and (u[4], u[5]) not in slots
-            slots[(u[4], u[5])] = (s, qs, t0, t1)
-            continue
+    assert all(len(w) in (4, 8) for w in work)
+    units = [tuple(w[i:i + 4]) for w in work for i in range(0, len(w), 4) if w[i] >= 0]
+    cover = {}
+    for s, qs, t0, t1 in units:
         assert (s, qs) not in cover  # one work item per query block
         cover[(s, qs)] = (t0, t1)
-    for (slot, piece), (s, qs, t0, t1) in list(slots.items()):
-        if piece == 0:
-            s1, qs1, m, t2 = slots[(slot, 1)]
-            assert (s1, qs1) == (s, qs) and t0 == 0 and m == t1 and t1 < t2
-            assert (s, qs) not in cover
-            cover[(s, qs)] = (0, t2)
     for s in range(len(cu) - 1):
         ql, pos0 = cu[s + 1] - cu[s], ctx[s] - (cu[s + 1] - cu[s])
         for qs in range(0, ql, 128):
@@ -101,18 +88,6 @@ def test_prefill_plan_covers_causal_ranges(monkeypatch):
     w = _check_plan([0, 10, 210, 310], [700, 264, 400], 32, "0", monkeypatch)
     assert all(len(r) == 4 for r in w)
     _check_plan([0, 8192], [8192], 24, "auto", monkeypatch)
-
-
-def test_prefill_plan_kv_split(monkeypatch):
-    """KV split of heavy causal blocks (off by default: measured slower): a threshold splits every heavier block into
-    two pieces that tile its range and share one merge slot; "0" keeps the 4-int items."""
-    w = _check_plan([0, 2048], [2048], 24, "auto", monkeypatch, split="0")
-    assert not w.split
-    w = _check_plan([0, 2048], [2048], 24, "auto", monkeypatch, split="24")
-    assert w.split
-    assert sum(1 for r in w for i in range(0, len(r), 8) if r[i] >= 0 and r[i + 4] >= 0) == 8  # 4 blocks, 2 pieces
-    _check_plan([0, 10, 210, 1310], [700, 264, 1400], 32, "1", monkeypatch, split="6")
-    _check_plan([0, 10, 210, 1310], [700, 264, 1400], 32, "0", monkeypatch, split="6")
 
 
 def test_extension_loads_and_matches_its_sources():

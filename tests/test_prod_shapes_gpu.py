@@ -75,7 +75,7 @@ def test_decode_tokens_prod_shapes(gpu, model, dtype, B):
         # decode buckets of an fp8 model run some projections W8A8 (ops.linear_a8, ModelRunner.a8_plan)
         r, bk = eng.runner, eng.runner.bucket(B)
         lg = reference_forward(r.w, p + out.token_ids[:-1], act_quant_rows=len(p) if rows > 64 else 0,
-                               decode_a8=dict(zip(("qkv", "gate_up", "o", "down"), r.a8_plan(bk))))[len(p) - 1:]
+                               decode_a8=r.oracle_plan(bk))[len(p) - 1:]
         chosen = lg.gather(1, torch.tensor(out.token_ids, device=lg.device).view(-1, 1)).squeeze(1)
         top = lg.max(1).values
         spread = lg.std(1)

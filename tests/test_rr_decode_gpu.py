@@ -154,3 +154,73 @@ def test_engine_rr_step_launch_count(gpu):
     L = r.L
     assert n_rr <= 5 * L + 6, (n_rr, L)
     assert n_nl - n_rr >= L, (n_nl, n_rr)
+
+
+@pytest.mark.parametrize("kind", ["mxfp4", "fp8"])
+@pytest.mark.parametrize("K,N,splitk,nparts", [(4096, 12288, 8, 4), (3072, 5120, 4, 2), (2048, 1024, 1, 1)])
+def test_linear_a8_rr_f32_slabs(gpu, kind, K, N, splitk, nparts):
+    """W8A8 / W4A8 batch-1 GEMM with the residual-reduce prologue: slabs == the block-quantised reference product
+    (x quantised to e4m3 with one E8M0 per 32 k, ops.quantize_blocks_fp8), h_out = x, ss_out += sum x^2."""
+    h, parts = _inputs(K, nparts, gpu, seed=K + N)
+    pw = ops.PackedWeight.from_dense((torch.randn(N, K, device=gpu) / math.sqrt(K)), kind)
+    h_out = torch.zeros(1, K, device=gpu)
+    ss = torch.zeros(2, dtype=torch.int64, device=gpu)
+    y = ops.linear_a8_rr(h, parts, h_out, pw, "f32", ss_out=ss, splitk=splitk)
+    torch.cuda.synchronize()
+    x = h.float() + parts.float().sum(0)
+    assert _rel(h_out, x) < 1e-6
+    q, s = ops.quantize_blocks_fp8(x, 32)
+    yr = ops.dequant_blocks_fp8(q, s) @ pw.dense().float().t()
+    assert _rel(y.sum(0), yr) < 2e-3
+    assert _rel(y.sum(0), x @ pw.dense().float().t()) < 6e-2  # e4m3 activations vs the exact product
+    want = x.pow(2).sum().item()
+    assert abs(ops.ss_float(ss[:1]).item() - want) / want < 1e-5 and ss[1] == 0
+
+
+@pytest.mark.parametrize("kind", ["mxfp4", "fp8"])
+@pytest.mark.parametrize("K,F,nparts", [(4096, 11008, 1), (3072, 8192, 4), (2048, 1024, 3)])
+def test_linear_a8_rr_silu_e4m3(gpu, kind, K, F, nparts):
+    """The gate_up form: SiLU(r g) * (r u) from the workgroup's own full-row RMS, written as the down projection's
+    e4m3 input (xf8 layout) with one E8M0 per 32 columns."""
+    h, parts = _inputs(K, nparts, gpu, seed=F + K)
+    wg, wu = torch.randn(F, K, device=gpu) / math.sqrt(K), torch.randn(F, K, device=gpu) / math.sqrt(K)
+    pw = ops.PackedWeight.from_dense(ops.interleave_gate_up(wg, wu), kind)
+    h_out = torch.zeros(1, K, device=gpu)
+    x8 = torch.zeros(16 * F, dtype=torch.uint8, device=gpu)
+    s8 = torch.full((64 * (F // 128),), 127, dtype=torch.uint8, device=gpu)
+    ops.linear_a8_rr(h, parts, h_out, pw, "silu", out=x8, out_s8=s8, eps=1e-5)
+    torch.cuda.synchronize()
+    got = ops.xf8_dequant(x8, 1, F, None, s8)
+    x = h.float() + parts.float().sum(0)
+    q, s = ops.quantize_blocks_fp8(x, 32)
+    xq = ops.dequant_blocks_fp8(q, s)
+    wd = pw.dense().float()
+    y = (xq @ wd.t()) * torch.rsqrt(x.pow(2).mean() + 1e-5)
+    y3 = y.view(1, F // 16, 2, 16)
+    want = (torch.nn.functional.silu(y3[:, :, 0]) * y3[:, :, 1]).reshape(1, F)
+    assert _rel(got, want) < 4e-2  # e4m3 output rounding
+    assert _rel(h_out, x) < 1e-6
+
+
+def test_engine_rr_a8_mxfp4_b1(gpu):
+    """MXFP4 engine at batch 1: the residual-reduce W4A8 step (qkv / gate_up quantise their own inputs; 5 launches per
+    layer, no quantising norm launch) against the fp32 oracle (the mxfp4 numerics criterion) and against the W4A8 step
+    with norm launches (launch count)."""
+    from llm_based_apache_spark_optimization_amd.engine import build_engine
+    from llm_based_apache_spark_optimization_amd.eval import numerics as nm
+
+    eng = build_engine("tiny-nsql", device=str(gpu), dtype="mxfp4", max_slots=4, max_model_len=512, seed=1)
+    r = eng.runner
+    assert r.rr_a8 and r.rr_decode, (r.a8_plan(1), r.wide_norm)
+    n_rr = r.count_step_kernels(1)
+    ids = [eng.encode("How many rows are there in the taxi table?")]
+    num = nm.teacher_forced_check(eng, ids, n_steps=16, check_rows=(0,))
+    assert num["ok"], num
+    r.rr_decode = False
+    r.graphs.clear()
+    n_nl = r.count_step_kernels(1)
+    num0 = nm.teacher_forced_check(eng, ids, n_steps=16, check_rows=(0,))
+    r.rr_decode = True
+    r.graphs.clear()
+    assert n_nl - n_rr >= 2 * r.L - 1, (n_nl, n_rr)
+    assert num["mean_kl"] < 2 * num0["mean_kl"] + 1e-3, (num, num0)
