@@ -99,9 +99,8 @@ __device__ __forceinline__ void ar_res_epilogue(const ArRes& res, long i, const 
   pk.x = pack2bf(hv.x, hv.y);
   pk.y = pack2bf(hv.z, hv.w);
   *reinterpret_cast<uint2*>(res.xn + (res.xmt ? xf_off(m, c, res.xmt) : (size_t)m * res.D + c)) = pk;
-  float sq = hv.x * hv.x + hv.y * hv.y + hv.z * hv.z + hv.w * hv.w;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sq += __shfl_xor(sq, o, 64);
+  // the row's wave sum on DPP / permlane (common.h), not __shfl_xor's ds_bpermute LDS round trips (whole wave active)
+  const float sq = wave_sum(hv.x * hv.x + hv.y * hv.y + hv.z * hv.z + hv.w * hv.w);
   if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(res.ss) + m, (unsigned long long)ss_to_q24(sq));
 }
 

@@ -221,13 +221,7 @@ class ModelRunner:
         # batch-1 residual-reduce step (_decode_step_rr): the qkv and gate_up GEMMs fold the residual add of the
         # previous row-parallel projection's slabs into their prologue (ops.linear_rr), so a layer issues 5 launches
         # (qkv, attention, o, gate_up, down) and no residual-add launch; TP = 1, bf16 weights, gammas folded
-        lw0 = weights.layers[0]
-        # quantised weights whose batch-1 step runs all four projections W8A8 / W4A8 (MXFP4): the qkv / gate_up GEMMs
-        # quantise their own residual-reduced input (ops.linear_a8_rr), so the two quantising norm launches go too
-        self.rr_a8 = all(self.a8_plan(1)) and ops.rr_a8_supported(lw0.wqkv, self.d) and ops.rr_a8_supported(
-            lw0.w_gate_up, self.d) and self._a8_splitk_b1() <= 4  # the prologue sums at most 4 slabs
-        self.rr_decode = (RR_DECODE and tps == 1 and self.wide_norm and (self.rr_a8 or (
-            ops.rr_supported(lw0.wqkv, self.d) and ops.rr_supported(lw0.w_gate_up, self.d))))
+        self._plan_rr()
         self.zero_slab = torch.zeros(1, 1, self.d, **f32)  # layer 0's "previous projection" in the W8A8 RR step
         self.h_alt = torch.zeros(1, self.d, **f32)  # the residual stream's second buffer (h_out never aliases h)
         self.graphs: dict = {}
@@ -273,6 +267,24 @@ class ModelRunner:
             return (False, False, False, False)
         qkv, gu, od = B > self.a8_min_batch, B > self.a8_mlp_min_batch, B <= self.a8_od_max_batch
         return (qkv, gu, od, gu and od and self.a8_down_ok)
+
+    def _plan_rr(self) -> None:
+        """rr_a8 / rr_decode from the current a8 buckets (``set_a8_buckets`` re-plans)."""
+        lw0 = self.w.layers[0]
+        # quantised weights whose batch-1 step runs all four projections W8A8 / W4A8 (MXFP4): the qkv / gate_up GEMMs
+        # quantise their own residual-reduced input (ops.linear_a8_rr), so the two quantising norm launches go too
+        self.rr_a8 = all(self.a8_plan(1)) and ops.rr_a8_supported(lw0.wqkv, self.d) and ops.rr_a8_supported(
+            lw0.w_gate_up, self.d) and self._a8_splitk_b1() <= 4  # the prologue sums at most 4 slabs
+        tps = 1 if self.tp is None else self.tp.size
+        self.rr_decode = (RR_DECODE and tps == 1 and self.wide_norm and (self.rr_a8 or (
+            ops.rr_supported(lw0.wqkv, self.d) and ops.rr_supported(lw0.w_gate_up, self.d))))
+
+    def set_a8_buckets(self, min_batch: int, mlp_min_batch: int, od_max_batch: int) -> None:
+        """Re-plan which decode buckets run W8A8 / W4A8 (``a8_plan``) and the batch-1 residual-reduce step; drops
+        captured graphs."""
+        self.a8_min_batch, self.a8_mlp_min_batch, self.a8_od_max_batch = min_batch, mlp_min_batch, od_max_batch
+        self._plan_rr()
+        self.graphs.clear()
 
     def _a8_splitk_b1(self) -> int:
         """The larger split-K of the batch-1 W8A8 / W4A8 o and down GEMMs (the slabs a residual-reduce prologue sums;
