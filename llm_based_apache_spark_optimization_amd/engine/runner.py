@@ -511,11 +511,11 @@ class ModelRunner:
         a8 = self.rr_a8
         if a8:
             ak = "fp8a" if w.layers[0].wqkv.kind == "fp8" else "fp4a"
-            sk_q = ops.pick_gemm_config(1, nqkv, d, "f32", xf=True, kind=ak)[1]
+            sk_q = ops.rr_config(nqkv, d, "f32", w.layers[0].wqkv.kind)[1]
             sk_o = ops.pick_gemm_config(1, d, self.H * self.D, "f32", xf=True, kind=ak)[1]
             sk_d = ops.pick_gemm_config(1, d, self.ffn_l, "f32", xf=True, kind=ak)[1]
         else:
-            sk_q = self._splitk(1, d, nqkv, tp_reduced=False)
+            sk_q = ops.rr_config(nqkv, d, "f32", w.layers[0].wqkv.kind)[1] if self.on_gpu else 1
             sk_o = self._splitk(1, self.H * self.D)
             sk_d = self._splitk(1, self.ffn_l)
         assert sk_o <= 4 and sk_d <= 4, "the residual-reduce prologue sums at most 4 slabs"

@@ -910,9 +910,27 @@ def linear_a8(x8: torch.Tensor, sx: Optional[torch.Tensor], M: int, w: PackedWei
     return out
 
 
+def rr_config(N: int, K: int, epi: str, kind: str = "bf16") -> tuple[int, int, int, int]:
+    """(nb, splitk, waves, div) of a batch-1 residual-reduce GEMM (``linear_rr`` / ``linear_a8_rr``): the measured
+    "NxK:epi:b1:rr[:kind]" entry of the tuning table (scripts/sweep_rr_b1.py -- the prologue re-reads the residual
+    slice once per workgroup, so the best n-block width differs from the plain kernel's), else the plain kernel's
+    pick.  kind: 'bf16' or the weight kind ('fp8' / 'mxfp4': the W8A8 / W4A8 kernel)."""
+    a8 = kind in ("fp8", "mxfp4")
+    e = _tuning_table().get(f"{N}x{K}:{epi}:b1:rr" + (f":{kind}" if a8 else ""))
+    if e is not None:
+        return e["nb"], (1 if epi == "silu" else e["splitk"]), e["waves"], e["div"]
+    if a8:
+        ak = "fp8a" if kind == "fp8" else "fp4a"
+        nb, sk, wv, dv = pick_gemm_config(1, N, K, "silu8" if epi == "silu" else epi, xf=True, kind=ak)
+    else:
+        nb, sk, wv, dv = pick_gemm_config(1, N, K, epi, kind=kind)
+    return nb, (1 if epi == "silu" else sk), wv, dv
+
+
 def linear_a8_rr(h: torch.Tensor, parts: torch.Tensor, h_out: torch.Tensor, w: PackedWeight, epi: str,
                  out: Optional[torch.Tensor] = None, out_s8: Optional[torch.Tensor] = None,
-                 ss_out: Optional[torch.Tensor] = None, eps: float = 1e-5, splitk: Optional[int] = None) -> torch.Tensor:
+                 ss_out: Optional[torch.Tensor] = None, eps: float = 1e-5, splitk: Optional[int] = None,
+                 nb: Optional[int] = None, waves: Optional[int] = None, div: Optional[int] = None) -> torch.Tensor:
     """Batch-1 W8A8 / W4A8 decode projection (fp8 or MXFP4 weights) with the residual add AND the activation
     quantisation in its prologue (gemm_fp8a.hip RR): x = h + sum_s parts[s] (h_out <- x), quantised to e4m3 with one
     E8M0 scale per 32 k -- no quantising norm launch before it.  The RMSNorm gamma is folded into W; the row scale
@@ -923,9 +941,9 @@ def linear_a8_rr(h: torch.Tensor, parts: torch.Tensor, h_out: torch.Tensor, w: P
         the slab consumer (``attn_decode(rownorm=...)``)."""
     K = w.K
     assert epi in ("f32", "silu") and parts.dim() == 3 and parts.shape[1] == 1
-    kind = "fp8a" if w.kind == "fp8" else "fp4a"
-    nb, sk0, waves, div = pick_gemm_config(1, w.N, K, "silu8" if epi == "silu" else epi, xf=True, kind=kind)
+    nb0, sk0, wv0, dv0 = rr_config(w.N, K, epi, w.kind)
     splitk = 1 if epi == "silu" else (sk0 if splitk is None else splitk)
+    nb, waves, div = nb0 if nb is None else nb, wv0 if waves is None else waves, dv0 if div is None else div
     if not _gpu(h):
         x = h.view(-1)[:K].float() + parts.float().sum(0).view(-1)
         h_out.view(-1)[:K].copy_(x)
@@ -1045,7 +1063,7 @@ def linear_rr(h: torch.Tensor, parts: torch.Tensor, h_out: torch.Tensor, w: Pack
     Replaces the ``res_add_ss`` launch between the two projections (one kernel boundary less per layer side)."""
     K = w.K
     assert epi in ("f32", "silu") and h.numel() >= K and parts.dim() == 3 and parts.shape[1] == 1
-    nb0, sk0, wv0, dv0 = pick_gemm_config(1, w.N, K, epi, kind=w.kind)
+    nb0, sk0, wv0, dv0 = rr_config(w.N, K, epi, w.kind)
     splitk = 1 if epi == "silu" else (sk0 if splitk is None else splitk)
     nb = nb0 if nb is None else nb
     if not _gpu(h):
