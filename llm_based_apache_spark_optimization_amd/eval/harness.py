@@ -6,7 +6,8 @@ an 8-line expected SQL; C21) and the 4-query evaluation (C22) over ``mistral``, 
 (native C++ ``_lsa_runtime.levenshtein`` in place of the python-Levenshtein extension) and end-to-end
 client wall-clock latency around each ``generate`` call — and the same printed summary.  Additions:
 p50 latency, output tokens and tokens/s per model (from the engine's ``eval_count`` /
-``eval_duration``, which the reference discarded), and a JSON report.
+``eval_duration``, which the reference discarded), a JSON report, and the Markdown model-comparison report of
+``eval.report`` (the reference's hand-written ``Model_Comparision_Report.docx``).
 
     python -m llm_based_apache_spark_optimization_amd.eval.harness --engine hip --max-tokens 128
 """
@@ -43,7 +44,8 @@ def evaluate_single(generate: GenerateFn, model_name: str, options: Optional[dic
         print(f"Edit Distance: {edit_distance}")
         print(f"Latency: {latency:.4f} sec")
         print("=" * 80)
-    return {"model": model_name, "exact_match": exact_match, "edit_distance": edit_distance, "latency": latency,
+    return {"model": model_name, "generated_sql": generated_sql, "exact_match": exact_match,
+            "edit_distance": edit_distance, "latency": latency,
             "eval_count": getattr(res, "eval_count", 0), "eval_duration": getattr(res, "eval_duration", 0)}
 
 
@@ -112,6 +114,7 @@ def main(argv=None) -> int:
     ap.add_argument("--max-tokens", type=int, default=128, help="num_predict per request")
     ap.add_argument("--temperature", type=float, default=0.0)
     ap.add_argument("--json", default="", help="write the report here")
+    ap.add_argument("--report", default="", help="write the Markdown model-comparison report here (eval.report)")
     ap.add_argument("--quiet", action="store_true")
     a = ap.parse_args(argv)
     s = Settings(engine=a.engine, remote_url=a.remote_url)
@@ -127,6 +130,11 @@ def main(argv=None) -> int:
     if a.json:
         with open(a.json, "w") as f:
             json.dump(report, f, indent=1)
+    if a.report:
+        from .report import render
+
+        with open(a.report, "w") as f:
+            f.write(render(report, random_weights=a.engine != "remote"))
     return 0
 
 

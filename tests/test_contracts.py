@@ -98,3 +98,31 @@ def test_eval_harness_metrics_and_summary(capsys):
 def test_generate_response_is_ollama_shaped():
     r = GenerateResponse(model="m", response="SELECT 1", eval_count=10, eval_duration=2_000_000_000)
     assert r.response == r["response"] == "SELECT 1" and r.tokens_per_second == 5.0
+
+
+def test_eval_report_structural_checks_and_render():
+    """eval.report: the reference's hand-written comparison report (Model_Comparision_Report.docx) generated from a
+    harness run -- structural checks made mechanical (text around the statement; the statement compiled against the
+    taxi schema) and the report's sections with the published reference numbers beside the measured ones."""
+    from llm_based_apache_spark_optimization_amd.eval.report import render, structural_checks
+
+    ok = structural_checks(prompts.EVAL_EXPECTED_SQL)
+    assert ok["valid"] and not ok["extra_text"], ok
+    chatty = structural_checks("To achieve this, you can use the following query:\n```sql\nSELECT * FROM taxi;\n```")
+    assert chatty["valid"] and chatty["extra_text"] and chatty["sql"] == "SELECT * FROM taxi;"
+    bad = structural_checks("SELECT V VendortID, SUM(total_amount) FROM taxi GROUP BY VendorID;")
+    assert not bad["valid"] and "no such column" in bad["error"], bad  # the reference's llama3.2 error
+    assert structural_checks("")["error"] == "no SQL statement"
+
+    answers = {q["nl"]: q["expected_sql"] for q in prompts.EVAL_QUERIES}
+    fb = FakeBackend(sql=lambda p, s: answers.get(p, "Sure! SELECT VendorID FROM taxi;"))
+    gen = lambda **kw: fb.generate(kw["model"], kw["prompt"], kw["system"], kw["options"])  # noqa: E731
+    models = ["mistral", "duckdb-nsql"]
+    single = [evaluate_single(gen, m, verbose=False) for m in models]
+    assert single[0]["generated_sql"].startswith("Sure!")
+    multi = evaluate_multi(gen, models, verbose=False)
+    md = render({"single": single, "multi": multi, "summary": summarize(multi, 4, verbose=False),
+                 "options": {"num_predict": 8}})
+    for section in ("## 1. Setup", "## 3. Results", "### 3.2 Four-query set", "## 4. Analysis", "## 5. Recommendations"):
+        assert section in md, section
+    assert "extra text around the query" in md and "456 / 53.73 s" in md and "4 / 4" in md
