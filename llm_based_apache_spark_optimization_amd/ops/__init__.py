@@ -1173,6 +1173,11 @@ def kv8_scratch(ctx: list[int], Hkv: int, device) -> tuple:
     return ko, vo, table
 
 
+# experiment overrides of the split-KV decode plan, {(B, Hkv): (chunk_blocks, nsplit, unsplit_max)} (in-engine A/Bs,
+# scripts/ab_rr_cfg.py "plan:B:Hkv" keys); empty in production
+DECODE_PLAN_OVERRIDES: dict = {}
+
+
 def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int, int]:
     """(chunk_blocks, nsplit, unsplit_max) grid plan of split-KV decode for contexts up to max_ctx.  The
     kernel picks each sequence's own split from its length (csrc/kernels/attention.hip eff_split):
@@ -1186,6 +1191,8 @@ def decode_split_plan(B: int, Hkv: int, max_ctx: int) -> tuple[int, int, int]:
     31.8 -> 16.8 us); 8 pairs (3B at batch 1) -> up to 32 splits of >= 2 blocks (17 at 2k context).
     Contexts of <= 4 blocks run unsplit (a combine costs more than it spreads), except on grids of <= 8
     pairs, where one block per split still wins (3B B=1 ctx 200: 8.65 -> 7.32 us)."""
+    if (B, Hkv) in DECODE_PLAN_OVERRIDES:
+        return tuple(DECODE_PLAN_OVERRIDES[(B, Hkv)])
     nblk = max(1, (max_ctx + 63) // 64)
     pairs = max(1, B * Hkv)
     if nblk <= 4:  # every sequence runs unsplit (eff_split): no empty split workgroups, no combine

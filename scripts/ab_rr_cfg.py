@@ -31,9 +31,12 @@ arms = {"table": {}, **({f"ov{i}": o for i, o in enumerate(ov)} if isinstance(ov
 res = {k: [] for k in arms}
 
 
-def use(o):
+def use(o):  # "plan:B:Hkv" keys override the split-KV decode plan (chunk_blocks, nsplit, unsplit_max)
     ops.TUNING_OVERRIDES.clear()
-    ops.TUNING_OVERRIDES.update(o)
+    ops.TUNING_OVERRIDES.update({k: v for k, v in o.items() if not k.startswith("plan:")})
+    ops.DECODE_PLAN_OVERRIDES.clear()
+    ops.DECODE_PLAN_OVERRIDES.update({tuple(int(x) for x in k.split(":")[1:]): tuple(v) for k, v in o.items()
+                                      if k.startswith("plan:")})
     r.graphs.clear()
 
 
