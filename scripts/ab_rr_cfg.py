@@ -31,9 +31,19 @@ arms = {"table": {}, **({f"ov{i}": o for i, o in enumerate(ov)} if isinstance(ov
 res = {k: [] for k in arms}
 
 
-def use(o):  # "plan:B:Hkv" keys override the split-KV decode plan (chunk_blocks, nsplit, unsplit_max)
+attr0 = {}
+
+
+def use(o):  # "plan:B:Hkv" keys override the split-KV decode plan (chunk_blocks, nsplit, unsplit_max); "attr:name"
+    # keys set a ModelRunner attribute for the arm (e.g. attr:fused_norm_max_batch)
+    for k, v in attr0.items():
+        setattr(r, k, v)
+    for k, v in o.items():
+        if k.startswith("attr:"):
+            attr0.setdefault(k[5:], getattr(r, k[5:]))
+            setattr(r, k[5:], tuple(v) if isinstance(v, list) else v)
     ops.TUNING_OVERRIDES.clear()
-    ops.TUNING_OVERRIDES.update({k: v for k, v in o.items() if not k.startswith("plan:")})
+    ops.TUNING_OVERRIDES.update({k: v for k, v in o.items() if not k.startswith(("plan:", "attr:"))})
     ops.DECODE_PLAN_OVERRIDES.clear()
     ops.DECODE_PLAN_OVERRIDES.update({tuple(int(x) for x in k.split(":")[1:]): tuple(v) for k, v in o.items()
                                       if k.startswith("plan:")})
