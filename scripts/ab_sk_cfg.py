@@ -2,7 +2,7 @@
 token of one request (prefill + first-token commit + host read-back) with the table vs with each override set, arms
 interleaved in one process (cdna_hip_programming.md §5.4 rule 24), median of the rounds.  The table was built from
 standalone cold-cache sweeps; in the engine each GEMM runs after the previous layer's kernels.
-Usage: ab_sk_cfg.py <model> <prompt_len> <requests> '<json list of {key: cfg}>' [rounds]"""
+Usage: ab_sk_cfg.py <model> <prompt_len> <requests> '<json list of {key: cfg} | {"ops:NAME": value}>' [rounds]"""
 import copy
 import json
 import statistics
@@ -27,9 +27,17 @@ ops.sk_config(plen * nreq, 4096, 4096, "bf16")  # loads the table
 base = copy.deepcopy(ops._sk_tuning)
 arms = {"table": {}, **{f"ov{i}": o for i, o in enumerate(ovs)}}
 times = {k: [] for k in arms}
+ops0 = {}
 for rnd in range(rounds + 1):
     for k, o in arms.items():
-        ops._sk_tuning = {**base, **{key: {"cfg": c} for key, c in o.items()}}
+        # "ops:NAME" keys set an ops module attribute for the arm (e.g. ops:ROPE_FUSED_MIN_M)
+        for name, v in ops0.items():
+            setattr(ops, name, v)
+        for key, v in o.items():
+            if key.startswith("ops:"):
+                ops0.setdefault(key[4:], getattr(ops, key[4:]))
+                setattr(ops, key[4:], v)
+        ops._sk_tuning = {**base, **{key: {"cfg": c} for key, c in o.items() if not key.startswith("ops:")}}
         torch.cuda.synchronize()
         t = time.perf_counter()
         eng.generate(prompts, sp)
@@ -37,6 +45,8 @@ for rnd in range(rounds + 1):
         if rnd > 0:
             times[k].append(dt)
 ops._sk_tuning = base
+for name, v in ops0.items():
+    setattr(ops, name, v)
 print(json.dumps({"model": model, "prompt_len": plen, "requests": nreq, "arms": {k: arms[k] for k in arms},
                   "ttft_ms": {k: round(1000 * statistics.median(v), 3) for k, v in times.items()},
                   "min_ms": {k: round(1000 * min(v), 3) for k, v in times.items()}}), flush=True)
