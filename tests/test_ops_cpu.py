@@ -131,3 +131,35 @@ def test_linear_rr_cpu_semantics():
     y = ops.linear_rr(h, parts, h_out, w, "f32", ss_out=ss2)
     assert torch.allclose(y.sum(0), want_f32.sum(0), rtol=1e-4, atol=1e-4)
     assert abs(ss2[0].item() - ss1[0].item()) <= 16 and ss2[1] == 0
+
+
+def test_rr_config_and_experiment_overrides(monkeypatch):
+    """ops.rr_config: the measured "NxK:epi:b1:rr[:kind]" entry, else the plain kernel's pick (SiLU always split-K 1);
+    TUNING_OVERRIDES / DECODE_PLAN_OVERRIDES (the in-engine A/B hooks) take precedence while set and are empty in
+    production."""
+    assert ops.TUNING_OVERRIDES == {} and ops.DECODE_PLAN_OVERRIDES == {}
+    # the MXFP4 7B qkv entry chosen in-engine (profiles/r6/decode_b1_cfg_ab_mi355x.jsonl)
+    assert ops.rr_config(12288, 4096, "f32", "mxfp4") == (2, 2, 4, 2)
+    # no RR entry: the plain kernel's table pick, SiLU forced to one split
+    assert ops.rr_config(22016, 4096, "f32", "bf16") == ops.pick_gemm_config(1, 22016, 4096, "f32", kind="bf16")
+    assert ops.rr_config(22016, 4096, "silu", "bf16")[1] == 1
+    monkeypatch.setitem(ops.TUNING_OVERRIDES, "12288x4096:f32:b1:rr:mxfp4", {"nb": 8, "splitk": 1, "waves": 8, "div": 4})
+    assert ops.rr_config(12288, 4096, "f32", "mxfp4") == (8, 1, 8, 4)
+    base = ops.decode_split_plan(1, 8, 2240)
+    monkeypatch.setitem(ops.DECODE_PLAN_OVERRIDES, (1, 8), (4, 9, 4))
+    assert ops.decode_split_plan(1, 8, 2240) == (4, 9, 4) and ops.decode_split_plan(2, 8, 2240) != (4, 9, 4)
+    monkeypatch.delitem(ops.DECODE_PLAN_OVERRIDES, (1, 8))
+    assert ops.decode_split_plan(1, 8, 2240) == base
+
+
+def test_runner_oracle_plan_and_a8_buckets():
+    """ModelRunner.oracle_plan: a8_plan as the oracle's decode_a8 dict plus the RR-step flag; set_a8_buckets re-plans
+    (CPU runners never run W8A8, so the plan stays all-off and the RR flag follows rr_decode only for quantised
+    weights)."""
+    from llm_based_apache_spark_optimization_amd.engine import build_engine
+
+    r = build_engine("tiny-nsql", device="cpu", max_slots=2, max_model_len=128).runner
+    plan = r.oracle_plan(1)
+    assert set(plan) == {"qkv", "gate_up", "o", "down", "rr"} and not any(plan.values())
+    r.set_a8_buckets(0, 0, 16)
+    assert r.a8_plan(1) == (False, False, False, False) and not r.rr_a8 and r.graphs == {}
