@@ -173,6 +173,31 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   unsigned long long* const stp = g_sk_stamps;
   int st_seg = 0, st_kt = 0;
 #endif
+#ifdef LSA_SK_PHASE
+  // (diagnostic LSA_SK_PHASE build, scripts/sk_phase.py) per-wave s_memtime cycles of the one-phase K-tile's parts,
+  // summed over the wave's K-tiles: [0] fragment reads + DMA issue + counted waits, [1] barrier 1, [2] MFMA issue,
+  // [3] barrier 2, [4] K-tiles -> g_sk_stamps[(block * 8 + wave) * 8 + k]
+  // sub-stamps of [0]: [5] fragment reads issued and returned (the stamp waits lgkmcnt), [6] LDS-DMA issue; the
+  // counted waits are the rest of [0]
+  unsigned long long ph_acc[7] = {0, 0, 0, 0, 0, 0, 0}, ph_t = 0, ph_t0 = 0;
+#define LSA_SK_PH(K)                                                             \
+  do {                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    const unsigned long long ph_now = __builtin_amdgcn_s_memtime();              \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    if ((K) >= 5) {                                                              \
+      ph_acc[(K)] += ph_now - ph_t0;                                             \
+      ph_t0 = ph_now;                                                            \
+    } else {                                                                     \
+      if ((K) > 0) ph_acc[(K) - 1] += ph_now - ph_t;                             \
+      if ((K) == 4) ++ph_acc[4];                                                 \
+      ph_t = ph_now;                                                             \
+      ph_t0 = ph_now;                                                            \
+    }                                                                            \
+  } while (0)
+#else
+#define LSA_SK_PH(K) (void)0
+#endif
   LSA_SK_STAMP(0, __builtin_amdgcn_s_memrealtime());
   constexpr int MI = C::MI, NQ0 = C::NQ0, NQ1 = C::NQ1;
   constexpr bool BIG = 2 * MI * WN >= 24;  // >= 96 accumulator VGPRs (256 x 256, 4-wave 128 x 192): smaller epilogue load batches
@@ -388,18 +413,25 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   // t - 1 completed (lgkmcnt) before a barrier that precedes the restage of its buffer.
 #define LSA_KTILE4(B, BS, t)                                                      \
   do {                                                                            \
+    LSA_SK_PH(0);                                                                 \
     read_all(B{});                                                                \
+    LSA_SK_PH(5);                                                                 \
     stage(I0{}, BS{}, (t) + 3);                                                   \
     stage(I1{}, BS{}, (t) + 3);                                                   \
     stage(I2{}, BS{}, (t) + 3);                                                   \
     stage(I3{}, BS{}, (t) + 3);                                                   \
+    LSA_SK_PH(6);                                                                 \
     LSA_WAITV(2 * C::WAIT3);                                                      \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                            \
+    LSA_SK_PH(1);                                                                 \
     __builtin_amdgcn_s_barrier();                                                 \
+    LSA_SK_PH(2);                                                                 \
     __builtin_amdgcn_sched_barrier(0);                                            \
     mma_all();                                                                    \
     __builtin_amdgcn_sched_barrier(0);                                            \
+    LSA_SK_PH(3);                                                                 \
     __builtin_amdgcn_s_barrier();                                                 \
+    LSA_SK_PH(4);                                                                 \
   } while (0)
     if constexpr (NBUF == 4) {
       stage(I0{}, I0{}, 0);
@@ -770,6 +802,13 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   LSA_SK_STAMP(3, __builtin_amdgcn_s_memrealtime());
   LSA_SK_STAMP(4, (unsigned long long)st_kt);
   LSA_SK_STAMP(5, (unsigned long long)st_seg);
+#ifdef LSA_SK_PHASE
+  if (g_sk_stamps && lane == 0) {
+    unsigned long long* o = g_sk_stamps + ((size_t)blockIdx.x * 8 + w) * 8;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) o[k] = ph_acc[k];
+  }
+#endif
 }
 
 template <int BM, int WN, int EPI, int NBUF, int KS, int NW>
