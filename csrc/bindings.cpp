@@ -51,7 +51,7 @@ int lsa_kv8_dequant(const void* kc, const void* vc, const float* ks, const float
                     int max_blocks, const int* ctx_lens, int nseq, int Hkv, int mb, void* ko, void* vo, hipStream_t s);
 int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                      const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
-                     void* out, hipStream_t s);
+                     void* out, int xf_mt, hipStream_t s);
 int lsa_argmax_commit(const float* logits, int B, int V, unsigned long long* part, int* out_tokens, int max_new,
                       int* gen_len, int* input_ids, int* positions, int* finished, const int* eos, int neos,
                       const int* limit, const int* eos_on, hipStream_t s);
@@ -73,15 +73,15 @@ void lsa_gemm_sk_one_phase(int on);
 int lsa_gemm_sk_rope(const void* X, int ldx, int M, int K, const void* Wf, int N, float* ws, int* tickets, int ncu,
                      int min_share, int cfg, const int* pos, const int* tok_seq, const int* block_tables,
                      int max_blocks, const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int H,
-                     int Hkv, int* grid_out, int* cfg_out, hipStream_t stream);
+                     int Hkv, int xf, int* grid_out, int* cfg_out, hipStream_t stream);
 int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
-                int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, hipStream_t stream);
+                int* tickets, int ncu, int min_share, int cfg, int xf, int* grid_out, int* cfg_out, hipStream_t stream);
 int lsa_silu_parts(const float* parts, int nparts, long part_stride, int M, int F, void* out, hipStream_t s);
 int lsa_silu_bf16(const void* y, int M, int F, void* out, hipStream_t s);
 void lsa_fp8_gemm_knobs(int waves, int depth);
 int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                        const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv, float scale,
-                       void* out, int ng, hipStream_t s);
+                       void* out, int ng, int xf_mt, hipStream_t s);
 int lsa_quant_rows_fp8(const void* x, int ldx, int M, int K, void* x8, int ld8, float* sx, hipStream_t s);
 int lsa_fp8_gemm_t256(const void* X8, int ldx, const float* sx, int M, int K, const void* Wq, const float* sw, int N,
                       void* out, int epi, int splitk, hipStream_t stream);
@@ -429,16 +429,35 @@ void quant_xf8(const at::Tensor& x, int64_t mt, at::Tensor& x8, at::Tensor& sx) 
 // large-M (prefill) linear layer on the stream-K 256x256 tile kernel (kernels/gemm_tile256.hip).  epi: 0 bf16 [M][N],
 // 1 f32 [M][N], 2 SiLU(gate) * up bf16 [M][N / 2], 3 h f32 [M][N] += x @ W^T.  ws / tickets: the per-stream
 // workspace (ops._sk_workspace).  cfg: -1 = the kernel's cost model, else a tile configuration index (+ 8: whole
-// tiles only; + 16 + 32 * mode: that epilogue mode for this call).  Returns grid * 16 + the configuration used.
-int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, at::Tensor& ws,
-                at::Tensor& tickets, int64_t ncu, int64_t min_share, int64_t cfg) {
+// tiles only; + 16 + 32 * mode: that epilogue mode for this call).  xf: + 1 x is a flat buffer in the fragment-major
+// layout (ops.to_xfrag) of ``rows`` rows, + 2 the SiLU output is written in it.  Returns grid * 16 + the configuration
+// used.
+// rows / K of a stream-K GEMM's X: the [M, K] row-major matrix, or (xf & 1) a flat fragment-major buffer of rows rows
+static std::pair<int64_t, int64_t> sk_x_shape(const at::Tensor& x, const at::Tensor& wf, int64_t N, int64_t xf,
+                                              int64_t rows) {
   need(x, at::kBFloat16, "x");
   need(wf, at::kBFloat16, "wf");
+  TORCH_CHECK(N > 0 && wf.numel() % N == 0, "gemm_sk: weight numel not a multiple of N");
+  if (xf & 1) {
+    const int64_t K = wf.numel() / N;
+    TORCH_CHECK(rows > 0 && x.is_contiguous() && x.numel() >= (rows + 15) / 16 * 16 * K,
+                "gemm_sk: fragment-major x needs rows and ceil(rows / 16) * 16 * K elements");
+    return {rows, K};
+  }
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
+  TORCH_CHECK(wf.numel() == N * x.size(1), "weight numel mismatch");
+  return {x.size(0), x.size(1)};
+}
+
+int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor& out, int64_t epi, at::Tensor& ws,
+                at::Tensor& tickets, int64_t ncu, int64_t min_share, int64_t cfg, int64_t xf, int64_t rows) {
   need(ws, at::kFloat, "ws");
   need(tickets, at::kInt, "tickets");
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
-  const int M = x.size(0), K = x.size(1);
-  TORCH_CHECK(M > 0 && N > 0 && wf.numel() == N * K, "weight numel mismatch");
+  TORCH_CHECK(xf >= 0 && xf <= 3 && (!(xf & 2) || (epi == 2 && N % 64 == 0)),
+              "gemm_sk: xf (+2 only with the SiLU epilogue and N / 2 % 32 == 0)");
+  const auto mk = sk_x_shape(x, wf, N, xf, rows);
+  const int M = (int)mk.first, K = (int)mk.second;
+  TORCH_CHECK(M > 0, "gemm_sk: no rows");
   TORCH_CHECK(ncu >= 8 && ncu <= 1024, "gemm_sk: ncu out of range");
   TORCH_CHECK(ws.numel() * 4 >= lsa_gemm_sk_ws_bytes((int)ncu) && tickets.numel() >= lsa_gemm_sk_tickets((int)ncu),
               "gemm_sk: workspace too small");
@@ -448,12 +467,14 @@ int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor
     TORCH_CHECK(out.numel() >= (int64_t)M * N, "f32 out too small");
   } else {
     need(out, at::kBFloat16, "out");
-    TORCH_CHECK(out.numel() >= (int64_t)M * (epi == 2 ? N / 2 : N), "bf16 out too small");
+    TORCH_CHECK(out.numel() >= (int64_t)((xf & 2) ? (M + 15) / 16 * 16 : M) * (epi == 2 ? N / 2 : N),
+                "bf16 out too small");
   }
   TORCH_CHECK(cfg >= -1 && cfg < 64, "gemm_sk: cfg");
   int grid = 0, used = 0;
-  check(lsa_gemm_sk(x.data_ptr(), x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), (int)epi, ws.data_ptr<float>(),
-                    tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, &grid, &used, cur_stream()),
+  check(lsa_gemm_sk(x.data_ptr(), (xf & 1) ? 0 : (int)x.stride(0), M, K, wf.data_ptr(), N, out.data_ptr(), (int)epi,
+                    ws.data_ptr<float>(), tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, (int)xf, &grid,
+                    &used, cur_stream()),
         "gemm_sk");
   return (int64_t)grid * 16 + used;
 }
@@ -464,9 +485,8 @@ int64_t gemm_sk(const at::Tensor& x, const at::Tensor& wf, int64_t N, at::Tensor
 int64_t gemm_sk_rope(const at::Tensor& x, const at::Tensor& wf, at::Tensor& ws, at::Tensor& tickets, int64_t ncu,
                      int64_t min_share, int64_t cfg, const at::Tensor& pos, const c10::optional<at::Tensor>& tok_seq,
                      const at::Tensor& block_tables, const at::Tensor& cos_t, const at::Tensor& sin_t,
-                     at::Tensor& q_out, at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv) {
-  need(x, at::kBFloat16, "x");
-  need(wf, at::kBFloat16, "wf");
+                     at::Tensor& q_out, at::Tensor& kc, at::Tensor& vc, int64_t H, int64_t Hkv, int64_t xf,
+                     int64_t rows) {
   need(ws, at::kFloat, "ws");
   need(tickets, at::kInt, "tickets");
   need(pos, at::kInt, "pos");
@@ -476,9 +496,11 @@ int64_t gemm_sk_rope(const at::Tensor& x, const at::Tensor& wf, at::Tensor& ws, 
   need(q_out, at::kBFloat16, "q_out");
   need(kc, at::kBFloat16, "kc");
   need(vc, at::kBFloat16, "vc");
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be a row-major matrix");
-  const int64_t M = x.size(0), K = x.size(1), N = (H + 2 * Hkv) * 128;
-  TORCH_CHECK(H > 0 && Hkv > 0 && wf.numel() == N * K, "gemm_sk_rope: weight numel != (H + 2 Hkv) * 128 * K");
+  TORCH_CHECK(xf == 0 || xf == 1, "gemm_sk_rope: xf 0 | 1");
+  const int64_t N = (H + 2 * Hkv) * 128;
+  TORCH_CHECK(H > 0 && Hkv > 0, "gemm_sk_rope: heads");
+  const auto mk = sk_x_shape(x, wf, N, xf, rows);
+  const int64_t M = mk.first, K = mk.second;
   TORCH_CHECK(pos.numel() >= M && q_out.is_contiguous() && q_out.numel() >= M * H * 128, "gemm_sk_rope: q_out / pos");
   TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(2) == 64 && kc.size(3) == 128 && kc.sizes() == vc.sizes() &&
                   kc.is_contiguous() && vc.is_contiguous(), "gemm_sk_rope: cache [blocks, Hkv, 64, 128]");
@@ -491,11 +513,11 @@ int64_t gemm_sk_rope(const at::Tensor& x, const at::Tensor& wf, at::Tensor& ws, 
   TORCH_CHECK(ncu >= 8 && ncu <= 1024 && ws.numel() * 4 >= lsa_gemm_sk_ws_bytes((int)ncu) &&
                   tickets.numel() >= lsa_gemm_sk_tickets((int)ncu), "gemm_sk_rope: workspace too small");
   int grid = 0, used = 0;
-  check(lsa_gemm_sk_rope(x.data_ptr(), x.stride(0), (int)M, (int)K, wf.data_ptr(), (int)N, ws.data_ptr<float>(),
+  check(lsa_gemm_sk_rope(x.data_ptr(), xf ? 0 : (int)x.stride(0), (int)M, (int)K, wf.data_ptr(), (int)N, ws.data_ptr<float>(),
                          tickets.data_ptr<int>(), (int)ncu, (int)min_share, (int)cfg, pos.data_ptr<int>(),
                          ptr<int>(tok_seq), block_tables.data_ptr<int>(), (int)block_tables.size(1),
                          cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), q_out.data_ptr(), kc.data_ptr(),
-                         vc.data_ptr(), (int)H, (int)Hkv, &grid, &used, cur_stream()),
+                         vc.data_ptr(), (int)H, (int)Hkv, (int)xf, &grid, &used, cur_stream()),
         "gemm_sk_rope");
   return (int64_t)grid * 16 + used;
 }
@@ -781,14 +803,19 @@ void kv8_dequant(const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& k
 
 void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& vc, const at::Tensor& block_tables,
                   const at::Tensor& cu_q, const at::Tensor& ctx_lens, const at::Tensor& work, int64_t H, int64_t Hkv,
-                  double scale, at::Tensor& out, int64_t rows32) {
+                  double scale, at::Tensor& out, int64_t rows32, int64_t xf_mt) {
   need(q, at::kBFloat16, "q");
   need(work, at::kInt, "work");
   need(cu_q, at::kInt, "cu_q");
   need(ctx_lens, at::kInt, "ctx_lens");
   need(block_tables, at::kInt, "block_tables");
   need(out, at::kBFloat16, "out");
-  TORCH_CHECK(q.dim() == 3 && q.size(1) == H && q.size(2) == 128 && out.sizes() == q.sizes(), "q / out [T, H, 128]");
+  TORCH_CHECK(q.dim() == 3 && q.size(1) == H && q.size(2) == 128, "q [T, H, 128]");
+  // out: [T, H, 128] row-major, or (xf_mt > 0) a flat buffer in the fragment-major layout of xf_mt 16-row tiles (the
+  // o projection's stream-K input)
+  TORCH_CHECK(xf_mt >= 0 && (xf_mt ? (out.is_contiguous() && xf_mt * 16 >= q.size(0) && out.numel() >= xf_mt * 16 * H * 128)
+                                   : out.sizes() == q.sizes()),
+              "attn_prefill: out [T, H, 128], or xf_mt >= T / 16 row tiles of fragment-major rows");
   TORCH_CHECK(cu_q.numel() == ctx_lens.numel() + 1 && block_tables.size(0) >= ctx_lens.numel(),
               "cu_q [nseq + 1], ctx_lens [nseq], block_tables [>= nseq, max_blocks]");
   if (rows32) {  // 32 x 32 MFMA kernel, 128 query rows per work item (kernels/attention_prefill32.hip)
@@ -798,13 +825,14 @@ void attn_prefill(const at::Tensor& q, const at::Tensor& kc, const at::Tensor& v
                 "attn_prefill32 work must be [n, 4 per group] int32");
     check(lsa_attn_prefill32(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                              block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
-                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 4), cur_stream()),
+                             work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)(work.size(1) / 4), (int)xf_mt,
+                             cur_stream()),
           "attn_prefill32");
     return;
   }
   check(lsa_attn_prefill(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), block_tables.data_ptr<int>(),
                          block_tables.size(1), cu_q.data_ptr<int>(), ctx_lens.data_ptr<int>(), work.data_ptr<int>(),
-                         work.size(0), H, Hkv, (float)scale, out.data_ptr(), cur_stream()),
+                         work.size(0), H, Hkv, (float)scale, out.data_ptr(), (int)xf_mt, cur_stream()),
         "attn_prefill");
 }
 
@@ -995,8 +1023,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi"), py::arg("nb"), py::arg("splitk"), py::arg("waves") = 4, py::arg("div") = 4,
         py::arg("rowss") = py::none(), py::arg("eps") = 1e-5, py::arg("h") = py::none(), py::arg("xout") = py::none(), py::arg("xmt") = 0, py::arg("ss_out") = py::none(), py::arg("tickets") = py::none());
   m.def("gemm_sk", &gemm_sk, py::arg("x"), py::arg("wf"), py::arg("N"), py::arg("out"), py::arg("epi"), py::arg("ws"),
-        py::arg("tickets"), py::arg("ncu"), py::arg("min_share") = 0, py::arg("cfg") = -1);
-  m.def("gemm_sk_rope", &gemm_sk_rope);
+        py::arg("tickets"), py::arg("ncu"), py::arg("min_share") = 0, py::arg("cfg") = -1, py::arg("xf") = 0,
+        py::arg("rows") = 0);
+  m.def("gemm_sk_rope", &gemm_sk_rope, py::arg("x"), py::arg("wf"), py::arg("ws"), py::arg("tickets"), py::arg("ncu"),
+        py::arg("min_share"), py::arg("cfg"), py::arg("pos"), py::arg("tok_seq"), py::arg("block_tables"),
+        py::arg("cos_t"), py::arg("sin_t"), py::arg("q_out"), py::arg("kc"), py::arg("vc"), py::arg("H"), py::arg("Hkv"),
+        py::arg("xf") = 0, py::arg("rows") = 0);
   m.def("gemm_sk_epilogue", [](int64_t mode) { lsa_gemm_sk_epilogue((int)mode); });
   m.def("gemm_sk_nbuf", [](int64_t n) { lsa_gemm_sk_nbuf((int)n); });
   m.def("gemm_sk_one_phase", [](int64_t on) { lsa_gemm_sk_one_phase((int)on); });
@@ -1054,7 +1086,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ss_out") = py::none(), py::arg("eps") = 1e-5);
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("block_tables"),
         py::arg("cu_q"), py::arg("ctx_lens"), py::arg("work"), py::arg("H"), py::arg("Hkv"), py::arg("scale"),
-        py::arg("out"), py::arg("rows32") = 0);
+        py::arg("out"), py::arg("rows32") = 0, py::arg("xf_mt") = 0);
   m.def("argmax_commit", &argmax_commit);
   m.def("sample_commit", &sample_commit);
   m.def("fp8_dequant", &fp8_dequant);

@@ -695,7 +695,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
                                                            const int* __restrict__ block_tables, int max_blocks,
                                                            const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
                                                            const int* __restrict__ work, int H, int Hkv,
-                                                           float scale_log2, uint16_t* __restrict__ out) {
+                                                           float scale_log2, uint16_t* __restrict__ out, int xf_mt) {
   constexpr int D = 128;
   constexpr int QW = 16 * QG;   // query rows per wave
   constexpr int QB = 4 * QW;    // query rows per workgroup
@@ -853,7 +853,8 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const uint16_t* __res
       if (qr < qlen) {
         uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D;
 #pragma unroll
-        for (int dt = 0; dt < 8; ++dt) orow[16 * dt + r] = f2bf(o[gi][dt][i] * inv);
+        for (int dt = 0; dt < 8; ++dt)  // row-major, or (xf_mt) the o projection's fragment-major input
+          (xf_mt ? out[xf_off(q0 + qr, h * D + 16 * dt + r, xf_mt)] : orow[16 * dt + r]) = f2bf(o[gi][dt][i] * inv);
       }
     }
   }
@@ -863,13 +864,13 @@ extern "C" int lsa_prefill_qblock() { return 64 * LSA_PREFILL_QG; }
 
 extern "C" int lsa_attn_prefill(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                 const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv,
-                                float scale, void* out, hipStream_t s) {
+                                float scale, void* out, int xf_mt, hipStream_t s) {
   if (nwork <= 0) return 0;
   if (H % Hkv) return -1;
   dim3 grid(nwork, H);
   hipLaunchKernelGGL(attn_prefill_kernel<LSA_PREFILL_QG>, grid, dim3(256), 0, s, reinterpret_cast<const uint16_t*>(q),
                      reinterpret_cast<const uint16_t*>(kc), reinterpret_cast<const uint16_t*>(vc), block_tables,
                      max_blocks, cu_q, ctx_lens, work, H, Hkv, scale * 1.4426950408889634f,
-                     reinterpret_cast<uint16_t*>(out));
+                     reinterpret_cast<uint16_t*>(out), xf_mt);
   return (int)hipGetLastError();
 }

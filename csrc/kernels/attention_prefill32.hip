@@ -114,7 +114,8 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
                                                                      const int* __restrict__ block_tables, int max_blocks,
                                                                      const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
                                                                      const int* __restrict__ work, int H, int Hkv,
-                                                                     float scale_log2, uint16_t* __restrict__ out) {
+                                                                     float scale_log2, uint16_t* __restrict__ out,
+                                                                     int xf_mt) {
   constexpr int WI = 4;  // ints per work item
   constexpr int D = 128;
   unsigned long long sg[6] = {0, 0, 0, 0, 0, 0}, st_t0 = 0, st_prev = 0;
@@ -379,6 +380,7 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
   const int qr = qs + w * 32 + r32;
   if (active && qr < qlen) {
     const float inv = lrow > 0.f ? 1.f / lrow : 0.f;
+    // row-major [T][H][128], or (xf_mt) the fragment-major layout the o projection's stream-K GEMM stages whole
     uint16_t* orow = out + ((size_t)(q0 + qr) * H + h) * D + 4 * hh;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
@@ -387,7 +389,8 @@ __global__ __launch_bounds__(256 * NG, 2) void attn_prefill32_kernel(const uint1
         uint2 pk;
         pk.x = pack2bf(o[db][4 * gq + 0] * inv, o[db][4 * gq + 1] * inv);
         pk.y = pack2bf(o[db][4 * gq + 2] * inv, o[db][4 * gq + 3] * inv);
-        *reinterpret_cast<uint2*>(orow + 32 * db + 8 * gq) = pk;
+        const int dd = 32 * db + 8 * gq + 4 * hh;
+        *reinterpret_cast<uint2*>(xf_mt ? out + xf_off(q0 + qr, h * D + dd, xf_mt) : orow + 32 * db + 8 * gq) = pk;
       }
   }
 }
@@ -404,7 +407,7 @@ extern "C" int lsa_p32_set_stamps(void* p) {
 // work: NG (seq, q_start, t0, t1) items per workgroup (seq < 0: that group idles), nwork workgroups
 extern "C" int lsa_attn_prefill32(const void* q, const void* kc, const void* vc, const int* block_tables, int max_blocks,
                                   const int* cu_q, const int* ctx_lens, const int* work, int nwork, int H, int Hkv,
-                                  float scale, void* out, int ng, hipStream_t s) {
+                                  float scale, void* out, int ng, int xf_mt, hipStream_t s) {
   if (nwork <= 0) return 0;
   if (H % Hkv) return -1;
   if (ng != 1 && ng != 2) return -2;
@@ -414,7 +417,7 @@ extern "C" int lsa_attn_prefill32(const void* q, const void* kc, const void* vc,
   hipLaunchKernelGGL((attn_prefill32_kernel<NGV, STV>), grid, dim3(256 * NGV), 0, s,                             \
                      reinterpret_cast<const uint16_t*>(q), reinterpret_cast<const uint16_t*>(kc),                 \
                      reinterpret_cast<const uint16_t*>(vc), block_tables, max_blocks, cu_q, ctx_lens, work, H, Hkv, \
-                     sl2, reinterpret_cast<uint16_t*>(out))
+                     sl2, reinterpret_cast<uint16_t*>(out), xf_mt)
 #define LSA_P32_NG(STV)                  \
   do {                                   \
     if (ng == 2) LSA_P32_LAUNCH(2, STV); \

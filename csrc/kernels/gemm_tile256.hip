@@ -92,6 +92,7 @@ struct SkPlan {
   int sk_tiles;         // tiles [0, sk_tiles) are stream-K, the rest data-parallel
   int sk_iters;         // sk_tiles * T (host-checked: sk_iters * (grid + 1) < 2^31, so 32-bit index math)
   int epl;              // epilogue: 0 = straight from the accumulators, 1 = through an LDS image (full-row stores)
+  int xf;               // fragment-major operands (common.h xf_off, ceil(M / 16) row tiles): +1 X, +2 the SiLU output
 };
 
 // EPI_ROPE (prefill qkv projection, bf16 KV cache): the GEMM's output row t is token t's q | k | v; the epilogue
@@ -221,7 +222,14 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
   // (one VGPR each), the K-tile's offset rides in the SGPR soffset -- no VALU per load in the K loop
   // (byte-exact ranges: an odd K's missing last k-step is staged from past the end, which the buffer unit reads as
   // zeros, so the MFMAs of that k-step add nothing and the K loop has no odd-tail branch)
-  const int xbytes = ((M - 1) * ldx + KB * 32) * 2, wbytes = NBtot * KB * 1024;
+  // fragment-major X (pl.xf & 1, the prefill activation layout): each staged fragment is one contiguous 1 KiB piece
+  // (16 rows x 32 k) at (k-step * xmt + row tile) KiB, where the row-major gather reads 16 rows x 64 B, half of each
+  // of 16 cache lines -- the ablation with contiguous pieces ran the 128-row tiles' K-tiles 17 % faster
+  // (profiles/r6/prefill_gemm_stamps.txt); the K-tile step is then KS * xmt KiB
+  const bool xfx = pl.xf & 1;
+  const int xmt = (M + 15) >> 4;
+  const int xstep = xfx ? KS * xmt * 1024 : KS * 64;
+  const int xbytes = xfx ? KB * xmt * 1024 : ((M - 1) * ldx + KB * 32) * 2, wbytes = NBtot * KB * 1024;
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)Wf, 0, wbytes, 0x00020000);
   int vx[2][C::GX], vw0[C::GW0], vw1[C::GW1];
@@ -244,8 +252,13 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
 #pragma unroll
       for (int e = 0; e < C::GX; ++e) {
         const int f = C::GX * w + e, wi = f / KS, ks = f % KS, wr_ = wi / MI, i = wi % MI;
-        const int row = min(mbase + wr_ * (BM / 2) + h * (BM / 4) + i * 16 + r16, M - 1);
-        vx[h][e] = (row * ldx + c16) * 2 + ks * 64;
+        const int row0 = mbase + wr_ * (BM / 2) + h * (BM / 4) + i * 16;
+        if (xfx) {
+          vx[h][e] = (ks * xmt + min(row0 >> 4, xmt - 1)) * 1024 + lane * 16;
+        } else {
+          const int row = min(row0 + r16, M - 1);
+          vx[h][e] = (row * ldx + c16) * 2 + ks * 64;
+        }
       }
 #pragma unroll
     for (int e = 0; e < C::GW0; ++e) {
@@ -271,7 +284,7 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
       const bool oob = tc * KS + f % KS >= KB;  // a k-step past K (the last K-tile's tail): staged as zeros
       void* dst = &lds[(B * C::BUFF + C::HOFF[H] + f) * 64];
       if constexpr (H < 2)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, vx[H][e], oob ? xbytes : tc * (KS * 64), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, vx[H][e], oob ? xbytes : tc * xstep, 0, 0);
       else if constexpr (H == 2)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)dst, 16, vw0[e], oob ? wbytes : tc * (KS * 1024), 0, 0);
       else
@@ -563,7 +576,10 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
           uint2 p;
           p.x = pack2bf(silu(acc[i][j][0]) * acc[i][j + 1][0], silu(acc[i][j][1]) * acc[i][j + 1][1]);
           p.y = pack2bf(silu(acc[i][j][2]) * acc[i][j + 1][2], silu(acc[i][j][3]) * acc[i][j + 1][3]);
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + (size_t)m * ldo + (nb >> 1) * 16 + 4 * g) = p;
+          const int c = (nb >> 1) * 16 + 4 * g;
+          // fragment-major (pl.xf & 2): a wave-instruction's 16 rows x 16 columns fill 512 contiguous bytes
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) +
+                                    ((pl.xf & 2) ? xf_off(m, c, (M + 15) >> 4) : (size_t)m * ldo + c)) = p;
         }
       } else {
 #pragma unroll
@@ -725,7 +741,8 @@ __device__ __forceinline__ void gemm_sk_body(const uint16_t* __restrict__ X, int
     }
   };
   auto finish_tile = [&]() {
-    if (EPI == EPI_ROPE || pl.epl) store_tile_lds();
+    // (a fragment-major SiLU output goes straight from the accumulators: their stores are already whole lines)
+    if (EPI == EPI_ROPE || (pl.epl && !(EPI == EPI_SILU && (pl.xf & 2)))) store_tile_lds();
     else if constexpr (EPI != EPI_ROPE) store_tile();
   };
 
@@ -908,13 +925,14 @@ extern "C" void lsa_gemm_sk_one_phase(int on) { g_sk_one = on ? 1 : 0; }
 
 template <int BM, int WN, int KS = 2, int NW = 8>
 static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const uint4* w, int NBtot, void* out, int ldo,
-                     float* ws, int* tickets, int ncu, int min_share, bool sk, int epl, int* grid_out,
+                     float* ws, int* tickets, int ncu, int min_share, bool sk, int epl, int xf, int* grid_out,
                      const RopeEpi& re, hipStream_t stream) {
   using C = TileCfg<BM, WN, KS, NW>;
   const int P = ncu * (NW == 4 ? 2 : 1);  // persistent workgroups: one per CU, or two of the 4-wave kind
   int grid = 0;
   SkPlan pl = sk_plan(M, KB, NBtot, BM, C::NBT, KS, P, min_share, sk, &grid);
   pl.epl = epl;
+  pl.xf = xf;
   if (pl.sk_tiles > 2 * P || grid > P || (long long)pl.sk_tiles * pl.T * (grid + 1) >= (1LL << 31)) return -3;
   if (grid_out) *grid_out = grid;
   switch (epi) {
@@ -965,11 +983,16 @@ static int sk_launch(int epi, const uint16_t* x, int ldx, int M, int KB, const u
 // out: bf16 [M][N] (EPI_BF16), f32 [M][N] (EPI_F32), bf16 [M][N / 2] (EPI_SILU), f32 h [M][N] accumulated (EPI_RES).
 // cfg: -1 = the cost model's pick, else an index into kSkCfgs (+ 8: whole tiles only, no stream-K remainder), + 16:
 // the epilogue mode given in bit 5 (+ 32 = through LDS) instead of lsa_gemm_sk_epilogue's; *cfg_out = the
-// configuration used (bits 0-3).
+// configuration used (bits 0-3).  xf: +1 X in the fragment-major layout of ceil(M / 16) row tiles (common.h xf_off;
+// ldx unused), +2 the EPI_SILU output in it -- the prefill activations the next GEMM stages as whole 1 KiB pieces.
 static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
-                        int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out, const RopeEpi& re,
-                        hipStream_t stream) {
+                        int* tickets, int ncu, int min_share, int cfg, int xf, int* grid_out, int* cfg_out,
+                        const RopeEpi& re, hipStream_t stream) {
   if (K % 32 != 0 || N % 16 != 0 || M <= 0 || ncu < 8 || ncu > 1024 || !ws || !tickets) return -1;
+  // fragment-major operands: X (+1; its whole buffer, K / 32 x ceil(M / 16) KiB, under the 2 GiB buffer range),
+  // the SiLU output (+2; whole 32-column k-steps: N / 2 % 32 == 0)
+  if (xf < 0 || xf > 3 || ((xf & 2) && (epi != EPI_SILU || N % 64)) || ((xf & 1) && (long long)(K / 32) * ((M + 15) / 16) >= (1 << 21)))
+    return -7;
   if (epi == EPI_SILU && N % 32 != 0) return -2;
   const bool even_wn = epi == EPI_SILU || epi == EPI_ROPE;  // tile configurations with an even n-block count/wave
   const int KB = K / 32, NBtot = N / 16;
@@ -1006,26 +1029,26 @@ static int gemm_sk_impl(const void* X, int ldx, int M, int K, const void* Wf, in
   const int ldo = epi == EPI_SILU ? N / 2 : N;
   switch (cfg) {
 #define LSA_SKC(I, BMV, WNV) \
-  case I: return sk_launch<BMV, WNV>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, stream);
+  case I: return sk_launch<BMV, WNV>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, xf, grid_out, re, stream);
     LSA_SKC(0, 256, 4)
     LSA_SKC(1, 256, 3)
     LSA_SKC(2, 256, 2)
     LSA_SKC(3, 128, 4)
     LSA_SKC(4, 128, 3)
     LSA_SKC(5, 128, 2)
-    case 6: return sk_launch<128, 6, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, stream);
-    case 7: return sk_launch<128, 4, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, grid_out, re, stream);
+    case 6: return sk_launch<128, 6, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, xf, grid_out, re, stream);
+    case 7: return sk_launch<128, 4, 2, 4>(epi, x, ldx, M, KB, w, NBtot, out, ldo, ws, tickets, ncu, min_share, sk, epl, xf, grid_out, re, stream);
 #undef LSA_SKC
     default: return -5;
   }
 }
 
 extern "C" int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf, int N, void* out, int epi, float* ws,
-                           int* tickets, int ncu, int min_share, int cfg, int* grid_out, int* cfg_out,
+                           int* tickets, int ncu, int min_share, int cfg, int xf, int* grid_out, int* cfg_out,
                            hipStream_t stream) {
   if (epi < 0 || epi > 3) return -4;
-  return gemm_sk_impl(X, ldx, M, K, Wf, N, out, epi, ws, tickets, ncu, min_share, cfg, grid_out, cfg_out, RopeEpi{},
-                      stream);
+  return gemm_sk_impl(X, ldx, M, K, Wf, N, out, epi, ws, tickets, ncu, min_share, cfg, xf, grid_out, cfg_out,
+                      RopeEpi{}, stream);
 }
 
 // the prefill qkv projection with RoPE + the paged bf16 KV-cache append fused into its epilogue (EPI_ROPE above);
@@ -1033,13 +1056,13 @@ extern "C" int lsa_gemm_sk(const void* X, int ldx, int M, int K, const void* Wf,
 extern "C" int lsa_gemm_sk_rope(const void* X, int ldx, int M, int K, const void* Wf, int N, float* ws, int* tickets,
                                 int ncu, int min_share, int cfg, const int* pos, const int* tok_seq,
                                 const int* block_tables, int max_blocks, const float* cos_t, const float* sin_t,
-                                void* q_out, void* kc, void* vc, int H, int Hkv, int* grid_out, int* cfg_out,
+                                void* q_out, void* kc, void* vc, int H, int Hkv, int xf, int* grid_out, int* cfg_out,
                                 hipStream_t stream) {
   if (H <= 0 || Hkv <= 0 || N != (H + 2 * Hkv) * 128 || !pos || !block_tables || !cos_t || !sin_t || !q_out || !kc ||
       !vc)
     return -6;
   const RopeEpi re{pos, tok_seq, block_tables, max_blocks, cos_t, sin_t, reinterpret_cast<uint16_t*>(q_out),
                    reinterpret_cast<uint16_t*>(kc), reinterpret_cast<uint16_t*>(vc), H, Hkv};
-  return gemm_sk_impl(X, ldx, M, K, Wf, N, nullptr, EPI_ROPE, ws, tickets, ncu, min_share, cfg, grid_out, cfg_out, re,
-                      stream);
+  return gemm_sk_impl(X, ldx, M, K, Wf, N, nullptr, EPI_ROPE, ws, tickets, ncu, min_share, cfg, xf & 1, grid_out,
+                      cfg_out, re, stream);
 }

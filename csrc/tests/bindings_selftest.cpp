@@ -120,13 +120,20 @@ int main() {
     auto o2 = T({300, 64}, F32), sw = T({64}, F32);
     // stream-K prefill GEMM: workspace of lsa_gemm_sk_ws_bytes(ncu) / tickets(ncu)
     auto wsk = T({2 * 8 * 65536}, F32), tks = T({32}, I32), ob = T({300, 64}, BF), wsb = T({64 * 128}, BF);
-    expect_ok("gemm_sk", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1); });
+    expect_ok("gemm_sk", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, 0, 0); });
     auto wsk_small = T({65536}, F32);
-    expect_reject("gemm_sk workspace", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk_small, tks, 8, 0, -1); });
-    expect_reject("gemm_sk residual dtype", [&] { gemm_sk(x, wsb, 64, ob, 3, wsk, tks, 8, 0, -1); });
+    expect_reject("gemm_sk workspace", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk_small, tks, 8, 0, -1, 0, 0); });
+    expect_reject("gemm_sk residual dtype", [&] { gemm_sk(x, wsb, 64, ob, 3, wsk, tks, 8, 0, -1, 0, 0); });
     auto hs = T({300, 64}, F32), hs_small = T({299, 64}, F32);
-    expect_ok("gemm_sk residual", [&] { gemm_sk(x, wsb, 64, hs, 3, wsk, tks, 8, 0, -1); });
-    expect_reject("gemm_sk residual too small", [&] { gemm_sk(x, wsb, 64, hs_small, 3, wsk, tks, 8, 0, -1); });
+    expect_ok("gemm_sk residual", [&] { gemm_sk(x, wsb, 64, hs, 3, wsk, tks, 8, 0, -1, 0, 0); });
+    expect_reject("gemm_sk residual too small", [&] { gemm_sk(x, wsb, 64, hs_small, 3, wsk, tks, 8, 0, -1, 0, 0); });
+    // fragment-major X (a flat buffer of ceil(300 / 16) * 16 rows) and SiLU output
+    auto xfr = T({304 * 128}, BF), xf_small = T({300 * 128}, BF), of = T({304 * 32}, BF);
+    expect_ok("gemm_sk fragment-major x", [&] { gemm_sk(xfr, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, 1, 300); });
+    expect_reject("gemm_sk fragment-major x too small", [&] { gemm_sk(xf_small, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, 1, 300); });
+    expect_reject("gemm_sk fragment-major x without rows", [&] { gemm_sk(xfr, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, 1, 0); });
+    expect_ok("gemm_sk fragment-major silu", [&] { gemm_sk(xfr, wsb, 64, of, 2, wsk, tks, 8, 0, -1, 3, 300); });
+    expect_reject("gemm_sk fragment-major bf16 out", [&] { gemm_sk(x, wsb, 64, ob, 0, wsk, tks, 8, 0, -1, 2, 0); });
     expect_ok("fp8_gemm_t256", [&] { fp8_gemm_t256(xq, sxq, wq, sw, 64, o2, 1, 1); });
     auto sw_small = T({32}, F32);
     expect_reject("fp8_gemm_t256 weight scales", [&] { fp8_gemm_t256(xq, sxq, wq, sw_small, 64, o2, 1, 1); });
@@ -181,14 +188,17 @@ int main() {
     expect_reject("kv8_dequant mb", [&] { kv8_dequant(k8, v8, ks, ks, bt, ctx, mb + 1, ko, ko); });
     // prefill: 2 sequences of 70 and 30 tokens
     auto qp = T({100, H, 128}, BF), outp = T({100, H, 128}, BF), cu = T({B + 1}, I32), work = T({2, 4}, I32);
-    expect_ok("attn_prefill32", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 1); });
+    expect_ok("attn_prefill32", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 1, 0); });
     auto work_bad = T({2, 5}, I32), work8 = T({2, 8}, I32);
-    expect_ok("attn_prefill32 paired", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 1); });
-    expect_reject("attn_prefill removed split mode", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 3); });
-    expect_reject("attn_prefill32 work", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work_bad, H, Hkv, 0.08, outp, 1); });
+    expect_ok("attn_prefill32 paired", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 1, 0); });
+    expect_reject("attn_prefill removed split mode", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work8, H, Hkv, 0.08, outp, 3, 0); });
+    expect_reject("attn_prefill32 work", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work_bad, H, Hkv, 0.08, outp, 1, 0); });
     auto cu_bad = T({B}, I32);
-    expect_reject("attn_prefill offsets", [&] { attn_prefill(qp, kc, vc, bt, cu_bad, ctx, work, H, Hkv, 0.08, outp, 1); });
-    expect_reject("attn_prefill rows32 mode", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 2); });
+    expect_reject("attn_prefill offsets", [&] { attn_prefill(qp, kc, vc, bt, cu_bad, ctx, work, H, Hkv, 0.08, outp, 1, 0); });
+    expect_reject("attn_prefill rows32 mode", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outp, 2, 0); });
+    auto outf = T({112 * H * 128}, BF);  // fragment-major output: ceil(100 / 16) = 7 row tiles
+    expect_ok("attn_prefill32 fragment-major out", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outf, 1, 7); });
+    expect_reject("attn_prefill fragment-major tiles", [&] { attn_prefill(qp, kc, vc, bt, cu, ctx, work, H, Hkv, 0.08, outf, 1, 6); });
     auto qkv = T({100, (H + 2 * Hkv) * 128}, BF), tpos = T({100}, I32), tseq = T({100}, I32), qo = T({100, H, 128}, BF);
     expect_ok("rope_append", [&] { rope_append(qkv, tpos, tseq, bt, cs, cs, qo, kc, vc, H, Hkv, none, none); });
     auto qo_small = T({99, H, 128}, BF);

@@ -882,10 +882,8 @@ class ModelRunner:
         f32 = dict(dtype=torch.float32, device=dev)
         bf = dict(dtype=torch.bfloat16, device=dev)
         h = torch.empty(T, d, **f32)
-        xn = torch.empty(T, d, **bf)
         qkv = torch.empty(T, (self.H + 2 * self.Hkv) * self.D, **bf)
         q = torch.empty(T, self.H, self.D, **bf)
-        attn = torch.empty(T, self.H * self.D, **bf)
         sk_o = self._splitk(T, self.H * self.D)
         sk_d = self._splitk(T, self.ffn_l)
         d_parts = None
@@ -897,15 +895,24 @@ class ModelRunner:
         tp1 = self.tp is None or self.tp.size == 1
         res_o = tp1 and T > 64 and ops.res_supported(w.layers[0].wo)
         res_d = tp1 and T > 64 and ops.res_supported(w.layers[0].w_down)
+        # fragment-major activations (ops.to_xfrag, ceil(T / 16) row tiles): the norms, the attention and the gate_up
+        # SiLU epilogue write every stream-K GEMM input in the order the GEMM stages it, one contiguous KiB per MFMA
+        # fragment (ops.PREFILL_XF)
+        xfp = res_o and res_d and ops.PREFILL_XF
+        rows = T if xfp else None
+        mt16 = 16 * ops.xfrag_tiles(T)
+        xn = torch.empty(mt16 * d, **bf) if xfp else torch.empty(T, d, **bf)
+        attn = torch.empty(mt16 * self.H * self.D, **bf) if xfp else torch.empty(T, self.H * self.D, **bf)
+        act = torch.empty(mt16 * (w.layers[0].w_gate_up.N // 2), **bf) if xfp else None
         for l, lw in enumerate(w.layers):
             if l == 0:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed)
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, ids=ids, emb=w.embed, rows=rows, xf=xfp)
             else:
-                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, write_h=not res_d)
-            self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T)
+                ops.add_rmsnorm(h, lw.attn_norm, self.eps, xn, parts=d_parts, write_h=not res_d, rows=rows, xf=xfp)
+            self._prefill_attention(xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T, xfp)
             if res_o:
-                ops.linear_res(attn, lw.wo, h)
-                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, write_h=False)
+                ops.linear_res(attn, lw.wo, h, rows=rows)
+                ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, write_h=False, rows=rows, xf=xfp)
             else:
                 o_parts = ops.linear(attn, lw.wo, "f32", splitk=sk_o)
                 if not self.on_gpu:
@@ -913,13 +920,15 @@ class ModelRunner:
                 o_parts = self._reduce_parts(o_parts)
                 ops.add_rmsnorm(h, lw.mlp_norm, self.eps, xn, parts=o_parts)
             sk_g = self._splitk(T, self.d, lw.w_gate_up.N)
-            if sk_g > 1:  # small tile grid: f32 split-K slabs, then silu(gate) * up over the slabs
+            if xfp:
+                ops.linear_sk(xn, lw.w_gate_up, "silu", act, rows=T, xf_out=True)
+            elif sk_g > 1:  # small tile grid: f32 split-K slabs, then silu(gate) * up over the slabs
                 act = ops.silu_parts(ops.linear(xn, lw.w_gate_up, "f32", splitk=sk_g),
                                      torch.empty(T, lw.w_gate_up.N // 2, **bf))
             else:
                 act = ops.linear(xn, lw.w_gate_up, "silu")
             if res_d:
-                ops.linear_res(act, lw.w_down, h)
+                ops.linear_res(act, lw.w_down, h, rows=rows)
                 d_parts = None
             else:
                 d_parts = ops.linear(act, lw.w_down, "f32", splitk=sk_d)
@@ -932,24 +941,30 @@ class ModelRunner:
         ops.add_rmsnorm(h, w.final_norm, self.eps, xl, parts=d_parts, row_idx=last, write_h=False)
         return xl
 
-    def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T):
+    def _prefill_attention(self, xn, lw, l, qkv, q, attn, posd, tsd, bt, cud, ctxd, work, T, xf=False):
+        """qkv projection + RoPE + KV-cache append + causal attention of one prefill layer.  xf: xn and attn are
+        flat fragment-major buffers of T rows (``_prefill_layers``)."""
         kc, vc = self.kv[l, 0], self.kv[l, 1]
         kvs = self._kv_scales(l)
+        rows = T if xf else None
+        out = attn if xf else attn.view(T, self.H, self.D)
+        akw = dict(work=work, cu_list=self._cu_host, kv_scales=kvs, kv8_scratch_=self._kv8_scratch, xf=xf)
         if self.on_gpu and ops.rope_fusable(lw.wqkv, self.kv_fp8, T) and bt.shape[1] > 0:
             # RoPE + the KV-cache append in the qkv GEMM's epilogue: no qkv round trip, no rope_append launch
-            ops.linear_rope(xn, lw.wqkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv)
-            ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
-                             work=work, cu_list=self._cu_host, kv_scales=kvs, kv8_scratch_=self._kv8_scratch)
+            ops.linear_rope(xn, lw.wqkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, rows=rows)
+            ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, out, **akw)
             return
         sk_q = self._splitk(T, self.d, (self.H + 2 * self.Hkv) * self.D)
-        if sk_q > 1:  # small tile grid: f32 split-K slabs, summed by rope_append while it rotates
+        if xf:
+            ops.linear_sk(xn, lw.wqkv, "bf16", qkv, rows=T)
+            ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)
+        elif sk_q > 1:  # small tile grid: f32 split-K slabs, summed by rope_append while it rotates
             parts = ops.linear(xn, lw.wqkv, "f32", splitk=sk_q)
             ops.rope_append(parts, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)
         else:
             ops.linear(xn, lw.wqkv, "bf16", out=qkv)
             ops.rope_append(qkv, posd, tsd, bt, self.cos, self.sin, q, kc, vc, self.H, self.Hkv, kv_scales=kvs)
-        ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, attn.view(T, self.H, self.D),
-                         work=work, cu_list=self._cu_host, kv_scales=kvs, kv8_scratch_=self._kv8_scratch)
+        ops.attn_prefill(q, kc, vc, bt, cud, ctxd, self.H, self.Hkv, self.scale, out, **akw)
 
     def _prefill_layers_sp(self, T, ids, posd, tsd, bt, cud, ctxd, last, work, n, commit):
         """Sequence-parallel prefill under TP: rank r owns rows [r*Tl, (r+1)*Tl) of the residual stream.

@@ -482,41 +482,62 @@ def sk_config(M: int, N: int, K: int, epi: str) -> int:
 
 
 def gemm_sk(x: torch.Tensor, wf: torch.Tensor, N: int, out: torch.Tensor, epi: str,
-            min_share: Optional[int] = None, cfg: Optional[int] = None) -> torch.Tensor:
+            min_share: Optional[int] = None, cfg: Optional[int] = None, rows: Optional[int] = None,
+            xf_out: bool = False) -> torch.Tensor:
     """out (epi 'bf16' / 'f32' / 'silu') or h (epi 'res': h[:M] += x @ W^T) from the stream-K prefill GEMM over the
     fragment-layout bf16 weight ``wf``.  cfg: None = the measured table (``sk_config``), -1 = the kernel's
-    tile-shape cost model, else an SK_CFGS index (+ 8: whole tiles only)."""
+    tile-shape cost model, else an SK_CFGS index (+ 8: whole tiles only).  rows: x is a flat buffer in the
+    fragment-major layout (``to_xfrag``) of that many rows; xf_out: the SiLU output is written in it."""
+    M, K = (rows, wf.numel() // N) if rows is not None else x.shape
     if cfg is None:
-        cfg = sk_config(x.shape[0], N, x.shape[1], epi)
+        cfg = sk_config(M, N, K, epi)
     ws, tk, ncu = _sk_workspace(x.device)
-    ext().gemm_sk(x, wf, N, out, _SK_EPI[epi], ws, tk, ncu, SK_MIN_SHARE if min_share is None else min_share, cfg)
+    ext().gemm_sk(x, wf, N, out, _SK_EPI[epi], ws, tk, ncu, SK_MIN_SHARE if min_share is None else min_share, cfg,
+                  (1 if rows is not None else 0) + (2 if xf_out else 0), rows or 0)
     return out
 
 
-def linear_res(x: torch.Tensor, w: PackedWeight, h: torch.Tensor) -> torch.Tensor:
+def linear_sk(x: torch.Tensor, w: PackedWeight, epi: str, out: torch.Tensor, rows: Optional[int] = None,
+              xf_out: bool = False) -> torch.Tensor:
+    """Prefill projection (M > 64) on the stream-K kernel into ``out`` (epi 'bf16' | 'silu'), with fragment-major
+    activations: rows = x is a flat ``to_xfrag`` buffer of that many rows; xf_out = the SiLU output is written in
+    that layout too (flat, >= xfrag_tiles(rows) * 16 * N / 2), the down projection's input."""
+    M = rows if rows is not None else x.shape[0]
+    if not _gpu(x):
+        y = ref.linear(from_xfrag(x, M, w.K) if rows is not None else x, w.dense(), epi)
+        f = to_xfrag(y) if xf_out else y
+        out.view(-1)[: f.numel()].copy_(f.reshape(-1))
+        return out
+    wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
+    return gemm_sk(x, wf, w.N, out, epi, rows=rows, xf_out=xf_out)
+
+
+def linear_res(x: torch.Tensor, w: PackedWeight, h: torch.Tensor, rows: Optional[int] = None) -> torch.Tensor:
     """h[:M] += x @ W^T in f32 (prefill o / down, M > 64, TP = 1): the residual add rides in the GEMM epilogue, so the
     norm after it reads h alone.  bf16 weights, or quantised ones through their bf16 dequantisation scratch; W8A8
-    fp8 prefill keeps its slab path (``res_supported``)."""
-    M = x.shape[0]
+    fp8 prefill keeps its slab path (``res_supported``).  rows: x is fragment-major (``to_xfrag``) with that many."""
+    M = rows if rows is not None else x.shape[0]
     if not _gpu(x):
-        h[:M] += ref.linear(x, w.dense(), "f32")
+        xr = from_xfrag(x, M, w.K) if rows is not None else x
+        h[:M] += ref.linear(xr, w.dense(), "f32")
         return h
     wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
-    return gemm_sk(x, wf, w.N, h, "res")
+    return gemm_sk(x, wf, w.N, h, "res", rows=rows)
 
 
 def linear_rope(x: torch.Tensor, w: PackedWeight, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc,
-                H: int, Hkv: int) -> None:
+                H: int, Hkv: int, rows: Optional[int] = None) -> None:
     """The prefill qkv projection with RoPE and the paged bf16 KV-cache append fused into the GEMM epilogue (M > 64,
     bf16 cache): q_out [T, H, 128] = rotated q, the cache gets rotated k and v at each token's slot.  CPU: the
-    unfused reference (bf16 qkv, then ``rope_append``)."""
+    unfused reference (bf16 qkv, then ``rope_append``).  rows: x is fragment-major (``to_xfrag``) with that many."""
+    M = rows if rows is not None else x.shape[0]
     if not _gpu(x):
-        qkv = linear(x, w, "bf16")
+        qkv = linear(from_xfrag(x, M, w.K) if rows is not None else x, w, "bf16")
         return ref.rope_append(qkv, pos, tok_seq, block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
     wf = w.data if w.kind == "bf16" else _dequant_scratch(w, x.device)
     ws, tk, ncu = _sk_workspace(x.device)
-    ext().gemm_sk_rope(x, wf, ws, tk, ncu, SK_MIN_SHARE, rope_config(x.shape[0], w.N, x.shape[1]), pos, tok_seq,
-                       block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv)
+    ext().gemm_sk_rope(x, wf, ws, tk, ncu, SK_MIN_SHARE, rope_config(M, w.N, w.K), pos, tok_seq,
+                       block_tables, cos_t, sin_t, q_out, kc, vc, H, Hkv, 1 if rows is not None else 0, rows or 0)
 
 
 def rope_config(M: int, N: int, K: int) -> int:
@@ -552,6 +573,10 @@ def res_supported(w: PackedWeight) -> bool:
 
 # prefill o / down: residual add in the GEMM epilogue (1) or an f32 GEMM output summed by the next add_rmsnorm (0)
 RES_FUSED = os.environ.get("LSA_RES_FUSED", "1") != "0"
+# TP = 1 prefill with every stream-K GEMM input in the fragment-major layout (engine.runner._prefill_layers): the
+# producers (add_rmsnorm, the prefill attention, the gate_up SiLU epilogue) write it, the GEMM stages each MFMA
+# fragment as one contiguous KiB instead of 16 half-lines
+PREFILL_XF = os.environ.get("LSA_PREFILL_XF", "1") != "0"
 
 
 def linear(x: torch.Tensor, w: PackedWeight, epi: str = "bf16", out: Optional[torch.Tensor] = None,
@@ -682,8 +707,9 @@ def num_cus(device) -> int:
 
 
 def xfrag_tiles(M: int) -> int:
-    """Row tiles (16 rows each) of the fragment-major activation layout for M rows (decode: M <= 64)."""
-    return 1 if M <= 16 else (2 if M <= 32 else 4)
+    """Row tiles (16 rows each) of the fragment-major activation layout for M rows: decode (M <= 64) rounds up to
+    1 | 2 | 4 tiles (the skinny kernels' MT), prefill (M > 64) to ceil(M / 16) (the stream-K GEMM's xf operands)."""
+    return 1 if M <= 16 else (2 if M <= 32 else (4 if M <= 64 else (M + 15) // 16))
 
 
 def to_xfrag(x: torch.Tensor) -> torch.Tensor:
@@ -1350,13 +1376,21 @@ def _pair_blocks(n_items: int, heads: int, longest: int, qblock: int) -> bool:
 
 
 def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, work=None, cu_list=None,
-                 kv_scales=None, kv8_scratch_=None):
+                 kv_scales=None, kv8_scratch_=None, xf: bool = False):
     """Causal prefill attention of packed sequences (cu_q offsets) over the paged cache.  ``work``: the
     ``prefill_plan`` of the same offsets (or None: planned here from ``cu_list`` / the device offsets).
     kv_scales = (ks, vs): fp8 cache -- the attended blocks are widened into ``kv8_scratch_`` (= kv8_scratch(ctx,
-    ...), built from the host context list; made here when not given) and the bf16 kernels run on that."""
+    ...), built from the host context list; made here when not given) and the bf16 kernels run on that.
+    xf: ``out`` is a flat buffer receiving the fragment-major layout (``to_xfrag``) of the [T, H * 128] rows -- the
+    o projection's stream-K input."""
+    T = q.shape[0]
     if not _gpu(q):
-        return ref.attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, kv_scales)
+        if not xf:
+            return ref.attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, kv_scales)
+        tmp = ref.attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, torch.empty_like(q), kv_scales)
+        f = to_xfrag(tmp.reshape(T, -1))
+        out.view(-1)[: f.numel()].copy_(f)
+        return out
     if kv_scales is not None:
         ko, vo, table = kv8_scratch_ if kv8_scratch_ is not None else kv8_scratch(ctx_lens.tolist(), Hkv, q.device)
         ext().kv8_dequant(kc, vc, kv_scales[0], kv_scales[1], block_tables, ctx_lens, table.shape[1], ko, vo)
@@ -1367,7 +1401,7 @@ def attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, H, Hkv, scale, out, wo
         plan = (prefill_plan(cu, ctx=ctx_lens.tolist(), heads=H, device=q.device) if work is None
                 else PrefillPlan(_prefill_kernel(cu), work))
     ext().attn_prefill(q, kc, vc, block_tables, cu_q, ctx_lens, plan.work, H, Hkv, scale, out,
-                       1 if plan.kernel == "32" else 0)
+                       1 if plan.kernel == "32" else 0, xfrag_tiles(T) if xf else 0)
     return out
 
 

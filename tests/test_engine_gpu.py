@@ -81,6 +81,29 @@ def test_prefill_logits_match_hf(gpu):
     assert rel < 3e-2, rel  # bf16 activations vs an fp32 reference
 
 
+@pytest.mark.parametrize("rope_fused", [False, True])
+def test_prefill_fragment_major_matches_row_major(gpu, monkeypatch, rope_fused):
+    """The fragment-major prefill activations (ops.PREFILL_XF: norms, attention and the gate_up SiLU epilogue write
+    the stream-K GEMM inputs in the MFMA fragment order) compute the same numbers in the same order as the row-major
+    path: the last-position logits of a 2-sequence prefill (T = 293, a partial last row tile) are bitwise equal, with
+    the unfused qkv GEMM and with the RoPE / cache-append epilogue."""
+    from llm_based_apache_spark_optimization_amd import ops
+
+    spec, m = _hf("tiny-llama3")
+    w = from_hf_state_dict(spec, m.state_dict(), gpu)
+    monkeypatch.setattr(ops, "ROPE_FUSED_MIN_M", 65 if rope_fused else 1 << 30)
+    got = {}
+    for xf in (False, True):
+        monkeypatch.setattr(ops, "PREFILL_XF", xf)
+        runner = ModelRunner(w, max_slots=2, max_model_len=512)
+        runner.set_slot(0, [1, 2, 3, 4], 4)  # 194 tokens: four 64-token blocks; 100 tokens: two
+        runner.set_slot(1, [5, 6], 4)
+        runner.prefill([(0, [1] + list(range(7, 200)), 0), (1, [1] + list(range(300, 399)), 0)])
+        got[xf] = runner.logits_l[:2].float().cpu()
+    assert torch.isfinite(got[True]).all()
+    assert torch.equal(got[True], got[False])
+
+
 def test_continuous_batching_mixed_lengths(gpu):
     eng = build_engine("tiny-nsql", device=str(gpu), max_slots=4, max_model_len=512, sync_every=4)
     ref = build_engine("tiny-nsql", device=str(gpu), max_slots=4, max_model_len=512, use_graphs=False)

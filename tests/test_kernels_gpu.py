@@ -232,6 +232,49 @@ def test_gemm_stream_k_epilogues(gpu, cfg, MNK, epi):
     assert _rel(out, _sk_ref(x.float(), w, epi)) < 1e-2, (M, N, K, epi, cfg)
 
 
+@pytest.mark.parametrize("cfg", [-1, 0, 3, 5, 6, 7, 12])
+@pytest.mark.parametrize("MNK", [(300, 3072, 1376), (2048, 5120, 1024), (1100, 800, 512), (65, 1536, 2048)])
+@pytest.mark.parametrize("epi", ["bf16", "silu", "res"])
+def test_gemm_stream_k_fragment_major(gpu, cfg, MNK, epi):
+    """Fragment-major X (ops.to_xfrag, ceil(M / 16) row tiles; the pad rows of the last tile hold NaN, which must not
+    reach a real row) and, for SiLU, a fragment-major output: bitwise equal to the row-major call of the same
+    configuration (the same MFMAs in the same order), every element written, tickets left zero.  K = 1376: an odd
+    k-step count, the last K-tile's missing step staged from past the buffer end."""
+    M, N, K = MNK
+    if epi == "silu" and cfg >= 0 and not ops.sk_cfg_pairs(cfg):
+        pytest.skip("SiLU needs an even n-block count per wave")
+    if epi == "silu" and N % 64:
+        pytest.skip("a fragment-major SiLU output holds whole 32-column k-steps")
+    torch.manual_seed(M + N + K)
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
+    pw = ops.PackedWeight.from_dense(w)
+    mt = ops.xfrag_tiles(M)
+    xp = torch.full((mt * 16, K), float("nan"), device=gpu, dtype=torch.bfloat16)
+    xp[:M] = x
+    xf = xp.view(mt, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).contiguous().view(-1)
+    assert torch.equal(ops.from_xfrag(xf, M, K), x)
+    ws, tk, ncu = ops._sk_workspace(gpu)
+    ncol = N // 2 if epi == "silu" else N
+    if epi == "res":
+        h0 = torch.randn(M, N, device=gpu)
+        a, b = h0.clone(), h0.clone()
+        ops.ext().gemm_sk(x, pw.data, N, a, 3, ws, tk, ncu, 4, cfg)
+        ops.ext().gemm_sk(xf, pw.data, N, b, 3, ws, tk, ncu, 4, cfg, 1, M)
+    else:
+        a = torch.full((M, ncol), float("nan"), device=gpu, dtype=torch.bfloat16)
+        ops.ext().gemm_sk(x, pw.data, N, a, ops._SK_EPI[epi], ws, tk, ncu, 4, cfg)
+        xo = epi == "silu"
+        b = torch.full(((mt * 16 if xo else M) * ncol,), float("nan"), device=gpu, dtype=torch.bfloat16)
+        ops.ext().gemm_sk(xf, pw.data, N, b, ops._SK_EPI[epi], ws, tk, ncu, 4, cfg, 3 if xo else 1, M)
+        b = ops.from_xfrag(b, M, ncol) if xo else b.view(M, ncol)
+    torch.cuda.synchronize()
+    assert int(tk.abs().sum()) == 0
+    assert not torch.isnan(b.float()).any()
+    assert torch.equal(a, b), (M, N, K, epi, cfg, _rel(b, a))
+    assert _rel(b, _sk_ref(x.float(), w, epi, h0 if epi == "res" else None)) < (1e-5 if epi == "res" else 1e-2)
+
+
 @pytest.mark.parametrize("ncu", [8, 24, 40])
 @pytest.mark.parametrize("MN", [(777, 1280), (2048, 10240), (1024, 4096)])
 def test_gemm_stream_k_dp_rounds(gpu, ncu, MN):
@@ -549,6 +592,11 @@ def test_attn_prefill(gpu, HH, case, kernel, monkeypatch):
     ops.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, scale, out)
     ref.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, scale, out2)
     assert _rel(out, out2) < 1e-2
+    # the fragment-major output (the o projection's stream-K input): the same values, rearranged
+    of = torch.full((ops.xfrag_tiles(T) * 16 * H * D,), float("nan"), device=gpu, dtype=torch.bfloat16)
+    ops.attn_prefill(q, kc, vc, bt, cu, cl, H, Hkv, scale, of, xf=True)
+    torch.cuda.synchronize()
+    assert torch.equal(ops.from_xfrag(of, T, H * D), out.view(T, H * D))
 
 
 @pytest.mark.parametrize("kernel", P_KERNELS)
