@@ -70,6 +70,7 @@ int lsa_fp8_gemm_cfg(const void* X, int ldx, int M, int K, const void* Wq, const
 void lsa_gemm_sk_epilogue(int mode);
 void lsa_gemm_sk_nbuf(int n);
 void lsa_gemm_sk_one_phase(int on);
+void lsa_rmsnorm_xf_tile_min(int rows);
 int lsa_gemm_sk_rope(const void* X, int ldx, int M, int K, const void* Wf, int N, float* ws, int* tickets, int ncu,
                      int min_share, int cfg, const int* pos, const int* tok_seq, const int* block_tables,
                      int max_blocks, const float* cos_t, const float* sin_t, void* q_out, void* kc, void* vc, int H,
@@ -1032,6 +1033,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_sk_epilogue", [](int64_t mode) { lsa_gemm_sk_epilogue((int)mode); });
   m.def("gemm_sk_nbuf", [](int64_t n) { lsa_gemm_sk_nbuf((int)n); });
   m.def("gemm_sk_one_phase", [](int64_t on) { lsa_gemm_sk_one_phase((int)on); });
+  m.def("rmsnorm_xf_tile_min", [](int64_t rows) { lsa_rmsnorm_xf_tile_min((int)rows); });
   m.def("gemm_sk_ws_bytes", [](int64_t ncu) { return lsa_gemm_sk_ws_bytes((int)ncu); });
   m.def("gemm_sk_tickets", [](int64_t ncu) { return (int64_t)lsa_gemm_sk_tickets((int)ncu); });
   m.def("fp4_gemm", &fp4_gemm, py::arg("x"), py::arg("wq"), py::arg("sw"), py::arg("N"), py::arg("out"), py::arg("epi"),

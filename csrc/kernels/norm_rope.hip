@@ -134,6 +134,58 @@ static void launch_rmsnorm(int np, int rows, int nt, hipStream_t s, float* h, co
 #undef LSA_RN
 }
 
+// Prefill RMSNorm of h into the fragment-major layout (the stream-K GEMM's X, ops.PREFILL_XF), D <= 4096: one
+// workgroup per 8 rows (half a 16-row tile).  Pass 1: wave w reads row w with whole-line loads, sums its squares
+// (DPP / permlane wave sum) and parks the f32 row in LDS.  Pass 2: lane (s, g, r) = (l >> 5, (l >> 3) & 3, l & 7)
+// takes row r's columns 32 ks + 8 g .. + 7 of k-step ks = 2 i + s, scales them and stores 16 B at its fragment lane
+// 16 g + 8 (tile half) + r: per instruction four 128-B runs in each of two fragments, all whole lines.  The
+// row-per-workgroup kernel above writes the layout as 16-B pieces of 64 different lines per instruction (3B 2k rows:
+// 18.4 us vs 9.7 row-major); a 16-row-tile kernel with the fragment mapping in both passes ran 16-21 us at every
+// size (1024 threads on rows / 16 CUs, half-line loads; scripts/bench_norm_xf.py).
+#define LSA_XFN_DMAX 4096
+__global__ __launch_bounds__(512) void rmsnorm_xf_kernel(const float* __restrict__ h, const uint16_t* __restrict__ w,
+                                                        float eps, uint16_t* __restrict__ xn, int M, int D, int mt) {
+  __shared__ __attribute__((aligned(16))) float img[8 * (LSA_XFN_DMAX + 4)];
+  __shared__ float rinv[8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.x, m = b * 8 + wv, ld = D + 4;
+  float ss = 0.f;
+  if (m < M) {
+    const float4* hr = reinterpret_cast<const float4*>(h + (size_t)m * D);
+#pragma unroll 4
+    for (int c4 = lane; c4 < D / 4; c4 += 64) {
+      const float4 a = hr[c4];
+      ss += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+      *reinterpret_cast<float4*>(&img[wv * ld + 4 * c4]) = a;
+    }
+  }
+  ss = wave_sum(ss);
+  if (lane == 0) rinv[wv] = m < M ? rsqrtf(ss / (float)D + eps) : 0.f;
+  __syncthreads();
+  const int s = lane >> 5, g = (lane >> 3) & 3, r = lane & 7, KS = D >> 5;
+  const int rb = b >> 1, fl = 16 * g + 8 * (b & 1) + r;
+  const float inv = rinv[r];
+  for (int i = wv; 2 * i < KS; i += 8) {
+    const int ks = 2 * i + s;
+    if (ks < KS) {
+      const int c = 32 * ks + 8 * g;
+      const float4 a = *reinterpret_cast<const float4*>(&img[r * ld + c]);
+      const float4 q = *reinterpret_cast<const float4*>(&img[r * ld + c + 4]);
+      float wf[8];
+      unpack8(*reinterpret_cast<const uint4*>(w + c), wf);
+      float v[8] = {a.x, a.y, a.z, a.w, q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = v[j] * inv * wf[j];
+      *reinterpret_cast<uint4*>(xn + ((size_t)(ks * mt + rb) * 64 + fl) * 8) = pack8(v);
+    }
+  }
+}
+
+// minimum rows for rmsnorm_xf_kernel (below it the row-per-workgroup kernel writes the layout);
+// lsa_rmsnorm_xf_tile_min sets it (A/B knob, scripts/bench_norm_xf.py)
+static int g_xf_tile_min = 512;
+extern "C" void lsa_rmsnorm_xf_tile_min(int rows) { g_xf_tile_min = rows; }
+
 // x8 / sx8 (optional): also write the output rows as fp8 e4m3 in the xf8 layout of xf_mt row tiles with a
 // per-row scale (the W8A8 decode GEMM input); xn may then be null (no bf16 copy)
 extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long part_stride, const int* ids,
@@ -145,6 +197,13 @@ extern "C" int lsa_add_rmsnorm(float* h, const float* parts, int nparts, long pa
   if (ss_out && (row_idx || ss_ld < rows || ss_nzero < 0)) return -4;
   if (x8 && (!sx8 || !xf_mt || D % 128 != 0 || row_idx)) return -5;
   if (!xn && !x8) return -6;
+  if (xf_mt && rows > 64 && rows >= g_xf_tile_min && D <= LSA_XFN_DMAX && !(parts && nparts) && !ids && !row_idx &&
+      !ss_out && !x8 && xn) {
+    // prefill norm of h alone into the fragment-major layout (write_h is a no-op without parts / ids)
+    hipLaunchKernelGGL(rmsnorm_xf_kernel, dim3((rows + 7) / 8), dim3(512), 0, s, h,
+                       reinterpret_cast<const uint16_t*>(w), eps, reinterpret_cast<uint16_t*>(xn), rows, D, xf_mt);
+    return (int)hipGetLastError();
+  }
   const int vec = D / 8;
   const uint16_t* e = reinterpret_cast<const uint16_t*>(emb);
   const uint16_t* ww = reinterpret_cast<const uint16_t*>(w);

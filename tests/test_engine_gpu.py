@@ -84,9 +84,10 @@ def test_prefill_logits_match_hf(gpu):
 @pytest.mark.parametrize("rope_fused", [False, True])
 def test_prefill_fragment_major_matches_row_major(gpu, monkeypatch, rope_fused):
     """The fragment-major prefill activations (ops.PREFILL_XF: norms, attention and the gate_up SiLU epilogue write
-    the stream-K GEMM inputs in the MFMA fragment order) compute the same numbers in the same order as the row-major
-    path: the last-position logits of a 2-sequence prefill (T = 293, a partial last row tile) are bitwise equal, with
-    the unfused qkv GEMM and with the RoPE / cache-append epilogue."""
+    the stream-K GEMM inputs in the MFMA fragment order) against the row-major path: the last-position logits of a
+    2-sequence prefill (T = 294, a partial last row tile), with the unfused qkv GEMM and with the RoPE / cache-append
+    epilogue.  The GEMMs and the attention are bitwise equal between the layouts (test_kernels_gpu); the 16-row-tile
+    norm sums its squares in another order, so the logits agree to bf16-rounding level."""
     from llm_based_apache_spark_optimization_amd import ops
 
     spec, m = _hf("tiny-llama3")
@@ -101,7 +102,8 @@ def test_prefill_fragment_major_matches_row_major(gpu, monkeypatch, rope_fused):
         runner.prefill([(0, [1] + list(range(7, 200)), 0), (1, [1] + list(range(300, 399)), 0)])
         got[xf] = runner.logits_l[:2].float().cpu()
     assert torch.isfinite(got[True]).all()
-    assert torch.equal(got[True], got[False])
+    assert (got[True] - got[False]).norm() / got[False].norm() < 1e-2
+    assert torch.equal(got[True].argmax(1), got[False].argmax(1))
 
 
 def test_continuous_batching_mixed_lengths(gpu):

@@ -406,6 +406,25 @@ def test_add_rmsnorm_xfrag(gpu, rows):
     assert torch.equal(ops.from_xfrag(xf, rows, D), xr)
 
 
+@pytest.mark.parametrize("rows", [65, 300, 2048])
+@pytest.mark.parametrize("D", [3072, 4096, 160])
+def test_add_rmsnorm_xfrag_prefill(gpu, rows, D):
+    """The prefill norm of h alone into the fragment-major layout (16-row-tile kernel, rows > 64; a partial last
+    tile at 65 / 300 rows; D = 160: fewer k-steps than waves) vs the fp32 reference, h untouched."""
+    torch.manual_seed(rows + D)
+    h = torch.randn(rows, D, device=gpu) * 3
+    w = torch.randn(D, device=gpu).to(torch.bfloat16)
+    h0 = h.clone()
+    xf = torch.full((ops.xfrag_tiles(rows) * 16 * D,), float("nan"), device=gpu, dtype=torch.bfloat16)
+    ops.add_rmsnorm(h, w, 1e-5, xf, write_h=False, rows=rows, xf=True)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h0)
+    want = h0 * torch.rsqrt(h0.pow(2).mean(1, keepdim=True) + 1e-5) * w.float()
+    got = ops.from_xfrag(xf, rows, D).float()
+    assert torch.isfinite(got).all()
+    assert _rel(got, want) < 1e-2
+
+
 @pytest.mark.parametrize("HH", [(32, 32), (24, 8)])
 def test_rope_append(gpu, HH):
     H, Hkv = HH
