@@ -406,11 +406,21 @@ def test_add_rmsnorm_xfrag(gpu, rows):
     assert torch.equal(ops.from_xfrag(xf, rows, D), xr)
 
 
-@pytest.mark.parametrize("rows", [65, 300, 2048])
+@pytest.mark.parametrize("kernel", ["rows8", "row_per_wg"])
+@pytest.mark.parametrize("rows", [65, 300, 777, 2048])
 @pytest.mark.parametrize("D", [3072, 4096, 160])
-def test_add_rmsnorm_xfrag_prefill(gpu, rows, D):
-    """The prefill norm of h alone into the fragment-major layout (16-row-tile kernel, rows > 64; a partial last
-    tile at 65 / 300 rows; D = 160: fewer k-steps than waves) vs the fp32 reference, h untouched."""
+def test_add_rmsnorm_xfrag_prefill(gpu, rows, D, kernel):
+    """The prefill norm of h alone into the fragment-major layout (the 8-row LDS-staged kernel, forced at every size
+    here, and the row-per-workgroup one; partial last tiles at 65 / 300 / 777 rows; D = 160: an odd k-step count)
+    vs the fp32 reference, h untouched."""
+    ops.ext().rmsnorm_xf_tile_min(65 if kernel == "rows8" else 1 << 30)
+    try:
+        _norm_xf_case(gpu, rows, D)
+    finally:
+        ops.ext().rmsnorm_xf_tile_min(512)
+
+
+def _norm_xf_case(gpu, rows, D):
     torch.manual_seed(rows + D)
     h = torch.randn(rows, D, device=gpu) * 3
     w = torch.randn(D, device=gpu).to(torch.bfloat16)
