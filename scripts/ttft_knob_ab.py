@@ -1,7 +1,8 @@
 """Time to first token under a kernel knob, arms interleaved in one process (cdna_hip_programming.md §5.4 rule 24): a
 one-token request (prefill + first-token commit + host read-back) for each case, median (and min) of the rounds.
 Knob 'one_phase': the stream-K GEMM's one-phase K-loop schedule for the 128-row tiles (ext.gemm_sk_one_phase);
-'prefill_xf': the fragment-major prefill activations (ops.PREFILL_XF);
+'prefill_xf': the fragment-major prefill activations (ops.PREFILL_XF); 'rope_fused_all': the RoPE / cache-append
+qkv epilogue at every prefill size (1) vs from 4096 rows (0, the default);
 'none': one arm, the loaded build (cross-build A/Bs: run it under LSA_HIP_SO=variants/<name>.so in turns).
 Usage: ttft_knob_ab.py [knob] [rounds] [case,...]"""
 import json
@@ -18,7 +19,8 @@ from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build
 knob = sys.argv[1] if len(sys.argv) > 1 else "one_phase"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 KNOBS = {"one_phase": lambda v: ops.ext().gemm_sk_one_phase(v), "none": lambda v: None,
-         "prefill_xf": lambda v: setattr(ops, "PREFILL_XF", bool(v))}
+         "prefill_xf": lambda v: setattr(ops, "PREFILL_XF", bool(v)),
+         "rope_fused_all": lambda v: setattr(ops, "ROPE_FUSED_MIN_M", 65 if v else 4096)}
 setk = KNOBS[knob]
 # (model, prompt tokens, requests in the batch): config 3 (3B explain, 2k prompt), config 2 (7B NL->SQL prompt),
 # the headline bench's batch-32 prefill (32 x 128 tokens)
