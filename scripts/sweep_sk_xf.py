@@ -13,7 +13,9 @@ from llm_based_apache_spark_optimization_amd import ops  # noqa: E402
 SHAPES = {"3b_qkv_m2048": (2048, 5120, 3072, "bf16"), "3b_o_m2048": (2048, 3072, 3072, "res"),
           "3b_gateup_m2048": (2048, 16384, 3072, "silu"), "3b_down_m2048": (2048, 3072, 8192, "res"),
           "7b_qkv_m4096": (4096, 12288, 4096, "bf16"), "7b_gateup_m4096": (4096, 22016, 4096, "silu"),
-          "7b_down_m4096": (4096, 4096, 11008, "res"), "7b_o_m4096": (4096, 4096, 4096, "res")}
+          "7b_down_m4096": (4096, 4096, 11008, "res"), "7b_o_m4096": (4096, 4096, 4096, "res"),
+          "7b_qkv_m300": (300, 12288, 4096, "bf16"), "7b_o_m300": (300, 4096, 4096, "res"),
+          "7b_gateup_m300": (300, 22016, 4096, "silu"), "7b_down_m300": (300, 4096, 11008, "res")}
 names = sys.argv[1].split(",") if len(sys.argv) > 1 else list(SHAPES)
 dev = torch.device("cuda:0")
 flush = torch.empty(128 << 20, device=dev)
