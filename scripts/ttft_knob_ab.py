@@ -2,7 +2,8 @@
 one-token request (prefill + first-token commit + host read-back) for each case, median (and min) of the rounds.
 Knob 'one_phase': the stream-K GEMM's one-phase K-loop schedule for the 128-row tiles (ext.gemm_sk_one_phase);
 'prefill_xf': the fragment-major prefill activations (ops.PREFILL_XF); 'rope_fused_all': the RoPE / cache-append
-qkv epilogue at every prefill size (1) vs from 4096 rows (0, the default);
+qkv epilogue at every prefill size (1) vs from 4096 rows (0, the default); 'gateup300_256': the 7B gate_up table
+entry at 300 rows, 256 x 256 whole tiles (1) vs 128 x 256 stream-K (0);
 'none': one arm, the loaded build (cross-build A/Bs: run it under LSA_HIP_SO=variants/<name>.so in turns).
 Usage: ttft_knob_ab.py [knob] [rounds] [case,...]"""
 import json
@@ -17,10 +18,18 @@ from llm_based_apache_spark_optimization_amd import ops  # noqa: E402
 from llm_based_apache_spark_optimization_amd.engine import SamplingParams, build_engine  # noqa: E402
 
 knob = sys.argv[1] if len(sys.argv) > 1 else "one_phase"
+
+
+def _table_cfg(key, cfg):  # one stream-K tuning-table entry (ops.sk_config) overridden in place
+    ops.sk_config(128, 128, 128, "bf16")  # loads the table
+    ops._sk_tuning[key] = dict(ops._sk_tuning.get(key, {}), cfg=cfg)
+
+
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 KNOBS = {"one_phase": lambda v: ops.ext().gemm_sk_one_phase(v), "none": lambda v: None,
          "prefill_xf": lambda v: setattr(ops, "PREFILL_XF", bool(v)),
-         "rope_fused_all": lambda v: setattr(ops, "ROPE_FUSED_MIN_M", 65 if v else 4096)}
+         "rope_fused_all": lambda v: setattr(ops, "ROPE_FUSED_MIN_M", 65 if v else 4096),
+         "gateup300_256": lambda v: _table_cfg("22016x4096:silu:m300", 24 if v else 19)}
 setk = KNOBS[knob]
 # (model, prompt tokens, requests in the batch): config 3 (3B explain, 2k prompt), config 2 (7B NL->SQL prompt),
 # the headline bench's batch-32 prefill (32 x 128 tokens)
