@@ -232,7 +232,7 @@ def test_gemm_stream_k_epilogues(gpu, cfg, MNK, epi):
     assert _rel(out, _sk_ref(x.float(), w, epi)) < 1e-2, (M, N, K, epi, cfg)
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 3, 5, 6, 7, 12])
+@pytest.mark.parametrize("cfg", [-1, 0, 3, 5, 6, 7, 8, 12])
 @pytest.mark.parametrize("MNK", [(300, 3072, 1376), (2048, 5120, 1024), (1100, 800, 512), (65, 1536, 2048)])
 @pytest.mark.parametrize("epi", ["bf16", "silu", "res"])
 def test_gemm_stream_k_fragment_major(gpu, cfg, MNK, epi):
